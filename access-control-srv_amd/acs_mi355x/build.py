@@ -1,0 +1,60 @@
+"""Build the native libraries in-tree (hipcc, gfx950).
+
+  lib/libacs_mi355x.so          product: HIP kernels + C ABI (include/acs_mi355x.h)
+  tests/native/libacs_core_host.so   test infrastructure: the evaluator core on the CPU
+
+Both are plain ``hipcc -shared`` builds so the .so files travel with the repo
+snapshot to the GPU box (no JIT cache).  Rebuilds only when a source is newer.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib", "libacs_mi355x.so")
+HOST_LIB = os.path.join(ROOT, "tests", "native", "libacs_core_host.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+_HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h")] + \
+    [os.path.join(ROOT, "include", "acs_mi355x.h")]
+
+
+def _stale(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _hipcc(src, out, extra=()):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           "-Wno-unused-function", "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, src, "-o", out + ".tmp"]
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+
+
+def build_product(force=False):
+    src = os.path.join(CSRC, "acs_kernels.hip")
+    if force or _stale(LIB, [src] + _HEADERS):
+        _hipcc(src, LIB)
+    return LIB
+
+
+def build_host_core(force=False):
+    src = os.path.join(ROOT, "tests", "native", "core_host.hip")
+    if force or _stale(HOST_LIB, [src] + _HEADERS):
+        _hipcc(src, HOST_LIB)
+    return HOST_LIB
+
+
+def build_all(force=False):
+    return build_product(force), build_host_core(force)
+
+
+if __name__ == "__main__":
+    print(build_all(force=True))

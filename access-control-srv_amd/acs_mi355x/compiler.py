@@ -1,0 +1,368 @@
+"""Policy-store compiler: ``policySets`` Map snapshot -> HBM tables.
+
+Everything that depends on a rule/policy/set alone is evaluated here once
+(targets' role / scoping-entity / hierarchicalRoleScoping scans, skipACL,
+scopedRoles, property presence, effect / evaluation_cacheable / combining
+algorithm codes, '#'-suffixes, regex rows).  What is left for the GPU is the
+request x target work.  Reference anchors:
+
+  targets' subject scan      accessController.ts:797-806, hierarchicalScope.ts:25-42,
+                             verifyACL.ts:13-25
+  policy effect / CA         accessController.ts:138-148, 832-838
+  rule ec / condition flags  accessController.ts:202-211, 228
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import layout as L
+from .jsops import MISSING, Unsupported, check_scalar, get, nullish, strict_eq, truthy, OBJECT_PROTO_KEYS
+
+CA_METHODS = {"denyOverrides": L.CA_DENY_OVERRIDES, "permitOverrides": L.CA_PERMIT_OVERRIDES,
+              "firstApplicable": L.CA_FIRST_APPLICABLE}
+_EFFECTS = {"PERMIT": L.EFF_PERMIT, "DENY": L.EFF_DENY, "NOT_APPLICABLE": L.EFF_NOT_APPLICABLE,
+            "INDETERMINATE": L.EFF_INDETERMINATE, "UNRECOGNIZED": L.EFF_UNRECOGNIZED}
+
+
+class Dictionary:
+    """String interner: equal ids <=> JS ===.  0 undefined, 1 null, 2 ''."""
+
+    def __init__(self):
+        self.ids = {"": L.ID_EMPTY}
+        self.strings = [MISSING, None, ""]
+
+    def __len__(self):
+        return len(self.strings)
+
+    def intern(self, v) -> int:
+        if v is MISSING:
+            return L.ID_UNDEF
+        if v is None:
+            return L.ID_NULL
+        if not isinstance(v, str):
+            raise Unsupported(f"non-string value {v!r}")
+        i = self.ids.get(v)
+        if i is None:
+            i = len(self.strings)
+            self.ids[v] = i
+            self.strings.append(v)
+        return i
+
+    def lookup(self, v):
+        if v is MISSING:
+            return L.ID_UNDEF
+        if v is None:
+            return L.ID_NULL
+        return self.ids.get(v)
+
+    def string(self, i):
+        return self.strings[i]
+
+
+class Overlay:
+    """Batch-local extension of a frozen Dictionary (request-only strings)."""
+
+    def __init__(self, base: Dictionary):
+        self.base = base
+        self.ids = {}
+        self.strings = []
+
+    def intern(self, v) -> int:
+        i = self.base.lookup(v) if (v is MISSING or v is None or isinstance(v, str)) else None
+        if i is not None:
+            return i
+        if not isinstance(v, str):
+            raise Unsupported(f"non-string value {v!r}")
+        i = self.ids.get(v)
+        if i is None:
+            i = len(self.base) + len(self.strings)
+            self.ids[v] = i
+            self.strings.append(v)
+        return i
+
+    def string(self, i):
+        n = len(self.base)
+        return self.base.string(i) if i < n else self.strings[i - n]
+
+
+def effect_code(e) -> int:
+    if e is MISSING:
+        return L.EFF_UNDEF
+    if e is None:
+        return L.EFF_NULL
+    if isinstance(e, str):
+        if e in OBJECT_PROTO_KEYS:
+            raise Unsupported(f"effect {e!r} resolves to an Object.prototype member")
+        if e in _EFFECTS:
+            return _EFFECTS[e]
+    return L.EFF_OTHER_TRUTHY if truthy(e) else L.EFF_OTHER_FALSY
+
+
+@dataclass
+class CompiledStore:
+    urns: dict
+    dictionary: Dictionary
+    sets: np.ndarray
+    pols: np.ndarray
+    rules: np.ndarray
+    targets: np.ndarray
+    rres: np.ndarray
+    pairs: np.ndarray
+    u32pool: np.ndarray
+    rx_rows: list                 # row index -> rule entity value (str / None / MISSING)
+    ec_values: list               # ec code -> raw JS value
+    id_user: int
+    # host-side objects for whatIsAllowed / response reconstruction, in table order
+    set_objs: list = field(default_factory=list)
+    pol_objs: list = field(default_factory=list)
+    rule_objs: list = field(default_factory=list)
+    stats: dict = field(default_factory=dict)
+
+    @property
+    def n_sets(self):
+        return len(self.sets)
+
+    @property
+    def n_pols(self):
+        return len(self.pols)
+
+    @property
+    def n_rules(self):
+        return len(self.rules)
+
+    def table_bytes(self):
+        return sum(a.nbytes for a in (self.sets, self.pols, self.rules, self.targets, self.rres,
+                                      self.pairs, self.u32pool))
+
+
+class _Builder:
+    def __init__(self, urns, cas):
+        self.urns = dict(urns)
+        self.ca_map = {}
+        for ca in cas:
+            m = ca.get("method")
+            if m not in CA_METHODS:
+                raise Unsupported(f"combining algorithm method {m!r}")
+            self.ca_map[ca.get("urn", MISSING)] = CA_METHODS[m]
+        self.d = Dictionary()
+        self.targets, self.rres, self.pairs, self.u32pool = [], [], [], []
+        self.rx_index = {}
+        self.rx_rows = []
+        self.ec_values = [MISSING, None, False, True]
+        self.ec_truthy = [False, False, False, True]
+        # URN ids (an absent URN is JS undefined and compares equal to undefined ids)
+        self.U = {k: self.d.intern(v) for k, v in self.urns.items()}
+
+    def urn(self, name):
+        return self.urns.get(name, MISSING)
+
+    def ca_code(self, urn):
+        key = urn if (urn is MISSING or urn is None or isinstance(urn, str)) else repr(urn)
+        return self.ca_map.get(key, L.CA_INVALID)
+
+    def ec_code(self, v):
+        for i, x in enumerate(self.ec_values):
+            if (x is v) or (type(x) is type(v) and x == v and not isinstance(v, (dict, list))):
+                return i
+        if len(self.ec_values) >= 255:
+            raise Unsupported("too many distinct evaluation_cacheable values")
+        self.ec_values.append(v)
+        self.ec_truthy.append(truthy(v))
+        return len(self.ec_values) - 1
+
+    def rx_row(self, value):
+        key = ("m",) if value is MISSING else (("n",) if value is None else ("s", value))
+        r = self.rx_index.get(key)
+        if r is None:
+            r = len(self.rx_rows)
+            if r >= 0xFFFF:
+                raise Unsupported("too many distinct rule entity values")
+            self.rx_index[key] = r
+            self.rx_rows.append(value)
+        return r
+
+    @staticmethod
+    def _attrs(lst, what):
+        if not isinstance(lst, list):
+            raise Unsupported(f"target {what} is not an array")
+        for a in lst:
+            if not isinstance(a, dict):
+                raise Unsupported(f"non-object entry in target {what}")
+            check_scalar(a.get("id", MISSING))
+            check_scalar(a.get("value", MISSING))
+        return lst
+
+    def add_pairs(self, lst):
+        off = len(self.pairs)
+        for a in lst:
+            self.pairs.append((self.d.intern(a.get("id", MISSING)), self.d.intern(a.get("value", MISSING))))
+        return off
+
+    def target(self, t) -> int:
+        if t is None or t is MISSING or not truthy(t):
+            return L.NONE32
+        if not isinstance(t, dict):
+            raise Unsupported("target is not an object")
+        subs = self._attrs(t.get("subjects", MISSING) if truthy(t.get("subjects", MISSING)) else [], "subjects")
+        acts = self._attrs(t.get("actions", MISSING) if truthy(t.get("actions", MISSING)) else [], "actions")
+        res = self._attrs(t.get("resources", MISSING) if truthy(t.get("resources", MISSING)) else [], "resources")
+        if "subjects" in t and not isinstance(t["subjects"], list):
+            raise Unsupported("subjects")
+        U = self.urn
+        rec = {}
+        flags = 0
+        # checkSubjectMatches: ruleRole = last role value (accessController.ts:802-806)
+        role = MISSING
+        for a in subs:
+            if strict_eq(a.get("id", MISSING), U("role")):
+                role = a.get("value", MISSING)
+        if len(subs) == 0:
+            flags |= L.TF_SUBJ_EMPTY
+        elif truthy(role):
+            flags |= L.TF_SUBJ_ROLE
+        if len(subs) > 0:
+            flags |= L.TF_HAS_SUBJECTS
+        rec["role"] = self.d.intern(role)
+        rec["subj_off"] = self.add_pairs(subs)
+        rec["subj_n"] = len(subs)
+        rec["act_off"] = self.add_pairs(acts)
+        rec["act_n"] = len(acts)
+        # checkHierarchicalScope subject scan (if / else-if chain, hierarchicalScope.ts:29-37)
+        hr_check, se = "true", MISSING
+        for a in subs:
+            i = a.get("id", MISSING)
+            if strict_eq(i, U("role")):
+                pass
+            elif strict_eq(i, U("hierarchicalRoleScoping")):
+                hr_check = a.get("value", MISSING)
+            elif strict_eq(i, U("roleScopingEntity")):
+                se = a.get("value", MISSING)
+        if len(subs) == 0 or not truthy(se):
+            flags |= L.TF_HR_TRIVIAL
+        if strict_eq(hr_check, "true"):
+            flags |= L.TF_HR_CHECK
+        rec["se"] = self.d.intern(se)
+        # verifyACLList subject scan (verifyACL.ts:17-25)
+        scoped = []
+        for a in subs:
+            i = a.get("id", MISSING)
+            if strict_eq(i, U("role")):
+                scoped.append(self.d.intern(a.get("value", MISSING)))
+            elif strict_eq(i, U("skipACL")):
+                flags |= L.TF_ACL_SKIP
+                break
+        rec["acl_roles_off"] = len(self.u32pool)
+        rec["acl_roles_n"] = len(scoped)
+        self.u32pool.extend(scoped)
+        # resources
+        if len(res) == 0:
+            flags |= L.TF_RES_EMPTY
+        rec["res_off"] = len(self.rres)
+        rec["res_n"] = len(res)
+        last_prop = MISSING
+        for a in res:
+            i, v = a.get("id", MISSING), a.get("value", MISSING)
+            kind = 0
+            if strict_eq(i, U("entity")):
+                kind |= L.K_ENT
+            if (nullish(i) and nullish(U("entity"))) or strict_eq(i, U("entity")):
+                kind |= L.K_ENT_LOOSE
+            if strict_eq(i, U("operation")):
+                kind |= L.K_OP
+            if strict_eq(i, U("property")):
+                kind |= L.K_PROP
+                flags |= L.TF_RULE_PROPS
+                last_prop = v
+            hs = L.ID_UNDEF
+            if kind & L.K_PROP and isinstance(v, str):
+                hs = self.d.intern(v[v.rfind("#") + 1:])
+            row = self.rx_row(v) if kind & L.K_ENT_LOOSE else 0
+            self.rres.append((self.d.intern(v), hs, row, kind, 0, 0))
+        rec["last_prop_value"] = self.d.intern(last_prop)
+        if isinstance(last_prop, str):
+            flags |= L.TF_LASTPROP_STR
+            if "#" in last_prop:
+                flags |= L.TF_LASTPROP_HASH
+        rec["flags"] = flags
+        self.targets.append(tuple(rec.get(n, 0) if n != "pad" else (0, 0) for n in L.TARGET_DT.names))
+        return len(self.targets) - 1
+
+
+def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> CompiledStore:
+    """Snapshot ``policy_sets`` (ordered Map of sets, see store.py) into tables."""
+    b = _Builder(urns, combining_algorithms)
+    sets, pols, rules = [], [], []
+    set_objs, pol_objs, rule_objs = [], [], []
+    for ps in policy_sets.values():
+        if not isinstance(ps, dict):
+            raise Unsupported("null policy set")
+        s_target = b.target(ps.get("target", MISSING))
+        p_begin = len(pols)
+        combin = ps.get("combinables")
+        if not isinstance(combin, dict):
+            raise Unsupported("policy set without combinables")
+        for pol in combin.values():
+            if pol is None or pol is MISSING:
+                pols.append((L.NONE32, len(rules), len(rules), 0, 0, 0, 0, L.PF_NULL))
+                pol_objs.append(None)
+                continue
+            p_target = b.target(pol.get("target", MISSING))
+            r_begin = len(rules)
+            rcomb = pol.get("combinables")
+            if not isinstance(rcomb, dict):
+                raise Unsupported("policy without combinables")
+            for rule in rcomb.values():
+                if rule is None or rule is MISSING:
+                    rules.append((L.NONE32, 0, 0, L.RF_NULL, 0))
+                    rule_objs.append(None)
+                    continue
+                r_target = b.target(rule.get("target", MISSING))
+                rf = 0
+                cond = rule.get("condition", MISSING)
+                clen = len(cond) if isinstance(cond, (str, list)) else get(cond, "length")
+                if truthy(clen):
+                    rf |= L.RF_HAS_CONDITION
+                ec = b.ec_code(rule.get("evaluation_cacheable", MISSING))
+                if b.ec_truthy[ec]:
+                    rf |= L.RF_EC_TRUTHY
+                if r_target != L.NONE32:
+                    rf |= L.RF_HAS_TARGET
+                rules.append((r_target, effect_code(rule.get("effect", MISSING)), ec, rf, 0))
+                rule_objs.append(rule)
+            pf = L.PF_EFFECT_TRUTHY if truthy(pol.get("effect", MISSING)) else 0
+            if p_target != L.NONE32:
+                pf |= L.PF_HAS_TARGET
+            pols.append((p_target, r_begin, len(rules), len(rcomb), effect_code(pol.get("effect", MISSING)),
+                         b.ec_code(pol.get("evaluation_cacheable", MISSING)),
+                         b.ca_code(pol.get("combining_algorithm", MISSING)), pf))
+            pol_objs.append(pol)
+        sets.append((s_target, p_begin, len(pols), b.ca_code(ps.get("combining_algorithm", MISSING)), (0, 0, 0)))
+        set_objs.append(ps)
+    cs = CompiledStore(
+        urns=b.urns, dictionary=b.d,
+        sets=np.array(sets, dtype=L.SET_DT) if sets else np.zeros(0, L.SET_DT),
+        pols=np.array(pols, dtype=L.POLICY_DT) if pols else np.zeros(0, L.POLICY_DT),
+        rules=np.array(rules, dtype=L.RULE_DT) if rules else np.zeros(0, L.RULE_DT),
+        targets=np.array(b.targets, dtype=L.TARGET_DT) if b.targets else np.zeros(0, L.TARGET_DT),
+        rres=np.array(b.rres, dtype=L.RULE_RES_DT) if b.rres else np.zeros(0, L.RULE_RES_DT),
+        pairs=np.array(b.pairs, dtype=L.PAIR_DT) if b.pairs else np.zeros(0, L.PAIR_DT),
+        u32pool=np.array(b.u32pool, dtype=np.uint32) if b.u32pool else np.zeros(0, np.uint32),
+        rx_rows=b.rx_rows, ec_values=b.ec_values, id_user=b.d.intern(b.urn("user")),
+        set_objs=set_objs, pol_objs=pol_objs, rule_objs=rule_objs)
+    cs.stats = {"sets": cs.n_sets, "policies": cs.n_pols, "rules": cs.n_rules, "targets": len(cs.targets),
+                "dictionary": len(b.d), "rx_rows": len(b.rx_rows), "table_bytes": cs.table_bytes()}
+    return cs
+
+
+def store_blob(cs: CompiledStore) -> bytes:
+    """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header)."""
+    import struct
+    hdr = struct.pack("<16I", 0x31534341, 1, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.targets), len(cs.rres),
+                      len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0)
+    parts = [hdr]
+    for a in (cs.sets, cs.pols, cs.rules, cs.targets, cs.rres, cs.pairs, cs.u32pool):
+        b = np.ascontiguousarray(a).tobytes()
+        parts.append(b + b"\0" * ((-len(b)) % 16))
+    return b"".join(parts)

@@ -1,0 +1,66 @@
+"""Packed layout of compiled tables and request batches (host side).
+
+Constants are read from ``csrc/acs_layout.h`` / ``csrc/acs_eval.h`` at import
+time so the host compiler/encoder and the HIP evaluator cannot drift; the
+numpy dtypes below mirror the C structs byte for byte (checked against the
+library's own ``sizeof`` by ``acs_layout_sizes`` in the tests).
+"""
+from __future__ import annotations
+
+import os
+import re
+
+import numpy as np
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+
+
+def _parse_constants(*headers):
+    consts = {}
+    pat = re.compile(r"\b([A-Z][A-Z0-9_]+)\s*=\s*([^,;{}\n/]+)")
+    for h in headers:
+        with open(os.path.join(CSRC, h)) as f:
+            src = f.read()
+        src = re.sub(r"//[^\n]*", "", src)
+        for name, expr in pat.findall(src):
+            e = re.sub(r"(\d+)u\b", r"\1", expr.strip())
+            e = e.replace("0xFFFFFFFFu", "0xFFFFFFFF")
+            try:
+                consts[name] = int(eval(e, {"__builtins__": {}}, dict(consts)))
+            except Exception:
+                pass
+    return consts
+
+
+C = _parse_constants("acs_layout.h", "acs_eval.h")
+globals().update(C)
+
+u8, u16, u32 = np.uint8, np.uint16, np.uint32
+
+TARGET_DT = np.dtype([("flags", u32), ("role", u32), ("se", u32), ("subj_off", u32), ("act_off", u32),
+                      ("res_off", u32), ("acl_roles_off", u32), ("last_prop_value", u32),
+                      ("subj_n", u16), ("act_n", u16), ("res_n", u16), ("acl_roles_n", u16),
+                      ("pad", u32, 2)])
+RULE_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("row", u16), ("kind", u8), ("pad", u8),
+                        ("pad2", u32)])
+SET_DT = np.dtype([("target", u32), ("pol_begin", u32), ("pol_end", u32), ("ca", u8), ("pad", u8, 3)])
+POLICY_DT = np.dtype([("target", u32), ("rule_begin", u32), ("rule_end", u32), ("map_size", u32),
+                      ("effect", u8), ("ec", u8), ("ca", u8), ("flags", u8)])
+RULE_DT = np.dtype([("target", u32), ("effect", u8), ("ec", u8), ("flags", u8), ("pad", u8)])
+PAIR_DT = np.dtype([("id", u32), ("value", u32)])
+REQ_HDR_DT = np.dtype([("flags", u32), ("nres", u8), ("nsubj", u8), ("nact", u8), ("nroles", u8),
+                       ("arena_off", u32), ("subject_id", u32)])
+REQ_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("col", u16), ("contains", u16), ("kind", u8),
+                       ("slot_a", u8), ("slot_b", u8), ("pad", u8)])
+DECISION_DT = np.dtype([("decision", u8), ("ec", u8), ("flags", u8), ("err", u8), ("aux", u32)])
+
+SIZES = {"TargetRec": TARGET_DT.itemsize, "RuleResAttr": RULE_RES_DT.itemsize, "SetRec": SET_DT.itemsize,
+         "PolicyRec": POLICY_DT.itemsize, "RuleRec": RULE_DT.itemsize, "ReqHdr": REQ_HDR_DT.itemsize,
+         "ReqRes": REQ_RES_DT.itemsize, "Decision": DECISION_DT.itemsize}
+assert SIZES == {"TargetRec": 48, "RuleResAttr": 16, "SetRec": 16, "PolicyRec": 20, "RuleRec": 8,
+                 "ReqHdr": 16, "ReqRes": 16, "Decision": 8}, SIZES
+
+DECISION_NAMES = {C["DEC_PERMIT"]: "PERMIT", C["DEC_DENY"]: "DENY", C["DEC_NOT_APPLICABLE"]: "NOT_APPLICABLE",
+                  C["DEC_INDETERMINATE"]: "INDETERMINATE", C["DEC_UNRECOGNIZED"]: "UNRECOGNIZED"}
+ERR_NAMES = {C["ERR_TYPE"]: "TypeError", C["ERR_INVALID_CA"]: "InvalidCombiningAlgorithm",
+             C["ERR_REGEX_SYNTAX"]: "SyntaxError", C["ERR_REGEX_HOST"]: "RegexHost"}

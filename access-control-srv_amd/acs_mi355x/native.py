@@ -1,0 +1,135 @@
+"""ctypes binding of the C ABI (include/acs_mi355x.h) — the product's only compute path.
+
+``load()`` raises if ``lib/libacs_mi355x.so`` is missing: there is no CPU
+fallback in the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import layout as L
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libacs_mi355x.so")
+
+
+class ReqBatchC(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("hdr", C.c_void_p), ("res", C.c_void_p), ("subj", C.c_void_p),
+                ("act", C.c_void_p), ("roles", C.c_void_p), ("arena", C.c_void_p), ("arena_words", C.c_size_t),
+                ("rx", C.c_void_p), ("rx_cols", C.c_uint32), ("rx_rows", C.c_uint32)]
+
+
+EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
+           "acs_what_is_allowed", "acs_what_is_allowed_device", "acs_last_kernel_ms", "acs_last_error",
+           "acs_layout_sizes", "acs_device_count"]
+
+
+def _declare(lib):
+    vp, u32 = C.c_void_p, C.c_uint32
+    pb = C.POINTER(ReqBatchC)
+    lib.acs_compile.restype = vp
+    lib.acs_compile.argtypes = [vp, C.c_size_t, C.c_int]
+    lib.acs_free.argtypes = [vp]
+    lib.acs_free.restype = None
+    lib.acs_is_allowed.argtypes = [vp, pb, vp]
+    lib.acs_is_allowed_device.argtypes = [vp, pb, vp, vp]
+    lib.acs_wia_words_per_request.argtypes = [vp]
+    lib.acs_wia_words_per_request.restype = u32
+    lib.acs_what_is_allowed.argtypes = [vp, pb, vp, vp, vp, vp]
+    lib.acs_what_is_allowed_device.argtypes = [vp, pb, vp, vp, vp, vp, vp]
+    lib.acs_last_kernel_ms.argtypes = [vp]
+    lib.acs_last_kernel_ms.restype = C.c_float
+    lib.acs_last_error.restype = C.c_char_p
+    lib.acs_layout_sizes.argtypes = [C.POINTER(u32), C.c_int]
+    return lib
+
+
+_LIB = None
+
+
+def load(path: str | None = None):
+    """Load the HIP library (fails loudly when it has not been built)."""
+    global _LIB
+    if _LIB is None or path:
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(f"MI355X evaluator library missing: {p} (run __graft_entry__.build())")
+        _LIB = _declare(C.CDLL(p))
+    return _LIB
+
+
+def last_error(lib=None):
+    return (lib or load()).acs_last_error().decode()
+
+
+def batch_struct(b, ptrs=None) -> ReqBatchC:
+    """acs_req_batch over host numpy arrays (ptrs=None) or a dict of device pointers."""
+    s = ReqBatchC()
+    s.n = b.n
+    if ptrs is None:
+        s.hdr = b.hdr.ctypes.data
+        s.res = b.res.ctypes.data
+        s.subj = b.subj.ctypes.data
+        s.act = b.act.ctypes.data
+        s.roles = b.roles.ctypes.data
+        s.arena = b.arena.ctypes.data if b.arena.size else b.hdr.ctypes.data
+        s.rx = b.rx.ctypes.data
+    else:
+        for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx"):
+            setattr(s, k, ptrs[k])
+    s.arena_words = int(b.arena.size)
+    s.rx_cols = int(b.rx.shape[0])
+    s.rx_rows = int(b.rx.shape[1])
+    return s
+
+
+class Tables:
+    """Device-resident compiled store on one GPU (wraps an acs_tables handle)."""
+
+    def __init__(self, blob: bytes, device: int = 0, lib=None):
+        self.lib = lib or load()
+        self._blob = blob
+        self.h = self.lib.acs_compile(blob, len(blob), device)
+        if not self.h:
+            raise RuntimeError(f"acs_compile failed: {last_error(self.lib)}")
+        self.device = device
+        self.words = int(self.lib.acs_wia_words_per_request(self.h))
+
+    def close(self):
+        if self.h:
+            self.lib.acs_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def is_allowed(self, batch) -> np.ndarray:
+        out = np.zeros(batch.n, L.DECISION_DT)
+        if batch.n:
+            s = batch_struct(batch)
+            if self.lib.acs_is_allowed(self.h, C.byref(s), out.ctypes.data) != 0:
+                raise RuntimeError(f"acs_is_allowed: {last_error(self.lib)}")
+        return out
+
+    def what_is_allowed(self, batch):
+        n = batch.n
+        bits = np.zeros((n, self.words), np.uint32)
+        obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)
+        obl_n = np.zeros(n, np.uint32)
+        out = np.zeros(n, L.DECISION_DT)
+        if n:
+            s = batch_struct(batch)
+            rc = self.lib.acs_what_is_allowed(self.h, C.byref(s), bits.ctypes.data, obl.ctypes.data,
+                                              obl_n.ctypes.data, out.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(f"acs_what_is_allowed: {last_error(self.lib)}")
+        return bits, obl, obl_n, out
+
+    def last_kernel_ms(self):
+        return float(self.lib.acs_last_kernel_ms(self.h))

@@ -1,0 +1,640 @@
+// acs_eval.h — per-request decision core of the MI355X access-control evaluator.
+//
+// One call evaluates one request against the whole compiled store, in the
+// reference's order (sets -> policies -> rules, Map order), so that decisions,
+// evaluation_cacheable, whatIsAllowed inclusion bits and the maskedProperty
+// push log are bit-identical to the TypeScript PDP.  The GPU kernels
+// (acs_kernels.hip) run it one request per lane; table records are read
+// through wave-uniform addresses (scalar loads), request data through
+// coalesced [slot][request] SoA arrays.
+//
+// Reference semantics restated (paths in restorecommerce/access-control-srv):
+//   isAllowed                 src/core/accessController.ts:88-324
+//   whatIsAllowed             src/core/accessController.ts:326-427
+//   checkMultipleEntities     src/core/accessController.ts:429-463
+//   resourceAttributesMatch   src/core/accessController.ts:465-654
+//   targetMatches             src/core/accessController.ts:661-672
+//   attributesMatch           src/core/accessController.ts:681-699
+//   checkSubjectMatches       src/core/accessController.ts:793-823
+//   decide + CAs              src/core/accessController.ts:832-893
+//   checkHierarchicalScope    src/core/hierarchicalScope.ts:10-259
+//   verifyACLList             src/core/verifyACL.ts:11-251
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "acs_layout.h"
+
+namespace acs {
+
+#define ACS_FN __host__ __device__ inline
+
+struct Pair {
+  uint32_t id, value;
+};
+
+// regex matrix cell bits (rule entity value row x request entity value column)
+enum RxBits : uint8_t { RX_HIT = 1, RX_RESET = 2, RX_THROW_TYPE = 4, RX_THROW_SYNTAX = 8, RX_HOST = 16 };
+
+struct Tables {
+  const SetRec* sets;
+  const PolicyRec* pols;
+  const RuleRec* rules;
+  const TargetRec* targets;
+  const RuleResAttr* rres;
+  const Pair* pairs;
+  const uint32_t* u32pool;
+  uint32_t n_sets, n_pols, n_rules;
+  uint32_t id_user;  // interned urns.user
+};
+
+struct Batch {
+  uint32_t n;
+  const ReqHdr* hdr;    // [n]
+  const ReqRes* res;    // [QMAX][n]
+  const Pair* subj;     // [SMAX][n]
+  const Pair* act;      // [AMAX][n]
+  const uint32_t* roles;  // [RMAX][n]
+  const uint32_t* arena;
+  const uint8_t* rx;    // [cols][rx_rows]
+  uint32_t rx_rows;
+};
+
+ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
+
+// tri-state result: 1 true, 0 false, <0 -ErrKind (the reference throws)
+typedef int tri;
+
+struct Fold {  // streaming decide(): first X else last / first element
+  uint8_t ca, n, locked, eff, ec;
+  ACS_FN explicit Fold(uint8_t ca_) : ca(ca_), n(0), locked(0), eff(EFF_UNDEF), ec(EC_UNDEF) {}
+  ACS_FN void push(uint8_t e, uint8_t c) {
+    if (ca == CA_FIRST_APPLICABLE) {
+      if (!n) { eff = e; ec = c; }
+    } else if (!locked) {
+      eff = e;
+      ec = c;
+      if (e == (ca == CA_DENY_OVERRIDES ? EFF_DENY : EFF_PERMIT)) locked = 1;
+    }
+    n = 1;
+  }
+};
+
+struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
+  uint32_t* out;  // [OBL_MAX][2] or nullptr
+  uint32_t n;
+  bool overflow;
+};
+
+struct Req {
+  const Tables& T;
+  const Batch& B;
+  uint32_t i;
+  ReqHdr h;
+  const uint32_t* ar;  // context arena of this request
+  uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
+  const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
+
+  ACS_FN Req(const Tables& t, const Batch& b, uint32_t idx) : T(t), B(b), i(idx) {
+    h = B.hdr[i];
+    ar = B.arena + h.arena_off;
+    uint32_t c0 = ar[0], c1 = ar[1];
+    n_grants = c0 & 0xFF; n_rolese = (c0 >> 8) & 0xFF; n_slots = (c0 >> 16) & 0xFF; n_roots = c0 >> 24;
+    n_tse = c1 & 0xFF; n_hrkeys = (c1 >> 8) & 0xFF;
+    grants = ar + 2;
+    rolese = grants + 3 * n_grants;
+    roots = rolese + 2 * n_rolese;
+    hrkeys = roots + n_roots;
+    slotoff = hrkeys + n_hrkeys;
+    tse = slotoff + n_slots;
+  }
+  ACS_FN ReqRes res(uint32_t j) const { return B.res[(size_t)j * B.n + i]; }
+  ACS_FN Pair subj(uint32_t j) const { return B.subj[(size_t)j * B.n + i]; }
+  ACS_FN Pair act(uint32_t j) const { return B.act[(size_t)j * B.n + i]; }
+  ACS_FN uint32_t role(uint32_t j) const { return B.roles[(size_t)j * B.n + i]; }
+  ACS_FN uint8_t rx(uint32_t col, uint32_t row) const { return B.rx[(size_t)col * B.rx_rows + row]; }
+  ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
+};
+
+// ------------------------------------------------------------------ attributesMatch (loose ==)
+ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const Req& R, bool subjects) {
+  uint32_t qn = subjects ? R.h.nsubj : R.h.nact;
+  for (uint32_t k = 0; k < rn; ++k) {
+    Pair a = rule[k];
+    bool found = false;
+    for (uint32_t j = 0; j < qn && !found; ++j) {
+      Pair q = subjects ? R.subj(j) : R.act(j);
+      found = loose_eq(q.id, a.id) && loose_eq(q.value, a.value);
+    }
+    if (!found) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ checkSubjectMatches
+ACS_FN bool subject_match(const TargetRec& t, const Req& R) {
+  if (t.flags & TF_SUBJ_EMPTY) return true;
+  if (t.flags & TF_SUBJ_ROLE) {
+    if (!R.flag(RQ_RA_TRUTHY)) return false;
+    for (uint32_t k = 0; k < R.h.nroles; ++k)
+      if (R.role(k) == t.role) return true;
+    return false;
+  }
+  return attrs_match(R.T.pairs + t.subj_off, t.subj_n, R, true);
+}
+
+// ------------------------------------------------------------------ resourceAttributesMatch
+// Request attrs [j0, j1) with requestPropertiesExist = rpe.  wia: 'whatIsAllowed' op.
+ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool regex, bool wia,
+                          uint32_t j0, uint32_t j1, bool rpe, OblLog* obl) {
+  if (t.flags & TF_RES_EMPTY) return 1;
+  const RuleResAttr* ra = R.T.rres + t.res_off;
+  bool em = false, pm = false, rp = false, om = false, skip_deny = true;
+  uint32_t ent_j = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const ReqRes q = R.res(j);
+    pm = false;
+    for (uint32_t k = 0; k < t.res_n; ++k) {
+      const RuleResAttr r = ra[k];
+      if (r.kind & K_PROP) rp = true;
+      if (!regex) {
+        if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
+          em = true;
+          ent_j = j;
+        } else if ((q.kind & K_OP) && (r.kind & K_OP) && q.value == r.value) {
+          om = true;
+        } else if (em && (q.kind & K_PROP) && (r.kind & K_PROP)) {
+          if ((q.contains >> ent_j) & 1u) {
+            if (r.value == q.value) pm = true;
+          } else if (effect == EFF_PERMIT) {
+            pm = true;
+          }
+        }
+      } else {
+        if ((q.kind & K_ENT) && (r.kind & K_ENT)) {
+          uint8_t c = R.rx(q.col, r.row);
+          if (c & RX_THROW_TYPE) return -(tri)ERR_TYPE;
+          if (c & RX_THROW_SYNTAX) return -(tri)ERR_REGEX_SYNTAX;
+          if (c & RX_HOST) return -(tri)ERR_REGEX_HOST;
+          ent_j = j;
+          if (c & RX_RESET) em = false;
+          if (c & RX_HIT) em = true;
+        } else if (em && (q.kind & K_PROP) && (r.kind & K_PROP)) {
+          if (r.hash_sfx == q.hash_sfx) pm = true;
+        }
+      }
+    }
+    const bool scope = (q.kind & K_PROP) || !rpe;
+    if (!wia) {
+      if (effect == EFF_DENY && scope && em && rp && pm) skip_deny = false;
+      if (effect == EFF_PERMIT && scope && em && rp && !pm) return 0;
+    } else {
+      // maskedProperty pushes (accessController.ts:592-640)
+      bool permit_mask = effect == EFF_PERMIT && scope && em && rp && !pm;
+      if (permit_mask && !rpe) return 0;
+      bool deny_mask = effect == EFF_DENY && scope && em && rp && (pm || !rpe);
+      if (permit_mask || deny_mask) {
+        uint32_t mask;
+        bool no_hash;
+        if (rpe && q.value > ID_EMPTY) {  // truthy request property value
+          mask = q.value;
+          no_hash = !(q.kind & K_HAS_HASH);
+        } else if (!rpe) {
+          mask = t.last_prop_value;
+          no_hash = (t.flags & TF_LASTPROP_STR) && !(t.flags & TF_LASTPROP_HASH);
+        } else {
+          mask = ID_UNDEF;
+          no_hash = false;
+        }
+        if (!no_hash && obl) {
+          if (obl->n < (uint32_t)OBL_MAX) {
+            if (obl->out) {
+              obl->out[2 * obl->n] = R.res(ent_j).value;
+              obl->out[2 * obl->n + 1] = mask;
+            }
+            obl->n++;
+          } else {
+            obl->overflow = true;
+          }
+        }
+      }
+    }
+  }
+  if (!wia && skip_deny && rp && rpe && effect == EFF_DENY && !pm) return 0;
+  if (!em && !om) return 0;
+  return 1;
+}
+
+// ------------------------------------------------------------------ targetMatches
+ACS_FN tri target_match(const TargetRec& t, const Req& R, uint8_t effect, bool regex, bool wia, OblLog* obl) {
+  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;  // requestTarget.subjects of undefined
+  if (!subject_match(t, R)) return 0;
+  if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
+  return resource_match(t, R, effect == EFF_UNDEF ? EFF_PERMIT : effect, regex, wia, 0, R.h.nres,
+                        R.flag(RQ_ANY_PROP), obl);
+}
+
+// ------------------------------------------------------------------ checkHierarchicalScope
+ACS_FN const uint32_t* slot_rec(const Req& R, uint32_t slot) { return R.ar + R.slotoff[slot]; }
+
+ACS_FN bool hr_direct(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
+  const uint32_t* rec = slot_rec(R, slot);
+  uint32_t n_owners = rec[1];
+  const uint32_t* p = rec + 2;
+  for (uint32_t o = 0; o < n_owners; ++o) {
+    uint32_t w = p[0], val = p[1], na = w >> 8;
+    const uint32_t* at = p + 2;
+    if ((w & 1u) && val == se) {
+      for (uint32_t g = 0; g < R.n_grants; ++g) {
+        const uint32_t* gr = R.grants + 3 * g;
+        if (gr[0] == role && gr[1] == se)
+          for (uint32_t a = 0; a < na; ++a)
+            if (at[3 * a] == gr[2]) return true;
+      }
+    }
+    p = at + 3 * na;
+  }
+  return false;
+}
+
+ACS_FN bool hr_tree(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
+  bool rse = false;
+  for (uint32_t k = 0; k < R.n_rolese && !rse; ++k) rse = R.rolese[2 * k] == role && R.rolese[2 * k + 1] == se;
+  if (!rse) return false;
+  uint32_t mask = 0;
+  for (uint32_t r = 0; r < R.n_roots; ++r)
+    if (R.roots[r] == role) mask |= 1u << r;
+  if (!mask) return false;
+  const uint32_t* rec = slot_rec(R, slot);
+  uint32_t n_owners = rec[1];
+  const uint32_t* p = rec + 2;
+  for (uint32_t o = 0; o < n_owners; ++o) {
+    uint32_t w = p[0], val = p[1], na = w >> 8;
+    const uint32_t* at = p + 2;
+    if ((w & 1u) && val == se)
+      for (uint32_t a = 0; a < na; ++a)
+        if ((at[3 * a + 1] & K_OI) && (at[3 * a + 2] & mask)) return true;
+    p = at + 3 * na;
+  }
+  return false;
+}
+
+ACS_FN tri hierarchical_scope(const TargetRec& t, const Req& R) {
+  if (t.flags & TF_HR_TRIVIAL) return 1;
+  if (R.flag(RQ_CTX_EMPTY)) return 0;
+  bool all_direct = true, all_ok = true;
+  const RuleResAttr* ra = R.T.rres + t.res_off;
+  for (uint32_t k = 0; k < t.res_n; ++k) {
+    const RuleResAttr r = ra[k];
+    if (r.kind & K_ENT_LOOSE) {
+      bool em = false;
+      for (uint32_t j = 0; j < R.h.nres; ++j) {
+        const ReqRes q = R.res(j);
+        uint32_t slot = NONE8;
+        if (q.kind & K_ENT_LOOSE) {
+          if (loose_eq(q.value, r.value)) {
+            em = true;
+          } else {
+            uint8_t c = R.rx(q.col, r.row);
+            if (c & RX_THROW_TYPE) return -(tri)ERR_TYPE;
+            if (c & RX_THROW_SYNTAX) return -(tri)ERR_REGEX_SYNTAX;
+            if (c & RX_HOST) return -(tri)ERR_REGEX_HOST;
+            if (c & RX_RESET) em = false;
+            if (c & RX_HIT) em = true;
+          }
+          continue;
+        } else if ((q.kind & K_RID_LOOSE) && em) {
+          slot = q.slot_a;
+        } else {
+          continue;
+        }
+        if (slot == NONE8) return 0;
+        if (slot_rec(R, slot)[0]) return 0;  // owners missing
+        bool d = hr_direct(R, slot, t.role, t.se);
+        all_direct = all_direct && d;
+        all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
+      }
+    } else if (r.kind & K_OP) {
+      for (uint32_t j = 0; j < R.h.nres; ++j) {
+        const ReqRes q = R.res(j);
+        if (!((q.kind & K_OP) && q.value == r.value)) continue;
+        uint32_t slot = q.slot_b;
+        if (slot == NONE8) return 0;
+        if (slot_rec(R, slot)[0]) return 0;
+        bool d = hr_direct(R, slot, t.role, t.se);
+        all_direct = all_direct && d;
+        all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
+      }
+    }
+  }
+  if (R.flag(RQ_RA_EMPTY)) return 0;
+  if (all_direct) return 1;
+  if (!(t.flags & TF_HR_CHECK)) return 0;
+  if (!R.flag(RQ_HRS_ITERABLE)) return -(tri)ERR_TYPE;  // getAllChildNodes(undefined)
+  return all_ok ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ verifyACLList
+ACS_FN bool in_list(const uint32_t* l, uint32_t n, uint32_t v) {
+  for (uint32_t k = 0; k < n; ++k)
+    if (l[k] == v) return true;
+  return false;
+}
+
+ACS_FN tri verify_acl(const TargetRec& t, const Req& R) {
+  if (t.flags & TF_ACL_SKIP) return 1;
+  uint32_t st = (R.h.flags >> RQ_ACL_SHIFT) & 3u;
+  if (st == ACL_RET_TRUE) return 1;
+  if (st == ACL_RET_FALSE) return 0;
+  if (R.flag(RQ_SUBJ_MISSING)) return -(tri)ERR_TYPE;
+  if (R.flag(RQ_RA_EMPTY)) return 0;
+  if (!R.flag(RQ_HRS_ITERABLE)) return -(tri)ERR_TYPE;  // getRoleOrgMapping(undefined)
+  const uint32_t* roles = R.T.u32pool + t.acl_roles_off;
+  const uint32_t nr = t.acl_roles_n;
+  if (R.flag(RQ_ACT_CREATE)) {
+    if (R.n_tse == 0) return 1;
+    bool valid = false;
+    for (uint32_t e = 0; e < R.n_tse; ++e) {
+      const uint32_t se = R.tse[3 * e], ni = R.tse[3 * e + 1];
+      const uint32_t* inst = R.ar + R.tse[3 * e + 2];
+      if (se == R.T.id_user) {
+        valid = true;
+        continue;
+      }
+      bool present = false;
+      for (uint32_t k = 0; k < R.n_rolese && !present; ++k)
+        present = R.rolese[2 * k + 1] == se && in_list(roles, nr, R.rolese[2 * k]);
+      if (!present) return 0;
+      uint32_t validated = 0;  // bitmask over inst indices
+      for (uint32_t kk = 0; kk < R.n_hrkeys; ++kk) {
+        if (!in_list(roles, nr, R.hrkeys[kk])) continue;
+        for (uint32_t x = 0; x < ni; ++x) {
+          if ((inst[2 * x + 1] >> kk) & 1u) {
+            valid = true;
+            validated |= 1u << x;
+            continue;
+          }
+          bool was = false;
+          for (uint32_t y = 0; y < ni && !was; ++y)
+            was = ((validated >> y) & 1u) && inst[2 * y] == inst[2 * x];
+          if (!was) {
+            valid = false;
+            break;
+          }
+        }
+      }
+      if (!valid) return 0;
+    }
+    return valid ? 1 : 0;
+  }
+  if (R.flag(RQ_ACT_RMD)) {
+    if (R.n_tse == 0) return 1;
+    for (uint32_t e = 0; e < R.n_tse; ++e) {
+      const uint32_t se = R.tse[3 * e], ni = R.tse[3 * e + 1];
+      const uint32_t* inst = R.ar + R.tse[3 * e + 2];
+      if (se == R.T.id_user)
+        for (uint32_t x = 0; x < ni; ++x)
+          if (inst[2 * x] == R.h.subject_id) return 1;
+      for (uint32_t g = 0; g < R.n_grants; ++g) {
+        const uint32_t* gr = R.grants + 3 * g;
+        if (gr[1] != se || !in_list(roles, nr, gr[0])) continue;
+        for (uint32_t x = 0; x < ni; ++x)
+          if (inst[2 * x] == gr[2]) return 1;
+      }
+    }
+    return 0;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ checkMultipleEntitiesMatch
+ACS_FN tri multiple_entities(const SetRec& S, const Req& R) {
+  for (uint32_t j = 0; j < R.h.nres; ++j) {
+    const ReqRes q = R.res(j);
+    if (!(q.kind & K_ENT)) continue;
+    bool multi = false;
+    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
+      const PolicyRec P = R.T.pols[p];
+      if (P.flags & PF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
+      if (P.target == NONE32) continue;
+      const TargetRec& t = R.T.targets[P.target];
+      if (t.res_n == 0) continue;
+      uint8_t pe = (P.flags & PF_EFFECT_TRUTHY) ? P.effect : EFF_UNDEF;  // no PERMIT default here
+      tri m = resource_match(t, R, pe, false, false, j, j + 1, (q.kind & K_PROP) != 0, nullptr);
+      if (m < 0) return m;
+      if (m) multi = true;
+    }
+    if (!multi) return 0;
+  }
+  return 1;
+}
+
+// ------------------------------------------------------------------ isAllowed
+ACS_FN Decision make_err(tri e) {
+  Decision d{};
+  d.decision = DEC_INDETERMINATE;
+  d.flags = OF_ERR;
+  d.err = (uint8_t)(-e);
+  return d;
+}
+
+ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
+  Req R(T, B, i);
+  Decision out{};
+  if (R.flag(RQ_HOST)) {
+    out.decision = DEC_INDETERMINATE;
+    out.flags = OF_HOST_REQ;
+    return out;
+  }
+  if (R.flag(RQ_NO_TARGET)) {
+    out.decision = DEC_DENY;
+    out.ec = EC_FALSE;
+    out.flags = OF_NO_TARGET;
+    return out;
+  }
+  uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
+  uint32_t last_set = 0;
+  for (uint32_t s = 0; s < T.n_sets; ++s) {
+    const SetRec S = T.sets[s];
+    if (S.target != NONE32) {
+      tri m = target_match(T.targets[S.target], R, EFF_PERMIT, false, false, nullptr);
+      if (m < 0) return make_err(m);
+      if (!m) continue;
+    }
+    // loop 2a: policyEffect prefix + first exact policy match (accessController.ts:136-157)
+    bool exact = false;
+    uint8_t pe = EFF_UNDEF;
+    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
+      const PolicyRec P = T.pols[p];
+      if (P.flags & PF_NULL) return make_err(-(tri)ERR_TYPE);
+      if (P.flags & PF_EFFECT_TRUTHY) pe = P.effect;
+      if (P.target != NONE32) {
+        tri m = target_match(T.targets[P.target], R, pe, false, false, nullptr);
+        if (m < 0) return make_err(m);
+        if (m) {
+          exact = true;
+          break;
+        }
+      }
+    }
+    if (exact && R.flag(RQ_MULTI_ENT)) {
+      tri m = multiple_entities(S, R);
+      if (m < 0) return make_err(m);
+      exact = m != 0;
+    }
+    Fold sf(S.ca);
+    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
+      const PolicyRec P = T.pols[p];
+      if (P.flags & PF_NULL) continue;
+      bool psm = true;
+      if (P.target != NONE32) {
+        const TargetRec& pt = T.targets[P.target];
+        tri m = target_match(pt, R, pe, !exact, false, nullptr);
+        if (m < 0) return make_err(m);
+        if (!m) continue;
+        if (pt.flags & TF_HAS_SUBJECTS) {
+          tri h = hierarchical_scope(pt, R);
+          if (h < 0) return make_err(h);
+          psm = h != 0;
+        }
+      }
+      if (P.map_size == 0 && (P.flags & PF_EFFECT_TRUTHY)) {
+        sf.push(P.effect, P.ec);
+        continue;
+      }
+      Fold rf(P.ca);
+      bool ec_rule = true;
+      for (uint32_t r = P.rule_begin; r < P.rule_end; ++r) {
+        const RuleRec Q = T.rules[r];
+        if (Q.flags & RF_NULL) continue;
+        if (!(Q.flags & RF_EC_TRUTHY)) ec_rule = false;
+        tri m = 1;
+        if (Q.target != NONE32) {
+          const TargetRec& rt = T.targets[Q.target];
+          m = target_match(rt, R, Q.effect, false, false, nullptr);
+          if (m < 0) return make_err(m);
+          if (!m) {
+            m = target_match(rt, R, Q.effect, true, false, nullptr);
+            if (m < 0) return make_err(m);
+          }
+          if (!m) continue;
+          m = hierarchical_scope(rt, R);
+          if (m < 0) return make_err(m);
+        }
+        if (m && (Q.flags & RF_HAS_CONDITION)) {
+          out.decision = DEC_INDETERMINATE;
+          out.flags = OF_HOST_COND;
+          out.aux = r;
+          return out;
+        }
+        if (m && Q.target != NONE32) {
+          m = verify_acl(T.targets[Q.target], R);
+          if (m < 0) return make_err(m);
+        }
+        if (m && psm) rf.push(Q.effect, ec_rule ? Q.ec : (uint8_t)EC_FALSE);
+      }
+      if (rf.n) {
+        if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA);
+        sf.push(rf.eff, rf.ec);
+      }
+    }
+    if (sf.n) {
+      if (sf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA);
+      eff = sf.eff;
+      ec = sf.ec;
+      last_set = s + 1;
+    }
+  }
+  if (!last_set) {
+    out.decision = DEC_INDETERMINATE;
+    out.ec = EC_UNDEF;
+    return out;
+  }
+  out.decision = (eff >= EFF_PERMIT && eff <= EFF_UNRECOGNIZED) ? eff : (uint8_t)DEC_INDETERMINATE;
+  out.ec = ec;
+  out.flags = OF_HAS_EFFECT;
+  out.aux = last_set;
+  return out;
+}
+
+// ------------------------------------------------------------------ whatIsAllowed
+// bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
+ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* bits, uint32_t* obl_out,
+                                uint32_t* obl_n) {
+  Req R(T, B, i);
+  Decision out{};
+  OblLog obl{obl_out, 0, false};
+  auto setbit = [&](uint32_t b) { bits[b >> 5] |= 1u << (b & 31); };
+  const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
+  if (R.flag(RQ_HOST)) {
+    out.flags = OF_HOST_REQ;
+    *obl_n = 0;
+    return out;
+  }
+  for (uint32_t s = 0; s < T.n_sets; ++s) {
+    const SetRec S = T.sets[s];
+    if (S.target != NONE32) {
+      tri m = target_match(T.targets[S.target], R, EFF_PERMIT, false, true, &obl);
+      if (m < 0) { *obl_n = 0; return make_err(m); }
+      if (!m) continue;
+    }
+    bool exact = false;
+    uint8_t pe = EFF_UNDEF;
+    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
+      const PolicyRec P = T.pols[p];
+      if (P.flags & PF_NULL) { *obl_n = 0; return make_err(-(tri)ERR_TYPE); }
+      if (P.flags & PF_EFFECT_TRUTHY) pe = P.effect;
+      if (P.target != NONE32) {
+        tri m = target_match(T.targets[P.target], R, pe, false, true, &obl);
+        if (m < 0) { *obl_n = 0; return make_err(m); }
+        if (m) {
+          exact = true;
+          break;
+        }
+      }
+    }
+    if (exact && R.flag(RQ_MULTI_ENT)) {
+      tri m = multiple_entities(S, R);
+      if (m < 0) { *obl_n = 0; return make_err(m); }
+      exact = m != 0;
+    }
+    bool any_pol = false;
+    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
+      const PolicyRec P = T.pols[p];
+      if (P.flags & PF_NULL) continue;
+      if (P.target != NONE32) {
+        tri m = target_match(T.targets[P.target], R, pe, !exact, true, &obl);
+        if (m < 0) { *obl_n = 0; return make_err(m); }
+        if (!m) continue;
+      }
+      bool any_rule = false;
+      for (uint32_t r = P.rule_begin; r < P.rule_end; ++r) {
+        const RuleRec Q = T.rules[r];
+        if (Q.flags & RF_NULL) continue;
+        tri m = 1;
+        if (Q.target != NONE32) {
+          const TargetRec& rt = T.targets[Q.target];
+          m = target_match(rt, R, Q.effect, false, true, &obl);
+          if (m < 0) { *obl_n = 0; return make_err(m); }
+          if (!m) {
+            m = target_match(rt, R, Q.effect, true, true, &obl);
+            if (m < 0) { *obl_n = 0; return make_err(m); }
+          }
+        }
+        if (m) {
+          setbit(rule_base + r);
+          any_rule = true;
+        }
+      }
+      if ((P.flags & PF_EFFECT_TRUTHY) || any_rule) {
+        setbit(pol_base + p);
+        any_pol = true;
+      }
+    }
+    if (any_pol) setbit(s);
+  }
+  *obl_n = obl.n;
+  if (obl.overflow) out.flags |= OF_OBL_OVERFLOW;
+  return out;
+}
+
+}  // namespace acs

@@ -1,0 +1,107 @@
+/* acs_mi355x.h — C ABI of the MI355X access-control evaluator (libacs_mi355x.so).
+ *
+ * Drop-in boundary for the decision path of restorecommerce/access-control-srv:
+ * the reference's AccessController.isAllowed / whatIsAllowed
+ * (src/core/accessController.ts:88-324, 326-427), reached from the gRPC handlers
+ * AccessControlService.isAllowed / whatIsAllowed (src/accessControlService.ts:62-101).
+ * A host shim (Python: acs_mi355x.controller; Node: INTEGRATION.md) keeps the
+ * reference's AccessController surface, compiles its `policySets` Map into a
+ * table image, encodes request batches, and calls these entry points.
+ *
+ * Plain pointers and sizes only.  Return 0 on success, a negative code on
+ * failure with a thread-local message from acs_last_error().  Per-request
+ * reference errors (a rejected isAllowed promise) are NOT ABI errors: they are
+ * reported in the request's acs_decision (flags & ACS_OF_ERR, err kind).
+ */
+#ifndef ACS_MI355X_H
+#define ACS_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACS_BLOB_MAGIC 0x31534341u /* "ACS1" */
+#define ACS_ABI_VERSION 1u
+
+/* Compiled policy-store image (host compiler output, see csrc/acs_layout.h).
+ * Header followed by 16-byte aligned sections in this order:
+ * sets, policies, rules, targets, rule resource attrs, (id,value) pairs, u32 pool. */
+typedef struct {
+  uint32_t magic, version;
+  uint32_t n_sets, n_pols, n_rules, n_targets, n_rres, n_pairs, n_u32pool;
+  uint32_t id_user;
+  uint32_t reserved[6];
+} acs_blob_header;
+
+typedef struct acs_tables acs_tables; /* device-resident tables, immutable once built */
+
+/* One request batch in the packed SoA layout of csrc/acs_layout.h.  The same
+ * struct describes host buffers (acs_is_allowed) or device buffers
+ * (acs_is_allowed_device). */
+typedef struct {
+  uint32_t n;
+  const void* hdr;     /* [n] ReqHdr                         */
+  const void* res;     /* [QMAX][n] ReqRes                   */
+  const void* subj;    /* [SMAX][n] (id,value) u32 pairs     */
+  const void* act;     /* [AMAX][n] (id,value) u32 pairs     */
+  const uint32_t* roles;  /* [RMAX][n]                        */
+  const uint32_t* arena;  /* context arena words               */
+  size_t arena_words;
+  const uint8_t* rx;      /* [rx_cols][rx_rows] regex matrix   */
+  uint32_t rx_cols, rx_rows;
+} acs_req_batch;
+
+/* 8-byte decision record (csrc/acs_layout.h: Decision). */
+typedef struct {
+  uint8_t decision; /* 2 PERMIT 3 DENY 4 NOT_APPLICABLE 5 INDETERMINATE 6 UNRECOGNIZED */
+  uint8_t ec;       /* evaluation_cacheable code */
+  uint8_t flags;    /* ACS_OF_* */
+  uint8_t err;      /* error kind when flags & ACS_OF_ERR */
+  uint32_t aux;     /* 1 + index of the last applicable policy set (0: none) / rule index */
+} acs_decision;
+
+#define ACS_OF_ERR 0x01u
+#define ACS_OF_HOST_COND 0x02u
+#define ACS_OF_HOST_REQ 0x04u
+#define ACS_OF_NO_TARGET 0x08u
+#define ACS_OF_HAS_EFFECT 0x10u
+#define ACS_OF_OBL_OVERFLOW 0x20u
+
+/* Replaces: the in-memory `AccessController.policySets` Map the reference scans
+ * per request (accessController.ts:32,125; loaded by accessControlService.ts:36-54).
+ * Uploads a compiled image to `device`.  NULL on error. */
+acs_tables* acs_compile(const void* blob, size_t n_bytes, int device);
+void acs_free(acs_tables* t);
+
+/* Replaces: AccessController.isAllowed (accessController.ts:88-324), for a batch.
+ * Host buffers in and out; synchronous (H2D, kernel, D2H on an internal stream). */
+int acs_is_allowed(acs_tables* t, const acs_req_batch* host_batch, acs_decision* out);
+
+/* Same, on device-resident buffers, enqueued on `stream` (a hipStream_t; NULL = default). */
+int acs_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, acs_decision* dev_out, void* stream);
+
+/* Replaces: AccessController.whatIsAllowed (accessController.ts:326-427).
+ * bits: [n][words_per_req] inclusion bitsets over (sets | policies | rules);
+ * obl: [n][ACS_OBL_MAX][2] maskedProperty push log (entity id, mask id), obl_n: [n]. */
+#define ACS_OBL_MAX 16
+uint32_t acs_wia_words_per_request(const acs_tables* t);
+int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t* bits, uint32_t* obl,
+                        uint32_t* obl_n, acs_decision* out);
+int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, uint32_t* dev_bits,
+                               uint32_t* dev_obl, uint32_t* dev_obl_n, acs_decision* dev_out, void* stream);
+
+/* Average kernel time (ms) of the last `*_device` launch measured with HIP events on
+ * its stream; -1 if none. */
+float acs_last_kernel_ms(const acs_tables* t);
+
+const char* acs_last_error(void);
+int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 8 packed structs, for host checks */
+int acs_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACS_MI355X_H */
