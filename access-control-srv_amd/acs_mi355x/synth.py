@@ -1,0 +1,355 @@
+"""Seeded synthetic workloads for the benchmark configurations.
+
+Stores are plain ``{policy_sets: [...]}`` documents (the shape ``populate``
+loads).  Request batches are generated directly in the packed layout with
+numpy (vectorised: millions of requests per second), and every request can be
+re-materialised as the JSON request the reference would receive
+(``decode(i)``), which is how the benchmark and the tests check a sample of a
+full-size batch against the CPU oracle.
+
+  c2: 100 sets x 2 policies x 5 rules (1k rules), flat roles, no HR/ACL data.
+  c3: 200 sets x 5 policies x 10 rules (10k rules), mixed CAs, 50% of rules
+      role-scoped to organizations, depth-8 4-ary org tree (21,845 orgs),
+      requests carrying hierarchical_scopes subtrees of it (Euler intervals).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import layout as L
+from .compiler import CompiledStore, Overlay
+from .encoder import RequestBatch
+from .regex import cell
+
+URN = {
+    "role": "urn:restorecommerce:acs:names:role",
+    "subjectID": "urn:oasis:names:tc:xacml:1.0:subject:subject-id",
+    "entity": "urn:restorecommerce:acs:names:model:entity",
+    "property": "urn:restorecommerce:acs:names:model:property",
+    "resourceID": "urn:oasis:names:tc:xacml:1.0:resource:resource-id",
+    "actionID": "urn:oasis:names:tc:xacml:1.0:action:action-id",
+    "rse": "urn:restorecommerce:acs:names:roleScopingEntity",
+    "rsi": "urn:restorecommerce:acs:names:roleScopingInstance",
+    "hrs": "urn:restorecommerce:acs:names:hierarchicalRoleScoping",
+    "ownerEntity": "urn:restorecommerce:acs:names:ownerIndicatoryEntity",
+    "ownerInstance": "urn:restorecommerce:acs:names:ownerInstance",
+}
+ACTIONS = ["urn:restorecommerce:acs:names:action:read", "urn:restorecommerce:acs:names:action:modify",
+           "urn:restorecommerce:acs:names:action:create", "urn:restorecommerce:acs:names:action:delete",
+           "urn:restorecommerce:acs:names:action:execute"]
+CAS = ["urn:oasis:names:tc:xacml:3.0:rule-combining-algorithm:deny-overrides",
+       "urn:oasis:names:tc:xacml:3.0:rule-combining-algorithm:permit-overrides",
+       "urn:oasis:names:tc:xacml:3.0:rule-combining-algorithm:first-applicable"]
+ORG_ENTITY = "urn:restorecommerce:acs:model:organization.Organization"
+N_ENT, N_ROLES, N_PROPS, N_USERS, N_RIDS = 256, 64, 8, 4096, 1024
+
+
+def entity(k):
+    return f"urn:restorecommerce:acs:model:ent{k}.Ent{k}"
+
+
+def prop(k, p):
+    return f"{entity(k)}#p{p}"
+
+
+def role(k):
+    return f"r{k}"
+
+
+def zipf_p(n, s=1.1):
+    w = 1.0 / np.arange(1, n + 1) ** s
+    return w / w.sum()
+
+
+def _ec(rng, r):
+    x = rng.random()
+    if x < 0.5:
+        r["evaluation_cacheable"] = True
+    elif x < 0.75:
+        r["evaluation_cacheable"] = False
+
+
+def _effect(rng):
+    x = rng.random()
+    if x < 0.001:
+        return "Permit"
+    return "PERMIT" if x < 0.7 else "DENY"
+
+
+# ------------------------------------------------------------------ org tree (c3)
+class OrgTree:
+    """Complete ``fanout``-ary tree of depth ``depth`` in preorder; node k is 'org{k}'.
+    Euler tour: subtree(k) = [k, k + size(level(k)))."""
+
+    def __init__(self, fanout=4, depth=8):
+        self.fanout, self.depth = fanout, depth
+        self.level_sizes = [sum(fanout ** i for i in range(depth - d)) for d in range(depth)]
+        self.n = n = self.level_sizes[0]
+        level = np.zeros(n, np.int32)
+        stack = [(0, 0)]
+        while stack:  # preorder ids: the children of x (level d) start at x+1, stride size(d+1)
+            x, d = stack.pop()
+            level[x] = d
+            if d + 1 < depth:
+                stride = self.level_sizes[d + 1]
+                stack.extend((x + 1 + k * stride, d + 1) for k in range(fanout))
+        self.level = level
+        self.size = np.array(self.level_sizes, np.int64)[level]
+
+    def name(self, k):
+        return f"org{k}"
+
+    def subtree_json(self, k, role=None):
+        """hierarchical_scopes entry for the subtree rooted at k (role on the root only)."""
+        def node(x):
+            d = int(self.level[x])
+            out = {"id": self.name(x)}
+            if d + 1 < self.depth:
+                kids, c = [], x + 1
+                for _ in range(self.fanout):
+                    kids.append(node(c))
+                    c += self.level_sizes[d + 1]
+                out["children"] = kids
+            return out
+        n = node(k)
+        if role is not None:
+            n = {"id": n["id"], "role": role, **({"children": n["children"]} if "children" in n else {})}
+        return n
+
+    def contains(self, root, x):
+        return root <= x < root + self.size[root]
+
+
+# ------------------------------------------------------------------ stores
+def c2_store(seed=0xACC0002, n_sets=100, n_pols=2, n_rules=5):
+    rng = np.random.default_rng(seed)
+    pe = zipf_p(N_ENT)
+    pr = zipf_p(N_ROLES)
+    pa = zipf_p(len(ACTIONS))
+    sets = []
+    for s in range(n_sets):
+        pols = []
+        for p in range(n_pols):
+            e = int(rng.choice(N_ENT, p=pe))
+            rules = []
+            for q in range(n_rules):
+                t = {}
+                if rng.random() < 0.9:
+                    t["subjects"] = [{"id": URN["role"], "value": role(int(rng.choice(N_ROLES, p=pr)))}]
+                else:
+                    t["subjects"] = [{"id": URN["subjectID"], "value": f"u{int(rng.integers(N_USERS))}"}]
+                res = [{"id": URN["entity"], "value": entity(e)}]
+                if rng.random() < 0.3:
+                    for pp in sorted(set(rng.integers(0, N_PROPS, size=int(rng.integers(1, 3))).tolist())):
+                        res.append({"id": URN["property"], "value": prop(e, pp)})
+                t["resources"] = res
+                if rng.random() < 0.8:
+                    t["actions"] = [{"id": URN["actionID"], "value": ACTIONS[int(rng.choice(len(ACTIONS), p=pa))]}]
+                r = {"id": f"r{s}_{p}_{q}", "target": t, "effect": _effect(rng)}
+                _ec(rng, r)
+                rules.append(r)
+            pol = {"id": f"p{s}_{p}", "combining_algorithm": CAS[int(rng.integers(3))], "rules": rules}
+            if rng.random() < 0.8:
+                pol["target"] = {"resources": [{"id": URN["entity"], "value": entity(e)}]}
+            if rng.random() < 0.1:
+                pol["effect"] = "PERMIT"
+            pols.append(pol)
+        sets.append({"id": f"s{s}", "combining_algorithm": CAS[int(rng.integers(3))], "policies": pols})
+    return {"policy_sets": sets}
+
+
+def c3_store(seed=0xACC0003, n_sets=200, n_pols=5, n_rules=10):
+    rng = np.random.default_rng(seed)
+    pe, pr, pa = zipf_p(N_ENT), zipf_p(N_ROLES), zipf_p(len(ACTIONS))
+    sets = []
+    for s in range(n_sets):
+        pols = []
+        for p in range(n_pols):
+            e = int(rng.choice(N_ENT, p=pe))
+            rules = []
+            for q in range(n_rules):
+                subs = [{"id": URN["role"], "value": role(int(rng.choice(N_ROLES, p=pr)))}]
+                if rng.random() < 0.5:
+                    subs.append({"id": URN["rse"], "value": ORG_ENTITY})
+                    if rng.random() < 0.25:
+                        subs.append({"id": URN["hrs"], "value": "false"})
+                res = [{"id": URN["entity"], "value": entity(e)}]
+                if rng.random() < 0.3:
+                    for pp in sorted(set(rng.integers(0, N_PROPS, size=int(rng.integers(1, 3))).tolist())):
+                        res.append({"id": URN["property"], "value": prop(e, pp)})
+                t = {"subjects": subs, "resources": res}
+                if rng.random() < 0.8:
+                    t["actions"] = [{"id": URN["actionID"], "value": ACTIONS[int(rng.choice(len(ACTIONS), p=pa))]}]
+                r = {"id": f"r{s}_{p}_{q}", "target": t, "effect": _effect(rng)}
+                _ec(rng, r)
+                rules.append(r)
+            pol = {"id": f"p{s}_{p}", "combining_algorithm": CAS[int(rng.integers(3))], "rules": rules}
+            if rng.random() < 0.8:
+                pol["target"] = {"resources": [{"id": URN["entity"], "value": entity(e)}]}
+            if rng.random() < 0.1:
+                pol["effect"] = "PERMIT"
+            pols.append(pol)
+        sets.append({"id": f"s{s}", "combining_algorithm": CAS[int(rng.integers(3))], "policies": pols})
+    return {"policy_sets": sets}
+
+
+# ------------------------------------------------------------------ requests (packed)
+@dataclass
+class SynthBatch:
+    batch: RequestBatch
+    draws: dict
+    kind: str
+    tree: OrgTree | None = None
+
+    def decode(self, i):
+        """JSON request (post-unmarshall shape) for packed request i."""
+        d = {k: v[i] for k, v in self.draws.items()}
+        e, r, a, u = int(d["ent"]), int(d["role"]), int(d["act"]), int(d["user"])
+        res = [{"id": URN["entity"], "value": entity(e)},
+               {"id": URN["resourceID"], "value": f"res{int(d['rid'])}"}]
+        for k in range(int(d["nprops"])):
+            pe = int(d["prop_ent"][k])
+            res.append({"id": URN["property"], "value": prop(pe, int(d["props"][k]))})
+        req = {"target": {"subjects": [{"id": URN["role"], "value": role(r)},
+                                       {"id": URN["subjectID"], "value": f"u{u}"}],
+                          "resources": res,
+                          "actions": [{"id": URN["actionID"], "value": ACTIONS[a]}]}}
+        subj = {"id": f"u{u}"}
+        if self.kind == "c2":
+            subj["role_associations"] = [{"role": role(r), "attributes": []}]
+            subj["hierarchical_scopes"] = []
+            req["context"] = {"subject": subj, "resources": []}
+        else:
+            t = self.tree
+            scope = int(d["scope"])
+            subj["role_associations"] = [{"role": role(r), "attributes": [
+                {"id": URN["rse"], "value": ORG_ENTITY,
+                 "attributes": [{"id": URN["rsi"], "value": t.name(scope)}]}]}]
+            subj["hierarchical_scopes"] = [t.subtree_json(scope, role(r))]
+            owner = int(d["owner"])
+            req["context"] = {"subject": subj, "resources": [{"id": f"res{int(d['rid'])}", "meta": {"owners": [
+                {"id": URN["ownerEntity"], "value": ORG_ENTITY,
+                 "attributes": [{"id": URN["ownerInstance"], "value": t.name(owner)}]}]}}]}
+        return req
+
+
+def _vocab(cs: CompiledStore, ov: Overlay):
+    I = ov.intern
+    return {
+        "ent": np.array([I(entity(k)) for k in range(N_ENT)], np.uint32),
+        "prop": np.array([[I(prop(k, p)) for p in range(N_PROPS)] for k in range(N_ENT)], np.uint32),
+        "psfx": np.array([I(f"p{p}") for p in range(N_PROPS)], np.uint32),
+        "role": np.array([I(role(k)) for k in range(N_ROLES)], np.uint32),
+        "user": np.array([I(f"u{k}") for k in range(N_USERS)], np.uint32),
+        "rid": np.array([I(f"res{k}") for k in range(N_RIDS)], np.uint32),
+        "act": np.array([I(a) for a in ACTIONS], np.uint32),
+        "urn_role": I(URN["role"]), "urn_subject": I(URN["subjectID"]), "urn_action": I(URN["actionID"]),
+    }
+
+
+def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree | None = None) -> SynthBatch:
+    """Generate n packed requests for config ``kind`` ('c2' or 'c3') against store ``cs``."""
+    rng = np.random.default_rng(seed)
+    ov = Overlay(cs.dictionary)
+    V = _vocab(cs, ov)
+    ent = rng.choice(N_ENT, size=n, p=zipf_p(N_ENT)).astype(np.int32)
+    rol = rng.choice(N_ROLES, size=n, p=zipf_p(N_ROLES)).astype(np.int32)
+    act = rng.choice(len(ACTIONS), size=n, p=zipf_p(len(ACTIONS))).astype(np.int32)
+    usr = rng.integers(0, N_USERS, size=n).astype(np.int32)
+    rid = rng.integers(0, N_RIDS, size=n).astype(np.int32)
+    nprops = rng.integers(0, 4, size=n).astype(np.int32)
+    props = np.stack([rng.permutation(N_PROPS)[:3] for _ in range(min(n, 4096))])[np.arange(n) % min(n, 4096)]
+    prop_ent = np.where(rng.random((n, 3)) < 0.9, ent[:, None], rng.choice(N_ENT, size=(n, 3))).astype(np.int32)
+    draws = {"ent": ent, "role": rol, "act": act, "user": usr, "rid": rid, "nprops": nprops, "props": props,
+             "prop_ent": prop_ent}
+
+    hdr = np.zeros(n, L.REQ_HDR_DT)
+    res = np.zeros((L.QMAX, n), L.REQ_RES_DT)
+    subj = np.zeros((L.SMAX, n), L.PAIR_DT)
+    actp = np.zeros((L.AMAX, n), L.PAIR_DT)
+    roles = np.zeros((L.RMAX, n), np.uint32)
+
+    # regex-matrix columns: one per entity value (column k <-> entity k)
+    rows = cs.rx_rows
+    rx = np.array([[cell(rv, entity(k)) for rv in rows] or [0] for k in range(N_ENT)], np.uint8)
+    # indexOf(entityName(entity k)) over property strings of entity j
+    names = [entity(k)[entity(k).rfind(":") + 1:] for k in range(N_ENT)]
+    cont = np.array([[names[k] in prop(j, 0) for j in range(N_ENT)] for k in range(N_ENT)], bool)
+
+    res["value"][0] = V["ent"][ent]
+    res["kind"][0] = L.K_ENT | L.K_ENT_LOOSE
+    res["col"][0] = ent
+    res["slot_a"][0] = res["slot_b"][0] = L.NONE8
+    res["value"][1] = V["rid"][rid]
+    res["kind"][1] = L.K_RID_LOOSE
+    res["slot_a"][1] = res["slot_b"][1] = L.NONE8
+    for k in range(3):
+        has = nprops > k
+        pe = prop_ent[:, k]
+        pp = props[:, k]
+        res["value"][2 + k] = np.where(has, V["prop"][pe, pp], 0)
+        res["kind"][2 + k] = np.where(has, L.K_PROP | L.K_HAS_HASH, 0)
+        res["hash_sfx"][2 + k] = np.where(has, V["psfx"][pp], 0)
+        res["contains"][2 + k] = np.where(has & cont[ent, pe], 1, 0)
+        res["slot_a"][2 + k] = res["slot_b"][2 + k] = L.NONE8
+    for k in range(5, L.QMAX):
+        res["slot_a"][k] = res["slot_b"][k] = L.NONE8
+    subj["id"][0], subj["value"][0] = V["urn_role"], V["role"][rol]
+    subj["id"][1], subj["value"][1] = V["urn_subject"], V["user"][usr]
+    actp["id"][0], actp["value"][0] = V["urn_action"], V["act"][act]
+    roles[0] = V["role"][rol]
+
+    flags = np.full(n, L.RQ_RA_TRUTHY | L.RQ_HRS_ITERABLE, np.uint32)
+    flags |= np.where(nprops > 0, L.RQ_ANY_PROP, 0).astype(np.uint32)
+    flags |= np.where(act == 2, L.RQ_ACT_CREATE, 0).astype(np.uint32)
+    flags |= np.where((act == 0) | (act == 1) | (act == 3), L.RQ_ACT_RMD, 0).astype(np.uint32)
+    hdr["nres"] = 2 + nprops
+    hdr["nsubj"] = 2
+    hdr["nact"] = 1
+    hdr["nroles"] = 1
+    hdr["subject_id"] = V["user"][usr]
+
+    if kind == "c2":
+        # no context resources: the first resource-id lookup finds no ACLs -> verifyACL true
+        flags |= np.uint32(L.ACL_RET_TRUE << L.RQ_ACL_SHIFT)
+        arena = np.zeros(2, np.uint32)
+        hdr["arena_off"] = 0
+    else:
+        tree = tree or OrgTree()
+        # subject scoped at a random org of depth 0..3, owner inside its subtree with p=0.6
+        lv = rng.integers(0, 4, size=n)
+        scope = np.zeros(n, np.int64)
+        for d in range(4):
+            nodes = np.flatnonzero(tree.level == d)
+            m = lv == d
+            scope[m] = nodes[rng.integers(len(nodes), size=int(m.sum()))]
+        inside = rng.random(n) < 0.6
+        off = (rng.random(n) * tree.size[scope]).astype(np.int64)
+        owner = np.where(inside, scope + off, rng.integers(0, tree.n, size=n))
+        draws.update({"scope": scope, "owner": owner})
+        org_id = np.array([ov.intern(tree.name(k)) for k in range(tree.n)], np.uint32)
+        urn_org = ov.intern(ORG_ENTITY)
+        # arena per request (22 words): counts, 1 grant, 1 rolese, 1 root, 1 hrkey, 1 slot, owner record
+        W = 22
+        ar = np.zeros((n, W), np.uint32)
+        ar[:, 0] = 1 | (1 << 8) | (1 << 16) | (1 << 24)
+        ar[:, 1] = 0 | (1 << 8)
+        ar[:, 2], ar[:, 3], ar[:, 4] = V["role"][rol], urn_org, org_id[scope]        # grant
+        ar[:, 5], ar[:, 6] = V["role"][rol], urn_org                                 # rolese
+        ar[:, 7] = V["role"][rol]                                                    # root raw role
+        ar[:, 8] = V["role"][rol]                                                    # hr key
+        ar[:, 9] = 10                                                                # slot 0 offset
+        ar[:, 10], ar[:, 11] = 0, 1                                                  # owners_empty, n_owners
+        ar[:, 12], ar[:, 13] = 1 | (1 << 8), urn_org                                 # is_oe | 1 attr, value
+        in_sub = (owner >= scope) & (owner < scope + tree.size[scope])
+        ar[:, 14], ar[:, 15], ar[:, 16] = org_id[owner], L.K_OI, in_sub.astype(np.uint32)
+        arena = ar.reshape(-1)
+        hdr["arena_off"] = (np.arange(n, dtype=np.int64) * W).astype(np.uint32)
+        res["slot_a"][1] = 0
+        flags |= np.uint32(L.ACL_RET_TRUE << L.RQ_ACL_SHIFT)  # owners-only meta: no ACLs
+    hdr["flags"] = flags
+    b = RequestBatch(n=n, hdr=hdr, res=res, subj=subj, act=actp, roles=roles, arena=arena, rx=rx,
+                     rx_rows=rx.shape[1], overlay=ov)
+    return SynthBatch(batch=b, draws=draws, kind=kind, tree=tree if kind != "c2" else None)

@@ -507,21 +507,29 @@ class Oracle:
 
     # ------------------------------------------------------------ HR scope
     def _flat_hr(self, scopes, rule_role):
-        """hierarchicalScope.ts:207-220: preorder unique truthy ids of the HR
-        subtrees whose top-level role === ruleRole (descendants unfiltered)."""
+        """hierarchicalScope.ts:207-220: unique truthy ids of the HR subtrees whose
+        top-level role === ruleRole (descendants unfiltered).  Only membership is
+        used by the caller, so it is returned as a set (memoised per request)."""
         if nullish(scopes):
             raise JSTypeError("undefined is not iterable")  # getAllChildNodes(undefined)
+        key = (id(scopes), rule_role if rule_role is UNDEF or isinstance(rule_role, str) else repr(rule_role))
+        memo = getattr(self, "_flat_memo", None)
+        if memo is not None and key in memo:
+            return memo[key]
         roots = [h for h in iterate(scopes) if strict_eq(get(h, "role"), rule_role)]
-        out, seen = [], set()
-
-        def walk(nodes):
-            for h in iterate(nodes):
-                hid = get(h, "id")
-                if truthy(hid) and not js_includes(out, hid):
-                    out.append(hid)
-                if length_gt0(get(h, "children")):
-                    walk(h["children"])
-        walk(roots)
+        out = set()
+        stack = list(reversed(roots))
+        while stack:
+            h = stack.pop()
+            hid = get(h, "id")
+            if truthy(hid):
+                if isinstance(hid, (dict, list)):
+                    raise OracleUnsupported("object-valued HR id")
+                out.add(hid)
+            if length_gt0(get(h, "children")):
+                stack.extend(reversed(iterate(h["children"])))
+        if memo is not None:
+            memo[key] = out
         return out
 
     def _check_hierarchical_scope(self, target, request):
@@ -643,7 +651,7 @@ class Oracle:
                         else:
                             insts.extend(get(a, "value") for a in iterate(oattrs)
                                          if strict_eq(get(a, "id"), self.U("ownerInstance")))
-                if not any(js_includes(insts, org) for org in flat):
+                if not any(isinstance(x, str) and x in flat for x in insts):
                     still.append(k)
             remaining = still
         return not remaining
@@ -799,6 +807,7 @@ class Oracle:
                                          "message": "Access request had no target. Skipping request"}}
         effect = UNDEF
         obligations = []
+        self._flat_memo = {}
         ctx = get(request, "context")
         if truthy(get(get(ctx, "subject"), "token")):
             raise OracleUnsupported("subject token (identity-srv / Redis I/O)")

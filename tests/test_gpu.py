@@ -1,0 +1,171 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+
+* every golden vector (isAllowed + whatIsAllowed) of the reference test suite,
+* randomised stores/requests that exercise the reference's quirks,
+* c2 / c3 / c4 synthetic configurations: a sample vs the oracle and the full
+  batch vs the CPU build of the same core (size-independent consistency),
+* edge shapes: empty batch, ragged sizes, maximum attribute counts, device API.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from kat_utils import load_kats, load_fixture, urns_for, check_asserts  # noqa: E402
+import randgen  # noqa: E402
+import host_core  # noqa: E402
+from diff_utils import oracle_outcome, gpu_outcome, build, norm_rq  # noqa: E402
+from oracle.acs_oracle import Oracle, FULL_URNS, DEFAULT_CAS  # noqa: E402
+from oracle.jsval import OracleUnsupported, JSError  # noqa: E402
+from acs_mi355x import store, compiler, encoder, results, native, synth, layout as L  # noqa: E402
+from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor  # noqa: E402
+
+KATS = load_kats()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    native.load()
+
+
+def gpu_tables(cs):
+    return native.Tables(compiler.store_blob(cs), 0)
+
+
+def test_kats_is_allowed_gpu():
+    by_fx = {}
+    for v in KATS:
+        by_fx.setdefault((v["fixture"], v["urns"]), []).append(v)
+    checked = 0
+    for (fx, u), vecs in by_fx.items():
+        cs = compiler.compile_store(store.populate(load_fixture(fx)), urns_for(vecs[0]), DEFAULT_CAS)
+        t = gpu_tables(cs)
+        ia = [v for v in vecs if v["op"] == "isAllowed"]
+        if ia:
+            b = encoder.Encoder(cs).encode([v["request"] for v in ia])
+            dec = t.is_allowed(b)
+            for v, d in zip(ia, dec):
+                oc = results.outcome(cs, d)
+                if oc[0] == "HOST" and fx == "conditions.yml":
+                    continue
+                assert oc[0] == "OK" and oc[1] == v["expect"]["decision"], (v["spec"], oc)
+                checked += 1
+        wa = [v for v in vecs if v["op"] == "whatIsAllowed"]
+        if wa:
+            b = encoder.Encoder(cs).encode([v["request"] for v in wa])
+            bits, obl, obl_n, out = t.what_is_allowed(b)
+            for k, v in enumerate(wa):
+                rq = results.reverse_query(cs, b.overlay, bits[k], obl[k][:obl_n[k]], out[k])
+                assert check_asserts(rq, v["expect"]["asserts"]) == [], v["spec"]
+                checked += 1
+        t.close()
+    assert checked >= 100
+
+
+@pytest.mark.parametrize("seed", range(0, 400, 4))
+def test_random_diff_gpu(seed):
+    for s in range(seed, seed + 4):
+        urns, doc, reqs = randgen.rand_case(s)
+        o, cs = build(urns, doc)
+        b = encoder.Encoder(cs).encode(reqs)
+        t = gpu_tables(cs)
+        dec = t.is_allowed(b)
+        bits, obl, obl_n, out = t.what_is_allowed(b)
+        t.close()
+        for i, req in enumerate(reqs):
+            got = gpu_outcome(cs, dec[i])
+            if got[0] != "HOST":
+                try:
+                    assert got == oracle_outcome(o, req), (s, i)
+                except OracleUnsupported:
+                    pass
+            try:
+                want = ("OK", norm_rq(o.what_is_allowed(req)))
+            except JSError as e:
+                want = ("ERR", e.kind)
+            except OracleUnsupported:
+                continue
+            try:
+                g = ("OK", norm_rq(results.reverse_query(cs, b.overlay, bits[i], obl[i][:obl_n[i]], out[i])))
+            except results.HostPathRequired:
+                continue
+            except results.EvaluationError as e:
+                g = ("ERR", e.kind)
+            assert g == want, (s, i)
+
+
+def _synth(kind, n):
+    doc = synth.c2_store() if kind == "c2" else synth.c3_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    return doc, cs, synth.requests(cs, n, kind)
+
+
+@pytest.mark.parametrize("kind,n,sample", [("c2", 300_000, 200), ("c3", 60_000, 40)])
+def test_synthetic_config_gpu(kind, n, sample):
+    doc, cs, sb = _synth(kind, n)
+    t = gpu_tables(cs)
+    dec = t.is_allowed(sb.batch)
+    # full batch: identical records to the CPU build of the same core
+    ref = host_core.is_allowed(cs, sb.batch)
+    assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
+    # sample vs the oracle on the decoded JSON requests
+    o = Oracle(FULL_URNS)
+    o.load(doc)
+    idx = np.random.default_rng(7).choice(n, size=sample, replace=False)
+    for i in idx:
+        assert gpu_outcome(cs, dec[i]) == oracle_outcome(o, sb.decode(int(i))), int(i)
+    # decision mix is non-trivial
+    codes = np.bincount(dec["decision"], minlength=7)
+    assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
+    t.close()
+
+
+def test_what_is_allowed_c4_gpu():
+    doc, cs, sb = _synth("c3", 8_000)
+    t = gpu_tables(cs)
+    bits, obl, obl_n, out = t.what_is_allowed(sb.batch)
+    rbits, robl, robl_n, rout = host_core.what_is_allowed(cs, sb.batch)
+    assert np.array_equal(bits, rbits) and np.array_equal(obl_n, robl_n)
+    o = Oracle(FULL_URNS)
+    o.load(doc)
+    for i in np.random.default_rng(3).choice(sb.batch.n, size=8, replace=False):
+        got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], obl[i][:obl_n[i]], out[i]))
+        assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
+    t.close()
+
+
+def test_device_api_and_ragged_sizes():
+    doc, cs, sb = _synth("c2", 70_001)  # not a multiple of the 256-lane block
+    t = gpu_tables(cs)
+    db = DeviceBatch(sb.batch, 0)
+    out = is_allowed_device(t, db)
+    torch.cuda.synchronize()
+    dec = decisions_from_tensor(out)
+    ref = t.is_allowed(sb.batch)
+    assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
+    empty = encoder.Encoder(cs).encode([])
+    assert t.is_allowed(empty).shape == (0,)
+    t.close()
+
+
+def test_max_attribute_counts():
+    urns, doc, _ = randgen.rand_case(11)
+    o, cs = build(urns, doc)
+    ent = randgen.ENTITIES
+    req = {"target": {"subjects": [{"id": randgen.U["role"], "value": "SimpleUser"}] * L.SMAX,
+                      "resources": [{"id": randgen.U["entity"], "value": ent[k % len(ent)]} for k in range(L.QMAX)],
+                      "actions": [{"id": randgen.U["actionID"], "value": randgen.ACTIONS[0]}] * L.AMAX},
+           "context": {"subject": {"id": "Alice", "role_associations": [{"role": "SimpleUser"}] * L.RMAX,
+                                   "hierarchical_scopes": []}, "resources": []}}
+    over = {"target": dict(req["target"], resources=req["target"]["resources"] * 2), "context": req["context"]}
+    b = encoder.Encoder(cs).encode([req, over])
+    t = gpu_tables(cs)
+    dec = t.is_allowed(b)
+    t.close()
+    got = gpu_outcome(cs, dec[0])
+    if got[0] != "HOST":
+        assert got == oracle_outcome(o, req)
+    assert results.outcome(cs, dec[1])[0] == "HOST"  # beyond packed capacity -> host, never wrong

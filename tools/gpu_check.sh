@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: gpu tests, smoke, bench, rocprof kernel-trace.  Each GPU step has its own
+# time limit; a crash/abort/timeout (rc not in {0,1}) stops the script before any further GPU use.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc" >> "$OUT/$name.log"
+  tail -n 3 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"tests smoke bench prof"}
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+    bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 --requests 2000000 --no-cpu-baseline ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+  esac
+done
+echo "== done"
