@@ -86,7 +86,7 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, acs_dec
 /* Replaces: AccessController.whatIsAllowed (accessController.ts:326-427).
  * bits: [n][words_per_req] inclusion bitsets over (sets | policies | rules);
  * obl: [n][ACS_OBL_MAX][2] maskedProperty push log (entity id, mask id), obl_n: [n]. */
-#define ACS_OBL_MAX 16
+#define ACS_OBL_MAX 64
 uint32_t acs_wia_words_per_request(const acs_tables* t);
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t* bits, uint32_t* obl,
                         uint32_t* obl_n, acs_decision* out);
