@@ -104,10 +104,9 @@ def effect_code(e) -> int:
 class CompiledStore:
     urns: dict
     dictionary: Dictionary
-    sets: np.ndarray
-    pols: np.ndarray
-    rules: np.ndarray
-    targets: np.ndarray
+    sets: np.ndarray              # NODE_DT
+    pols: np.ndarray              # NODE_DT
+    rules: np.ndarray             # NODE_DT
     rres: np.ndarray
     pairs: np.ndarray
     u32pool: np.ndarray
@@ -133,8 +132,7 @@ class CompiledStore:
         return len(self.rules)
 
     def table_bytes(self):
-        return sum(a.nbytes for a in (self.sets, self.pols, self.rules, self.targets, self.rres,
-                                      self.pairs, self.u32pool))
+        return sum(a.nbytes for a in (self.sets, self.pols, self.rules, self.rres, self.pairs, self.u32pool))
 
 
 class _Builder:
@@ -147,7 +145,7 @@ class _Builder:
                 raise Unsupported(f"combining algorithm method {m!r}")
             self.ca_map[ca.get("urn", MISSING)] = CA_METHODS[m]
         self.d = Dictionary()
-        self.targets, self.rres, self.pairs, self.u32pool = [], [], [], []
+        self.rres, self.pairs, self.u32pool = [], [], []
         self.rx_index = {}
         self.rx_rows = []
         self.ec_values = [MISSING, None, False, True]
@@ -200,9 +198,10 @@ class _Builder:
             self.pairs.append((self.d.intern(a.get("id", MISSING)), self.d.intern(a.get("value", MISSING))))
         return off
 
-    def target(self, t) -> int:
+    def target(self, t) -> dict:
+        """Inline target fields of a node record ({} when the node has no target)."""
         if t is None or t is MISSING or not truthy(t):
-            return L.NONE32
+            return {}
         if not isinstance(t, dict):
             raise Unsupported("target is not an object")
         subs = self._attrs(t.get("subjects", MISSING) if truthy(t.get("subjects", MISSING)) else [], "subjects")
@@ -285,84 +284,94 @@ class _Builder:
             flags |= L.TF_LASTPROP_STR
             if "#" in last_prop:
                 flags |= L.TF_LASTPROP_HASH
-        rec["flags"] = flags
-        self.targets.append(tuple(rec.get(n, 0) if n != "pad" else (0, 0) for n in L.TARGET_DT.names))
-        return len(self.targets) - 1
+        rec["tflags"] = flags
+        return rec
+
+
+def _node(fields: dict):
+    return tuple(fields.get(n, 0) if n != "pad" else (0, 0, 0) for n in L.NODE_DT.names)
 
 
 def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> CompiledStore:
-    """Snapshot ``policy_sets`` (ordered Map of sets, see store.py) into tables."""
+    """Snapshot ``policy_sets`` (ordered Map of sets, see store.py) into node tables."""
     b = _Builder(urns, combining_algorithms)
     sets, pols, rules = [], [], []
     set_objs, pol_objs, rule_objs = [], [], []
     for ps in policy_sets.values():
         if not isinstance(ps, dict):
             raise Unsupported("null policy set")
-        s_target = b.target(ps.get("target", MISSING))
-        p_begin = len(pols)
+        sn = b.target(ps.get("target", MISSING))
+        sn["nflags"] = L.NF_HAS_TARGET if sn else 0
+        sn["child_begin"] = len(pols)
         combin = ps.get("combinables")
         if not isinstance(combin, dict):
             raise Unsupported("policy set without combinables")
+        pe_at = L.EFF_UNDEF
         for pol in combin.values():
             if pol is None or pol is MISSING:
-                pols.append((L.NONE32, len(rules), len(rules), 0, 0, 0, 0, L.PF_NULL))
+                pols.append(_node({"nflags": L.NF_NULL, "child_begin": len(rules), "child_end": len(rules),
+                                   "fe": len(rules), "pe_at": pe_at}))
                 pol_objs.append(None)
                 continue
-            p_target = b.target(pol.get("target", MISSING))
-            r_begin = len(rules)
+            pn = b.target(pol.get("target", MISSING))
+            nf = L.NF_HAS_TARGET if pn else 0
+            if truthy(pol.get("effect", MISSING)):
+                nf |= L.NF_EFFECT_TRUTHY
+                pe_at = effect_code(pol["effect"])   # accessController.ts:138-140
+            pn.update(nflags=nf, child_begin=len(rules), effect=effect_code(pol.get("effect", MISSING)),
+                      ec=b.ec_code(pol.get("evaluation_cacheable", MISSING)),
+                      ca=b.ca_code(pol.get("combining_algorithm", MISSING)), pe_at=pe_at)
             rcomb = pol.get("combinables")
             if not isinstance(rcomb, dict):
                 raise Unsupported("policy without combinables")
+            fe = None
             for rule in rcomb.values():
                 if rule is None or rule is MISSING:
-                    rules.append((L.NONE32, 0, 0, L.RF_NULL, 0))
+                    rules.append(_node({"nflags": L.NF_NULL}))
                     rule_objs.append(None)
                     continue
-                r_target = b.target(rule.get("target", MISSING))
-                rf = 0
+                rn = b.target(rule.get("target", MISSING))
+                rf = L.NF_HAS_TARGET if rn else 0
                 cond = rule.get("condition", MISSING)
                 clen = len(cond) if isinstance(cond, (str, list)) else get(cond, "length")
                 if truthy(clen):
-                    rf |= L.RF_HAS_CONDITION
+                    rf |= L.NF_HAS_CONDITION
                 ec = b.ec_code(rule.get("evaluation_cacheable", MISSING))
                 if b.ec_truthy[ec]:
-                    rf |= L.RF_EC_TRUTHY
-                if r_target != L.NONE32:
-                    rf |= L.RF_HAS_TARGET
-                rules.append((r_target, effect_code(rule.get("effect", MISSING)), ec, rf, 0))
+                    rf |= L.NF_EC_TRUTHY
+                elif fe is None:
+                    fe = len(rules)  # first non-null rule with falsy evaluation_cacheable
+                rn.update(nflags=rf, effect=effect_code(rule.get("effect", MISSING)), ec=ec)
+                rules.append(_node(rn))
                 rule_objs.append(rule)
-            pf = L.PF_EFFECT_TRUTHY if truthy(pol.get("effect", MISSING)) else 0
-            if p_target != L.NONE32:
-                pf |= L.PF_HAS_TARGET
-            pols.append((p_target, r_begin, len(rules), len(rcomb), effect_code(pol.get("effect", MISSING)),
-                         b.ec_code(pol.get("evaluation_cacheable", MISSING)),
-                         b.ca_code(pol.get("combining_algorithm", MISSING)), pf))
+            pn.update(child_end=len(rules), map_size=len(rcomb), fe=len(rules) if fe is None else fe)
+            pols.append(_node(pn))
             pol_objs.append(pol)
-        sets.append((s_target, p_begin, len(pols), b.ca_code(ps.get("combining_algorithm", MISSING)), (0, 0, 0)))
+        sn.update(child_end=len(pols), ca=b.ca_code(ps.get("combining_algorithm", MISSING)))
+        sets.append(_node(sn))
         set_objs.append(ps)
+
+    def arr(x, dt):
+        return np.array(x, dtype=dt) if x else np.zeros(0, dt)
     cs = CompiledStore(
         urns=b.urns, dictionary=b.d,
-        sets=np.array(sets, dtype=L.SET_DT) if sets else np.zeros(0, L.SET_DT),
-        pols=np.array(pols, dtype=L.POLICY_DT) if pols else np.zeros(0, L.POLICY_DT),
-        rules=np.array(rules, dtype=L.RULE_DT) if rules else np.zeros(0, L.RULE_DT),
-        targets=np.array(b.targets, dtype=L.TARGET_DT) if b.targets else np.zeros(0, L.TARGET_DT),
-        rres=np.array(b.rres, dtype=L.RULE_RES_DT) if b.rres else np.zeros(0, L.RULE_RES_DT),
-        pairs=np.array(b.pairs, dtype=L.PAIR_DT) if b.pairs else np.zeros(0, L.PAIR_DT),
+        sets=arr(sets, L.NODE_DT), pols=arr(pols, L.NODE_DT), rules=arr(rules, L.NODE_DT),
+        rres=arr(b.rres, L.RULE_RES_DT), pairs=arr(b.pairs, L.PAIR_DT),
         u32pool=np.array(b.u32pool, dtype=np.uint32) if b.u32pool else np.zeros(0, np.uint32),
         rx_rows=b.rx_rows, ec_values=b.ec_values, id_user=b.d.intern(b.urn("user")),
         set_objs=set_objs, pol_objs=pol_objs, rule_objs=rule_objs)
-    cs.stats = {"sets": cs.n_sets, "policies": cs.n_pols, "rules": cs.n_rules, "targets": len(cs.targets),
-                "dictionary": len(b.d), "rx_rows": len(b.rx_rows), "table_bytes": cs.table_bytes()}
+    cs.stats = {"sets": cs.n_sets, "policies": cs.n_pols, "rules": cs.n_rules, "dictionary": len(b.d),
+                "rx_rows": len(b.rx_rows), "table_bytes": cs.table_bytes()}
     return cs
 
 
 def store_blob(cs: CompiledStore) -> bytes:
     """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header)."""
     import struct
-    hdr = struct.pack("<16I", 0x31534341, 1, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.targets), len(cs.rres),
-                      len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0)
+    hdr = struct.pack("<16I", 0x31534341, 2, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
+                      len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0, 0)
     parts = [hdr]
-    for a in (cs.sets, cs.pols, cs.rules, cs.targets, cs.rres, cs.pairs, cs.u32pool):
+    for a in (cs.sets, cs.pols, cs.rules, cs.rres, cs.pairs, cs.u32pool):
         b = np.ascontiguousarray(a).tobytes()
         parts.append(b + b"\0" * ((-len(b)) % 16))
     return b"".join(parts)

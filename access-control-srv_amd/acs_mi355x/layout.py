@@ -37,16 +37,13 @@ globals().update(C)
 
 u8, u16, u32 = np.uint8, np.uint16, np.uint32
 
-TARGET_DT = np.dtype([("flags", u32), ("role", u32), ("se", u32), ("subj_off", u32), ("act_off", u32),
-                      ("res_off", u32), ("acl_roles_off", u32), ("last_prop_value", u32),
-                      ("subj_n", u16), ("act_n", u16), ("res_n", u16), ("acl_roles_n", u16),
-                      ("pad", u32, 2)])
+NODE_DT = np.dtype([("tflags", u32), ("role", u32), ("se", u32), ("subj_off", u32), ("act_off", u32),
+                    ("res_off", u32), ("acl_roles_off", u32), ("last_prop_value", u32),
+                    ("subj_n", u16), ("act_n", u16), ("res_n", u16), ("acl_roles_n", u16),
+                    ("child_begin", u32), ("child_end", u32), ("map_size", u32), ("fe", u32),
+                    ("effect", u8), ("ec", u8), ("ca", u8), ("nflags", u8), ("pe_at", u8), ("pad", u8, 3)])
 RULE_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("row", u16), ("kind", u8), ("pad", u8),
                         ("pad2", u32)])
-SET_DT = np.dtype([("target", u32), ("pol_begin", u32), ("pol_end", u32), ("ca", u8), ("pad", u8, 3)])
-POLICY_DT = np.dtype([("target", u32), ("rule_begin", u32), ("rule_end", u32), ("map_size", u32),
-                      ("effect", u8), ("ec", u8), ("ca", u8), ("flags", u8)])
-RULE_DT = np.dtype([("target", u32), ("effect", u8), ("ec", u8), ("flags", u8), ("pad", u8)])
 PAIR_DT = np.dtype([("id", u32), ("value", u32)])
 REQ_HDR_DT = np.dtype([("flags", u32), ("nres", u8), ("nsubj", u8), ("nact", u8), ("nroles", u8),
                        ("arena_off", u32), ("subject_id", u32)])
@@ -54,11 +51,9 @@ REQ_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("col", u16), ("contai
                        ("slot_a", u8), ("slot_b", u8), ("pad", u8)])
 DECISION_DT = np.dtype([("decision", u8), ("ec", u8), ("flags", u8), ("err", u8), ("aux", u32)])
 
-SIZES = {"TargetRec": TARGET_DT.itemsize, "RuleResAttr": RULE_RES_DT.itemsize, "SetRec": SET_DT.itemsize,
-         "PolicyRec": POLICY_DT.itemsize, "RuleRec": RULE_DT.itemsize, "ReqHdr": REQ_HDR_DT.itemsize,
+SIZES = {"NodeRec": NODE_DT.itemsize, "RuleResAttr": RULE_RES_DT.itemsize, "ReqHdr": REQ_HDR_DT.itemsize,
          "ReqRes": REQ_RES_DT.itemsize, "Decision": DECISION_DT.itemsize}
-assert SIZES == {"TargetRec": 48, "RuleResAttr": 16, "SetRec": 16, "PolicyRec": 20, "RuleRec": 8,
-                 "ReqHdr": 16, "ReqRes": 16, "Decision": 8}, SIZES
+assert SIZES == {"NodeRec": 64, "RuleResAttr": 16, "ReqHdr": 16, "ReqRes": 16, "Decision": 8}, SIZES
 
 DECISION_NAMES = {C["DEC_PERMIT"]: "PERMIT", C["DEC_DENY"]: "DENY", C["DEC_NOT_APPLICABLE"]: "NOT_APPLICABLE",
                   C["DEC_INDETERMINATE"]: "INDETERMINATE", C["DEC_UNRECOGNIZED"]: "UNRECOGNIZED"}

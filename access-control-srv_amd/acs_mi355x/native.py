@@ -24,7 +24,7 @@ class ReqBatchC(C.Structure):
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
            "acs_what_is_allowed", "acs_what_is_allowed_device", "acs_last_kernel_ms", "acs_last_error",
-           "acs_layout_sizes", "acs_device_count"]
+           "acs_layout_sizes", "acs_device_count", "acs_set_option"]
 
 
 def _declare(lib):
@@ -44,6 +44,7 @@ def _declare(lib):
     lib.acs_last_kernel_ms.restype = C.c_float
     lib.acs_last_error.restype = C.c_char_p
     lib.acs_layout_sizes.argtypes = [C.POINTER(u32), C.c_int]
+    lib.acs_set_option.argtypes = [vp, C.c_int, C.c_int]
     return lib
 
 
@@ -130,6 +131,10 @@ class Tables:
             if rc != 0:
                 raise RuntimeError(f"acs_what_is_allowed: {last_error(self.lib)}")
         return bits, obl, obl_n, out
+
+    def set_sort(self, enable: bool):
+        if self.lib.acs_set_option(self.h, 1, int(bool(enable))) != 0:
+            raise RuntimeError(last_error(self.lib))
 
     def last_kernel_ms(self):
         return float(self.lib.acs_last_kernel_ms(self.h))

@@ -112,14 +112,14 @@ def reverse_query(cs, overlay, bits_row, obl_pairs, d, reason=None):
         ps = cs.set_objs[s]
         rec = {"combining_algorithm": ps.get("combining_algorithm", MISSING), **_pick(ps, ("id", "target", "effect")),
                "policies": []}
-        for p in range(int(cs.sets[s]["pol_begin"]), int(cs.sets[s]["pol_end"])):
+        for p in range(int(cs.sets[s]["child_begin"]), int(cs.sets[s]["child_end"])):
             if p not in pol_set:
                 continue
             po = cs.pol_objs[p]
             prq = {"combining_algorithm": po.get("combining_algorithm", MISSING),
                    **_pick(po, ("id", "target", "effect", "evaluation_cacheable")), "rules": [],
                    "has_rules": bool(po.get("combinables"))}
-            for r in range(int(cs.pols[p]["rule_begin"]), int(cs.pols[p]["rule_end"])):
+            for r in range(int(cs.pols[p]["child_begin"]), int(cs.pols[p]["child_end"])):
                 if r in rule_set:
                     ro = cs.rule_objs[r]
                     prq["rules"].append({"context_query": ro.get("context_query", MISSING),

@@ -1,12 +1,13 @@
 // acs_eval.h — per-request decision core of the MI355X access-control evaluator.
 //
-// One call evaluates one request against the whole compiled store, in the
-// reference's order (sets -> policies -> rules, Map order), so that decisions,
+// One call evaluates one request against the whole compiled store in the
+// reference's order (sets -> policies -> rules, Map order), so decisions,
 // evaluation_cacheable, whatIsAllowed inclusion bits and the maskedProperty
 // push log are bit-identical to the TypeScript PDP.  The GPU kernels
-// (acs_kernels.hip) run it one request per lane; table records are read
-// through wave-uniform addresses (scalar loads), request data through
-// coalesced [slot][request] SoA arrays.
+// (acs_kernels.hip) run it one request per lane over requests sorted so that a
+// wave shares its entity/role/action: node records are read through
+// wave-uniform addresses (scalar loads of one 64-B record per set/policy/rule),
+// the request's resource attributes live in registers (RQ template).
 //
 // Reference semantics restated (paths in restorecommerce/access-control-srv):
 //   isAllowed                 src/core/accessController.ts:88-324
@@ -36,10 +37,9 @@ struct Pair {
 enum RxBits : uint8_t { RX_HIT = 1, RX_RESET = 2, RX_THROW_TYPE = 4, RX_THROW_SYNTAX = 8, RX_HOST = 16 };
 
 struct Tables {
-  const SetRec* sets;
-  const PolicyRec* pols;
-  const RuleRec* rules;
-  const TargetRec* targets;
+  const NodeRec* sets;
+  const NodeRec* pols;
+  const NodeRec* rules;
   const RuleResAttr* rres;
   const Pair* pairs;
   const uint32_t* u32pool;
@@ -49,13 +49,13 @@ struct Tables {
 
 struct Batch {
   uint32_t n;
-  const ReqHdr* hdr;    // [n]
-  const ReqRes* res;    // [QMAX][n]
-  const Pair* subj;     // [SMAX][n]
-  const Pair* act;      // [AMAX][n]
+  const ReqHdr* hdr;      // [n]
+  const ReqRes* res;      // [QMAX][n]
+  const Pair* subj;       // [SMAX][n]
+  const Pair* act;        // [AMAX][n]
   const uint32_t* roles;  // [RMAX][n]
   const uint32_t* arena;
-  const uint8_t* rx;    // [cols][rx_rows]
+  const uint8_t* rx;      // [cols][rx_rows]
   uint32_t rx_rows;
 };
 
@@ -85,17 +85,18 @@ struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
   bool overflow;
 };
 
-struct Req {
+// ------------------------------------------------------------------ request views
+// Context arena + headers shared by both request views.
+struct ReqCtx {
   const Tables& T;
   const Batch& B;
   uint32_t i;
   ReqHdr h;
-  const uint32_t* ar;  // context arena of this request
+  const uint32_t* ar;
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
 
-  ACS_FN Req(const Tables& t, const Batch& b, uint32_t idx) : T(t), B(b), i(idx) {
-    h = B.hdr[i];
+  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : T(t), B(b), i(idx), h(hd) {
     ar = B.arena + h.arena_off;
     uint32_t c0 = ar[0], c1 = ar[1];
     n_grants = c0 & 0xFF; n_rolese = (c0 >> 8) & 0xFF; n_slots = (c0 >> 16) & 0xFF; n_roots = c0 >> 24;
@@ -107,7 +108,6 @@ struct Req {
     slotoff = hrkeys + n_hrkeys;
     tse = slotoff + n_slots;
   }
-  ACS_FN ReqRes res(uint32_t j) const { return B.res[(size_t)j * B.n + i]; }
   ACS_FN Pair subj(uint32_t j) const { return B.subj[(size_t)j * B.n + i]; }
   ACS_FN Pair act(uint32_t j) const { return B.act[(size_t)j * B.n + i]; }
   ACS_FN uint32_t role(uint32_t j) const { return B.roles[(size_t)j * B.n + i]; }
@@ -115,14 +115,32 @@ struct Req {
   ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
 };
 
+// Resource attributes staged in LDS by the kernel (slots < LDS_SLOTS, column = lane,
+// stride = block size): dynamic indexing without scratch, one ds_read_b128 per use.
+constexpr int LDS_SLOTS = 8;
+
+struct ReqLds : ReqCtx {
+  const ReqRes* col;  // this lane's LDS column
+  uint32_t stride;
+  ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st)
+      : ReqCtx(t, b, idx, hd), col(c), stride(st) {}
+  ACS_FN ReqRes res(int j) const { return j < LDS_SLOTS ? col[j * stride] : B.res[(size_t)j * B.n + i]; }
+};
+
+// Resource attributes read from HBM on every use (host build of the core).
+struct ReqMem : ReqCtx {
+  ACS_FN ReqMem(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : ReqCtx(t, b, idx, hd) {}
+  ACS_FN ReqRes res(int j) const { return B.res[(size_t)j * B.n + i]; }
+};
+
 // ------------------------------------------------------------------ attributesMatch (loose ==)
-ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const Req& R, bool subjects) {
-  uint32_t qn = subjects ? R.h.nsubj : R.h.nact;
+ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const ReqCtx& R, bool subjects) {
+  const uint32_t qn = subjects ? R.h.nsubj : R.h.nact;
   for (uint32_t k = 0; k < rn; ++k) {
-    Pair a = rule[k];
+    const Pair a = rule[k];
     bool found = false;
     for (uint32_t j = 0; j < qn && !found; ++j) {
-      Pair q = subjects ? R.subj(j) : R.act(j);
+      const Pair q = subjects ? R.subj(j) : R.act(j);
       found = loose_eq(q.id, a.id) && loose_eq(q.value, a.value);
     }
     if (!found) return false;
@@ -131,9 +149,9 @@ ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const Req& R, bool subjec
 }
 
 // ------------------------------------------------------------------ checkSubjectMatches
-ACS_FN bool subject_match(const TargetRec& t, const Req& R) {
-  if (t.flags & TF_SUBJ_EMPTY) return true;
-  if (t.flags & TF_SUBJ_ROLE) {
+ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
+  if (t.tflags & TF_SUBJ_EMPTY) return true;
+  if (t.tflags & TF_SUBJ_ROLE) {
     if (!R.flag(RQ_RA_TRUTHY)) return false;
     for (uint32_t k = 0; k < R.h.nroles; ++k)
       if (R.role(k) == t.role) return true;
@@ -144,13 +162,15 @@ ACS_FN bool subject_match(const TargetRec& t, const Req& R) {
 
 // ------------------------------------------------------------------ resourceAttributesMatch
 // Request attrs [j0, j1) with requestPropertiesExist = rpe.  wia: 'whatIsAllowed' op.
-ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool regex, bool wia,
-                          uint32_t j0, uint32_t j1, bool rpe, OblLog* obl) {
-  if (t.flags & TF_RES_EMPTY) return 1;
+template <class RQ>
+ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool regex, bool wia, int j0, int j1,
+                          bool rpe, OblLog* obl) {
+  if (t.tflags & TF_RES_EMPTY) return 1;
   const RuleResAttr* ra = R.T.rres + t.res_off;
   bool em = false, pm = false, rp = false, om = false, skip_deny = true;
-  uint32_t ent_j = 0;
-  for (uint32_t j = j0; j < j1; ++j) {
+  int ent_j = 0;
+  uint32_t ent_val = 0;
+  for (int j = j0; j < j1; ++j) {
     const ReqRes q = R.res(j);
     pm = false;
     for (uint32_t k = 0; k < t.res_n; ++k) {
@@ -160,6 +180,7 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
         if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
           em = true;
           ent_j = j;
+          ent_val = q.value;
         } else if ((q.kind & K_OP) && (r.kind & K_OP) && q.value == r.value) {
           om = true;
         } else if (em && (q.kind & K_PROP) && (r.kind & K_PROP)) {
@@ -171,11 +192,11 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
         }
       } else {
         if ((q.kind & K_ENT) && (r.kind & K_ENT)) {
-          uint8_t c = R.rx(q.col, r.row);
+          const uint8_t c = R.rx(q.col, r.row);
           if (c & RX_THROW_TYPE) return -(tri)ERR_TYPE;
           if (c & RX_THROW_SYNTAX) return -(tri)ERR_REGEX_SYNTAX;
           if (c & RX_HOST) return -(tri)ERR_REGEX_HOST;
-          ent_j = j;
+          ent_val = q.value;
           if (c & RX_RESET) em = false;
           if (c & RX_HIT) em = true;
         } else if (em && (q.kind & K_PROP) && (r.kind & K_PROP)) {
@@ -189,9 +210,9 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
       if (effect == EFF_PERMIT && scope && em && rp && !pm) return 0;
     } else {
       // maskedProperty pushes (accessController.ts:592-640)
-      bool permit_mask = effect == EFF_PERMIT && scope && em && rp && !pm;
+      const bool permit_mask = effect == EFF_PERMIT && scope && em && rp && !pm;
       if (permit_mask && !rpe) return 0;
-      bool deny_mask = effect == EFF_DENY && scope && em && rp && (pm || !rpe);
+      const bool deny_mask = effect == EFF_DENY && scope && em && rp && (pm || !rpe);
       if (permit_mask || deny_mask) {
         uint32_t mask;
         bool no_hash;
@@ -200,7 +221,7 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
           no_hash = !(q.kind & K_HAS_HASH);
         } else if (!rpe) {
           mask = t.last_prop_value;
-          no_hash = (t.flags & TF_LASTPROP_STR) && !(t.flags & TF_LASTPROP_HASH);
+          no_hash = (t.tflags & TF_LASTPROP_STR) && !(t.tflags & TF_LASTPROP_HASH);
         } else {
           mask = ID_UNDEF;
           no_hash = false;
@@ -208,7 +229,7 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
         if (!no_hash && obl) {
           if (obl->n < (uint32_t)OBL_MAX) {
             if (obl->out) {
-              obl->out[2 * obl->n] = R.res(ent_j).value;
+              obl->out[2 * obl->n] = ent_val;
               obl->out[2 * obl->n + 1] = mask;
             }
             obl->n++;
@@ -225,23 +246,24 @@ ACS_FN tri resource_match(const TargetRec& t, const Req& R, uint8_t effect, bool
 }
 
 // ------------------------------------------------------------------ targetMatches
-ACS_FN tri target_match(const TargetRec& t, const Req& R, uint8_t effect, bool regex, bool wia, OblLog* obl) {
+template <class RQ>
+ACS_FN tri target_match(const NodeRec& t, const RQ& R, uint8_t effect, bool regex, bool wia, OblLog* obl) {
   if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;  // requestTarget.subjects of undefined
   if (!subject_match(t, R)) return 0;
   if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
-  return resource_match(t, R, effect == EFF_UNDEF ? EFF_PERMIT : effect, regex, wia, 0, R.h.nres,
+  return resource_match(t, R, effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect, regex, wia, 0, R.h.nres,
                         R.flag(RQ_ANY_PROP), obl);
 }
 
 // ------------------------------------------------------------------ checkHierarchicalScope
-ACS_FN const uint32_t* slot_rec(const Req& R, uint32_t slot) { return R.ar + R.slotoff[slot]; }
+ACS_FN const uint32_t* slot_rec(const ReqCtx& R, uint32_t slot) { return R.ar + R.slotoff[slot]; }
 
-ACS_FN bool hr_direct(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
+ACS_FN bool hr_direct(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   const uint32_t* rec = slot_rec(R, slot);
-  uint32_t n_owners = rec[1];
+  const uint32_t n_owners = rec[1];
   const uint32_t* p = rec + 2;
   for (uint32_t o = 0; o < n_owners; ++o) {
-    uint32_t w = p[0], val = p[1], na = w >> 8;
+    const uint32_t w = p[0], val = p[1], na = w >> 8;
     const uint32_t* at = p + 2;
     if ((w & 1u) && val == se) {
       for (uint32_t g = 0; g < R.n_grants; ++g) {
@@ -256,7 +278,7 @@ ACS_FN bool hr_direct(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
   return false;
 }
 
-ACS_FN bool hr_tree(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
+ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   bool rse = false;
   for (uint32_t k = 0; k < R.n_rolese && !rse; ++k) rse = R.rolese[2 * k] == role && R.rolese[2 * k + 1] == se;
   if (!rse) return false;
@@ -265,10 +287,10 @@ ACS_FN bool hr_tree(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
     if (R.roots[r] == role) mask |= 1u << r;
   if (!mask) return false;
   const uint32_t* rec = slot_rec(R, slot);
-  uint32_t n_owners = rec[1];
+  const uint32_t n_owners = rec[1];
   const uint32_t* p = rec + 2;
   for (uint32_t o = 0; o < n_owners; ++o) {
-    uint32_t w = p[0], val = p[1], na = w >> 8;
+    const uint32_t w = p[0], val = p[1], na = w >> 8;
     const uint32_t* at = p + 2;
     if ((w & 1u) && val == se)
       for (uint32_t a = 0; a < na; ++a)
@@ -278,8 +300,9 @@ ACS_FN bool hr_tree(const Req& R, uint32_t slot, uint32_t role, uint32_t se) {
   return false;
 }
 
-ACS_FN tri hierarchical_scope(const TargetRec& t, const Req& R) {
-  if (t.flags & TF_HR_TRIVIAL) return 1;
+template <class RQ>
+ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
+  if (t.tflags & TF_HR_TRIVIAL) return 1;
   if (R.flag(RQ_CTX_EMPTY)) return 0;
   bool all_direct = true, all_ok = true;
   const RuleResAttr* ra = R.T.rres + t.res_off;
@@ -287,40 +310,36 @@ ACS_FN tri hierarchical_scope(const TargetRec& t, const Req& R) {
     const RuleResAttr r = ra[k];
     if (r.kind & K_ENT_LOOSE) {
       bool em = false;
-      for (uint32_t j = 0; j < R.h.nres; ++j) {
+      for (int j = 0; j < (int)R.h.nres; ++j) {
         const ReqRes q = R.res(j);
-        uint32_t slot = NONE8;
         if (q.kind & K_ENT_LOOSE) {
           if (loose_eq(q.value, r.value)) {
             em = true;
           } else {
-            uint8_t c = R.rx(q.col, r.row);
+            const uint8_t c = R.rx(q.col, r.row);
             if (c & RX_THROW_TYPE) return -(tri)ERR_TYPE;
             if (c & RX_THROW_SYNTAX) return -(tri)ERR_REGEX_SYNTAX;
             if (c & RX_HOST) return -(tri)ERR_REGEX_HOST;
             if (c & RX_RESET) em = false;
             if (c & RX_HIT) em = true;
           }
-          continue;
         } else if ((q.kind & K_RID_LOOSE) && em) {
-          slot = q.slot_a;
-        } else {
-          continue;
+          const uint32_t slot = q.slot_a;
+          if (slot == NONE8) return 0;
+          if (slot_rec(R, slot)[0]) return 0;  // owners missing
+          const bool d = hr_direct(R, slot, t.role, t.se);
+          all_direct = all_direct && d;
+          all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
         }
-        if (slot == NONE8) return 0;
-        if (slot_rec(R, slot)[0]) return 0;  // owners missing
-        bool d = hr_direct(R, slot, t.role, t.se);
-        all_direct = all_direct && d;
-        all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
       }
     } else if (r.kind & K_OP) {
-      for (uint32_t j = 0; j < R.h.nres; ++j) {
+      for (int j = 0; j < (int)R.h.nres; ++j) {
         const ReqRes q = R.res(j);
         if (!((q.kind & K_OP) && q.value == r.value)) continue;
-        uint32_t slot = q.slot_b;
+        const uint32_t slot = q.slot_b;
         if (slot == NONE8) return 0;
         if (slot_rec(R, slot)[0]) return 0;
-        bool d = hr_direct(R, slot, t.role, t.se);
+        const bool d = hr_direct(R, slot, t.role, t.se);
         all_direct = all_direct && d;
         all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
       }
@@ -328,7 +347,7 @@ ACS_FN tri hierarchical_scope(const TargetRec& t, const Req& R) {
   }
   if (R.flag(RQ_RA_EMPTY)) return 0;
   if (all_direct) return 1;
-  if (!(t.flags & TF_HR_CHECK)) return 0;
+  if (!(t.tflags & TF_HR_CHECK)) return 0;
   if (!R.flag(RQ_HRS_ITERABLE)) return -(tri)ERR_TYPE;  // getAllChildNodes(undefined)
   return all_ok ? 1 : 0;
 }
@@ -340,9 +359,9 @@ ACS_FN bool in_list(const uint32_t* l, uint32_t n, uint32_t v) {
   return false;
 }
 
-ACS_FN tri verify_acl(const TargetRec& t, const Req& R) {
-  if (t.flags & TF_ACL_SKIP) return 1;
-  uint32_t st = (R.h.flags >> RQ_ACL_SHIFT) & 3u;
+ACS_FN tri verify_acl(const NodeRec& t, const ReqCtx& R) {
+  if (t.tflags & TF_ACL_SKIP) return 1;
+  const uint32_t st = (R.h.flags >> RQ_ACL_SHIFT) & 3u;
   if (st == ACL_RET_TRUE) return 1;
   if (st == ACL_RET_FALSE) return 0;
   if (R.flag(RQ_SUBJ_MISSING)) return -(tri)ERR_TYPE;
@@ -374,8 +393,7 @@ ACS_FN tri verify_acl(const TargetRec& t, const Req& R) {
             continue;
           }
           bool was = false;
-          for (uint32_t y = 0; y < ni && !was; ++y)
-            was = ((validated >> y) & 1u) && inst[2 * y] == inst[2 * x];
+          for (uint32_t y = 0; y < ni && !was; ++y) was = ((validated >> y) & 1u) && inst[2 * y] == inst[2 * x];
           if (!was) {
             valid = false;
             break;
@@ -407,19 +425,18 @@ ACS_FN tri verify_acl(const TargetRec& t, const Req& R) {
 }
 
 // ------------------------------------------------------------------ checkMultipleEntitiesMatch
-ACS_FN tri multiple_entities(const SetRec& S, const Req& R) {
-  for (uint32_t j = 0; j < R.h.nres; ++j) {
+template <class RQ>
+ACS_FN tri multiple_entities(const NodeRec& S, const RQ& R) {
+  for (int j = 0; j < (int)R.h.nres; ++j) {
     const ReqRes q = R.res(j);
     if (!(q.kind & K_ENT)) continue;
     bool multi = false;
-    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
-      const PolicyRec P = R.T.pols[p];
-      if (P.flags & PF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
-      if (P.target == NONE32) continue;
-      const TargetRec& t = R.T.targets[P.target];
-      if (t.res_n == 0) continue;
-      uint8_t pe = (P.flags & PF_EFFECT_TRUTHY) ? P.effect : EFF_UNDEF;  // no PERMIT default here
-      tri m = resource_match(t, R, pe, false, false, j, j + 1, (q.kind & K_PROP) != 0, nullptr);
+    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+      const NodeRec P = R.T.pols[p];
+      if (P.nflags & NF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
+      if (!(P.nflags & NF_HAS_TARGET) || P.res_n == 0) continue;
+      const uint8_t pe = (P.nflags & NF_EFFECT_TRUTHY) ? P.effect : (uint8_t)EFF_UNDEF;  // no PERMIT default
+      const tri m = resource_match(P, R, pe, false, false, j, j + 1, (q.kind & K_PROP) != 0, nullptr);
       if (m < 0) return m;
       if (m) multi = true;
     }
@@ -437,38 +454,28 @@ ACS_FN Decision make_err(tri e) {
   return d;
 }
 
-ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
-  Req R(T, B, i);
+template <class RQ>
+ACS_FN Decision is_allowed_t(const RQ& R) {
+  const Tables& T = R.T;
   Decision out{};
-  if (R.flag(RQ_HOST)) {
-    out.decision = DEC_INDETERMINATE;
-    out.flags = OF_HOST_REQ;
-    return out;
-  }
-  if (R.flag(RQ_NO_TARGET)) {
-    out.decision = DEC_DENY;
-    out.ec = EC_FALSE;
-    out.flags = OF_NO_TARGET;
-    return out;
-  }
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;
   for (uint32_t s = 0; s < T.n_sets; ++s) {
-    const SetRec S = T.sets[s];
-    if (S.target != NONE32) {
-      tri m = target_match(T.targets[S.target], R, EFF_PERMIT, false, false, nullptr);
+    const NodeRec S = T.sets[s];
+    if (S.nflags & NF_HAS_TARGET) {
+      const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
       if (m < 0) return make_err(m);
       if (!m) continue;
     }
-    // loop 2a: policyEffect prefix + first exact policy match (accessController.ts:136-157)
+    // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
     bool exact = false;
     uint8_t pe = EFF_UNDEF;
-    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
-      const PolicyRec P = T.pols[p];
-      if (P.flags & PF_NULL) return make_err(-(tri)ERR_TYPE);
-      if (P.flags & PF_EFFECT_TRUTHY) pe = P.effect;
-      if (P.target != NONE32) {
-        tri m = target_match(T.targets[P.target], R, pe, false, false, nullptr);
+    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+      const NodeRec P = T.pols[p];
+      if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+      pe = P.pe_at;
+      if (P.nflags & NF_HAS_TARGET) {
+        const tri m = target_match(P, R, pe, false, false, nullptr);
         if (m < 0) return make_err(m);
         if (m) {
           exact = true;
@@ -477,60 +484,57 @@ ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
       }
     }
     if (exact && R.flag(RQ_MULTI_ENT)) {
-      tri m = multiple_entities(S, R);
+      const tri m = multiple_entities(S, R);
       if (m < 0) return make_err(m);
       exact = m != 0;
     }
     Fold sf(S.ca);
-    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
-      const PolicyRec P = T.pols[p];
-      if (P.flags & PF_NULL) continue;
+    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+      const NodeRec P = T.pols[p];
+      if (P.nflags & NF_NULL) continue;
       bool psm = true;
-      if (P.target != NONE32) {
-        const TargetRec& pt = T.targets[P.target];
-        tri m = target_match(pt, R, pe, !exact, false, nullptr);
+      if (P.nflags & NF_HAS_TARGET) {
+        const tri m = target_match(P, R, pe, !exact, false, nullptr);
         if (m < 0) return make_err(m);
         if (!m) continue;
-        if (pt.flags & TF_HAS_SUBJECTS) {
-          tri h = hierarchical_scope(pt, R);
+        if (P.tflags & TF_HAS_SUBJECTS) {
+          const tri h = hierarchical_scope(P, R);
           if (h < 0) return make_err(h);
           psm = h != 0;
         }
       }
-      if (P.map_size == 0 && (P.flags & PF_EFFECT_TRUTHY)) {
+      if (P.map_size == 0 && (P.nflags & NF_EFFECT_TRUTHY)) {
         sf.push(P.effect, P.ec);
         continue;
       }
       Fold rf(P.ca);
-      bool ec_rule = true;
-      for (uint32_t r = P.rule_begin; r < P.rule_end; ++r) {
-        const RuleRec Q = T.rules[r];
-        if (Q.flags & RF_NULL) continue;
-        if (!(Q.flags & RF_EC_TRUTHY)) ec_rule = false;
+      for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
+        const NodeRec Q = T.rules[r];
+        if (Q.nflags & NF_NULL) continue;
         tri m = 1;
-        if (Q.target != NONE32) {
-          const TargetRec& rt = T.targets[Q.target];
-          m = target_match(rt, R, Q.effect, false, false, nullptr);
+        if (Q.nflags & NF_HAS_TARGET) {
+          m = target_match(Q, R, Q.effect, false, false, nullptr);
           if (m < 0) return make_err(m);
           if (!m) {
-            m = target_match(rt, R, Q.effect, true, false, nullptr);
+            m = target_match(Q, R, Q.effect, true, false, nullptr);
             if (m < 0) return make_err(m);
           }
           if (!m) continue;
-          m = hierarchical_scope(rt, R);
+          m = hierarchical_scope(Q, R);
           if (m < 0) return make_err(m);
         }
-        if (m && (Q.flags & RF_HAS_CONDITION)) {
+        if (m && (Q.nflags & NF_HAS_CONDITION)) {
           out.decision = DEC_INDETERMINATE;
           out.flags = OF_HOST_COND;
           out.aux = r;
           return out;
         }
-        if (m && Q.target != NONE32) {
-          m = verify_acl(T.targets[Q.target], R);
+        if (m && (Q.nflags & NF_HAS_TARGET)) {
+          m = verify_acl(Q, R);
           if (m < 0) return make_err(m);
         }
-        if (m && psm) rf.push(Q.effect, ec_rule ? Q.ec : (uint8_t)EC_FALSE);
+        // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
+        if (m && psm) rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
       }
       if (rf.n) {
         if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA);
@@ -556,36 +560,56 @@ ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
   return out;
 }
 
-// ------------------------------------------------------------------ whatIsAllowed
-// bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
-ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* bits, uint32_t* obl_out,
-                                uint32_t* obl_n) {
-  Req R(T, B, i);
+ACS_FN Decision early_decision(const ReqHdr& h, bool* done) {
   Decision out{};
-  OblLog obl{obl_out, 0, false};
-  auto setbit = [&](uint32_t b) { bits[b >> 5] |= 1u << (b & 31); };
-  const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
-  if (R.flag(RQ_HOST)) {
+  *done = true;
+  if (h.flags & RQ_HOST) {
+    out.decision = DEC_INDETERMINATE;
     out.flags = OF_HOST_REQ;
-    *obl_n = 0;
     return out;
   }
+  if (h.flags & RQ_NO_TARGET) {
+    out.decision = DEC_DENY;
+    out.ec = EC_FALSE;
+    out.flags = OF_NO_TARGET;
+    return out;
+  }
+  *done = false;
+  return out;
+}
+
+ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
+  const ReqHdr h = B.hdr[i];
+  bool done;
+  Decision d = early_decision(h, &done);
+  if (done) return d;
+  return is_allowed_t(ReqMem(T, B, i, h));
+}
+
+// ------------------------------------------------------------------ whatIsAllowed
+// bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
+template <class RQ>
+ACS_FN Decision what_is_allowed_t(const RQ& R, uint32_t* bits, OblLog& obl) {
+  const Tables& T = R.T;
+  Decision out{};
+  auto setbit = [&](uint32_t b) { bits[b >> 5] |= 1u << (b & 31); };
+  const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
   for (uint32_t s = 0; s < T.n_sets; ++s) {
-    const SetRec S = T.sets[s];
-    if (S.target != NONE32) {
-      tri m = target_match(T.targets[S.target], R, EFF_PERMIT, false, true, &obl);
-      if (m < 0) { *obl_n = 0; return make_err(m); }
+    const NodeRec S = T.sets[s];
+    if (S.nflags & NF_HAS_TARGET) {
+      const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
+      if (m < 0) return make_err(m);
       if (!m) continue;
     }
     bool exact = false;
     uint8_t pe = EFF_UNDEF;
-    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
-      const PolicyRec P = T.pols[p];
-      if (P.flags & PF_NULL) { *obl_n = 0; return make_err(-(tri)ERR_TYPE); }
-      if (P.flags & PF_EFFECT_TRUTHY) pe = P.effect;
-      if (P.target != NONE32) {
-        tri m = target_match(T.targets[P.target], R, pe, false, true, &obl);
-        if (m < 0) { *obl_n = 0; return make_err(m); }
+    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+      const NodeRec P = T.pols[p];
+      if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+      pe = P.pe_at;
+      if (P.nflags & NF_HAS_TARGET) {
+        const tri m = target_match(P, R, pe, false, true, &obl);
+        if (m < 0) return make_err(m);
         if (m) {
           exact = true;
           break;
@@ -593,31 +617,30 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
       }
     }
     if (exact && R.flag(RQ_MULTI_ENT)) {
-      tri m = multiple_entities(S, R);
-      if (m < 0) { *obl_n = 0; return make_err(m); }
+      const tri m = multiple_entities(S, R);
+      if (m < 0) return make_err(m);
       exact = m != 0;
     }
     bool any_pol = false;
-    for (uint32_t p = S.pol_begin; p < S.pol_end; ++p) {
-      const PolicyRec P = T.pols[p];
-      if (P.flags & PF_NULL) continue;
-      if (P.target != NONE32) {
-        tri m = target_match(T.targets[P.target], R, pe, !exact, true, &obl);
-        if (m < 0) { *obl_n = 0; return make_err(m); }
+    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+      const NodeRec P = T.pols[p];
+      if (P.nflags & NF_NULL) continue;
+      if (P.nflags & NF_HAS_TARGET) {
+        const tri m = target_match(P, R, pe, !exact, true, &obl);
+        if (m < 0) return make_err(m);
         if (!m) continue;
       }
       bool any_rule = false;
-      for (uint32_t r = P.rule_begin; r < P.rule_end; ++r) {
-        const RuleRec Q = T.rules[r];
-        if (Q.flags & RF_NULL) continue;
+      for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
+        const NodeRec Q = T.rules[r];
+        if (Q.nflags & NF_NULL) continue;
         tri m = 1;
-        if (Q.target != NONE32) {
-          const TargetRec& rt = T.targets[Q.target];
-          m = target_match(rt, R, Q.effect, false, true, &obl);
-          if (m < 0) { *obl_n = 0; return make_err(m); }
+        if (Q.nflags & NF_HAS_TARGET) {
+          m = target_match(Q, R, Q.effect, false, true, &obl);
+          if (m < 0) return make_err(m);
           if (!m) {
-            m = target_match(rt, R, Q.effect, true, true, &obl);
-            if (m < 0) { *obl_n = 0; return make_err(m); }
+            m = target_match(Q, R, Q.effect, true, true, &obl);
+            if (m < 0) return make_err(m);
           }
         }
         if (m) {
@@ -625,16 +648,29 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
           any_rule = true;
         }
       }
-      if ((P.flags & PF_EFFECT_TRUTHY) || any_rule) {
+      if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
         setbit(pol_base + p);
         any_pol = true;
       }
     }
     if (any_pol) setbit(s);
   }
-  *obl_n = obl.n;
   if (obl.overflow) out.flags |= OF_OBL_OVERFLOW;
   return out;
+}
+
+ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* bits, uint32_t* obl_out,
+                                uint32_t* obl_n) {
+  const ReqHdr h = B.hdr[i];
+  OblLog obl{obl_out, 0, false};
+  Decision d{};
+  if (h.flags & RQ_HOST) {
+    d.flags = OF_HOST_REQ;
+  } else {
+    d = what_is_allowed_t(ReqMem(T, B, i, h), bits, obl);
+  }
+  *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
+  return d;
 }
 
 }  // namespace acs

@@ -15,6 +15,8 @@
 #include "../../include/acs_mi355x.h"
 #include "acs_eval.h"
 
+#include <hipcub/hipcub.hpp>
+
 using namespace acs;
 
 namespace {
@@ -34,22 +36,71 @@ int fail(const std::string& msg) {
 
 constexpr int BLOCK = 256;
 
-__global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, Decision* __restrict__ out) {
-  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= B.n) return;
-  out[i] = is_allowed(T, B, i);
+// Sort key that makes a wave share its entity, role and action (so table-driven
+// branches are wave-uniform): [entity id:15 | role id:10 | action id:7].
+__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __restrict__ keys,
+                                                          uint32_t* __restrict__ idx) {
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= B.n) return;
+  const ReqHdr h = B.hdr[k];
+  uint32_t ent = 0;
+  for (uint32_t j = 0; j < h.nres; ++j) {
+    const ReqRes q = B.res[(size_t)j * B.n + k];
+    if (q.kind & K_ENT) {
+      ent = q.value;
+      break;
+    }
+  }
+  const uint32_t role = h.nroles ? B.roles[k] : 0u;
+  const uint32_t act = h.nact ? B.act[k].value : 0u;
+  keys[k] = ((ent & 0x7FFFu) << 17) | ((role & 0x3FFu) << 7) | (act & 0x7Fu);
+  idx[k] = k;
 }
 
-__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, uint32_t words,
-                                                                uint32_t* __restrict__ bits,
+// K1: one request per lane; its resource attributes are staged in this lane's LDS column.
+__global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+                                                           Decision* __restrict__ out) {
+  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= B.n) return;
+  const uint32_t i = perm ? perm[k] : k;
+  const ReqHdr h = B.hdr[i];
+  bool done;
+  Decision d = early_decision(h, &done);
+  if (!done) {
+    ReqRes* col = stage + threadIdx.x;
+    const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK));
+  }
+  out[i] = d;
+}
+
+// K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane.
+__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+                                                                uint32_t words, uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
-  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= B.n) return;
+  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= B.n) return;
+  const uint32_t i = perm ? perm[k] : k;
   uint32_t* my_bits = bits + (size_t)i * words;
   for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
-  out[i] = what_is_allowed(T, B, i, my_bits, obl + (size_t)i * 2 * OBL_MAX, obl_n + i);
+  const ReqHdr h = B.hdr[i];
+  OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
+  Decision d{};
+  if (h.flags & RQ_HOST) {
+    d.flags = OF_HOST_REQ;
+  } else {
+    ReqRes* col = stage + threadIdx.x;
+    const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    d = what_is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), my_bits, log);
+  }
+  obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
+  out[i] = d;
 }
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -63,6 +114,10 @@ struct acs_tables {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = -1.f;
+  int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
+  // sort workspace, grown on demand: keys/idx double buffers + hipcub temp storage
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
 };
 
 extern "C" {
@@ -76,10 +131,9 @@ int acs_device_count(void) {
 }
 
 int acs_layout_sizes(uint32_t* out, int n) {
-  const uint32_t s[8] = {sizeof(TargetRec), sizeof(RuleResAttr), sizeof(SetRec), sizeof(PolicyRec),
-                         sizeof(RuleRec), sizeof(ReqHdr), sizeof(ReqRes), sizeof(Decision)};
-  for (int k = 0; k < n && k < 8; ++k) out[k] = s[k];
-  return 8;
+  const uint32_t s[5] = {sizeof(NodeRec), sizeof(RuleResAttr), sizeof(ReqHdr), sizeof(ReqRes), sizeof(Decision)};
+  for (int k = 0; k < n && k < 5; ++k) out[k] = s[k];
+  return 5;
 }
 
 acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
@@ -93,11 +147,10 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     fail("acs_compile: bad blob magic/version");
     return nullptr;
   }
-  const size_t sz[7] = {h.n_sets * sizeof(SetRec),       h.n_pols * sizeof(PolicyRec), h.n_rules * sizeof(RuleRec),
-                        h.n_targets * sizeof(TargetRec), h.n_rres * sizeof(RuleResAttr), h.n_pairs * sizeof(Pair),
-                        h.n_u32pool * sizeof(uint32_t)};
-  size_t off[7], total = 0, src = align16(sizeof h);
-  for (int k = 0; k < 7; ++k) {
+  const size_t sz[6] = {h.n_sets * sizeof(NodeRec), h.n_pols * sizeof(NodeRec), h.n_rules * sizeof(NodeRec),
+                        h.n_rres * sizeof(RuleResAttr), h.n_pairs * sizeof(Pair), h.n_u32pool * sizeof(uint32_t)};
+  size_t off[6], total = 0, src = align16(sizeof h);
+  for (int k = 0; k < 6; ++k) {
     off[k] = total;
     total += align16(sz[k]);
   }
@@ -117,13 +170,12 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     return nullptr;
   }
   char* base = (char*)t->dev;
-  t->view.sets = (const SetRec*)(base + off[0]);
-  t->view.pols = (const PolicyRec*)(base + off[1]);
-  t->view.rules = (const RuleRec*)(base + off[2]);
-  t->view.targets = (const TargetRec*)(base + off[3]);
-  t->view.rres = (const RuleResAttr*)(base + off[4]);
-  t->view.pairs = (const Pair*)(base + off[5]);
-  t->view.u32pool = (const uint32_t*)(base + off[6]);
+  t->view.sets = (const NodeRec*)(base + off[0]);
+  t->view.pols = (const NodeRec*)(base + off[1]);
+  t->view.rules = (const NodeRec*)(base + off[2]);
+  t->view.rres = (const RuleResAttr*)(base + off[3]);
+  t->view.pairs = (const Pair*)(base + off[4]);
+  t->view.u32pool = (const uint32_t*)(base + off[5]);
   t->view.n_sets = h.n_sets;
   t->view.n_pols = h.n_pols;
   t->view.n_rules = h.n_rules;
@@ -138,6 +190,7 @@ void acs_free(acs_tables* t) {
   if (t->ev0) (void)hipEventDestroy(t->ev0);
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
+  if (t->ws) (void)hipFree(t->ws);
   delete t;
 }
 
@@ -161,13 +214,52 @@ static Batch to_batch(const acs_req_batch* b) {
   return B;
 }
 
+int acs_set_option(acs_tables* t, int option, int value) {
+  if (!t) return fail("acs_set_option: null tables");
+  if (option == ACS_OPT_SORT) {
+    t->sort = value ? 1 : 0;
+    return 0;
+  }
+  return fail("acs_set_option: unknown option");
+}
+
+// Coherence sort: permutation of request indices ordered by (entity, role, action).
+static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
+  *perm = nullptr;
+  if (!t->sort || B.n < 2 * BLOCK) return 0;
+  const size_t n = B.n;
+  size_t temp = 0;
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32, s));
+  const size_t need = 4 * n * sizeof(uint32_t) + temp + 256;
+  if (need > t->ws_bytes) {
+    if (t->ws) HIP_OK(hipFree(t->ws));
+    t->ws = nullptr;
+    t->ws_bytes = 0;
+    HIP_OK(hipMalloc(&t->ws, need));
+    t->ws_bytes = need;
+  }
+  uint32_t* keys_in = (uint32_t*)t->ws;
+  uint32_t* keys_out = keys_in + n;
+  uint32_t* idx_in = keys_out + n;
+  uint32_t* idx_out = idx_in + n;
+  void* tmp = (void*)(((uintptr_t)(idx_out + n) + 255) & ~uintptr_t(255));
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, B, keys_in, idx_in);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, 0, 32, s));
+  *perm = idx_out;
+  return 0;
+}
+
 int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* out, void* stream) {
   if (!t || !b) return fail("acs_is_allowed_device: null argument");
   if (b->n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Batch B = to_batch(b);
+  const uint32_t* perm = nullptr;
+  if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
-  hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, (Decision*)out);
+  hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, perm, (Decision*)out);
   HIP_OK(hipGetLastError());
   return 0;
 }
@@ -178,8 +270,10 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   if (b->n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Batch B = to_batch(b);
+  const uint32_t* perm = nullptr;
+  if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
-  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, acs_wia_words_per_request(t),
+  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, perm, acs_wia_words_per_request(t),
                      bits, obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   return 0;

@@ -71,17 +71,31 @@ enum TargetFlags : uint32_t {
   TF_LASTPROP_HASH = 1u << 9,// ... containing '#'
 };
 
-struct TargetRec {           // 48 B, one per non-null target of a set/policy/rule
-  uint32_t flags;
+// One set / policy / rule with its target inline (64 B: a single scalar load per node).
+enum NodeFlags : uint8_t {
+  NF_NULL = 1u << 0,           // null Map entry (policy: TypeError in loop 2a; rule: skipped)
+  NF_HAS_TARGET = 1u << 1,     // !!node.target
+  NF_EFFECT_TRUTHY = 1u << 2,  // !!node.effect
+  NF_HAS_CONDITION = 1u << 3,  // rule.condition?.length
+  NF_EC_TRUTHY = 1u << 4,      // !!rule.evaluation_cacheable
+};
+
+struct NodeRec {
+  uint32_t tflags;           // TargetFlags of the inline target (0 without target)
   uint32_t role;             // last subjects value with id === urns.role (raw, may be UNDEF)
   uint32_t se;               // last roleScopingEntity value
-  uint32_t subj_off;         // ATTRS mode: (id,value) pairs in pair pool
-  uint32_t act_off;          // (id,value) pairs in pair pool
+  uint32_t subj_off;         // ATTRS mode: (id,value) pairs in the pair pool
+  uint32_t act_off;          // (id,value) pairs in the pair pool
   uint32_t res_off;          // RuleResAttr pool
-  uint32_t acl_roles_off;    // scopedRoles (role values in subject order) in u32 pool
+  uint32_t acl_roles_off;    // scopedRoles (role values in subject order) in the u32 pool
   uint32_t last_prop_value;  // value of the last property attr (whatIsAllowed mask source)
   uint16_t subj_n, act_n, res_n, acl_roles_n;
-  uint32_t pad[2];
+  uint32_t child_begin, child_end;  // set: its policies; policy: its rules
+  uint32_t map_size;         // policy: combinables.size (null entries included)
+  uint32_t fe;               // policy: first non-null rule with falsy evaluation_cacheable (else child_end)
+  uint8_t effect, ec, ca, nflags;
+  uint8_t pe_at;             // policy: loop-2a policyEffect after visiting this policy
+  uint8_t pad[3];
 };
 
 struct RuleResAttr {         // 16 B
@@ -91,27 +105,6 @@ struct RuleResAttr {         // 16 B
   uint8_t kind;
   uint8_t pad;
   uint32_t pad2;
-};
-
-enum PolicyFlags : uint8_t { PF_NULL = 1u << 0, PF_EFFECT_TRUTHY = 1u << 1, PF_HAS_TARGET = 1u << 2 };
-enum RuleFlags : uint8_t { RF_NULL = 1u << 0, RF_HAS_CONDITION = 1u << 1, RF_EC_TRUTHY = 1u << 2, RF_HAS_TARGET = 1u << 3 };
-
-struct SetRec {              // 16 B
-  uint32_t target;           // NONE32: no target
-  uint32_t pol_begin, pol_end;
-  uint8_t ca, pad[3];
-};
-
-struct PolicyRec {           // 20 B
-  uint32_t target;
-  uint32_t rule_begin, rule_end;
-  uint32_t map_size;         // policy.combinables.size (null entries included)
-  uint8_t effect, ec, ca, flags;
-};
-
-struct RuleRec {             // 8 B
-  uint32_t target;
-  uint8_t effect, ec, flags, pad;
 };
 
 // ---------------------------------------------------------------- request batch

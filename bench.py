@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--requests", type=int, default=0, help="requests per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sort", action="store_true", help="disable the (entity, role, action) coherence sort")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,6 +108,7 @@ def main():
     cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
     sb = synth.requests(cs, n, kind, seed=0xACC1000 + 17 * rank)
     tables = native.Tables(compiler.store_blob(cs), local)
+    tables.set_sort(not args.no_sort)
     db = DeviceBatch(sb.batch, local)
     out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -147,6 +149,7 @@ def main():
             "config": {"workload": desc, "requests_per_gpu": n, "policy_sets": cs.n_sets, "policies": cs.n_pols,
                        "rules": cs.n_rules, "table_bytes": cs.table_bytes(), "parallelism": f"requests dp{world}",
                        "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])}},
+            "coherence_sort": not args.no_sort,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "is_allowed_kernel",
                          "kernel_ms": kern_ms, "bytes_per_decision": per_dec, "bytes_parts": parts},

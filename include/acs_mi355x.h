@@ -24,16 +24,17 @@ extern "C" {
 #endif
 
 #define ACS_BLOB_MAGIC 0x31534341u /* "ACS1" */
-#define ACS_ABI_VERSION 1u
+#define ACS_ABI_VERSION 2u
 
 /* Compiled policy-store image (host compiler output, see csrc/acs_layout.h).
- * Header followed by 16-byte aligned sections in this order:
- * sets, policies, rules, targets, rule resource attrs, (id,value) pairs, u32 pool. */
+ * Header followed by 16-byte aligned sections in this order: set / policy / rule
+ * node records (64 B each, target inline), rule resource attrs, (id,value) pairs,
+ * u32 pool. */
 typedef struct {
   uint32_t magic, version;
-  uint32_t n_sets, n_pols, n_rules, n_targets, n_rres, n_pairs, n_u32pool;
+  uint32_t n_sets, n_pols, n_rules, n_rres, n_pairs, n_u32pool;
   uint32_t id_user;
-  uint32_t reserved[6];
+  uint32_t reserved[7];
 } acs_blob_header;
 
 typedef struct acs_tables acs_tables; /* device-resident tables, immutable once built */
@@ -93,12 +94,18 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t
 int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, uint32_t* dev_bits,
                                uint32_t* dev_obl, uint32_t* dev_obl_n, acs_decision* dev_out, void* stream);
 
+/* Options.  ACS_OPT_SORT (default 1): before evaluating, the device entry points
+ * order the batch by (entity, role, action) with a radix sort so that every
+ * wave shares its table-driven branches; results are written in input order. */
+#define ACS_OPT_SORT 1
+int acs_set_option(acs_tables* t, int option, int value);
+
 /* Average kernel time (ms) of the last `*_device` launch measured with HIP events on
  * its stream; -1 if none. */
 float acs_last_kernel_ms(const acs_tables* t);
 
 const char* acs_last_error(void);
-int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 8 packed structs, for host checks */
+int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 5 packed structs, for host checks */
 int acs_device_count(void);
 
 #ifdef __cplusplus

@@ -18,21 +18,19 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   std::memcpy(&h, blob, sizeof h);
   if (h.magic != ACS_BLOB_MAGIC) return false;
   const char* p = (const char*)blob + a16(sizeof h);
-  const size_t sz[7] = {h.n_sets * sizeof(SetRec),       h.n_pols * sizeof(PolicyRec), h.n_rules * sizeof(RuleRec),
-                        h.n_targets * sizeof(TargetRec), h.n_rres * sizeof(RuleResAttr), h.n_pairs * sizeof(Pair),
-                        h.n_u32pool * sizeof(uint32_t)};
-  const char* s[7];
-  for (int k = 0; k < 7; ++k) {
+  const size_t sz[6] = {h.n_sets * sizeof(NodeRec), h.n_pols * sizeof(NodeRec), h.n_rules * sizeof(NodeRec),
+                        h.n_rres * sizeof(RuleResAttr), h.n_pairs * sizeof(Pair), h.n_u32pool * sizeof(uint32_t)};
+  const char* s[6];
+  for (int k = 0; k < 6; ++k) {
     s[k] = p;
     p += a16(sz[k]);
   }
-  T->sets = (const SetRec*)s[0];
-  T->pols = (const PolicyRec*)s[1];
-  T->rules = (const RuleRec*)s[2];
-  T->targets = (const TargetRec*)s[3];
-  T->rres = (const RuleResAttr*)s[4];
-  T->pairs = (const Pair*)s[5];
-  T->u32pool = (const uint32_t*)s[6];
+  T->sets = (const NodeRec*)s[0];
+  T->pols = (const NodeRec*)s[1];
+  T->rules = (const NodeRec*)s[2];
+  T->rres = (const RuleResAttr*)s[3];
+  T->pairs = (const Pair*)s[4];
+  T->u32pool = (const uint32_t*)s[5];
   T->n_sets = h.n_sets;
   T->n_pols = h.n_pols;
   T->n_rules = h.n_rules;
