@@ -24,7 +24,7 @@ class ReqBatchC(C.Structure):
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
            "acs_what_is_allowed", "acs_what_is_allowed_device", "acs_last_kernel_ms", "acs_last_error",
-           "acs_layout_sizes", "acs_device_count", "acs_set_option"]
+           "acs_layout_sizes", "acs_device_count", "acs_set_option", "acs_kernel_times"]
 
 
 def _declare(lib):
@@ -45,6 +45,7 @@ def _declare(lib):
     lib.acs_last_error.restype = C.c_char_p
     lib.acs_layout_sizes.argtypes = [C.POINTER(u32), C.c_int]
     lib.acs_set_option.argtypes = [vp, C.c_int, C.c_int]
+    lib.acs_kernel_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
     return lib
 
 
@@ -135,6 +136,17 @@ class Tables:
     def set_sort(self, enable: bool):
         if self.lib.acs_set_option(self.h, 1, int(bool(enable))) != 0:
             raise RuntimeError(last_error(self.lib))
+
+    def set_timing(self, enable: bool):
+        if self.lib.acs_set_option(self.h, 2, int(bool(enable))) != 0:
+            raise RuntimeError(last_error(self.lib))
+
+    def kernel_times(self, n: int):
+        buf = (C.c_float * n)()
+        m = self.lib.acs_kernel_times(self.h, buf, n)
+        if m < 0:
+            raise RuntimeError(last_error(self.lib))
+        return list(buf)[:m]
 
     def last_kernel_ms(self):
         return float(self.lib.acs_last_kernel_ms(self.h))

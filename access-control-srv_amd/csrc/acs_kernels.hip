@@ -115,6 +115,11 @@ struct acs_tables {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
+  // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
+  static constexpr int RING = 256;
+  int timing = 0;
+  hipEvent_t tev[2 * RING] = {};
+  uint64_t launches = 0;
   // sort workspace, grown on demand: keys/idx double buffers + hipcub temp storage
   void* ws = nullptr;
   size_t ws_bytes = 0;
@@ -191,6 +196,8 @@ void acs_free(acs_tables* t) {
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
   if (t->ws) (void)hipFree(t->ws);
+  for (hipEvent_t e : t->tev)
+    if (e) (void)hipEventDestroy(e);
   delete t;
 }
 
@@ -218,6 +225,15 @@ int acs_set_option(acs_tables* t, int option, int value) {
   if (!t) return fail("acs_set_option: null tables");
   if (option == ACS_OPT_SORT) {
     t->sort = value ? 1 : 0;
+    return 0;
+  }
+  if (option == ACS_OPT_TIMING) {
+    if (value && !t->tev[0]) {
+      HIP_OK(hipSetDevice(t->device));
+      for (hipEvent_t& e : t->tev) HIP_OK(hipEventCreate(&e));
+    }
+    t->timing = value ? 1 : 0;
+    t->launches = 0;
     return 0;
   }
   return fail("acs_set_option: unknown option");
@@ -259,9 +275,27 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
   const uint32_t* perm = nullptr;
   if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
+  const int slot = (int)(t->launches % acs_tables::RING);
+  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, perm, (Decision*)out);
   HIP_OK(hipGetLastError());
+  if (t->timing) {
+    HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
+    t->launches++;
+  }
   return 0;
+}
+
+int acs_kernel_times(acs_tables* t, float* ms, int n) {
+  if (!t || !t->timing) return fail("acs_kernel_times: timing not enabled");
+  const int avail = (int)(t->launches < (uint64_t)acs_tables::RING ? t->launches : acs_tables::RING);
+  const int m = n < avail ? n : avail;
+  for (int k = 0; k < m; ++k) {
+    const int slot = (int)((t->launches - m + k) % acs_tables::RING);
+    HIP_OK(hipEventSynchronize(t->tev[2 * slot + 1]));
+    HIP_OK(hipEventElapsedTime(&ms[k], t->tev[2 * slot], t->tev[2 * slot + 1]));
+  }
+  return m;
 }
 
 int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,

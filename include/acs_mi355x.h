@@ -98,7 +98,12 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, ui
  * order the batch by (entity, role, action) with a radix sort so that every
  * wave shares its table-driven branches; results are written in input order. */
 #define ACS_OPT_SORT 1
+/* ACS_OPT_TIMING: record HIP events on the launch stream around every K1 kernel of
+ * acs_is_allowed_device; acs_kernel_times returns the durations (ms) of the last n
+ * launches (a ring of 256), returning how many were written. */
+#define ACS_OPT_TIMING 2
 int acs_set_option(acs_tables* t, int option, int value);
+int acs_kernel_times(acs_tables* t, float* ms, int n);
 
 /* Average kernel time (ms) of the last `*_device` launch measured with HIP events on
  * its stream; -1 if none. */
