@@ -131,7 +131,9 @@ def test_what_is_allowed_c4_gpu():
     assert np.array_equal(bits, rbits) and np.array_equal(obl_n, robl_n)
     o = Oracle(FULL_URNS)
     o.load(doc)
-    for i in np.random.default_rng(3).choice(sb.batch.n, size=8, replace=False):
+    ok = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) == 0)
+    assert len(ok) > 0.3 * sb.batch.n  # log overflow -> host path, never a wrong answer
+    for i in np.random.default_rng(3).choice(ok, size=8, replace=False):
         got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], obl[i][:obl_n[i]], out[i]))
         assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
     t.close()
