@@ -118,6 +118,7 @@ class CompiledStore:
     pol_objs: list = field(default_factory=list)
     rule_objs: list = field(default_factory=list)
     stats: dict = field(default_factory=dict)
+    cand_spec: tuple = ((), (), ())  # per set/policy/rule: None (always), rows list
 
     @property
     def n_sets(self):
@@ -280,6 +281,14 @@ class _Builder:
             row = self.rx_row(v) if kind & L.K_ENT_LOOSE else 0
             self.rres.append((self.d.intern(v), hs, row, kind, 0, 0))
         rec["last_prop_value"] = self.d.intern(last_prop)
+        # candidate spec: a target can only match requests whose entity hits one of its
+        # entity rows (resourceAttributesMatch needs entityMatch or operationMatch)
+        has_op = any(strict_eq(a.get("id", MISSING), U("operation")) for a in res)
+        if len(res) == 0 or has_op:
+            rec["_cand"] = None  # always a candidate
+        else:
+            rec["_cand"] = [self.rx_row(a.get("value", MISSING)) for a in res
+                            if strict_eq(a.get("id", MISSING), U("entity"))]
         if isinstance(last_prop, str):
             flags |= L.TF_LASTPROP_STR
             if "#" in last_prop:
@@ -288,7 +297,11 @@ class _Builder:
         return rec
 
 
-def _node(fields: dict):
+def _node(fields: dict, spec: list):
+    """Pack one node record; append its candidate spec (None = always, list of rows)."""
+    spec.append(fields.pop("_cand", None) if fields.get("nflags", 0) & L.NF_HAS_TARGET else
+                ([] if fields.get("nflags", 0) & L.NF_NULL and spec is not None and fields.get("_rule") else None))
+    fields.pop("_rule", None)
     return tuple(fields.get(n, 0) if n != "pad" else (0, 0, 0) for n in L.NODE_DT.names)
 
 
@@ -297,6 +310,7 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
     b = _Builder(urns, combining_algorithms)
     sets, pols, rules = [], [], []
     set_objs, pol_objs, rule_objs = [], [], []
+    spec_s, spec_p, spec_r = [], [], []
     for ps in policy_sets.values():
         if not isinstance(ps, dict):
             raise Unsupported("null policy set")
@@ -310,7 +324,7 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
         for pol in combin.values():
             if pol is None or pol is MISSING:
                 pols.append(_node({"nflags": L.NF_NULL, "child_begin": len(rules), "child_end": len(rules),
-                                   "fe": len(rules), "pe_at": pe_at}))
+                                   "fe": len(rules), "pe_at": pe_at}, spec_p))
                 pol_objs.append(None)
                 continue
             pn = b.target(pol.get("target", MISSING))
@@ -327,7 +341,7 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
             fe = None
             for rule in rcomb.values():
                 if rule is None or rule is MISSING:
-                    rules.append(_node({"nflags": L.NF_NULL}))
+                    rules.append(_node({"nflags": L.NF_NULL, "_rule": True}, spec_r))
                     rule_objs.append(None)
                     continue
                 rn = b.target(rule.get("target", MISSING))
@@ -342,13 +356,14 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
                 elif fe is None:
                     fe = len(rules)  # first non-null rule with falsy evaluation_cacheable
                 rn.update(nflags=rf, effect=effect_code(rule.get("effect", MISSING)), ec=ec)
-                rules.append(_node(rn))
+                rules.append(_node(rn, spec_r))
                 rule_objs.append(rule)
             pn.update(child_end=len(rules), map_size=len(rcomb), fe=len(rules) if fe is None else fe)
-            pols.append(_node(pn))
+            pols.append(_node(pn, spec_p))
             pol_objs.append(pol)
-        sn.update(child_end=len(pols), ca=b.ca_code(ps.get("combining_algorithm", MISSING)))
-        sets.append(_node(sn))
+        sn.update(child_end=len(pols), ca=b.ca_code(ps.get("combining_algorithm", MISSING)),
+                  pe_at=pe_at)  # set: policyEffect after a full loop-2a scan
+        sets.append(_node(sn, spec_s))
         set_objs.append(ps)
 
     def arr(x, dt):
@@ -359,7 +374,8 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
         rres=arr(b.rres, L.RULE_RES_DT), pairs=arr(b.pairs, L.PAIR_DT),
         u32pool=np.array(b.u32pool, dtype=np.uint32) if b.u32pool else np.zeros(0, np.uint32),
         rx_rows=b.rx_rows, ec_values=b.ec_values, id_user=b.d.intern(b.urn("user")),
-        set_objs=set_objs, pol_objs=pol_objs, rule_objs=rule_objs)
+        set_objs=set_objs, pol_objs=pol_objs, rule_objs=rule_objs,
+        cand_spec=(spec_s, spec_p, spec_r))
     cs.stats = {"sets": cs.n_sets, "policies": cs.n_pols, "rules": cs.n_rules, "dictionary": len(b.d),
                 "rx_rows": len(b.rx_rows), "table_bytes": cs.table_bytes()}
     return cs
@@ -368,7 +384,7 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
 def store_blob(cs: CompiledStore) -> bytes:
     """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header)."""
     import struct
-    hdr = struct.pack("<16I", 0x31534341, 2, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
+    hdr = struct.pack("<16I", 0x31534341, 3, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
                       len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0, 0)
     parts = [hdr]
     for a in (cs.sets, cs.pols, cs.rules, cs.rres, cs.pairs, cs.u32pool):

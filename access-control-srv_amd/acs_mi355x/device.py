@@ -26,6 +26,8 @@ class DeviceBatch:
         self.dev = torch.device("cuda", device)
         self.t = {k: _to_dev(getattr(batch, k) if getattr(batch, k).size else np.zeros(4, np.uint32), self.dev)
                   for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx")}
+        if batch.cand is not None:
+            self.t["cand"] = _to_dev(batch.cand, self.dev)
         self.ptrs = {k: v.data_ptr() for k, v in self.t.items()}
         self.struct = batch_struct(batch, self.ptrs)
         self.nbytes = sum(v.numel() for v in self.t.values())

@@ -29,6 +29,7 @@ from . import layout as L
 from .compiler import CompiledStore, Overlay
 from .jsops import (MISSING, Unsupported, check_scalar, find_by, get, is_empty, nullish, or_list,
                     strict_eq, truthy)
+from . import candidates
 from .regex import cell
 
 
@@ -45,9 +46,13 @@ class RequestBatch:
     rx_rows: int
     overlay: Overlay
     host_reasons: dict = field(default_factory=dict)
+    cand: np.ndarray | None = None   # [rx_cols + 1, W] candidate bitsets (candidates.py)
+    cand_wp: int = 0
+    cand_wr: int = 0
 
     def nbytes(self):
-        return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx))
+        return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
+            (self.cand.nbytes if self.cand is not None else 0)
 
 
 def _attr_list(v, what):
@@ -208,7 +213,7 @@ class Encoder:
             if kind & L.K_ENT_LOOSE:
                 key = ("m",) if v is MISSING else (("n",) if v is None else ("s", v))
                 col = cols.setdefault(key, len(cols))
-                if col > 0xFFFF:
+                if col >= 0xFFFE:
                     raise Unsupported("too many distinct entity values in batch")
             packed_res.append((vid, hs, col, contains, kind, sa, sb, 0))
         for vid, sb in keys_b.items():  # HR map key shared by a resource id and an operation name
@@ -412,13 +417,30 @@ class Encoder:
             arena.extend(words)
         rows = self.cs.rx_rows
         rx = np.zeros((max(len(cols), 1), max(len(rows), 1)), np.uint8)
+        col_values = [None] * len(cols)
         for key, c in cols.items():
+            v = MISSING if key[0] == "m" else (None if key[0] == "n" else key[1])
+            col_values[c] = v
             cached = self._rx_cache.get(key)
             if cached is None:
-                v = MISSING if key[0] == "m" else (None if key[0] == "n" else key[1])
                 cached = np.array([cell(rv, v) for rv in rows] or [0], np.uint8)
                 self._rx_cache[key] = cached
             rx[c, :] = cached
-        return RequestBatch(n=n, hdr=hdr, res=res, subj=subj, act=act, roles=roles,
-                            arena=np.array(arena, np.uint32), rx=rx, rx_rows=max(len(rows), 1),
-                            overlay=ov, host_reasons=reasons)
+        b = RequestBatch(n=n, hdr=hdr, res=res, subj=subj, act=act, roles=roles,
+                         arena=np.array(arena, np.uint32), rx=rx, rx_rows=max(len(rows), 1),
+                         overlay=ov, host_reasons=reasons)
+        attach_candidates(self.cs, b, col_values)
+        return b
+
+
+def attach_candidates(cs, b: RequestBatch, col_values):
+    """Candidate bitsets for the batch's entity columns + each request's column in its flags."""
+    ncols = b.rx.shape[0]
+    assert len(col_values) <= ncols
+    # pad: columns without a value (an all-empty batch) get no candidates beyond the "always" nodes
+    vals = list(col_values) + [object()] * (ncols - len(col_values))
+    b.cand = candidates.build(cs, vals, b.rx)
+    ws, wp, _ = candidates.section_words(cs)
+    b.cand_wp, b.cand_wr = ws, ws + wp
+    pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
+    b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (pcol.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

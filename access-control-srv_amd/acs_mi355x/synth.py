@@ -352,4 +352,6 @@ def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree
     hdr["flags"] = flags
     b = RequestBatch(n=n, hdr=hdr, res=res, subj=subj, act=actp, roles=roles, arena=arena, rx=rx,
                      rx_rows=rx.shape[1], overlay=ov)
+    from .encoder import attach_candidates
+    attach_candidates(cs, b, [entity(k) for k in range(N_ENT)])
     return SynthBatch(batch=b, draws=draws, kind=kind, tree=tree if kind != "c2" else None)

@@ -57,6 +57,48 @@ struct Batch {
   const uint32_t* arena;
   const uint8_t* rx;      // [cols][rx_rows]
   uint32_t rx_rows;
+  const uint32_t* cand;   // [cols+1][cand_words] candidate bitsets (sets | policies | rules)
+  uint32_t cand_words, cand_wp, cand_wr;  // row length, word offsets of the policy / rule sections
+};
+
+// Candidate filter of a wave (GPU: the union of its lanes' columns, gathered with
+// ballots; host build: the request's own column).  Wave-uniform by construction.
+struct Filter {
+  const uint32_t* cand;
+  uint32_t W, wp, wr;
+  uint32_t n;        // number of columns (0 with all = true)
+  uint32_t col[4];
+  bool all;          // no filtering
+  ACS_FN uint32_t word(uint32_t w) const {
+    if (all) return ~0u;
+    uint32_t x = 0;
+    for (uint32_t k = 0; k < n; ++k) x |= cand[(size_t)col[k] * W + w];
+    return x;
+  }
+};
+
+// Ascending iteration over the candidate indices in [b, e) of one bitset section.
+struct CandRange {
+  const Filter& F;
+  uint32_t off, base, e, bits;
+  ACS_FN CandRange(const Filter& f, uint32_t section_off, uint32_t b, uint32_t e_)
+      : F(f), off(section_off), base(b & ~31u), e(e_), bits(0) {
+    if (b < e) bits = F.word(off + (b >> 5)) & (~0u << (b & 31));
+  }
+  ACS_FN bool next(uint32_t& out) {
+    for (;;) {
+      if (bits) {
+        const uint32_t x = base + (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        if (x >= e) return false;
+        out = x;
+        return true;
+      }
+      base += 32;
+      if (base >= e) return false;
+      bits = F.word(off + (base >> 5));
+    }
+  }
 };
 
 ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
@@ -455,12 +497,14 @@ ACS_FN Decision make_err(tri e) {
 }
 
 template <class RQ>
-ACS_FN Decision is_allowed_t(const RQ& R) {
+ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
   const Tables& T = R.T;
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;
-  for (uint32_t s = 0; s < T.n_sets; ++s) {
+  CandRange sets(F, 0, 0, T.n_sets);
+  uint32_t s;
+  while (sets.next(s)) {
     const NodeRec S = T.sets[s];
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
@@ -469,17 +513,21 @@ ACS_FN Decision is_allowed_t(const RQ& R) {
     }
     // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
     bool exact = false;
-    uint8_t pe = EFF_UNDEF;
-    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
-      const NodeRec P = T.pols[p];
-      if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
-      pe = P.pe_at;
-      if (P.nflags & NF_HAS_TARGET) {
-        const tri m = target_match(P, R, pe, false, false, nullptr);
-        if (m < 0) return make_err(m);
-        if (m) {
-          exact = true;
-          break;
+    uint8_t pe = S.pe_at;  // after a full scan
+    {
+      CandRange pols(F, F.wp, S.child_begin, S.child_end);
+      uint32_t p;
+      while (pols.next(p)) {
+        const NodeRec P = T.pols[p];
+        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+        if (P.nflags & NF_HAS_TARGET) {
+          const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
+          if (m < 0) return make_err(m);
+          if (m) {
+            exact = true;
+            pe = P.pe_at;
+            break;
+          }
         }
       }
     }
@@ -489,7 +537,9 @@ ACS_FN Decision is_allowed_t(const RQ& R) {
       exact = m != 0;
     }
     Fold sf(S.ca);
-    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+    CandRange pols(F, F.wp, S.child_begin, S.child_end);
+    uint32_t p;
+    while (pols.next(p)) {
       const NodeRec P = T.pols[p];
       if (P.nflags & NF_NULL) continue;
       bool psm = true;
@@ -508,7 +558,9 @@ ACS_FN Decision is_allowed_t(const RQ& R) {
         continue;
       }
       Fold rf(P.ca);
-      for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
+      CandRange rules(F, F.wr, P.child_begin, P.child_end);
+      uint32_t r;
+      while (rules.next(r)) {
         const NodeRec Q = T.rules[r];
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
@@ -578,23 +630,39 @@ ACS_FN Decision early_decision(const ReqHdr& h, bool* done) {
   return out;
 }
 
+// Filter of a single request (host build / per-lane reference).
+ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
+  Filter F{};
+  F.cand = B.cand;
+  F.W = B.cand_words;
+  F.wp = B.cand_wp;
+  F.wr = B.cand_wr;
+  const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
+  F.all = B.cand == nullptr || pc == PCOL_ALL || (h.flags & RQ_NO_TARGET);
+  F.n = F.all ? 0 : 1;
+  F.col[0] = pc;
+  return F;
+}
+
 ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
   const ReqHdr h = B.hdr[i];
   bool done;
   Decision d = early_decision(h, &done);
   if (done) return d;
-  return is_allowed_t(ReqMem(T, B, i, h));
+  return is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h));
 }
 
 // ------------------------------------------------------------------ whatIsAllowed
 // bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
 template <class RQ>
-ACS_FN Decision what_is_allowed_t(const RQ& R, uint32_t* bits, OblLog& obl) {
+ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, OblLog& obl) {
   const Tables& T = R.T;
   Decision out{};
   auto setbit = [&](uint32_t b) { bits[b >> 5] |= 1u << (b & 31); };
   const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
-  for (uint32_t s = 0; s < T.n_sets; ++s) {
+  CandRange sets(F, 0, 0, T.n_sets);
+  uint32_t s;
+  while (sets.next(s)) {
     const NodeRec S = T.sets[s];
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
@@ -602,17 +670,21 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, uint32_t* bits, OblLog& obl) {
       if (!m) continue;
     }
     bool exact = false;
-    uint8_t pe = EFF_UNDEF;
-    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
-      const NodeRec P = T.pols[p];
-      if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
-      pe = P.pe_at;
-      if (P.nflags & NF_HAS_TARGET) {
-        const tri m = target_match(P, R, pe, false, true, &obl);
-        if (m < 0) return make_err(m);
-        if (m) {
-          exact = true;
-          break;
+    uint8_t pe = S.pe_at;
+    {
+      CandRange pols(F, F.wp, S.child_begin, S.child_end);
+      uint32_t p;
+      while (pols.next(p)) {
+        const NodeRec P = T.pols[p];
+        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+        if (P.nflags & NF_HAS_TARGET) {
+          const tri m = target_match(P, R, P.pe_at, false, true, &obl);
+          if (m < 0) return make_err(m);
+          if (m) {
+            exact = true;
+            pe = P.pe_at;
+            break;
+          }
         }
       }
     }
@@ -622,7 +694,9 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, uint32_t* bits, OblLog& obl) {
       exact = m != 0;
     }
     bool any_pol = false;
-    for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
+    CandRange pols(F, F.wp, S.child_begin, S.child_end);
+    uint32_t p;
+    while (pols.next(p)) {
       const NodeRec P = T.pols[p];
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
@@ -631,7 +705,9 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, uint32_t* bits, OblLog& obl) {
         if (!m) continue;
       }
       bool any_rule = false;
-      for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
+      CandRange rules(F, F.wr, P.child_begin, P.child_end);
+      uint32_t r;
+      while (rules.next(r)) {
         const NodeRec Q = T.rules[r];
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
@@ -667,7 +743,7 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
   if (h.flags & RQ_HOST) {
     d.flags = OF_HOST_REQ;
   } else {
-    d = what_is_allowed_t(ReqMem(T, B, i, h), bits, obl);
+    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h), bits, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
   return d;

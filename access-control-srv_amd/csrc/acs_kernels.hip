@@ -57,21 +57,55 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
   idx[k] = k;
 }
 
+// Union of the candidate columns of the wave's active requests (<= 4 distinct after the
+// coherence sort; more, or an unfiltered request, disables filtering for the wave).
+// Called with every lane of the wave present, before any lane diverges.
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t pcol) {
+  Filter F{};
+  F.cand = B.cand;
+  F.W = B.cand_words;
+  F.wp = B.cand_wp;
+  F.wr = B.cand_wr;
+  F.all = B.cand == nullptr;
+  F.n = 0;
+  uint64_t pending = __ballot(valid);
+  while (pending && !F.all) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t c = __builtin_amdgcn_readlane(pcol, leader);
+    if (c == PCOL_ALL || F.n == 4) {
+      F.all = true;
+      break;
+    }
+    F.col[F.n++] = c;
+    pending &= ~__ballot(valid && pcol == c);
+  }
+  if (F.all) F.n = 0;
+  return F;
+}
+
+__device__ inline uint32_t request_pcol(const ReqHdr& h) {
+  return (h.flags & RQ_NO_TARGET) ? PCOL_ALL : (h.flags >> RQ_PCOL_SHIFT);
+}
+
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 __global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  if (k >= B.n) return;
-  const uint32_t i = perm ? perm[k] : k;
-  const ReqHdr h = B.hdr[i];
-  bool done;
-  Decision d = early_decision(h, &done);
+  const bool in = k < B.n;
+  const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  ReqHdr h{};
+  if (in) h = B.hdr[i];
+  bool done = true;
+  Decision d{};
+  if (in) d = early_decision(h, &done);
+  const Filter F = wave_filter(B, in && !done, request_pcol(h));
+  if (!in) return;
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK));
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
   }
   out[i] = d;
 }
@@ -84,20 +118,24 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
                                                                 Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  if (k >= B.n) return;
-  const uint32_t i = perm ? perm[k] : k;
+  const bool in = k < B.n;
+  const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  ReqHdr h{};
+  if (in) h = B.hdr[i];
+  const bool host = (h.flags & RQ_HOST) != 0;
+  const Filter F = wave_filter(B, in && !host, request_pcol(h));
+  if (!in) return;
   uint32_t* my_bits = bits + (size_t)i * words;
   for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
-  const ReqHdr h = B.hdr[i];
   OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
   Decision d{};
-  if (h.flags & RQ_HOST) {
+  if (host) {
     d.flags = OF_HOST_REQ;
   } else {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    d = what_is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), my_bits, log);
+    d = what_is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F, my_bits, log);
   }
   obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
   out[i] = d;
@@ -218,6 +256,10 @@ static Batch to_batch(const acs_req_batch* b) {
   B.arena = b->arena;
   B.rx = b->rx;
   B.rx_rows = b->rx_rows;
+  B.cand = b->cand;
+  B.cand_words = b->cand_words;
+  B.cand_wp = b->cand_wp;
+  B.cand_wr = b->cand_wr;
   return B;
 }
 
@@ -346,6 +388,9 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
       D.up(b->roles, n * RMAX * sizeof(uint32_t), (const void**)&D.d.roles, s) ||
       D.up(b->arena, b->arena_words * sizeof(uint32_t), (const void**)&D.d.arena, s) ||
       D.up(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&D.d.rx, s))
+    return -1;
+  if (b->cand && D.up(b->cand, ((size_t)b->rx_cols + 1) * b->cand_words * sizeof(uint32_t),
+                      (const void**)&D.d.cand, s))
     return -1;
   return 0;
 }

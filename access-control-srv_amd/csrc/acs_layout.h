@@ -126,8 +126,9 @@ enum ReqFlags : uint32_t {
   RQ_ACT_CREATE = 1u << 9,   // actions[0] is {actionID, create}
   RQ_ACT_RMD = 1u << 10,     // actions[0] is {actionID, read|modify|delete}
   RQ_ACL_SHIFT = 11,         // 2 bits: verifyACL request-loop outcome
-  RQ_HAS_TARGET_SUBJ = 1u << 13, // unused (reserved)
+  RQ_PCOL_SHIFT = 16,        // 16 bits: candidate column of the request's entity attrs
 };
+constexpr uint32_t PCOL_ALL = 0xFFFF;  // several distinct entity columns / unfiltered request
 enum AclState : uint32_t { ACL_CONTINUE = 0, ACL_RET_TRUE = 1, ACL_RET_FALSE = 2 };
 
 struct ReqHdr {              // 16 B

@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 #define ACS_BLOB_MAGIC 0x31534341u /* "ACS1" */
-#define ACS_ABI_VERSION 2u
+#define ACS_ABI_VERSION 3u
 
 /* Compiled policy-store image (host compiler output, see csrc/acs_layout.h).
  * Header followed by 16-byte aligned sections in this order: set / policy / rule
@@ -53,6 +53,10 @@ typedef struct {
   size_t arena_words;
   const uint8_t* rx;      /* [rx_cols][rx_rows] regex matrix   */
   uint32_t rx_cols, rx_rows;
+  /* [rx_cols + 1][cand_words] candidate bitsets over (sets | policies | rules) per entity
+   * column (last row: requests without entity attributes); NULL = evaluate every node. */
+  const uint32_t* cand;
+  uint32_t cand_words, cand_wp, cand_wr;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */

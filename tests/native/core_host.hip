@@ -49,6 +49,10 @@ static Batch host_batch(const acs_req_batch* b) {
   B.arena = b->arena;
   B.rx = b->rx;
   B.rx_rows = b->rx_rows;
+  B.cand = b->cand;
+  B.cand_words = b->cand_words;
+  B.cand_wp = b->cand_wp;
+  B.cand_wr = b->cand_wr;
   return B;
 }
 
