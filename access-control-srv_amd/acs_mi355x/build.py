@@ -1,6 +1,8 @@
 """Build the native libraries in-tree (hipcc, gfx950).
 
   lib/libacs_mi355x.so          product: HIP kernels + C ABI (include/acs_mi355x.h)
+  lib/acs_mi355x.node           N-API addon over the C ABI for a Node/TS host (gcc; needs
+                                /usr/include/node, skipped when the headers are absent)
   tests/native/libacs_core_host.so   test infrastructure: the evaluator core on the CPU
 
 Both are plain ``hipcc -shared`` builds so the .so files travel with the repo
@@ -45,6 +47,25 @@ def build_product(force=False):
     return LIB
 
 
+NAPI_SRC = os.path.join(PKG, "napi", "acs_napi.c")
+NAPI_OUT = os.path.join(PKG, "lib", "acs_mi355x.node")
+NODE_INC = "/usr/include/node"
+
+
+def build_napi(force=False):
+    """gcc build of the N-API addon, linked to libacs_mi355x.so via $ORIGIN (None if no headers)."""
+    if not os.path.exists(os.path.join(NODE_INC, "node_api.h")):
+        return None
+    lib = build_product()
+    if force or _stale(NAPI_OUT, [NAPI_SRC, lib, os.path.join(ROOT, "include", "acs_mi355x.h")]):
+        cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+               "-I", NODE_INC, NAPI_SRC, "-o", NAPI_OUT + ".tmp", "-L", os.path.dirname(lib), "-lacs_mi355x",
+               "-Wl,-rpath,$ORIGIN"]
+        subprocess.run(cmd, check=True)
+        os.replace(NAPI_OUT + ".tmp", NAPI_OUT)
+    return NAPI_OUT
+
+
 def build_host_core(force=False):
     src = os.path.join(ROOT, "tests", "native", "core_host.hip")
     if force or _stale(HOST_LIB, [src] + _HEADERS):
@@ -53,7 +74,7 @@ def build_host_core(force=False):
 
 
 def build_all(force=False):
-    return build_product(force), build_host_core(force)
+    return build_product(force), build_host_core(force), build_napi(force)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,69 @@
+"""N-API addon (lib/acs_mi355x.node): loads in Node with the full surface (CPU), and
+a Node-driven batch is bit-identical to the Python-driven C ABI (GPU)."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from acs_mi355x import build, compiler, store, synth
+from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
+
+NODE = shutil.which("node")
+pytestmark = pytest.mark.skipif(NODE is None or not os.path.exists("/usr/include/node/node_api.h")
+                                and not os.path.exists(build.NAPI_OUT), reason="no node / N-API headers")
+RUNNER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "js", "acs_napi_run.js")
+
+
+def _addon():
+    p = build.build_napi() if os.path.exists("/usr/include/node/node_api.h") else build.NAPI_OUT
+    assert p and os.path.exists(p)
+    return p
+
+
+def test_addon_loads_with_surface():
+    p = _addon()
+    js = ("const a=require(process.argv[1]);"
+          "console.log(JSON.stringify({keys:Object.keys(a).sort(),sizes:a.layoutSizes()}));"
+          "let msg='';try{a.compile(new Uint8Array(64),0)}catch(e){msg=e.message};console.log(msg)")
+    r = subprocess.run([NODE, "-e", js, p], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.splitlines()[0])
+    assert info["keys"] == sorted(["compile", "free", "isAllowed", "isAllowedAsync", "whatIsAllowed",
+                                   "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
+    assert info["sizes"] == [64, 16, 16, 16, 8]
+    assert "magic" in r.stdout.splitlines()[1]  # a bad image is rejected with acs_last_error's message
+
+
+def _dump(tmp, cs, b):
+    tmp.joinpath("blob.bin").write_bytes(compiler.store_blob(cs))
+    for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx", "cand"):
+        tmp.joinpath(k + ".bin").write_bytes(np.ascontiguousarray(getattr(b, k)).tobytes())
+    tmp.joinpath("meta.json").write_text(json.dumps({
+        "n": b.n, "rxCols": int(b.rx.shape[0]), "rxRows": int(b.rx_rows), "candWords": int(b.cand.shape[1]),
+        "candWp": int(b.cand_wp), "candWr": int(b.cand_wr)}))
+
+
+@pytest.mark.gpu
+def test_node_batch_matches_c_abi(tmp_path):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from acs_mi355x import native
+    _addon()
+    cs = compiler.compile_store(store.populate(synth.c2_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 20_000, "c2", seed=99)
+    _dump(tmp_path, cs, sb.batch)
+    r = subprocess.run([NODE, RUNNER, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    t = native.Tables(compiler.store_blob(cs), 0)
+    want = t.is_allowed(sb.batch).view(np.uint8).reshape(-1)
+    bits, obl, obl_n, out = t.what_is_allowed(sb.batch)
+    t.close()
+    for f in ("out_sync.bin", "out_async.bin"):
+        assert np.array_equal(np.frombuffer(tmp_path.joinpath(f).read_bytes(), np.uint8), want), f
+    assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_bits.bin").read_bytes(), np.uint32),
+                          bits.reshape(-1))
+    assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_obl_n.bin").read_bytes(), np.uint32), obl_n)
