@@ -433,14 +433,16 @@ class Encoder:
         return b
 
 
-def attach_candidates(cs, b: RequestBatch, col_values):
-    """Candidate bitsets for the batch's entity columns + each request's column in its flags."""
+def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True):
+    """Candidate rows for the batch's request classes + each request's class id in its flags."""
     ncols = b.rx.shape[0]
     assert len(col_values) <= ncols
     # pad: columns without a value (an all-empty batch) get no candidates beyond the "always" nodes
     vals = list(col_values) + [object()] * (ncols - len(col_values))
-    b.cand = candidates.build(cs, vals, b.rx)
+    ent = candidates.entity_candidates(cs, vals, b.rx)
     ws, wp, _ = candidates.section_words(cs)
     b.cand_wp, b.cand_wr = ws, ws + wp
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
-    b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (pcol.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))
+    roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
+    cls, b.cand = candidates.classes(cs, b.hdr, roles, pcol, ent)
+    b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

@@ -20,7 +20,8 @@ class ReqBatchC(C.Structure):
     _fields_ = [("n", C.c_uint32), ("hdr", C.c_void_p), ("res", C.c_void_p), ("subj", C.c_void_p),
                 ("act", C.c_void_p), ("roles", C.c_void_p), ("arena", C.c_void_p), ("arena_words", C.c_size_t),
                 ("rx", C.c_void_p), ("rx_cols", C.c_uint32), ("rx_rows", C.c_uint32),
-                ("cand", C.c_void_p), ("cand_words", C.c_uint32), ("cand_wp", C.c_uint32), ("cand_wr", C.c_uint32)]
+                ("cand", C.c_void_p), ("cand_words", C.c_uint32), ("cand_wp", C.c_uint32), ("cand_wr", C.c_uint32),
+                ("cand_rows", C.c_uint32)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -90,6 +91,7 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
     s.rx_rows = int(b.rx.shape[1])
     if b.cand is not None:
         s.cand_words, s.cand_wp, s.cand_wr = b.cand.shape[1], b.cand_wp, b.cand_wr
+        s.cand_rows = b.cand.shape[0]
     return s
 
 

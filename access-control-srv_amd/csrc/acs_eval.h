@@ -57,8 +57,9 @@ struct Batch {
   const uint32_t* arena;
   const uint8_t* rx;      // [cols][rx_rows]
   uint32_t rx_rows;
-  const uint32_t* cand;   // [cols+1][cand_words] candidate bitsets (sets | policies | rules)
+  const uint32_t* cand;   // [cand_rows][cand_words] candidate bitsets (sets | policies | rules) per class
   uint32_t cand_words, cand_wp, cand_wr;  // row length, word offsets of the policy / rule sections
+  uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
 };
 
 // Candidate filter of a wave (GPU: the union of its lanes' columns, gathered with
@@ -638,7 +639,7 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
-  F.all = B.cand == nullptr || pc == PCOL_ALL || (h.flags & RQ_NO_TARGET);
+  F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
   F.n = F.all ? 0 : 1;
   F.col[0] = pc;
   return F;

@@ -36,24 +36,27 @@ int fail(const std::string& msg) {
 
 constexpr int BLOCK = 256;
 
-// Sort key that makes a wave share its entity, role and action (so table-driven
-// branches are wave-uniform): [entity id:15 | role id:10 | action id:7].
+// Sort key that makes a wave share its request class (entity column x required roles,
+// hence one candidate row) and action, so table-driven branches are wave-uniform:
+// [class:16 | action id:16].  Unfiltered requests (PCOL_ALL) group by first entity id.
 __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __restrict__ keys,
                                                           uint32_t* __restrict__ idx) {
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   if (k >= B.n) return;
   const ReqHdr h = B.hdr[k];
-  uint32_t ent = 0;
-  for (uint32_t j = 0; j < h.nres; ++j) {
-    const ReqRes q = B.res[(size_t)j * B.n + k];
-    if (q.kind & K_ENT) {
-      ent = q.value;
-      break;
+  uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
+  uint32_t low = h.nact ? B.act[k].value : 0u;
+  if (cls >= B.cand_rows) {
+    cls = B.cand_rows;  // one bucket after the filtered classes (keeps the key range tight)
+    for (uint32_t j = 0; j < h.nres; ++j) {
+      const ReqRes q = B.res[(size_t)j * B.n + k];
+      if (q.kind & K_ENT) {
+        low = q.value;
+        break;
+      }
     }
   }
-  const uint32_t role = h.nroles ? B.roles[k] : 0u;
-  const uint32_t act = h.nact ? B.act[k].value : 0u;
-  keys[k] = ((ent & 0x7FFFu) << 17) | ((role & 0x3FFu) << 7) | (act & 0x7Fu);
+  keys[k] = (cls << 16) | (low & 0xFFFFu);
   idx[k] = k;
 }
 
@@ -72,7 +75,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t pcol) 
   while (pending && !F.all) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t c = __builtin_amdgcn_readlane(pcol, leader);
-    if (c == PCOL_ALL || F.n == 4) {
+    if (c == PCOL_ALL || c >= B.cand_rows || F.n == 4) {
       F.all = true;
       break;
     }
@@ -260,6 +263,7 @@ static Batch to_batch(const acs_req_batch* b) {
   B.cand_words = b->cand_words;
   B.cand_wp = b->cand_wp;
   B.cand_wr = b->cand_wr;
+  B.cand_rows = b->cand ? b->cand_rows : 0u;
   return B;
 }
 
@@ -281,14 +285,16 @@ int acs_set_option(acs_tables* t, int option, int value) {
   return fail("acs_set_option: unknown option");
 }
 
-// Coherence sort: permutation of request indices ordered by (entity, role, action).
+// Coherence sort: permutation of request indices ordered by (class, action).
 static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
   *perm = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
+  int end_bit = 16;  // keys < (cand_rows + 1) << 16
+  while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - 16)) != 0) ++end_bit;
   size_t temp = 0;
   HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 32, s));
+                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, end_bit, s));
   const size_t need = 4 * n * sizeof(uint32_t) + temp + 256;
   if (need > t->ws_bytes) {
     if (t->ws) HIP_OK(hipFree(t->ws));
@@ -304,7 +310,7 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   void* tmp = (void*)(((uintptr_t)(idx_out + n) + 255) & ~uintptr_t(255));
   hipLaunchKernelGGL(sort_keys_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, B, keys_in, idx_in);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, 0, 32, s));
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, 0, end_bit, s));
   *perm = idx_out;
   return 0;
 }
@@ -389,7 +395,7 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
       D.up(b->arena, b->arena_words * sizeof(uint32_t), (const void**)&D.d.arena, s) ||
       D.up(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&D.d.rx, s))
     return -1;
-  if (b->cand && D.up(b->cand, ((size_t)b->rx_cols + 1) * b->cand_words * sizeof(uint32_t),
+  if (b->cand && D.up(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t),
                       (const void**)&D.d.cand, s))
     return -1;
   return 0;

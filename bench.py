@@ -30,18 +30,85 @@ WORKLOADS = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
 
+def _node_bytes(nodes):
+    """Bytes of a node record plus the pools it references (pairs 8 B, rule attrs 16 B, ACL roles 4 B)."""
+    return (64 + 8 * (nodes["subj_n"].astype(np.int64) + nodes["act_n"]) + 16 * nodes["res_n"].astype(np.int64)
+            + 4 * nodes["acl_roles_n"].astype(np.int64))
+
+
+def scan_bytes(cs, batch, wave=64):
+    """Table bytes the K1 waves visit, counted from the same candidate rows the kernel uses:
+    requests in coherence-sort order, 64 per wave, the union of <= 4 class rows per wave
+    (more, or an unfiltered class: the whole table); a policy is visited only inside a
+    visited set, a rule only inside a visited policy.  Returns total bytes for the batch."""
+    from acs_mi355x import layout as L
+    n = batch.n
+    cand = batch.cand
+    R = 0 if cand is None else cand.shape[0]
+    h = batch.hdr
+    cls = (h["flags"] >> np.uint32(L.RQ_PCOL_SHIFT)).astype(np.int64)
+    cls = np.where(cls >= R, R, cls)
+    low = np.where(h["nact"] > 0, batch.act["value"][0], 0).astype(np.int64) & 0xFFFF
+    order = np.argsort((cls << 16) | low, kind="stable")
+    cw = cls[order]
+    ns, npol, nr = cs.n_sets, cs.n_pols, cs.n_rules
+    bs, bp, br = _node_bytes(cs.sets), _node_bytes(cs.pols), _node_bytes(cs.rules)
+    par_p = np.repeat(np.arange(ns), (cs.sets["child_end"] - cs.sets["child_begin"]).astype(np.int64))
+    par_r = np.repeat(np.arange(npol), (cs.pols["child_end"] - cs.pols["child_begin"]).astype(np.int64))
+    full = int(bs.sum() + bp.sum() + br.sum())
+    ws = (ns + 31) // 32
+    wp = (npol + 31) // 32
+    cache = {}
+
+    def union_bytes(key):
+        if key in cache:
+            return cache[key]
+        if any(c >= R for c in key) or len(key) > 4:
+            cache[key] = full
+            return full
+        row = np.bitwise_or.reduce(cand[list(key)], axis=0)
+        bits = np.unpackbits(row.view(np.uint8), bitorder="little").astype(bool)
+        s = bits[:ns]
+        p = bits[32 * ws:32 * ws + npol] & s[par_p]
+        r = bits[32 * (ws + wp):32 * (ws + wp) + nr] & p[par_r]
+        v = int(bs[s].sum() + bp[p].sum() + br[r].sum())
+        cache[key] = v
+        return v
+
+    total = 0
+    for w0 in range(0, n, wave):
+        total += union_bytes(tuple(np.unique(cw[w0:w0 + wave]).tolist()))
+    return total, full
+
+
 def algorithmic_bytes(cs, batch):
-    """Per-decision algorithmic bytes: B_req + B_ctx + B_out + B_scan/64."""
+    """Per-decision algorithmic bytes: B_req + B_ctx + B_out + B_scan/T, with
+    B_scan the table bytes each 64-request tile actually visits (candidate rows, see scan_bytes)."""
     h = batch.hdr
     b_req = 16 + 16 * h["nres"].astype(np.float64) + 8 * h["nsubj"] + 8 * h["nact"] + 4 * h["nroles"]
-    # context arena words actually owned per request (shared arenas count once per request anyway)
-    if batch.n > 1 and h["arena_off"][-1] > 0:
-        ctx = batch.arena.size * 4.0 / batch.n
-    else:
-        ctx = float(batch.arena.size * 4)
-    b_scan = float(cs.table_bytes())  # brute-force tile: the whole table per 64-request wave
-    per = float(b_req.mean()) + ctx + 8.0 + b_scan / 64.0
-    return per, {"B_req": float(b_req.mean()), "B_ctx": ctx, "B_out": 8.0, "B_scan_per_tile": b_scan, "T": 64}
+    # context arena bytes each request reads (its own record; a shared record counts for every request)
+    offs = h["arena_off"].astype(np.int64)
+    uo = np.unique(offs)
+    size = np.diff(np.append(uo, batch.arena.size))
+    ctx = float(4.0 * size[np.searchsorted(uo, offs)].mean()) if batch.n else 0.0
+    scan_total, full = scan_bytes(cs, batch)
+    b_scan_per_dec = scan_total / max(batch.n, 1)
+    per = float(b_req.mean()) + ctx + 8.0 + b_scan_per_dec
+    return per, {"B_req": float(b_req.mean()), "B_ctx": ctx, "B_out": 8.0, "B_scan_per_decision": b_scan_per_dec,
+                 "B_scan_per_tile": b_scan_per_dec * 64, "table_bytes_full": full, "T": 64,
+                 "bruteforce_bytes_per_decision": float(b_req.mean()) + ctx + 8.0 + full / 64.0}
+
+
+def measured_traffic(config, kernel="is_allowed_kernel"):
+    """HBM bytes per K1 launch from the committed PMC pass of the same bench command
+    (profiles/traffic.json, written by tools/pmc.sh: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    e = d.get(config, {}).get(kernel)
+    return (e["bytes_per_launch"], e["source"]) if e else (None, None)
 
 
 def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
@@ -83,7 +150,8 @@ def main():
     ap.add_argument("--requests", type=int, default=0, help="requests per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-sort", action="store_true", help="disable the (entity, role, action) coherence sort")
+    ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,7 +165,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from acs_mi355x import compiler, native, store, synth
+    from acs_mi355x import compiler, native, store, synth, layout as L
     from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor
     from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
 
@@ -138,11 +206,22 @@ def main():
         elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
     dec = decisions_from_tensor(out)
+    pcie = None
+    if rank == 0 and not args.no_pcie:
+        # host buffers through acs_is_allowed: H2D + sort + K1 + D2H (reported beside, never `value`)
+        tables.is_allowed(sb.batch)
+        t1 = time.perf_counter()
+        host_dec = tables.is_allowed(sb.batch)
+        pcie_s = time.perf_counter() - t1
+        pcie = {"value": n / pcie_s, "unit": "decisions/s", "ms": pcie_s * 1e3, "input_bytes": int(sb.batch.nbytes()),
+                "identical_to_device_path": bool(np.array_equal(host_dec.view(np.uint64), dec.view(np.uint64)))}
     if rank == 0:
         per_dec, parts = algorithmic_bytes(cs, sb.batch)
         achieved = per_dec * n / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = measured_traffic(kind)
         value = world * n * args.steps / elapsed
         mix = np.bincount(dec["decision"], minlength=7)
+        host = int(((dec["flags"] & (L.OF_HOST_REQ | L.OF_HOST_COND)) != 0).sum())
         line = {
             "metric": "authorization decisions/sec (isAllowed)", "value": value, "unit": "decisions/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -150,13 +229,18 @@ def main():
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": desc, "requests_per_gpu": n, "policy_sets": cs.n_sets, "policies": cs.n_pols,
                        "rules": cs.n_rules, "table_bytes": cs.table_bytes(), "parallelism": f"requests dp{world}",
-                       "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])}},
+                       "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])},
+                       "host_fallback_fraction": host / n, "request_classes": int(sb.batch.cand.shape[0])},
             "coherence_sort": not args.no_sort,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "is_allowed_kernel",
-                         "kernel_ms": kern_ms, "step_gpu_ms": step_ms, "bytes_per_decision": per_dec,
-                         "bytes_parts": parts},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_unit": "HBM bytes per K1 launch (rocprofv3 PMC)",
+                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": per_dec * n,
+                         "kernel": "is_allowed_kernel", "kernel_ms": kern_ms, "step_gpu_ms": step_ms,
+                         "bytes_per_decision": per_dec, "bytes_parts": parts},
         }
+        if pcie:
+            line["pcie_inclusive"] = pcie
         if world == 1 and not args.no_cpu_baseline:
             cb, par = cpu_baseline(kind, doc, sb, dec, cs, args.cpu_seconds)
             line["cpu_baseline"] = cb

@@ -53,10 +53,12 @@ typedef struct {
   size_t arena_words;
   const uint8_t* rx;      /* [rx_cols][rx_rows] regex matrix   */
   uint32_t rx_cols, rx_rows;
-  /* [rx_cols + 1][cand_words] candidate bitsets over (sets | policies | rules) per entity
-   * column (last row: requests without entity attributes); NULL = evaluate every node. */
+  /* [cand_rows][cand_words] candidate bitsets over (sets | policies | rules), one row per
+   * request class (entity column x required roles, acs_mi355x/candidates.py); the class id
+   * is in ReqHdr.flags >> 16.  NULL = evaluate every node. */
   const uint32_t* cand;
   uint32_t cand_words, cand_wp, cand_wr;
+  uint32_t cand_rows;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */

@@ -53,6 +53,7 @@ static Batch host_batch(const acs_req_batch* b) {
   B.cand_words = b->cand_words;
   B.cand_wp = b->cand_wp;
   B.cand_wr = b->cand_wr;
+  B.cand_rows = b->cand ? b->cand_rows : 0u;
   return B;
 }
 

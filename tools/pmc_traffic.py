@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Per-launch HBM bytes of a kernel from the tools/pmc.sh counter passes.
+
+traffic = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes, averaged over dispatches:
+rocprofv3 reports both in KiB, and on gfx950 FETCH_SIZE counts half the bytes of
+wide coalesced reads (MI355X_MICROARCH.md, HBM section).  Writes/updates
+<out>[config][kernel] = {bytes_per_launch, fetch_kib, write_kib, dispatches, source}.
+usage: pmc_traffic.py <pmc dir> <config> <out.json> [kernel-substring]
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def read(path, kernel):
+    vals = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if kernel in r.get("Kernel_Name", ""):
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    pmc, config, out = sys.argv[1:4]
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "is_allowed_kernel"
+    fetch = read(os.path.join(pmc, "g3", "pmc_counter_collection.csv"), kernel)["FETCH_SIZE"]
+    write = read(os.path.join(pmc, "g4", "pmc_counter_collection.csv"), kernel)["WRITE_SIZE"]
+    if not fetch or not write:
+        sys.exit("no FETCH_SIZE / WRITE_SIZE rows for " + kernel)
+    f = sum(fetch) / len(fetch)
+    w = sum(write) / len(write)
+    d = json.load(open(out)) if os.path.exists(out) else {}
+    d.setdefault(config, {})[kernel.split("(")[0]] = {
+        "bytes_per_launch": (2 * f + w) * 1024, "fetch_kib": f, "write_kib": w, "dispatches": len(fetch),
+        "source": os.environ.get("TRAFFIC_SOURCE", pmc)}
+    json.dump(d, open(out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(d[config]))
+
+
+if __name__ == "__main__":
+    main()
