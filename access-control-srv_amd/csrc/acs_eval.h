@@ -29,6 +29,34 @@ namespace acs {
 
 #define ACS_FN __host__ __device__ inline
 
+template <class T, int NW = sizeof(T) / 4>
+ACS_FN T load_words(const T* p);
+
+// Value every active lane of the wave holds identically (a table index or bitset word of
+// the wave-shared candidate iteration): move it to an SGPR so the node records behind it
+// are fetched with scalar loads.  Identity in the host build of the core.
+ACS_FN uint32_t wave_uniform(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane(x);
+#else
+  return x;
+#endif
+}
+
+// Table records are read as whole dwords and unpacked in registers: with a wave-uniform
+// address this is one s_load_dwordx{4,16} (scalar loads have no byte / short forms).
+template <class T, int NW>
+ACS_FN T load_words(const T* p) {
+  static_assert(sizeof(T) == 4 * NW, "record must be a whole number of dwords");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  uint32_t v[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = w[k];
+  T out;
+  __builtin_memcpy(&out, v, sizeof(T));
+  return out;
+}
+
 struct Pair {
   uint32_t id, value;
 };
@@ -62,23 +90,25 @@ struct Batch {
   uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
 };
 
-// Candidate filter of a wave (GPU: the union of its lanes' columns, gathered with
-// ballots; host build: the request's own column).  Wave-uniform by construction.
+// Candidate filter of a wave (GPU: the union of its lanes' class rows, gathered with
+// ballots; host build: the request's own row).  Wave-uniform by construction; the rows
+// are explicit pointers (no dynamically indexed array, so the filter stays in SGPRs).
 struct Filter {
-  const uint32_t* cand;
-  uint32_t W, wp, wr;
-  uint32_t n;        // number of columns (0 with all = true)
-  uint32_t col[4];
-  bool all;          // no filtering
+  const uint32_t* row[4];  // class rows (nullptr: unused)
+  uint32_t wp, wr;         // word offsets of the policy / rule sections
+  bool all;                // no filtering
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
-    uint32_t x = 0;
-    for (uint32_t k = 0; k < n; ++k) x |= cand[(size_t)col[k] * W + w];
-    return x;
+    uint32_t x = row[0][w];
+    if (row[1]) x |= row[1][w];
+    if (row[2]) x |= row[2][w];
+    if (row[3]) x |= row[3][w];
+    return wave_uniform(x);
   }
 };
 
-// Ascending iteration over the candidate indices in [b, e) of one bitset section.
+// Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
+// lane that is still inside the loop holds the same iterator state.
 struct CandRange {
   const Filter& F;
   uint32_t off, base, e, bits;
@@ -89,7 +119,7 @@ struct CandRange {
   ACS_FN bool next(uint32_t& out) {
     for (;;) {
       if (bits) {
-        const uint32_t x = base + (uint32_t)__builtin_ctz(bits);
+        const uint32_t x = wave_uniform(base + (uint32_t)__builtin_ctz(bits));
         bits &= bits - 1;
         if (x >= e) return false;
         out = x;
@@ -167,7 +197,15 @@ struct ReqLds : ReqCtx {
   uint32_t stride;
   ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st)
       : ReqCtx(t, b, idx, hd), col(c), stride(st) {}
-  ACS_FN ReqRes res(int j) const { return j < LDS_SLOTS ? col[j * stride] : B.res[(size_t)j * B.n + i]; }
+  ACS_FN ReqRes res(int j) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) const ReqRes lds_res;  // ds_read, not flat
+    if (j < LDS_SLOTS) return ((lds_res*)col)[j * stride];
+#else
+    if (j < LDS_SLOTS) return col[j * stride];
+#endif
+    return B.res[(size_t)j * B.n + i];
+  }
 };
 
 // Resource attributes read from HBM on every use (host build of the core).
@@ -180,7 +218,7 @@ struct ReqMem : ReqCtx {
 ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const ReqCtx& R, bool subjects) {
   const uint32_t qn = subjects ? R.h.nsubj : R.h.nact;
   for (uint32_t k = 0; k < rn; ++k) {
-    const Pair a = rule[k];
+    const Pair a = load_words(rule + wave_uniform(k));
     bool found = false;
     for (uint32_t j = 0; j < qn && !found; ++j) {
       const Pair q = subjects ? R.subj(j) : R.act(j);
@@ -217,7 +255,7 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
     const ReqRes q = R.res(j);
     pm = false;
     for (uint32_t k = 0; k < t.res_n; ++k) {
-      const RuleResAttr r = ra[k];
+      const RuleResAttr r = load_words(ra + wave_uniform(k));
       if (r.kind & K_PROP) rp = true;
       if (!regex) {
         if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
@@ -350,7 +388,7 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
   bool all_direct = true, all_ok = true;
   const RuleResAttr* ra = R.T.rres + t.res_off;
   for (uint32_t k = 0; k < t.res_n; ++k) {
-    const RuleResAttr r = ra[k];
+    const RuleResAttr r = load_words(ra + wave_uniform(k));
     if (r.kind & K_ENT_LOOSE) {
       bool em = false;
       for (int j = 0; j < (int)R.h.nres; ++j) {
@@ -475,7 +513,7 @@ ACS_FN tri multiple_entities(const NodeRec& S, const RQ& R) {
     if (!(q.kind & K_ENT)) continue;
     bool multi = false;
     for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
-      const NodeRec P = R.T.pols[p];
+      const NodeRec P = load_words(R.T.pols + p);
       if (P.nflags & NF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
       if (!(P.nflags & NF_HAS_TARGET) || P.res_n == 0) continue;
       const uint8_t pe = (P.nflags & NF_EFFECT_TRUTHY) ? P.effect : (uint8_t)EFF_UNDEF;  // no PERMIT default
@@ -506,7 +544,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = T.sets[s];
+    const NodeRec S = load_words(T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
       if (m < 0) return make_err(m);
@@ -519,7 +557,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = T.pols[p];
+        const NodeRec P = load_words(T.pols + p);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
@@ -541,7 +579,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = T.pols[p];
+      const NodeRec P = load_words(T.pols + p);
       if (P.nflags & NF_NULL) continue;
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
@@ -562,7 +600,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = T.rules[r];
+        const NodeRec Q = load_words(T.rules + r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
@@ -634,14 +672,11 @@ ACS_FN Decision early_decision(const ReqHdr& h, bool* done) {
 // Filter of a single request (host build / per-lane reference).
 ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   Filter F{};
-  F.cand = B.cand;
-  F.W = B.cand_words;
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
-  F.n = F.all ? 0 : 1;
-  F.col[0] = pc;
+  F.row[0] = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
   return F;
 }
 
@@ -664,7 +699,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = T.sets[s];
+    const NodeRec S = load_words(T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
       if (m < 0) return make_err(m);
@@ -676,7 +711,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = T.pols[p];
+        const NodeRec P = load_words(T.pols + p);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, true, &obl);
@@ -698,7 +733,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = T.pols[p];
+      const NodeRec P = load_words(T.pols + p);
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
         const tri m = target_match(P, R, pe, !exact, true, &obl);
@@ -709,7 +744,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = T.rules[r];
+        const NodeRec Q = load_words(T.rules + r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {

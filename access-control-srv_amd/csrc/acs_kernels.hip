@@ -60,29 +60,32 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
   idx[k] = k;
 }
 
-// Union of the candidate columns of the wave's active requests (<= 4 distinct after the
+// Union of the candidate class rows of the wave's active requests (<= 4 distinct after the
 // coherence sort; more, or an unfiltered request, disables filtering for the wave).
 // Called with every lane of the wave present, before any lane diverges.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t pcol) {
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls) {
   Filter F{};
-  F.cand = B.cand;
-  F.W = B.cand_words;
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   F.all = B.cand == nullptr;
-  F.n = 0;
+  uint32_t n = 0;
   uint64_t pending = __ballot(valid);
   while (pending && !F.all) {
     const int leader = __builtin_ctzll(pending);
-    const uint32_t c = __builtin_amdgcn_readlane(pcol, leader);
-    if (c == PCOL_ALL || c >= B.cand_rows || F.n == 4) {
+    const uint32_t c = __builtin_amdgcn_readlane(cls, leader);
+    if (c == PCOL_ALL || c >= B.cand_rows || n == 4) {
       F.all = true;
       break;
     }
-    F.col[F.n++] = c;
-    pending &= ~__ballot(valid && pcol == c);
+    const uint32_t* r = B.cand + (size_t)c * B.cand_words;
+    if (n == 0) F.row[0] = r;
+    else if (n == 1) F.row[1] = r;
+    else if (n == 2) F.row[2] = r;
+    else F.row[3] = r;
+    ++n;
+    pending &= ~__ballot(valid && cls == c);
   }
-  if (F.all) F.n = 0;
+  if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
   return F;
 }
 
