@@ -215,4 +215,11 @@ def classes(cs, hdr, roles, pcol, ent):
             pol_any = np.zeros((len(ck), cs.n_sets), bool)
         s &= pol_any & nonempty[None, :]
         out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+    # heaviest classes first: the kernel's sort key orders waves by class id, so the longest
+    # waves are dispatched first (longest-processing-time-first; no tail of heavy waves)
+    cost = np.unpackbits(out.view(np.uint8), axis=1).sum(axis=1)
+    rank = np.empty(len(cost), np.int64)
+    rank[np.argsort(-cost, kind="stable")] = np.arange(len(cost))
+    out = np.ascontiguousarray(out[np.argsort(rank)])
+    cls[active] = rank[inv].astype(np.uint32)
     return cls, out

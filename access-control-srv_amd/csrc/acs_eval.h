@@ -95,10 +95,14 @@ struct Batch {
 // are explicit pointers (no dynamically indexed array, so the filter stays in SGPRs).
 struct Filter {
   const uint32_t* row[4];  // class rows (nullptr: unused)
+  const uint32_t* lds;     // GPU: the wave's OR of all its class rows, in LDS (nullptr: use row[])
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   bool all;                // no filtering
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (lds) return wave_uniform(((__attribute__((address_space(3))) const uint32_t*)lds)[w]);
+#endif
     uint32_t x = row[0][w];
     if (row[1]) x |= row[1][w];
     if (row[2]) x |= row[2][w];

@@ -38,16 +38,19 @@ constexpr int BLOCK = 256;
 
 // Sort key that makes a wave share its request class (entity column x required roles,
 // hence one candidate row) and action, so table-driven branches are wave-uniform:
-// [class:16 | action id:16].  Unfiltered requests (PCOL_ALL) group by first entity id.
+// [bucket:16 | action id:16].  Class ids come heaviest-first from the host (most
+// candidate nodes), and unfiltered requests (PCOL_ALL) take bucket 0, so the longest
+// waves start first and the launch has no long tail.  Unfiltered requests group by
+// their first entity id.
 __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __restrict__ keys,
                                                           uint32_t* __restrict__ idx) {
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   if (k >= B.n) return;
   const ReqHdr h = B.hdr[k];
-  uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
-  uint32_t low = h.nact ? B.act[k].value : 0u;
+  const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
+  uint32_t low = h.nact ? B.act[k].value : 0u, bucket = cls + 1;
   if (cls >= B.cand_rows) {
-    cls = B.cand_rows;  // one bucket after the filtered classes (keeps the key range tight)
+    bucket = 0;
     for (uint32_t j = 0; j < h.nres; ++j) {
       const ReqRes q = B.res[(size_t)j * B.n + k];
       if (q.kind & K_ENT) {
@@ -56,37 +59,59 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
       }
     }
   }
-  keys[k] = (cls << 16) | (low & 0xFFFFu);
+  keys[k] = (bucket << 16) | (low & 0xFFFFu);
   idx[k] = k;
 }
 
-// Union of the candidate class rows of the wave's active requests (<= 4 distinct after the
-// coherence sort; more, or an unfiltered request, disables filtering for the wave).
-// Called with every lane of the wave present, before any lane diverges.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls) {
+// Candidate filter of a wave, built with every lane present before any lane diverges.
+// With an LDS row (`lds` = this wave's W-word region) the filter is the OR of the class
+// rows of all the wave's active requests, however many classes the wave spans.  Without
+// one (tables too large for LDS) it keeps up to 4 row pointers, else no filtering.  An
+// unfiltered request (PCOL_ALL) disables filtering for its wave.
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t* lds) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   F.all = B.cand == nullptr;
+  const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
+  if (lds && !F.all)
+    for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
   uint32_t n = 0;
   uint64_t pending = __ballot(valid);
   while (pending && !F.all) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t c = __builtin_amdgcn_readlane(cls, leader);
-    if (c == PCOL_ALL || c >= B.cand_rows || n == 4) {
+    if (c == PCOL_ALL || c >= B.cand_rows || (!lds && n == 4)) {
       F.all = true;
       break;
     }
-    const uint32_t* r = B.cand + (size_t)c * B.cand_words;
-    if (n == 0) F.row[0] = r;
-    else if (n == 1) F.row[1] = r;
-    else if (n == 2) F.row[2] = r;
-    else F.row[3] = r;
+    const uint32_t* r = B.cand + (size_t)c * W;
+    if (lds) {
+      for (uint32_t w = lane; w < W; w += 64) lds[w] |= r[w];
+    } else if (n == 0) {
+      F.row[0] = r;
+    } else if (n == 1) {
+      F.row[1] = r;
+    } else if (n == 2) {
+      F.row[2] = r;
+    } else {
+      F.row[3] = r;
+    }
     ++n;
     pending &= ~__ballot(valid && cls == c);
   }
   if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
+  if (!F.all && lds) F.lds = lds;
   return F;
+}
+
+// Dynamic LDS: one W-word union row per wave when W <= LDS_FILTER_WORDS.
+constexpr uint32_t LDS_FILTER_WORDS = 1024;
+extern __shared__ uint32_t acs_dyn_lds[];
+
+__device__ inline uint32_t* wave_lds_row(const Batch& B) {
+  if (!B.cand || B.cand_words > LDS_FILTER_WORDS) return nullptr;
+  return acs_dyn_lds + (threadIdx.x >> 6) * B.cand_words;
 }
 
 __device__ inline uint32_t request_pcol(const ReqHdr& h) {
@@ -105,7 +130,7 @@ __global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, co
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
-  const Filter F = wave_filter(B, in && !done, request_pcol(h));
+  const Filter F = wave_filter(B, in && !done, request_pcol(h), wave_lds_row(B));
   if (!in) return;
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
@@ -129,7 +154,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h));
+  const Filter F = wave_filter(B, in && !host, request_pcol(h), wave_lds_row(B));
   if (!in) return;
   uint32_t* my_bits = bits + (size_t)i * words;
   for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
@@ -148,6 +173,10 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
 }
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+size_t filter_lds_bytes(const Batch& B) {
+  return (B.cand && B.cand_words <= LDS_FILTER_WORDS) ? (size_t)(BLOCK / 64) * B.cand_words * 4 : 0;
+}
 
 }  // namespace
 
@@ -328,7 +357,7 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, perm, (Decision*)out);
+  hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
@@ -358,7 +387,7 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   const uint32_t* perm = nullptr;
   if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
-  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), 0, s, t->view, B, perm, acs_wia_words_per_request(t),
+  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, acs_wia_words_per_request(t),
                      bits, obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   return 0;

@@ -38,8 +38,9 @@ def _node_bytes(nodes):
 
 def scan_bytes(cs, batch, wave=64):
     """Table bytes the K1 waves visit, counted from the same candidate rows the kernel uses:
-    requests in coherence-sort order, 64 per wave, the union of <= 4 class rows per wave
-    (more, or an unfiltered class: the whole table); a policy is visited only inside a
+    requests in coherence-sort order, 64 per wave, the union of the wave's class rows (an
+    unfiltered class, or > 4 classes when the row is too long for LDS: the whole table); a
+    policy is visited only inside a
     visited set, a rule only inside a visited policy.  Returns total bytes for the batch."""
     from acs_mi355x import layout as L
     n = batch.n
@@ -49,7 +50,8 @@ def scan_bytes(cs, batch, wave=64):
     cls = (h["flags"] >> np.uint32(L.RQ_PCOL_SHIFT)).astype(np.int64)
     cls = np.where(cls >= R, R, cls)
     low = np.where(h["nact"] > 0, batch.act["value"][0], 0).astype(np.int64) & 0xFFFF
-    order = np.argsort((cls << 16) | low, kind="stable")
+    bucket = np.where(cls >= R, 0, cls + 1)  # sort_keys_kernel: unfiltered first, then class ids
+    order = np.argsort((bucket << 16) | low, kind="stable")
     cw = cls[order]
     ns, npol, nr = cs.n_sets, cs.n_pols, cs.n_rules
     bs, bp, br = _node_bytes(cs.sets), _node_bytes(cs.pols), _node_bytes(cs.rules)
@@ -63,7 +65,8 @@ def scan_bytes(cs, batch, wave=64):
     def union_bytes(key):
         if key in cache:
             return cache[key]
-        if any(c >= R for c in key) or len(key) > 4:
+        lds_union = cand is not None and cand.shape[1] <= 1024  # K1 ORs every class row in LDS
+        if any(c >= R for c in key) or (len(key) > 4 and not lds_union):
             cache[key] = full
             return full
         row = np.bitwise_or.reduce(cand[list(key)], axis=0)

@@ -22,6 +22,8 @@ for s in $STEPS; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     nosort) step bench_nosort 600 python bench.py --steps 5 --warmup 1 --no-sort --no-cpu-baseline ;;
+    quick) step bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie ;;
+    quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
