@@ -47,6 +47,17 @@ def build_product(force=False):
     return LIB
 
 
+PROF_LIB = os.path.join(PKG, "lib", "libacs_mi355x_prof.so")
+
+
+def build_prof(force=False):
+    """Phase-profiling variant of the product library (-DACS_PHASE_PROF; tools/phase_prof.py)."""
+    src = os.path.join(CSRC, "acs_kernels.hip")
+    if force or _stale(PROF_LIB, [src] + _HEADERS):
+        _hipcc(src, PROF_LIB, ("-DACS_PHASE_PROF",))
+    return PROF_LIB
+
+
 NAPI_SRC = os.path.join(PKG, "napi", "acs_napi.c")
 NAPI_OUT = os.path.join(PKG, "lib", "acs_mi355x.node")
 NODE_INC = "/usr/include/node"

@@ -43,6 +43,18 @@ ACS_FN uint32_t wave_uniform(uint32_t x) {
 #endif
 }
 
+// Phase profiling (tools/phase_prof.py; a separate -DACS_PHASE_PROF build only): per-lane
+// cycle counters of the evaluation phases, summed per wave by the kernel.
+enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET, PH_RULE_TARGET, PH_RULE_HR,
+                 PH_RULE_ACL, PH_N };
+#if defined(ACS_PHASE_PROF)
+#define PROF_T0(v) const uint64_t v = __builtin_readcyclecounter()
+#define PROF_ADD(k, v) (R.prof[k] += __builtin_readcyclecounter() - (v))
+#else
+#define PROF_T0(v)
+#define PROF_ADD(k, v)
+#endif
+
 // Table records are read as whole dwords and unpacked in registers: with a wave-uniform
 // address this is one s_load_dwordx{4,16} (scalar loads have no byte / short forms).
 template <class T, int NW>
@@ -172,6 +184,9 @@ struct ReqCtx {
   const uint32_t* ar;
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
+#if defined(ACS_PHASE_PROF)
+  mutable uint64_t prof[PH_N] = {};
+#endif
 
   ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : T(t), B(b), i(idx), h(hd) {
     ar = B.arena + h.arena_off;
@@ -338,6 +353,19 @@ ACS_FN tri target_match(const NodeRec& t, const RQ& R, uint8_t effect, bool rege
   if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
   return resource_match(t, R, effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect, regex, wia, 0, R.h.nres,
                         R.flag(RQ_ANY_PROP), obl);
+}
+
+// Rule targets: the exact pass, then the RegExp retry (accessController.ts:214-219, 400-409).
+// Subjects and actions do not depend on the mode, so when they fail both passes are false.
+template <class RQ>
+ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, bool wia, OblLog* obl) {
+  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
+  if (!subject_match(t, R)) return 0;
+  if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
+  const uint8_t eff = effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect;
+  const tri m = resource_match(t, R, eff, false, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
+  if (m != 0) return m;
+  return resource_match(t, R, eff, true, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
 }
 
 // ------------------------------------------------------------------ checkHierarchicalScope
@@ -540,7 +568,18 @@ ACS_FN Decision make_err(tri e) {
 }
 
 template <class RQ>
+ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F);
+
+template <class RQ>
 ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
+  PROF_T0(t_total);
+  const Decision d = is_allowed_body(R, F);
+  PROF_ADD(PH_TOTAL, t_total);
+  return d;
+}
+
+template <class RQ>
+ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
   const Tables& T = R.T;
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
@@ -550,13 +589,16 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
   while (sets.next(s)) {
     const NodeRec S = load_words(T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
+      PROF_T0(t0);
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
+      PROF_ADD(PH_SET_TARGET, t0);
       if (m < 0) return make_err(m);
       if (!m) continue;
     }
     // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
     bool exact = false;
     uint8_t pe = S.pe_at;  // after a full scan
+    PROF_T0(t2a);
     {
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
@@ -574,8 +616,11 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
         }
       }
     }
+    PROF_ADD(PH_POL_EXACT, t2a);
     if (exact && R.flag(RQ_MULTI_ENT)) {
+      PROF_T0(tm);
       const tri m = multiple_entities(S, R);
+      PROF_ADD(PH_MULTI, tm);
       if (m < 0) return make_err(m);
       exact = m != 0;
     }
@@ -587,14 +632,19 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
       if (P.nflags & NF_NULL) continue;
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
+        PROF_T0(tp);
         const tri m = target_match(P, R, pe, !exact, false, nullptr);
         if (m < 0) return make_err(m);
-        if (!m) continue;
+        if (!m) {
+          PROF_ADD(PH_POL_TARGET, tp);
+          continue;
+        }
         if (P.tflags & TF_HAS_SUBJECTS) {
           const tri h = hierarchical_scope(P, R);
           if (h < 0) return make_err(h);
           psm = h != 0;
         }
+        PROF_ADD(PH_POL_TARGET, tp);
       }
       if (P.map_size == 0 && (P.nflags & NF_EFFECT_TRUTHY)) {
         sf.push(P.effect, P.ec);
@@ -608,14 +658,14 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
-          m = target_match(Q, R, Q.effect, false, false, nullptr);
+          PROF_T0(tr);
+          m = target_match_retry(Q, R, Q.effect, false, nullptr);
           if (m < 0) return make_err(m);
-          if (!m) {
-            m = target_match(Q, R, Q.effect, true, false, nullptr);
-            if (m < 0) return make_err(m);
-          }
+          PROF_ADD(PH_RULE_TARGET, tr);
           if (!m) continue;
+          PROF_T0(th);
           m = hierarchical_scope(Q, R);
+          PROF_ADD(PH_RULE_HR, th);
           if (m < 0) return make_err(m);
         }
         if (m && (Q.nflags & NF_HAS_CONDITION)) {
@@ -625,7 +675,9 @@ ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
           return out;
         }
         if (m && (Q.nflags & NF_HAS_TARGET)) {
+          PROF_T0(ta);
           m = verify_acl(Q, R);
+          PROF_ADD(PH_RULE_ACL, ta);
           if (m < 0) return make_err(m);
         }
         // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
@@ -752,12 +804,8 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
-          m = target_match(Q, R, Q.effect, false, true, &obl);
+          m = target_match_retry(Q, R, Q.effect, true, &obl);
           if (m < 0) return make_err(m);
-          if (!m) {
-            m = target_match(Q, R, Q.effect, true, true, &obl);
-            if (m < 0) return make_err(m);
-          }
         }
         if (m) {
           setbit(rule_base + r);

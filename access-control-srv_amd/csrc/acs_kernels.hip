@@ -118,6 +118,10 @@ __device__ inline uint32_t request_pcol(const ReqHdr& h) {
   return (h.flags & RQ_NO_TARGET) ? PCOL_ALL : (h.flags >> RQ_PCOL_SHIFT);
 }
 
+#if defined(ACS_PHASE_PROF)
+__device__ unsigned long long acs_phase_acc[PH_N];
+#endif
+
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 __global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
@@ -131,14 +135,32 @@ __global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, co
   Decision d{};
   if (in) d = early_decision(h, &done);
   const Filter F = wave_filter(B, in && !done, request_pcol(h), wave_lds_row(B));
+#if defined(ACS_PHASE_PROF)
+  uint64_t prof_lane[PH_N] = {};
+  if (!in) done = true;
+#else
   if (!in) return;
+#endif
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+#if defined(ACS_PHASE_PROF)
+    const ReqLds R(T, B, i, h, col, BLOCK);
+    d = is_allowed_t(R, F);
+    for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
+#else
     d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
+#endif
   }
-  out[i] = d;
+#if defined(ACS_PHASE_PROF)
+  if (in) out[i] = d;
+  for (int k = 0; k < PH_N; ++k) {  // lane-cycles per phase, one atomic per wave
+    uint64_t v = prof_lane[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63u) == 0) atomicAdd(&acs_phase_acc[k], (unsigned long long)v);
+  }
+#endif
 }
 
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane.
@@ -201,6 +223,18 @@ struct acs_tables {
 extern "C" {
 
 const char* acs_last_error(void) { return g_err.c_str(); }
+
+#if defined(ACS_PHASE_PROF)
+// Profiling build only: read and reset the per-phase lane-cycle sums.
+int acs_phase_read(unsigned long long* out, int n) {
+  unsigned long long h[PH_N] = {}, z[PH_N] = {};
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(acs_phase_acc), sizeof h));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_phase_acc), z, sizeof z));
+  for (int k = 0; k < n && k < PH_N; ++k) out[k] = h[k];
+  return PH_N;
+}
+#endif
 
 int acs_device_count(void) {
   int n = 0;
