@@ -153,7 +153,9 @@ __global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, co
     d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
 #endif
   }
-#if defined(ACS_PHASE_PROF)
+#if !defined(ACS_PHASE_PROF)
+  out[i] = d;
+#else
   if (in) out[i] = d;
   for (int k = 0; k < PH_N; ++k) {  // lane-cycles per phase, one atomic per wave
     uint64_t v = prof_lane[k];
