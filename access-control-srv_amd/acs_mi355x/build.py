@@ -58,6 +58,15 @@ def build_prof(force=False):
     return PROF_LIB
 
 
+def build_variant(name, defines, force=False):
+    """Experimental build of the product library with extra -D flags (lib/variants/<name>.so)."""
+    out = os.path.join(PKG, "lib", "variants", name + ".so")
+    src = os.path.join(CSRC, "acs_kernels.hip")
+    if force or _stale(out, [src] + _HEADERS):
+        _hipcc(src, out, tuple("-D" + d for d in defines))
+    return out
+
+
 NAPI_SRC = os.path.join(PKG, "napi", "acs_napi.c")
 NAPI_OUT = os.path.join(PKG, "lib", "acs_mi355x.node")
 NODE_INC = "/usr/include/node"

@@ -184,6 +184,7 @@ struct ReqCtx {
   const uint32_t* ar;
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
+  uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
 #endif
@@ -199,10 +200,30 @@ struct ReqCtx {
     hrkeys = roots + n_roots;
     slotoff = hrkeys + n_hrkeys;
     tse = slotoff + n_slots;
+    const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
+    const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
+    const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
+    s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
+    role0 = h.nroles > 0 ? B.roles[i] : 0u;
+    role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
   }
-  ACS_FN Pair subj(uint32_t j) const { return B.subj[(size_t)j * B.n + i]; }
-  ACS_FN Pair act(uint32_t j) const { return B.act[(size_t)j * B.n + i]; }
-  ACS_FN uint32_t role(uint32_t j) const { return B.roles[(size_t)j * B.n + i]; }
+  // The first subject / action / role attributes live in registers: target matching reads
+  // them for every visited node, and the rows are gathered in sort order (uncoalesced).
+  ACS_FN Pair subj(uint32_t j) const {
+    if (j >= 2) return B.subj[(size_t)j * B.n + i];
+    Pair p;
+    p.id = j == 0 ? s0i : s1i;  // value selects (no address taken: stays in registers)
+    p.value = j == 0 ? s0v : s1v;
+    return p;
+  }
+  ACS_FN Pair act(uint32_t j) const {
+    if (j >= 1) return B.act[(size_t)j * B.n + i];
+    Pair p;
+    p.id = a0i;
+    p.value = a0v;
+    return p;
+  }
+  ACS_FN uint32_t role(uint32_t j) const { return j >= 2 ? B.roles[(size_t)j * B.n + i] : (j == 0 ? role0 : role1); }
   ACS_FN uint8_t rx(uint32_t col, uint32_t row) const { return B.rx[(size_t)col * B.rx_rows + row]; }
   ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
 };

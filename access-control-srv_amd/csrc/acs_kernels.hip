@@ -123,7 +123,10 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
-__global__ __launch_bounds__(BLOCK) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+#ifndef ACS_K1_WAVES_PER_EU
+#define ACS_K1_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;

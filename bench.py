@@ -155,6 +155,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--lib", default=None, help="evaluate with another build of libacs_mi355x (experiments)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,6 +179,8 @@ def main():
     doc = synth.c2_store() if kind == "c2" else synth.c3_store()
     cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
     sb = synth.requests(cs, n, kind, seed=0xACC1000 + 17 * rank)
+    if args.lib:
+        native.load(args.lib)
     tables = native.Tables(compiler.store_blob(cs), local)
     tables.set_sort(not args.no_sort)
     tables.set_timing(True)
