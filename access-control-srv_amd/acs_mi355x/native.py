@@ -26,7 +26,12 @@ class ReqBatchC(C.Structure):
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
            "acs_what_is_allowed", "acs_what_is_allowed_device", "acs_last_kernel_ms", "acs_last_error",
-           "acs_layout_sizes", "acs_device_count", "acs_set_option", "acs_kernel_times"]
+           "acs_layout_sizes", "acs_device_count", "acs_set_option", "acs_kernel_times",
+           "acs_shard_keys_device", "acs_shard_decode_device"]
+
+
+class ShardC(C.Structure):
+    _fields_ = [("set_base", C.c_uint32), ("pol_base", C.c_uint32), ("rule_base", C.c_uint32)]
 
 
 def _declare(lib):
@@ -48,6 +53,8 @@ def _declare(lib):
     lib.acs_layout_sizes.argtypes = [C.POINTER(u32), C.c_int]
     lib.acs_set_option.argtypes = [vp, C.c_int, C.c_int]
     lib.acs_kernel_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    lib.acs_shard_keys_device.argtypes = [vp, vp, C.c_size_t, C.POINTER(ShardC), vp, vp]
+    lib.acs_shard_decode_device.argtypes = [vp, C.c_size_t, vp, vp]
     return lib
 
 

@@ -60,7 +60,20 @@ enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET,
 template <class T, int NW>
 ACS_FN T load_words(const T* p) {
   static_assert(sizeof(T) == 4 * NW, "record must be a whole number of dwords");
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_VECTOR_TABLES)
+  // Every caller passes a wave-uniform record address (table index of the wave-shared
+  // candidate iteration).  Re-assert that on the pointer itself — the compiler's
+  // uniformity analysis loses it across the per-lane early exits of the node loops — and
+  // read through the constant address space (the tables are read-only for the launch):
+  // one s_load_dwordx{2,4,8,16} into SGPRs instead of per-lane vector loads.
+  typedef __attribute__((address_space(4))) const uint32_t const_u32;
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint64_t u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32 |
+                     __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const const_u32* w = (const const_u32*)(uintptr_t)u;
+#else
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+#endif
   uint32_t v[NW];
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];
@@ -580,11 +593,14 @@ ACS_FN tri multiple_entities(const NodeRec& S, const RQ& R) {
 }
 
 // ------------------------------------------------------------------ isAllowed
-ACS_FN Decision make_err(tri e) {
+// at = 1 + index of the policy set whose evaluation threw (0: request level); the
+// rule-sharded reduction orders terminal events by it (shard_key below).
+ACS_FN Decision make_err(tri e, uint32_t at = 0) {
   Decision d{};
   d.decision = DEC_INDETERMINATE;
   d.flags = OF_ERR;
   d.err = (uint8_t)(-e);
+  d.aux = at;
   return d;
 }
 
@@ -613,7 +629,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       PROF_T0(t0);
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
       PROF_ADD(PH_SET_TARGET, t0);
-      if (m < 0) return make_err(m);
+      if (m < 0) return make_err(m, s + 1);
       if (!m) continue;
     }
     // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
@@ -625,10 +641,10 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       uint32_t p;
       while (pols.next(p)) {
         const NodeRec P = load_words(T.pols + p);
-        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
             pe = P.pe_at;
@@ -642,7 +658,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       PROF_T0(tm);
       const tri m = multiple_entities(S, R);
       PROF_ADD(PH_MULTI, tm);
-      if (m < 0) return make_err(m);
+      if (m < 0) return make_err(m, s + 1);
       exact = m != 0;
     }
     Fold sf(S.ca);
@@ -655,14 +671,14 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       if (P.nflags & NF_HAS_TARGET) {
         PROF_T0(tp);
         const tri m = target_match(P, R, pe, !exact, false, nullptr);
-        if (m < 0) return make_err(m);
+        if (m < 0) return make_err(m, s + 1);
         if (!m) {
           PROF_ADD(PH_POL_TARGET, tp);
           continue;
         }
         if (P.tflags & TF_HAS_SUBJECTS) {
           const tri h = hierarchical_scope(P, R);
-          if (h < 0) return make_err(h);
+          if (h < 0) return make_err(h, s + 1);
           psm = h != 0;
         }
         PROF_ADD(PH_POL_TARGET, tp);
@@ -681,13 +697,13 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
         if (Q.nflags & NF_HAS_TARGET) {
           PROF_T0(tr);
           m = target_match_retry(Q, R, Q.effect, false, nullptr);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
           PROF_ADD(PH_RULE_TARGET, tr);
           if (!m) continue;
           PROF_T0(th);
           m = hierarchical_scope(Q, R);
           PROF_ADD(PH_RULE_HR, th);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
         }
         if (m && (Q.nflags & NF_HAS_CONDITION)) {
           out.decision = DEC_INDETERMINATE;
@@ -699,18 +715,18 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
           PROF_T0(ta);
           m = verify_acl(Q, R);
           PROF_ADD(PH_RULE_ACL, ta);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
         }
         // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
         if (m && psm) rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
       }
       if (rf.n) {
-        if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA);
+        if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA, s + 1);
         sf.push(rf.eff, rf.ec);
       }
     }
     if (sf.n) {
-      if (sf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA);
+      if (sf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA, s + 1);
       eff = sf.eff;
       ec = sf.ec;
       last_set = s + 1;
@@ -779,7 +795,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
     const NodeRec S = load_words(T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
-      if (m < 0) return make_err(m);
+      if (m < 0) return make_err(m, s + 1);
       if (!m) continue;
     }
     bool exact = false;
@@ -789,10 +805,10 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       uint32_t p;
       while (pols.next(p)) {
         const NodeRec P = load_words(T.pols + p);
-        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE);
+        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, true, &obl);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
             pe = P.pe_at;
@@ -803,7 +819,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
     }
     if (exact && R.flag(RQ_MULTI_ENT)) {
       const tri m = multiple_entities(S, R);
-      if (m < 0) return make_err(m);
+      if (m < 0) return make_err(m, s + 1);
       exact = m != 0;
     }
     bool any_pol = false;
@@ -814,7 +830,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
         const tri m = target_match(P, R, pe, !exact, true, &obl);
-        if (m < 0) return make_err(m);
+        if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
       }
       bool any_rule = false;
@@ -826,7 +842,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
           m = target_match_retry(Q, R, Q.effect, true, &obl);
-          if (m < 0) return make_err(m);
+          if (m < 0) return make_err(m, s + 1);
         }
         if (m) {
           setbit(rule_base + r);
@@ -855,6 +871,78 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
     d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h), bits, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
+  return d;
+}
+
+// ------------------------------------------------------------------ rule-sharded isAllowed (C1)
+// whole policy sets are partitioned over ranks and every rank evaluates every
+// request against its own sets.  Sets are independent except for two cross-set rules of
+// isAllowed (accessController.ts:125-295): the LAST set with a policy effect decides
+// (`effect` is overwritten per set, :293-295), and the FIRST set whose evaluation throws or
+// reaches a rule condition ends the request.  One 64-bit key per request and rank turns
+// both into a plain integer MAX across ranks:
+//   bit 62       terminal event (error, rule condition, request-level host / no target)
+//   bits 61..33  terminal: SHARD_ORDER_MAX - at (at = 1 + global set index; 0: request level)
+//                else    : 1 + global index of the last applicable set (0: none)
+//   bit 32       payload is a global rule index (a rule condition was reached)
+//   bits 31..0   payload: decision | ec << 8 | flags << 16 | err << 24, or that rule index
+// Keys stay below 2^63, so a signed int64 all-reduce MAX (RCCL, gloo) orders them as well.
+struct ShardBase {
+  uint32_t set_base, pol_base, rule_base;  // global index of the rank's first set / policy / rule
+};
+constexpr uint32_t SHARD_ORDER_MAX = (1u << 29) - 1;
+
+// Policy set that holds (local) rule r: child ranges are contiguous and ascending.
+ACS_FN uint32_t set_of_rule(const Tables& T, uint32_t r) {
+  uint32_t lo = 0, hi = T.n_pols;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (T.pols[mid].child_begin <= r) lo = mid; else hi = mid;
+  }
+  uint32_t a = 0, b = T.n_sets;
+  while (b - a > 1) {
+    const uint32_t mid = (a + b) / 2;
+    if (T.sets[mid].child_begin <= lo) a = mid; else b = mid;
+  }
+  return a;
+}
+
+ACS_FN uint64_t shard_key(const Tables& T, const Decision& d, const ShardBase& b) {
+  const uint64_t term = 1ull << 62;
+  const uint64_t payload = (uint64_t)d.decision | (uint64_t)d.ec << 8 | (uint64_t)d.flags << 16 |
+                           (uint64_t)d.err << 24;
+  if (d.flags & OF_HOST_COND) {
+    const uint32_t at = set_of_rule(T, d.aux) + b.set_base + 1;
+    return term | (uint64_t)(SHARD_ORDER_MAX - at) << 33 | (1ull << 32) | (uint64_t)(d.aux + b.rule_base);
+  }
+  if (d.flags & OF_ERR) {
+    const uint32_t at = d.aux ? d.aux + b.set_base : 0u;
+    return term | (uint64_t)(SHARD_ORDER_MAX - at) << 33 | payload;
+  }
+  if (d.flags & (OF_HOST_REQ | OF_NO_TARGET)) return term | (uint64_t)SHARD_ORDER_MAX << 33 | payload;
+  const uint32_t last = d.aux ? d.aux + b.set_base : 0u;
+  return (uint64_t)last << 33 | payload;
+}
+
+// Reduced key -> the decision record an unsharded evaluation writes (global indices).
+ACS_FN Decision shard_decode(uint64_t key) {
+  Decision d{};
+  if (key & (1ull << 32)) {
+    d.decision = DEC_INDETERMINATE;
+    d.flags = OF_HOST_COND;
+    d.aux = (uint32_t)key;
+    return d;
+  }
+  const uint32_t order = (uint32_t)(key >> 33) & SHARD_ORDER_MAX;
+  d.decision = (uint8_t)key;
+  d.ec = (uint8_t)(key >> 8);
+  d.flags = (uint8_t)(key >> 16);
+  d.err = (uint8_t)(key >> 24);
+  if (key & (1ull << 62)) {
+    d.aux = (d.flags & OF_ERR) ? SHARD_ORDER_MAX - order : 0u;
+  } else {
+    d.aux = order;
+  }
   return d;
 }
 

@@ -199,6 +199,19 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   out[i] = d;
 }
 
+// Rule-sharded isAllowed (C1): local decisions -> 64-bit MAX-reducible keys, and back.
+__global__ __launch_bounds__(BLOCK) void shard_key_kernel(Tables T, const Decision* __restrict__ d, uint32_t n,
+                                                          ShardBase b, uint64_t* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n) keys[i] = shard_key(T, d[i], b);
+}
+
+__global__ __launch_bounds__(BLOCK) void shard_decode_kernel(const uint64_t* __restrict__ keys, uint32_t n,
+                                                             Decision* __restrict__ out) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n) out[i] = shard_decode(keys[i]);
+}
+
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 size_t filter_lds_bytes(const Batch& B) {
@@ -428,6 +441,28 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, acs_wia_words_per_request(t),
                      bits, obl, obl_n, (Decision*)out);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+int acs_shard_keys_device(acs_tables* t, const acs_decision* dec, size_t n, const acs_shard* shard, uint64_t* keys,
+                          void* stream) {
+  if (!t || !shard || (n && (!dec || !keys))) return fail("acs_shard_keys_device: null argument");
+  if (n > 0xFFFFFFFFull) return fail("acs_shard_keys_device: batch too large");
+  if (n == 0) return 0;
+  const ShardBase b{shard->set_base, shard->pol_base, shard->rule_base};
+  hipLaunchKernelGGL(shard_key_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                     (hipStream_t)stream, t->view, (const Decision*)dec, (uint32_t)n, b, keys);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+int acs_shard_decode_device(const uint64_t* keys, size_t n, acs_decision* out, void* stream) {
+  if (n && (!keys || !out)) return fail("acs_shard_decode_device: null argument");
+  if (n > 0xFFFFFFFFull) return fail("acs_shard_decode_device: batch too large");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(shard_decode_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                     (hipStream_t)stream, keys, (uint32_t)n, (Decision*)out);
   HIP_OK(hipGetLastError());
   return 0;
 }

@@ -156,6 +156,9 @@ def main():
     ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--lib", default=None, help="evaluate with another build of libacs_mi355x (experiments)")
+    ap.add_argument("--rule-shard", action="store_true",
+                    help="configs[4] variant ii: whole policy sets sharded over ranks, every rank evaluates the "
+                         "same requests, one all-reduce MAX of 64-bit decision keys (RCCL) combines them")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +172,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from acs_mi355x import compiler, native, store, synth, layout as L
+    from acs_mi355x import compiler, native, shard, store, synth, layout as L
     from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor
     from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
 
@@ -177,8 +180,16 @@ def main():
     desc, n_default = WORKLOADS[kind]
     n = args.requests or n_default
     doc = synth.c2_store() if kind == "c2" else synth.c3_store()
-    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
-    sb = synth.requests(cs, n, kind, seed=0xACC1000 + 17 * rank)
+    full_map = store.populate(doc)
+    if args.rule_shard:
+        # variant ii: this rank's run of whole policy sets; the same requests on every rank
+        set_lo, set_hi = shard.partition(full_map, world)[rank]
+        sbase = shard.base(full_map, set_lo)
+        cs = compiler.compile_store(shard.slice_store(full_map, set_lo, set_hi), FULL_URNS, DEFAULT_CAS)
+        sb = synth.requests(cs, n, kind, seed=0xACC1000)
+    else:
+        cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
+        sb = synth.requests(cs, n, kind, seed=0xACC1000 + 17 * rank)
     if args.lib:
         native.load(args.lib)
     tables = native.Tables(compiler.store_blob(cs), local)
@@ -187,9 +198,22 @@ def main():
     db = DeviceBatch(sb.batch, local)
     out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    if args.rule_shard:
+        local_out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+        keys = torch.empty((n,), dtype=torch.int64, device=dev)
+
+    def step():
+        if not args.rule_shard:
+            is_allowed_device(tables, db, out, stream)
+            return
+        is_allowed_device(tables, db, local_out, stream)
+        shard.keys_device(tables, local_out, sbase, keys, stream)
+        if dist:
+            tdist.all_reduce(keys, op=tdist.ReduceOp.MAX)  # C1: RCCL over xGMI, 8 B per request
+        shard.decode_device(tables.lib, keys, out, stream)
 
     for _ in range(args.warmup):
-        is_allowed_device(tables, db, out, stream)
+        step()
     torch.cuda.synchronize(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -198,7 +222,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        is_allowed_device(tables, db, out, stream)
+        step()
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     if dist:
@@ -212,8 +236,19 @@ def main():
         elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
     dec = decisions_from_tensor(out)
+    shard_check = None
+    if args.rule_shard and rank == 0:
+        # size-independent property: the set-sharded + all-reduced records equal an
+        # unsharded evaluation of the whole store on the same requests, bit for bit
+        cs_full = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
+        sb_full = synth.requests(cs_full, n, kind, seed=0xACC1000)
+        t_full = native.Tables(compiler.store_blob(cs_full), local)
+        want = decisions_from_tensor(is_allowed_device(t_full, DeviceBatch(sb_full.batch, local)))
+        t_full.close()
+        shard_check = {"ranks": world, "sets": [set_lo, set_hi], "requests": n,
+                       "identical_to_unsharded": bool(np.array_equal(want.view(np.uint64), dec.view(np.uint64)))}
     pcie = None
-    if rank == 0 and not args.no_pcie:
+    if rank == 0 and not args.no_pcie and not args.rule_shard:
         # host buffers through acs_is_allowed: H2D + sort + K1 + D2H (reported beside, never `value`)
         tables.is_allowed(sb.batch)
         t1 = time.perf_counter()
@@ -225,16 +260,22 @@ def main():
         per_dec, parts = algorithmic_bytes(cs, sb.batch)
         achieved = per_dec * n / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = measured_traffic(kind)
-        value = world * n * args.steps / elapsed
+        # request sharding: every rank decides its own n requests; rule sharding: the ranks
+        # decide the same n requests together
+        value = (1 if args.rule_shard else world) * n * args.steps / elapsed
         mix = np.bincount(dec["decision"], minlength=7)
         host = int(((dec["flags"] & (L.OF_HOST_REQ | L.OF_HOST_COND)) != 0).sum())
         line = {
             "metric": "authorization decisions/sec (isAllowed)", "value": value, "unit": "decisions/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong" if args.rule_shard else "weak",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": desc, "requests_per_gpu": n, "policy_sets": cs.n_sets, "policies": cs.n_pols,
-                       "rules": cs.n_rules, "table_bytes": cs.table_bytes(), "parallelism": f"requests dp{world}",
+            "config": {"workload": desc + (" [policy sets sharded over ranks + all-reduce MAX]" if args.rule_shard
+                                           else ""),
+                       "requests_per_gpu": n, "policy_sets": cs.n_sets, "policies": cs.n_pols,
+                       "rules": cs.n_rules, "table_bytes": cs.table_bytes(),
+                       "parallelism": f"policy-set shards x{world}" if args.rule_shard else f"requests dp{world}",
                        "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])},
                        "host_fallback_fraction": host / n, "request_classes": int(sb.batch.cand.shape[0])},
             "coherence_sort": not args.no_sort,
@@ -247,6 +288,8 @@ def main():
         }
         if pcie:
             line["pcie_inclusive"] = pcie
+        if shard_check:
+            line["rule_shard"] = shard_check
         if world == 1 and not args.no_cpu_baseline:
             cb, par = cpu_baseline(kind, doc, sb, dec, cs, args.cpu_seconds)
             line["cpu_baseline"] = cb

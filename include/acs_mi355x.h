@@ -100,6 +100,22 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t
 int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, uint32_t* dev_bits,
                                uint32_t* dev_obl, uint32_t* dev_obl_n, acs_decision* dev_out, void* stream);
 
+/* Rule-sharded isAllowed (configs[4] variant ii).  A rank compiles only the
+ * policy sets [set_base, set_base + n_sets) of the store (whole sets, Map order) and
+ * evaluates every request against them with acs_is_allowed_device.  acs_shard_keys_device
+ * turns its decision records into 64-bit keys whose integer MAX over ranks (an RCCL
+ * all-reduce, ncclMax on int64) reproduces the reference's two cross-set rules: the last
+ * set with a policy effect decides (accessController.ts:293-295) and the first set whose
+ * evaluation throws or reaches a rule condition ends the request (:125-295).
+ * acs_shard_decode_device turns the reduced keys back into the records an unsharded
+ * evaluation writes (aux = global set / rule index).  csrc/acs_eval.h: shard_key. */
+typedef struct {
+  uint32_t set_base, pol_base, rule_base; /* global index of the rank's first set / policy / rule */
+} acs_shard;
+int acs_shard_keys_device(acs_tables* t, const acs_decision* dev_dec, size_t n, const acs_shard* shard,
+                          uint64_t* dev_keys, void* stream);
+int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* dev_out, void* stream);
+
 /* Options.  ACS_OPT_SORT (default 1): before evaluating, the device entry points
  * order the batch by (entity, role, action) with a radix sort so that every
  * wave shares its table-driven branches; results are written in input order. */

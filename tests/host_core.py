@@ -8,7 +8,7 @@ import numpy as np
 from acs_mi355x import layout as L
 from acs_mi355x.build import build_host_core
 from acs_mi355x.compiler import store_blob
-from acs_mi355x.native import ReqBatchC, batch_struct
+from acs_mi355x.native import ReqBatchC, ShardC, batch_struct
 
 _LIB = None
 
@@ -20,7 +20,27 @@ def lib():
         vp = C.c_void_p
         _LIB.acs_host_is_allowed.argtypes = [vp, C.c_size_t, C.POINTER(ReqBatchC), vp]
         _LIB.acs_host_what_is_allowed.argtypes = [vp, C.c_size_t, C.POINTER(ReqBatchC), vp, vp, vp, vp]
+        _LIB.acs_host_shard_keys.argtypes = [vp, C.c_size_t, vp, C.c_size_t, C.POINTER(ShardC), vp]
+        _LIB.acs_host_shard_decode.argtypes = [vp, C.c_size_t, vp]
+        _LIB.acs_host_shard_decode.restype = None
     return _LIB
+
+
+def shard_keys(cs, dec, base):
+    """Local decision records -> rule-sharded reduction keys (int64 view of the u64 keys)."""
+    blob = store_blob(cs)
+    dec = np.ascontiguousarray(dec)
+    keys = np.zeros(len(dec), np.int64)
+    s = ShardC(*base)
+    assert lib().acs_host_shard_keys(blob, len(blob), dec.ctypes.data, len(dec), C.byref(s), keys.ctypes.data) == 0
+    return keys
+
+
+def shard_decode(keys):
+    keys = np.ascontiguousarray(keys, np.int64)
+    out = np.zeros(len(keys), L.DECISION_DT)
+    lib().acs_host_shard_decode(keys.ctypes.data, len(keys), out.ctypes.data)
+    return out
 
 
 def is_allowed(cs, batch):

@@ -68,6 +68,28 @@ extern "C" int acs_host_is_allowed(const void* blob, size_t n, const acs_req_bat
   return 0;
 }
 
+// Rule-sharded reduction keys / decode (csrc/acs_eval.h shard_key) on the host, for the
+// world-size-2 gloo tests of the sharded path.
+extern "C" int acs_host_shard_keys(const void* blob, size_t n, const acs_decision* dec, size_t m,
+                                   const acs_shard* s, uint64_t* keys) {
+  Tables T;
+  if (!host_tables(blob, n, &T)) return -1;
+  const ShardBase b{s->set_base, s->pol_base, s->rule_base};
+  for (size_t i = 0; i < m; ++i) {
+    Decision d;
+    std::memcpy(&d, &dec[i], sizeof d);
+    keys[i] = shard_key(T, d, b);
+  }
+  return 0;
+}
+
+extern "C" void acs_host_shard_decode(const uint64_t* keys, size_t m, acs_decision* out) {
+  for (size_t i = 0; i < m; ++i) {
+    const Decision d = shard_decode(keys[i]);
+    std::memcpy(&out[i], &d, sizeof d);
+  }
+}
+
 extern "C" int acs_host_what_is_allowed(const void* blob, size_t n, const acs_req_batch* b, uint32_t* bits,
                                         uint32_t* obl, uint32_t* obl_n, acs_decision* out) {
   Tables T;

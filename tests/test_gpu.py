@@ -18,7 +18,7 @@ import host_core  # noqa: E402
 from diff_utils import oracle_outcome, gpu_outcome, build, norm_rq  # noqa: E402
 from oracle.acs_oracle import Oracle, FULL_URNS, DEFAULT_CAS  # noqa: E402
 from oracle.jsval import OracleUnsupported, JSError  # noqa: E402
-from acs_mi355x import store, compiler, encoder, results, native, synth, layout as L  # noqa: E402
+from acs_mi355x import store, compiler, encoder, results, native, shard, synth, layout as L  # noqa: E402
 from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor  # noqa: E402
 
 KATS = load_kats()
@@ -137,6 +137,45 @@ def test_what_is_allowed_c4_gpu():
         got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], obl[i][:obl_n[i]], out[i]))
         assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
     t.close()
+
+
+def _shard_reduce_gpu(urns, full_map, world, make_batch):
+    """Evaluate `world` policy-set shards one after another on this GPU and reduce their
+    keys with MAX, as the RCCL all-reduce of the rule-sharded bench does across GPUs."""
+    keys = []
+    for r in range(world):
+        a, b = shard.partition(full_map, world)[r]
+        cs = compiler.compile_store(shard.slice_store(full_map, a, b), urns, DEFAULT_CAS)
+        t = gpu_tables(cs)
+        dec = is_allowed_device(t, DeviceBatch(make_batch(cs), 0))
+        keys.append(shard.keys_device(t, dec, shard.base(full_map, a)))
+        torch.cuda.synchronize()
+        t.close()
+    red = torch.stack(keys).max(dim=0).values
+    return decisions_from_tensor(shard.decode_device(native.load(), red))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_rule_shard_c3_gpu(world):
+    doc, cs, sb = _synth("c3", 60_000)
+    full = store.populate(doc)
+    t = gpu_tables(cs)
+    want = decisions_from_tensor(is_allowed_device(t, DeviceBatch(sb.batch, 0)))
+    t.close()
+    got = _shard_reduce_gpu(FULL_URNS, full, world, lambda c: synth.requests(c, 60_000, "c3").batch)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+def test_rule_shard_random_gpu():
+    terminal = 0
+    for seed in range(60):
+        urns, doc, reqs = randgen.rand_case(seed)
+        o, cs = build(urns, doc)
+        want = gpu_tables(cs).is_allowed(encoder.Encoder(cs).encode(reqs))
+        got = _shard_reduce_gpu(urns, store.populate(doc), 2, lambda c: encoder.Encoder(c).encode(reqs))
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64)), seed
+        terminal += int(((want["flags"] & (L.OF_ERR | L.OF_HOST_COND)) != 0).sum())
+    assert terminal > 0
 
 
 def test_device_api_and_ragged_sizes():

@@ -26,6 +26,16 @@ for s in $STEPS; do
     quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
+    ab) for v in ${VARIANTS:-vector_tables}; do
+          step "bench_$v" 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie \
+            --lib access-control-srv_amd/lib/variants/$v.so
+        done ;;
+    ab3) for v in ${VARIANTS:-vector_tables}; do
+          step "bench_c3_$v" 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie \
+            --lib access-control-srv_amd/lib/variants/$v.so
+        done ;;
+    shard) step bench_rule_shard 600 python bench.py --rule-shard --steps 20 --warmup 3 --no-cpu-baseline ;;
+    shard3) step bench_c3_rule_shard 900 python bench.py --config c3 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
   esac
 done
