@@ -36,6 +36,8 @@ from .jsops import MISSING
 _HIT_LIKE = L.RX_HIT | L.RX_THROW_TYPE | L.RX_THROW_SYNTAX | L.RX_HOST
 MAX_CLASSES = L.PCOL_ALL  # ids 0 .. 0xFFFE
 _CHUNK = 2048
+_MAX_ACTION_KEYS = 62
+_KEY_ROW_BYTES = 512 << 20  # candidate rows computed per batch before dedupe
 
 
 def words(n):
@@ -149,77 +151,163 @@ def _role_sets(hdr, roles, role_ids):
     return rows
 
 
-def classes(cs, hdr, roles, pcol, ent):
-    """Class id per request (u32, PCOL_ALL = unfiltered) and the class rows [C, W] u32."""
+def action_keys(hdr, act):
+    """Per request: index of its action key — 0: no action attribute, 1: several (unfiltered),
+    2 + k: the k-th distinct single (id, value) pair of the batch — and the pairs [K, 2]."""
+    nact = hdr["nact"].astype(np.int64)
+    ak = np.where(nact == 0, 0, 1).astype(np.int64)
+    one = nact == 1
+    packed = (act["id"][0].astype(np.uint64) << np.uint64(32)) | act["value"][0].astype(np.uint64)
+    uk, inv = np.unique(packed[one], return_inverse=True)
+    if len(uk) > _MAX_ACTION_KEYS:  # a batch of exotic actions: keep the most frequent ones
+        cnt = np.bincount(inv, minlength=len(uk))
+        keep = np.argsort(-cnt, kind="stable")[:_MAX_ACTION_KEYS]
+        remap = np.full(len(uk), -1, np.int64)
+        remap[keep] = np.arange(len(keep))
+        uk = uk[keep]
+        inv = remap[inv]
+        ak[np.flatnonzero(one)] = np.where(inv >= 0, inv + 2, 1)
+    else:
+        ak[np.flatnonzero(one)] = inv + 2
+    pairs = np.stack([(uk >> np.uint64(32)).astype(np.int64), (uk & np.uint64(0xFFFFFFFF)).astype(np.int64)],
+                     axis=1) if len(uk) else np.zeros((0, 2), np.int64)
+    return ak, pairs
+
+
+def _loose(a, b):
+    return (a == b) | ((a <= L.ID_NULL) & (b <= L.ID_NULL))
+
+
+def action_candidates(cs, pairs):
+    """bool [2 + K, n] per section: nodes whose target can pass ``attributesMatch(rule.actions,
+    request.actions)`` (accessController.ts:681-699: every target action attribute loosely equal
+    to some request action attribute) for a request with no action (row 0), several actions
+    (row 1: unfiltered) or the single action pair k (row 2 + k).  Nodes without a target or
+    without action attributes are candidates in every row."""
+    out = []
+    pool = cs.pairs
+    for nodes in (cs.sets, cs.pols, cs.rules):
+        n = len(nodes)
+        need = ((nodes["nflags"] & L.NF_HAS_TARGET) != 0) & (nodes["act_n"] > 0)
+        rows = np.ones((2 + len(pairs), n), bool)
+        rows[0] = ~need
+        idx = np.flatnonzero(need)
+        if len(idx) and len(pairs):
+            cnt = nodes["act_n"][idx].astype(np.int64)
+            owner = np.repeat(idx, cnt)
+            start = np.repeat(nodes["act_off"][idx].astype(np.int64) - np.cumsum(cnt) + cnt, cnt)
+            pidx = start + np.arange(cnt.sum())
+            pid = pool["id"][pidx].astype(np.int64)
+            pval = pool["value"][pidx].astype(np.int64)
+            for k, (qi, qv) in enumerate(pairs):
+                bad = ~(_loose(pid, qi) & _loose(pval, qv))
+                fails = np.bincount(owner[bad], minlength=n)
+                rows[2 + k] = (~need) | (fails == 0)
+        out.append(rows)
+    return tuple(out)
+
+
+def classes(cs, hdr, roles, pcol, ent, act=None):
+    """Class id per request (u32, PCOL_ALL = unfiltered) and the class rows [C, W] u32.
+
+    A class row is the AND of three node filters — entity column, role associations,
+    action — and requests whose rows come out identical share a class (so the coherence
+    sort groups them).  When the keys would need too much memory (large stores) the key is
+    coarsened: (entity, action), then entity alone."""
     role_ids, req_rows = role_requirements(cs)
     nrr = len(role_ids)
     n = len(hdr)
     active = (pcol != L.PCOL_ALL) & ((hdr["flags"] & (L.RQ_HOST | L.RQ_NO_TARGET)) == 0)
+    cls = np.full(n, L.PCOL_ALL, np.uint32)
+    ws, wp, wr = section_words(cs)
+    W = ws + wp + wr
+    if not active.any():
+        return cls, np.zeros((1, W), np.uint32)
+    if act is not None:
+        ak, apairs = action_keys(hdr, act)
+    else:
+        ak, apairs = np.ones(n, np.int64), np.zeros((0, 2), np.int64)
+    A = action_candidates(cs, apairs)
     rs = _role_sets(hdr, roles, role_ids)
     used = rs[:, ::-1]  # largest rows first; -1 padding last
-    width = int((used >= 0).sum(axis=1).max()) if n else 0
-    key = np.concatenate([pcol.astype(np.int64)[:, None], used[:, :max(width, 1)]], axis=1)
-    cls = np.full(n, L.PCOL_ALL, np.uint32)
-    if not active.any():
-        return cls, np.zeros((1, sum(section_words(cs))), np.uint32)
-    if key.shape[1] <= 4 and nrr < (1 << 15):
-        # pack into one int64 for a fast unique: pcol:16 | up to 3 rows of 15 bits (+1 offset)
-        packed = key[:, 0].copy()
-        for j in range(1, key.shape[1]):
-            packed = (packed << 15) | (key[:, j] + 1)
-        uk, inv = np.unique(packed[active], return_inverse=True)
-        first = np.zeros(len(uk), np.int64)
-        first[inv[::-1]] = np.flatnonzero(active)[::-1]
-        ckey = key[first]
-    else:
-        ckey, inv = np.unique(key[active], axis=0, return_inverse=True)
-        inv = inv.reshape(-1)
-    if len(ckey) > MAX_CLASSES:  # too many classes: entity-only filtering
-        ckey, inv = np.unique(key[active, :1], axis=0, return_inverse=True)
-        ckey = np.concatenate([ckey, np.full((len(ckey), 1), -1, np.int64)], axis=1)
-        inv = inv.reshape(-1)
-        role_filter = False
-    else:
-        role_filter = True
-    cls[active] = inv.astype(np.uint32)
-
+    width = max(int((used >= 0).sum(axis=1).max()) if n else 0, 1)
     E_s, E_p, E_r = ent
-    ws, wp, wr = section_words(cs)
+    A_s, A_p, A_r = A
     b_s = cs.sets["child_begin"].astype(np.int64)
     e_s = cs.sets["child_end"].astype(np.int64)
     nonempty = e_s > b_s
-    out = np.zeros((len(ckey), ws + wp + wr), np.uint32)
-    for c0 in range(0, len(ckey), _CHUNK):
-        ck = ckey[c0:c0 + _CHUNK]
-        pc = ck[:, 0]
-        M = np.zeros((len(ck), nrr + 1), bool)
-        M[:, nrr] = True  # "no role requirement" column
-        if role_filter:
-            for j in range(1, ck.shape[1]):
-                v = ck[:, j]
-                ok = v >= 0
-                M[np.flatnonzero(ok), v[ok]] = True
-        else:
-            M[:, :] = True
+    for level in ("entity+roles+action", "entity+action", "entity"):
+        cols = [pcol.astype(np.int64)[:, None]]
+        if level != "entity":
+            cols.append(ak[:, None])
+        if level == "entity+roles+action":
+            cols.append(used[:, :width])
+        key = np.concatenate(cols, axis=1)
+        ckey, inv = _unique_rows(key[active])
+        if len(ckey) * W * 4 > _KEY_ROW_BYTES and level != "entity":
+            continue
+        role_filter = level == "entity+roles+action"
+        action_filter = level != "entity"
+        out = np.zeros((len(ckey), W), np.uint32)
+        for c0 in range(0, len(ckey), _CHUNK):
+            ck = ckey[c0:c0 + _CHUNK]
+            pc = ck[:, 0]
+            a = ck[:, 1] if action_filter else np.ones(len(ck), np.int64)
+            M = np.zeros((len(ck), nrr + 1), bool)
+            M[:, nrr] = True  # "no role requirement" column
+            if role_filter:
+                for j in range(2, ck.shape[1]):
+                    v = ck[:, j]
+                    ok = v >= 0
+                    M[np.flatnonzero(ok), v[ok]] = True
+            else:
+                M[:, :] = True
 
-        def role_ok(rr):
-            return M[:, np.where(rr >= 0, rr, nrr)]
+            def role_ok(rr):
+                return M[:, np.where(rr >= 0, rr, nrr)]
 
-        p = E_p[pc] & role_ok(req_rows[1])
-        r = E_r[pc] & role_ok(req_rows[2])
-        s = E_s[pc] & role_ok(req_rows[0])
-        if cs.n_pols:
-            cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
-            pol_any = (cum[:, e_s] - cum[:, b_s]) > 0
-        else:
-            pol_any = np.zeros((len(ck), cs.n_sets), bool)
-        s &= pol_any & nonempty[None, :]
-        out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+            p = E_p[pc] & role_ok(req_rows[1]) & A_p[a]
+            r = E_r[pc] & role_ok(req_rows[2]) & A_r[a]
+            s = E_s[pc] & role_ok(req_rows[0]) & A_s[a]
+            if cs.n_pols:
+                cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
+                pol_any = (cum[:, e_s] - cum[:, b_s]) > 0
+            else:
+                pol_any = np.zeros((len(ck), cs.n_sets), bool)
+            s &= pol_any & nonempty[None, :]
+            out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+        # requests whose rows are identical share one class
+        urows, rinv = _unique_rows(out)
+        if len(urows) <= MAX_CLASSES or level == "entity":
+            break
+    if len(urows) > MAX_CLASSES:  # entity level: at most one class per entity column (< 0xFFFE)
+        raise ValueError("too many request classes")
     # heaviest classes first: the kernel's sort key orders waves by class id, so the longest
     # waves are dispatched first (longest-processing-time-first; no tail of heavy waves)
-    cost = np.unpackbits(out.view(np.uint8), axis=1).sum(axis=1)
+    cost = np.unpackbits(urows.view(np.uint8), axis=1).sum(axis=1)
     rank = np.empty(len(cost), np.int64)
     rank[np.argsort(-cost, kind="stable")] = np.arange(len(cost))
-    out = np.ascontiguousarray(out[np.argsort(rank)])
-    cls[active] = rank[inv].astype(np.uint32)
-    return cls, out
+    urows = np.ascontiguousarray(urows[np.argsort(rank)])
+    cls[active] = rank[rinv[inv]].astype(np.uint32)
+    return cls, urows
+
+
+def _unique_rows(a):
+    """(unique rows, inverse) of a 2-D integer array; narrow keys are packed into one int64."""
+    if a.shape[0] == 0:
+        return a[:0], np.zeros(0, np.int64)
+    if a.shape[1] == 0:
+        return a[:1], np.zeros(a.shape[0], np.int64)
+    if a.dtype.kind == "i":
+        lo = a.min(axis=0)
+        span = a.max(axis=0) - lo + 1
+        bits = [int(x).bit_length() for x in span]
+        if sum(bits) <= 63:
+            packed = np.zeros(a.shape[0], np.int64)
+            for j, b in enumerate(bits):
+                packed = (packed << b) | (a[:, j] - lo[j])
+            _, first, inv = np.unique(packed, return_index=True, return_inverse=True)
+            return a[first], inv.reshape(-1)
+    v = np.ascontiguousarray(a).view(np.dtype((np.void, a.dtype.itemsize * a.shape[1]))).reshape(-1)
+    _, first, inv = np.unique(v, return_index=True, return_inverse=True)
+    return a[first], inv.reshape(-1)

@@ -444,5 +444,5 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     b.cand_wp, b.cand_wr = ws, ws + wp
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
     roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
-    cls, b.cand = candidates.classes(cs, b.hdr, roles, pcol, ent)
+    cls, b.cand = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

@@ -102,7 +102,14 @@ class OrgTree:
         return f"org{k}"
 
     def subtree_json(self, k, role=None):
-        """hierarchical_scopes entry for the subtree rooted at k (role on the root only)."""
+        """hierarchical_scopes entry for the subtree rooted at k (role on the root only).
+        Memoised: requests scoped at the same org share one (read-only) JSON tree."""
+        memo = self.__dict__.setdefault("_json_memo", {})
+        if (k, role) not in memo:
+            memo[(k, role)] = self._subtree_json(k, role)
+        return memo[(k, role)]
+
+    def _subtree_json(self, k, role=None):
         def node(x):
             d = int(self.level[x])
             out = {"id": self.name(x)}

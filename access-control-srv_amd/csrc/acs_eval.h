@@ -29,9 +29,6 @@ namespace acs {
 
 #define ACS_FN __host__ __device__ inline
 
-template <class T, int NW = sizeof(T) / 4>
-ACS_FN T load_words(const T* p);
-
 // Value every active lane of the wave holds identically (a table index or bitset word of
 // the wave-shared candidate iteration): move it to an SGPR so the node records behind it
 // are fetched with scalar loads.  Identity in the host build of the core.
@@ -55,33 +52,6 @@ enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET,
 #define PROF_ADD(k, v)
 #endif
 
-// Table records are read as whole dwords and unpacked in registers: with a wave-uniform
-// address this is one s_load_dwordx{4,16} (scalar loads have no byte / short forms).
-template <class T, int NW>
-ACS_FN T load_words(const T* p) {
-  static_assert(sizeof(T) == 4 * NW, "record must be a whole number of dwords");
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_VECTOR_TABLES)
-  // Every caller passes a wave-uniform record address (table index of the wave-shared
-  // candidate iteration).  Re-assert that on the pointer itself — the compiler's
-  // uniformity analysis loses it across the per-lane early exits of the node loops — and
-  // read through the constant address space (the tables are read-only for the launch):
-  // one s_load_dwordx{2,4,8,16} into SGPRs instead of per-lane vector loads.
-  typedef __attribute__((address_space(4))) const uint32_t const_u32;
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  const uint64_t u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32 |
-                     __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const const_u32* w = (const const_u32*)(uintptr_t)u;
-#else
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
-#endif
-  uint32_t v[NW];
-#pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = w[k];
-  T out;
-  __builtin_memcpy(&out, v, sizeof(T));
-  return out;
-}
-
 struct Pair {
   uint32_t id, value;
 };
@@ -98,7 +68,57 @@ struct Tables {
   const uint32_t* u32pool;
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
+  uint64_t lo, hi;   // device: lowest / highest record address inside the table allocation
 };
+
+#if defined(ACS_CHECK_UNIFORM)
+__device__ unsigned long long acs_nonuniform[4];  // debug build only
+#endif
+
+// Table records are read as whole dwords and unpacked in registers: with a wave-uniform
+// address this is one s_load_dwordx{2,4,8,16} (scalar loads have no byte / short forms).
+template <class X, int NW = sizeof(X) / 4>
+ACS_FN X load_words(const Tables& T, const X* p) {
+  static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ACS_SCALAR_TABLES)
+  // EXPERIMENTAL, off by default: every caller passes a wave-uniform record
+  // address, so re-asserting it with readfirstlane and reading through the constant
+  // address space gives one scalar load per record instead of per-lane vector loads
+  // (c2 K1 1.87 -> 1.54 ms).  But scalar instructions run whatever the exec mask, and in
+  // blocks the compiler enters with no active lane readfirstlane returns a stale lane-0
+  // value; measured on MI355X, such stale scalar loads leak into live lanes' results
+  // (wrong decisions on the golden vectors, or illegal addresses without the clamp
+  // below), and the exec guard only hides it for some code layouts.  The product keeps
+  // vector loads until the node loops are restructured so that no table load sits in a
+  // divergent region.
+  if (__builtin_amdgcn_read_exec() == 0) return X{};
+  typedef __attribute__((address_space(4))) const uint32_t const_u32;
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  uint64_t u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32 |
+               __builtin_amdgcn_readfirstlane((uint32_t)a);
+#if defined(ACS_CHECK_UNIFORM)  // debug build: count loads whose address differs across active lanes
+  {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    const uint64_t diff = __ballot(a != u);
+    if (diff != 0 && (uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(ex)) {
+      atomicAdd(&acs_nonuniform[0], 1ull);
+      atomicAdd(&acs_nonuniform[sizeof(X) == 64 ? 1 : sizeof(X) == 16 ? 2 : 3], 1ull);
+    }
+  }
+#endif
+  u = u < T.lo ? T.lo : (u > T.hi ? T.hi : u);
+  const const_u32* w = (const const_u32*)(uintptr_t)u;
+#else
+  (void)T;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+#endif
+  uint32_t v[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = w[k];
+  X out;
+  __builtin_memcpy(&out, v, sizeof(X));
+  return out;
+}
 
 struct Batch {
   uint32_t n;
@@ -271,7 +291,7 @@ struct ReqMem : ReqCtx {
 ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const ReqCtx& R, bool subjects) {
   const uint32_t qn = subjects ? R.h.nsubj : R.h.nact;
   for (uint32_t k = 0; k < rn; ++k) {
-    const Pair a = load_words(rule + wave_uniform(k));
+    const Pair a = load_words(R.T, rule + wave_uniform(k));
     bool found = false;
     for (uint32_t j = 0; j < qn && !found; ++j) {
       const Pair q = subjects ? R.subj(j) : R.act(j);
@@ -308,7 +328,7 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
     const ReqRes q = R.res(j);
     pm = false;
     for (uint32_t k = 0; k < t.res_n; ++k) {
-      const RuleResAttr r = load_words(ra + wave_uniform(k));
+      const RuleResAttr r = load_words(R.T, ra + wave_uniform(k));
       if (r.kind & K_PROP) rp = true;
       if (!regex) {
         if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
@@ -454,7 +474,7 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
   bool all_direct = true, all_ok = true;
   const RuleResAttr* ra = R.T.rres + t.res_off;
   for (uint32_t k = 0; k < t.res_n; ++k) {
-    const RuleResAttr r = load_words(ra + wave_uniform(k));
+    const RuleResAttr r = load_words(R.T, ra + wave_uniform(k));
     if (r.kind & K_ENT_LOOSE) {
       bool em = false;
       for (int j = 0; j < (int)R.h.nres; ++j) {
@@ -579,7 +599,7 @@ ACS_FN tri multiple_entities(const NodeRec& S, const RQ& R) {
     if (!(q.kind & K_ENT)) continue;
     bool multi = false;
     for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
-      const NodeRec P = load_words(R.T.pols + p);
+      const NodeRec P = load_words(R.T, R.T.pols + p);
       if (P.nflags & NF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
       if (!(P.nflags & NF_HAS_TARGET) || P.res_n == 0) continue;
       const uint8_t pe = (P.nflags & NF_EFFECT_TRUTHY) ? P.effect : (uint8_t)EFF_UNDEF;  // no PERMIT default
@@ -624,7 +644,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = load_words(T.sets + s);
+    const NodeRec S = load_words(T, T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
       PROF_T0(t0);
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
@@ -640,7 +660,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = load_words(T.pols + p);
+        const NodeRec P = load_words(T, T.pols + p);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
@@ -665,7 +685,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = load_words(T.pols + p);
+      const NodeRec P = load_words(T, T.pols + p);
       if (P.nflags & NF_NULL) continue;
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
@@ -691,7 +711,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = load_words(T.rules + r);
+        const NodeRec Q = load_words(T, T.rules + r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
@@ -792,7 +812,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = load_words(T.sets + s);
+    const NodeRec S = load_words(T, T.sets + s);
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
       if (m < 0) return make_err(m, s + 1);
@@ -804,7 +824,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = load_words(T.pols + p);
+        const NodeRec P = load_words(T, T.pols + p);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, true, &obl);
@@ -826,7 +846,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = load_words(T.pols + p);
+      const NodeRec P = load_words(T, T.pols + p);
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
         const tri m = target_match(P, R, pe, !exact, true, &obl);
@@ -837,7 +857,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = load_words(T.rules + r);
+        const NodeRec Q = load_words(T, T.rules + r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {

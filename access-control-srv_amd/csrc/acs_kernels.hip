@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -236,6 +237,9 @@ struct acs_tables {
   // sort workspace, grown on demand: keys/idx double buffers + hipcub temp storage
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // host-buffer entry points (internal stream, events, workspace) may be called from
+  // several host threads at once (e.g. the N-API addon's libuv pool): one at a time
+  std::mutex mu;
 };
 
 extern "C" {
@@ -251,6 +255,18 @@ int acs_phase_read(unsigned long long* out, int n) {
   HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_phase_acc), z, sizeof z));
   for (int k = 0; k < n && k < PH_N; ++k) out[k] = h[k];
   return PH_N;
+}
+#endif
+
+#if defined(ACS_CHECK_UNIFORM)
+// Debug build only: read and reset the non-uniform table-load counters.
+int acs_debug_read(unsigned long long* out, int n) {
+  unsigned long long h[4] = {}, z[4] = {};
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(acs_nonuniform), sizeof h));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_nonuniform), z, sizeof z));
+  for (int k = 0; k < n && k < 4; ++k) out[k] = h[k];
+  return 4;
 }
 #endif
 
@@ -291,7 +307,8 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   }
   auto* t = new acs_tables();
   t->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, total ? total : 16) != hipSuccess ||
+  const size_t alloc = total + 64;  // clamp window [base, base + total] for 64-B record loads
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
       hipMemcpy(t->dev, (const char*)blob + src, total, hipMemcpyHostToDevice) != hipSuccess ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
@@ -310,6 +327,8 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_pols = h.n_pols;
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
+  t->view.lo = (uint64_t)(uintptr_t)base;
+  t->view.hi = (uint64_t)(uintptr_t)base + alloc - 64;
   return t;
 }
 
@@ -439,9 +458,15 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   const uint32_t* perm = nullptr;
   if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
+  const int slot = (int)(t->launches % acs_tables::RING);
+  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, acs_wia_words_per_request(t),
                      bits, obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
+  if (t->timing) {
+    HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
+    t->launches++;
+  }
   return 0;
 }
 
@@ -512,6 +537,7 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
 int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
   if (!t || !b || !out) return fail("acs_is_allowed: null argument");
   if (b->n == 0) return 0;
+  std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;
   if (upload_batch(D, b, t->stream)) return -1;
@@ -530,6 +556,7 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
                         acs_decision* out) {
   if (!t || !b || !bits || !obl || !obl_n || !out) return fail("acs_what_is_allowed: null argument");
   if (b->n == 0) return 0;
+  std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;
   if (upload_batch(D, b, t->stream)) return -1;

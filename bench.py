@@ -26,6 +26,8 @@ import torch  # noqa: E402
 WORKLOADS = {
     "c2": ("c2: isAllowed, 1M requests/GPU vs 100 policy sets / 200 policies / 1k rules, flat roles", 1_000_000),
     "c3": ("c3: isAllowed, 10M requests/GPU vs 10k rules, mixed CAs + HR role scoping (depth-8 org tree)", 10_000_000),
+    "c4": ("c4: whatIsAllowed, 1M reverse queries/GPU vs 10k rules (c3 store, 30% of rules with properties), "
+           "inclusion bitsets over sets|policies|rules + maskedProperty logs", 1_000_000),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 
@@ -115,33 +117,122 @@ def measured_traffic(config, kernel="is_allowed_kernel"):
 
 
 def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
-    """Oracle ('port') timed on a bounded sample of the same workload, single core;
-    the same sample is checked against the GPU decisions."""
-    from oracle.acs_oracle import Oracle, FULL_URNS
-    from diff_utils import oracle_outcome, gpu_outcome
-    o = Oracle(FULL_URNS)
-    o.load(doc)
-    rng = np.random.default_rng(1234)
-    idx = rng.permutation(sb.batch.n)
-    reqs = []
-    mism = 0
+    """The C++ oracle (oracle/acs_oracle.cpp: the reference's per-request serial algorithm,
+    'port') on a bounded random sample of the same batch, std::thread x up to 16 host
+    cores (the GPU box's CPU share); only evaluation is timed (requests are decoded to the
+    reference's JSON shape and parsed first).  Every sampled outcome is also compared with
+    the GPU's decision record (parity)."""
+    from oracle import acs_oracle_c
+    from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
+    from diff_utils import gpu_outcome
+    acs_oracle_c.build()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    co = acs_oracle_c.COracle(FULL_URNS, DEFAULT_CAS, doc)
+    idx = np.random.default_rng(1234).permutation(sb.batch.n)
+    chunk = 20_000 if kind == "c2" else 250  # c3 requests carry HR trees of up to 21,845 orgs
+    done = busy = mism = unsup = host = 0
+    while busy < seconds and done < len(idx):
+        part = idx[done:done + chunk]
+        out, sec = co.raw([sb.decode(int(i)) for i in part], threads)
+        busy += sec
+        for i, r in zip(part, out):
+            want = acs_oracle_c.outcome(r)
+            got = gpu_outcome(cs, gpu_dec[i])
+            if want[0] == "UNSUPPORTED":
+                unsup += 1
+            elif got[0] == "HOST":
+                host += 1
+            elif got != want:
+                mism += 1
+        done += len(part)
+    co.close()
+    return {"value": done / busy, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": f"{done} random requests of the same {kind} batch through oracle/acs_oracle.cpp (C++17 "
+                      f"restatement of the reference's per-request serial algorithm, std::thread x {threads}), "
+                      f"{busy:.1f}s of evaluation wall time"}, \
+        {"oracle_sample": done, "mismatches": mism, "oracle_unsupported": unsup, "gpu_host_path": host}
+
+
+def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist):
+    """c4: one step = K2 over a resident batch of whatIsAllowed requests (c3 store and request
+    generator); outputs: per-request inclusion bitset over (sets | policies | rules), the
+    maskedProperty push log, its length and the 8-B record.  Parity: a random sample vs
+    the Python oracle's whatIsAllowed (rule sets bit-exact, obligations in push order)."""
+    from acs_mi355x import compiler, native, results, synth, layout as L
+    from acs_mi355x.device import DeviceBatch, what_is_allowed_device
+    from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS, Oracle
+    from diff_utils import norm_rq
+    import torch.distributed as tdist
+    cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, n, "c3", seed=0xACC1004 + 17 * rank)
+    tables = native.Tables(compiler.store_blob(cs), local)
+    tables.set_timing(True)
+    db = DeviceBatch(sb.batch, local)
+    stream = torch.cuda.current_stream(dev)
+    bufs = what_is_allowed_device(tables, db, None, stream)
+    for _ in range(args.warmup):
+        what_is_allowed_device(tables, db, bufs, stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    done = 0
-    for i in idx:
-        q = sb.decode(int(i))
+    for _ in range(args.steps):
+        what_is_allowed_device(tables, db, bufs, stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean(tables.kernel_times(args.steps)))
+    if dist:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    if rank == 0:
+        bits = bufs[0].cpu().numpy().view(np.uint32)
+        obl = bufs[1].cpu().numpy().view(np.uint32)
+        obl_n = bufs[2].cpu().numpy().view(np.uint32)
+        rec = bufs[3].cpu().numpy().reshape(-1).view(L.DECISION_DT)
+        words = bits.shape[1]
+        per_req, parts = algorithmic_bytes(cs, sb.batch)
+        # K2 writes the inclusion bitset, the log entries it pushes, the log length and the record
+        out_b = 4 * words + 8 * float(obl_n.mean()) + 4 + 8
+        per = per_req - 8.0 + out_b
+        parts.update({"B_out": out_b, "bitset_bytes": 4 * words, "obligation_entries_mean": float(obl_n.mean())})
+        achieved = per * n / (kern_ms * 1e-3) / 1e9
+        # parity sample vs the oracle (bounded: the Python oracle scans 10k rules per request)
+        o = Oracle(FULL_URNS)
+        o.load(doc)
+        rng = np.random.default_rng(4321)
+        ok = np.flatnonzero((rec["flags"] & (L.OF_OBL_OVERFLOW | L.OF_HOST_REQ)) == 0)
+        mism = checked = 0
         t1 = time.perf_counter()
-        w = oracle_outcome(o, q)
-        done += 1
-        reqs.append(time.perf_counter() - t1)
-        if w != gpu_outcome(cs, gpu_dec[i]):
-            mism += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    busy = sum(reqs)
-    return {"value": done / busy, "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"{done} random requests of the same {kind} batch through oracle/acs_oracle.py "
-                      f"(Python restatement of the reference TS, 1 thread), {busy:.1f}s of CPU work"}, \
-        {"oracle_sample": done, "mismatches": mism}
+        for i in rng.permutation(ok):
+            got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], obl[i][:obl_n[i]], rec[i]))
+            checked += 1
+            mism += got != norm_rq(o.what_is_allowed(sb.decode(int(i))))
+            if time.perf_counter() - t1 > args.cpu_seconds:
+                break
+        line = {
+            "metric": "whatIsAllowed reverse queries/sec", "value": world * n * args.steps / elapsed,
+            "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": desc, "requests_per_gpu": n, "policy_sets": cs.n_sets, "policies": cs.n_pols,
+                       "rules": cs.n_rules, "bitset_words_per_request": words, "parallelism": f"requests dp{world}",
+                       "host_path_fraction": float(1 - len(ok) / n)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic("c4", "what_is_allowed_kernel")[0],
+                         "kernel": "what_is_allowed_kernel", "kernel_ms": kern_ms, "bytes_per_query": per,
+                         "bytes_parts": parts, "output_GBps": (4 * words + 8 * float(obl_n.mean()) + 12) * n /
+                         (kern_ms * 1e-3) / 1e9},
+            "parity": {"oracle_sample": checked, "mismatches": int(mism),
+                       "note": "rule sets + obligations vs oracle/acs_oracle.py whatIsAllowed"},
+        }
+        print(json.dumps(line), flush=True)
+    tables.close()
+    if dist:
+        tdist.destroy_process_group()
 
 
 def main():
@@ -181,6 +272,8 @@ def main():
     n = args.requests or n_default
     doc = synth.c2_store() if kind == "c2" else synth.c3_store()
     full_map = store.populate(doc)
+    if kind == "c4":
+        return bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist)
     if args.rule_shard:
         # variant ii: this rank's run of whole policy sets; the same requests on every rank
         set_lo, set_hi = shard.partition(full_map, world)[rank]

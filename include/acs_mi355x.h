@@ -84,10 +84,13 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device);
 void acs_free(acs_tables* t);
 
 /* Replaces: AccessController.isAllowed (accessController.ts:88-324), for a batch.
- * Host buffers in and out; synchronous (H2D, kernel, D2H on an internal stream). */
+ * Host buffers in and out; synchronous (H2D, kernel, D2H on an internal stream).  Safe to
+ * call from several host threads on one handle (calls are serialised per handle). */
 int acs_is_allowed(acs_tables* t, const acs_req_batch* host_batch, acs_decision* out);
 
-/* Same, on device-resident buffers, enqueued on `stream` (a hipStream_t; NULL = default). */
+/* Same, on device-resident buffers, enqueued on `stream` (a hipStream_t; NULL = default).
+ * The handle's sort workspace is shared: issue the *_device calls of one handle on one
+ * stream (or serialise them). */
 int acs_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, acs_decision* dev_out, void* stream);
 
 /* Replaces: AccessController.whatIsAllowed (accessController.ts:326-427).
@@ -120,8 +123,8 @@ int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* de
  * order the batch by (entity, role, action) with a radix sort so that every
  * wave shares its table-driven branches; results are written in input order. */
 #define ACS_OPT_SORT 1
-/* ACS_OPT_TIMING: record HIP events on the launch stream around every K1 kernel of
- * acs_is_allowed_device; acs_kernel_times returns the durations (ms) of the last n
+/* ACS_OPT_TIMING: record HIP events on the launch stream around every eval kernel (K1 of
+ * acs_is_allowed_device, K2 of acs_what_is_allowed_device); acs_kernel_times returns the durations (ms) of the last n
  * launches (a ring of 256), returning how many were written. */
 #define ACS_OPT_TIMING 2
 int acs_set_option(acs_tables* t, int option, int value);
