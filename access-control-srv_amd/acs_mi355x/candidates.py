@@ -36,6 +36,7 @@ from .jsops import MISSING
 _HIT_LIKE = L.RX_HIT | L.RX_THROW_TYPE | L.RX_THROW_SYNTAX | L.RX_HOST
 MAX_CLASSES = L.PCOL_ALL  # ids 0 .. 0xFFFE
 _CHUNK = 2048
+_CHUNK_NODE_BITS = 1 << 27  # bools per section array of one chunk (large stores: fewer keys)
 _MAX_ACTION_KEYS = 62
 _KEY_ROW_BYTES = 512 << 20  # candidate rows computed per batch before dedupe
 
@@ -249,8 +250,9 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
         role_filter = level == "entity+roles+action"
         action_filter = level != "entity"
         out = np.zeros((len(ckey), W), np.uint32)
-        for c0 in range(0, len(ckey), _CHUNK):
-            ck = ckey[c0:c0 + _CHUNK]
+        chunk = max(8, min(_CHUNK, _CHUNK_NODE_BITS // max(1, cs.n_sets + cs.n_pols + cs.n_rules)))
+        for c0 in range(0, len(ckey), chunk):
+            ck = ckey[c0:c0 + chunk]
             pc = ck[:, 0]
             a = ck[:, 1] if action_filter else np.ones(len(ck), np.int64)
             M = np.zeros((len(ck), nrr + 1), bool)

@@ -202,6 +202,67 @@ def c3_store(seed=0xACC0003, n_sets=200, n_pols=5, n_rules=10):
     return {"policy_sets": sets}
 
 
+def c5_store(seed=0xACC0005, n_sets=1000, n_pols=10, n_rules=100):
+    """c5: 1,000 sets x 10 policies x 100 rules = 1M rules, the c3 rule mix (roles, 50%
+    organization-scoped with 25% of those hierarchicalRoleScoping 'false', 30% with
+    properties, 80% with an action), drawn vectorised (one draw per attribute kind)."""
+    rng = np.random.default_rng(seed)
+    P, R = n_sets * n_pols, n_sets * n_pols * n_rules
+    pol_ent = rng.choice(N_ENT, size=P, p=zipf_p(N_ENT))
+    pol_ca = rng.integers(3, size=P)
+    pol_tgt = rng.random(P) < 0.8
+    pol_eff = rng.random(P) < 0.1
+    set_ca = rng.integers(3, size=n_sets)
+    r_role = rng.choice(N_ROLES, size=R, p=zipf_p(N_ROLES))
+    r_rse = rng.random(R) < 0.5
+    r_hrs = rng.random(R) < 0.25
+    r_props = rng.random(R) < 0.3
+    r_np = rng.integers(1, 3, size=R)
+    r_pp = rng.integers(0, N_PROPS, size=(R, 2))
+    r_act = rng.random(R) < 0.8
+    r_a = rng.choice(len(ACTIONS), size=R, p=zipf_p(len(ACTIONS)))
+    x = rng.random(R)
+    r_eff = np.where(x < 0.001, 2, np.where(x < 0.7, 0, 1))
+    y = rng.random(R)
+    r_ec = np.where(y < 0.5, 1, np.where(y < 0.75, 0, -1))
+    effects = ["PERMIT", "DENY", "Permit"]
+    role_v = [role(k) for k in range(N_ROLES)]
+    ent_v = [entity(k) for k in range(N_ENT)]
+    sets, k = [], 0
+    for s in range(n_sets):
+        pols = []
+        for p in range(n_pols):
+            pi = s * n_pols + p
+            e = int(pol_ent[pi])
+            rules = []
+            for q in range(n_rules):
+                subs = [{"id": URN["role"], "value": role_v[r_role[k]]}]
+                if r_rse[k]:
+                    subs.append({"id": URN["rse"], "value": ORG_ENTITY})
+                    if r_hrs[k]:
+                        subs.append({"id": URN["hrs"], "value": "false"})
+                res = [{"id": URN["entity"], "value": ent_v[e]}]
+                if r_props[k]:
+                    for pp in sorted(set(r_pp[k, :r_np[k]].tolist())):
+                        res.append({"id": URN["property"], "value": prop(e, pp)})
+                t = {"subjects": subs, "resources": res}
+                if r_act[k]:
+                    t["actions"] = [{"id": URN["actionID"], "value": ACTIONS[r_a[k]]}]
+                r = {"id": f"r{s}_{p}_{q}", "target": t, "effect": effects[r_eff[k]]}
+                if r_ec[k] >= 0:
+                    r["evaluation_cacheable"] = bool(r_ec[k])
+                rules.append(r)
+                k += 1
+            pol = {"id": f"p{s}_{p}", "combining_algorithm": CAS[pol_ca[pi]], "rules": rules}
+            if pol_tgt[pi]:
+                pol["target"] = {"resources": [{"id": URN["entity"], "value": ent_v[e]}]}
+            if pol_eff[pi]:
+                pol["effect"] = "PERMIT"
+            pols.append(pol)
+        sets.append({"id": f"s{s}", "combining_algorithm": CAS[set_ca[s]], "policies": pols})
+    return {"policy_sets": sets}
+
+
 # ------------------------------------------------------------------ requests (packed)
 @dataclass
 class SynthBatch:

@@ -141,12 +141,21 @@ struct Batch {
 struct Filter {
   const uint32_t* row[4];  // class rows (nullptr: unused)
   const uint32_t* lds;     // GPU: the wave's OR of all its class rows, in LDS (nullptr: use row[])
+  const uint32_t* list;    // GPU, rows too long for LDS: the wave's > 4 class ids, in LDS
+  const uint32_t* cand;    // ... and the class-row table they index ([C][W])
+  uint32_t nlist, W;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   bool all;                // no filtering
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (lds) return wave_uniform(((__attribute__((address_space(3))) const uint32_t*)lds)[w]);
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    if (lds) return wave_uniform(((lds_u32*)lds)[w]);
+    if (list) {  // OR of every class row of the wave, word by word (large stores, mixed waves)
+      uint32_t x = 0;
+      for (uint32_t k = 0; k < nlist; ++k) x |= cand[(size_t)wave_uniform(((lds_u32*)list)[k]) * W + w];
+      return wave_uniform(x);
+    }
 #endif
     uint32_t x = row[0][w];
     if (row[1]) x |= row[1][w];
@@ -315,6 +324,9 @@ ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
 }
 
 // ------------------------------------------------------------------ resourceAttributesMatch
+#ifndef ACS_RA_CACHE
+#define ACS_RA_CACHE 4  // rule resource attributes held in registers per resource_match call
+#endif
 // Request attrs [j0, j1) with requestPropertiesExist = rpe.  wia: 'whatIsAllowed' op.
 template <class RQ>
 ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool regex, bool wia, int j0, int j1,
@@ -324,16 +336,22 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
   bool em = false, pm = false, rp = false, om = false, skip_deny = true;
   int ent_j = 0;
   uint32_t ent_val = 0;
+  // The target's attributes are the same for every lane: the first ACS_RA_CACHE are loaded
+  // once per call (all in flight together) instead of once per request attribute.
+  RuleResAttr rc[ACS_RA_CACHE > 0 ? ACS_RA_CACHE : 1];
+#pragma unroll
+  for (int k = 0; k < ACS_RA_CACHE; ++k)
+    if (k < (int)t.res_n) rc[k] = load_words(R.T, ra + k);
   for (int j = j0; j < j1; ++j) {
     const ReqRes q = R.res(j);
     pm = false;
-    for (uint32_t k = 0; k < t.res_n; ++k) {
-      const RuleResAttr r = load_words(R.T, ra + wave_uniform(k));
+    // one (request attr, rule attr) step of the ordered double loop; <0: the reference throws
+    auto step = [&](const RuleResAttr& r, int jj) -> tri {
       if (r.kind & K_PROP) rp = true;
       if (!regex) {
         if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
           em = true;
-          ent_j = j;
+          ent_j = jj;
           ent_val = q.value;
         } else if ((q.kind & K_OP) && (r.kind & K_OP) && q.value == r.value) {
           om = true;
@@ -357,6 +375,18 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
           if (r.hash_sfx == q.hash_sfx) pm = true;
         }
       }
+      return 0;
+    };
+#pragma unroll
+    for (int k = 0; k < ACS_RA_CACHE; ++k) {
+      if (k < (int)t.res_n) {
+        const tri e = step(rc[k], j);
+        if (e < 0) return e;
+      }
+    }
+    for (uint32_t k = ACS_RA_CACHE; k < t.res_n; ++k) {
+      const tri e = step(load_words(R.T, ra + wave_uniform(k)), j);
+      if (e < 0) return e;
     }
     const bool scope = (q.kind & K_PROP) || !rpe;
     if (!wia) {

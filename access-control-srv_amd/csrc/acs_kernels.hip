@@ -65,14 +65,17 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
 }
 
 // Candidate filter of a wave, built with every lane present before any lane diverges.
-// With an LDS row (`lds` = this wave's W-word region) the filter is the OR of the class
-// rows of all the wave's active requests, however many classes the wave spans.  Without
-// one (tables too large for LDS) it keeps up to 4 row pointers, else no filtering.  An
+// With an LDS row (`lds` = this wave's W-word region, W <= LDS_FILTER_WORDS) the filter is
+// the OR of the class rows of all the wave's active requests, however many classes the
+// wave spans.  With rows too long for LDS (large stores) it keeps up to 4 row pointers, or
+// — a wave of more classes — their ids in this wave's LDS list, OR-ed word by word.  An
 // unfiltered request (PCOL_ALL) disables filtering for its wave.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t* lds) {
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t* lds, uint32_t* list) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
+  F.cand = B.cand;
+  F.W = B.cand_words;
   F.all = B.cand == nullptr;
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   if (lds && !F.all)
@@ -82,37 +85,51 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   while (pending && !F.all) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t c = __builtin_amdgcn_readlane(cls, leader);
-    if (c == PCOL_ALL || c >= B.cand_rows || (!lds && n == 4)) {
+    if (c == PCOL_ALL || c >= B.cand_rows) {
       F.all = true;
       break;
     }
     const uint32_t* r = B.cand + (size_t)c * W;
     if (lds) {
       for (uint32_t w = lane; w < W; w += 64) lds[w] |= r[w];
-    } else if (n == 0) {
-      F.row[0] = r;
-    } else if (n == 1) {
-      F.row[1] = r;
-    } else if (n == 2) {
-      F.row[2] = r;
     } else {
-      F.row[3] = r;
+      if (lane == 0) list[n] = c;  // at most 64 distinct classes per wave
+      if (n == 0) {
+        F.row[0] = r;
+      } else if (n == 1) {
+        F.row[1] = r;
+      } else if (n == 2) {
+        F.row[2] = r;
+      } else if (n == 3) {
+        F.row[3] = r;
+      }
     }
     ++n;
     pending &= ~__ballot(valid && cls == c);
   }
   if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
   if (!F.all && lds) F.lds = lds;
+  if (!F.all && !lds && n > 4) {
+    F.list = list;
+    F.nlist = n;
+  }
   return F;
 }
 
-// Dynamic LDS: one W-word union row per wave when W <= LDS_FILTER_WORDS.
+// Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS, else a 64-entry
+// class list.
 constexpr uint32_t LDS_FILTER_WORDS = 1024;
+constexpr uint32_t LDS_LIST_WORDS = 64;
 extern __shared__ uint32_t acs_dyn_lds[];
 
 __device__ inline uint32_t* wave_lds_row(const Batch& B) {
   if (!B.cand || B.cand_words > LDS_FILTER_WORDS) return nullptr;
   return acs_dyn_lds + (threadIdx.x >> 6) * B.cand_words;
+}
+
+__device__ inline uint32_t* wave_lds_list(const Batch& B) {
+  if (!B.cand || B.cand_words <= LDS_FILTER_WORDS) return nullptr;
+  return acs_dyn_lds + (threadIdx.x >> 6) * LDS_LIST_WORDS;
 }
 
 __device__ inline uint32_t request_pcol(const ReqHdr& h) {
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
-  const Filter F = wave_filter(B, in && !done, request_pcol(h), wave_lds_row(B));
+  const Filter F = wave_filter(B, in && !done, request_pcol(h), wave_lds_row(B), wave_lds_list(B));
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
@@ -182,7 +199,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h), wave_lds_row(B));
+  const Filter F = wave_filter(B, in && !host, request_pcol(h), wave_lds_row(B), wave_lds_list(B));
   if (!in) return;
   uint32_t* my_bits = bits + (size_t)i * words;
   for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
@@ -216,7 +233,8 @@ __global__ __launch_bounds__(BLOCK) void shard_decode_kernel(const uint64_t* __r
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 size_t filter_lds_bytes(const Batch& B) {
-  return (B.cand && B.cand_words <= LDS_FILTER_WORDS) ? (size_t)(BLOCK / 64) * B.cand_words * 4 : 0;
+  if (!B.cand) return 0;
+  return (size_t)(BLOCK / 64) * (B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_LIST_WORDS) * 4;
 }
 
 }  // namespace

@@ -28,8 +28,25 @@ WORKLOADS = {
     "c3": ("c3: isAllowed, 10M requests/GPU vs 10k rules, mixed CAs + HR role scoping (depth-8 org tree)", 10_000_000),
     "c4": ("c4: whatIsAllowed, 1M reverse queries/GPU vs 10k rules (c3 store, 30% of rules with properties), "
            "inclusion bitsets over sets|policies|rules + maskedProperty logs", 1_000_000),
+    "c5": ("c5: isAllowed, 1M-request batches/GPU vs 1M rules (1,000 sets x 10 policies x 100 rules, c3 rule mix "
+           "+ HR scoping)", 1_000_000),
 }
+
+
+def make_store(kind):
+    from acs_mi355x import synth
+    return {"c2": synth.c2_store, "c3": synth.c3_store, "c4": synth.c3_store, "c5": synth.c5_store}[kind]()
+
+
+def request_kind(kind):
+    return "c2" if kind == "c2" else "c3"  # c4 / c5 draw c3-shaped requests (HR context)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
+_T0 = time.time()
+
+
+def log(msg):
+    """Setup progress on stderr (large configs take minutes to compile / encode)."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def _node_bytes(nodes):
@@ -41,9 +58,8 @@ def _node_bytes(nodes):
 def scan_bytes(cs, batch, wave=64):
     """Table bytes the K1 waves visit, counted from the same candidate rows the kernel uses:
     requests in coherence-sort order, 64 per wave, the union of the wave's class rows (an
-    unfiltered class, or > 4 classes when the row is too long for LDS: the whole table); a
-    policy is visited only inside a
-    visited set, a rule only inside a visited policy.  Returns total bytes for the batch."""
+    unfiltered class: the whole table); a policy is visited only inside a visited set, a rule
+    only inside a visited policy.  Returns total bytes for the batch."""
     from acs_mi355x import layout as L
     n = batch.n
     cand = batch.cand
@@ -67,8 +83,8 @@ def scan_bytes(cs, batch, wave=64):
     def union_bytes(key):
         if key in cache:
             return cache[key]
-        lds_union = cand is not None and cand.shape[1] <= 1024  # K1 ORs every class row in LDS
-        if any(c >= R for c in key) or (len(key) > 4 and not lds_union):
+        # K1 ORs every class row of the wave (in LDS, or word by word for long rows)
+        if any(c >= R for c in key):
             cache[key] = full
             return full
         row = np.bitwise_or.reduce(cand[list(key)], axis=0)
@@ -129,7 +145,7 @@ def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
     threads = max(1, min(16, os.cpu_count() or 1))
     co = acs_oracle_c.COracle(FULL_URNS, DEFAULT_CAS, doc)
     idx = np.random.default_rng(1234).permutation(sb.batch.n)
-    chunk = 20_000 if kind == "c2" else 250  # c3 requests carry HR trees of up to 21,845 orgs
+    chunk = {"c2": 20_000, "c3": 250}.get(kind, 32)  # c3/c5 requests carry HR trees of up to 21,845 orgs
     done = busy = mism = unsup = host = 0
     while busy < seconds and done < len(idx):
         part = idx[done:done + chunk]
@@ -165,6 +181,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     import torch.distributed as tdist
     cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
     sb = synth.requests(cs, n, "c3", seed=0xACC1004 + 17 * rank)
+    log(f"compiled {cs.n_rules} rules; encoded {n} requests")
     tables = native.Tables(compiler.store_blob(cs), local)
     tables.set_timing(True)
     db = DeviceBatch(sb.batch, local)
@@ -270,8 +287,10 @@ def main():
     kind = args.config
     desc, n_default = WORKLOADS[kind]
     n = args.requests or n_default
-    doc = synth.c2_store() if kind == "c2" else synth.c3_store()
+    log(f"config {kind}: generating the store")
+    doc = make_store(kind)
     full_map = store.populate(doc)
+    log("store populated")
     if kind == "c4":
         return bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist)
     if args.rule_shard:
@@ -279,10 +298,11 @@ def main():
         set_lo, set_hi = shard.partition(full_map, world)[rank]
         sbase = shard.base(full_map, set_lo)
         cs = compiler.compile_store(shard.slice_store(full_map, set_lo, set_hi), FULL_URNS, DEFAULT_CAS)
-        sb = synth.requests(cs, n, kind, seed=0xACC1000)
+        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000)
     else:
         cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
-        sb = synth.requests(cs, n, kind, seed=0xACC1000 + 17 * rank)
+        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000 + 17 * rank)
+    log(f"compiled {cs.n_rules} rules; encoded {n} requests ({sb.batch.cand.shape[0]} classes)")
     if args.lib:
         native.load(args.lib)
     tables = native.Tables(compiler.store_blob(cs), local)
@@ -328,13 +348,14 @@ def main():
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
+    log("timed steps done")
     dec = decisions_from_tensor(out)
     shard_check = None
     if args.rule_shard and rank == 0:
         # size-independent property: the set-sharded + all-reduced records equal an
         # unsharded evaluation of the whole store on the same requests, bit for bit
         cs_full = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
-        sb_full = synth.requests(cs_full, n, kind, seed=0xACC1000)
+        sb_full = synth.requests(cs_full, n, request_kind(kind), seed=0xACC1000)
         t_full = native.Tables(compiler.store_blob(cs_full), local)
         want = decisions_from_tensor(is_allowed_device(t_full, DeviceBatch(sb_full.batch, local)))
         t_full.close()
@@ -350,6 +371,7 @@ def main():
         pcie = {"value": n / pcie_s, "unit": "decisions/s", "ms": pcie_s * 1e3, "input_bytes": int(sb.batch.nbytes()),
                 "identical_to_device_path": bool(np.array_equal(host_dec.view(np.uint64), dec.view(np.uint64)))}
     if rank == 0:
+        log("counting algorithmic bytes")
         per_dec, parts = algorithmic_bytes(cs, sb.batch)
         achieved = per_dec * n / (kern_ms * 1e-3) / 1e9
         traffic, traffic_src = measured_traffic(kind)
@@ -384,6 +406,7 @@ def main():
         if shard_check:
             line["rule_shard"] = shard_check
         if world == 1 and not args.no_cpu_baseline:
+            log("CPU baseline (C++ oracle)")
             cb, par = cpu_baseline(kind, doc, sb, dec, cs, args.cpu_seconds)
             line["cpu_baseline"] = cb
             line["parity"] = par

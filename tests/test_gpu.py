@@ -123,6 +123,22 @@ def test_synthetic_config_gpu(kind, n, sample):
     t.close()
 
 
+def test_large_store_class_list_gpu():
+    """Rows longer than the LDS union (W > 1024 words): waves of up to 4 classes use row
+    pointers, mixed waves the LDS class list — both bit-identical to the CPU build."""
+    doc = synth.c5_store(n_sets=60)  # 60 sets x 10 x 100 = 60k rules, W ~ 1.9k words
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 30_000, "c3", tree=synth.OrgTree(fanout=4, depth=5))
+    assert sb.batch.cand.shape[1] > 1024
+    t = gpu_tables(cs)
+    dec = t.is_allowed(sb.batch)
+    t.close()
+    ref = host_core.is_allowed(cs, sb.batch)
+    assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
+    codes = np.bincount(dec["decision"], minlength=7)
+    assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
+
+
 def test_what_is_allowed_c4_gpu():
     doc, cs, sb = _synth("c3", 8_000)
     t = gpu_tables(cs)
