@@ -39,6 +39,8 @@ _CHUNK = 2048
 _CHUNK_NODE_BITS = 1 << 27  # bools per section array of one chunk (large stores: fewer keys)
 _MAX_ACTION_KEYS = 62
 _KEY_ROW_BYTES = 512 << 20  # candidate rows computed per batch before dedupe
+_ROLE_ROW_BYTES = 256 << 20  # role-factor rows per batch
+FORCE_LEVEL = None  # tests: pin the class key level (and with it the role factor)
 
 
 def words(n):
@@ -223,7 +225,7 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
     ws, wp, wr = section_words(cs)
     W = ws + wp + wr
     if not active.any():
-        return cls, np.zeros((1, W), np.uint32)
+        return cls, np.zeros((1, W), np.uint32), None, None
     if act is not None:
         ak, apairs = action_keys(hdr, act)
     else:
@@ -237,7 +239,8 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
     b_s = cs.sets["child_begin"].astype(np.int64)
     e_s = cs.sets["child_end"].astype(np.int64)
     nonempty = e_s > b_s
-    for level in ("entity+roles+action", "entity+action", "entity"):
+    levels = ("entity+roles+action", "entity+action", "entity")
+    for level in (levels if FORCE_LEVEL is None else (FORCE_LEVEL,)):
         cols = [pcol.astype(np.int64)[:, None]]
         if level != "entity":
             cols.append(ak[:, None])
@@ -291,7 +294,46 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
     rank[np.argsort(-cost, kind="stable")] = np.arange(len(cost))
     urows = np.ascontiguousarray(urows[np.argsort(rank)])
     cls[active] = rank[rinv[inv]].astype(np.uint32)
-    return cls, urows
+    if role_filter or nrr == 0:
+        return cls, urows, None, None
+    rkey, rbits = _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty)
+    return cls, urows, rkey, rbits
+
+
+def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty):
+    """Role factor for class rows keyed without roles (large stores): one row per distinct
+    role-association set of the batch — the nodes a request holding those roles can reach
+    through checkSubjectMatches (accessController.ts:797-806) — and each request's row
+    index (0xFFFF: no role filtering).  The kernel ANDs it with the class row; both are
+    supersets of the joint filter, so their AND is too."""
+    ws, wp, wr = section_words(cs)
+    W = ws + wp + wr
+    n = len(rs)
+    rkey = np.full(n, 0xFFFF, np.uint32)
+    keys, inv = _unique_rows(rs[active])
+    if len(keys) == 0 or len(keys) * W * 4 > _ROLE_ROW_BYTES or len(keys) >= 0xFFFF:
+        return None, None
+    rkey[active] = inv.astype(np.uint32)
+    out = np.zeros((len(keys), W), np.uint32)
+    chunk = max(8, min(_CHUNK, _CHUNK_NODE_BITS // max(1, cs.n_sets + cs.n_pols + cs.n_rules)))
+    for c0 in range(0, len(keys), chunk):
+        ck = keys[c0:c0 + chunk]
+        M = np.zeros((len(ck), nrr + 1), bool)
+        M[:, nrr] = True  # "no role requirement" column
+        for j in range(ck.shape[1]):
+            v = ck[:, j]
+            ok = v >= 0
+            M[np.flatnonzero(ok), v[ok]] = True
+
+        def role_ok(rr):
+            return M[:, np.where(rr >= 0, rr, nrr)]
+
+        s, p, r = role_ok(req_rows[0]), role_ok(req_rows[1]), role_ok(req_rows[2])
+        if cs.n_pols:
+            cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
+            s = s & ((cum[:, e_s] - cum[:, b_s]) > 0) & nonempty[None, :]
+        out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+    return rkey, out
 
 
 def _unique_rows(a):

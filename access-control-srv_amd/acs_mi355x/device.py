@@ -28,6 +28,9 @@ class DeviceBatch:
                   for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx")}
         if batch.cand is not None:
             self.t["cand"] = _to_dev(batch.cand, self.dev)
+        if batch.role_key is not None:
+            self.t["role_key"] = _to_dev(batch.role_key, self.dev)
+            self.t["role_bits"] = _to_dev(batch.role_bits, self.dev)
         self.ptrs = {k: v.data_ptr() for k, v in self.t.items()}
         self.struct = batch_struct(batch, self.ptrs)
         self.nbytes = sum(v.numel() for v in self.t.values())

@@ -49,10 +49,13 @@ class RequestBatch:
     cand: np.ndarray | None = None   # [rx_cols + 1, W] candidate bitsets (candidates.py)
     cand_wp: int = 0
     cand_wr: int = 0
+    role_key: np.ndarray | None = None   # [n] u32 role-factor row per request (large stores)
+    role_bits: np.ndarray | None = None  # [role rows, W] u32
 
     def nbytes(self):
         return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
-            (self.cand.nbytes if self.cand is not None else 0)
+            (self.cand.nbytes if self.cand is not None else 0) + \
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
 
 
 def _attr_list(v, what):
@@ -444,5 +447,5 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     b.cand_wp, b.cand_wr = ws, ws + wp
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
     roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
-    cls, b.cand = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act)
+    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

@@ -21,7 +21,8 @@ class ReqBatchC(C.Structure):
                 ("act", C.c_void_p), ("roles", C.c_void_p), ("arena", C.c_void_p), ("arena_words", C.c_size_t),
                 ("rx", C.c_void_p), ("rx_cols", C.c_uint32), ("rx_rows", C.c_uint32),
                 ("cand", C.c_void_p), ("cand_words", C.c_uint32), ("cand_wp", C.c_uint32), ("cand_wr", C.c_uint32),
-                ("cand_rows", C.c_uint32)]
+                ("cand_rows", C.c_uint32), ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
+                ("role_rows", C.c_uint32)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -89,16 +90,21 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
         s.arena = b.arena.ctypes.data if b.arena.size else b.hdr.ctypes.data
         s.rx = b.rx.ctypes.data
         s.cand = b.cand.ctypes.data if b.cand is not None else None
+        if b.role_key is not None:
+            s.role_key, s.role_rows_bits = b.role_key.ctypes.data, b.role_bits.ctypes.data
     else:
         for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx"):
             setattr(s, k, ptrs[k])
         s.cand = ptrs.get("cand")
+        s.role_key, s.role_rows_bits = ptrs.get("role_key"), ptrs.get("role_bits")
     s.arena_words = int(b.arena.size)
     s.rx_cols = int(b.rx.shape[0])
     s.rx_rows = int(b.rx.shape[1])
     if b.cand is not None:
         s.cand_words, s.cand_wp, s.cand_wr = b.cand.shape[1], b.cand_wp, b.cand_wr
         s.cand_rows = b.cand.shape[0]
+    if b.role_key is not None:
+        s.role_rows = b.role_bits.shape[0]
     return s
 
 

@@ -133,6 +133,9 @@ struct Batch {
   const uint32_t* cand;   // [cand_rows][cand_words] candidate bitsets (sets | policies | rules) per class
   uint32_t cand_words, cand_wp, cand_wr;  // row length, word offsets of the policy / rule sections
   uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
+  const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
+  const uint32_t* role_bits;  // [role_rows][cand_words]
+  uint32_t role_rows;
 };
 
 // Candidate filter of a wave (GPU: the union of its lanes' class rows, gathered with
@@ -140,27 +143,37 @@ struct Batch {
 // are explicit pointers (no dynamically indexed array, so the filter stays in SGPRs).
 struct Filter {
   const uint32_t* row[4];  // class rows (nullptr: unused)
-  const uint32_t* lds;     // GPU: the wave's OR of all its class rows, in LDS (nullptr: use row[])
-  const uint32_t* list;    // GPU, rows too long for LDS: the wave's > 4 class ids, in LDS
-  const uint32_t* cand;    // ... and the class-row table they index ([C][W])
-  uint32_t nlist, W;
+  const uint32_t* rrow[4]; // role-factor rows AND-ed with row[k] (nullptr: none)
+  const uint32_t* lds;     // GPU: the wave's OR of all its (class & role) rows, in LDS
+  const uint32_t* list;    // GPU, rows too long for LDS: the wave's > 4 (class, role key) pairs, in LDS
+  const uint32_t* cand;    // ... and the row tables they index ([C][W], [role_rows][W])
+  const uint32_t* rbits;
+  uint32_t nlist, W, nroles;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   bool all;                // no filtering
+  ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
+    uint32_t x = cand[(size_t)c * W + w];
+    if (rk < nroles) x &= rbits[(size_t)rk * W + w];
+    return x;
+  }
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
     if (lds) return wave_uniform(((lds_u32*)lds)[w]);
-    if (list) {  // OR of every class row of the wave, word by word (large stores, mixed waves)
+    if (list) {  // OR of every (class & role) row of the wave, word by word (large stores, mixed waves)
       uint32_t x = 0;
-      for (uint32_t k = 0; k < nlist; ++k) x |= cand[(size_t)wave_uniform(((lds_u32*)list)[k]) * W + w];
+      for (uint32_t k = 0; k < nlist; ++k) {
+        const uint32_t key = wave_uniform(((lds_u32*)list)[k]);
+        x |= pair_word(key >> 16, key & 0xFFFFu, w);
+      }
       return wave_uniform(x);
     }
 #endif
-    uint32_t x = row[0][w];
-    if (row[1]) x |= row[1][w];
-    if (row[2]) x |= row[2][w];
-    if (row[3]) x |= row[3][w];
+    uint32_t x = row[0][w] & (rrow[0] ? rrow[0][w] : ~0u);
+    if (row[1]) x |= row[1][w] & (rrow[1] ? rrow[1][w] : ~0u);
+    if (row[2]) x |= row[2][w] & (rrow[2] ? rrow[2][w] : ~0u);
+    if (row[3]) x |= row[3][w] & (rrow[3] ? rrow[3][w] : ~0u);
     return wave_uniform(x);
   }
 };
@@ -272,7 +285,10 @@ struct ReqCtx {
 
 // Resource attributes staged in LDS by the kernel (slots < LDS_SLOTS, column = lane,
 // stride = block size): dynamic indexing without scratch, one ds_read_b128 per use.
-constexpr int LDS_SLOTS = 8;
+#ifndef ACS_LDS_SLOTS
+#define ACS_LDS_SLOTS 8
+#endif
+constexpr int LDS_SLOTS = ACS_LDS_SLOTS;
 
 struct ReqLds : ReqCtx {
   const ReqRes* col;  // this lane's LDS column
@@ -823,12 +839,18 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   return F;
 }
 
+ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h, uint32_t i) {
+  Filter F = request_filter(B, h);
+  if (!F.all && B.role_key && B.role_key[i] < B.role_rows) F.rrow[0] = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
+  return F;
+}
+
 ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
   const ReqHdr h = B.hdr[i];
   bool done;
   Decision d = early_decision(h, &done);
   if (done) return d;
-  return is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h));
+  return is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i));
 }
 
 // ------------------------------------------------------------------ whatIsAllowed
@@ -918,7 +940,7 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
   if (h.flags & RQ_HOST) {
     d.flags = OF_HOST_REQ;
   } else {
-    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h), bits, obl);
+    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
   return d;

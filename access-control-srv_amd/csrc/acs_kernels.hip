@@ -37,9 +37,9 @@ int fail(const std::string& msg) {
 
 constexpr int BLOCK = 256;
 
-// Sort key that makes a wave share its request class (entity column x required roles,
-// hence one candidate row) and action, so table-driven branches are wave-uniform:
-// [bucket:16 | action id:16].  Class ids come heaviest-first from the host (most
+// Sort key that makes a wave share its request class (one candidate row) and action — or,
+// with a role factor, its role key — so table-driven branches are wave-uniform:
+// [bucket:16 | action id or role key:16].  Class ids come heaviest-first from the host (most
 // candidate nodes), and unfiltered requests (PCOL_ALL) take bucket 0, so the longest
 // waves start first and the launch has no long tail.  Unfiltered requests group by
 // their first entity id.
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
   if (k >= B.n) return;
   const ReqHdr h = B.hdr[k];
   const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
-  uint32_t low = h.nact ? B.act[k].value : 0u, bucket = cls + 1;
+  uint32_t low = B.role_key ? B.role_key[k] : (h.nact ? B.act[k].value : 0u), bucket = cls + 1;
   if (cls >= B.cand_rows) {
     bucket = 0;
     for (uint32_t j = 0; j < h.nres; ++j) {
@@ -64,48 +64,51 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
   idx[k] = k;
 }
 
-// Candidate filter of a wave, built with every lane present before any lane diverges.
+// Candidate filter of a wave, built with every lane present before any lane diverges.  A
+// request's row is its class row, AND-ed with its role-factor row when the batch has one.
 // With an LDS row (`lds` = this wave's W-word region, W <= LDS_FILTER_WORDS) the filter is
-// the OR of the class rows of all the wave's active requests, however many classes the
-// wave spans.  With rows too long for LDS (large stores) it keeps up to 4 row pointers, or
-// — a wave of more classes — their ids in this wave's LDS list, OR-ed word by word.  An
-// unfiltered request (PCOL_ALL) disables filtering for its wave.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t* lds, uint32_t* list) {
+// the OR of the rows of all the wave's active requests, however many (class, role key)
+// pairs the wave spans.  With rows too long for LDS (large stores) it keeps up to 4 row
+// pointer pairs, or — a more mixed wave — the pairs in this wave's LDS list, OR-ed word by
+// word.  An unfiltered request (PCOL_ALL) disables filtering for its wave.
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds,
+                                     uint32_t* list) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   F.cand = B.cand;
+  F.rbits = B.role_bits;
+  F.nroles = B.role_key ? B.role_rows : 0u;
   F.W = B.cand_words;
   F.all = B.cand == nullptr;
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   if (lds && !F.all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
+  const uint32_t key = cls << 16 | (rk < F.nroles ? rk : 0xFFFFu);
   uint32_t n = 0;
   uint64_t pending = __ballot(valid);
   while (pending && !F.all) {
     const int leader = __builtin_ctzll(pending);
-    const uint32_t c = __builtin_amdgcn_readlane(cls, leader);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader), c = k >> 16, r = k & 0xFFFFu;
     if (c == PCOL_ALL || c >= B.cand_rows) {
       F.all = true;
       break;
     }
-    const uint32_t* r = B.cand + (size_t)c * W;
+    const uint32_t* row = B.cand + (size_t)c * W;
+    const uint32_t* rrow = r < F.nroles ? B.role_bits + (size_t)r * W : nullptr;
     if (lds) {
-      for (uint32_t w = lane; w < W; w += 64) lds[w] |= r[w];
+      for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
     } else {
-      if (lane == 0) list[n] = c;  // at most 64 distinct classes per wave
-      if (n == 0) {
-        F.row[0] = r;
-      } else if (n == 1) {
-        F.row[1] = r;
-      } else if (n == 2) {
-        F.row[2] = r;
-      } else if (n == 3) {
-        F.row[3] = r;
+      if (lane == 0) list[n] = k;  // at most 64 distinct (class, role key) pairs per wave
+      if (n < 4) {
+        if (n == 0) { F.row[0] = row; F.rrow[0] = rrow; }
+        else if (n == 1) { F.row[1] = row; F.rrow[1] = rrow; }
+        else if (n == 2) { F.row[2] = row; F.rrow[2] = rrow; }
+        else { F.row[3] = row; F.rrow[3] = rrow; }
       }
     }
     ++n;
-    pending &= ~__ballot(valid && cls == c);
+    pending &= ~__ballot(valid && key == k);
   }
   if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
   if (!F.all && lds) F.lds = lds;
@@ -142,7 +145,7 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
-#define ACS_K1_WAVES_PER_EU 1
+#define ACS_K1_WAVES_PER_EU 4  // measured: 4 waves/SIMD (VGPR <= 128) beats 3 (+12% c2, +13% c3), 5+ spill
 #endif
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
-  const Filter F = wave_filter(B, in && !done, request_pcol(h), wave_lds_row(B), wave_lds_list(B));
+  const Filter F = wave_filter(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu, wave_lds_row(B),
+                               wave_lds_list(B));
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
@@ -199,7 +203,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h), wave_lds_row(B), wave_lds_list(B));
+  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu, wave_lds_row(B),
+                               wave_lds_list(B));
   if (!in) return;
   uint32_t* my_bits = bits + (size_t)i * words;
   for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
@@ -385,6 +390,9 @@ static Batch to_batch(const acs_req_batch* b) {
   B.cand_wp = b->cand_wp;
   B.cand_wr = b->cand_wr;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
+  B.role_key = b->cand ? b->role_key : nullptr;
+  B.role_bits = b->role_rows_bits;
+  B.role_rows = b->role_key ? b->role_rows : 0u;
   return B;
 }
 
@@ -546,6 +554,10 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
     return -1;
   if (b->cand && D.up(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t),
                       (const void**)&D.d.cand, s))
+    return -1;
+  if (b->role_key && (D.up(b->role_key, n * sizeof(uint32_t), (const void**)&D.d.role_key, s) ||
+                      D.up(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
+                           (const void**)&D.d.role_rows_bits, s)))
     return -1;
   return 0;
 }

@@ -13,7 +13,8 @@
  *   whatIsAllowed(handle, batch) -> {bits, obl, oblN, out}   acs_what_is_allowed
  *   wordsPerRequest(handle), layoutSizes(), deviceCount(), lastError()
  * `batch` = {n, hdr, res, subj, act, roles, arena, rx, rxCols, rxRows,
- *            cand, candWords, candWp, candWr, candRows}: typed arrays / Buffers in the
+ *            cand, candWords, candWp, candWr, candRows[, roleKey, roleRowsBits, roleRows]}:
+ *            typed arrays / Buffers in the
  * layout of csrc/acs_layout.h (what acs_mi355x/encoder.py produces).
  */
 #define NAPI_VERSION 8
@@ -112,6 +113,13 @@ static int read_batch(napi_env env, napi_value obj, acs_req_batch* b) {
   if (prop_u32(env, obj, "candWords", &b->cand_words) || prop_u32(env, obj, "candWp", &b->cand_wp) ||
       prop_u32(env, obj, "candWr", &b->cand_wr) || prop_u32(env, obj, "candRows", &b->cand_rows))
     return -1;
+  /* optional role factor (large stores): roleKey [n] u32, roleRowsBits, roleRows */
+  if (prop_bytes(env, obj, "roleKey", &p, &len)) return -1;
+  b->role_key = (const uint32_t*)p;
+  if (prop_bytes(env, obj, "roleRowsBits", &p, &len)) return -1;
+  b->role_rows_bits = (const uint32_t*)p;
+  if (prop_u32(env, obj, "roleRows", &b->role_rows)) return -1;
+  if (!b->role_key) b->role_rows = 0;
   return 0;
 }
 

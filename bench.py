@@ -57,9 +57,9 @@ def _node_bytes(nodes):
 
 def scan_bytes(cs, batch, wave=64):
     """Table bytes the K1 waves visit, counted from the same candidate rows the kernel uses:
-    requests in coherence-sort order, 64 per wave, the union of the wave's class rows (an
-    unfiltered class: the whole table); a policy is visited only inside a visited set, a rule
-    only inside a visited policy.  Returns total bytes for the batch."""
+    requests in coherence-sort order, 64 per wave, the union of the wave's (class row AND
+    role-factor row) filters (an unfiltered class: the whole table); a policy is visited only
+    inside a visited set, a rule only inside a visited policy.  Returns total bytes."""
     from acs_mi355x import layout as L
     n = batch.n
     cand = batch.cand
@@ -67,10 +67,16 @@ def scan_bytes(cs, batch, wave=64):
     h = batch.hdr
     cls = (h["flags"] >> np.uint32(L.RQ_PCOL_SHIFT)).astype(np.int64)
     cls = np.where(cls >= R, R, cls)
-    low = np.where(h["nact"] > 0, batch.act["value"][0], 0).astype(np.int64) & 0xFFFF
+    rk_all = batch.role_key.astype(np.int64) if batch.role_key is not None else np.full(n, 0xFFFF, np.int64)
+    nrk = 0 if batch.role_bits is None else batch.role_bits.shape[0]
+    if batch.role_key is not None:
+        low = rk_all & 0xFFFF
+    else:
+        low = np.where(h["nact"] > 0, batch.act["value"][0], 0).astype(np.int64) & 0xFFFF
     bucket = np.where(cls >= R, 0, cls + 1)  # sort_keys_kernel: unfiltered first, then class ids
     order = np.argsort((bucket << 16) | low, kind="stable")
-    cw = cls[order]
+    pair = (cls << 16) | np.where(rk_all < nrk, rk_all, 0xFFFF)
+    pw = pair[order]
     ns, npol, nr = cs.n_sets, cs.n_pols, cs.n_rules
     bs, bp, br = _node_bytes(cs.sets), _node_bytes(cs.pols), _node_bytes(cs.rules)
     par_p = np.repeat(np.arange(ns), (cs.sets["child_end"] - cs.sets["child_begin"]).astype(np.int64))
@@ -83,11 +89,16 @@ def scan_bytes(cs, batch, wave=64):
     def union_bytes(key):
         if key in cache:
             return cache[key]
-        # K1 ORs every class row of the wave (in LDS, or word by word for long rows)
-        if any(c >= R for c in key):
+        # K1 ORs every (class & role) row of the wave (in LDS, or word by word for long rows)
+        if any((k >> 16) >= R for k in key):
             cache[key] = full
             return full
-        row = np.bitwise_or.reduce(cand[list(key)], axis=0)
+        row = np.zeros(cand.shape[1], np.uint32)
+        for k in key:
+            x = cand[k >> 16]
+            if (k & 0xFFFF) < nrk:
+                x = x & batch.role_bits[k & 0xFFFF]
+            row |= x
         bits = np.unpackbits(row.view(np.uint8), bitorder="little").astype(bool)
         s = bits[:ns]
         p = bits[32 * ws:32 * ws + npol] & s[par_p]
@@ -98,7 +109,7 @@ def scan_bytes(cs, batch, wave=64):
 
     total = 0
     for w0 in range(0, n, wave):
-        total += union_bytes(tuple(np.unique(cw[w0:w0 + wave]).tolist()))
+        total += union_bytes(tuple(np.unique(pw[w0:w0 + wave]).tolist()))
     return total, full
 
 

@@ -59,6 +59,13 @@ typedef struct {
   const uint32_t* cand;
   uint32_t cand_words, cand_wp, cand_wr;
   uint32_t cand_rows;
+  /* Optional role factor (large stores, where class rows keyed by roles would not fit):
+   * [role_rows][cand_words] bitsets of the nodes a request with that role-association set
+   * can reach (checkSubjectMatches, accessController.ts:793-823), AND-ed with the class
+   * row; role_key[n] picks the row per request (>= role_rows: unfiltered).  NULL = none. */
+  const uint32_t* role_key;
+  const uint32_t* role_rows_bits;
+  uint32_t role_rows;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */

@@ -54,6 +54,9 @@ static Batch host_batch(const acs_req_batch* b) {
   B.cand_wp = b->cand_wp;
   B.cand_wr = b->cand_wr;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
+  B.role_key = b->cand ? b->role_key : nullptr;
+  B.role_bits = b->role_rows_bits;
+  B.role_rows = b->role_key ? b->role_rows : 0u;
   return B;
 }
 

@@ -139,6 +139,27 @@ def test_large_store_class_list_gpu():
     assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
 
 
+@pytest.mark.parametrize("kind", ["c3", "c5_small"])
+def test_role_factor_gpu(kind, monkeypatch):
+    """Class rows keyed by (entity, action) AND-ed with the role factor (the large-store
+    filter): in the LDS union (c3, W <= 1024) and in the row-pointer / LDS-list modes
+    (c5_small, W > 1024) the records equal the CPU build's."""
+    from acs_mi355x import candidates
+    monkeypatch.setattr(candidates, "FORCE_LEVEL", "entity+action")
+    doc = synth.c3_store() if kind == "c3" else synth.c5_store(n_sets=60)
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 40_000, "c3", tree=synth.OrgTree(fanout=4, depth=5))
+    assert sb.batch.role_key is not None
+    t = gpu_tables(cs)
+    dec = t.is_allowed(sb.batch)
+    db = DeviceBatch(sb.batch, 0)
+    dev = decisions_from_tensor(is_allowed_device(t, db))
+    t.close()
+    ref = host_core.is_allowed(cs, sb.batch)
+    assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
+    assert np.array_equal(dev.view(np.uint64), ref.view(np.uint64))
+
+
 def test_what_is_allowed_c4_gpu():
     doc, cs, sb = _synth("c3", 8_000)
     t = gpu_tables(cs)
