@@ -289,6 +289,9 @@ class _Builder:
         else:
             rec["_cand"] = [self.rx_row(a.get("value", MISSING)) for a in res
                             if strict_eq(a.get("id", MISSING), U("entity"))]
+        if len(res) > 0 and not any(strict_eq(a.get("id", MISSING), U("property")) or
+                                    strict_eq(a.get("id", MISSING), U("operation")) for a in res):
+            flags |= L.TF_RES_ENT_ONLY
         if isinstance(last_prop, str):
             flags |= L.TF_LASTPROP_STR
             if "#" in last_prop:

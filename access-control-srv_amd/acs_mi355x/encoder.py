@@ -161,6 +161,10 @@ class Encoder:
             res_rows.append([v, kind])
         if n_ent > 1:
             flags |= L.RQ_MULTI_ENT
+        # the only entity attribute's slot for the kernel's entity-only fast path
+        ent_slots = [j for j, (_, k) in enumerate(res_rows) if k & L.K_ENT]
+        ent_field = 0 if not ent_slots else (ent_slots[0] + 1 if len(ent_slots) == 1 and ent_slots[0] < 6 else 7)
+        flags |= ent_field << L.RQ_ENT_SHIFT
 
         ctx_res = []
         if not ctx_empty:

@@ -369,7 +369,7 @@ def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree
     actp["id"][0], actp["value"][0] = V["urn_action"], V["act"][act]
     roles[0] = V["role"][rol]
 
-    flags = np.full(n, L.RQ_RA_TRUTHY | L.RQ_HRS_ITERABLE, np.uint32)
+    flags = np.full(n, L.RQ_RA_TRUTHY | L.RQ_HRS_ITERABLE | (1 << L.RQ_ENT_SHIFT), np.uint32)  # entity at slot 0
     flags |= np.where(nprops > 0, L.RQ_ANY_PROP, 0).astype(np.uint32)
     flags |= np.where(act == 2, L.RQ_ACT_CREATE, 0).astype(np.uint32)
     flags |= np.where((act == 0) | (act == 1) | (act == 3), L.RQ_ACT_RMD, 0).astype(np.uint32)

@@ -293,8 +293,17 @@ constexpr int LDS_SLOTS = ACS_LDS_SLOTS;
 struct ReqLds : ReqCtx {
   const ReqRes* col;  // this lane's LDS column
   uint32_t stride;
+  uint32_t e0_val, e0_col;  // the request's only entity attribute (RQ_ENT_SHIFT field 1..6)
   ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st)
-      : ReqCtx(t, b, idx, hd), col(c), stride(st) {}
+      : ReqCtx(t, b, idx, hd), col(c), stride(st) {
+    const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
+    e0_val = e0_col = 0;
+    if (e >= 1 && e <= 6) {
+      const ReqRes q = res((int)e - 1);
+      e0_val = q.value;
+      e0_col = q.col;
+    }
+  }
   ACS_FN ReqRes res(int j) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const ReqRes lds_res;  // ds_read, not flat
@@ -308,7 +317,16 @@ struct ReqLds : ReqCtx {
 
 // Resource attributes read from HBM on every use (host build of the core).
 struct ReqMem : ReqCtx {
-  ACS_FN ReqMem(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : ReqCtx(t, b, idx, hd) {}
+  uint32_t e0_val, e0_col;
+  ACS_FN ReqMem(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : ReqCtx(t, b, idx, hd) {
+    const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
+    e0_val = e0_col = 0;
+    if (e >= 1 && e <= 6) {
+      const ReqRes q = res((int)e - 1);
+      e0_val = q.value;
+      e0_col = q.col;
+    }
+  }
   ACS_FN ReqRes res(int j) const { return B.res[(size_t)j * B.n + i]; }
 };
 
@@ -349,6 +367,34 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
                           bool rpe, OblLog* obl) {
   if (t.tflags & TF_RES_EMPTY) return 1;
   const RuleResAttr* ra = R.T.rres + t.res_off;
+  const uint32_t ent = (R.h.flags >> RQ_ENT_SHIFT) & 7u;
+#if defined(ACS_NO_ENT_FASTPATH)  // A/B builds only
+  if (false) {
+#else
+  if ((t.tflags & TF_RES_ENT_ONLY) && ent != 7u && j0 == 0 && j1 == (int)R.h.nres) {
+#endif
+    // Target without property / operation attributes and a request with at most one entity
+    // attribute: every property / mask / skipDenyRule branch needs a rule property, so the
+    // ordered double loop reduces to entityMatch over the rule's entity attributes (exact:
+    // sticky equality; RegExp: reset / hit in order, throws first-come) — same result.
+    if (ent == 0) return 0;
+    bool em = false;
+    for (uint32_t k = 0; k < t.res_n; ++k) {
+      const RuleResAttr r = k < ACS_RA_CACHE ? load_words(R.T, ra + k) : load_words(R.T, ra + wave_uniform(k));
+      if (!(r.kind & K_ENT)) continue;
+      if (!regex) {
+        if (R.e0_val == r.value) em = true;
+      } else {
+        const uint8_t c = R.rx(R.e0_col, r.row);
+        if (c & RX_THROW_TYPE) return -(tri)ERR_TYPE;
+        if (c & RX_THROW_SYNTAX) return -(tri)ERR_REGEX_SYNTAX;
+        if (c & RX_HOST) return -(tri)ERR_REGEX_HOST;
+        if (c & RX_RESET) em = false;
+        if (c & RX_HIT) em = true;
+      }
+    }
+    return em ? 1 : 0;
+  }
   bool em = false, pm = false, rp = false, om = false, skip_deny = true;
   int ent_j = 0;
   uint32_t ent_val = 0;

@@ -69,6 +69,8 @@ enum TargetFlags : uint32_t {
   TF_HAS_SUBJECTS = 1u << 7, // subjects.length > 0 (policySubjectMatch gate)
   TF_LASTPROP_STR = 1u << 8, // last property value is a string
   TF_LASTPROP_HASH = 1u << 9,// ... containing '#'
+  TF_RES_ENT_ONLY = 1u << 10,// non-empty resources without property / operation attrs:
+                             // resourceAttributesMatch reduces to its entity test
 };
 
 // One set / policy / rule with its target inline (64 B: a single scalar load per node).
@@ -126,6 +128,7 @@ enum ReqFlags : uint32_t {
   RQ_ACT_CREATE = 1u << 9,   // actions[0] is {actionID, create}
   RQ_ACT_RMD = 1u << 10,     // actions[0] is {actionID, read|modify|delete}
   RQ_ACL_SHIFT = 11,         // 2 bits: verifyACL request-loop outcome
+  RQ_ENT_SHIFT = 13,         // 3 bits: 0 no entity attr, 1+j the only one at slot j (j < 6), 7 other
   RQ_PCOL_SHIFT = 16,        // 16 bits: candidate column of the request's entity attrs
 };
 constexpr uint32_t PCOL_ALL = 0xFFFF;  // several distinct entity columns / unfiltered request
