@@ -359,7 +359,7 @@ ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
 
 // ------------------------------------------------------------------ resourceAttributesMatch
 #ifndef ACS_RA_CACHE
-#define ACS_RA_CACHE 4  // rule resource attributes held in registers per resource_match call
+#define ACS_RA_CACHE 2  // rule resource attributes held in registers per resource_match call (A/B: 2 >= 4 > 0)
 #endif
 // Request attrs [j0, j1) with requestPropertiesExist = rpe.  wia: 'whatIsAllowed' op.
 template <class RQ>

@@ -7,11 +7,12 @@ OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 CFG=${CFG:-c2}
 EXTRA=${EXTRA:-}
+KERNEL=${KERNEL:-is_allowed_kernel}
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 run() {
   local name=$1; shift
   echo "== pmc $name ($(date +%T))"
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "is_allowed_kernel" -d $OUT/$name -o pmc \
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$KERNEL" -d $OUT/$name -o pmc \
     --output-format csv -- python3 bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-pcie $EXTRA \
     > $OUT/$name.log 2>&1
   local rc=$?
@@ -22,5 +23,5 @@ run g1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_
 run g2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VMEM_WR
 run g3 FETCH_SIZE
 run g4 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum
-python3 tools/pmc_traffic.py $OUT $CFG $OUT/traffic.json || true
+python3 tools/pmc_traffic.py $OUT $CFG $OUT/traffic.json $KERNEL || true
 echo "== pmc done"
