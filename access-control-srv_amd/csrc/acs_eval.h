@@ -144,11 +144,11 @@ struct Batch {
 struct Filter {
   const uint32_t* row[4];  // class rows (nullptr: unused)
   const uint32_t* rrow[4]; // role-factor rows AND-ed with row[k] (nullptr: none)
-  const uint32_t* lds;     // GPU: the wave's OR of all its (class & role) rows, in LDS
+  const uint32_t* lds;     // GPU: the wave's OR of all its (class & role) rows, words [0, lds_n), in LDS
   const uint32_t* list;    // GPU, rows too long for LDS: the wave's > 4 (class, role key) pairs, in LDS
   const uint32_t* cand;    // ... and the row tables they index ([C][W], [role_rows][W])
   const uint32_t* rbits;
-  uint32_t nlist, W, nroles;
+  uint32_t nlist, W, nroles, lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   bool all;                // no filtering
   ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
@@ -160,7 +160,7 @@ struct Filter {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-    if (lds) return wave_uniform(((lds_u32*)lds)[w]);
+    if (lds && w < lds_n) return wave_uniform(((lds_u32*)lds)[w]);
     if (list) {  // OR of every (class & role) row of the wave, word by word (large stores, mixed waves)
       uint32_t x = 0;
       for (uint32_t k = 0; k < nlist; ++k) {

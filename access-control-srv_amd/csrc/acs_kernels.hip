@@ -64,6 +64,13 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
   idx[k] = k;
 }
 
+// Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS; for longer rows
+// (large stores) a LDS_PREFIX_WORDS union prefix (sets + policies at c5) and a 64-entry
+// (class, role key) list for the rest — 8 KB per 256-thread block, so the block's LDS
+// (32 KB attribute staging + filter) still allows 4 blocks per CU.
+constexpr uint32_t LDS_FILTER_WORDS = 1024;
+constexpr uint32_t LDS_PREFIX_WORDS = 448;
+constexpr uint32_t LDS_LIST_WORDS = 64;
 // Candidate filter of a wave, built with every lane present before any lane diverges.  A
 // request's row is its class row, AND-ed with its role-factor row when the batch has one.
 // With an LDS row (`lds` = this wave's W-word region, W <= LDS_FILTER_WORDS) the filter is
@@ -82,8 +89,11 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   F.W = B.cand_words;
   F.all = B.cand == nullptr;
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
+  // the LDS union covers the whole row, or (long rows) the set + policy prefix
+  const uint32_t LW = W <= LDS_FILTER_WORDS ? W : (W < LDS_PREFIX_WORDS ? W : LDS_PREFIX_WORDS);
+  F.lds_n = LW;
   if (lds && !F.all)
-    for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
+    for (uint32_t w = lane; w < LW; w += 64) lds[w] = 0u;
   const uint32_t key = cls << 16 | (rk < F.nroles ? rk : 0xFFFFu);
   uint32_t n = 0;
   uint64_t pending = __ballot(valid);
@@ -96,9 +106,9 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
     }
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t* rrow = r < F.nroles ? B.role_bits + (size_t)r * W : nullptr;
-    if (lds) {
-      for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
-    } else {
+    if (lds)
+      for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
+    if (list) {
       if (lane == 0) list[n] = k;  // at most 64 distinct (class, role key) pairs per wave
       if (n < 4) {
         if (n == 0) { F.row[0] = row; F.rrow[0] = rrow; }
@@ -112,27 +122,27 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   }
   if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
   if (!F.all && lds) F.lds = lds;
-  if (!F.all && !lds && n > 4) {
+  if (!F.all && list && n > 4) {
     F.list = list;
     F.nlist = n;
   }
   return F;
 }
 
-// Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS, else a 64-entry
-// class list.
-constexpr uint32_t LDS_FILTER_WORDS = 1024;
-constexpr uint32_t LDS_LIST_WORDS = 64;
 extern __shared__ uint32_t acs_dyn_lds[];
 
+__device__ inline uint32_t lds_wave_words(const Batch& B) {
+  return B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_PREFIX_WORDS + LDS_LIST_WORDS;
+}
+
 __device__ inline uint32_t* wave_lds_row(const Batch& B) {
-  if (!B.cand || B.cand_words > LDS_FILTER_WORDS) return nullptr;
-  return acs_dyn_lds + (threadIdx.x >> 6) * B.cand_words;
+  if (!B.cand) return nullptr;
+  return acs_dyn_lds + (threadIdx.x >> 6) * lds_wave_words(B);
 }
 
 __device__ inline uint32_t* wave_lds_list(const Batch& B) {
   if (!B.cand || B.cand_words <= LDS_FILTER_WORDS) return nullptr;
-  return acs_dyn_lds + (threadIdx.x >> 6) * LDS_LIST_WORDS;
+  return acs_dyn_lds + (threadIdx.x >> 6) * lds_wave_words(B) + LDS_PREFIX_WORDS;
 }
 
 __device__ inline uint32_t request_pcol(const ReqHdr& h) {
@@ -239,7 +249,7 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 size_t filter_lds_bytes(const Batch& B) {
   if (!B.cand) return 0;
-  return (size_t)(BLOCK / 64) * (B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_LIST_WORDS) * 4;
+  return (size_t)(BLOCK / 64) * (B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_PREFIX_WORDS + LDS_LIST_WORDS) * 4;
 }
 
 }  // namespace
