@@ -902,10 +902,12 @@ ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
 // ------------------------------------------------------------------ whatIsAllowed
 // bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
 template <class RQ>
-ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, OblLog& obl) {
+// bits: word w of this request's bitset lives at bits[w * stride] (1: a row; the GPU writes
+// a column of a word-major [words][n] buffer so a wave's stores coalesce)
+ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, size_t stride, OblLog& obl) {
   const Tables& T = R.T;
   Decision out{};
-  auto setbit = [&](uint32_t b) { bits[b >> 5] |= 1u << (b & 31); };
+  auto setbit = [&](uint32_t b) { bits[(size_t)(b >> 5) * stride] |= 1u << (b & 31); };
   const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;
@@ -986,7 +988,7 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
   if (h.flags & RQ_HOST) {
     d.flags = OF_HOST_REQ;
   } else {
-    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits, obl);
+    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits, 1, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
   return d;

@@ -200,9 +200,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #endif
 }
 
-// K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane.
+// K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
+// order k).  The bitset goes to a word-major scratch buffer tmp[words][n] at column k, so a
+// wave's zeroing and bit updates are coalesced 256-B accesses; bitset_transpose_kernel
+// then writes each column to its request's row of the [n][words] output.
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
-                                                                uint32_t words, uint32_t* __restrict__ bits,
+                                                                uint32_t words, uint32_t* __restrict__ tmp,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
@@ -213,23 +216,48 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu, wave_lds_row(B),
-                               wave_lds_list(B));
+  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                               wave_lds_row(B), wave_lds_list(B));
   if (!in) return;
-  uint32_t* my_bits = bits + (size_t)i * words;
-  for (uint32_t w = 0; w < words; ++w) my_bits[w] = 0;
+  uint32_t* col = tmp + k;
+  for (uint32_t w = 0; w < words; ++w) col[(size_t)w * B.n] = 0;
   OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
   Decision d{};
   if (host) {
     d.flags = OF_HOST_REQ;
   } else {
-    ReqRes* col = stage + threadIdx.x;
+    ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    d = what_is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F, my_bits, log);
+    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, col, B.n, log);
   }
   obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
   out[i] = d;
+}
+
+// tmp[words][n] (column k = the k-th request in perm order) -> bits[perm[k]][words].  A
+// 256-thread block moves a 64-column x 32-word tile through LDS: coalesced 256-B reads of
+// tmp rows, 128-B contiguous writes per output row.
+constexpr uint32_t TP_COLS = 64, TP_WORDS = 32;
+__global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t* __restrict__ tmp, uint32_t n,
+                                                                 uint32_t words, const uint32_t* __restrict__ perm,
+                                                                 uint32_t* __restrict__ bits) {
+  __shared__ uint32_t tile[TP_WORDS][TP_COLS + 1];
+  const uint32_t k0 = blockIdx.x * TP_COLS, w0 = blockIdx.y * TP_WORDS;
+  const uint32_t t = threadIdx.x, c = t & 63u;
+  for (uint32_t r = t >> 6; r < TP_WORDS; r += BLOCK / 64) {
+    const uint32_t w = w0 + r, k = k0 + c;
+    tile[r][c] = (w < words && k < n) ? tmp[(size_t)w * n + k] : 0u;
+  }
+  __syncthreads();
+  const uint32_t row = t >> 2, part = (t & 3u) * 8u, k = k0 + row;
+  if (k >= n) return;
+  uint32_t* dst = bits + (size_t)(perm ? perm[k] : k) * words;
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t w = w0 + part + q;
+    if (w < words) dst[w] = tile[part + q][row];
+  }
 }
 
 // Rule-sharded isAllowed (C1): local decisions -> 64-bit MAX-reducible keys, and back.
@@ -270,6 +298,9 @@ struct acs_tables {
   // sort workspace, grown on demand: keys/idx double buffers + hipcub temp storage
   void* ws = nullptr;
   size_t ws_bytes = 0;
+  // K2 word-major bitset scratch ([words][n] u32), grown on demand
+  void* wbuf = nullptr;
+  size_t wbuf_bytes = 0;
   // host-buffer entry points (internal stream, events, workspace) may be called from
   // several host threads at once (e.g. the N-API addon's libuv pool): one at a time
   std::mutex mu;
@@ -373,6 +404,7 @@ void acs_free(acs_tables* t) {
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
   if (t->ws) (void)hipFree(t->ws);
+  if (t->wbuf) (void)hipFree(t->wbuf);
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
@@ -494,11 +526,25 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   const uint32_t* perm = nullptr;
   if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
+  const uint32_t words = acs_wia_words_per_request(t);
+  const size_t need = (size_t)words * b->n * sizeof(uint32_t);
+  if (need > t->wbuf_bytes) {
+    if (t->wbuf) HIP_OK(hipFree(t->wbuf));
+    t->wbuf = nullptr;
+    t->wbuf_bytes = 0;
+    HIP_OK(hipMalloc(&t->wbuf, need ? need : 16));
+    t->wbuf_bytes = need;
+  }
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, acs_wia_words_per_request(t),
-                     bits, obl, obl_n, (Decision*)out);
+  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, words,
+                     (uint32_t*)t->wbuf, obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
+  if (words) {
+    hipLaunchKernelGGL(bitset_transpose_kernel, dim3((b->n + TP_COLS - 1) / TP_COLS, (words + TP_WORDS - 1) / TP_WORDS),
+                       dim3(BLOCK), 0, s, (const uint32_t*)t->wbuf, b->n, words, perm, bits);
+    HIP_OK(hipGetLastError());
+  }
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
     t->launches++;
