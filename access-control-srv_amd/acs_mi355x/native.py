@@ -13,7 +13,8 @@ import numpy as np
 from . import layout as L
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG, "lib", "libacs_mi355x.so")
+# ACS_MI355X_LIB: an alternative build of the same library (A/B experiments only)
+LIB_PATH = os.environ.get("ACS_MI355X_LIB") or os.path.join(PKG, "lib", "libacs_mi355x.so")
 
 
 class ReqBatchC(C.Structure):

@@ -113,8 +113,17 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
 #endif
   uint32_t v[NW];
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_NO_VLR)
+  // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
+  // the wave-uniform record moves to SGPRs: its fields feed scalar compares and branches and
+  // free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself proves
+  // the address uniform it emits s_load; nothing here forces a scalar load.
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = __builtin_amdgcn_readfirstlane(w[k]);
+#else
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];
+#endif
   X out;
   __builtin_memcpy(&out, v, sizeof(X));
   return out;
