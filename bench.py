@@ -158,10 +158,14 @@ def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
     idx = np.random.default_rng(1234).permutation(sb.batch.n)
     chunk = {"c2": 20_000, "c3": 250}.get(kind, 32)  # c3/c5 requests carry HR trees of up to 21,845 orgs
     done = busy = mism = unsup = host = 0
-    while busy < seconds and done < len(idx):
+    wall0 = time.perf_counter()
+    # bounded: ~`seconds` of oracle evaluation, and at most 3x that in wall time (decoding
+    # c3/c5 requests to JSON — HR trees of up to 21,845 orgs — costs more than evaluating)
+    while busy < seconds and done < len(idx) and time.perf_counter() - wall0 < 3 * seconds + 10:
         part = idx[done:done + chunk]
         out, sec = co.raw([sb.decode(int(i)) for i in part], threads)
         busy += sec
+        log(f"cpu baseline: {done + len(part)} requests, {busy:.1f}s evaluation")
         for i, r in zip(part, out):
             want = acs_oracle_c.outcome(r)
             got = gpu_outcome(cs, gpu_dec[i])
@@ -176,7 +180,7 @@ def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
     return {"value": done / busy, "unit": "decisions/s", "cores": threads, "kind": "port",
             "sample": f"{done} random requests of the same {kind} batch through oracle/acs_oracle.cpp (C++17 "
                       f"restatement of the reference's per-request serial algorithm, std::thread x {threads}), "
-                      f"{busy:.1f}s of evaluation wall time"}, \
+                      f"{busy:.1f}s of evaluation wall time (requests decoded and parsed beforehand)"}, \
         {"oracle_sample": done, "mismatches": mism, "oracle_unsupported": unsup, "gpu_host_path": host}
 
 
