@@ -44,6 +44,20 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 _T0 = time.time()
 
 
+REHEARSAL = False
+
+
+def allreduce_max(t):
+    """torch.distributed all-reduce MAX in place (RCCL on device tensors; gloo rehearsal via host)."""
+    import torch.distributed as tdist
+    if REHEARSAL:
+        c = t.cpu()
+        tdist.all_reduce(c, op=tdist.ReduceOp.MAX)
+        t.copy_(c)
+    else:
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+
+
 def log(msg):
     """Setup progress on stderr (large configs take minutes to compile / encode)."""
     print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
@@ -218,7 +232,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     kern_ms = float(np.mean(tables.kernel_times(args.steps)))
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        allreduce_max(t)
         elapsed, kern_ms = float(t[0]), float(t[1])
     if rank == 0:
         bits = bufs[0].cpu().numpy().view(np.uint32)
@@ -289,10 +303,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    global REHEARSAL
+    # ACS_BENCH_REHEARSAL=1: several ranks on ONE GPU over gloo (collectives through host
+    # copies) — exercises the multi-rank code paths on a 1-GPU box; its numbers are not a
+    # measurement.  Real runs: one rank per GPU over RCCL ("nccl").
+    REHEARSAL = dist and os.environ.get("ACS_BENCH_REHEARSAL") == "1"
+    if REHEARSAL:
+        local = 0
     if dist:
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if REHEARSAL:
+            tdist.init_process_group("gloo")
+        else:
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -338,7 +362,7 @@ def main():
         is_allowed_device(tables, db, local_out, stream)
         shard.keys_device(tables, local_out, sbase, keys, stream)
         if dist:
-            tdist.all_reduce(keys, op=tdist.ReduceOp.MAX)  # C1: RCCL over xGMI, 8 B per request
+            allreduce_max(keys)  # C1: RCCL over xGMI, 8 B per request
         shard.decode_device(tables.lib, keys, out, stream)
 
     for _ in range(args.warmup):
@@ -361,7 +385,7 @@ def main():
     kern_ms = float(np.mean(tables.kernel_times(args.steps)))       # K1 alone, library events
     if dist:
         t = torch.tensor([elapsed, kern_ms, step_ms], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        allreduce_max(t)
         elapsed, kern_ms, step_ms = float(t[0]), float(t[1]), float(t[2])
 
     log("timed steps done")
@@ -421,6 +445,8 @@ def main():
             line["pcie_inclusive"] = pcie
         if shard_check:
             line["rule_shard"] = shard_check
+        if REHEARSAL:
+            line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:
             log("CPU baseline (C++ oracle)")
             cb, par = cpu_baseline(kind, doc, sb, dec, cs, args.cpu_seconds)
