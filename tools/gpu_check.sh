@@ -26,6 +26,10 @@ for s in $STEPS; do
     quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
+    abtest) for v in ${VARIANTS:-scalar_tables}; do
+          ACS_MI355X_LIB=access-control-srv_amd/lib/variants/$v.so step "pytest_gpu_$v" 600 \
+            python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+        done ;;
     ab) for v in ${VARIANTS:-scalar_tables}; do
           step "bench_$v" 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie \
             --lib access-control-srv_amd/lib/variants/$v.so
