@@ -17,9 +17,10 @@ Evaluation goes through the C ABI only (``native.Tables`` on a GPU).  The
 policy store is compiled into an immutable table image on first use after a
 mutation; ``*_batch`` methods evaluate many requests in one launch (the
 micro-batch of SURVEY §8(b)).  Requests the GPU path reports to the host
-(subject token I/O, JS ``condition``, non-exact RegExp, obligation-log overflow)
-go to ``host_evaluator(op, request)`` when one is given, else raise
-``HostPathRequired``.  A request the reference would reject (its promise
+(subject token I/O, JS ``condition``, non-exact RegExp) go to ``host_evaluator(op, request)`` when one is given, else raise
+``HostPathRequired``.  whatIsAllowed requests with more than OBL_MAX maskedProperty
+pushes stay on the GPU: an obligation-only pass re-runs them with a longer log
+(``Tables.resolve_overflow``).  A request the reference would reject (its promise
 throws) raises ``EvaluationError`` with the JS error kind.
 """
 from __future__ import annotations
@@ -217,11 +218,13 @@ class AccessController:
         self._ensure()
         b = self._encoder.encode(requests)
         bits, obl, obl_n, dec = self._tables.what_is_allowed(b)
+        long_logs = self._tables.resolve_overflow(b, dec)  # > OBL_MAX pushes: obligation-only GPU pass
         self.stats["requests"] += len(requests)
         out = []
         for i, req in enumerate(requests):
             try:
-                out.append(results.reverse_query(self._cs, b.overlay, bits[i], obl[i][:obl_n[i]], dec[i],
+                log = long_logs[i] if i in long_logs else obl[i][:obl_n[i]]
+                out.append(results.reverse_query(self._cs, b.overlay, bits[i], log, dec[i],
                                                  b.host_reasons.get(i)))
             except HostPathRequired as e:
                 try:

@@ -63,5 +63,44 @@ def what_is_allowed_device(tables, db: DeviceBatch, bufs=None, stream=None):
     return bufs
 
 
+def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int = 1024, stream=None):
+    """Obligation-only passes for the requests whose K2 log overflowed (record flag
+    OF_OBL_OVERFLOW in ``bufs[3]``): ``cap`` entries each, then the still-truncated ones once
+    more at their exact count.  Returns [(idx, cap, obl [m][cap][2], obl_n [m])] per pass (int32
+    tensors; later passes supersede earlier ones).  Syncs the stream to size each pass."""
+    st = stream or torch.cuda.current_stream(db.dev)
+    with torch.cuda.stream(st):
+        flags = bufs[3][:, 2]
+        idx = torch.nonzero(flags & L.OF_OBL_OVERFLOW).flatten()
+        # request-class order, as K2's coherence sort: a wave then shares its candidate row
+        cls = (db.t["hdr"].view(torch.int32).view(-1, 4)[idx, 0] >> L.RQ_PCOL_SHIFT) & 0xFFFF
+        idx = idx[torch.sort(cls, stable=True).indices].to(torch.int32)
+        passes = []
+        while idx.numel():
+            m = idx.numel()
+            obl = torch.empty((m, cap, 2), dtype=torch.int32, device=db.dev)
+            obl_n = torch.empty((m,), dtype=torch.int32, device=db.dev)
+            rc = tables.lib.acs_what_is_allowed_obl_device(tables.h, C.byref(db.struct), idx.data_ptr(), m, cap,
+                                                           obl.data_ptr(), obl_n.data_ptr(), C.c_void_p(st.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"acs_what_is_allowed_obl_device: {last_error(tables.lib)}")
+            passes.append((idx, cap, obl, obl_n))
+            more = obl_n > cap
+            if not bool(more.any()):
+                break
+            idx, cap = idx[more], int(obl_n[more].max())
+    return passes
+
+
+def overflow_logs(passes) -> dict:
+    """{request index: [k][2] uint32 pairs} from resolve_overflow_device's passes."""
+    logs = {}
+    for idx, cap, obl, obl_n in passes:
+        idx, obl, obl_n = idx.cpu().numpy(), obl.cpu().numpy().view(np.uint32), obl_n.cpu().numpy()
+        for k in np.flatnonzero(obl_n <= cap):
+            logs[int(idx[k])] = obl[k, :obl_n[k]]
+    return logs
+
+
 def decisions_from_tensor(out: torch.Tensor) -> np.ndarray:
     return out.cpu().numpy().reshape(-1).view(L.DECISION_DT)

@@ -29,7 +29,8 @@ class ReqBatchC(C.Structure):
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
            "acs_what_is_allowed", "acs_what_is_allowed_device", "acs_last_kernel_ms", "acs_last_error",
            "acs_layout_sizes", "acs_device_count", "acs_set_option", "acs_kernel_times",
-           "acs_shard_keys_device", "acs_shard_decode_device"]
+           "acs_shard_keys_device", "acs_shard_decode_device", "acs_what_is_allowed_obl",
+           "acs_what_is_allowed_obl_device"]
 
 
 class ShardC(C.Structure):
@@ -49,6 +50,8 @@ def _declare(lib):
     lib.acs_wia_words_per_request.restype = u32
     lib.acs_what_is_allowed.argtypes = [vp, pb, vp, vp, vp, vp]
     lib.acs_what_is_allowed_device.argtypes = [vp, pb, vp, vp, vp, vp, vp]
+    lib.acs_what_is_allowed_obl.argtypes = [vp, pb, vp, C.c_size_t, u32, vp, vp]
+    lib.acs_what_is_allowed_obl_device.argtypes = [vp, pb, vp, C.c_size_t, u32, vp, vp, vp]
     lib.acs_last_kernel_ms.argtypes = [vp]
     lib.acs_last_kernel_ms.restype = C.c_float
     lib.acs_last_error.restype = C.c_char_p
@@ -109,6 +112,27 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
     return s
 
 
+OVERFLOW_CAP = 1024  # first obligation-only pass: log entries per overflowed request
+
+
+def resolve_overflow(tables, batch, out, cap: int = OVERFLOW_CAP) -> dict:
+    """Full maskedProperty logs of the requests whose K2 log overflowed (OF_OBL_OVERFLOW):
+    {request index: [k][2] pairs}, from the obligation-only pass (``cap`` entries first, then
+    each still-truncated request once more at its exact count).  Clears the flag in ``out``."""
+    idx = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) != 0).astype(np.uint32)
+    logs = {}
+    while len(idx):
+        obl, obl_n = tables.what_is_allowed_obl(batch, idx, cap)
+        done = obl_n <= cap
+        for k in np.flatnonzero(done):
+            logs[int(idx[k])] = obl[k, :obl_n[k]].copy()
+        idx, cap = idx[~done], (int(obl_n[~done].max()) if (~done).any() else cap)
+    if logs:
+        flags = out["flags"]
+        flags[np.fromiter(logs, np.int64, len(logs))] &= np.uint8(~L.OF_OBL_OVERFLOW & 0xFF)
+    return logs
+
+
 class Tables:
     """Device-resident compiled store on one GPU (wraps an acs_tables handle)."""
 
@@ -153,6 +177,24 @@ class Tables:
             if rc != 0:
                 raise RuntimeError(f"acs_what_is_allowed: {last_error(self.lib)}")
         return bits, obl, obl_n, out
+
+    def what_is_allowed_obl(self, batch, idx, cap: int):
+        """Obligation-only pass over requests ``idx`` of ``batch`` with a ``cap``-entry log each:
+        (obl [m][cap][2], obl_n [m] = total pushes per request)."""
+        idx = np.ascontiguousarray(idx, np.uint32)
+        m = len(idx)
+        obl = np.zeros((m, cap, 2), np.uint32)
+        obl_n = np.zeros(m, np.uint32)
+        if m:
+            s = batch_struct(batch)
+            rc = self.lib.acs_what_is_allowed_obl(self.h, C.byref(s), idx.ctypes.data, m, cap, obl.ctypes.data,
+                                                  obl_n.ctypes.data)
+            if rc != 0:
+                raise RuntimeError(f"acs_what_is_allowed_obl: {last_error(self.lib)}")
+        return obl, obl_n
+
+    def resolve_overflow(self, batch, out, cap: int = OVERFLOW_CAP) -> dict:
+        return resolve_overflow(self, batch, out, cap)
 
     def set_sort(self, enable: bool):
         if self.lib.acs_set_option(self.h, 1, int(bool(enable))) != 0:

@@ -233,9 +233,11 @@ struct Fold {  // streaming decide(): first X else last / first element
 };
 
 struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
-  uint32_t* out;  // [OBL_MAX][2] or nullptr
-  uint32_t n;
-  bool overflow;
+  uint32_t* out;  // [cap][2] or nullptr
+  uint32_t n;     // entries written (<= cap)
+  bool overflow;  // a push found the log full
+  uint32_t cap = OBL_MAX;
+  uint32_t total = 0;  // every push, written or not (sizes the overflow pass)
 };
 
 // ------------------------------------------------------------------ request views
@@ -482,7 +484,8 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
           no_hash = false;
         }
         if (!no_hash && obl) {
-          if (obl->n < (uint32_t)OBL_MAX) {
+          obl->total++;
+          if (obl->n < obl->cap) {
             if (obl->out) {
               obl->out[2 * obl->n] = ent_val;
               obl->out[2 * obl->n + 1] = mask;
@@ -916,7 +919,9 @@ template <class RQ>
 ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, size_t stride, OblLog& obl) {
   const Tables& T = R.T;
   Decision out{};
-  auto setbit = [&](uint32_t b) { bits[(size_t)(b >> 5) * stride] |= 1u << (b & 31); };
+  auto setbit = [&](uint32_t b) {  // bits == nullptr: the obligation-only pass
+    if (bits) bits[(size_t)(b >> 5) * stride] |= 1u << (b & 31);
+  };
   const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
   CandRange sets(F, 0, 0, T.n_sets);
   uint32_t s;

@@ -235,6 +235,40 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   out[i] = d;
 }
 
+// Obligation-only pass: lane k re-runs whatIsAllowed for request idx[k]
+// — one whose K2 log overflowed (OF_OBL_OVERFLOW) — with a cap-entry maskedProperty log
+// and no bitset, so long obligation lists stay on the GPU instead of the host path.
+// obl_n[k] = the request's total push count (> cap: re-run with that cap); an index
+// outside the batch writes 0xFFFFFFFF and reads nothing.
+__global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Batch B, const uint32_t* __restrict__ idx,
+                                                                    uint32_t m, uint32_t cap, uint32_t* __restrict__ obl,
+                                                                    uint32_t* __restrict__ obl_n) {
+  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t i = k < m ? idx[k] : 0u;
+  const bool in = k < m && i < B.n;
+  ReqHdr h{};
+  if (in) h = B.hdr[i];
+  const bool host = (h.flags & RQ_HOST) != 0;
+  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                               wave_lds_row(B), wave_lds_list(B));
+  if (k >= m) return;
+  if (!in) {
+    obl_n[k] = 0xFFFFFFFFu;
+    return;
+  }
+  uint32_t total = 0;
+  if (!host) {
+    OblLog log{obl + (size_t)k * 2 * cap, 0, false, cap, 0};
+    ReqRes* scol = stage + threadIdx.x;
+    const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
+    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, nullptr, 0, log);
+    total = (d.flags & OF_ERR) ? 0u : log.total;
+  }
+  obl_n[k] = total;
+}
+
 // tmp[words][n] (column k = the k-th request in perm order) -> bits[perm[k]][words].  A
 // 256-thread block moves a 64-column x 32-word tile through LDS: coalesced 256-B reads of
 // tmp rows, 128-B contiguous writes per output row.
@@ -552,6 +586,21 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   return 0;
 }
 
+constexpr uint32_t OBL_CAP_LIMIT = 1u << 20;
+
+int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t cap,
+                                   uint32_t* obl, uint32_t* obl_n, void* stream) {
+  if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl_device: null argument");
+  if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl_device: cap must be in [1, 2^20]");
+  if (m > 0xFFFFFFFFull) return fail("acs_what_is_allowed_obl_device: too many requests");
+  if (m == 0 || b->n == 0) return 0;
+  Batch B = to_batch(b);
+  hipLaunchKernelGGL(what_is_allowed_obl_kernel, dim3((unsigned)((m + BLOCK - 1) / BLOCK)), dim3(BLOCK),
+                     filter_lds_bytes(B), (hipStream_t)stream, t->view, B, idx, (uint32_t)m, cap, obl, obl_n);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
 int acs_shard_keys_device(acs_tables* t, const acs_decision* dec, size_t n, const acs_shard* shard, uint64_t* keys,
                           void* stream) {
   if (!t || !shard || (n && (!dec || !keys))) return fail("acs_shard_keys_device: null argument");
@@ -663,6 +712,31 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
   HIP_OK(hipMemcpyAsync(out, dout, b->n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
   HIP_OK(hipEventElapsedTime(&t->last_ms, t->ev0, t->ev1));
+  return 0;
+}
+
+int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t cap,
+                            uint32_t* obl, uint32_t* obl_n) {
+  if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl: null argument");
+  if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl: cap must be in [1, 2^20]");
+  if (m == 0) return 0;
+  for (size_t k = 0; k < m; ++k)
+    if (idx[k] >= b->n) return fail("acs_what_is_allowed_obl: request index outside the batch");
+  std::lock_guard<std::mutex> lock(t->mu);
+  HIP_OK(hipSetDevice(t->device));
+  DevBatch D;
+  if (upload_batch(D, b, t->stream)) return -1;
+  void* didx = D.alloc(m * sizeof(uint32_t));
+  void* dobl = D.alloc(m * 2 * (size_t)cap * sizeof(uint32_t));
+  void* dobln = D.alloc(m * sizeof(uint32_t));
+  if (!didx || !dobl || !dobln) return fail("acs_what_is_allowed_obl: hipMalloc failed");
+  HIP_OK(hipMemcpyAsync(didx, idx, m * sizeof(uint32_t), hipMemcpyHostToDevice, t->stream));
+  if (acs_what_is_allowed_obl_device(t, &D.d, (const uint32_t*)didx, m, cap, (uint32_t*)dobl, (uint32_t*)dobln,
+                                     t->stream))
+    return -1;
+  HIP_OK(hipMemcpyAsync(obl, dobl, m * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl_n, dobln, m * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipStreamSynchronize(t->stream));
   return 0;
 }
 

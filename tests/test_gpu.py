@@ -176,6 +176,57 @@ def test_what_is_allowed_c4_gpu():
     t.close()
 
 
+@pytest.mark.parametrize("cap", [1024, 70])
+def test_what_is_allowed_overflow_pass_gpu(cap):
+    """Requests with > OBL_MAX maskedProperty pushes: the obligation-only pass returns the
+    whole log (its first OBL_MAX entries are K2's log), and the reverse query built from it
+    equals the oracle's (rule sets and obligations).  cap=70 forces the exact-count re-run."""
+    doc, cs, sb = _synth("c3", 8_000)
+    t = gpu_tables(cs)
+    bits, obl, obl_n, out = t.what_is_allowed(sb.batch)
+    over = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) != 0)
+    assert len(over) > 0
+    logs = t.resolve_overflow(sb.batch, out, cap=cap)
+    assert sorted(logs) == over.tolist()
+    assert not (out["flags"] & L.OF_OBL_OVERFLOW).any()
+    for i in over:
+        assert len(logs[i]) > L.OBL_MAX and np.array_equal(logs[i][:L.OBL_MAX], obl[i])
+    if cap < 1024:  # some logs needed the exact-count re-run
+        assert max(len(v) for v in logs.values()) > cap
+    # the device form on the same indices agrees with the host form
+    db = DeviceBatch(sb.batch, 0)
+    didx = torch.from_numpy(over.astype(np.int32)).cuda()
+    m, big = len(over), max(len(v) for v in logs.values())
+    dobl = torch.zeros((m, big, 2), dtype=torch.int32, device="cuda")
+    dn = torch.zeros(m, dtype=torch.int32, device="cuda")
+    import ctypes as C
+    rc = t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), didx.data_ptr(), m, big, dobl.data_ptr(),
+                                               dn.data_ptr(), None)
+    assert rc == 0, native.last_error(t.lib)
+    torch.cuda.synchronize()
+    dn = dn.cpu().numpy().view(np.uint32)
+    dobl = dobl.cpu().numpy().view(np.uint32)
+    for k, i in enumerate(over):
+        assert dn[k] == len(logs[i]) and np.array_equal(dobl[k, :dn[k]], logs[i])
+    o = Oracle(FULL_URNS)
+    o.load(doc)
+    for i in np.random.default_rng(5).choice(over, size=min(6, len(over)), replace=False):
+        got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], logs[i], out[i]))
+        assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
+    # out-of-range indices: rejected by the host form, marked by the device form
+    with pytest.raises(RuntimeError):
+        t.what_is_allowed_obl(sb.batch, np.array([sb.batch.n], np.uint32), 8)
+    bad = torch.tensor([sb.batch.n, int(over[0])], dtype=torch.int32, device="cuda")
+    bn = torch.zeros(2, dtype=torch.int32, device="cuda")
+    bo = torch.zeros((2, big, 2), dtype=torch.int32, device="cuda")
+    assert t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), bad.data_ptr(), 2, big, bo.data_ptr(),
+                                                 bn.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    bn = bn.cpu().numpy().view(np.uint32)
+    assert bn[0] == 0xFFFFFFFF and bn[1] == len(logs[int(over[0])])
+    t.close()
+
+
 def _shard_reduce_gpu(urns, full_map, world, make_batch):
     """Evaluate `world` policy-set shards one after another on this GPU and reduce their
     keys with MAX, as the RCCL all-reduce of the rule-sharded bench does across GPUs."""

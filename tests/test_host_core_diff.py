@@ -45,3 +45,31 @@ def test_what_is_allowed_diff(seed):
         except results.EvaluationError as e:
             got = ("ERR", e.kind)
         assert got == want, (seed, i)
+
+
+def test_what_is_allowed_overflow_pass_host():
+    """Obligation-only pass (CPU build of the core): requests whose log exceeded OBL_MAX get
+    their whole maskedProperty log, K2's truncated log is its prefix, and the reverse query
+    built from it equals the oracle's; cap 70 exercises the exact-count re-run."""
+    import numpy as np
+    from acs_mi355x import compiler, store, synth, layout as L
+    from oracle.acs_oracle import Oracle, FULL_URNS, DEFAULT_CAS
+    doc = synth.c3_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 2_000, "c3")
+    t = host_core.Tables(compiler.store_blob(cs))
+    bits, obl, obl_n, out = t.what_is_allowed(sb.batch)
+    over = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) != 0)
+    assert len(over) > 0
+    logs = t.resolve_overflow(sb.batch, out.copy(), cap=70)
+    assert sorted(logs) == over.tolist()
+    assert max(len(v) for v in logs.values()) > 70
+    for i in over:
+        assert len(logs[i]) > L.OBL_MAX and np.array_equal(logs[i][:L.OBL_MAX], obl[i])
+    o = Oracle(FULL_URNS)
+    o.load(doc)
+    rec = out.copy()
+    rec["flags"][over] &= np.uint8(~L.OF_OBL_OVERFLOW & 0xFF)
+    for i in over[:4]:
+        got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], logs[i], rec[i]))
+        assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
