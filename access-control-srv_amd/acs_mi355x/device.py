@@ -63,11 +63,12 @@ def what_is_allowed_device(tables, db: DeviceBatch, bufs=None, stream=None):
     return bufs
 
 
-def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int = 1024, stream=None):
+def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int = 1024, chunks: int = 8, stream=None):
     """Obligation-only passes for the requests whose K2 log overflowed (record flag
-    OF_OBL_OVERFLOW in ``bufs[3]``): ``cap`` entries each, then the still-truncated ones once
-    more at their exact count.  Returns [(idx, cap, obl [m][cap][2], obl_n [m])] per pass (int32
-    tensors; later passes supersede earlier ones).  Syncs the stream to size each pass."""
+    OF_OBL_OVERFLOW in ``bufs[3]``): the policy sets cut into ``chunks`` ranges with ``cap``
+    entries each, then the still-truncated requests once more at their exact count.  Returns
+    [(idx [m], cap, obl [chunks][m][cap][2], obl_n [chunks][m])] per pass (int32 tensors; later
+    passes supersede earlier ones).  Syncs the stream to size each pass."""
     st = stream or torch.cuda.current_stream(db.dev)
     with torch.cuda.stream(st):
         flags = bufs[3][:, 2]
@@ -78,27 +79,31 @@ def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int = 1024, stre
         passes = []
         while idx.numel():
             m = idx.numel()
-            obl = torch.empty((m, cap, 2), dtype=torch.int32, device=db.dev)
-            obl_n = torch.empty((m,), dtype=torch.int32, device=db.dev)
-            rc = tables.lib.acs_what_is_allowed_obl_device(tables.h, C.byref(db.struct), idx.data_ptr(), m, cap,
-                                                           obl.data_ptr(), obl_n.data_ptr(), C.c_void_p(st.cuda_stream))
+            obl = torch.empty((chunks, m, cap, 2), dtype=torch.int32, device=db.dev)
+            obl_n = torch.empty((chunks, m), dtype=torch.int32, device=db.dev)
+            rc = tables.lib.acs_what_is_allowed_obl_device(tables.h, C.byref(db.struct), idx.data_ptr(), m, chunks,
+                                                           cap, obl.data_ptr(), obl_n.data_ptr(),
+                                                           C.c_void_p(st.cuda_stream))
             if rc != 0:
                 raise RuntimeError(f"acs_what_is_allowed_obl_device: {last_error(tables.lib)}")
             passes.append((idx, cap, obl, obl_n))
-            more = obl_n > cap
+            more = (obl_n > cap).any(dim=0)
             if not bool(more.any()):
                 break
-            idx, cap = idx[more], int(obl_n[more].max())
+            idx, cap = idx[more], int(obl_n[:, more].max())
     return passes
 
 
 def overflow_logs(passes) -> dict:
     """{request index: [k][2] uint32 pairs} from resolve_overflow_device's passes."""
+    from .native import join_chunk_logs
     logs = {}
     for idx, cap, obl, obl_n in passes:
-        idx, obl, obl_n = idx.cpu().numpy(), obl.cpu().numpy().view(np.uint32), obl_n.cpu().numpy()
-        for k in np.flatnonzero(obl_n <= cap):
-            logs[int(idx[k])] = obl[k, :obl_n[k]]
+        idx = idx.cpu().numpy()
+        joined = join_chunk_logs(obl.cpu().numpy().view(np.uint32), obl_n.cpu().numpy().view(np.uint32), cap)
+        for j, lg in enumerate(joined):
+            if lg is not None:
+                logs[int(idx[j])] = lg
     return logs
 
 

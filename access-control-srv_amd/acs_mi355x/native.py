@@ -50,8 +50,8 @@ def _declare(lib):
     lib.acs_wia_words_per_request.restype = u32
     lib.acs_what_is_allowed.argtypes = [vp, pb, vp, vp, vp, vp]
     lib.acs_what_is_allowed_device.argtypes = [vp, pb, vp, vp, vp, vp, vp]
-    lib.acs_what_is_allowed_obl.argtypes = [vp, pb, vp, C.c_size_t, u32, vp, vp]
-    lib.acs_what_is_allowed_obl_device.argtypes = [vp, pb, vp, C.c_size_t, u32, vp, vp, vp]
+    lib.acs_what_is_allowed_obl.argtypes = [vp, pb, vp, C.c_size_t, u32, u32, vp, vp]
+    lib.acs_what_is_allowed_obl_device.argtypes = [vp, pb, vp, C.c_size_t, u32, u32, vp, vp, vp]
     lib.acs_last_kernel_ms.argtypes = [vp]
     lib.acs_last_kernel_ms.restype = C.c_float
     lib.acs_last_error.restype = C.c_char_p
@@ -112,21 +112,36 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
     return s
 
 
-OVERFLOW_CAP = 1024  # first obligation-only pass: log entries per overflowed request
+OVERFLOW_CAP = 1024  # first obligation-only pass: log entries per overflowed request and set range
+OVERFLOW_CHUNKS = 8  # policy-set ranges per request in the obligation-only pass
 
 
-def resolve_overflow(tables, batch, out, cap: int = OVERFLOW_CAP) -> dict:
+def join_chunk_logs(obl, obl_n, cap):
+    """Per request j: the concatenation over set ranges c of obl[c, j, :obl_n[c, j]], or None
+    when some range's log was truncated (obl_n > cap)."""
+    out = []
+    for j in range(obl.shape[1]):
+        n = obl_n[:, j]
+        out.append(None if (n > cap).any() else
+                   np.concatenate([obl[c, j, :n[c]] for c in range(obl.shape[0])]).reshape(-1, 2))
+    return out
+
+
+def resolve_overflow(tables, batch, out, cap: int = OVERFLOW_CAP, chunks: int = OVERFLOW_CHUNKS) -> dict:
     """Full maskedProperty logs of the requests whose K2 log overflowed (OF_OBL_OVERFLOW):
-    {request index: [k][2] pairs}, from the obligation-only pass (``cap`` entries first, then
-    each still-truncated request once more at its exact count).  Clears the flag in ``out``."""
+    {request index: [k][2] pairs}, from the obligation-only pass (``cap`` entries per set range
+    first, then each still-truncated request once more at its exact count).  Clears the flag
+    in ``out``."""
     idx = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) != 0).astype(np.uint32)
     logs = {}
     while len(idx):
-        obl, obl_n = tables.what_is_allowed_obl(batch, idx, cap)
-        done = obl_n <= cap
-        for k in np.flatnonzero(done):
-            logs[int(idx[k])] = obl[k, :obl_n[k]].copy()
-        idx, cap = idx[~done], (int(obl_n[~done].max()) if (~done).any() else cap)
+        obl, obl_n = tables.what_is_allowed_obl(batch, idx, cap, chunks)
+        joined = join_chunk_logs(obl, obl_n, cap)
+        for j, lg in enumerate(joined):
+            if lg is not None:
+                logs[int(idx[j])] = lg
+        left = np.array([lg is None for lg in joined])
+        idx, cap = idx[left], (int(obl_n[:, left].max()) if left.any() else cap)
     if logs:
         flags = out["flags"]
         flags[np.fromiter(logs, np.int64, len(logs))] &= np.uint8(~L.OF_OBL_OVERFLOW & 0xFF)
@@ -178,23 +193,23 @@ class Tables:
                 raise RuntimeError(f"acs_what_is_allowed: {last_error(self.lib)}")
         return bits, obl, obl_n, out
 
-    def what_is_allowed_obl(self, batch, idx, cap: int):
-        """Obligation-only pass over requests ``idx`` of ``batch`` with a ``cap``-entry log each:
-        (obl [m][cap][2], obl_n [m] = total pushes per request)."""
+    def what_is_allowed_obl(self, batch, idx, cap: int, chunks: int = OVERFLOW_CHUNKS):
+        """Obligation-only pass over requests ``idx`` of ``batch``, the policy sets cut into
+        ``chunks`` ranges: (obl [chunks][m][cap][2], obl_n [chunks][m] = pushes per range)."""
         idx = np.ascontiguousarray(idx, np.uint32)
         m = len(idx)
-        obl = np.zeros((m, cap, 2), np.uint32)
-        obl_n = np.zeros(m, np.uint32)
+        obl = np.zeros((chunks, m, cap, 2), np.uint32)
+        obl_n = np.zeros((chunks, m), np.uint32)
         if m:
             s = batch_struct(batch)
-            rc = self.lib.acs_what_is_allowed_obl(self.h, C.byref(s), idx.ctypes.data, m, cap, obl.ctypes.data,
-                                                  obl_n.ctypes.data)
+            rc = self.lib.acs_what_is_allowed_obl(self.h, C.byref(s), idx.ctypes.data, m, chunks, cap,
+                                                  obl.ctypes.data, obl_n.ctypes.data)
             if rc != 0:
                 raise RuntimeError(f"acs_what_is_allowed_obl: {last_error(self.lib)}")
         return obl, obl_n
 
-    def resolve_overflow(self, batch, out, cap: int = OVERFLOW_CAP) -> dict:
-        return resolve_overflow(self, batch, out, cap)
+    def resolve_overflow(self, batch, out, cap: int = OVERFLOW_CAP, chunks: int = OVERFLOW_CHUNKS) -> dict:
+        return resolve_overflow(self, batch, out, cap, chunks)
 
     def set_sort(self, enable: bool):
         if self.lib.acs_set_option(self.h, 1, int(bool(enable))) != 0:

@@ -916,14 +916,17 @@ ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
 template <class RQ>
 // bits: word w of this request's bitset lives at bits[w * stride] (1: a row; the GPU writes
 // a column of a word-major [words][n] buffer so a wave's stores coalesce)
-ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, size_t stride, OblLog& obl) {
+// [s_begin, s_end): the policy sets evaluated (whatIsAllowed keeps no state across sets but the
+// push log, so a request's log is the concatenation of the logs of consecutive set ranges).
+ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, size_t stride, OblLog& obl,
+                                  uint32_t s_begin = 0, uint32_t s_end = NONE32) {
   const Tables& T = R.T;
   Decision out{};
   auto setbit = [&](uint32_t b) {  // bits == nullptr: the obligation-only pass
     if (bits) bits[(size_t)(b >> 5) * stride] |= 1u << (b & 31);
   };
   const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
-  CandRange sets(F, 0, 0, T.n_sets);
+  CandRange sets(F, 0, s_begin, s_end < T.n_sets ? s_end : T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
     const NodeRec S = load_words(T, T.sets + s);

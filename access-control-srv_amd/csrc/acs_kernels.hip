@@ -235,66 +235,77 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   out[i] = d;
 }
 
-// Obligation-only pass: lane k re-runs whatIsAllowed for request idx[k]
-// — one whose K2 log overflowed (OF_OBL_OVERFLOW) — with a cap-entry maskedProperty log
-// and no bitset, so long obligation lists stay on the GPU instead of the host path.
-// obl_n[k] = the request's total push count (> cap: re-run with that cap); an index
-// outside the batch writes 0xFFFFFFFF and reads nothing.
+// Obligation-only pass for requests idx[0..m) — those whose K2 log
+// overflowed (OF_OBL_OVERFLOW) — with a cap-entry maskedProperty log and no bitset, so long
+// obligation lists stay on the GPU instead of the host path.  whatIsAllowed keeps no state
+// across policy sets except the log, so the sets are cut into `chunks` contiguous ranges
+// and lane k evaluates range c = k / m of request idx[k % m]: chunks x more waves, each
+// 1/chunks as long (the pass is one wave's traversal deep: 461 waves at c4).
+// obl[c][j] / obl_n[c][j]: range c's log and total push count (> cap: re-run with that
+// cap); a request's log is the concatenation over c.  An index outside the batch writes
+// 0xFFFFFFFF and reads nothing.
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Batch B, const uint32_t* __restrict__ idx,
-                                                                    uint32_t m, uint32_t cap, uint32_t* __restrict__ obl,
+                                                                    uint32_t m, uint32_t chunks, uint32_t cap,
+                                                                    uint32_t* __restrict__ obl,
                                                                     uint32_t* __restrict__ obl_n) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  const uint32_t i = k < m ? idx[k] : 0u;
-  const bool in = k < m && i < B.n;
+  // each range's lanes start on a wave boundary (m padded to 64): the set range, and with it
+  // the candidate iteration, is wave-uniform
+  const uint64_t mp = ((uint64_t)m + 63u) & ~(uint64_t)63u;
+  const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t c = (uint32_t)(t / mp), j = (uint32_t)(t % mp);
+  const bool live = c < chunks && j < m;
+  const uint64_t k = (uint64_t)c * m + j;  // output slot [c][j]
+  const uint32_t i = live ? idx[j] : 0u;
+  const bool in = live && i < B.n;
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                wave_lds_row(B), wave_lds_list(B));
-  if (k >= m) return;
+  if (!live) return;
   if (!in) {
     obl_n[k] = 0xFFFFFFFFu;
     return;
   }
   uint32_t total = 0;
   if (!host) {
-    OblLog log{obl + (size_t)k * 2 * cap, 0, false, cap, 0};
+    OblLog log{obl + k * 2 * cap, 0, false, cap, 0};
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, nullptr, 0, log);
+    for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = B.res[(size_t)q * B.n + i];
+    const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks), s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
+    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, nullptr, 0, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
   }
   obl_n[k] = total;
 }
 
 // tmp[words][n] (column k = the k-th request in perm order) -> bits[perm[k]][words].  A
-// 256-thread block moves a 64-column x 32-word tile through LDS: coalesced 256-B reads of
-// tmp rows, 128-B contiguous writes per output row.
-constexpr uint32_t TP_COLS = 64, TP_WORDS = 32;
+// 256-thread block moves a 64-column x 64-word tile through LDS: every load instruction
+// reads 256 contiguous bytes of a tmp row, every store instruction writes 256 contiguous
+// bytes (64 words) of one output row — both fully coalesced (the previous 32-word tile
+// stored 4-byte pieces of 16 rows per instruction: 1.29 ms for 1M c4 rows).
+constexpr uint32_t TP_COLS = 64, TP_WORDS = 64;
 __global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t* __restrict__ tmp, uint32_t n,
                                                                  uint32_t words, const uint32_t* __restrict__ perm,
                                                                  uint32_t* __restrict__ bits) {
   __shared__ uint32_t tile[TP_WORDS][TP_COLS + 1];
   const uint32_t k0 = blockIdx.x * TP_COLS, w0 = blockIdx.y * TP_WORDS;
-  const uint32_t t = threadIdx.x, c = t & 63u;
-  for (uint32_t r = t >> 6; r < TP_WORDS; r += BLOCK / 64) {
-    const uint32_t w = w0 + r, k = k0 + c;
-    tile[r][c] = (w < words && k < n) ? tmp[(size_t)w * n + k] : 0u;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (uint32_t r = wave; r < TP_WORDS; r += BLOCK / 64) {
+    const uint32_t w = w0 + r, k = k0 + lane;
+    tile[r][lane] = (w < words && k < n) ? tmp[(size_t)w * n + k] : 0u;
   }
   __syncthreads();
-  const uint32_t row = t >> 2, part = (t & 3u) * 8u, k = k0 + row;
-  if (k >= n) return;
-  uint32_t* dst = bits + (size_t)(perm ? perm[k] : k) * words;
-#pragma unroll
-  for (uint32_t q = 0; q < 8; ++q) {
-    const uint32_t w = w0 + part + q;
-    if (w < words) dst[w] = tile[part + q][row];
+  const uint32_t w = w0 + lane;
+  for (uint32_t r = wave; r < TP_COLS; r += BLOCK / 64) {
+    const uint32_t k = k0 + r;
+    if (k >= n) break;
+    if (w < words) bits[(size_t)(perm ? perm[k] : k) * words + w] = tile[lane][r];
   }
 }
 
-// Rule-sharded isAllowed (C1): local decisions -> 64-bit MAX-reducible keys, and back.
 __global__ __launch_bounds__(BLOCK) void shard_key_kernel(Tables T, const Decision* __restrict__ d, uint32_t n,
                                                           ShardBase b, uint64_t* __restrict__ keys) {
   const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -588,15 +599,17 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
 
 constexpr uint32_t OBL_CAP_LIMIT = 1u << 20;
 
-int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t cap,
-                                   uint32_t* obl, uint32_t* obl_n, void* stream) {
+int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m,
+                                   uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n, void* stream) {
   if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl_device: null argument");
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl_device: cap must be in [1, 2^20]");
-  if (m > 0xFFFFFFFFull) return fail("acs_what_is_allowed_obl_device: too many requests");
+  if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl_device: chunks must be in [1, 64]");
+  if (m > 0xFFFFFFFFull || m * chunks > 0xFFFFFFFFull) return fail("acs_what_is_allowed_obl_device: too many requests");
   if (m == 0 || b->n == 0) return 0;
   Batch B = to_batch(b);
-  hipLaunchKernelGGL(what_is_allowed_obl_kernel, dim3((unsigned)((m + BLOCK - 1) / BLOCK)), dim3(BLOCK),
-                     filter_lds_bytes(B), (hipStream_t)stream, t->view, B, idx, (uint32_t)m, cap, obl, obl_n);
+  const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
+  hipLaunchKernelGGL(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), dim3(BLOCK),
+                     filter_lds_bytes(B), (hipStream_t)stream, t->view, B, idx, (uint32_t)m, chunks, cap, obl, obl_n);
   HIP_OK(hipGetLastError());
   return 0;
 }
@@ -715,10 +728,11 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
   return 0;
 }
 
-int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t cap,
-                            uint32_t* obl, uint32_t* obl_n) {
+int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t chunks,
+                            uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
   if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl: null argument");
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl: cap must be in [1, 2^20]");
+  if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl: chunks must be in [1, 64]");
   if (m == 0) return 0;
   for (size_t k = 0; k < m; ++k)
     if (idx[k] >= b->n) return fail("acs_what_is_allowed_obl: request index outside the batch");
@@ -726,16 +740,17 @@ int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;
   if (upload_batch(D, b, t->stream)) return -1;
+  const size_t lanes = m * chunks;
   void* didx = D.alloc(m * sizeof(uint32_t));
-  void* dobl = D.alloc(m * 2 * (size_t)cap * sizeof(uint32_t));
-  void* dobln = D.alloc(m * sizeof(uint32_t));
+  void* dobl = D.alloc(lanes * 2 * (size_t)cap * sizeof(uint32_t));
+  void* dobln = D.alloc(lanes * sizeof(uint32_t));
   if (!didx || !dobl || !dobln) return fail("acs_what_is_allowed_obl: hipMalloc failed");
   HIP_OK(hipMemcpyAsync(didx, idx, m * sizeof(uint32_t), hipMemcpyHostToDevice, t->stream));
-  if (acs_what_is_allowed_obl_device(t, &D.d, (const uint32_t*)didx, m, cap, (uint32_t*)dobl, (uint32_t*)dobln,
-                                     t->stream))
+  if (acs_what_is_allowed_obl_device(t, &D.d, (const uint32_t*)didx, m, chunks, cap, (uint32_t*)dobl,
+                                     (uint32_t*)dobln, t->stream))
     return -1;
-  HIP_OK(hipMemcpyAsync(obl, dobl, m * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl_n, dobln, m * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl, dobl, lanes * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl_n, dobln, lanes * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
   return 0;
 }

@@ -113,14 +113,17 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, ui
 /* Obligation-only pass (no reference counterpart: the reference's obligations list is
  * unbounded, accessController.ts:592-640).  Re-evaluates the m requests idx[0..m) of the
  * batch — those whose acs_what_is_allowed record carries OF_OBL_OVERFLOW — with a
- * cap-entry maskedProperty log each (1 <= cap <= 2^20).  obl: [m][cap][2];
- * obl_n[k] = the request's total push count (> cap: still truncated, re-run with
- * cap = obl_n[k]); 0xFFFFFFFF (device form) = idx[k] outside the batch, which the
- * host form rejects with an error. */
+ * cap-entry maskedProperty log per lane (1 <= cap <= 2^20) and no bitset.  The policy sets
+ * are cut into `chunks` (1..64) contiguous ranges evaluated by separate lanes:
+ * obl: [chunks][m][cap][2], obl_n: [chunks][m] = that range's total push count (> cap:
+ * still truncated, re-run with cap = obl_n); request j's log is the concatenation of its
+ * ranges' logs in range order.  0xFFFFFFFF (device form) = idx[j] outside the batch, which
+ * the host form rejects with an error. */
 int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* host_batch, const uint32_t* idx, size_t m,
-                            uint32_t cap, uint32_t* obl, uint32_t* obl_n);
+                            uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n);
 int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* dev_batch, const uint32_t* dev_idx, size_t m,
-                                   uint32_t cap, uint32_t* dev_obl, uint32_t* dev_obl_n, void* stream);
+                                   uint32_t chunks, uint32_t cap, uint32_t* dev_obl, uint32_t* dev_obl_n,
+                                   void* stream);
 
 /* Rule-sharded isAllowed (configs[4] variant ii).  A rank compiles only the
  * policy sets [set_base, set_base + n_sets) of the store (whole sets, Map order) and

@@ -24,7 +24,7 @@ def lib():
         _LIB.acs_host_shard_decode.argtypes = [vp, C.c_size_t, vp]
         _LIB.acs_host_shard_decode.restype = None
         _LIB.acs_host_what_is_allowed_obl.argtypes = [vp, C.c_size_t, C.POINTER(ReqBatchC), vp, C.c_size_t,
-                                                      C.c_uint32, vp, vp]
+                                                      C.c_uint32, C.c_uint32, vp, vp]
     return _LIB
 
 
@@ -94,19 +94,19 @@ class Tables:
         self._call(lib().acs_host_what_is_allowed, batch, bits, obl, obl_n, out)
         return bits, obl, obl_n, out
 
-    def what_is_allowed_obl(self, batch, idx, cap):
+    def what_is_allowed_obl(self, batch, idx, cap, chunks=8):
         idx = np.ascontiguousarray(idx, np.uint32)
-        obl = np.zeros((len(idx), cap, 2), np.uint32)
-        obl_n = np.zeros(len(idx), np.uint32)
+        obl = np.zeros((chunks, len(idx), cap, 2), np.uint32)
+        obl_n = np.zeros((chunks, len(idx)), np.uint32)
         if len(idx):
             s = batch_struct(batch)
             assert lib().acs_host_what_is_allowed_obl(self.blob, len(self.blob), C.byref(s), idx.ctypes.data, len(idx),
-                                                      cap, obl.ctypes.data, obl_n.ctypes.data) == 0
+                                                      chunks, cap, obl.ctypes.data, obl_n.ctypes.data) == 0
         return obl, obl_n
 
-    def resolve_overflow(self, batch, out, cap=1024):
+    def resolve_overflow(self, batch, out, cap=1024, chunks=8):
         from acs_mi355x.native import resolve_overflow
-        return resolve_overflow(self, batch, out, cap)
+        return resolve_overflow(self, batch, out, cap, chunks)
 
     def close(self):
         pass

@@ -108,24 +108,30 @@ extern "C" int acs_host_what_is_allowed(const void* blob, size_t n, const acs_re
   return 0;
 }
 
-// Obligation-only pass (acs_what_is_allowed_obl's CPU twin): requests idx[0..m) with a
-// cap-entry log each and no bitset; obl_n[k] = total pushes of the request.
+// Obligation-only pass (acs_what_is_allowed_obl's CPU twin): requests idx[0..m) with the
+// policy sets cut into `chunks` ranges, a cap-entry log per (range, request) and no bitset;
+// obl_n[c][j] = total pushes of range c of request j.
 extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const acs_req_batch* b, const uint32_t* idx,
-                                            size_t m, uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
+                                            size_t m, uint32_t chunks, uint32_t cap, uint32_t* obl,
+                                            uint32_t* obl_n) {
   Tables T;
   if (!host_tables(blob, n, &T)) return -1;
   Batch B = host_batch(b);
-  for (size_t k = 0; k < m; ++k) {
-    const uint32_t i = idx[k];
-    if (i >= B.n) return -1;
-    const ReqHdr h = B.hdr[i];
-    OblLog log{obl + k * 2 * (size_t)cap, 0, false, cap, 0};
-    uint32_t total = 0;
-    if (!(h.flags & RQ_HOST)) {
-      const Decision d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), nullptr, 0, log);
-      total = (d.flags & OF_ERR) ? 0u : log.total;
+  for (uint32_t c = 0; c < chunks; ++c)
+    for (size_t j = 0; j < m; ++j) {
+      const uint32_t i = idx[j];
+      if (i >= B.n) return -1;
+      const size_t k = (size_t)c * m + j;
+      const ReqHdr h = B.hdr[i];
+      OblLog log{obl + k * 2 * (size_t)cap, 0, false, cap, 0};
+      uint32_t total = 0;
+      if (!(h.flags & RQ_HOST)) {
+        const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks);
+        const uint32_t s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
+        const Decision d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), nullptr, 0, log, s0, s1);
+        total = (d.flags & OF_ERR) ? 0u : log.total;
+      }
+      obl_n[k] = total;
     }
-    obl_n[k] = total;
-  }
   return 0;
 }

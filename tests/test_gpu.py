@@ -193,21 +193,21 @@ def test_what_is_allowed_overflow_pass_gpu(cap):
         assert len(logs[i]) > L.OBL_MAX and np.array_equal(logs[i][:L.OBL_MAX], obl[i])
     if cap < 1024:  # some logs needed the exact-count re-run
         assert max(len(v) for v in logs.values()) > cap
-    # the device form on the same indices agrees with the host form
+    # the device form on the same indices agrees with the host form, for 1 and 5 set ranges
+    import ctypes as C
     db = DeviceBatch(sb.batch, 0)
     didx = torch.from_numpy(over.astype(np.int32)).cuda()
     m, big = len(over), max(len(v) for v in logs.values())
-    dobl = torch.zeros((m, big, 2), dtype=torch.int32, device="cuda")
-    dn = torch.zeros(m, dtype=torch.int32, device="cuda")
-    import ctypes as C
-    rc = t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), didx.data_ptr(), m, big, dobl.data_ptr(),
-                                               dn.data_ptr(), None)
-    assert rc == 0, native.last_error(t.lib)
-    torch.cuda.synchronize()
-    dn = dn.cpu().numpy().view(np.uint32)
-    dobl = dobl.cpu().numpy().view(np.uint32)
-    for k, i in enumerate(over):
-        assert dn[k] == len(logs[i]) and np.array_equal(dobl[k, :dn[k]], logs[i])
+    for chunks in (1, 5):
+        dobl = torch.zeros((chunks, m, big, 2), dtype=torch.int32, device="cuda")
+        dn = torch.zeros((chunks, m), dtype=torch.int32, device="cuda")
+        rc = t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), didx.data_ptr(), m, chunks, big,
+                                                   dobl.data_ptr(), dn.data_ptr(), None)
+        assert rc == 0, native.last_error(t.lib)
+        torch.cuda.synchronize()
+        joined = native.join_chunk_logs(dobl.cpu().numpy().view(np.uint32), dn.cpu().numpy().view(np.uint32), big)
+        for k, i in enumerate(over):
+            assert np.array_equal(joined[k], logs[i])
     o = Oracle(FULL_URNS)
     o.load(doc)
     for i in np.random.default_rng(5).choice(over, size=min(6, len(over)), replace=False):
@@ -217,13 +217,13 @@ def test_what_is_allowed_overflow_pass_gpu(cap):
     with pytest.raises(RuntimeError):
         t.what_is_allowed_obl(sb.batch, np.array([sb.batch.n], np.uint32), 8)
     bad = torch.tensor([sb.batch.n, int(over[0])], dtype=torch.int32, device="cuda")
-    bn = torch.zeros(2, dtype=torch.int32, device="cuda")
-    bo = torch.zeros((2, big, 2), dtype=torch.int32, device="cuda")
-    assert t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), bad.data_ptr(), 2, big, bo.data_ptr(),
+    bn = torch.zeros((1, 2), dtype=torch.int32, device="cuda")
+    bo = torch.zeros((1, 2, big, 2), dtype=torch.int32, device="cuda")
+    assert t.lib.acs_what_is_allowed_obl_device(t.h, C.byref(db.struct), bad.data_ptr(), 2, 1, big, bo.data_ptr(),
                                                  bn.data_ptr(), None) == 0
     torch.cuda.synchronize()
     bn = bn.cpu().numpy().view(np.uint32)
-    assert bn[0] == 0xFFFFFFFF and bn[1] == len(logs[int(over[0])])
+    assert bn[0, 0] == 0xFFFFFFFF and bn[0, 1] == len(logs[int(over[0])])
     t.close()
 
 
