@@ -308,18 +308,40 @@ def _node(fields: dict, spec: list):
     return tuple(fields.get(n, 0) if n != "pad" else (0, 0, 0) for n in L.NODE_DT.names)
 
 
-def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> CompiledStore:
-    """Snapshot ``policy_sets`` (ordered Map of sets, see store.py) into node tables."""
-    b = _Builder(urns, combining_algorithms)
-    sets, pols, rules = [], [], []
-    set_objs, pol_objs, rule_objs = [], [], []
-    spec_s, spec_p, spec_r = [], [], []
-    for ps in policy_sets.values():
-        if not isinstance(ps, dict):
-            raise Unsupported("null policy set")
+@dataclass
+class _Fragment:
+    """One policy set compiled on its own: node records with fragment-local child ranges and
+    pool offsets (assemble() shifts them), its candidate specs and host-side objects."""
+    obj: dict
+    sets: np.ndarray
+    pols: np.ndarray
+    rules: np.ndarray
+    rres: np.ndarray
+    pairs: np.ndarray
+    u32pool: np.ndarray
+    spec: tuple
+    pol_objs: list
+    rule_objs: list
+
+
+def _arr(x, dt):
+    return np.array(x, dtype=dt) if x else np.zeros(0, dt)
+
+
+def _compile_set(b: _Builder, ps) -> _Fragment:
+    """Compile one policy set (accessController.ts:125-295 per-set state: policyEffect prefix,
+    evaluation_cacheable prefix, child ranges) with the shared dictionary / regex rows of
+    ``b`` and fresh, fragment-local pools."""
+    if not isinstance(ps, dict):
+        raise Unsupported("null policy set")
+    saved = (b.rres, b.pairs, b.u32pool)
+    b.rres, b.pairs, b.u32pool = [], [], []
+    try:
+        pols, rules, pol_objs, rule_objs = [], [], [], []
+        spec_s, spec_p, spec_r = [], [], []
         sn = b.target(ps.get("target", MISSING))
         sn["nflags"] = L.NF_HAS_TARGET if sn else 0
-        sn["child_begin"] = len(pols)
+        sn["child_begin"] = 0
         combin = ps.get("combinables")
         if not isinstance(combin, dict):
             raise Unsupported("policy set without combinables")
@@ -366,22 +388,96 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
             pol_objs.append(pol)
         sn.update(child_end=len(pols), ca=b.ca_code(ps.get("combining_algorithm", MISSING)),
                   pe_at=pe_at)  # set: policyEffect after a full loop-2a scan
-        sets.append(_node(sn, spec_s))
-        set_objs.append(ps)
+        sets = [_node(sn, spec_s)]
+        return _Fragment(ps, _arr(sets, L.NODE_DT), _arr(pols, L.NODE_DT), _arr(rules, L.NODE_DT),
+                         _arr(b.rres, L.RULE_RES_DT), _arr(b.pairs, L.PAIR_DT),
+                         np.array(b.u32pool, dtype=np.uint32) if b.u32pool else np.zeros(0, np.uint32),
+                         (spec_s, spec_p, spec_r), pol_objs, rule_objs)
+    finally:
+        b.rres, b.pairs, b.u32pool = saved
 
-    def arr(x, dt):
-        return np.array(x, dtype=dt) if x else np.zeros(0, dt)
+
+def _assemble(b: _Builder, frags: list) -> CompiledStore:
+    """Concatenate fragments in Map order, shifting child ranges and pool offsets."""
+    ns = [len(f.pols) for f in frags]
+    nr = [len(f.rules) for f in frags]
+    sizes = {k: [len(getattr(f, k)) for f in frags] for k in ("rres", "pairs", "u32pool")}
+
+    def starts(v):
+        return np.concatenate([[0], np.cumsum(v, dtype=np.int64)[:-1]]).astype(np.uint32) if v else np.zeros(0, np.uint32)
+
+    pol0, rule0 = starts(ns), starts(nr)
+    res0, pair0, u320 = starts(sizes["rres"]), starts(sizes["pairs"]), starts(sizes["u32pool"])
+
+    pools = [("subj_off", pair0), ("act_off", pair0), ("res_off", res0), ("acl_roles_off", u320)]
+
+    def cat(key, shifts):
+        if not frags:
+            return np.zeros(0, L.NODE_DT)
+        a = np.concatenate([getattr(f, key) for f in frags])
+        owner = np.repeat(np.arange(len(frags)), [len(getattr(f, key)) for f in frags])
+        for field_, base in shifts:
+            a[field_] += base[owner]
+        tgt = (a["nflags"] & L.NF_HAS_TARGET) != 0  # target-less nodes keep pool offsets 0
+        for field_, base in pools:
+            a[field_][tgt] += base[owner[tgt]]
+        return a
+
+    sets = cat("sets", [("child_begin", pol0), ("child_end", pol0)])
+    pols = cat("pols", [("child_begin", rule0), ("child_end", rule0), ("fe", rule0)])
+    rules = cat("rules", [])
+
+    def pool(key, dt):
+        return np.concatenate([getattr(f, key) for f in frags]) if frags else np.zeros(0, dt)
+
     cs = CompiledStore(
-        urns=b.urns, dictionary=b.d,
-        sets=arr(sets, L.NODE_DT), pols=arr(pols, L.NODE_DT), rules=arr(rules, L.NODE_DT),
-        rres=arr(b.rres, L.RULE_RES_DT), pairs=arr(b.pairs, L.PAIR_DT),
-        u32pool=np.array(b.u32pool, dtype=np.uint32) if b.u32pool else np.zeros(0, np.uint32),
-        rx_rows=b.rx_rows, ec_values=b.ec_values, id_user=b.d.intern(b.urn("user")),
-        set_objs=set_objs, pol_objs=pol_objs, rule_objs=rule_objs,
-        cand_spec=(spec_s, spec_p, spec_r))
+        urns=b.urns, dictionary=b.d, sets=sets, pols=pols, rules=rules, rres=pool("rres", L.RULE_RES_DT),
+        pairs=pool("pairs", L.PAIR_DT), u32pool=pool("u32pool", np.uint32),
+        rx_rows=list(b.rx_rows), ec_values=list(b.ec_values), id_user=b.d.intern(b.urn("user")),
+        set_objs=[f.obj for f in frags], pol_objs=[o for f in frags for o in f.pol_objs],
+        rule_objs=[o for f in frags for o in f.rule_objs],
+        cand_spec=tuple([x for f in frags for x in f.spec[i]] for i in range(3)))
     cs.stats = {"sets": cs.n_sets, "policies": cs.n_pols, "rules": cs.n_rules, "dictionary": len(b.d),
                 "rx_rows": len(b.rx_rows), "table_bytes": cs.table_bytes()}
     return cs
+
+
+class IncrementalCompiler:
+    """Recompiles only the policy sets that changed (store mutations
+    through updatePolicySet / updatePolicy / updateRule / remove* / Map edits,
+    accessController.ts:897-937, resourceManager.ts:156-1047).  Each set is compiled into a
+    fragment against a shared, append-only dictionary and regex-row index, so unchanged
+    fragments stay valid; compile() reuses a fragment when its key is not marked dirty and
+    the Map still holds the same set object, then re-concatenates (offset shifts only).
+    Interned ids of an incremental image can differ from a fresh compile's, and strings of
+    removed rules stay in the dictionary; the tables are otherwise equal field for field
+    (tests/test_incremental.py)."""
+
+    def __init__(self, urns: dict, combining_algorithms: list):
+        self.b = _Builder(urns, combining_algorithms)
+        self.frags = {}
+        self.stats = {"compiles": 0, "sets_compiled": 0, "sets_reused": 0}
+
+    def compile(self, policy_sets: dict, dirty=None) -> CompiledStore:
+        """``dirty``: keys whose sets changed in place (None: every set)."""
+        frags, new = [], {}
+        for key, ps in policy_sets.items():
+            f = self.frags.get(key)
+            if f is None or f.obj is not ps or dirty is None or key in dirty:
+                f = _compile_set(self.b, ps)
+                self.stats["sets_compiled"] += 1
+            else:
+                self.stats["sets_reused"] += 1
+            frags.append(f)
+            new[key] = f
+        self.frags = new
+        self.stats["compiles"] += 1
+        return _assemble(self.b, frags)
+
+
+def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> CompiledStore:
+    """Snapshot ``policy_sets`` (ordered Map of sets, see store.py) into node tables."""
+    return IncrementalCompiler(urns, combining_algorithms).compile(policy_sets)
 
 
 def store_blob(cs: CompiledStore) -> bytes:

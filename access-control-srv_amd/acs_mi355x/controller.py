@@ -38,30 +38,33 @@ class InvalidCombiningAlgorithm(Exception):
     """errors.InvalidCombiningAlgorithm of the reference (accessController.ts:57,837)."""
 
 
+_ALL = object()  # invalidate(): every policy set may have changed
+
+
 class _Store(dict):
     """The ``policySets`` Map: a dict (insertion order == JS Map order) that tells its
-    controller when it changes.  Nested ``combinables`` maps are plain dicts; edits
-    made through the controller's update*/remove* methods are tracked, direct nested
-    edits need ``invalidate()``."""
+    controller which sets change.  Nested ``combinables`` maps are plain dicts; edits
+    made through the controller's update*/remove* methods are tracked per set, direct
+    nested edits need ``invalidate(setID)`` (or ``invalidate()`` for all sets)."""
 
     def __init__(self, owner, *a):
         super().__init__(*a)
         self._owner = owner
 
-    def _touch(self):
-        self._owner.invalidate()
+    def _touch(self, key=_ALL):
+        self._owner.invalidate(key)
 
     def __setitem__(self, k, v):
         super().__setitem__(k, v)
-        self._touch()
+        self._touch(k)
 
     def __delitem__(self, k):
         super().__delitem__(k)
-        self._touch()
+        self._touch(k)
 
     def pop(self, *a):
         r = super().pop(*a)
-        self._touch()
+        self._touch(a[0])
         return r
 
     def clear(self):
@@ -104,6 +107,8 @@ class AccessController:
         self.device = device
         self.host_evaluator = host_evaluator
         self._engine = engine
+        self._compiler = None  # compiler.IncrementalCompiler, created on first compile
+        self._dirty, self._all_dirty = set(), True
         self._policy_sets = _Store(self)
         self._cs = None
         self._tables = None
@@ -121,8 +126,14 @@ class AccessController:
         self._policy_sets = _Store(self, m.items() if hasattr(m, "items") else m)
         self.invalidate()
 
-    def invalidate(self):
-        """Mark the compiled image stale; the next evaluation recompiles."""
+    def invalidate(self, policySetID=_ALL):
+        """Mark the compiled image stale; the next evaluation recompiles the sets marked
+        here (``policySetID``), or every set (no argument), and reuses the others'
+        compiled fragments (compiler.IncrementalCompiler)."""
+        if policySetID is _ALL:
+            self._all_dirty = True
+        else:
+            self._dirty.add(_key(policySetID))
         self._cs = None
 
     def clearPolicies(self):
@@ -138,13 +149,13 @@ class AccessController:
         ps = self._policy_sets.get(_key(policySetID))
         if ps is not None:  # _.isNil guard, accessController.ts:907-909
             ps["combinables"][_key(policy.get("id", MISSING))] = policy
-            self.invalidate()
+            self.invalidate(policySetID)
 
     def removePolicy(self, policySetID, policyID):
         ps = self._policy_sets.get(_key(policySetID))
         if ps is not None:
             ps["combinables"].pop(_key(policyID), None)
-            self.invalidate()
+            self.invalidate(policySetID)
 
     def updateRule(self, policySetID, policyID, rule: dict):
         ps = self._policy_sets.get(_key(policySetID))
@@ -152,7 +163,7 @@ class AccessController:
             pol = ps["combinables"].get(_key(policyID))
             if pol is not None:
                 pol["combinables"][_key(rule.get("id", MISSING))] = rule
-                self.invalidate()
+                self.invalidate(policySetID)
 
     def removeRule(self, policySetID, policyID, ruleID):
         ps = self._policy_sets.get(_key(policySetID))
@@ -160,13 +171,16 @@ class AccessController:
             pol = ps["combinables"].get(_key(policyID))
             if pol is not None:
                 pol["combinables"].pop(_key(ruleID), None)
-                self.invalidate()
+                self.invalidate(policySetID)
 
     # ------------------------------------------------------------------ tables
     def _ensure(self):
         if self._cs is not None:
             return
-        cs = compiler.compile_store(self._policy_sets, self.urns, self.combiningAlgorithms)
+        if self._compiler is None:
+            self._compiler = compiler.IncrementalCompiler(self.urns, self.combiningAlgorithms)
+        cs = self._compiler.compile(self._policy_sets, None if self._all_dirty else self._dirty)
+        self._dirty, self._all_dirty = set(), False
         blob = compiler.store_blob(cs)
         if self._tables is not None:
             self._tables.close()

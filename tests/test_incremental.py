@@ -1,0 +1,158 @@
+"""Incremental recompile: after store mutations through the
+controller (updatePolicySet / updatePolicy / updateRule / remove* / Map edits,
+accessController.ts:897-937), only the touched policy sets are recompiled
+(compiler.IncrementalCompiler) and the image equals a fresh compile of the same Map
+field for field, with interned ids compared as the strings they stand for.  Decisions
+through the CPU build of the core are identical to a fresh controller's."""
+import copy
+import random
+
+import numpy as np
+import pytest
+
+import host_core
+import randgen
+from oracle.acs_oracle import DEFAULT_CAS, FULL_URNS
+from acs_mi355x import compiler, encoder, store as pstore, synth, layout as L
+from acs_mi355x.controller import AccessController
+
+ID_FIELDS = ("role", "se", "last_prop_value")
+POOL_FIELDS = ("subj_off", "act_off", "res_off", "acl_roles_off")
+
+
+def canonical(cs):
+    """Tables with every interned id replaced by its string and pool offsets by contents."""
+    d = cs.dictionary
+
+    def s(i):
+        v = d.string(int(i))
+        return ("str", v) if isinstance(v, str) else repr(v)
+
+    def node(n):
+        rec = {k: int(n[k]) for k in L.NODE_DT.names if k not in ID_FIELDS + POOL_FIELDS + ("pad", "ec")}
+        rec.update({k: s(n[k]) for k in ID_FIELDS})
+        rec["ec"] = repr(cs.ec_values[int(n["ec"])])
+        if n["nflags"] & L.NF_HAS_TARGET:
+            rec["subj"] = [(s(p["id"]), s(p["value"])) for p in cs.pairs[n["subj_off"]:n["subj_off"] + n["subj_n"]]]
+            rec["act"] = [(s(p["id"]), s(p["value"])) for p in cs.pairs[n["act_off"]:n["act_off"] + n["act_n"]]]
+            rec["res"] = [(s(r["value"]), s(r["hash_sfx"]), int(r["kind"]),
+                           repr(cs.rx_rows[int(r["row"])]) if r["kind"] & L.K_ENT_LOOSE else None)
+                          for r in cs.rres[n["res_off"]:n["res_off"] + n["res_n"]]]
+            rec["acl"] = [s(x) for x in cs.u32pool[n["acl_roles_off"]:n["acl_roles_off"] + n["acl_roles_n"]]]
+        return rec
+
+    spec = [[None if sp is None else sorted(repr(cs.rx_rows[r]) for r in sp) for sp in sec] for sec in cs.cand_spec]
+    return ([node(n) for n in cs.sets], [node(n) for n in cs.pols], [node(n) for n in cs.rules], spec,
+            s(cs.id_user))
+
+
+def _ctl(urns):
+    return AccessController({"urns": urns, "combiningAlgorithms": DEFAULT_CAS}, engine=host_core.Tables)
+
+
+def _mutate(rng, ctl, pool_sets):
+    """One random store mutation through the reference's surface; returns its name."""
+    keys = list(ctl.policySets)
+    op = rng.choice(["updateRule", "removeRule", "updatePolicy", "removePolicy", "updatePolicySet",
+                     "removePolicySet", "map_set", "map_pop"])
+    if not keys:
+        op = "updatePolicySet"
+    k = rng.choice(keys) if keys else None
+    ps = ctl.policySets.get(k) if keys else None
+    pols = list(ps["combinables"]) if ps else []
+    donor = copy.deepcopy(rng.choice(pool_sets))
+    donor_pols = [p for p in donor["combinables"].values() if isinstance(p, dict)]
+    donor_rules = [r for p in donor_pols for r in p["combinables"].values() if isinstance(r, dict)]
+    if op == "updateRule" and pols and donor_rules:
+        pk = rng.choice(pols)
+        if isinstance(ps["combinables"][pk], dict):
+            r = copy.deepcopy(rng.choice(donor_rules))
+            ctl.updateRule(k, pk, r)
+    elif op == "removeRule" and pols:
+        pk = rng.choice(pols)
+        pol = ps["combinables"][pk]
+        if isinstance(pol, dict) and pol["combinables"]:
+            ctl.removeRule(k, pk, rng.choice(list(pol["combinables"])))
+    elif op == "updatePolicy" and donor_pols:
+        ctl.updatePolicy(k, copy.deepcopy(rng.choice(donor_pols)))
+    elif op == "removePolicy" and pols:
+        ctl.removePolicy(k, rng.choice(pols))
+    elif op == "updatePolicySet":
+        donor["id"] = f"new{rng.randrange(10**6)}" if rng.random() < 0.5 or not keys else k
+        ctl.updatePolicySet(donor)
+    elif op == "removePolicySet":
+        ctl.removePolicySet(k)
+    elif op == "map_set":
+        ctl.policySets[k] = donor
+    elif op == "map_pop":
+        ctl.policySets.pop(k)
+    return op
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_incremental_matches_fresh_compile(seed):
+    urns, doc, reqs = randgen.rand_case(seed)
+    try:
+        base = pstore.populate(doc)
+        compiler.compile_store(base, urns, DEFAULT_CAS)
+    except Exception:
+        pytest.skip("store outside the compiled subset")
+    donors = list(pstore.populate(randgen.rand_case(seed + 1000)[1]).values()) or list(base.values())
+    rng = random.Random(seed)
+    ctl = _ctl(urns)
+    ctl.policySets = base
+    ctl.isAllowed_batch(reqs[:1])
+    for step in range(6):
+        op = _mutate(rng, ctl, donors)
+        try:
+            got = ctl.isAllowed_batch(reqs)
+            fresh_cs = compiler.compile_store(ctl.policySets, urns, DEFAULT_CAS)
+        except Exception as e:  # a mutation can make the store unsupported: both paths must agree
+            with pytest.raises(type(e)):
+                compiler.compile_store(ctl.policySets, urns, DEFAULT_CAS)
+            return
+        assert canonical(ctl._cs) == canonical(fresh_cs), (seed, step, op)
+        fresh = _ctl(urns)
+        fresh.policySets = pstore.populate({"policy_sets": []}) if not ctl.policySets else dict(ctl.policySets)
+        want = fresh.isAllowed_batch(reqs)
+        assert [repr(x) for x in got] == [repr(x) for x in want], (seed, step, op)
+
+
+def test_incremental_recompiles_only_touched_sets():
+    doc = synth.c3_store()
+    ctl = _ctl(FULL_URNS)
+    ctl.policySets = pstore.populate(doc)
+    sb_cs = compiler.compile_store(ctl.policySets, FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(sb_cs, 2_000, "c3")
+    reqs = [sb.decode(i) for i in range(200)]
+    ctl.isAllowed_batch(reqs)
+    st = ctl._compiler.stats
+    assert st["sets_compiled"] == 200 and st["sets_reused"] == 0
+    keys = list(ctl.policySets)
+    ps = ctl.policySets[keys[7]]
+    pk = next(iter(ps["combinables"]))
+    rule = copy.deepcopy(next(iter(ps["combinables"][pk]["combinables"].values())))
+    rule["effect"] = "DENY" if rule.get("effect") == "PERMIT" else "PERMIT"
+    ctl.updateRule(keys[7], pk, rule)
+    got = ctl.isAllowed_batch(reqs)
+    assert st["sets_compiled"] == 201 and st["sets_reused"] == 199
+    ctl.removePolicySet(keys[3])
+    ctl.isAllowed_batch(reqs)
+    assert st["sets_compiled"] == 201 and st["sets_reused"] == 199 + 199
+    assert canonical(ctl._cs) == canonical(compiler.compile_store(ctl.policySets, FULL_URNS, DEFAULT_CAS))
+    fresh = _ctl(FULL_URNS)
+    fresh.policySets = dict(ctl.policySets)
+    assert [repr(x) for x in ctl.isAllowed_batch(reqs)] == [repr(x) for x in fresh.isAllowed_batch(reqs)]
+    assert got  # the updated rule was evaluated
+
+
+def test_fresh_compile_is_byte_stable():
+    """compile_store (one IncrementalCompiler pass) gives the same blob twice."""
+    m = pstore.populate(synth.c2_store())
+    a = compiler.store_blob(compiler.compile_store(m, FULL_URNS, DEFAULT_CAS))
+    b = compiler.store_blob(compiler.compile_store(m, FULL_URNS, DEFAULT_CAS))
+    assert a == b
+    ic = compiler.IncrementalCompiler(FULL_URNS, DEFAULT_CAS)
+    ic.compile(m)
+    assert compiler.store_blob(ic.compile(m, dirty=set())) == a  # all fragments reused
+    assert np.array_equal(np.frombuffer(a[:64], np.uint32)[2:5], [100, 200, 1000])
