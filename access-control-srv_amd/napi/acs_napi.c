@@ -284,6 +284,36 @@ static napi_value js_what_is_allowed(napi_env env, napi_callback_info info) {
   return res;
 }
 
+/* whatIsAllowedObl(handle, batch, idx: Uint32Array, chunks, cap) -> {obl, oblN}: the
+ * obligation-only pass (acs_what_is_allowed_obl) for requests whose whatIsAllowed record
+ * carries ACS_OF_OBL_OVERFLOW; obl [chunks][m][cap][2], oblN [chunks][m]. */
+static napi_value js_what_is_allowed_obl(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5], res;
+  acs_req_batch b;
+  void *idx, *obl, *obl_n;
+  size_t idx_len;
+  uint32_t chunks = 0, cap = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  acs_tables* t = argc == 5 ? get_handle(env, argv[0]) : NULL;
+  if (!t || read_batch(env, argv[1], &b) || get_bytes(env, argv[2], &idx, &idx_len) || idx_len % 4 ||
+      napi_get_value_uint32(env, argv[3], &chunks) != napi_ok || napi_get_value_uint32(env, argv[4], &cap) != napi_ok ||
+      chunks == 0 || chunks > 64 || cap == 0 || cap > (1u << 20)) {
+    napi_throw_type_error(env, NULL, "whatIsAllowedObl(handle, batch, idx: Uint32Array, chunks 1..64, cap 1..2^20)");
+    return NULL;
+  }
+  const size_t m = idx_len / 4;
+  napi_value a_obl = new_u32(env, m * chunks * (size_t)cap * 2, &obl);
+  napi_value a_obl_n = new_u32(env, m * chunks, &obl_n);
+  if (!a_obl || !a_obl_n) return NULL;
+  if (acs_what_is_allowed_obl(t, &b, (const uint32_t*)idx, m, chunks, cap, (uint32_t*)obl, (uint32_t*)obl_n) != 0)
+    return throw_acs(env, "acs_what_is_allowed_obl");
+  CHECK(env, napi_create_object(env, &res));
+  CHECK(env, napi_set_named_property(env, res, "obl", a_obl));
+  CHECK(env, napi_set_named_property(env, res, "oblN", a_obl_n));
+  return res;
+}
+
 /* ------------------------------------------------------------------ misc */
 static napi_value js_words(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -329,6 +359,7 @@ static napi_value init(napi_env env, napi_value exports) {
       {"isAllowed", NULL, js_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isAllowedAsync", NULL, js_is_allowed_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"whatIsAllowed", NULL, js_what_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"whatIsAllowedObl", NULL, js_what_is_allowed_obl, NULL, NULL, NULL, napi_enumerable, NULL},
       {"wordsPerRequest", NULL, js_words, NULL, NULL, NULL, napi_enumerable, NULL},
       {"layoutSizes", NULL, js_layout_sizes, NULL, NULL, NULL, napi_enumerable, NULL},
       {"deviceCount", NULL, js_device_count, NULL, NULL, NULL, napi_enumerable, NULL},

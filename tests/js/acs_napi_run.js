@@ -22,6 +22,11 @@ for (const k of ['hdr', 'res', 'subj', 'act', 'roles', 'arena', 'rx', 'cand']) b
   fs.writeFileSync(path.join(dir, 'wia_bits.bin'), Buffer.from(w.bits.buffer));
   fs.writeFileSync(path.join(dir, 'wia_obl_n.bin'), Buffer.from(w.oblN.buffer));
   fs.writeFileSync(path.join(dir, 'wia_out.bin'), w.out);
+  // obligation-only pass over the first 16 requests, 3 set ranges, 128-entry logs
+  const idx = new Uint32Array(16).map((_, i) => i);
+  const o = addon.whatIsAllowedObl(h, batch, idx, 3, 128);
+  fs.writeFileSync(path.join(dir, 'obl.bin'), Buffer.from(o.obl.buffer));
+  fs.writeFileSync(path.join(dir, 'obl_n.bin'), Buffer.from(o.oblN.buffer));
   addon.free(h);
   console.log(JSON.stringify({ ok: true, words: w.bits.length / meta.n }));
 })().catch((e) => { console.error(e); process.exit(1); });

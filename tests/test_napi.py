@@ -31,7 +31,7 @@ def test_addon_loads_with_surface():
     r = subprocess.run([NODE, "-e", js, p], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     info = json.loads(r.stdout.splitlines()[0])
-    assert info["keys"] == sorted(["compile", "free", "isAllowed", "isAllowedAsync", "whatIsAllowed",
+    assert info["keys"] == sorted(["compile", "free", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
                                    "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
     assert info["sizes"] == [64, 16, 16, 16, 8]
     assert "magic" in r.stdout.splitlines()[1]  # a bad image is rejected with acs_last_error's message
@@ -62,7 +62,10 @@ def test_node_batch_matches_c_abi(tmp_path):
     t = native.Tables(compiler.store_blob(cs), 0)
     want = t.is_allowed(sb.batch).view(np.uint8).reshape(-1)
     bits, obl, obl_n, out = t.what_is_allowed(sb.batch)
+    pobl, pobl_n = t.what_is_allowed_obl(sb.batch, np.arange(16, dtype=np.uint32), 128, 3)
     t.close()
+    assert np.array_equal(np.frombuffer(tmp_path.joinpath("obl_n.bin").read_bytes(), np.uint32), pobl_n.reshape(-1))
+    assert np.array_equal(np.frombuffer(tmp_path.joinpath("obl.bin").read_bytes(), np.uint32), pobl.reshape(-1))
     for f in ("out_sync.bin", "out_async.bin"):
         assert np.array_equal(np.frombuffer(tmp_path.joinpath(f).read_bytes(), np.uint8), want), f
     assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_bits.bin").read_bytes(), np.uint32),
