@@ -156,3 +156,38 @@ def test_fresh_compile_is_byte_stable():
     ic.compile(m)
     assert compiler.store_blob(ic.compile(m, dirty=set())) == a  # all fragments reused
     assert np.array_equal(np.frombuffer(a[:64], np.uint32)[2:5], [100, 200, 1000])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_incremental_gpu(seed):
+    """The same mutation sequences through the default (GPU) engine: every recompiled image
+    decides like a fresh controller's, and whatIsAllowed agrees too."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    urns, doc, reqs = randgen.rand_case(seed)
+    try:
+        base = pstore.populate(doc)
+        compiler.compile_store(base, urns, DEFAULT_CAS)
+    except Exception:
+        pytest.skip("store outside the compiled subset")
+    donors = list(pstore.populate(randgen.rand_case(seed + 1000)[1]).values()) or list(base.values())
+    rng = random.Random(seed)
+    opts = {"urns": urns, "combiningAlgorithms": DEFAULT_CAS}
+    ctl = AccessController(opts)
+    ctl.policySets = base
+    ctl.isAllowed_batch(reqs[:1])
+    for step in range(5):
+        op = _mutate(rng, ctl, donors)
+        try:
+            got = ctl.isAllowed_batch(reqs)
+            got_w = ctl.whatIsAllowed_batch(reqs)
+        except Exception:
+            return  # an unsupported store: covered by the CPU test's both-paths-agree check
+        fresh = AccessController(opts)
+        fresh.policySets = dict(ctl.policySets)
+        assert [repr(x) for x in got] == [repr(x) for x in fresh.isAllowed_batch(reqs)], (seed, step, op)
+        assert [repr(x) for x in got_w] == [repr(x) for x in fresh.whatIsAllowed_batch(reqs)], (seed, step, op)
+        fresh.close()
+    ctl.close()

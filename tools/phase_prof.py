@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where K1's time goes: per-phase lane-cycles from the -DACS_PHASE_PROF build.
 
-usage: python tools/phase_prof.py [c2|c3] [requests]
+usage: python tools/phase_prof.py [c2|c3|c5] [requests]
 Prints, per phase, the share of lane-cycles inside is_allowed_t (set targets, the
 exact-policy scan, multi-entity check, policy targets, rule targets, HR, ACL; the
 rest is iteration / bookkeeping) and the kernel time of the profiling build.
@@ -30,9 +30,9 @@ def main():
     lib_path = build.build_prof()
     lib = native.load(lib_path)
     lib.acs_phase_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    cs = compiler.compile_store(store.populate(synth.c2_store() if kind == "c2" else synth.c3_store()),
-                                FULL_URNS, DEFAULT_CAS)
-    sb = synth.requests(cs, n, kind)
+    mk = {"c2": synth.c2_store, "c3": synth.c3_store, "c5": synth.c5_store}[kind]
+    cs = compiler.compile_store(store.populate(mk()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, n, "c2" if kind == "c2" else "c3")
     t = native.Tables(compiler.store_blob(cs), 0)
     t.set_timing(True)
     db = DeviceBatch(sb.batch, 0)
