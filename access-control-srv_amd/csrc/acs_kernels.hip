@@ -17,6 +17,23 @@
 #include "acs_eval.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+
+// Coherence-sort algorithm.  rocprim's default dispatch runs a block sort + ~10 merge
+// passes for n <= 2^20 (c2's whole 1M batch: 0.17 ms); a merge-sort limit of 0 forces the
+// onesweep radix passes over [0, end_bit).  Both are stable sorts of the same keys, so the
+// permutation is identical.  -DACS_SORT_HIPCUB keeps the default dispatch (A/B variant).
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                           rocprim::default_config, 0>;
+static hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout,
+                             const uint32_t* vin, uint32_t* vout, int n, int end_bit, hipStream_t s) {
+#if defined(ACS_SORT_HIPCUB)
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, end_bit, s);
+#else
+  return rocprim::radix_sort_pairs<SortCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                            (unsigned)end_bit, s);
+#endif
+}
 
 using namespace acs;
 
@@ -43,7 +60,10 @@ constexpr int BLOCK = 256;
 // candidate nodes), and unfiltered requests (PCOL_ALL) take bucket 0, so the longest
 // waves start first and the launch has no long tail.  Unfiltered requests group by
 // their first entity id.
-__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __restrict__ keys,
+// The low field keeps `lowbits` bits (role keys are dense, so all of them; action ids and
+// entity ids are folded mod 2^lowbits): fewer key bits, fewer onesweep passes.  A fold
+// collision only merges two groups, which costs coherence, never correctness.
+__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t* __restrict__ keys,
                                                           uint32_t* __restrict__ idx) {
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   if (k >= B.n) return;
@@ -60,7 +80,7 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t* __r
       }
     }
   }
-  keys[k] = (bucket << 16) | (low & 0xFFFFu);
+  keys[k] = (bucket << lowbits) | (low & ((1u << lowbits) - 1u));
   idx[k] = k;
 }
 
@@ -506,11 +526,18 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   *perm = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
-  int end_bit = 16;  // keys < (cand_rows + 1) << 16
-  while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - 16)) != 0) ++end_bit;
+  uint32_t lowbits = 8;  // action / entity ids folded to 8 bits
+  if (B.role_key) {
+    lowbits = 1;
+    while (lowbits < 16 && (B.role_rows - 1) >> lowbits) ++lowbits;
+  }
+#if defined(ACS_SORT_KEY16)
+  lowbits = 16;  // A/B variant: the unfolded 16-bit low field
+#endif
+  int end_bit = (int)lowbits;  // keys < (cand_rows + 1) << lowbits
+  while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - lowbits)) != 0) ++end_bit;
   size_t temp = 0;
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                            (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, end_bit, s));
+  HIP_OK(sort_pairs(nullptr, temp, nullptr, nullptr, nullptr, nullptr, (int)n, end_bit, s));
   const size_t need = 4 * n * sizeof(uint32_t) + temp + 256;
   if (need > t->ws_bytes) {
     if (t->ws) HIP_OK(hipFree(t->ws));
@@ -524,9 +551,9 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   uint32_t* idx_in = keys_out + n;
   uint32_t* idx_out = idx_in + n;
   void* tmp = (void*)(((uintptr_t)(idx_out + n) + 255) & ~uintptr_t(255));
-  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, B, keys_in, idx_in);
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, B, lowbits, keys_in, idx_in);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, 0, end_bit, s));
+  HIP_OK(sort_pairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, end_bit, s));
   *perm = idx_out;
   return 0;
 }
