@@ -173,6 +173,25 @@ __device__ inline uint32_t request_pcol(const ReqHdr& h) {
 __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 
+// XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs round-robin
+// (block b -> XCD b % 8), and each XCD has its own L2.  After the coherence sort, runs of
+// neighbouring blocks share a request class and so the same candidate nodes; remapping
+// each group of 8*G consecutive blocks so that XCD x takes the logical blocks
+// [x*G, x*G+G) of the group keeps a class's table reads in one L2 instead of eight.
+// Groups stay in launch order (heaviest classes first); the partial last group is
+// identity-mapped.  G = 0 disables the remap.
+#ifndef ACS_XCD_GROUP
+#define ACS_XCD_GROUP 0
+#endif
+__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
+  constexpr uint32_t G = ACS_XCD_GROUP, NX = 8;
+  if (G == 0) return b;
+  const uint32_t span = NX * G;
+  if (b >= nb / span * span) return b;
+  const uint32_t r = b % span;
+  return b - r + (r % NX) * G + r / NX;
+}
+
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
 #define ACS_K1_WAVES_PER_EU 4  // measured: 4 waves/SIMD (VGPR <= 128) beats 3 (+12% c2, +13% c3), 5+ spill
@@ -180,7 +199,7 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t k = xcd_block(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
   ReqHdr h{};

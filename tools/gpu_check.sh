@@ -38,6 +38,11 @@ for s in $STEPS; do
           step "bench_c3_$v" 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie \
             --lib access-control-srv_amd/lib/variants/$v.so
         done ;;
+    quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
+    ab5) for v in ${VARIANTS:-scalar_tables}; do
+          step "bench_c5_$v" 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
+            --lib access-control-srv_amd/lib/variants/$v.so
+        done ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
     c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
     c5shard) step bench_c5_rule_shard 1200 python bench.py --config c5 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
