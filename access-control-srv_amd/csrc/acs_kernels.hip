@@ -325,12 +325,18 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
 // reads 256 contiguous bytes of a tmp row, every store instruction writes 256 contiguous
 // bytes (64 words) of one output row — both fully coalesced (the previous 32-word tile
 // stored 4-byte pieces of 16 rows per instruction: 1.29 ms for 1M c4 rows).
+// Tile order (ACS_TP_MODE): output rows are `words` u32 long (c4: 1400 B), so a row's
+// 256-B segments are not line-aligned and neighbouring segments share cache lines.
+//   0: grid (column tiles, word tiles) — a row's segments are written far apart in time;
+//   1: grid (word tiles, column tiles) — a row's segments are written by consecutive blocks;
+//   2: one block per column tile walks all word tiles — each row written by one block.
+#ifndef ACS_TP_MODE
+#define ACS_TP_MODE 0
+#endif
 constexpr uint32_t TP_COLS = 64, TP_WORDS = 64;
-__global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t* __restrict__ tmp, uint32_t n,
-                                                                 uint32_t words, const uint32_t* __restrict__ perm,
-                                                                 uint32_t* __restrict__ bits) {
-  __shared__ uint32_t tile[TP_WORDS][TP_COLS + 1];
-  const uint32_t k0 = blockIdx.x * TP_COLS, w0 = blockIdx.y * TP_WORDS;
+__device__ inline void transpose_tile(uint32_t (*tile)[TP_COLS + 1], const uint32_t* __restrict__ tmp, uint32_t n,
+                                      uint32_t words, const uint32_t* __restrict__ perm, uint32_t* __restrict__ bits,
+                                      uint32_t k0, uint32_t w0) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   for (uint32_t r = wave; r < TP_WORDS; r += BLOCK / 64) {
     const uint32_t w = w0 + r, k = k0 + lane;
@@ -343,6 +349,32 @@ __global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t*
     if (k >= n) break;
     if (w < words) bits[(size_t)(perm ? perm[k] : k) * words + w] = tile[lane][r];
   }
+}
+__global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t* __restrict__ tmp, uint32_t n,
+                                                                 uint32_t words, const uint32_t* __restrict__ perm,
+                                                                 uint32_t* __restrict__ bits) {
+  __shared__ uint32_t tile[TP_WORDS][TP_COLS + 1];
+#if ACS_TP_MODE == 2
+  for (uint32_t w0 = 0; w0 < words; w0 += TP_WORDS) {
+    transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.x * TP_COLS, w0);
+    __syncthreads();  // the tile is reused by the next word range
+  }
+#elif ACS_TP_MODE == 1
+  transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.y * TP_COLS, blockIdx.x * TP_WORDS);
+#else
+  transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.x * TP_COLS, blockIdx.y * TP_WORDS);
+#endif
+}
+static dim3 transpose_grid(uint32_t n, uint32_t words) {
+  const uint32_t ct = (n + TP_COLS - 1) / TP_COLS, wt = (words + TP_WORDS - 1) / TP_WORDS;
+#if ACS_TP_MODE == 2
+  (void)wt;
+  return dim3(ct);
+#elif ACS_TP_MODE == 1
+  return dim3(wt, ct);
+#else
+  return dim3(ct, wt);
+#endif
 }
 
 __global__ __launch_bounds__(BLOCK) void shard_key_kernel(Tables T, const Decision* __restrict__ d, uint32_t n,
@@ -632,8 +664,7 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
                      (uint32_t*)t->wbuf, obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (words) {
-    hipLaunchKernelGGL(bitset_transpose_kernel, dim3((b->n + TP_COLS - 1) / TP_COLS, (words + TP_WORDS - 1) / TP_WORDS),
-                       dim3(BLOCK), 0, s, (const uint32_t*)t->wbuf, b->n, words, perm, bits);
+    hipLaunchKernelGGL(bitset_transpose_kernel, transpose_grid(b->n, words), dim3(BLOCK), 0, s, (const uint32_t*)t->wbuf, b->n, words, perm, bits);
     HIP_OK(hipGetLastError());
   }
   if (t->timing) {

@@ -43,11 +43,17 @@ for s in $STEPS; do
           step "bench_c5_$v" 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
             --lib access-control-srv_amd/lib/variants/$v.so
         done ;;
+    quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
+    ab4) for v in ${VARIANTS:-scalar_tables}; do
+          step "bench_c4_$v" 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie \
+            --lib access-control-srv_amd/lib/variants/$v.so
+        done ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
     c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
     c5shard) step bench_c5_rule_shard 1200 python bench.py --config c5 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
     shard) step bench_rule_shard 600 python bench.py --rule-shard --steps 20 --warmup 3 --no-cpu-baseline ;;
     shard3) step bench_c3_rule_shard 900 python bench.py --config c3 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
+    prof4) step rocprof_c4 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
   esac
 done
