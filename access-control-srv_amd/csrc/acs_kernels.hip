@@ -577,7 +577,10 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   *perm = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
-  uint32_t lowbits = 8;  // action / entity ids folded to 8 bits
+#ifndef ACS_SORT_LOWBITS
+#define ACS_SORT_LOWBITS 4
+#endif
+  uint32_t lowbits = ACS_SORT_LOWBITS;  // action / entity ids folded to 4 bits (c2: 16-bit keys, 2 passes)
   if (B.role_key) {
     lowbits = 1;
     while (lowbits < 16 && (B.role_rows - 1) >> lowbits) ++lowbits;
@@ -587,6 +590,7 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
 #endif
   int end_bit = (int)lowbits;  // keys < (cand_rows + 1) << lowbits
   while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - lowbits)) != 0) ++end_bit;
+  if (end_bit < 1) end_bit = 1;
   size_t temp = 0;
   HIP_OK(sort_pairs(nullptr, temp, nullptr, nullptr, nullptr, nullptr, (int)n, end_bit, s));
   const size_t need = 4 * n * sizeof(uint32_t) + temp + 256;
