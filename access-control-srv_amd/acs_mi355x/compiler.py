@@ -483,7 +483,7 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
 def store_blob(cs: CompiledStore) -> bytes:
     """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header)."""
     import struct
-    hdr = struct.pack("<16I", 0x31534341, 3, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
+    hdr = struct.pack("<16I", 0x31534341, 4, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
                       len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0, 0)
     parts = [hdr]
     for a in (cs.sets, cs.pols, cs.rules, cs.rres, cs.pairs, cs.u32pool):

@@ -7,13 +7,18 @@ Both depend only on the two strings, so they are tabulated once per
 (row value, column value) pair and the kernel reads one byte per pair.
 
 JS RegExp semantics are reproduced exactly for literal patterns (substring
-search) and for a conservative metacharacter subset; any other pattern is
-marked RX_HOST so the kernel reports the request to the host instead of
-guessing.
+search) and for a conservative metacharacter subset, translated to Python ``re``
+where the two engines differ (``$`` is end of input in V8 but also matches before
+a trailing newline in Python, so it becomes ``\Z``); any other pattern is marked
+RX_HOST so the kernel reports the request to the host instead of guessing.  The
+subset is pinned against V8 itself: tests/golden/regex_cells.json (written by
+tests/golden/gen_regex_cells.js under node) holds ~10k (rule value, request value)
+cells and tests/test_regex_v8.py requires every non-host cell to equal V8's.
 """
 from __future__ import annotations
 
 import re
+import warnings
 
 from .jsops import nullish
 from .layout import RX_HIT, RX_RESET, RX_THROW_TYPE, RX_THROW_SYNTAX, RX_HOST
@@ -30,13 +35,33 @@ def _split_entity(v: str):
     return prefix, segs[0], segs[-1]
 
 
+def _to_python(pattern: str) -> str:
+    """The safe-subset JS pattern as a Python ``re`` pattern with the same matches: an
+    unescaped ``$`` outside a character class asserts end of input (V8, no multiline flag)
+    -> ``\Z``.  ``[]`` / ``[^]`` (JS: empty / any-char classes) never reach here, so a
+    ``]`` inside a class always closes it, in both engines."""
+    out, in_class = [], False
+    for ch in pattern:
+        if in_class:
+            in_class = ch != "]"
+            out.append(ch)
+        elif ch == "[":
+            in_class = True
+            out.append(ch)
+        else:
+            out.append(r"\Z" if ch == "$" else ch)
+    return "".join(out)
+
+
 def _regex_hit(pattern: str, subject: str):
     if _LITERAL.match(pattern):
         return RX_HIT if pattern in subject else 0
     if not _SAFE.match(pattern) or "(?" in pattern or "[]" in pattern or "[^]" in pattern:
         return RX_HOST
     try:
-        rx = re.compile(pattern)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # "possible nested set" for '[[' (a literal '[' in both engines)
+            rx = re.compile(_to_python(pattern))
     except re.error:
         return RX_THROW_SYNTAX
     return RX_HIT if rx.search(subject) else 0

@@ -85,11 +85,23 @@ def fold_obligations(cs, overlay, pairs):
     return out
 
 
+def bits_layout(n_sets, n_pols, n_rules):
+    """Word offsets of the policy / rule sections and the row length of a whatIsAllowed
+    inclusion bitset (csrc/acs_eval.h BitsLayout): each section starts on a 4-word boundary."""
+    def up4(x):
+        return (x + 3) & ~3
+    wp = up4((n_sets + 31) // 32)
+    wr = wp + up4((n_pols + 31) // 32)
+    return wp, wr, wr + up4((n_rules + 31) // 32)
+
+
 def inclusion(cs, bits_row):
     """Bitset row -> (set indices, policy indices, rule indices)."""
     b = np.unpackbits(bits_row.view(np.uint8), bitorder="little")
     ns, npol, nr = cs.n_sets, cs.n_pols, cs.n_rules
-    return (np.flatnonzero(b[:ns]), np.flatnonzero(b[ns:ns + npol]), np.flatnonzero(b[ns + npol:ns + npol + nr]))
+    wp, wr, _ = bits_layout(ns, npol, nr)
+    return (np.flatnonzero(b[:ns]), np.flatnonzero(b[32 * wp:32 * wp + npol]),
+            np.flatnonzero(b[32 * wr:32 * wr + nr]))
 
 
 def _pick(obj, keys):

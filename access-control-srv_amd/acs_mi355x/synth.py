@@ -103,27 +103,28 @@ class OrgTree:
 
     def subtree_json(self, k, role=None):
         """hierarchical_scopes entry for the subtree rooted at k (role on the root only).
-        Memoised: requests scoped at the same org share one (read-only) JSON tree."""
+        Memoised, and every node's dict is built once for the whole tree: a subtree is
+        shared, read-only, by its parent and by every request scoped at it."""
         memo = self.__dict__.setdefault("_json_memo", {})
         if (k, role) not in memo:
-            memo[(k, role)] = self._subtree_json(k, role)
+            if role is not None:
+                n = self.subtree_json(k)
+                memo[(k, role)] = {"id": n["id"], "role": role, **({"children": n["children"]} if "children" in n else {})}
+            else:
+                # children first (deepest level up), so each node is built from memoised kids
+                for x in sorted(self._subtree_nodes(k), key=lambda x: -int(self.level[x])):
+                    if (x, None) in memo:
+                        continue
+                    d = int(self.level[x])
+                    out = {"id": self.name(x)}
+                    if d + 1 < self.depth:
+                        stride = self.level_sizes[d + 1]
+                        out["children"] = [memo[(x + 1 + c * stride, None)] for c in range(self.fanout)]
+                    memo[(x, None)] = out
         return memo[(k, role)]
 
-    def _subtree_json(self, k, role=None):
-        def node(x):
-            d = int(self.level[x])
-            out = {"id": self.name(x)}
-            if d + 1 < self.depth:
-                kids, c = [], x + 1
-                for _ in range(self.fanout):
-                    kids.append(node(c))
-                    c += self.level_sizes[d + 1]
-                out["children"] = kids
-            return out
-        n = node(k)
-        if role is not None:
-            n = {"id": n["id"], "role": role, **({"children": n["children"]} if "children" in n else {})}
-        return n
+    def _subtree_nodes(self, k):
+        return range(k, k + int(self.size[k]))
 
     def contains(self, root, x):
         return root <= x < root + self.size[root]
@@ -271,8 +272,11 @@ class SynthBatch:
     kind: str
     tree: OrgTree | None = None
 
-    def decode(self, i):
-        """JSON request (post-unmarshall shape) for packed request i."""
+    def decode(self, i, shared=None):
+        """JSON request (post-unmarshall shape) for packed request i.  ``shared``: a
+        SharedValues table — the request's hierarchical_scopes tree (up to 21,845 orgs at
+        c3) is then the placeholder {"$shared": k} for the table's k-th value, which the C++
+        oracle parses once for all the requests naming it (oracle/acs_oracle_c.COracle.raw)."""
         d = {k: v[i] for k, v in self.draws.items()}
         e, r, a, u = int(d["ent"]), int(d["role"]), int(d["act"]), int(d["user"])
         res = [{"id": URN["entity"], "value": entity(e)},
@@ -295,12 +299,29 @@ class SynthBatch:
             subj["role_associations"] = [{"role": role(r), "attributes": [
                 {"id": URN["rse"], "value": ORG_ENTITY,
                  "attributes": [{"id": URN["rsi"], "value": t.name(scope)}]}]}]
-            subj["hierarchical_scopes"] = [t.subtree_json(scope, role(r))]
+            tree = t.subtree_json(scope, role(r))
+            if shared is not None and "children" in tree:  # one shared children list per scope org
+                tree = dict(tree, children=shared.ref(scope, tree["children"]))
+            subj["hierarchical_scopes"] = [tree]
             owner = int(d["owner"])
             req["context"] = {"subject": subj, "resources": [{"id": f"res{int(d['rid'])}", "meta": {"owners": [
                 {"id": URN["ownerEntity"], "value": ORG_ENTITY,
                  "attributes": [{"id": URN["ownerInstance"], "value": t.name(owner)}]}]}}]}
         return req
+
+
+class SharedValues:
+    """Values shared by many decoded requests, referenced as {"$shared": k}."""
+
+    def __init__(self):
+        self.index, self.values = {}, []
+
+    def ref(self, key, value):
+        k = self.index.get(key)
+        if k is None:
+            k = self.index[key] = len(self.values)
+            self.values.append(value)
+        return {"$shared": k}
 
 
 def _vocab(cs: CompiledStore, ov: Overlay):

@@ -68,50 +68,15 @@ struct Tables {
   const uint32_t* u32pool;
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
-  uint64_t lo, hi;   // device: lowest / highest record address inside the table allocation
 };
-
-#if defined(ACS_CHECK_UNIFORM)
-__device__ unsigned long long acs_nonuniform[4];  // debug build only
-#endif
 
 // Table records are read as whole dwords and unpacked in registers: with a wave-uniform
 // address this is one s_load_dwordx{2,4,8,16} (scalar loads have no byte / short forms).
 template <class X, int NW = sizeof(X) / 4>
 ACS_FN X load_words(const Tables& T, const X* p) {
   static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
-#if defined(__HIP_DEVICE_COMPILE__) && defined(ACS_SCALAR_TABLES)
-  // EXPERIMENTAL, off by default: every caller passes a wave-uniform record
-  // address, so re-asserting it with readfirstlane and reading through the constant
-  // address space gives one scalar load per record instead of per-lane vector loads
-  // (c2 K1 1.87 -> 1.54 ms).  But scalar instructions run whatever the exec mask, and in
-  // blocks the compiler enters with no active lane readfirstlane returns a stale lane-0
-  // value; measured on MI355X, such stale scalar loads leak into live lanes' results
-  // (wrong decisions on the golden vectors, or illegal addresses without the clamp
-  // below), and the exec guard only hides it for some code layouts.  The product keeps
-  // vector loads until the node loops are restructured so that no table load sits in a
-  // divergent region.
-  if (__builtin_amdgcn_read_exec() == 0) return X{};
-  typedef __attribute__((address_space(4))) const uint32_t const_u32;
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  uint64_t u = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32 |
-               __builtin_amdgcn_readfirstlane((uint32_t)a);
-#if defined(ACS_CHECK_UNIFORM)  // debug build: count loads whose address differs across active lanes
-  {
-    const uint64_t ex = __builtin_amdgcn_read_exec();
-    const uint64_t diff = __ballot(a != u);
-    if (diff != 0 && (uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(ex)) {
-      atomicAdd(&acs_nonuniform[0], 1ull);
-      atomicAdd(&acs_nonuniform[sizeof(X) == 64 ? 1 : sizeof(X) == 16 ? 2 : 3], 1ull);
-    }
-  }
-#endif
-  u = u < T.lo ? T.lo : (u > T.hi ? T.hi : u);
-  const const_u32* w = (const const_u32*)(uintptr_t)u;
-#else
   (void)T;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
-#endif
   uint32_t v[NW];
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_NO_VLR)
   // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
@@ -912,20 +877,75 @@ ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
 }
 
 // ------------------------------------------------------------------ whatIsAllowed
-// bits: [sets | policies | rules] inclusion bitset of this request (words_per_req u32).
-template <class RQ>
-// bits: word w of this request's bitset lives at bits[w * stride] (1: a row; the GPU writes
-// a column of a word-major [words][n] buffer so a wave's stores coalesce)
+// Inclusion bitset row of one request: sets | policies | rules, each section starting on a
+// 4-word (16-B) boundary, so a section's 16-B chunks belong to it alone.
+struct BitsLayout {
+  uint32_t wp, wr, words;  // word offsets of the policy / rule sections, row length (multiple of 4)
+};
+ACS_FN uint32_t up4(uint32_t x) { return (x + 3u) & ~3u; }
+ACS_FN BitsLayout bits_layout(uint32_t n_sets, uint32_t n_pols, uint32_t n_rules) {
+  BitsLayout L;
+  L.wp = up4((n_sets + 31u) / 32u);
+  L.wr = L.wp + up4((n_pols + 31u) / 32u);
+  L.words = L.wr + up4((n_rules + 31u) / 32u);
+  return L;
+}
+
+// Bit sinks.  whatIsAllowed visits sets, policies and rules in ascending index order within
+// each section, so each section's bits arrive with non-decreasing word index.
+struct NullSink {  // the obligation-only pass: no bitset
+  template <int S> ACS_FN void set(uint32_t, uint32_t) {}
+  ACS_FN void finish() {}
+};
+struct RowSink {   // host build: OR into a zeroed row
+  uint32_t* row;
+  template <int S> ACS_FN void set(uint32_t w, uint32_t bit) { row[w] |= bit; }
+  ACS_FN void finish() {}
+};
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// GPU: each section's current 16-B chunk is accumulated in registers and stored once when the
+// traversal moves past it; the chunks it skipped are stored as zeros.  Every word of the
+// row is written exactly once (no zeroing pass, no read-modify-write, no scratch), 16 B per
+// store, and a lane writes its row front to back, so L2 merges the pieces into whole lines.
+struct ChunkSink {
+  uint4* row;
+  uint32_t cur[3], lim[3];
+  uint4 buf[3];
+  ACS_FN ChunkSink(uint32_t* r, const BitsLayout& L) : row(reinterpret_cast<uint4*>(r)) {
+    cur[0] = 0; lim[0] = L.wp >> 2;
+    cur[1] = L.wp >> 2; lim[1] = L.wr >> 2;
+    cur[2] = L.wr >> 2; lim[2] = L.words >> 2;
+    for (int k = 0; k < 3; ++k) buf[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  template <int S> ACS_FN void flush(uint32_t upto) {
+    row[cur[S]] = buf[S];
+    for (uint32_t c = cur[S] + 1; c < upto; ++c) row[c] = make_uint4(0u, 0u, 0u, 0u);
+    cur[S] = upto;
+    buf[S] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  template <int S> ACS_FN void set(uint32_t w, uint32_t bit) {
+    const uint32_t c = w >> 2, q = w & 3u;
+    if (c != cur[S]) flush<S>(c);
+    buf[S].x |= q == 0u ? bit : 0u;
+    buf[S].y |= q == 1u ? bit : 0u;
+    buf[S].z |= q == 2u ? bit : 0u;
+    buf[S].w |= q == 3u ? bit : 0u;
+  }
+  ACS_FN void finish() {
+    if (cur[0] < lim[0]) flush<0>(lim[0]);
+    if (cur[1] < lim[1]) flush<1>(lim[1]);
+    if (cur[2] < lim[2]) flush<2>(lim[2]);
+  }
+};
+#endif
+
 // [s_begin, s_end): the policy sets evaluated (whatIsAllowed keeps no state across sets but the
 // push log, so a request's log is the concatenation of the logs of consecutive set ranges).
-ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, size_t stride, OblLog& obl,
+template <class RQ, class Sink>
+ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, const BitsLayout& BL, Sink& bits, OblLog& obl,
                                   uint32_t s_begin = 0, uint32_t s_end = NONE32) {
   const Tables& T = R.T;
   Decision out{};
-  auto setbit = [&](uint32_t b) {  // bits == nullptr: the obligation-only pass
-    if (bits) bits[(size_t)(b >> 5) * stride] |= 1u << (b & 31);
-  };
-  const uint32_t pol_base = T.n_sets, rule_base = T.n_sets + T.n_pols;
   CandRange sets(F, 0, s_begin, s_end < T.n_sets ? s_end : T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
@@ -982,22 +1002,23 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, uint32_t* bits, 
           if (m < 0) return make_err(m, s + 1);
         }
         if (m) {
-          setbit(rule_base + r);
+          bits.template set<2>(BL.wr + (r >> 5), 1u << (r & 31));
           any_rule = true;
         }
       }
       if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
-        setbit(pol_base + p);
+        bits.template set<1>(BL.wp + (p >> 5), 1u << (p & 31));
         any_pol = true;
       }
     }
-    if (any_pol) setbit(s);
+    if (any_pol) bits.template set<0>(s >> 5, 1u << (s & 31));
   }
   if (obl.overflow) out.flags |= OF_OBL_OVERFLOW;
   return out;
 }
 
-ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* bits, uint32_t* obl_out,
+// Host build: row = this request's zeroed BitsLayout row.
+ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* row, uint32_t* obl_out,
                                 uint32_t* obl_n) {
   const ReqHdr h = B.hdr[i];
   OblLog obl{obl_out, 0, false};
@@ -1005,7 +1026,9 @@ ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uin
   if (h.flags & RQ_HOST) {
     d.flags = OF_HOST_REQ;
   } else {
-    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits, 1, obl);
+    RowSink sink{row};
+    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits_layout(T.n_sets, T.n_pols, T.n_rules),
+                          sink, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;
   return d;

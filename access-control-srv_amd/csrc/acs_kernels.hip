@@ -4,36 +4,21 @@
 //                             table records via wave-uniform (scalar) loads, request
 //                             SoA rows via coalesced vector loads; 8 B decision out.
 // K2 what_is_allowed_kernel : same traversal without HR/ACL/condition/combine; writes
-//                             the (sets|policies|rules) inclusion bitset + mask log.
+//                             each request's (sets|policies|rules) inclusion bitset row
+//                             once, 16 B at a time, + the maskedProperty log.
+// Coherence sort            : hand-written LSD radix sort (8-bit digits) of the
+//                             (class, low) keys -> the permutation K1 / K2 run in.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/acs_mi355x.h"
 #include "acs_eval.h"
-
-#include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
-
-// Coherence-sort algorithm.  rocprim's default dispatch runs a block sort + ~10 merge
-// passes for n <= 2^20 (c2's whole 1M batch: 0.17 ms); a merge-sort limit of 0 forces the
-// onesweep radix passes over [0, end_bit).  Both are stable sorts of the same keys, so the
-// permutation is identical.  -DACS_SORT_HIPCUB keeps the default dispatch (A/B variant).
-using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                           rocprim::default_config, 0>;
-static hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout,
-                             const uint32_t* vin, uint32_t* vout, int n, int end_bit, hipStream_t s) {
-#if defined(ACS_SORT_HIPCUB)
-  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, end_bit, s);
-#else
-  return rocprim::radix_sort_pairs<SortCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u,
-                                            (unsigned)end_bit, s);
-#endif
-}
 
 using namespace acs;
 
@@ -56,17 +41,14 @@ constexpr int BLOCK = 256;
 
 // Sort key that makes a wave share its request class (one candidate row) and action — or,
 // with a role factor, its role key — so table-driven branches are wave-uniform:
-// [bucket:16 | action id or role key:16].  Class ids come heaviest-first from the host (most
-// candidate nodes), and unfiltered requests (PCOL_ALL) take bucket 0, so the longest
-// waves start first and the launch has no long tail.  Unfiltered requests group by
-// their first entity id.
-// The low field keeps `lowbits` bits (role keys are dense, so all of them; action ids and
-// entity ids are folded mod 2^lowbits): fewer key bits, fewer onesweep passes.  A fold
-// collision only merges two groups, which costs coherence, never correctness.
-__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t* __restrict__ keys,
-                                                          uint32_t* __restrict__ idx) {
-  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  if (k >= B.n) return;
+// [bucket | low field].  Class ids come heaviest-first from the host (most candidate
+// nodes), and unfiltered requests (PCOL_ALL) take bucket 0, so the longest waves start
+// first and the launch has no long tail.  Unfiltered requests group by their first entity
+// id.  The low field keeps `lowbits` bits (role keys are dense, so all of them; action and
+// entity ids are folded mod 2^lowbits): fewer key bits, fewer radix passes.  A fold
+// collision only merges two groups, which costs coherence, never correctness: results are
+// written to out[perm[k]], so any permutation gives the same records.
+__device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits) {
   const ReqHdr h = B.hdr[k];
   const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
   uint32_t low = B.role_key ? B.role_key[k] : (h.nact ? B.act[k].value : 0u), bucket = cls + 1;
@@ -80,8 +62,142 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowb
       }
     }
   }
-  keys[k] = (bucket << lowbits) | (low & ((1u << lowbits) - 1u));
-  idx[k] = k;
+  return (bucket << lowbits) | (low & ((1u << lowbits) - 1u));
+}
+
+// ---------------------------------------------------------------- LSD radix sort
+// Keys of up to 32 bits, 8-bit digits, ceil(end_bit / 8) passes.  Each pass:
+//   histogram  per 2048-key tile, counts[tile][digit] (written whole — no memset);
+//   tile scan  per group of 64 tiles, one thread per digit: the exclusive prefix over the
+//              group's tiles (in place) and the group total gsum[group][digit];
+//   group scan one block: per digit, the exclusive prefix over groups, then the digit
+//              bases (exclusive scan of the 256 digit totals) folded in;
+//   scatter    stable: a tile is ranked 256 keys per round in index order; inside a wave,
+//              lanes with equal digits are found with 8 ballots (one per digit bit) and
+//              ranked by the popcount of the lower lanes; the waves' per-digit counts go
+//              through LDS.  Position = gbase[group][d] + counts[tile][d] + rank.
+// Pass 0's histogram is fused into the key kernel.
+constexpr uint32_t SORT_ITEMS = 8;                    // keys per thread per tile
+constexpr uint32_t SORT_TILE = BLOCK * SORT_ITEMS;    // 2048
+constexpr uint32_t RADIX = 256;
+constexpr uint32_t SCAN_GROUP = 64;                   // tiles per tile-scan group
+
+__device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_null, const Batch* B,
+                                      uint32_t lowbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
+                                      uint32_t shift, uint32_t* counts) {
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * SORT_TILE;
+  for (uint32_t r = 0; r < SORT_ITEMS; ++r) {
+    const uint32_t i = t0 + r * BLOCK + threadIdx.x;
+    if (i >= n) break;
+    uint32_t key;
+    if (B) {
+      key = sort_key(*B, i, lowbits);
+      keys_out[i] = key;
+      idx_out[i] = i;
+    } else {
+      key = keys_or_null[i];
+    }
+    atomicAdd(&hist[(key >> shift) & (RADIX - 1)], 1u);
+  }
+  __syncthreads();
+  counts[(size_t)blockIdx.x * RADIX + threadIdx.x] = hist[threadIdx.x];
+}
+
+__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t* __restrict__ keys,
+                                                          uint32_t* __restrict__ idx, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t hist[RADIX];
+  tile_histogram(hist, nullptr, &B, lowbits, keys, idx, B.n, 0, counts);
+}
+
+__global__ __launch_bounds__(BLOCK) void radix_histogram_kernel(const uint32_t* __restrict__ keys, uint32_t n,
+                                                                uint32_t shift, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t hist[RADIX];
+  tile_histogram(hist, keys, nullptr, 0, nullptr, nullptr, n, shift, counts);
+}
+
+__global__ __launch_bounds__(RADIX) void radix_tile_scan_kernel(uint32_t* __restrict__ counts, uint32_t nt,
+                                                                uint32_t* __restrict__ gsum) {
+  const uint32_t d = threadIdx.x, b0 = blockIdx.x * SCAN_GROUP;
+  const uint32_t b1 = b0 + SCAN_GROUP < nt ? b0 + SCAN_GROUP : nt;
+  uint32_t c[SCAN_GROUP];
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN_GROUP; ++k) c[k] = b0 + k < b1 ? counts[(size_t)(b0 + k) * RADIX + d] : 0u;
+  uint32_t run = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < SCAN_GROUP; ++k) {
+    if (b0 + k < b1) counts[(size_t)(b0 + k) * RADIX + d] = run;
+    run += c[k];
+  }
+  gsum[(size_t)blockIdx.x * RADIX + d] = run;
+}
+
+__global__ __launch_bounds__(RADIX) void radix_group_scan_kernel(uint32_t* __restrict__ gsum, uint32_t ng) {
+  __shared__ uint32_t tot[RADIX];
+  const uint32_t d = threadIdx.x;
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < ng; ++g) {
+    const uint32_t v = gsum[(size_t)g * RADIX + d];
+    gsum[(size_t)g * RADIX + d] = run;
+    run += v;
+  }
+  tot[d] = run;
+  __syncthreads();
+  for (uint32_t off = 1; off < RADIX; off <<= 1) {  // inclusive scan of the digit totals
+    const uint32_t v = d >= off ? tot[d - off] : 0u;
+    __syncthreads();
+    tot[d] += v;
+    __syncthreads();
+  }
+  const uint32_t base = tot[d] - run;
+  for (uint32_t g = 0; g < ng; ++g) gsum[(size_t)g * RADIX + d] += base;
+}
+
+__global__ __launch_bounds__(BLOCK) void radix_scatter_kernel(const uint32_t* __restrict__ kin,
+                                                              const uint32_t* __restrict__ vin,
+                                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                              const uint32_t* __restrict__ counts,
+                                                              const uint32_t* __restrict__ gbase, uint32_t n,
+                                                              uint32_t shift, uint32_t write_keys) {
+  __shared__ uint32_t base[RADIX];
+  __shared__ uint32_t wcnt[BLOCK / 64][RADIX];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  base[threadIdx.x] = counts[(size_t)blockIdx.x * RADIX + threadIdx.x] +
+                      gbase[(size_t)(blockIdx.x / SCAN_GROUP) * RADIX + threadIdx.x];
+  const uint32_t t0 = blockIdx.x * SORT_TILE;
+  for (uint32_t r = 0; r < SORT_ITEMS; ++r) {
+    if (t0 + r * BLOCK >= n) break;  // block-uniform
+#pragma unroll
+    for (uint32_t w = 0; w < BLOCK / 64; ++w) wcnt[w][threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = t0 + r * BLOCK + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t key = valid ? kin[i] : 0u, val = valid ? vin[i] : 0u;
+    const uint32_t d = (key >> shift) & (RADIX - 1);
+    uint64_t same = __ballot(valid);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 8; ++bit) {
+      const uint64_t bb = __ballot((d >> bit) & 1u);
+      same &= ((d >> bit) & 1u) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(same & lt);
+    if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(same);
+    __syncthreads();
+    uint32_t pos = base[d] + rank;
+    for (uint32_t w = 0; w < wave; ++w) pos += wcnt[w][d];
+    __syncthreads();  // every lane has read base[] before it advances
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < BLOCK / 64; ++w) tot += wcnt[w][threadIdx.x];
+    base[threadIdx.x] += tot;
+    if (valid) {
+      vout[pos] = val;
+      if (write_keys) kout[pos] = key;
+    }
+    __syncthreads();  // wcnt is cleared by the next round
+  }
 }
 
 // Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS; for longer rows
@@ -173,25 +289,6 @@ __device__ inline uint32_t request_pcol(const ReqHdr& h) {
 __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 
-// XCD-aware block order.  The dispatcher deals workgroups to the 8 XCDs round-robin
-// (block b -> XCD b % 8), and each XCD has its own L2.  After the coherence sort, runs of
-// neighbouring blocks share a request class and so the same candidate nodes; remapping
-// each group of 8*G consecutive blocks so that XCD x takes the logical blocks
-// [x*G, x*G+G) of the group keeps a class's table reads in one L2 instead of eight.
-// Groups stay in launch order (heaviest classes first); the partial last group is
-// identity-mapped.  G = 0 disables the remap.
-#ifndef ACS_XCD_GROUP
-#define ACS_XCD_GROUP 0
-#endif
-__device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
-  constexpr uint32_t G = ACS_XCD_GROUP, NX = 8;
-  if (G == 0) return b;
-  const uint32_t span = NX * G;
-  if (b >= nb / span * span) return b;
-  const uint32_t r = b % span;
-  return b - r + (r % NX) * G + r / NX;
-}
-
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
 #define ACS_K1_WAVES_PER_EU 4  // measured: 4 waves/SIMD (VGPR <= 128) beats 3 (+12% c2, +13% c3), 5+ spill
@@ -199,7 +296,7 @@ __device__ inline uint32_t xcd_block(uint32_t b, uint32_t nb) {
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                            Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_block(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
   ReqHdr h{};
@@ -240,11 +337,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 }
 
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
-// order k).  The bitset goes to a word-major scratch buffer tmp[words][n] at column k, so a
-// wave's zeroing and bit updates are coalesced 256-B accesses; bitset_transpose_kernel
-// then writes each column to its request's row of the [n][words] output.
+// order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
+// once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
-                                                                uint32_t words, uint32_t* __restrict__ tmp,
+                                                                BitsLayout BL, uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
@@ -258,8 +354,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                wave_lds_row(B), wave_lds_list(B));
   if (!in) return;
-  uint32_t* col = tmp + k;
-  for (uint32_t w = 0; w < words; ++w) col[(size_t)w * B.n] = 0;
+  ChunkSink sink(bits + (size_t)i * BL.words, BL);
   OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
   Decision d{};
   if (host) {
@@ -268,8 +363,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, col, B.n, log);
+    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, BL, sink, log);
   }
+  sink.finish();
   obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
   out[i] = d;
 }
@@ -314,67 +410,11 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = B.res[(size_t)q * B.n + i];
     const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks), s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
-    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, nullptr, 0, log, s0, s1);
+    NullSink none;
+    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, BitsLayout{}, none, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
   }
   obl_n[k] = total;
-}
-
-// tmp[words][n] (column k = the k-th request in perm order) -> bits[perm[k]][words].  A
-// 256-thread block moves a 64-column x 64-word tile through LDS: every load instruction
-// reads 256 contiguous bytes of a tmp row, every store instruction writes 256 contiguous
-// bytes (64 words) of one output row — both fully coalesced (the previous 32-word tile
-// stored 4-byte pieces of 16 rows per instruction: 1.29 ms for 1M c4 rows).
-// Tile order (ACS_TP_MODE): output rows are `words` u32 long (c4: 1400 B), so a row's
-// 256-B segments are not line-aligned and neighbouring segments share cache lines.
-//   0: grid (column tiles, word tiles) — a row's segments are written far apart in time;
-//   1: grid (word tiles, column tiles) — a row's segments are written by consecutive blocks;
-//   2: one block per column tile walks all word tiles — each row written by one block.
-#ifndef ACS_TP_MODE
-#define ACS_TP_MODE 0
-#endif
-constexpr uint32_t TP_COLS = 64, TP_WORDS = 64;
-__device__ inline void transpose_tile(uint32_t (*tile)[TP_COLS + 1], const uint32_t* __restrict__ tmp, uint32_t n,
-                                      uint32_t words, const uint32_t* __restrict__ perm, uint32_t* __restrict__ bits,
-                                      uint32_t k0, uint32_t w0) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (uint32_t r = wave; r < TP_WORDS; r += BLOCK / 64) {
-    const uint32_t w = w0 + r, k = k0 + lane;
-    tile[r][lane] = (w < words && k < n) ? tmp[(size_t)w * n + k] : 0u;
-  }
-  __syncthreads();
-  const uint32_t w = w0 + lane;
-  for (uint32_t r = wave; r < TP_COLS; r += BLOCK / 64) {
-    const uint32_t k = k0 + r;
-    if (k >= n) break;
-    if (w < words) bits[(size_t)(perm ? perm[k] : k) * words + w] = tile[lane][r];
-  }
-}
-__global__ __launch_bounds__(BLOCK) void bitset_transpose_kernel(const uint32_t* __restrict__ tmp, uint32_t n,
-                                                                 uint32_t words, const uint32_t* __restrict__ perm,
-                                                                 uint32_t* __restrict__ bits) {
-  __shared__ uint32_t tile[TP_WORDS][TP_COLS + 1];
-#if ACS_TP_MODE == 2
-  for (uint32_t w0 = 0; w0 < words; w0 += TP_WORDS) {
-    transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.x * TP_COLS, w0);
-    __syncthreads();  // the tile is reused by the next word range
-  }
-#elif ACS_TP_MODE == 1
-  transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.y * TP_COLS, blockIdx.x * TP_WORDS);
-#else
-  transpose_tile(tile, tmp, n, words, perm, bits, blockIdx.x * TP_COLS, blockIdx.y * TP_WORDS);
-#endif
-}
-static dim3 transpose_grid(uint32_t n, uint32_t words) {
-  const uint32_t ct = (n + TP_COLS - 1) / TP_COLS, wt = (words + TP_WORDS - 1) / TP_WORDS;
-#if ACS_TP_MODE == 2
-  (void)wt;
-  return dim3(ct);
-#elif ACS_TP_MODE == 1
-  return dim3(wt, ct);
-#else
-  return dim3(ct, wt);
-#endif
 }
 
 __global__ __launch_bounds__(BLOCK) void shard_key_kernel(Tables T, const Decision* __restrict__ d, uint32_t n,
@@ -411,12 +451,9 @@ struct acs_tables {
   int timing = 0;
   hipEvent_t tev[2 * RING] = {};
   uint64_t launches = 0;
-  // sort workspace, grown on demand: keys/idx double buffers + hipcub temp storage
+  // sort workspace, grown on demand: keys/idx double buffers + per-tile digit counts
   void* ws = nullptr;
   size_t ws_bytes = 0;
-  // K2 word-major bitset scratch ([words][n] u32), grown on demand
-  void* wbuf = nullptr;
-  size_t wbuf_bytes = 0;
   // host-buffer entry points (internal stream, events, workspace) may be called from
   // several host threads at once (e.g. the N-API addon's libuv pool): one at a time
   std::mutex mu;
@@ -435,18 +472,6 @@ int acs_phase_read(unsigned long long* out, int n) {
   HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_phase_acc), z, sizeof z));
   for (int k = 0; k < n && k < PH_N; ++k) out[k] = h[k];
   return PH_N;
-}
-#endif
-
-#if defined(ACS_CHECK_UNIFORM)
-// Debug build only: read and reset the non-uniform table-load counters.
-int acs_debug_read(unsigned long long* out, int n) {
-  unsigned long long h[4] = {}, z[4] = {};
-  HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpyFromSymbol(h, HIP_SYMBOL(acs_nonuniform), sizeof h));
-  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_nonuniform), z, sizeof z));
-  for (int k = 0; k < n && k < 4; ++k) out[k] = h[k];
-  return 4;
 }
 #endif
 
@@ -507,8 +532,6 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_pols = h.n_pols;
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
-  t->view.lo = (uint64_t)(uintptr_t)base;
-  t->view.hi = (uint64_t)(uintptr_t)base + alloc - 64;
   return t;
 }
 
@@ -520,14 +543,13 @@ void acs_free(acs_tables* t) {
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
   if (t->ws) (void)hipFree(t->ws);
-  if (t->wbuf) (void)hipFree(t->wbuf);
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
 }
 
 uint32_t acs_wia_words_per_request(const acs_tables* t) {
-  return (t->view.n_sets + t->view.n_pols + t->view.n_rules + 31) / 32;
+  return bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules).words;
 }
 
 float acs_last_kernel_ms(const acs_tables* t) { return t ? t->last_ms : -1.f; }
@@ -572,28 +594,24 @@ int acs_set_option(acs_tables* t, int option, int value) {
   return fail("acs_set_option: unknown option");
 }
 
-// Coherence sort: permutation of request indices ordered by (class, action).
+// Coherence sort: permutation of request indices ordered by (class, low field).
 static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
   *perm = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
-#ifndef ACS_SORT_LOWBITS
-#define ACS_SORT_LOWBITS 4
-#endif
-  uint32_t lowbits = ACS_SORT_LOWBITS;  // action / entity ids folded to 4 bits (c2: 16-bit keys, 2 passes)
+  // Low field: the dense role key with a role factor; otherwise none — a class row already
+  // folds in the action filter (measured: 0 low bits time the same as 4 or 8, r01_sort).
+  uint32_t lowbits = 0;
   if (B.role_key) {
     lowbits = 1;
     while (lowbits < 16 && (B.role_rows - 1) >> lowbits) ++lowbits;
   }
-#if defined(ACS_SORT_KEY16)
-  lowbits = 16;  // A/B variant: the unfolded 16-bit low field
-#endif
-  int end_bit = (int)lowbits;  // keys < (cand_rows + 1) << lowbits
+  uint32_t end_bit = lowbits;  // keys < (cand_rows + 1) << lowbits
   while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - lowbits)) != 0) ++end_bit;
-  if (end_bit < 1) end_bit = 1;
-  size_t temp = 0;
-  HIP_OK(sort_pairs(nullptr, temp, nullptr, nullptr, nullptr, nullptr, (int)n, end_bit, s));
-  const size_t need = 4 * n * sizeof(uint32_t) + temp + 256;
+  const uint32_t passes = end_bit ? (end_bit + 7) / 8 : 1;
+  const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
+  const uint32_t ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
+  const size_t need = 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
   if (need > t->ws_bytes) {
     if (t->ws) HIP_OK(hipFree(t->ws));
     t->ws = nullptr;
@@ -601,15 +619,32 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
     HIP_OK(hipMalloc(&t->ws, need));
     t->ws_bytes = need;
   }
-  uint32_t* keys_in = (uint32_t*)t->ws;
-  uint32_t* keys_out = keys_in + n;
-  uint32_t* idx_in = keys_out + n;
-  uint32_t* idx_out = idx_in + n;
-  void* tmp = (void*)(((uintptr_t)(idx_out + n) + 255) & ~uintptr_t(255));
-  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, B, lowbits, keys_in, idx_in);
+  uint32_t* k0 = (uint32_t*)t->ws;
+  uint32_t* k1 = k0 + n;
+  uint32_t* v0 = k1 + n;
+  uint32_t* v1 = v0 + n;
+  uint32_t* counts = v1 + n;
+  uint32_t* gsum = counts + (size_t)RADIX * nt;
+  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, k0, v0, counts);
   HIP_OK(hipGetLastError());
-  HIP_OK(sort_pairs(tmp, temp, keys_in, keys_out, idx_in, idx_out, (int)n, end_bit, s));
-  *perm = idx_out;
+  for (uint32_t p = 0; p < passes; ++p) {
+    if (p > 0) {
+      hipLaunchKernelGGL(radix_histogram_kernel, dim3(nt), dim3(BLOCK), 0, s, (const uint32_t*)k0, (uint32_t)n,
+                         8 * p, counts);
+      HIP_OK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(radix_tile_scan_kernel, dim3(ng), dim3(RADIX), 0, s, counts, nt, gsum);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(radix_group_scan_kernel, dim3(1), dim3(RADIX), 0, s, gsum, ng);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(radix_scatter_kernel, dim3(nt), dim3(BLOCK), 0, s, (const uint32_t*)k0, (const uint32_t*)v0,
+                       k1, v1, (const uint32_t*)counts, (const uint32_t*)gsum, (uint32_t)n, 8 * p,
+                       (uint32_t)(p + 1 < passes));
+    HIP_OK(hipGetLastError());
+    std::swap(k0, k1);
+    std::swap(v0, v1);
+  }
+  *perm = v0;
   return 0;
 }
 
@@ -653,24 +688,13 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   const uint32_t* perm = nullptr;
   if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
-  const uint32_t words = acs_wia_words_per_request(t);
-  const size_t need = (size_t)words * b->n * sizeof(uint32_t);
-  if (need > t->wbuf_bytes) {
-    if (t->wbuf) HIP_OK(hipFree(t->wbuf));
-    t->wbuf = nullptr;
-    t->wbuf_bytes = 0;
-    HIP_OK(hipMalloc(&t->wbuf, need ? need : 16));
-    t->wbuf_bytes = need;
-  }
+  if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
+  const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, words,
-                     (uint32_t*)t->wbuf, obl, obl_n, (Decision*)out);
+  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, BL, bits,
+                     obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
-  if (words) {
-    hipLaunchKernelGGL(bitset_transpose_kernel, transpose_grid(b->n, words), dim3(BLOCK), 0, s, (const uint32_t*)t->wbuf, b->n, words, perm, bits);
-    HIP_OK(hipGetLastError());
-  }
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
     t->launches++;

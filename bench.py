@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: isAllowed decisions/sec of the MI355X evaluator (BASELINE.json metric).
 
-A step = one K1 launch evaluating one full batch of synthetic requests that is
-already resident in HBM (default: c2 = 1M requests x 1k rules, flat roles,
-SURVEY.md §8(d)).  Multi-GPU: one process per GPU (torch.distributed.run), each
-rank evaluates its own 1M-request shard against replicated tables (weak
-scaling, no data-path collective); timing = barrier + sync on both sides, max
-over ranks.  Rank 0 prints one JSON line with the roofline and CPU-baseline
-objects described in DESIGN.md.
+A step = the coherence sort + one K1 launch evaluating one full batch of synthetic
+requests that is already resident in HBM.  Default workload: c3 = 10M requests x 10k
+rules, mixed combining algorithms + HR role scoping, the north star's
+10k-rule configuration.  Multi-GPU: one process per GPU; `--gpus N` without a
+torch.distributed environment launches the N ranks itself (torch.distributed.run on
+127.0.0.1, before anything touches the GPU).  Each rank evaluates its own batch against
+replicated tables (weak scaling, no data-path collective); timing = barrier + sync on
+both sides, max over ranks.  Rank 0 prints one JSON line with the roofline, CPU-baseline
+and parity objects described in DESIGN.md §9; parity = a >= 1 % random sample of the timed
+batch re-decided by the C++ oracle (BASELINE.md's gate).
 """
 import argparse
 import json
@@ -145,41 +148,91 @@ def algorithmic_bytes(cs, batch):
                  "bruteforce_bytes_per_decision": float(b_req.mean()) + ctx + 8.0 + full / 64.0}
 
 
-def measured_traffic(config, kernel="is_allowed_kernel"):
-    """HBM bytes per K1 launch from the committed PMC pass of the same bench command
-    (profiles/traffic.json, written by tools/pmc.sh: FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE)."""
+def traffic_key(config, requests, world, mode):
+    """profiles/traffic.json key: the run shape a PMC pass measured (config, requests per
+    rank, ranks, request / rule sharding)."""
+    return f"{config}/n{requests}/w{world}/{mode}"
+
+
+def measured_traffic(key, kernel="is_allowed_kernel"):
+    """HBM bytes per launch of `kernel` from the committed PMC passes of the same bench
+    command (profiles/traffic.json, written by tools/pmc.sh + tools/pmc_traffic.py), or
+    (None, None) when no pass measured this exact run shape.  Entry: FETCH_SIZE x 2 +
+    WRITE_SIZE (MI355X_MICROARCH.md gfx950 note; the x2 is calibrated for wide streaming
+    reads only, so the entry also carries the gather calibration when one was measured)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
-    e = d.get(config, {}).get(kernel)
-    return (e["bytes_per_launch"], e["source"]) if e else (None, None)
+    e = d.get(key, {}).get(kernel)
+    return (e["bytes_per_launch"], e) if e else (None, None)
 
 
-def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
-    """The C++ oracle (oracle/acs_oracle.cpp: the reference's per-request serial algorithm,
-    'port') on a bounded random sample of the same batch, std::thread x up to 16 host
-    cores (the GPU box's CPU share); only evaluation is timed (requests are decoded to the
-    reference's JSON shape and parsed first).  Every sampled outcome is also compared with
-    the GPU's decision record (parity)."""
+def launch(args):
+    """`--gpus N` outside a torch.distributed environment: run N ranks of this same command
+    through torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as CHILD
+    processes — nothing here has touched the GPU — and exit with their status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"launching {args.gpus} ranks: torch.distributed.run on 127.0.0.1:{port}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def selftest(world, rank):
+    """`--selftest`: the launcher and the collective path without a GPU (gloo on CPU):
+    every rank all-reduces its rank id with MAX, rank 0 prints what it saw."""
+    import torch.distributed as tdist
+    if world > 1:
+        tdist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        seen = int(t.item())
+        assert tdist.get_world_size() == world
+    else:
+        seen = 0
+    if rank == 0:
+        print(json.dumps({"selftest": True, "world_size": world, "max_rank_seen": seen}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
+    """Parity gate + CPU baseline from ONE oracle run: a random sample of the timed batch
+    (``fraction`` of it, BASELINE.md's >= 1 %; c5's 1M-rule store only a bounded sample) is
+    decoded to the reference's JSON request shape and re-decided by the C++ oracle
+    (oracle/acs_oracle.cpp: the reference's per-request serial algorithm, 'port'),
+    std::thread x up to 16 host cores (the GPU box's CPU share).  Every sampled outcome is
+    compared with the GPU's decision record; the oracle's evaluation wall time (decode and
+    JSON parse excluded) is the CPU baseline.  HR scope trees are shared between requests
+    through {"$shared": k} placeholders so each is serialised and parsed once."""
     from oracle import acs_oracle_c
     from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
     from diff_utils import gpu_outcome
+    from acs_mi355x.synth import SharedValues
     acs_oracle_c.build()
     threads = max(1, min(16, os.cpu_count() or 1))
     co = acs_oracle_c.COracle(FULL_URNS, DEFAULT_CAS, doc)
-    idx = np.random.default_rng(1234).permutation(sb.batch.n)
-    chunk = {"c2": 20_000, "c3": 250}.get(kind, 32)  # c3/c5 requests carry HR trees of up to 21,845 orgs
+    n = sb.batch.n
+    want_n = max(1, int(round(fraction * n)))
+    idx = np.random.default_rng(1234).permutation(n)[:want_n]
+    chunk = {"c2": 50_000, "c3": 10_000}.get(kind, 16)
     done = busy = mism = unsup = host = 0
     wall0 = time.perf_counter()
-    # bounded: ~`seconds` of oracle evaluation, and at most 3x that in wall time (decoding
-    # c3/c5 requests to JSON — HR trees of up to 21,845 orgs — costs more than evaluating)
-    while busy < seconds and done < len(idx) and time.perf_counter() - wall0 < 3 * seconds + 10:
+    while done < len(idx) and busy < seconds and time.perf_counter() - wall0 < 2 * seconds + 30:
         part = idx[done:done + chunk]
-        out, sec = co.raw([sb.decode(int(i)) for i in part], threads)
+        sh = SharedValues()
+        reqs = [sb.decode(int(i), sh) for i in part]
+        out, sec = co.raw(reqs, threads, shared=sh.values)
         busy += sec
-        log(f"cpu baseline: {done + len(part)} requests, {busy:.1f}s evaluation")
         for i, r in zip(part, out):
             want = acs_oracle_c.outcome(r)
             got = gpu_outcome(cs, gpu_dec[i])
@@ -190,12 +243,16 @@ def cpu_baseline(kind, doc, sb, gpu_dec, cs, seconds):
             elif got != want:
                 mism += 1
         done += len(part)
+        log(f"oracle parity: {done}/{len(idx)} requests, {busy:.1f}s oracle evaluation, {mism} mismatches")
     co.close()
-    return {"value": done / busy, "unit": "decisions/s", "cores": threads, "kind": "port",
-            "sample": f"{done} random requests of the same {kind} batch through oracle/acs_oracle.cpp (C++17 "
-                      f"restatement of the reference's per-request serial algorithm, std::thread x {threads}), "
-                      f"{busy:.1f}s of evaluation wall time (requests decoded and parsed beforehand)"}, \
-        {"oracle_sample": done, "mismatches": mism, "oracle_unsupported": unsup, "gpu_host_path": host}
+    cb = {"value": done / busy, "unit": "decisions/s", "cores": threads, "kind": "port",
+          "sample": f"{done} random requests of the same {kind} batch through oracle/acs_oracle.cpp (C++17 "
+                    f"restatement of the reference's per-request serial algorithm; per-request HR flattening "
+                    f"memoised, so faster than the reference's own loop), std::thread x {threads}, "
+                    f"{busy:.1f}s of evaluation wall time (requests decoded and parsed beforehand)"}
+    par = {"oracle_sample": done, "sample_fraction": done / n, "mismatches": mism,
+           "oracle_unsupported": unsup, "gpu_host_path": host, "checker": "oracle/acs_oracle.cpp"}
+    return cb, par
 
 
 def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist):
@@ -296,7 +353,8 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
                                            "k2_only_queries_per_s": n / (k2_only_ms * 1e-3),
                                            "max_log": int(max((len(v) for v in long_logs.values()), default=0))}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic("c4", "what_is_allowed_kernel")[0],
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic(traffic_key("c4", n, world, "requests"),
+                                                                                      "what_is_allowed_kernel")[0],
                          "kernel": "what_is_allowed_kernel (+ bitset_transpose_kernel, timed together)",
                          "kernel_ms": kern_ms, "bytes_per_query": per,
                          "bytes_parts": parts, "output_GBps": (4 * words + 8 * float(obl_n.mean()) + 12) * n /
@@ -315,10 +373,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--config", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--requests", type=int, default=0, help="requests per GPU (default: the config's)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-fraction", type=float, default=0.01,
+                    help="fraction of the timed batch re-decided by the C++ oracle (BASELINE.md: >= 1 %%)")
+    ap.add_argument("--cpu-seconds", type=float, default=90.0, help="bound on the oracle's evaluation time")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle parity + CPU baseline leg")
+    ap.add_argument("--selftest", action="store_true", help="launcher / collective check on CPU (gloo), no GPU")
     ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--lib", default=None, help="evaluate with another build of libacs_mi355x (experiments)")
@@ -326,10 +387,17 @@ def main():
                     help="configs[4] variant ii: whole policy sets sharded over ranks, every rank evaluates the "
                          "same requests, one all-reduce MAX of 64-bit decision keys (RCCL) combines them")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))  # parent: spawns the ranks, touches no GPU
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with --nproc-per-node "
+                         f"{args.gpus}, or run without a torch.distributed environment)")
+    if args.selftest:
+        return selftest(world, rank)
     dist = world > 1
     global REHEARSAL
     # ACS_BENCH_REHEARSAL=1: several ranks on ONE GPU over gloo (collectives through host
@@ -347,6 +415,8 @@ def main():
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if dist:
+        assert tdist.get_world_size() == args.gpus
 
     from acs_mi355x import compiler, native, shard, store, synth, layout as L
     from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor
@@ -442,7 +512,8 @@ def main():
         log("counting algorithmic bytes")
         per_dec, parts = algorithmic_bytes(cs, sb.batch)
         achieved = per_dec * n / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = measured_traffic(kind)
+        mode = "rules" if args.rule_shard else "requests"
+        traffic, traffic_src = measured_traffic(traffic_key(kind, n, world, mode))
         # request sharding: every rank decides its own n requests; rule sharding: the ranks
         # decide the same n requests together
         value = (1 if args.rule_shard else world) * n * args.steps / elapsed
@@ -460,12 +531,14 @@ def main():
                        "rules": cs.n_rules, "table_bytes": cs.table_bytes(),
                        "parallelism": f"policy-set shards x{world}" if args.rule_shard else f"requests dp{world}",
                        "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])},
-                       "host_fallback_fraction": host / n, "request_classes": int(sb.batch.cand.shape[0])},
+                       "host_fallback_fraction": host / n, "request_classes": int(sb.batch.cand.shape[0]),
+                       "ranks_confirmed": world},
             "coherence_sort": not args.no_sort,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_unit": "HBM bytes per K1 launch (rocprofv3 PMC)",
-                         "traffic_source": traffic_src, "algorithmic_bytes_per_launch": per_dec * n,
+                         "traffic_key": traffic_key(kind, n, world, mode), "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": per_dec * n,
                          "kernel": "is_allowed_kernel", "kernel_ms": kern_ms, "step_gpu_ms": step_ms,
                          "bytes_per_decision": per_dec, "bytes_parts": parts},
         }
@@ -476,8 +549,9 @@ def main():
         if REHEARSAL:
             line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:
-            log("CPU baseline (C++ oracle)")
-            cb, par = cpu_baseline(kind, doc, sb, dec, cs, args.cpu_seconds)
+            log("oracle parity + CPU baseline (C++ oracle)")
+            frac = args.parity_fraction if kind in ("c2", "c3") else 64 / n  # c5: 1M rules, a bounded sample
+            cb, par = oracle_parity(kind, doc, sb, dec, cs, frac, args.cpu_seconds)
             line["cpu_baseline"] = cb
             line["parity"] = par
         print(json.dumps(line), flush=True)

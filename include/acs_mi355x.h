@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 #define ACS_BLOB_MAGIC 0x31534341u /* "ACS1" */
-#define ACS_ABI_VERSION 3u
+#define ACS_ABI_VERSION 4u
 
 /* Compiled policy-store image (host compiler output, see csrc/acs_layout.h).
  * Header followed by 16-byte aligned sections in this order: set / policy / rule
@@ -101,8 +101,13 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* host_batch, acs_decision*
 int acs_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, acs_decision* dev_out, void* stream);
 
 /* Replaces: AccessController.whatIsAllowed (accessController.ts:326-427).
- * bits: [n][words_per_req] inclusion bitsets over (sets | policies | rules);
- * obl: [n][ACS_OBL_MAX][2] maskedProperty push log (entity id, mask id), obl_n: [n]. */
+ * bits: [n][words_per_req] inclusion bitsets, one row per request: the set section at word
+ * 0, the policy section at word wp = up4(ceil(S/32)), the rule section at word
+ * wr = wp + up4(ceil(P/32)); words_per_req = wr + up4(ceil(R/32)) (up4: round up to a
+ * multiple of 4, so every section starts on a 16-byte boundary); bit i of a section is
+ * bit (i & 31) of its word i >> 5.  The device form needs a 16-byte aligned `bits`.
+ * obl: [n][ACS_OBL_MAX][2] maskedProperty push log (entity id, mask id), obl_n: [n]; log entries
+ * past a request's count are unspecified. */
 #define ACS_OBL_MAX 64
 uint32_t acs_wia_words_per_request(const acs_tables* t);
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t* bits, uint32_t* obl,
@@ -142,8 +147,9 @@ int acs_shard_keys_device(acs_tables* t, const acs_decision* dev_dec, size_t n, 
 int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* dev_out, void* stream);
 
 /* Options.  ACS_OPT_SORT (default 1): before evaluating, the device entry points
- * order the batch by (entity, role, action) with a radix sort so that every
- * wave shares its table-driven branches; results are written in input order. */
+ * order the batch by request class (entity, roles, action; + role key with a role factor)
+ * with an LSD radix sort so that every wave shares its table-driven branches; results are
+ * written in input order. */
 #define ACS_OPT_SORT 1
 /* ACS_OPT_TIMING: record HIP events on the launch stream around every eval kernel (K1 of
  * acs_is_allowed_device, K2 of acs_what_is_allowed_device); acs_kernel_times returns the durations (ms) of the last n

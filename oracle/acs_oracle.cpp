@@ -44,8 +44,10 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -93,6 +95,10 @@ struct Parser {
   const char* p;
   const char* e;
   Arena& ar;
+  // Optional table of pre-parsed values: an object {"$shared": k} parses to shared[k]
+  // itself (large sub-documents common to many requests — a synthetic batch's HR scope
+  // trees — are parsed once; the oracle never mutates request values).
+  const std::vector<VP>* shared = nullptr;
   Parser(const char* s, size_t n, Arena& a) : p(s), e(s + n), ar(a) {}
   void ws() {
     while (p < e && (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r')) ++p;
@@ -199,6 +205,11 @@ struct Parser {
         }
         if (p < e && *p == '}') {
           ++p;
+          if (shared && v->o.size() == 1 && v->o[0].first == "$shared" && v->o[0].second->t == T::Num) {
+            const double k = v->o[0].second->n;
+            if (k < 0 || k >= (double)shared->size()) bad();
+            return (*shared)[(size_t)k];
+          }
           return v;
         }
         bad();
@@ -493,6 +504,27 @@ bool js_regex_search(const std::string& pattern, const std::string& subject) {
   if (!all_in(pattern, "*+?|()[]^$", true) || pattern.find("(?") != std::string::npos ||
       pattern.find("[]") != std::string::npos || pattern.find("[^]") != std::string::npos)
     unsupported("regex pattern outside the restated subset");
+  // V8 rejects a quantifier that follows a quantifier ("Nothing to repeat": a**, a*+, a???);
+  // libstdc++'s ECMAScript grammar accepts them, so the check is explicit (pinned by
+  // tests/golden/regex_cells.json).  A '?' right after a quantifier is its lazy marker.
+  {
+    bool in_class = false;
+    int quant = 0;  // 0: previous token not a quantifier, 1: a quantifier, 2: quantifier + lazy '?'
+    for (char c : pattern) {
+      if (in_class) {
+        in_class = c != ']';
+        continue;
+      }
+      if (c == '*' || c == '+' || c == '?') {
+        if (quant == 1 && c == '?') quant = 2;
+        else if (quant) throw JSError{3};
+        else quant = 1;
+        continue;
+      }
+      quant = 0;
+      if (c == '[') in_class = true;
+    }
+  }
   try {
     std::regex rx(pattern, std::regex::ECMAScript);
     return std::regex_search(subject, rx);
@@ -583,6 +615,9 @@ struct Effect {
   VP ec = UNDEF;
 };
 
+enum UrnName {U_roleScopingEntity, U_roleScopingInstance, U_hierarchicalRoleScoping, U_ownerEntity, U_ownerInstance, U_resourceID, U_entity, U_role, U_operation, U_aclIndicatoryEntity, U_aclInstance, U_actionID, U_create, U_modify, U_read, U_delete, U_user, U_skipACL, U_property, U_maskedProperty, U_COUNT};
+const char* const kUrnNames[U_COUNT] = {"roleScopingEntity", "roleScopingInstance", "hierarchicalRoleScoping", "ownerEntity", "ownerInstance", "resourceID", "entity", "role", "operation", "aclIndicatoryEntity", "aclInstance", "actionID", "create", "modify", "read", "delete", "user", "skipACL", "property", "maskedProperty"};
+
 enum Method { M_DENY, M_PERMIT, M_FIRST };
 
 struct Oracle {
@@ -590,8 +625,9 @@ struct Oracle {
   std::map<std::string, std::string> urns;
   std::unordered_map<std::string, Method> cas;
   OrderedMap<PolicySet> sets;
-  // URN values as JS values (UNDEF when the config lacks them)
-  std::unordered_map<std::string, VP> U;
+  // URN values as JS values (UNDEF when the config lacks them), indexed by UrnName: an
+  // array read per lookup (the matchers run it per rule and request attribute)
+  VP U[U_COUNT];
   VP S_PERMIT, S_DENY, S_TRUE;
 
   VP str_val(const std::string& s) {
@@ -600,20 +636,10 @@ struct Oracle {
     return v;
   }
 
-  VP u(const char* name) const {
-    auto it = U.find(name);
-    return it == U.end() ? UNDEF : it->second;
-  }
+  VP u(UrnName k) const { return U[k]; }
 
   void init_urns(VP cfg) {
-    static const char* names[] = {"roleScopingEntity", "roleScopingInstance", "hierarchicalRoleScoping",
-                                  "ownerEntity", "ownerInstance", "resourceID", "entity", "role", "operation",
-                                  "aclIndicatoryEntity", "aclInstance", "actionID", "create", "modify", "read",
-                                  "delete", "user", "skipACL", "property", "maskedProperty"};
-    for (const char* n : names) {
-      VP v = get(cfg, n);
-      if (v->t != T::Undef) U[n] = v;
-    }
+    for (int k = 0; k < U_COUNT; ++k) U[k] = get(cfg, kUrnNames[k]);
     S_PERMIT = str_val("PERMIT");
     S_DENY = str_val("DENY");
     S_TRUE = str_val("true");
@@ -686,7 +712,7 @@ struct Oracle {
 
   bool subject_matches(VP rule_subs, VP req_subs, VP request) const {  // :793-823
     VP ctx = get(request, "context");
-    VP role_urn = u("role");
+    VP role_urn = u(U_role);
     if (nullish(rule_subs) || length_of(rule_subs) == 0) return true;
     VP rule_role = UNDEF;
     for (VP s : iterate(rule_subs))
@@ -734,7 +760,7 @@ struct Oracle {
 
   bool resource_attrs_match(VP rule_attrs, const std::vector<VP>& req_list, VP effect, bool regex) const {
     // :465-654, operation 'isAllowed'
-    VP ent = u("entity"), prop_urn = u("property"), op_urn = u("operation");
+    VP ent = u(U_entity), prop_urn = u(U_property), op_urn = u(U_operation);
     bool entity_match = false, property_match = false, rule_props = false, req_props = false;
     bool operation_match = false, skip_deny = true;
     VP req_entity_urn = nullptr;  // '' initially
@@ -806,7 +832,7 @@ struct Oracle {
   }
 
   bool multiple_entities_match(const PolicySet& ps, VP request) const {  // :429-463
-    VP ent = u("entity");
+    VP ent = u(U_entity);
     for (VP qa : or_empty(get(get(request, "target"), "resources"))) {
       if (!strict_eq(prop(qa, "id"), ent)) continue;
       bool multi = false;
@@ -825,10 +851,47 @@ struct Oracle {
   }
 
   // ---------------------------------------------------------------- HR scope
-  using Flat = std::set<std::string>;
+  // The flattened HR ids of one (hierarchical_scopes, rule role): views into the request's
+  // own strings, plus the id sets of children arrays taken from the call's shared-value
+  // table (computed once per thread for every request that names them; a pure function of
+  // immutable input, so memoising it changes no result).
+  using IdSet = std::unordered_set<std::string_view>;
+  struct Flat {
+    IdSet own;
+    std::vector<const IdSet*> shared;
+    bool count(std::string_view v) const {
+      if (own.count(v)) return true;
+      for (const IdSet* s : shared)
+        if (s->count(v)) return true;
+      return false;
+    }
+  };
+  struct SharedIds {  // per worker thread, for one acs_oracle_is_allowed_shared call
+    const std::unordered_set<VP>* shared_values = nullptr;
+    std::unordered_map<VP, IdSet> ids;
+  };
   struct Memo {
     std::map<std::pair<VP, std::string>, Flat> flat;
+    SharedIds* cache = nullptr;
   };
+
+  static void collect_ids(VP h, IdSet& out, std::vector<VP>& stack) {
+    stack.push_back(h);
+    while (!stack.empty()) {
+      VP x = stack.back();
+      stack.pop_back();
+      VP hid = get(x, "id");
+      if (truthy(hid)) {
+        if (is_obj(hid)) unsupported("object-valued HR id");
+        if (hid->t == T::Str) out.insert(std::string_view(hid->s));
+      }
+      VP ch = get(x, "children");
+      if (length_gt0(ch)) {
+        const std::vector<VP>& kids = iterate(ch);
+        for (auto k = kids.rbegin(); k != kids.rend(); ++k) stack.push_back(*k);
+      }
+    }
+  }
 
   const Flat& flat_hr(VP scopes, VP rule_role, Memo& memo) const {  // hierarchicalScope.ts:207-220
     if (nullish(scopes)) type_error();
@@ -837,21 +900,24 @@ struct Oracle {
     if (it != memo.flat.end()) return it->second;
     Flat out;
     std::vector<VP> stack;
-    const std::vector<VP>& roots_all = iterate(scopes);
-    for (auto r = roots_all.rbegin(); r != roots_all.rend(); ++r)
-      if (strict_eq(get(*r, "role"), rule_role)) stack.push_back(*r);
-    while (!stack.empty()) {
-      VP h = stack.back();
-      stack.pop_back();
-      VP hid = get(h, "id");
-      if (truthy(hid)) {
-        if (is_obj(hid)) unsupported("object-valued HR id");
-        if (hid->t == T::Str) out.insert(hid->s);
-      }
-      VP ch = get(h, "children");
-      if (length_gt0(ch)) {
-        const std::vector<VP>& kids = iterate(ch);
-        for (auto k = kids.rbegin(); k != kids.rend(); ++k) stack.push_back(*k);
+    for (VP r : iterate(scopes)) {
+      if (!strict_eq(get(r, "role"), rule_role)) continue;
+      VP ch = get(r, "children");
+      if (memo.cache && memo.cache->shared_values && memo.cache->shared_values->count(ch) && length_gt0(ch)) {
+        VP hid = get(r, "id");
+        if (truthy(hid)) {
+          if (is_obj(hid)) unsupported("object-valued HR id");
+          if (hid->t == T::Str) out.own.insert(std::string_view(hid->s));
+        }
+        auto c = memo.cache->ids.find(ch);
+        if (c == memo.cache->ids.end()) {
+          IdSet ids;
+          for (VP k : iterate(ch)) collect_ids(k, ids, stack);
+          c = memo.cache->ids.emplace(ch, std::move(ids)).first;
+        }
+        out.shared.push_back(&c->second);
+      } else {
+        collect_ids(r, out.own, stack);
       }
     }
     return memo.flat.emplace(key, std::move(out)).first->second;
@@ -863,12 +929,12 @@ struct Oracle {
     if (length_of(subs) == 0) return true;
     VP hr_check = S_TRUE;
     VP rule_role = UNDEF, scoping_entity = UNDEF;
-    VP role_urn = u("role");
+    VP role_urn = u(U_role);
     for (VP s : or_empty(subs)) {
       VP sid = get(s, "id");
       if (strict_eq(sid, role_urn)) rule_role = get(s, "value");
-      else if (strict_eq(sid, u("hierarchicalRoleScoping"))) hr_check = prop(s, "value");
-      else if (strict_eq(sid, u("roleScopingEntity"))) scoping_entity = prop(s, "value");
+      else if (strict_eq(sid, u(U_hierarchicalRoleScoping))) hr_check = prop(s, "value");
+      else if (strict_eq(sid, u(U_roleScopingEntity))) scoping_entity = prop(s, "value");
     }
     if (!truthy(scoping_entity)) return true;
     VP ctx = get(request, "context");
@@ -877,7 +943,7 @@ struct Oracle {
     VP ctx_resources = truthy(ctx_resources_v) ? ctx_resources_v : &kEmptyArr;
     VP req_target = get(request, "target");
     for (VP attr : or_empty(t.resources)) {
-      if (loose_eq(get(attr, "id"), u("entity"))) {
+      if (loose_eq(get(attr, "id"), u(U_entity))) {
         VP eoo = get(attr, "value");
         bool entities_match = false;
         for (VP qa : or_empty(prop(req_target, "resources"))) {
@@ -887,7 +953,7 @@ struct Oracle {
             const auto rh = regex_entity(eoo, get(qa, "value"));
             if (rh.first) entities_match = false;
             if (rh.second) entities_match = true;
-          } else if (loose_eq(get(qa, "id"), u("resourceID")) && entities_match) {
+          } else if (loose_eq(get(qa, "id"), u(U_resourceID)) && entities_match) {
             VP inst_id = get(qa, "value");
             VP res = lodash_find(ctx_resources, "instance.id", inst_id);
             if (truthy(res)) res = get(res, "instance");
@@ -901,7 +967,7 @@ struct Oracle {
             }
           }
         }
-      } else if (strict_eq(get(attr, "id"), u("operation"))) {
+      } else if (strict_eq(get(attr, "id"), u(U_operation))) {
         VP eoo = get(attr, "value");
         for (VP qa : or_empty(prop(req_target, "resources"))) {
           if (strict_eq(get(qa, "id"), get(attr, "id")) && strict_eq(get(qa, "value"), get(attr, "value"))) {
@@ -922,7 +988,7 @@ struct Oracle {
     std::vector<VP> reduced;
     for (VP r : iterate(ras))
       if (strict_eq(prop(r, "role"), rule_role)) reduced.push_back(r);
-    VP rse = u("roleScopingEntity"), oe = u("ownerEntity"), rsi = u("roleScopingInstance");
+    VP rse = u(U_roleScopingEntity), oe = u(U_ownerEntity), rsi = u(U_roleScopingInstance);
     auto direct = [&](VP owner) -> bool {
       for (VP ra : reduced) {
         VP attrs = get(ra, "attributes");
@@ -982,9 +1048,9 @@ struct Oracle {
           VP oattrs = get(owner, "attributes");
           if (nullish(oattrs)) continue;
           for (VP a : iterate(oattrs))
-            if (strict_eq(get(a, "id"), u("ownerInstance"))) {
+            if (strict_eq(get(a, "id"), u(U_ownerInstance))) {
               VP v = get(a, "value");
-              if (v->t == T::Str && flat.count(v->s)) hit = true;
+              if (v->t == T::Str && flat.count(std::string_view(v->s))) hit = true;
             }
         }
         if (!hit) still.push_back(owners);
@@ -998,9 +1064,9 @@ struct Oracle {
   bool verify_acl(const Target& t, VP request) const {  // verifyACL.ts:11-251
     std::vector<VP> scoped_roles;
     for (VP a : or_empty(t.subjects)) {
-      if (strict_eq(prop(a, "id"), u("role"))) {
+      if (strict_eq(prop(a, "id"), u(U_role))) {
         scoped_roles.push_back(get(a, "value"));
-      } else if (strict_eq(prop(a, "id"), u("skipACL"))) {
+      } else if (strict_eq(prop(a, "id"), u(U_skipACL))) {
         return true;
       }
     }
@@ -1016,7 +1082,7 @@ struct Oracle {
     OrderedMap<std::vector<VP>> tmap;  // scopingEntity -> instances
     std::vector<VP> t_entities;
     for (VP qa : or_empty(prop(req_target, "resources"))) {
-      if (!(loose_eq(prop(qa, "id"), u("resourceID")) || strict_eq(prop(qa, "id"), u("operation")))) continue;
+      if (!(loose_eq(prop(qa, "id"), u(U_resourceID)) || strict_eq(prop(qa, "id"), u(U_operation)))) continue;
       VP inst_id = prop(qa, "value");
       VP res = lodash_find(ctx_resources, "instance.id", inst_id);
       VP acl_list = UNDEF;
@@ -1028,7 +1094,7 @@ struct Oracle {
       }
       if (lodash_is_empty(acl_list)) return true;
       for (VP acl : iterate(acl_list)) {
-        if (!strict_eq(get(acl, "id"), u("aclIndicatoryEntity"))) return false;
+        if (!strict_eq(get(acl, "id"), u(U_aclIndicatoryEntity))) return false;
         VP se = prop(acl, "value");
         const std::string k = map_key(se);
         if (!tmap.index.count(k)) {
@@ -1038,7 +1104,7 @@ struct Oracle {
         VP attrs = prop(acl, "attributes");
         if (!truthy(attrs) || length_of(attrs) == 0) return false;
         for (VP at : iterate(attrs)) {
-          if (!strict_eq(prop(at, "id"), u("aclInstance"))) return false;
+          if (!strict_eq(prop(at, "id"), u(U_aclInstance))) return false;
           tmap.items[tmap.index[k]].second.push_back(prop(at, "value"));
         }
       }
@@ -1053,13 +1119,13 @@ struct Oracle {
       VP role = get(ra, "role");
       if (!js_includes(scoped_roles, role)) continue;
       for (VP rattr : or_empty(get(ra, "attributes"))) {
-        if (strict_eq(get(rattr, "id"), u("roleScopingEntity")) && js_includes(t_entities, get(rattr, "value"))) {
+        if (strict_eq(get(rattr, "id"), u(U_roleScopingEntity)) && js_includes(t_entities, get(rattr, "value"))) {
           VP rse_v = get(rattr, "value");
           const std::string k = map_key(rse_v);
           if (!smap.index.count(k)) smap.set(k, {});  // !subjectScopedInstancesMap.get(k) -> []
           if (length_gt0(get(rattr, "attributes")))
             for (VP ri : iterate(get(rattr, "attributes")))
-              if (strict_eq(get(ri, "id"), u("roleScopingInstance")))
+              if (strict_eq(get(ri, "id"), u(U_roleScopingInstance)))
                 smap.items[smap.index[k]].second.push_back(get(ri, "value"));
         }
       }
@@ -1085,12 +1151,12 @@ struct Oracle {
     };
     walk(get(subj, "hierarchical_scopes"), UNDEF);
     VP a0 = truthy(actions) && actions->t == T::Arr && !actions->a.empty() ? actions->a[0] : UNDEF;
-    const bool is_action = truthy(actions) && truthy(a0) && strict_eq(prop(a0, "id"), u("actionID"));
-    if (is_action && strict_eq(prop(a0, "value"), u("create"))) {
+    const bool is_action = truthy(actions) && truthy(a0) && strict_eq(prop(a0, "id"), u(U_actionID));
+    if (is_action && strict_eq(prop(a0, "value"), u(U_create))) {
       bool valid = false;
       if (t_entities.empty()) return true;
       for (VP se : t_entities) {
-        if (strict_eq(se, u("user"))) {
+        if (strict_eq(se, u(U_user))) {
           valid = true;
           continue;
         }
@@ -1115,12 +1181,12 @@ struct Oracle {
       }
       if (valid) return true;
     }
-    if (is_action && (strict_eq(prop(a0, "value"), u("read")) || strict_eq(prop(a0, "value"), u("modify")) ||
-                      strict_eq(prop(a0, "value"), u("delete")))) {
+    if (is_action && (strict_eq(prop(a0, "value"), u(U_read)) || strict_eq(prop(a0, "value"), u(U_modify)) ||
+                      strict_eq(prop(a0, "value"), u(U_delete)))) {
       if (t_entities.empty()) return true;
       for (VP se : t_entities) {
         const std::vector<VP>& t_inst = tmap.items[tmap.index[map_key(se)]].second;
-        if (strict_eq(se, u("user")))
+        if (strict_eq(se, u(U_user)))
           if (js_includes(t_inst, get(subj, "id"))) return true;
         auto it = smap.index.find(map_key(se));
         if (it != smap.index.end())
@@ -1150,7 +1216,7 @@ struct Oracle {
     return 5;
   }
 
-  Outcome is_allowed(VP request) const {
+  Outcome is_allowed(VP request, SharedIds* cache = nullptr) const {
     Outcome out;
     if (!truthy(get(request, "target"))) {  // :91-102
       out.decision = 3;
@@ -1159,6 +1225,7 @@ struct Oracle {
       return out;
     }
     Memo memo;
+    memo.cache = cache;
     VP ctx = get(request, "context");
     if (truthy(get(get(ctx, "subject"), "token"))) unsupported("subject token (identity-srv / Redis I/O)");
     bool have_effect = false;
@@ -1181,7 +1248,7 @@ struct Oracle {
       if (exact) {
         long n_ent = 0;
         for (VP a : or_empty(get(get(request, "target"), "resources")))
-          if (strict_eq(get(a, "id"), u("entity"))) ++n_ent;
+          if (strict_eq(get(a, "id"), u(U_entity))) ++n_ent;
         if (n_ent > 1) exact = multiple_entities_match(pset, request);
       }
       for (auto& pkv : pset.policies.items) {  // loop 2b (:167-290)
@@ -1266,14 +1333,50 @@ void* acs_oracle_create(const char* urns, const char* cas, const char* doc) {
 
 void acs_oracle_free(void* h) { delete (Oracle*)h; }
 
+// One step of the entity namespace / RegExp test (regex_entity) for two string values
+// (NULL = JSON null): 1 HIT | 2 RESET, 4 TypeError, 8 SyntaxError, -1 outside the restated
+// subset.  tests/test_regex_v8.py checks it against V8 (tests/golden/regex_cells.json).
+int acs_oracle_regex_cell(const char* rule, const char* req) {
+  static const Oracle kNoStore{};
+  Val rv, qv;
+  if (rule) { rv.t = T::Str; rv.s = rule; } else { rv.t = T::Null; }
+  if (req) { qv.t = T::Str; qv.s = req; } else { qv.t = T::Null; }
+  try {
+    const auto rh = kNoStore.regex_entity(&rv, &qv);
+    return (rh.first ? 2 : 0) | (rh.second ? 1 : 0);
+  } catch (const JSError& e) {
+    return e.kind == 1 ? 4 : 8;
+  } catch (const Unsupported&) {
+    return -1;
+  }
+}
+
 // requests: a JSON array of n requests.  out: 4 int32 per request (Outcome).  Evaluation
 // (not parsing) is timed and spread over `threads` std::threads; *seconds gets its wall time.
+int acs_oracle_is_allowed_shared(void* h, const char* shared_json, const char* requests, size_t n, int threads,
+                                 int32_t* out, double* seconds);
+
 int acs_oracle_is_allowed(void* h, const char* requests, size_t n, int threads, int32_t* out, double* seconds) {
+  return acs_oracle_is_allowed_shared(h, nullptr, requests, n, threads, out, seconds);
+}
+
+// shared_json: NULL, or a JSON array whose k-th element replaces every {"$shared": k} object
+// of the requests (parsed once, shared read-only by the requests that name it).
+int acs_oracle_is_allowed_shared(void* h, const char* shared_json, const char* requests, size_t n, int threads,
+                                 int32_t* out, double* seconds) {
   auto* o = (Oracle*)h;
   Arena arena;
   VP arr;
+  std::vector<VP> shared;
   try {
+    if (shared_json) {
+      Parser ps(shared_json, strlen(shared_json), arena);
+      VP sv = ps.value();
+      if (sv->t != T::Arr) throw std::runtime_error("shared: expected a JSON array");
+      shared = sv->a;
+    }
     Parser p(requests, strlen(requests), arena);
+    if (shared_json) p.shared = &shared;
     arr = p.value();
   } catch (const std::exception& e) {
     g_err = e.what();
@@ -1285,7 +1388,10 @@ int acs_oracle_is_allowed(void* h, const char* requests, size_t n, int threads, 
   }
   if (threads < 1) threads = 1;
   std::atomic<size_t> next{0};
+  const std::unordered_set<VP> shared_set(shared.begin(), shared.end());
   auto work = [&] {
+    Oracle::SharedIds cache;
+    cache.shared_values = &shared_set;
     for (;;) {
       const size_t i = next.fetch_add(64);
       if (i >= n) return;
@@ -1293,7 +1399,7 @@ int acs_oracle_is_allowed(void* h, const char* requests, size_t n, int threads, 
       for (size_t k = i; k < e; ++k) {
         Outcome r;
         try {
-          r = o->is_allowed(arr->a[k]);
+          r = o->is_allowed(arr->a[k], &cache);
         } catch (const JSError& err) {
           r.kind = 1;
           r.code = err.kind;

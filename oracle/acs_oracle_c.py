@@ -47,7 +47,10 @@ def lib():
         _LIB.acs_oracle_free.argtypes = [C.c_void_p]
         _LIB.acs_oracle_is_allowed.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_int, C.c_void_p,
                                                C.POINTER(C.c_double)]
+        _LIB.acs_oracle_is_allowed_shared.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, C.c_int,
+                                                      C.c_void_p, C.POINTER(C.c_double)]
         _LIB.acs_oracle_last_error.restype = C.c_char_p
+        _LIB.acs_oracle_regex_cell.argtypes = [C.c_char_p, C.c_char_p]
     return _LIB
 
 
@@ -75,14 +78,18 @@ class COracle:
         except Exception:
             pass
 
-    def raw(self, requests, threads=1):
+    def raw(self, requests, threads=1, shared=None):
         """(int32 [n, 4] outcome records, evaluation seconds): kind (0 ok, 1 rejects, 2
-        unsupported), decision code, evaluation_cacheable code, status / error kind."""
+        unsupported), decision code, evaluation_cacheable code, status / error kind.
+        ``shared``: values that {"$shared": k} objects inside the requests stand for (parsed
+        once; see SynthBatch.decode(i, shared=...))."""
         n = len(requests)
         out = np.zeros((n, 4), np.int32)
         sec = C.c_double(0.0)
         text = b"[" + b",".join(_json(r) for r in requests) + b"]"
-        rc = lib().acs_oracle_is_allowed(self.h, text, n, int(threads), out.ctypes.data, C.byref(sec))
+        stext = None if shared is None else b"[" + b",".join(_json(v) for v in shared) + b"]"
+        rc = lib().acs_oracle_is_allowed_shared(self.h, stext, text, n, int(threads), out.ctypes.data,
+                                                C.byref(sec))
         if rc != 0:
             raise RuntimeError(f"acs_oracle_is_allowed: {lib().acs_oracle_last_error().decode()}")
         return out, sec.value
@@ -92,6 +99,13 @@ class COracle:
         ('OK', decision, ec, status) / ('ERR', kind) / ('UNSUPPORTED',)."""
         out, _ = self.raw(requests, threads)
         return [outcome(r) for r in out]
+
+
+def regex_cell(rule_value, req_value) -> int:
+    """One entity namespace / RegExp step of the C++ oracle (None = null): bits as in
+    tests/golden/regex_cells.json, -1 when the pattern is outside its restated subset."""
+    enc = (lambda v: None if v is None else v.encode())
+    return int(lib().acs_oracle_regex_cell(enc(rule_value), enc(req_value)))
 
 
 def outcome(r):

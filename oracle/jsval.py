@@ -298,18 +298,38 @@ _SIMPLE_LITERAL = re.compile(r"^[A-Za-z0-9_\-\s#@%&=,;'\"<>~`!]*$")
 _SAFE_REGEX = re.compile(r"^[A-Za-z0-9_\-*+?|()\[\]^$]*$")
 
 
+def _v8_dollar(pattern: str) -> str:
+    """V8's ``$`` (no multiline flag) asserts end of input; Python's ``$`` also matches
+    before a trailing newline.  Outside character classes it becomes ``\\Z``."""
+    out, in_class = [], False
+    for ch in pattern:
+        if in_class:
+            in_class = ch != "]"
+            out.append(ch)
+        elif ch == "[":
+            in_class = True
+            out.append(ch)
+        else:
+            out.append("\\Z" if ch == "$" else ch)
+    return "".join(out)
+
+
 def js_regex_search(pattern: str, subject: str) -> bool:
     """``subject.match(new RegExp(pattern)) != null`` for patterns in a safe subset.
 
     Raises JSSyntaxError where V8 rejects the pattern; OracleUnsupported when
-    the oracle cannot guarantee V8-identical semantics.
+    the oracle cannot guarantee V8-identical semantics.  Pinned against V8 by
+    tests/golden/regex_cells.json (tests/golden/gen_regex_cells.js, run under node).
     """
     if _SIMPLE_LITERAL.match(pattern):
         return pattern in subject
     if not _SAFE_REGEX.match(pattern) or "(?" in pattern or "[]" in pattern or "[^]" in pattern:
         raise OracleUnsupported(f"regex pattern outside the restated subset: {pattern!r}")
     try:
-        rx = re.compile(pattern)
+        import warnings
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            rx = re.compile(_v8_dollar(pattern))
     except re.error as e:  # V8 rejects the same malformed forms in this subset
         raise JSSyntaxError(f"Invalid regular expression: /{pattern}/: {e}")
     return rx.search(subject) is not None

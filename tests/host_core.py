@@ -54,8 +54,9 @@ def is_allowed(cs, batch):
 
 
 def what_is_allowed(cs, batch):
+    from acs_mi355x.results import bits_layout
     blob = store_blob(cs)
-    words = (cs.n_sets + cs.n_pols + cs.n_rules + 31) // 32
+    words = bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)[2]
     n = batch.n
     bits = np.zeros((n, max(words, 1)), np.uint32)
     obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)
@@ -84,8 +85,9 @@ class Tables:
         return out
 
     def what_is_allowed(self, batch):
+        from acs_mi355x.results import bits_layout
         h = np.frombuffer(self.blob[:64], np.uint32)
-        words = max((int(h[2]) + int(h[3]) + int(h[4]) + 31) // 32, 1)
+        words = max(bits_layout(int(h[2]), int(h[3]), int(h[4]))[2], 1)
         n = batch.n
         bits = np.zeros((n, words), np.uint32)
         obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)

@@ -98,7 +98,7 @@ extern "C" int acs_host_what_is_allowed(const void* blob, size_t n, const acs_re
   Tables T;
   if (!host_tables(blob, n, &T)) return -1;
   Batch B = host_batch(b);
-  const uint32_t words = (T.n_sets + T.n_pols + T.n_rules + 31) / 32;
+  const uint32_t words = bits_layout(T.n_sets, T.n_pols, T.n_rules).words;
   for (uint32_t i = 0; i < B.n; ++i) {
     uint32_t* mb = bits + (size_t)i * words;
     for (uint32_t w = 0; w < words; ++w) mb[w] = 0;
@@ -128,7 +128,9 @@ extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const ac
       if (!(h.flags & RQ_HOST)) {
         const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks);
         const uint32_t s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
-        const Decision d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), nullptr, 0, log, s0, s1);
+        NullSink none;
+        const Decision d =
+            what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), BitsLayout{}, none, log, s0, s1);
         total = (d.flags & OF_ERR) ? 0u : log.total;
       }
       obl_n[k] = total;

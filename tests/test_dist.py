@@ -113,3 +113,34 @@ def test_partition_balanced_and_contiguous():
         sizes = [b - a for a, b in parts]
         assert max(sizes) - min(sizes) <= max(2, len(full) // 10)
     assert shard.partition(full, 300)[-1] == (len(full), len(full)) or len(full) >= 300
+
+
+# ---------------------------------------------------------------- the bench launcher
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=e)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    return r.returncode, lines, r.stderr
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_bench_launcher_spawns_ranks(n):
+    """`bench.py --gpus N` (no torch.distributed env) launches N ranks itself through
+    torch.distributed.run; every rank joins the collective (gloo here, RCCL on GPUs) and
+    rank 0 alone prints the line."""
+    rc, lines, err = _bench("--gpus", str(n), "--selftest")
+    assert rc == 0, err
+    assert lines == [{"selftest": True, "world_size": n, "max_rank_seen": n - 1}]
+
+
+def test_bench_launcher_rejects_world_mismatch():
+    rc, lines, err = _bench("--gpus", "2", "--selftest", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines and "--gpus 2 but WORLD_SIZE=1" in err

@@ -1,9 +1,12 @@
-"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracles.
 
 * every golden vector (isAllowed + whatIsAllowed) of the reference test suite,
 * randomised stores/requests that exercise the reference's quirks,
-* c2 / c3 / c4 synthetic configurations: a sample vs the oracle and the full
-  batch vs the CPU build of the same core (size-independent consistency),
+* c2 / c3 synthetic configurations: the WHOLE batch vs the C++ oracle (and a sample vs
+  the Python oracle); c4 whatIsAllowed vs the Python oracle; c5 (1M rules) and the
+  large-store filter modes on oracle samples, plus the CPU build of the same core as a
+  full-batch consistency check,
+* rule sharding (2/3/8 shards, c3 and c5 scale) vs an unsharded evaluation,
 * edge shapes: empty batch, ragged sizes, maximum attribute counts, device API.
 """
 import numpy as np
@@ -103,15 +106,39 @@ def _synth(kind, n):
     return doc, cs, synth.requests(cs, n, kind)
 
 
+def coracle_check(doc, cs, sb, dec, idx, chunk=10_000):
+    """The requests idx of a synthetic batch, decoded to the reference's JSON shape, re-decided
+    by the C++ oracle (16 threads; HR trees shared via placeholders): every outcome must
+    equal the GPU's record.  Returns the number compared."""
+    from oracle import acs_oracle_c
+    co = acs_oracle_c.COracle(FULL_URNS, DEFAULT_CAS, doc)
+    checked = 0
+    try:
+        for k in range(0, len(idx), chunk):
+            part = idx[k:k + chunk]
+            sh = synth.SharedValues()
+            out, _ = co.raw([sb.decode(int(i), sh) for i in part], 16, shared=sh.values)
+            for i, r in zip(part, out):
+                want = acs_oracle_c.outcome(r)
+                assert want[0] != "UNSUPPORTED", int(i)
+                assert gpu_outcome(cs, dec[i]) == want, int(i)
+                checked += 1
+    finally:
+        co.close()
+    return checked
+
+
 @pytest.mark.parametrize("kind,n,sample", [("c2", 300_000, 200), ("c3", 60_000, 40)])
 def test_synthetic_config_gpu(kind, n, sample):
     doc, cs, sb = _synth(kind, n)
     t = gpu_tables(cs)
     dec = t.is_allowed(sb.batch)
+    # the whole batch vs the C++ oracle (the reference's algorithm over the JSON requests)
+    assert coracle_check(doc, cs, sb, dec, np.arange(n)) == n
     # full batch: identical records to the CPU build of the same core
     ref = host_core.is_allowed(cs, sb.batch)
     assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
-    # sample vs the oracle on the decoded JSON requests
+    # sample vs the Python oracle on the decoded JSON requests
     o = Oracle(FULL_URNS)
     o.load(doc)
     idx = np.random.default_rng(7).choice(n, size=sample, replace=False)
@@ -137,6 +164,8 @@ def test_large_store_class_list_gpu():
     assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
     codes = np.bincount(dec["decision"], minlength=7)
     assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
+    idx = np.random.default_rng(11).choice(sb.batch.n, size=300, replace=False)
+    assert coracle_check(doc, cs, sb, dec, idx) == 300
 
 
 @pytest.mark.parametrize("kind", ["c3", "c5_small"])
@@ -158,6 +187,8 @@ def test_role_factor_gpu(kind, monkeypatch):
     ref = host_core.is_allowed(cs, sb.batch)
     assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
     assert np.array_equal(dev.view(np.uint64), ref.view(np.uint64))
+    idx = np.random.default_rng(12).choice(sb.batch.n, size=300, replace=False)
+    assert coracle_check(doc, cs, sb, dev, idx) == 300
 
 
 def test_what_is_allowed_c4_gpu():
@@ -170,7 +201,7 @@ def test_what_is_allowed_c4_gpu():
     o.load(doc)
     ok = np.flatnonzero((out["flags"] & L.OF_OBL_OVERFLOW) == 0)
     assert len(ok) > 0.3 * sb.batch.n  # log overflow -> host path, never a wrong answer
-    for i in np.random.default_rng(3).choice(ok, size=8, replace=False):
+    for i in np.random.default_rng(3).choice(ok, size=120, replace=False):
         got = norm_rq(results.reverse_query(cs, sb.batch.overlay, bits[i], obl[i][:obl_n[i]], out[i]))
         assert got == norm_rq(o.what_is_allowed(sb.decode(int(i)))), int(i)
     t.close()

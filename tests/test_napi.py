@@ -65,7 +65,12 @@ def test_node_batch_matches_c_abi(tmp_path):
     pobl, pobl_n = t.what_is_allowed_obl(sb.batch, np.arange(16, dtype=np.uint32), 128, 3)
     t.close()
     assert np.array_equal(np.frombuffer(tmp_path.joinpath("obl_n.bin").read_bytes(), np.uint32), pobl_n.reshape(-1))
-    assert np.array_equal(np.frombuffer(tmp_path.joinpath("obl.bin").read_bytes(), np.uint32), pobl.reshape(-1))
+    # log entries past a range's count are unspecified (device scratch): compare the logs
+    nobl = np.frombuffer(tmp_path.joinpath("obl.bin").read_bytes(), np.uint32).reshape(pobl.shape)
+    for c in range(pobl.shape[0]):
+        for j in range(pobl.shape[1]):
+            k = min(int(pobl_n[c, j]), pobl.shape[2])
+            assert np.array_equal(nobl[c, j, :k], pobl[c, j, :k]), (c, j)
     for f in ("out_sync.bin", "out_async.bin"):
         assert np.array_equal(np.frombuffer(tmp_path.joinpath(f).read_bytes(), np.uint8), want), f
     assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_bits.bin").read_bytes(), np.uint32),
