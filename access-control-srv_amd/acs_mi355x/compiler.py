@@ -457,6 +457,19 @@ class IncrementalCompiler:
         self.b = _Builder(urns, combining_algorithms)
         self.frags = {}
         self.stats = {"compiles": 0, "sets_compiled": 0, "sets_reused": 0}
+        self._base = None  # append-only table sizes right after the first (full) compile
+
+    def _sizes(self):
+        return len(self.b.d), len(self.b.rx_rows), len(self.b.ec_values)
+
+    def stale(self) -> bool:
+        """The shared dictionary, regex rows and evaluation_cacheable values only grow: strings
+        of replaced / removed rules stay.  True once any of them has more than doubled since
+        the full compile (a fresh compiler then reclaims them; the regex matrix each batch
+        computes is one cell per row, so stale rows cost every encode)."""
+        if self._base is None:
+            return False
+        return any(now > 2 * base + 64 for now, base in zip(self._sizes(), self._base))
 
     def compile(self, policy_sets: dict, dirty=None) -> CompiledStore:
         """``dirty``: keys whose sets changed in place (None: every set)."""
@@ -472,6 +485,8 @@ class IncrementalCompiler:
             new[key] = f
         self.frags = new
         self.stats["compiles"] += 1
+        if self._base is None:
+            self._base = self._sizes()
         return _assemble(self.b, frags)
 
 

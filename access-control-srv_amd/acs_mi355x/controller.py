@@ -75,6 +75,22 @@ class _Store(dict):
         super().update(*a, **kw)
         self._touch()
 
+    def popitem(self):
+        k, v = super().popitem()
+        self._touch(k)
+        return k, v
+
+    def setdefault(self, k, default=None):
+        if k in self:
+            return self[k]
+        self[k] = default  # __setitem__ tracks it
+        return default
+
+    def __ior__(self, other):
+        super().__ior__(other)
+        self._touch()
+        return self
+
     # JS Map spellings used by callers of the reference
     def set(self, k, v):
         self[k] = v
@@ -174,12 +190,28 @@ class AccessController:
                 self.invalidate(policySetID)
 
     # ------------------------------------------------------------------ tables
+    def _fresh_compiler(self):
+        self._compiler = compiler.IncrementalCompiler(self.urns, self.combiningAlgorithms)
+        self.stats["compiler_resets"] = self.stats.get("compiler_resets", 0) + 1
+
     def _ensure(self):
         if self._cs is not None:
             return
-        if self._compiler is None:
-            self._compiler = compiler.IncrementalCompiler(self.urns, self.combiningAlgorithms)
-        cs = self._compiler.compile(self._policy_sets, None if self._all_dirty else self._dirty)
+        # A fresh compiler (empty dictionary / regex rows) when every set is recompiled anyway
+        # (new Map, clearPolicies, invalidate()), or when the append-only tables have grown
+        # past twice their live size through updates; never an unbounded dictionary.
+        if self._compiler is None or self._all_dirty or self._compiler.stale():
+            self._fresh_compiler()
+            self._all_dirty = True
+        try:
+            cs = self._compiler.compile(self._policy_sets, None if self._all_dirty else self._dirty)
+        except Unsupported:
+            if self._all_dirty:
+                raise
+            # a capacity cap (65,535 regex rows, 255 evaluation_cacheable values) hit by stale
+            # entries: recompile everything from scratch; a live-store overflow raises again
+            self._fresh_compiler()
+            cs = self._compiler.compile(self._policy_sets, None)
         self._dirty, self._all_dirty = set(), False
         blob = compiler.store_blob(cs)
         if self._tables is not None:

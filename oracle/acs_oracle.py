@@ -163,13 +163,16 @@ def populate_store(doc):
 
 
 class NodeConditionEvaluator:
-    """utils.ts:47-56 ``conditionMatches`` executed by Node's own ``eval``.
+    """utils.ts:47-56 ``conditionMatches`` evaluated by Node's JS engine.
 
-    ``target`` and ``context`` are in scope exactly as in the reference; a
-    function-valued result is called with (request, target, context).
+    ``target``, ``context`` and ``request`` are in scope as in the reference's ``eval``;
+    a function-valued result is called with (request, target, context).  The condition
+    text comes from test fixtures, so it runs in a fresh ``vm`` context holding only those
+    three values — no ``require``, ``process`` or module scope — under a 1 s time limit.
     """
 
     _SCRIPT = r"""
+const vm = require('vm');
 const rl = require('readline').createInterface({input: process.stdin});
 rl.on('line', (line) => {
   const msg = JSON.parse(line);
@@ -179,7 +182,8 @@ rl.on('line', (line) => {
     const r = ((condition, request) => {
       const { target, context } = request;
       condition = condition.replace(/\\n/g, '\n');
-      const evalResult = eval(condition);
+      const sandbox = vm.createContext({target, context, request});
+      const evalResult = vm.runInContext(condition, sandbox, {timeout: 1000});
       if (typeof evalResult === 'function') { return evalResult(request, target, context); }
       return evalResult;
     })(msg.condition, request);

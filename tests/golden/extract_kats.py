@@ -8,8 +8,10 @@ does not have).  It extracts, for every ``it(...)`` block of
     test/microservice.spec.ts
 
 that calls isAllowed / whatIsAllowed: the policy fixture in force, the
-``buildRequest`` options (a plain JS object literal, parsed with Node's JSON
-serialiser — no reference code is executed), the request post-edits the test
+``buildRequest`` options (a plain JS object literal, read by the restricted
+literal parser below — objects, arrays, strings, numbers, true / false / null /
+undefined and comments, nothing else; no reference text is ever executed), the
+request post-edits the test
 makes, and the asserted outcome (decision / status, or the whatIsAllowed
 structure assertions as path checks).  Each vector records its spec file:line.
 The fixture YAMLs the vectors refer to are converted to JSON next to it.
@@ -21,7 +23,6 @@ from __future__ import annotations
 import json
 import os
 import re
-import subprocess
 import sys
 
 import yaml
@@ -33,10 +34,138 @@ from build_request import build_request  # noqa: E402
 SPECS = ["core.spec.ts", "properties.spec.ts", "acl.spec.ts", "microservice.spec.ts"]
 
 
+class LiteralError(ValueError):
+    pass
+
+
+_UNDEF = object()
+
+
 def js_literal_to_json(text: str):
-    out = subprocess.run(["node", "-e", f"process.stdout.write(JSON.stringify(({text})))"],
-                         capture_output=True, text=True, check=True)
-    return json.loads(out.stdout)
+    """Value of a JS object / array / scalar literal, as JSON.stringify would give it
+    (``undefined`` object members dropped, ``undefined`` array items -> null).  A restricted
+    recursive-descent parser: anything but objects, arrays, quoted strings, numbers,
+    true / false / null / undefined, trailing commas and comments raises LiteralError —
+    the text comes from the reference's spec files and is never evaluated."""
+    i, n = 0, len(text)
+
+    def ws():
+        nonlocal i
+        while i < n:
+            if text[i].isspace():
+                i += 1
+            elif text.startswith("//", i):
+                j = text.find("\n", i)
+                i = n if j < 0 else j + 1
+            elif text.startswith("/*", i):
+                j = text.find("*/", i + 2)
+                if j < 0:
+                    raise LiteralError("unterminated comment")
+                i = j + 2
+            else:
+                return
+
+    def string():
+        nonlocal i
+        q = text[i]
+        i += 1
+        out = []
+        while i < n and text[i] != q:
+            c = text[i]
+            if c == "\\":
+                i += 1
+                if i >= n:
+                    raise LiteralError("bad escape")
+                e = text[i]
+                simple = {"n": "\n", "t": "\t", "r": "\r", "b": "\b", "f": "\f", "v": "\v", "0": "\0"}
+                if e in simple:
+                    out.append(simple[e])
+                elif e == "u":
+                    out.append(chr(int(text[i + 1:i + 5], 16)))
+                    i += 4
+                elif e == "\n":
+                    pass  # line continuation
+                else:
+                    out.append(e)
+                i += 1
+            else:
+                out.append(c)
+                i += 1
+        if i >= n:
+            raise LiteralError("unterminated string")
+        i += 1
+        return "".join(out)
+
+    def ident():
+        nonlocal i
+        m = re.match(r"[A-Za-z_$][\w$]*", text[i:])
+        if not m:
+            raise LiteralError(f"unexpected {text[i:i + 20]!r}")
+        i += m.end()
+        return m.group(0)
+
+    def value():
+        nonlocal i
+        ws()
+        if i >= n:
+            raise LiteralError("unexpected end")
+        c = text[i]
+        if c == "{":
+            i += 1
+            obj = {}
+            while True:
+                ws()
+                if text[i] == "}":
+                    i += 1
+                    return obj
+                key = string() if text[i] in "'\"" else ident()
+                ws()
+                if text[i] != ":":
+                    raise LiteralError(f"expected ':' after {key!r}")
+                i += 1
+                v = value()
+                if v is not _UNDEF:
+                    obj[key] = v
+                else:
+                    obj.pop(key, None)
+                ws()
+                if text[i] == ",":
+                    i += 1
+                elif text[i] != "}":
+                    raise LiteralError("expected ',' or '}'")
+        if c == "[":
+            i += 1
+            arr = []
+            while True:
+                ws()
+                if text[i] == "]":
+                    i += 1
+                    return arr
+                v = value()
+                arr.append(None if v is _UNDEF else v)
+                ws()
+                if text[i] == ",":
+                    i += 1
+                elif text[i] != "]":
+                    raise LiteralError("expected ',' or ']'")
+        if c in "'\"":
+            return string()
+        m = re.match(r"-?(\d+\.?\d*(e[+-]?\d+)?|\.\d+)", text[i:], re.I)
+        if m:
+            i += m.end()
+            x = float(m.group(0))
+            return int(x) if x.is_integer() else x
+        word = ident()
+        consts = {"true": True, "false": False, "null": None, "undefined": _UNDEF}
+        if word not in consts:
+            raise LiteralError(f"identifier {word!r} is not a literal")
+        return consts[word]
+
+    v = value()
+    ws()
+    if i != n:
+        raise LiteralError(f"trailing text {text[i:i + 20]!r}")
+    return None if v is _UNDEF else v
 
 
 def matching_paren(src: str, i: int) -> int:

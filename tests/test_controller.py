@@ -210,3 +210,41 @@ def test_controller_default_engine_gpu():
     for v, r in zip(vecs, ctl.isAllowed_batch([v["request"] for v in vecs])):
         assert r["decision"] == v["expect"]["decision"]
     ctl.close()
+
+
+def test_many_updates_keep_tables_bounded():
+    """Hundreds of updateRule / removeRule cycles on one controller, each with a new entity
+    value: stale dictionary entries / regex rows are reclaimed by a fresh compile, decisions
+    stay equal to the oracle's, and the append-only tables stay near the live store's size."""
+    urns = randgen.U
+    doc = {"policy_sets": [{"id": "s", "combining_algorithm": randgen.CAS[0], "policies": [
+        {"id": "p", "combining_algorithm": randgen.CAS[1], "rules": []}]}]}
+    ctl = _ctl(urns)
+    ctl.policySets = pstore.populate(doc)
+    o = Oracle(urns=urns)
+    o.load(doc)
+
+    def rule(k):
+        return {"id": f"r{k % 3}", "effect": "PERMIT" if k % 2 else "DENY",
+                "target": {"subjects": [{"id": urns["role"], "value": "u"}],
+                           "resources": [{"id": urns["entity"], "value": f"urn:x:model:e{k}.E{k}"}]}}
+
+    def req(k):
+        return {"target": {"subjects": [{"id": urns["role"], "value": "u"}],
+                           "resources": [{"id": urns["entity"], "value": f"urn:x:model:e{k}.E{k}"}]},
+                "context": {"subject": {"id": "a", "role_associations": [{"role": "u"}], "hierarchical_scopes": []},
+                            "resources": []}}
+    for k in range(400):
+        a, b = _wrap(ry=rule(k))
+        ctl.updateRule("s", "p", a)
+        o.update_rule("s", "p", b)
+        if k % 7 == 0:
+            ctl.removeRule("s", "p", f"r{(k + 1) % 3}")
+            o.remove_rule("s", "p", f"r{(k + 1) % 3}")
+        if k % 4 == 0:  # a compile: each one interns the live rules' values
+            ctl.isAllowed(req(k))
+        if k % 25 == 0:
+            for q in (req(k), req(k - 1), req(k + 1)):
+                assert _outcome(ctl.isAllowed(q)) == oracle_outcome(o, q)
+    assert ctl.stats["compiler_resets"] >= 2
+    assert len(ctl._compiler.b.rx_rows) <= 2 * 3 + 64

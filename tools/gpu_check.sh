@@ -18,11 +18,13 @@ step() {  # name limit cmd...
 STEPS=${STEPS:-"tests smoke bench prof"}
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    tests) step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ;;
+    rehearse) step rehearse_launcher 600 env ACS_BENCH_REHEARSAL=1 python bench.py --gpus 2 --config c2 --steps 5 --warmup 1 --no-cpu-baseline ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+    bench) step bench 900 python bench.py --steps 20 --warmup 3 ;;
+    bench2) step bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 ;;
     nosort) step bench_nosort 600 python bench.py --steps 5 --warmup 1 --no-sort --no-cpu-baseline ;;
-    quick) step bench_quick 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie ;;
+    quick) step bench_quick 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline --no-pcie ;;
     quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
@@ -54,7 +56,7 @@ for s in $STEPS; do
     shard) step bench_rule_shard 600 python bench.py --rule-shard --steps 20 --warmup 3 --no-cpu-baseline ;;
     shard3) step bench_c3_rule_shard 900 python bench.py --config c3 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
     prof4) step rocprof_c4 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 bench.py --config c4 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --config c2 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
   esac
 done
 echo "== done"
