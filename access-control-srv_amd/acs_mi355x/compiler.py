@@ -495,13 +495,56 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
     return IncrementalCompiler(urns, combining_algorithms).compile(policy_sets)
 
 
-def store_blob(cs: CompiledStore) -> bytes:
-    """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header)."""
+# URN config names the native request codec (csrc/acs_codec.cpp) reads, in this order.
+CODEC_URNS = ("entity", "property", "operation", "resourceID", "actionID", "role", "roleScopingEntity",
+              "roleScopingInstance", "hierarchicalRoleScoping", "ownerEntity", "ownerInstance",
+              "aclIndicatoryEntity", "aclInstance", "create", "read", "modify", "delete", "user", "skipACL",
+              "maskedProperty")
+CODEC_MAGIC, CODEC_VERSION = 0x43534341, 1  # "ACSC"
+
+
+def codec_section(cs: CompiledStore) -> bytes:
+    """What the native request codec needs besides the node tables (include/acs_mi355x.h,
+    acs_codec_create): the interned dictionary (id -> UTF-8 string), the URN ids, the rule
+    entity value of every regex-matrix row and the per-node candidate specs (candidates.py)."""
     import struct
-    hdr = struct.pack("<16I", 0x31534341, 4, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
-                      len(cs.pairs), len(cs.u32pool), cs.id_user, 0, 0, 0, 0, 0, 0, 0)
-    parts = [hdr]
+    d = cs.dictionary
+    urn_ids = [d.intern(cs.urns.get(k, MISSING)) if isinstance(cs.urns.get(k, MISSING), str) or
+               cs.urns.get(k, MISSING) is MISSING else L.ID_UNDEF for k in CODEC_URNS]
+    rx = [d.lookup(v) for v in cs.rx_rows]
+    spec = [x for sec in cs.cand_spec for x in sec]
+    kind = np.array([1 if x is None else (2 if x else 0) for x in spec], np.uint8)
+    ptr = np.zeros(len(spec) + 1, np.uint32)
+    idx = []
+    for k, x in enumerate(spec):
+        if x:
+            idx.extend(x)
+        ptr[k + 1] = len(idx)
+    enc = [s.encode("utf-8", "surrogatepass") if isinstance(s, str) else b"" for s in d.strings]
+    offs = np.zeros(len(enc) + 1, np.uint32)
+    offs[1:] = np.cumsum([len(e) for e in enc]) if enc else []
+    sbytes = b"".join(enc)
+
+    def pad4(b):
+        return b + b"\0" * ((-len(b)) % 4)
+    hdr = struct.pack("<8I", CODEC_MAGIC, CODEC_VERSION, len(enc), len(CODEC_URNS), len(rx), len(spec), len(idx),
+                      len(sbytes))
+    return b"".join([hdr, np.array(urn_ids, np.uint32).tobytes(), np.array(rx, np.uint32).tobytes(),
+                     pad4(kind.tobytes()), ptr.tobytes(), np.array(idx, np.uint32).tobytes(), offs.tobytes(),
+                     pad4(sbytes)])
+
+
+def store_blob(cs: CompiledStore, codec: bool = True) -> bytes:
+    """Serialise tables into the acs_compile() image (include/acs_mi355x.h: acs_blob_header),
+    followed by the codec section (header reserved[0] / [1] = its byte offset / length)."""
+    import struct
+    parts = []
     for a in (cs.sets, cs.pols, cs.rules, cs.rres, cs.pairs, cs.u32pool):
         b = np.ascontiguousarray(a).tobytes()
         parts.append(b + b"\0" * ((-len(b)) % 16))
-    return b"".join(parts)
+    body = b"".join(parts)
+    sec = codec_section(cs) if codec else b""
+    off = 64 + len(body) if sec else 0
+    hdr = struct.pack("<16I", 0x31534341, 4, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
+                      len(cs.pairs), len(cs.u32pool), cs.id_user, off, len(sec), 0, 0, 0, 0, 0)
+    return hdr + body + sec

@@ -71,6 +71,8 @@ def cell(rule_value, req_value) -> int:
     """Bits for one (rule entity value, request entity value) pair."""
     if nullish(rule_value) or nullish(req_value):
         return RX_THROW_TYPE  # nsEntityArray[0] / reqNSEntityArray[0] of undefined
+    if not (rule_value.isascii() and req_value.isascii()):
+        return RX_HOST  # toUpperCase / RegExp over non-ASCII text: the host decides (Unicode-version exact)
     r_prefix, r_first, r_last = _split_entity(rule_value)
     q_prefix, q_first, q_last = _split_entity(req_value)
     bits = RX_RESET if r_prefix != q_prefix else 0

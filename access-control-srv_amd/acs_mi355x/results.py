@@ -33,6 +33,15 @@ class EvaluationError(Exception):
         self.kind = kind
 
 
+def _raise_err(d):
+    """An error record: the reference's rejection, or — ERR_REGEX_HOST — an entity RegExp
+    cell outside the precomputed subset, which only the host can decide."""
+    if int(d["flags"]) & L.OF_ERR:
+        if int(d["err"]) == L.ERR_REGEX_HOST:
+            raise HostPathRequired("entity RegExp outside the precomputed subset")
+        raise EvaluationError(L.ERR_NAMES.get(int(d["err"]), "Error"))
+
+
 def _ec_value(cs, code):
     return cs.ec_values[code] if code < len(cs.ec_values) else MISSING
 
@@ -44,8 +53,7 @@ def decision_record(cs, d, reason=None):
         raise HostPathRequired(reason or "request flagged for the host path")
     if flags & L.OF_HOST_COND:
         raise HostPathRequired("rule condition (JS eval)", int(d["aux"]))
-    if flags & L.OF_ERR:
-        raise EvaluationError(L.ERR_NAMES.get(int(d["err"]), "Error"))
+    _raise_err(d)
     if flags & L.OF_NO_TARGET:
         return {"decision": "DENY", "evaluation_cacheable": False, "obligations": [],
                 "operation_status": {"code": 400, "message": "Access request had no target. Skipping request"}}
@@ -113,8 +121,7 @@ def reverse_query(cs, overlay, bits_row, obl_pairs, d, reason=None):
     flags = int(d["flags"])
     if flags & L.OF_HOST_REQ:
         raise HostPathRequired(reason or "request flagged for the host path")
-    if flags & L.OF_ERR:
-        raise EvaluationError(L.ERR_NAMES.get(int(d["err"]), "Error"))
+    _raise_err(d)
     if flags & L.OF_OBL_OVERFLOW:
         raise HostPathRequired("maskedProperty log overflow")
     sets, pols, rules = inclusion(cs, bits_row)

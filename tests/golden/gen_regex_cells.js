@@ -87,6 +87,24 @@ for (const p of patterns) {
     for (const q of requestValues) pairs.push([rv, q, cell(rv, q)]);
   }
 }
+// Seeded random patterns over the metacharacter subset the evaluator computes itself
+// (letters, digits, '-', '_', '|', '(', ')', '[', ']', '^', '$', '*', '+', '?'): V8 decides
+// both which of them are SyntaxErrors and what they match.
+let seed = 0xACC5;
+const rnd = (k) => { seed = (seed * 1103515245 + 12345) & 0x7fffffff; return seed % k; };
+const alphabet = ['E', 'n', 't', '1', '2', '-', '_', '|', '(', ')', '[', ']', '^', '$', '*', '+', '?'];
+const fuzzSubjects = ['urn:x:model:ent.Ent1', 'urn:x:model:ent.Ent12', 'urn:x:model:ent.Ent1\n', 'urn:x:model:ent.nt',
+                      'urn:x:model:ent.E-1', 'urn:x:model:ent.', 'urn:x:model:ent.t2t'];
+const seen = new Set();
+while (seen.size < 1500) {
+  let p = '';
+  const len = 1 + rnd(7);
+  for (let k = 0; k < len; ++k) p += alphabet[rnd(alphabet.length)];
+  if (seen.has(p)) continue;
+  seen.add(p);
+  const rv = 'urn:x:model:ent.' + p;
+  for (const q of fuzzSubjects) pairs.push([rv, q, cell(rv, q)]);
+}
 // nullish operands (JSON null): the TypeError cells
 for (const q of ['urn:x:model:ent.Ent1', null]) pairs.push([null, q, cell(null, q)]);
 pairs.push(['urn:x:model:ent.Ent1', null, cell('urn:x:model:ent.Ent1', null)]);

@@ -82,7 +82,8 @@ def test_cpp_oracle_equal_v8():
 
 
 def test_host_decisions_agree_with_v8_where_product_and_oracle_both_decide():
-    """Product and oracle send the same patterns to the host: one shared subset."""
+    """The product sends to the host every pattern the oracle cannot restate (plus non-ASCII
+    values, which the oracle computes and the product leaves to the host)."""
     o = Oracle(FULL_URNS)
     for rv, qv, _ in PAIRS:
         p_host = bool(cell(rv, qv) & L.RX_HOST)
@@ -93,7 +94,10 @@ def test_host_decisions_agree_with_v8_where_product_and_oracle_both_decide():
             o_host = True
         except JSError:
             o_host = False
-        assert p_host == o_host, (rv, qv)
+        if o_host:
+            assert p_host, (rv, qv)
+        elif p_host:
+            assert not (rv.isascii() and qv.isascii()), (rv, qv)
 
 
 # ---------------------------------------------------------------- stores from the patterns
@@ -111,6 +115,8 @@ def regex_store_cases():
     by_pat = {}
     for rv in dict.fromkeys(rv for rv, _, _ in PAIRS if rv is not None):
         by_pat.setdefault(rv[rv.rfind(":") + 1:].split(".")[-1], []).append(rv)
+    # the curated patterns (each under all 4 namespace prefixes); the fuzzed ones are cell tests
+    by_pat = {k: v for k, v in by_pat.items() if len(v) >= 4}
     reqv = sorted({qv for _, qv, _ in PAIRS if qv is not None})
     reqs = []
     for k, qv in enumerate(reqv):
