@@ -21,8 +21,10 @@ HOST_LIB = os.path.join(ROOT, "tests", "native", "libacs_core_host.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-_HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h")] + \
+_HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h", "acs_json.h")] + \
     [os.path.join(ROOT, "include", "acs_mi355x.h")]
+# host-only C++ of the product library: the native request codec and its JSON reader
+_HOST_SRCS = [os.path.join(CSRC, f) for f in ("acs_codec.cpp", "acs_json.cpp")]
 
 
 def _stale(out, srcs):
@@ -32,18 +34,30 @@ def _stale(out, srcs):
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
-def _hipcc(src, out, extra=()):
+def _hipcc(src, out, extra=(), host_srcs=()):
+    """hipcc for gfx950; `host_srcs` (plain C++, no device code) are compiled with g++ into
+    objects next to `out` and linked into the same shared library."""
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    objs = []
+    for h in host_srcs:
+        o = out + "." + os.path.basename(h) + ".o"
+        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread",
+                        "-I", CSRC, "-I", os.path.join(ROOT, "include"), "-c", h, "-o", o], check=True)
+        objs.append(o)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-function", "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, src, "-o", out + ".tmp"]
+           "-Wno-unused-function", "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, src,
+           *(["-x", "none", *objs] if objs else []),
+           "-lpthread", "-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
 
 
 def build_product(force=False):
     src = os.path.join(CSRC, "acs_kernels.hip")
-    if force or _stale(LIB, [src] + _HEADERS):
-        _hipcc(src, LIB)
+    if force or _stale(LIB, [src] + _HEADERS + _HOST_SRCS):
+        _hipcc(src, LIB, host_srcs=_HOST_SRCS)
     return LIB
 
 
@@ -53,8 +67,8 @@ PROF_LIB = os.path.join(PKG, "lib", "libacs_mi355x_prof.so")
 def build_prof(force=False):
     """Phase-profiling variant of the product library (-DACS_PHASE_PROF; tools/phase_prof.py)."""
     src = os.path.join(CSRC, "acs_kernels.hip")
-    if force or _stale(PROF_LIB, [src] + _HEADERS):
-        _hipcc(src, PROF_LIB, ("-DACS_PHASE_PROF",))
+    if force or _stale(PROF_LIB, [src] + _HEADERS + _HOST_SRCS):
+        _hipcc(src, PROF_LIB, ("-DACS_PHASE_PROF",), host_srcs=_HOST_SRCS)
     return PROF_LIB
 
 
@@ -62,8 +76,8 @@ def build_variant(name, defines, force=False):
     """Experimental build of the product library with extra -D flags (lib/variants/<name>.so)."""
     out = os.path.join(PKG, "lib", "variants", name + ".so")
     src = os.path.join(CSRC, "acs_kernels.hip")
-    if force or _stale(out, [src] + _HEADERS):
-        _hipcc(src, out, tuple("-D" + d for d in defines))
+    if force or _stale(out, [src] + _HEADERS + _HOST_SRCS):
+        _hipcc(src, out, tuple("-D" + d for d in defines), host_srcs=_HOST_SRCS)
     return out
 
 

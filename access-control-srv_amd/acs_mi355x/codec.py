@@ -1,0 +1,169 @@
+"""ctypes binding of the native request codec (include/acs_mi355x.h: acs_codec_*).
+
+JSON request text -> packed batch on host threads (csrc/acs_codec.cpp, the C++ restatement
+of encoder.py).  ``NativeCodec(blob).encode(json_bytes)`` returns a ``CodecBatch`` whose
+arrays are zero-copy numpy views of the codec's buffers with the attribute names of
+encoder.RequestBatch, so native.Tables / device.DeviceBatch / results take either.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+
+import numpy as np
+
+from . import layout as L
+from .jsops import MISSING
+from .native import ReqBatchC, last_error, load
+
+_DECLARED = set()
+
+
+def _lib():
+    lib = load()
+    if id(lib) not in _DECLARED:
+        vp = C.c_void_p
+        lib.acs_codec_create.restype = vp
+        lib.acs_codec_create.argtypes = [vp, C.c_size_t]
+        lib.acs_codec_free.argtypes = [vp]
+        lib.acs_codec_free.restype = None
+        lib.acs_codec_set_subject_scopes.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        lib.acs_codec_evict_subject.argtypes = [vp, C.c_char_p, C.c_size_t]
+        lib.acs_codec_encode.restype = vp
+        lib.acs_codec_encode.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_int]
+        lib.acs_codec_batch_view.argtypes = [vp, C.POINTER(ReqBatchC)]
+        lib.acs_codec_batch_reason.restype = C.c_char_p
+        lib.acs_codec_batch_reason.argtypes = [vp, C.c_uint32]
+        lib.acs_codec_string.argtypes = [vp, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        lib.acs_codec_batch_stats.argtypes = [vp, C.POINTER(C.c_double), C.c_int]
+        lib.acs_codec_batch_free.argtypes = [vp]
+        lib.acs_codec_batch_free.restype = None
+        _DECLARED.add(id(lib))
+    return lib
+
+
+def _view(ptr, dtype, count):
+    if count == 0 or not ptr:
+        return np.zeros(0, dtype)
+    buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=count)
+
+
+class _Strings:
+    """Overlay-compatible id -> string view of one encoded batch."""
+
+    def __init__(self, batch):
+        self._b = batch
+
+    def string(self, i):
+        s, n = C.c_void_p(), C.c_size_t()
+        k = _lib().acs_codec_string(self._b.h, int(i), C.byref(s), C.byref(n))
+        if k == 0:
+            return MISSING
+        if k == 1:
+            return None
+        if k < 0:
+            raise KeyError(i)
+        return C.string_at(s.value, n.value).decode("utf-8", "surrogatepass") if n.value else ""
+
+
+class CodecBatch:
+    """One encoded batch (owns the codec's buffers until close())."""
+
+    def __init__(self, handle, codec):
+        self.h = handle
+        self._codec = codec  # the batch reads the codec's dictionary: keep it alive
+        s = ReqBatchC()
+        if _lib().acs_codec_batch_view(handle, C.byref(s)) != 0:
+            raise RuntimeError(last_error())
+        self.struct = s
+        n = self.n = int(s.n)
+        self.hdr = _view(s.hdr, L.REQ_HDR_DT, n)
+        self.res = _view(s.res, L.REQ_RES_DT, L.QMAX * n).reshape(L.QMAX, n)
+        self.subj = _view(s.subj, L.PAIR_DT, L.SMAX * n).reshape(L.SMAX, n)
+        self.act = _view(s.act, L.PAIR_DT, L.AMAX * n).reshape(L.AMAX, n)
+        self.roles = _view(s.roles, np.uint32, L.RMAX * n).reshape(L.RMAX, n)
+        self.arena = _view(s.arena, np.uint32, int(s.arena_words))
+        self.rx = _view(s.rx, np.uint8, s.rx_cols * s.rx_rows).reshape(s.rx_cols, s.rx_rows)
+        self.rx_rows = int(s.rx_rows)
+        W = int(s.cand_words)
+        self.cand = _view(s.cand, np.uint32, s.cand_rows * W).reshape(s.cand_rows, W) if s.cand else None
+        self.cand_wp, self.cand_wr = int(s.cand_wp), int(s.cand_wr)
+        self.role_key = _view(s.role_key, np.uint32, n) if s.role_key else None
+        self.role_bits = (_view(s.role_rows_bits, np.uint32, s.role_rows * W).reshape(s.role_rows, W)
+                          if s.role_key else None)
+        self.overlay = _Strings(self)
+        self.host_reasons = {}
+        for i in np.flatnonzero((self.hdr["flags"] & np.uint32(L.RQ_HOST)) != 0):
+            r = _lib().acs_codec_batch_reason(handle, int(i))
+            self.host_reasons[int(i)] = r.decode() if r else "host path"
+
+    def stats(self):
+        out = (C.c_double * 6)()
+        _lib().acs_codec_batch_stats(self.h, out, 6)
+        return {"encode_s": out[0], "regex_s": out[1], "classes_s": out[2], "total_s": out[3],
+                "hr_cache_hits": int(out[4]), "hr_cache_misses": int(out[5])}
+
+    def nbytes(self):
+        return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
+            (self.cand.nbytes if self.cand is not None else 0) + \
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
+
+    def close(self):
+        if self.h:
+            for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx", "cand", "role_key", "role_bits"):
+                setattr(self, k, None)
+            _lib().acs_codec_batch_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NativeCodec:
+    """The native encoder of one compiled store image (compiler.store_blob)."""
+
+    def __init__(self, blob: bytes):
+        self._blob = blob
+        self.h = _lib().acs_codec_create(blob, len(blob))
+        if not self.h:
+            raise RuntimeError(last_error())
+
+    def set_subject_scopes(self, key: str, scopes) -> None:
+        """Register (or replace) a subject's hierarchical_scopes forest; requests name it with
+        context.subject["$hrs"] = key (the createHRScope / Redis cache of the reference)."""
+        k = key.encode()
+        text = scopes if isinstance(scopes, (bytes, bytearray)) else json.dumps(scopes).encode()
+        if _lib().acs_codec_set_subject_scopes(self.h, k, len(k), bytes(text), len(text)) != 0:
+            raise RuntimeError(last_error())
+
+    def evict_subject(self, key: str) -> bool:
+        k = key.encode()
+        return _lib().acs_codec_evict_subject(self.h, k, len(k)) == 1
+
+    def encode(self, requests, threads: int = 1) -> CodecBatch:
+        """``requests``: JSON text (bytes/str) of an array of requests, or a list to serialise."""
+        if isinstance(requests, str):
+            text = requests.encode("utf-8", "surrogatepass")
+        elif isinstance(requests, (bytes, bytearray, memoryview)):
+            text = bytes(requests)
+        else:
+            text = json.dumps(requests, ensure_ascii=False, separators=(",", ":")).encode("utf-8", "surrogatepass")
+        h = _lib().acs_codec_encode(self.h, text, len(text), int(threads))
+        if not h:
+            raise RuntimeError(last_error())
+        return CodecBatch(h, self)
+
+    def close(self):
+        if self.h:
+            _lib().acs_codec_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

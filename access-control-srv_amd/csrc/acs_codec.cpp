@@ -23,7 +23,9 @@
 // request then costs one hash lookup per owner instance instead of a tree walk.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <regex>
@@ -277,3 +279,1373 @@ void build_forest(HrForest& F, const JV* hrs) {
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------ the codec (per store image)
+struct acs_codec {
+  // store image
+  uint32_t S = 0, P = 0, R = 0, ws = 0, wp = 0, wr = 0, W = 0;
+  std::vector<NodeRec> nodes;  // sets | policies | rules
+  std::vector<Pair> pairs;
+  // dictionary
+  std::string sbytes;
+  std::vector<uint32_t> soff;
+  std::unordered_map<std::string_view, uint32_t> dict;
+  uint32_t n_dict = 0;
+  uint32_t urn[U_COUNT] = {};
+  std::string_view urn_s[U_COUNT];
+  // regex rows
+  std::vector<uint32_t> rx_row_id;
+  std::vector<RxPattern> rx_pat;
+  std::unordered_map<uint32_t, uint32_t> row_of_id;  // dictionary id of a row's value -> row
+  // candidate specs (candidates.py): per rx row the nodes whose entity spec lists it; nodes
+  // always a candidate; per required role the nodes requiring it
+  std::vector<uint32_t> row_ptr, row_nodes;
+  std::vector<uint32_t> always_bits;          // [W]
+  std::vector<uint32_t> role_ids;             // sorted
+  std::vector<int32_t> node_role;             // per node: index into role_ids or -1
+  std::vector<uint32_t> norole_bits;          // [W]
+  std::vector<std::vector<uint32_t>> role_node_list;  // per role row: node indices
+  std::vector<uint8_t> node_need_act;
+  // caches
+  std::shared_mutex hr_mu;
+  std::unordered_map<uint64_t, std::vector<std::shared_ptr<const HrForest>>> hr_inline;
+  std::unordered_map<std::string, std::shared_ptr<const HrForest>> hr_subject;
+  size_t hr_bytes = 0;
+  std::mutex col_mu;
+  std::unordered_map<std::string, std::shared_ptr<const std::vector<uint8_t>>> rx_cols;     // value key -> cells
+  std::unordered_map<std::string, std::shared_ptr<const std::vector<uint32_t>>> ent_rows;   // value key -> [W]
+  std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint32_t>>> act_rows;      // pair -> [W]
+  std::atomic<uint64_t> hr_hits{0}, hr_misses{0};
+
+  // global node index -> (section word offset, bit)
+  uint32_t node_word(uint32_t g) const {
+    if (g < S) return g >> 5;
+    if (g < S + P) return ws + ((g - S) >> 5);
+    return ws + wp + ((g - S - P) >> 5);
+  }
+  uint32_t node_bit(uint32_t g) const {
+    const uint32_t l = g < S ? g : (g < S + P ? g - S : g - S - P);
+    return 1u << (l & 31);
+  }
+  std::string_view string_of(uint32_t id) const {
+    if (id >= n_dict) return {};
+    return std::string_view(sbytes.data() + soff[id], soff[id + 1] - soff[id]);
+  }
+  uint32_t lookup(std::string_view s) const {
+    auto it = dict.find(s);
+    return it == dict.end() ? NONE32 : it->second;
+  }
+};
+
+namespace {
+
+template <class T>
+bool take(const uint8_t*& p, const uint8_t* e, std::vector<T>& out, size_t n, size_t align = 4) {
+  const size_t bytes = n * sizeof(T);
+  if ((size_t)(e - p) < bytes) return false;
+  out.resize(n);
+  if (n) memcpy(out.data(), p, bytes);
+  p += (bytes + align - 1) / align * align;
+  return true;
+}
+
+bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err) {
+  acs_blob_header h;
+  if (!blob || n_bytes < sizeof h) return err = "blob too small", false;
+  memcpy(&h, blob, sizeof h);
+  if (h.magic != ACS_BLOB_MAGIC || h.version != ACS_ABI_VERSION) return err = "bad blob magic/version", false;
+  const uint32_t off = h.reserved[0], len = h.reserved[1];
+  if (!off || (size_t)off + len > n_bytes) return err = "blob has no codec section (compiler.store_blob)", false;
+  c->S = h.n_sets;
+  c->P = h.n_pols;
+  c->R = h.n_rules;
+  c->ws = words_of(c->S);
+  c->wp = words_of(c->P);
+  c->wr = words_of(c->R);
+  c->W = c->ws + c->wp + c->wr;
+  // node tables (16-B aligned sections after the 64-B header)
+  const uint8_t* base = (const uint8_t*)blob;
+  const uint8_t* p = base + 64;
+  const uint8_t* e = base + off;
+  auto a16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+  const size_t nn = (size_t)c->S + c->P + c->R;
+  if ((size_t)(e - p) < a16(nn * 64)) return err = "truncated node tables", false;
+  c->nodes.resize(nn);
+  memcpy(c->nodes.data(), p, c->S * 64);
+  p += a16(c->S * 64ull);
+  memcpy(c->nodes.data() + c->S, p, c->P * 64ull);
+  p += a16(c->P * 64ull);
+  memcpy(c->nodes.data() + c->S + c->P, p, c->R * 64ull);
+  p += a16(c->R * 64ull);
+  p += a16(h.n_rres * 16ull);
+  if ((size_t)(e - p) < h.n_pairs * 8ull) return err = "truncated pair pool", false;
+  c->pairs.resize(h.n_pairs);
+  if (h.n_pairs) memcpy(c->pairs.data(), p, h.n_pairs * 8ull);
+  // codec section
+  p = base + off;
+  e = p + len;
+  uint32_t hd[8];
+  if (len < sizeof hd) return err = "truncated codec section", false;
+  memcpy(hd, p, sizeof hd);
+  p += sizeof hd;
+  if (hd[0] != CODEC_MAGIC || hd[1] != CODEC_VERSION) return err = "bad codec section magic/version", false;
+  const uint32_t n_str = hd[2], n_urn = hd[3], n_rx = hd[4], n_spec = hd[5], n_idx = hd[6], n_sb = hd[7];
+  if (n_urn != U_COUNT || n_spec != nn) return err = "codec section does not match the tables", false;
+  std::vector<uint32_t> urns, spec_ptr, spec_idx;
+  std::vector<uint8_t> kind;
+  if (!take(p, e, urns, n_urn) || !take(p, e, c->rx_row_id, n_rx) || !take(p, e, kind, n_spec) ||
+      !take(p, e, spec_ptr, n_spec + 1) || !take(p, e, spec_idx, n_idx) || !take(p, e, c->soff, n_str + 1))
+    return err = "truncated codec section", false;
+  if ((size_t)(e - p) < n_sb || c->soff.back() != n_sb) return err = "bad codec string table", false;
+  c->sbytes.assign((const char*)p, n_sb);
+  c->n_dict = n_str;
+  c->dict.reserve(n_str * 2);
+  for (uint32_t i = ID_EMPTY; i < n_str; ++i) c->dict.emplace(c->string_of(i), i);
+  for (int k = 0; k < U_COUNT; ++k) {
+    c->urn[k] = urns[k];
+    c->urn_s[k] = c->string_of(urns[k]);
+  }
+  c->rx_pat.resize(n_rx);
+  for (uint32_t r = 0; r < n_rx; ++r) {
+    const uint32_t id = c->rx_row_id[r];
+    c->row_of_id.emplace(id, r);
+    prepare_pattern(c->rx_pat[r], id <= ID_NULL, c->string_of(id));
+  }
+  // candidate specs
+  c->always_bits.assign(c->W, 0);
+  std::vector<std::vector<uint32_t>> per_row(n_rx);
+  for (uint32_t g = 0; g < nn; ++g) {
+    if (kind[g] == 1) c->always_bits[c->node_word(g)] |= c->node_bit(g);
+    else if (kind[g] == 2)
+      for (uint32_t k = spec_ptr[g]; k < spec_ptr[g + 1]; ++k)
+        if (spec_idx[k] < n_rx) per_row[spec_idx[k]].push_back(g);
+  }
+  c->row_ptr.assign(n_rx + 1, 0);
+  for (uint32_t r = 0; r < n_rx; ++r) {
+    c->row_ptr[r + 1] = c->row_ptr[r] + (uint32_t)per_row[r].size();
+    c->row_nodes.insert(c->row_nodes.end(), per_row[r].begin(), per_row[r].end());
+  }
+  // role requirements (candidates.role_requirements) and action requirements
+  c->node_role.assign(nn, -1);
+  c->node_need_act.assign(nn, 0);
+  std::vector<uint32_t> req_role(nn, NONE32);
+  for (uint32_t g = 0; g < nn; ++g) {
+    const NodeRec& N = c->nodes[g];
+    const bool tgt = (N.nflags & NF_HAS_TARGET) != 0;
+    if (tgt && (N.tflags & TF_SUBJ_ROLE) && !(N.tflags & TF_SUBJ_EMPTY)) {
+      req_role[g] = N.role;
+      c->role_ids.push_back(N.role);
+    }
+    c->node_need_act[g] = tgt && N.act_n > 0;
+  }
+  std::sort(c->role_ids.begin(), c->role_ids.end());
+  c->role_ids.erase(std::unique(c->role_ids.begin(), c->role_ids.end()), c->role_ids.end());
+  c->norole_bits.assign(c->W, 0);
+  c->role_node_list.assign(c->role_ids.size(), {});
+  for (uint32_t g = 0; g < nn; ++g) {
+    if (req_role[g] == NONE32) {
+      c->norole_bits[c->node_word(g)] |= c->node_bit(g);
+    } else {
+      const int k = (int)(std::lower_bound(c->role_ids.begin(), c->role_ids.end(), req_role[g]) - c->role_ids.begin());
+      c->node_role[g] = k;
+      c->role_node_list[k].push_back(g);
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ encoded batch
+struct ThreadStrings {  // one encoder thread's batch-local strings (ids base + k)
+  uint32_t base = 0;
+  std::vector<std::string> strs;
+};
+
+struct acs_codec_batch {
+  const acs_codec* codec = nullptr;
+  uint32_t n = 0;
+  std::vector<ReqHdr> hdr;
+  std::vector<ReqRes> res;  // [QMAX][n]
+  std::vector<Pair> subj, act;
+  std::vector<uint32_t> roles, arena;
+  std::vector<uint8_t> rx;  // [rx_cols][rx_rows]
+  uint32_t rx_cols = 1, rx_rows = 1;
+  std::vector<uint32_t> cand;
+  uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0;
+  std::vector<uint32_t> role_key, role_bits;
+  uint32_t role_rows = 0;
+  std::vector<const char*> reason;  // per request: why it goes to the host (nullptr: it does not)
+  std::vector<ThreadStrings> strings;
+  double seconds[4] = {};  // parse+encode, regex matrix, candidate classes, total
+  uint64_t hr_hits = 0, hr_misses = 0;
+};
+
+namespace {
+
+uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xC2B2AE3D27D4EB4Full);
+  size_t k = 0;
+  for (; k + 8 <= n; k += 8) {
+    uint64_t w;
+    memcpy(&w, p + k, 8);
+    h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 31;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p + k, n - k);
+  h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 29;
+  return h;
+}
+
+constexpr size_t HR_CACHE_BYTES = size_t(512) << 20;
+
+struct Col {  // one distinct entity value of the batch (a regex-matrix column)
+  std::string key;  // 'm' undefined, 'n' null, 's' + value
+  uint32_t first;   // first use: request index * QMAX + attribute index
+};
+
+struct Shared {  // batch-wide state of the encoder threads
+  std::mutex mu;
+  std::unordered_map<std::string, uint32_t> col_index;
+  std::vector<Col> cols;
+};
+
+class Encoder {
+ public:
+  Encoder(acs_codec& c, acs_codec_batch& b, Shared& sh, uint32_t t) : C(c), B(b), SH(sh), parser_(ar_) {
+    strs_ = &B.strings[t];
+  }
+  void encode(uint32_t i, const char* p, const char* e);
+  std::vector<uint32_t> arena;  // this thread's context arena words
+  uint64_t hits = 0, misses = 0;
+
+ private:
+  uint32_t intern_sv(std::string_view s) {
+    const uint32_t id = C.lookup(s);
+    if (id != NONE32) return id;
+    auto it = local_.find(s);
+    if (it != local_.end()) return it->second;
+    if (strs_->strs.size() >= (1u << LOCAL_BITS)) unsup("too many batch-local strings");
+    strs_->strs.emplace_back(s);
+    const uint32_t v = strs_->base + (uint32_t)strs_->strs.size() - 1;
+    pool_.emplace_back(s);  // stable storage for the key view
+    local_.emplace(std::string_view(pool_.back()), v);
+    return v;
+  }
+  uint32_t intern(const JV* v) {
+    if (v->t == J_UNDEF) return ID_UNDEF;
+    if (v->t == J_NULL) return ID_NULL;
+    if (v->t != J_STR) unsup("non-string attribute scalar");
+    return intern_sv(v->str());
+  }
+  uint32_t intern(const Scalar& s) { return s.kind == 0 ? ID_UNDEF : s.kind == 1 ? ID_NULL : intern_sv(s.s); }
+  // strict equality with a URN (undefined URN: only an absent value equals it)
+  bool eq_urn(const JV* v, int u) const {
+    if (C.urn[u] == ID_UNDEF) return v->t == J_UNDEF;
+    return v->t == J_STR && v->str() == C.urn_s[u];
+  }
+  bool loose_urn(const JV* v, int u) const {  // (nullish(v) && nullish(urn)) || v === urn
+    return (nullish(v) && C.urn[u] == ID_UNDEF) || eq_urn(v, u);
+  }
+  static void check_scalar(const JV* v) {
+    if (!(v->t == J_UNDEF || v->t == J_NULL || v->t == J_STR)) unsup("non-string attribute scalar");
+  }
+  static const JV* attr_list(const JV* v, uint32_t& n) {  // _attr_list
+    n = 0;
+    if (!truthy(v)) return nullptr;
+    if (v->t != J_ARR) unsup("non-array list value");
+    for (uint32_t k = 0; k < v->n; ++k) {
+      const JV* a = &v->a[k];
+      if (a->t != J_OBJ) unsup("non-object attribute entry");
+      check_scalar(get(a, "id"));
+      check_scalar(get(a, "value"));
+    }
+    n = v->n;
+    return v->a;
+  }
+  static const JV* dict_list(const JV* v, uint32_t& n) {  // _dict_list
+    n = 0;
+    if (nullish(v)) return nullptr;
+    if (v->t != J_ARR) unsup("list value is not an array");
+    for (uint32_t k = 0; k < v->n; ++k)
+      if (v->a[k].t != J_OBJ) unsup("non-object list entry");
+    n = v->n;
+    return v->a;
+  }
+  // lodash _.find(coll, [path, value]) for a string / null / undefined value
+  static const JV* find_by(const JV* coll, uint32_t nc, bool instance_id, const JV* value) {
+    for (uint32_t k = 0; k < nc; ++k) {
+      const JV* o = &coll[k];
+      const JV* ov = instance_id ? get(get(o, "instance"), "id") : get(o, "id");
+      if (ov->t == J_UNDEF) continue;  // an absent path never equals (JSON has no undefined members)
+      if (ov->t == J_OBJ || ov->t == J_ARR) continue;
+      if (value->t == J_NULL ? ov->t == J_NULL : (value->t == J_STR && ov->t == J_STR && ov->str() == value->str()))
+        return o;
+    }
+    return &kUndef;
+  }
+  uint32_t column(const JV* v, uint32_t i) {  // i: request index * QMAX + attribute index
+    std::string key = v->t == J_UNDEF ? std::string("m") : v->t == J_NULL ? std::string("n") : "s" + std::string(v->str());
+    auto it = cols_.find(key);
+    if (it != cols_.end()) {
+      return it->second;
+    }
+    std::lock_guard<std::mutex> lock(SH.mu);
+    auto g = SH.col_index.find(key);
+    uint32_t c;
+    if (g == SH.col_index.end()) {
+      if (SH.cols.size() >= 0xFFFE) unsup("too many distinct entity values in batch");
+      c = (uint32_t)SH.cols.size();
+      SH.col_index.emplace(key, c);
+      SH.cols.push_back({key, i});
+    } else {
+      c = g->second;
+      if (i < SH.cols[c].first) SH.cols[c].first = i;
+    }
+    cols_.emplace(std::move(key), c);
+    return c;
+  }
+  std::shared_ptr<const HrForest> inline_forest(const JV* raw);
+  std::shared_ptr<const HrForest> subject_forest(const JV* key);
+  void encode_one(uint32_t i, const JV* req);
+
+  acs_codec& C;
+  acs_codec_batch& B;
+  Shared& SH;
+  ThreadStrings* strs_;
+  Arena ar_, ar2_;
+  Parser parser_;
+  std::unordered_map<std::string_view, uint32_t> local_;
+  std::deque<std::string> pool_;
+  std::unordered_map<std::string, uint32_t> cols_;
+};
+
+std::shared_ptr<const HrForest> Encoder::inline_forest(const JV* raw) {
+  const uint64_t h = hash_bytes(raw->s, raw->n);
+  {
+    std::shared_lock<std::shared_mutex> lock(C.hr_mu);
+    auto it = C.hr_inline.find(h);
+    if (it != C.hr_inline.end())
+      for (const auto& f : it->second)
+        if (f->text.size() == raw->n && memcmp(f->text.data(), raw->s, raw->n) == 0) {
+          ++hits;
+          return f;
+        }
+  }
+  ++misses;
+  auto F = std::make_shared<HrForest>();
+  F->text.assign(raw->s, raw->n);
+  ar2_.reset();
+  Parser p2(ar2_);
+  const JV* v = p2.parse(raw->s, raw->s + raw->n);
+  build_forest(*F, v);
+  std::unique_lock<std::shared_mutex> lock(C.hr_mu);
+  if (C.hr_bytes + F->bytes() > HR_CACHE_BYTES) {
+    C.hr_inline.clear();
+    C.hr_bytes = 0;
+  }
+  C.hr_bytes += F->bytes();
+  C.hr_inline[h].push_back(F);
+  return F;
+}
+
+std::shared_ptr<const HrForest> Encoder::subject_forest(const JV* key) {
+  if (key->t != J_STR) unsup("$hrs subject key is not a string");
+  std::shared_lock<std::shared_mutex> lock(C.hr_mu);
+  auto it = C.hr_subject.find(std::string(key->str()));
+  if (it == C.hr_subject.end()) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+  ++hits;
+  return it->second;
+}
+
+void Encoder::encode(uint32_t i, const char* p, const char* e) {
+  ar_.reset();
+  const JV* req = parser_.parse(p, e, "hierarchical_scopes");
+  try {
+    encode_one(i, req);
+  } catch (const Unsup& u) {
+    ReqHdr& h = B.hdr[i];
+    h = ReqHdr{};
+    h.flags = RQ_HOST;
+    h.arena_off = (uint32_t)arena.size();
+    arena.push_back(0);
+    arena.push_back(0);
+    for (int j = 0; j < QMAX; ++j) B.res[(size_t)j * B.n + i] = ReqRes{};
+    for (int j = 0; j < SMAX; ++j) B.subj[(size_t)j * B.n + i] = Pair{};
+    for (int j = 0; j < AMAX; ++j) B.act[(size_t)j * B.n + i] = Pair{};
+    for (int j = 0; j < RMAX; ++j) B.roles[(size_t)j * B.n + i] = 0;
+    B.reason[i] = u.why;
+  }
+}
+
+// encoder.py Encoder._encode_one, restated.
+void Encoder::encode_one(uint32_t i, const JV* req) {
+  const uint32_t n = B.n;
+  uint32_t flags = 0;
+  if (req->t != J_OBJ) unsup("request is not an object");
+  const JV* target = get(req, "target");
+  const JV *subjects = nullptr, *resources = nullptr, *actions = nullptr;
+  uint32_t ns = 0, nr = 0, na = 0;
+  if (!truthy(target)) {
+    flags |= RQ_NO_TARGET;
+  } else {
+    if (target->t != J_OBJ) unsup("target is not an object");
+    subjects = attr_list(get(target, "subjects"), ns);
+    resources = attr_list(get(target, "resources"), nr);
+    actions = attr_list(get(target, "actions"), na);
+  }
+  if (ns > (uint32_t)SMAX || nr > (uint32_t)QMAX || na > (uint32_t)AMAX) unsup("request list exceeds packed capacity");
+
+  const JV* ctx = get(req, "context");
+  const bool ctx_empty = is_empty(ctx);
+  if (!nullish(ctx) && ctx->t != J_OBJ) unsup("context is not an object");
+  if (ctx_empty) flags |= RQ_CTX_EMPTY;
+  const JV* subj = get(ctx, "subject");
+  if (!nullish(subj) && subj->t != J_OBJ) unsup("context.subject is not an object");
+  if (truthy(get(subj, "token"))) unsup("subject token: identity-srv / HR-scope I/O (accessController.ts:110-123)");
+  if (ctx_empty || nullish(subj)) flags |= RQ_SUBJ_MISSING;
+  const JV* ras_v = get(subj, "role_associations");
+  if (truthy(ras_v)) flags |= RQ_RA_TRUTHY;
+  if (is_empty(ras_v)) flags |= RQ_RA_EMPTY;
+  uint32_t n_ras = 0;
+  const JV* ras = truthy(ras_v) ? dict_list(ras_v, n_ras) : nullptr;
+  if (n_ras > (uint32_t)RMAX) unsup("too many role associations");
+  const JV* hrs = get(subj, "hierarchical_scopes");
+  std::shared_ptr<const HrForest> forest;
+  if (hrs->t == J_RAW) {
+    if (hrs->raw == J_ARR) forest = inline_forest(hrs);
+    else if (hrs->raw != J_NULL) unsup("hierarchical_scopes is not an array");
+  } else if (hrs->t == J_UNDEF) {
+    const JV* key = get(subj, "$hrs");  // the subject's registered forest (createHRScope's cache)
+    if (key->t != J_UNDEF) forest = subject_forest(key);
+  } else if (hrs->t == J_ARR || hrs->t == J_OBJ) {
+    unsup("hierarchical_scopes outside the codec's forest cache");  // (only reached without raw_key)
+  } else if (!nullish(hrs)) {
+    unsup("hierarchical_scopes is not an array");
+  }
+  if (forest) {
+    if (forest->why) unsup(forest->why);
+    if (forest->is_array) flags |= RQ_HRS_ITERABLE;
+  }
+
+  // ---- resources: kinds, ids, regex columns, suffixes, indexOf masks
+  uint8_t kinds[QMAX] = {};
+  int n_ent = 0;
+  for (uint32_t j = 0; j < nr; ++j) {
+    const JV* id = get(&resources[j], "id");
+    const JV* v = get(&resources[j], "value");
+    uint8_t kind = 0;
+    if (eq_urn(id, U_ENT)) {
+      kind |= K_ENT;
+      ++n_ent;
+    }
+    if (loose_urn(id, U_ENT)) kind |= K_ENT_LOOSE;
+    if (eq_urn(id, U_OP)) kind |= K_OP;
+    if (eq_urn(id, U_PROP)) {
+      kind |= K_PROP;
+      flags |= RQ_ANY_PROP;
+    }
+    if (loose_urn(id, U_RID)) kind |= K_RID_LOOSE;
+    if (v->t == J_STR && v->str().find('#') != std::string_view::npos) kind |= K_HAS_HASH;
+    kinds[j] = kind;
+  }
+  if (n_ent > 1) flags |= RQ_MULTI_ENT;
+  {
+    int first = -1, cnt = 0;
+    for (uint32_t j = 0; j < nr; ++j)
+      if (kinds[j] & K_ENT) {
+        if (first < 0) first = (int)j;
+        ++cnt;
+      }
+    const uint32_t ent_field = first < 0 ? 0u : (cnt == 1 && first < 6 ? (uint32_t)first + 1 : 7u);
+    flags |= ent_field << RQ_ENT_SHIFT;
+  }
+  const JV* ctx_res = nullptr;
+  uint32_t n_ctx = 0;
+  if (!ctx_empty) {
+    const JV* cr = get(ctx, "resources");
+    if (truthy(cr)) {
+      if (cr->t != J_ARR) unsup("context.resources is not an array");
+      ctx_res = cr->a;
+      n_ctx = cr->n;
+    }
+  }
+  std::vector<const JV*> slot_objs;
+  auto slot_of = [&](const JV* obj) -> uint8_t {
+    if (!truthy(obj)) return NONE8;
+    for (size_t k = 0; k < slot_objs.size(); ++k)
+      if (slot_objs[k] == obj) return (uint8_t)k;
+    if (slot_objs.size() >= (size_t)MAX_SLOTS) unsup("too many context resources");
+    slot_objs.push_back(obj);
+    return (uint8_t)(slot_objs.size() - 1);
+  };
+  auto resolve_a = [&](const JV* v) -> const JV* {  // hierarchicalScope.ts:106-112 / verifyACL.ts:40-48
+    const JV* o = find_by(ctx_res, n_ctx, true, v);
+    if (truthy(o)) return get(o, "instance");
+    return find_by(ctx_res, n_ctx, false, v);
+  };
+  ReqRes rows[QMAX] = {};
+  std::vector<std::pair<uint32_t, uint8_t>> keys_a, keys_b;  // first slot per interned value
+  for (uint32_t j = 0; j < nr; ++j) {
+    const JV* v = get(&resources[j], "value");
+    const uint8_t kind = kinds[j];
+    uint8_t sa = NONE8, sb = NONE8;
+    if (kind & (K_RID_LOOSE | K_OP)) sa = slot_of(resolve_a(v));
+    if (kind & K_OP) sb = slot_of(find_by(ctx_res, n_ctx, false, v));
+    const uint32_t vid = intern(v);
+    auto setdefault = [](std::vector<std::pair<uint32_t, uint8_t>>& m, uint32_t k, uint8_t s) {
+      for (auto& x : m)
+        if (x.first == k) return;
+      m.push_back({k, s});
+    };
+    if (kind & K_RID_LOOSE) setdefault(keys_a, vid, sa);
+    if (kind & K_OP) setdefault(keys_b, vid, sb);
+    uint32_t hs = ID_UNDEF;
+    uint16_t contains = 0;
+    if ((kind & K_PROP) && v->t == J_STR) {
+      const std::string_view vs = v->str();
+      const size_t h = vs.rfind('#');
+      hs = intern_sv(h == std::string_view::npos ? vs : vs.substr(h + 1));
+      for (uint32_t i2 = 0; i2 < nr; ++i2) {
+        if (!(kinds[i2] & K_ENT)) continue;
+        const JV* v2 = get(&resources[i2], "value");
+        std::string_view name = "undefined";
+        if (v2->t == J_STR) {
+          const std::string_view s2 = v2->str();
+          const size_t c = s2.rfind(':');
+          name = c == std::string_view::npos ? s2 : s2.substr(c + 1);
+        }
+        if (vs.find(name) != std::string_view::npos) contains |= (uint16_t)(1u << i2);
+      }
+    }
+    uint16_t col = 0;
+    if (kind & K_ENT_LOOSE) col = (uint16_t)column(v, i * QMAX + j);
+    ReqRes& q = rows[j];
+    q.value = vid;
+    q.hash_sfx = hs;
+    q.col = col;
+    q.contains = contains;
+    q.kind = kind;
+    q.slot_a = sa;
+    q.slot_b = sb;
+  }
+  for (auto& b : keys_b)  // HR map key shared by a resource id and an operation name
+    for (auto& a : keys_a)
+      if (a.first == b.first && a.second != b.second) unsup("resource-id / operation key collision in HR owners map");
+
+  // ---- role associations -> roles, (role, se) pairs, (role, se, inst) grants
+  uint32_t roles[RMAX] = {};
+  std::vector<uint32_t> rolese, grants;
+  for (uint32_t k = 0; k < n_ras; ++k) {
+    const JV* ra = &ras[k];
+    const JV* role = get(ra, "role");
+    check_scalar(role);
+    const uint32_t rid = intern(role);
+    roles[k] = rid;
+    const JV* attrs = get(ra, "attributes");
+    uint32_t n_at = 0;
+    const JV* at = truthy(attrs) ? dict_list(attrs, n_at) : nullptr;
+    for (uint32_t x = 0; x < n_at; ++x) {
+      const JV* rae = &at[x];
+      if (!eq_urn(get(rae, "id"), U_RSE)) continue;
+      const JV* sev = get(rae, "value");
+      check_scalar(sev);
+      const uint32_t se = intern(sev);
+      rolese.push_back(rid);
+      rolese.push_back(se);
+      const JV* insts = get(rae, "attributes");
+      uint32_t n_in = 0;
+      const JV* in = truthy(insts) ? dict_list(insts, n_in) : nullptr;
+      for (uint32_t y = 0; y < n_in; ++y)
+        if (eq_urn(get(&in[y], "id"), U_RSI)) {
+          const JV* iv = get(&in[y], "value");
+          check_scalar(iv);
+          grants.push_back(rid);
+          grants.push_back(se);
+          grants.push_back(intern(iv));
+        }
+    }
+  }
+  if (grants.size() / 3 > 255 || rolese.size() / 2 > 255) unsup("too many role scoping grants");
+
+  // ---- hierarchical_scopes: roots and effective-role keys from the cached forest
+  std::vector<uint32_t> roots, hr_keys;
+  if (forest && forest->is_array) {
+    for (const Scalar& r : forest->roots) roots.push_back(intern(r));
+    for (const Scalar& k : forest->keys) hr_keys.push_back(intern(k));
+  }
+  auto masks_of = [&](const JV* v) -> uint64_t {
+    if (!forest || v->t != J_STR) return 0;
+    auto it = forest->masks.find(std::string(v->str()));
+    return it == forest->masks.end() ? 0 : it->second;
+  };
+
+  // ---- verifyACL request loop (verifyACL.ts:37-88)
+  uint32_t acl_state = ACL_CONTINUE;
+  std::vector<std::pair<uint32_t, std::vector<const JV*>>> tse;
+  for (uint32_t j = 0; j < nr && acl_state == ACL_CONTINUE; ++j) {
+    const JV* aid = get(&resources[j], "id");
+    if (!(loose_urn(aid, U_RID) || eq_urn(aid, U_OP))) continue;
+    const JV* obj = resolve_a(get(&resources[j], "value"));
+    const JV* acls = &kUndef;
+    if (truthy(obj)) {
+      const JV* al = get(get(obj, "meta"), "acls");
+      if (al->t == J_ARR && al->n > 0) acls = al;
+      else if (truthy(al) && al->t != J_ARR) unsup("meta.acls is not an array");
+    }
+    if (is_empty(acls)) {
+      acl_state = ACL_RET_TRUE;
+      break;
+    }
+    uint32_t n_acl = 0;
+    const JV* al = dict_list(acls, n_acl);
+    for (uint32_t x = 0; x < n_acl && acl_state == ACL_CONTINUE; ++x) {
+      const JV* acl = &al[x];
+      if (!eq_urn(get(acl, "id"), U_ACLIE)) {
+        acl_state = ACL_RET_FALSE;
+        break;
+      }
+      const JV* sev = get(acl, "value");
+      check_scalar(sev);
+      const uint32_t se = intern(sev);
+      size_t e = 0;
+      while (e < tse.size() && tse[e].first != se) ++e;
+      if (e == tse.size()) tse.push_back({se, {}});
+      const JV* attrs = get(acl, "attributes");
+      if (!truthy(attrs) || (attrs->t == J_ARR && attrs->n == 0)) {
+        acl_state = ACL_RET_FALSE;
+        break;
+      }
+      uint32_t n_at = 0;
+      const JV* at = dict_list(attrs, n_at);
+      for (uint32_t y = 0; y < n_at; ++y) {
+        if (eq_urn(get(&at[y], "id"), U_ACLI)) {
+          const JV* iv = get(&at[y], "value");
+          check_scalar(iv);
+          tse[e].second.push_back(iv);
+        } else {
+          acl_state = ACL_RET_FALSE;
+          break;
+        }
+      }
+    }
+  }
+  flags |= acl_state << RQ_ACL_SHIFT;
+  if (na > 0) {
+    const JV* a0 = &actions[0];
+    if (eq_urn(get(a0, "id"), U_ACTID)) {
+      const JV* v0 = get(a0, "value");
+      if (eq_urn(v0, U_CREATE)) flags |= RQ_ACT_CREATE;
+      else if (eq_urn(v0, U_READ) || eq_urn(v0, U_MODIFY) || eq_urn(v0, U_DELETE)) flags |= RQ_ACT_RMD;
+    }
+  }
+
+  // ---- arena
+  std::vector<uint32_t> w = {0, 0};
+  w.insert(w.end(), grants.begin(), grants.end());
+  w.insert(w.end(), rolese.begin(), rolese.end());
+  w.insert(w.end(), roots.begin(), roots.end());
+  w.insert(w.end(), hr_keys.begin(), hr_keys.end());
+  const size_t slot_base = w.size();
+  w.resize(w.size() + slot_objs.size(), 0);
+  const size_t tse_base = w.size();
+  w.resize(w.size() + 3 * tse.size(), 0);
+  for (size_t s = 0; s < slot_objs.size(); ++s) {
+    w[slot_base + s] = (uint32_t)w.size();
+    const JV* obj = slot_objs[s];
+    const JV* meta = obj->t == J_OBJ ? get(obj, "meta") : &kUndef;
+    const JV* owners = get(meta, "owners");
+    const bool empty = is_empty(meta) || is_empty(owners);
+    uint32_t n_o = 0;
+    const JV* ol = empty ? nullptr : dict_list(owners, n_o);
+    w.push_back(empty ? 1u : 0u);
+    w.push_back(n_o);
+    for (uint32_t k = 0; k < n_o; ++k) {
+      const JV* o = &ol[k];
+      const JV* attrs = get(o, "attributes");
+      uint32_t n_at = 0;
+      const JV* at = nullish(attrs) ? nullptr : dict_list(attrs, n_at);
+      const uint32_t is_oe = eq_urn(get(o, "id"), U_OE) ? 1u : 0u;
+      const JV* ov = get(o, "value");
+      check_scalar(ov);
+      w.push_back(is_oe | (n_at << 8));
+      w.push_back(intern(ov));
+      for (uint32_t x = 0; x < n_at; ++x) {
+        const JV* av = get(&at[x], "value");
+        check_scalar(av);
+        w.push_back(intern(av));
+        w.push_back(eq_urn(get(&at[x], "id"), U_OI) ? (uint32_t)K_OI : 0u);
+        w.push_back((uint32_t)masks_of(av));
+      }
+    }
+  }
+  for (size_t e = 0; e < tse.size(); ++e) {
+    const auto& insts = tse[e].second;
+    if (insts.size() > 32) unsup("too many ACL instances for one scoping entity");
+    w[tse_base + 3 * e] = tse[e].first;
+    w[tse_base + 3 * e + 1] = (uint32_t)insts.size();
+    w[tse_base + 3 * e + 2] = (uint32_t)w.size();
+    for (const JV* v : insts) {
+      w.push_back(intern(v));
+      w.push_back((uint32_t)(masks_of(v) >> 32));
+    }
+  }
+  if (tse.size() > 255) unsup("too many ACL scoping entities");
+  w[0] = (uint32_t)(grants.size() / 3) | (uint32_t)(rolese.size() / 2) << 8 | (uint32_t)slot_objs.size() << 16 |
+         (uint32_t)roots.size() << 24;
+  w[1] = (uint32_t)tse.size() | (uint32_t)hr_keys.size() << 8;
+
+  const JV* sid = get(subj, "id");
+  check_scalar(sid);
+  ReqHdr h{};
+  h.flags = flags;
+  h.nres = (uint8_t)nr;
+  h.nsubj = (uint8_t)ns;
+  h.nact = (uint8_t)na;
+  h.nroles = (uint8_t)n_ras;
+  h.subject_id = intern(sid);
+  Pair sp[SMAX] = {}, ap[AMAX] = {};
+  for (uint32_t k = 0; k < ns; ++k) sp[k] = Pair{intern(get(&subjects[k], "id")), intern(get(&subjects[k], "value"))};
+  for (uint32_t k = 0; k < na; ++k) ap[k] = Pair{intern(get(&actions[k], "id")), intern(get(&actions[k], "value"))};
+  // commit (nothing above wrote the batch: an Unsupported leaves no partial request)
+  h.arena_off = (uint32_t)arena.size();
+  arena.insert(arena.end(), w.begin(), w.end());
+  B.hdr[i] = h;
+  for (int j = 0; j < QMAX; ++j) B.res[(size_t)j * n + i] = rows[j];
+  for (int j = 0; j < SMAX; ++j) B.subj[(size_t)j * n + i] = sp[j];
+  for (int j = 0; j < AMAX; ++j) B.act[(size_t)j * n + i] = ap[j];
+  for (int j = 0; j < RMAX; ++j) B.roles[(size_t)j * n + i] = roles[j];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ candidate classes
+namespace {
+
+using Row = std::vector<uint32_t>;
+
+struct Classes {
+  acs_codec& C;
+  acs_codec_batch& B;
+  int threads;
+  Row valid;  // real node bits of the W-word layout
+  std::vector<std::string> col_keys;  // per regex-matrix column: its value key ('' = padding)
+  Classes(acs_codec& c, acs_codec_batch& b, int t) : C(c), B(b), threads(t) {
+    valid.assign(C.W, 0);
+    auto fill = [&](uint32_t off, uint32_t n) {
+      for (uint32_t k = 0; k < n; ++k) valid[off + (k >> 5)] |= 1u << (k & 31);
+    };
+    fill(0, C.S);
+    fill(C.ws, C.P);
+    fill(C.ws + C.wp, C.R);
+  }
+  void set_node(Row& r, uint32_t g) const { r[C.node_word(g)] |= C.node_bit(g); }
+
+  // entity_candidates: nodes whose target can hit the column's value (or always candidates)
+  std::shared_ptr<const Row> entity_row(const std::string& key, const std::vector<uint8_t>& cells) {
+    {
+      std::lock_guard<std::mutex> lock(C.col_mu);
+      auto it = C.ent_rows.find(key);
+      if (it != C.ent_rows.end()) return it->second;
+    }
+    auto row = std::make_shared<Row>(C.always_bits);
+    uint32_t exact = NONE32;
+    if (key[0] == 'm') exact = ID_UNDEF;
+    else if (key[0] == 'n') exact = ID_NULL;
+    else exact = C.lookup(std::string_view(key).substr(1));
+    uint32_t exact_row = NONE32;
+    if (exact != NONE32) {
+      auto r = C.row_of_id.find(exact);
+      if (r != C.row_of_id.end()) exact_row = r->second;
+    }
+    for (uint32_t r = 0; r < (uint32_t)C.rx_pat.size(); ++r) {
+      if (!((cells[r] & HIT_LIKE) || r == exact_row)) continue;
+      for (uint32_t k = C.row_ptr[r]; k < C.row_ptr[r + 1]; ++k) set_node(*row, C.row_nodes[k]);
+    }
+    std::lock_guard<std::mutex> lock(C.col_mu);
+    if (C.ent_rows.size() > 65536) C.ent_rows.clear();
+    C.ent_rows.emplace(key, row);
+    return row;
+  }
+
+  // action_candidates row 2 + k: nodes whose target actions all loosely equal the pair
+  std::shared_ptr<const Row> action_row(uint32_t id, uint32_t value) {
+    const uint64_t key = (uint64_t)id << 32 | value;
+    const bool cacheable = id < C.n_dict && value < C.n_dict;
+    if (cacheable) {
+      std::lock_guard<std::mutex> lock(C.col_mu);
+      auto it = C.act_rows.find(key);
+      if (it != C.act_rows.end()) return it->second;
+    }
+    auto row = std::make_shared<Row>(C.W, 0u);
+    auto leq = [](uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); };
+    const uint32_t nn = C.S + C.P + C.R;
+    for (uint32_t g = 0; g < nn; ++g) {
+      bool ok = true;
+      if (C.node_need_act[g]) {
+        const NodeRec& N = C.nodes[g];
+        for (uint32_t k = 0; k < N.act_n && ok; ++k) {
+          const Pair& pr = C.pairs[N.act_off + k];
+          ok = leq(pr.id, id) && leq(pr.value, value);
+        }
+      }
+      if (ok) set_node(*row, g);
+    }
+    if (cacheable) {
+      std::lock_guard<std::mutex> lock(C.col_mu);
+      if (C.act_rows.size() > 4096) C.act_rows.clear();
+      C.act_rows.emplace(key, row);
+    }
+    return row;
+  }
+
+  Row no_action_row() const {  // row 0: a request without action attributes
+    Row r(C.W, 0u);
+    const uint32_t nn = C.S + C.P + C.R;
+    for (uint32_t g = 0; g < nn; ++g)
+      if (!C.node_need_act[g]) r[C.node_word(g)] |= C.node_bit(g);
+    return r;
+  }
+
+  Row role_filter_fn(const int32_t* rows, int nrows) const {
+    Row r(C.norole_bits);
+    for (int k = 0; k < nrows; ++k)
+      for (uint32_t g : C.role_node_list[rows[k]]) r[C.node_word(g)] |= C.node_bit(g);
+    return r;
+  }
+
+  // set section: keep a set only if one of its policies is kept and it has policies
+  void sets_need_policies(Row& r) const {
+    for (uint32_t s = 0; s < C.S; ++s) {
+      const NodeRec& N = C.nodes[s];
+      bool any = false;
+      for (uint32_t p = N.child_begin; p < N.child_end && !any; ++p) any = (r[C.ws + (p >> 5)] >> (p & 31)) & 1u;
+      if (!any) r[s >> 5] &= ~(1u << (s & 31));
+    }
+  }
+
+  Row class_row(uint32_t pc, uint32_t a, const int32_t* roles, int nroles, bool role_filter,
+                const std::vector<std::shared_ptr<const Row>>& ent,
+                const std::vector<std::shared_ptr<const Row>>& arow) const {
+    Row r(*ent[pc]);
+    const Row& A = *arow[a];
+    for (uint32_t w = 0; w < C.W; ++w) r[w] &= A[w] & valid[w];
+    if (role_filter) {
+      const Row f = role_filter_fn(roles, nroles);
+      for (uint32_t w = 0; w < C.W; ++w) r[w] &= f[w];
+    }
+    sets_need_policies(r);
+    return r;
+  }
+
+  void run();
+};
+
+uint64_t row_hash(const uint32_t* r, size_t n) { return hash_bytes((const char*)r, n * 4); }
+
+void Classes::run() {
+  const uint32_t n = B.n, W = C.W;
+  const uint32_t ncols = B.rx_cols;
+  B.cand_words = W;
+  B.cand_wp = C.ws;
+  B.cand_wr = C.ws + C.wp;
+  // primary column per request (candidates.primary_columns)
+  std::vector<uint32_t> pcol(n, ncols);
+  std::vector<uint8_t> active(n, 0);
+  bool any_active = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    bool seen = false;
+    for (uint32_t j = 0; j < B.hdr[i].nres; ++j) {
+      const ReqRes& q = B.res[(size_t)j * n + i];
+      if (!(q.kind & K_ENT)) continue;
+      if (!seen) pcol[i] = q.col;
+      else if (pcol[i] != q.col) pcol[i] = PCOL_ALL;
+      seen = true;
+    }
+    active[i] = pcol[i] != PCOL_ALL && !(B.hdr[i].flags & (RQ_HOST | RQ_NO_TARGET));
+    any_active = any_active || active[i];
+  }
+  std::vector<uint32_t> cls(n, PCOL_ALL);
+  auto finish = [&]() {
+    for (uint32_t i = 0; i < n; ++i) B.hdr[i].flags = (B.hdr[i].flags & 0xFFFFu) | cls[i] << RQ_PCOL_SHIFT;
+  };
+  if (!any_active) {
+    B.cand.assign(W ? W : 1, 0u);
+    B.cand_rows = 1;
+    finish();
+    return;
+  }
+  // entity rows per column (+ the no-entity column: always candidates)
+  std::vector<std::shared_ptr<const Row>> ent(ncols + 1);
+  {
+    const std::vector<std::string>& keys = col_keys;
+    for (uint32_t c = 0; c < ncols; ++c) {
+      if (keys[c].empty()) {
+        ent[c] = std::make_shared<Row>(C.always_bits);
+        continue;
+      }
+      std::vector<uint8_t> cells(B.rx.begin() + (size_t)c * B.rx_rows,
+                                 B.rx.begin() + (size_t)c * B.rx_rows + C.rx_pat.size());
+      ent[c] = entity_row(keys[c], cells);
+    }
+    ent[ncols] = std::make_shared<Row>(C.always_bits);
+  }
+  // action keys (candidates.action_keys): 0 none, 1 several / unfiltered, 2 + k a single pair
+  std::vector<uint32_t> ak(n, 0);
+  std::vector<uint64_t> pairs_k;
+  {
+    std::unordered_map<uint64_t, uint32_t> cnt;
+    for (uint32_t i = 0; i < n; ++i)
+      if (B.hdr[i].nact == 1) ++cnt[(uint64_t)B.act[i].id << 32 | B.act[i].value];
+    std::vector<std::pair<uint64_t, uint32_t>> v(cnt.begin(), cnt.end());
+    std::sort(v.begin(), v.end());
+    if (v.size() > 62) {
+      std::stable_sort(v.begin(), v.end(), [](auto& a, auto& b) { return a.second > b.second; });
+      v.resize(62);
+      std::sort(v.begin(), v.end());
+    }
+    std::unordered_map<uint64_t, uint32_t> idx;
+    for (uint32_t k = 0; k < v.size(); ++k) {
+      idx[v[k].first] = k;
+      pairs_k.push_back(v[k].first);
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t na = B.hdr[i].nact;
+      if (na == 0) ak[i] = 0;
+      else if (na > 1) ak[i] = 1;
+      else {
+        auto it = idx.find((uint64_t)B.act[i].id << 32 | B.act[i].value);
+        ak[i] = it == idx.end() ? 1 : 2 + it->second;
+      }
+    }
+  }
+  std::vector<std::shared_ptr<const Row>> arow(2 + pairs_k.size());
+  arow[0] = std::make_shared<Row>(no_action_row());
+  arow[1] = std::make_shared<Row>(valid);
+  for (size_t k = 0; k < pairs_k.size(); ++k)
+    arow[2 + k] = action_row((uint32_t)(pairs_k[k] >> 32), (uint32_t)pairs_k[k]);
+  // role sets: sorted distinct role rows some target requires
+  const int RW = RMAX;
+  std::vector<int32_t> rs((size_t)n * RW, -1);
+  std::vector<uint8_t> nrs(n, 0);
+  const bool have_roles = !C.role_ids.empty();
+  for (uint32_t i = 0; i < n && have_roles; ++i) {
+    if (!(B.hdr[i].flags & RQ_RA_TRUTHY)) continue;
+    int32_t* r = &rs[(size_t)i * RW];
+    int m = 0;
+    for (uint32_t k = 0; k < B.hdr[i].nroles; ++k) {
+      const uint32_t v = B.roles[(size_t)k * n + i];
+      auto it = std::lower_bound(C.role_ids.begin(), C.role_ids.end(), v);
+      if (it != C.role_ids.end() && *it == v) r[m++] = (int32_t)(it - C.role_ids.begin());
+    }
+    std::sort(r, r + m);
+    m = (int)(std::unique(r, r + m) - r);
+    nrs[i] = (uint8_t)m;
+  }
+  const size_t KEY_ROW_BYTES = size_t(512) << 20, ROLE_ROW_BYTES = size_t(256) << 20;
+  const uint32_t MAX_CLASSES = PCOL_ALL;
+  for (int level = 0; level < 3; ++level) {
+    const bool role_filter = level == 0 && have_roles;
+    const bool action_filter = level < 2;
+    // distinct keys of the active requests
+    std::unordered_map<std::string, uint32_t> kidx;
+    std::vector<uint32_t> key_of(n, NONE32), key_first;
+    std::string kb;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!active[i]) continue;
+      kb.assign((const char*)&pcol[i], 4);
+      if (action_filter) kb.append((const char*)&ak[i], 4);
+      if (role_filter) kb.append((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      auto it = kidx.find(kb);
+      if (it == kidx.end()) {
+        it = kidx.emplace(kb, (uint32_t)key_first.size()).first;
+        key_first.push_back(i);
+      }
+      key_of[i] = it->second;
+    }
+    const size_t nk = key_first.size();
+    if (level < 2 && nk * W * 4 > KEY_ROW_BYTES) continue;
+    std::vector<Row> rows(nk);
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+      for (;;) {
+        const size_t k = next.fetch_add(1);
+        if (k >= nk) return;
+        const uint32_t i = key_first[k];
+        rows[k] = class_row(pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter, ent, arow);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads && (size_t)t < nk; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    // identical rows share a class; heaviest (most candidate nodes) first
+    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    std::vector<uint32_t> urow_of_key(nk), urows;
+    for (size_t k = 0; k < nk; ++k) {
+      const uint64_t h = row_hash(rows[k].data(), W);
+      auto& bucket = by_hash[h];
+      uint32_t u = NONE32;
+      for (uint32_t x : bucket)
+        if (rows[urows[x]] == rows[k]) {
+          u = x;
+          break;
+        }
+      if (u == NONE32) {
+        u = (uint32_t)urows.size();
+        urows.push_back((uint32_t)k);
+        bucket.push_back(u);
+      }
+      urow_of_key[k] = u;
+    }
+    if (urows.size() > MAX_CLASSES && level < 2) continue;
+    if (urows.size() > MAX_CLASSES) {
+      acs_internal_set_error("acs_codec_encode: too many request classes");
+      throw Unsup{"too many request classes"};
+    }
+    std::vector<uint32_t> cost(urows.size()), order(urows.size()), rank(urows.size());
+    for (size_t u = 0; u < urows.size(); ++u) {
+      uint32_t c = 0;
+      for (uint32_t w = 0; w < W; ++w) c += (uint32_t)__builtin_popcount(rows[urows[u]][w]);
+      cost[u] = c;
+      order[u] = (uint32_t)u;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    for (size_t k = 0; k < order.size(); ++k) rank[order[k]] = (uint32_t)k;
+    B.cand.assign((size_t)urows.size() * W, 0u);
+    for (size_t u = 0; u < urows.size(); ++u)
+      std::copy(rows[urows[u]].begin(), rows[urows[u]].end(), B.cand.begin() + (size_t)rank[u] * W);
+    B.cand_rows = (uint32_t)urows.size();
+    for (uint32_t i = 0; i < n; ++i)
+      if (active[i]) cls[i] = rank[urow_of_key[key_of[i]]];
+    finish();
+    if (role_filter || !have_roles) return;
+    // role factor (candidates._role_factor): one row per distinct role set of the active requests
+    std::unordered_map<std::string, uint32_t> sidx;
+    std::vector<uint32_t> set_first;
+    std::vector<uint32_t> rkey(n, 0xFFFFu);
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!active[i]) continue;
+      kb.assign((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      auto it = sidx.find(kb);
+      if (it == sidx.end()) {
+        it = sidx.emplace(kb, (uint32_t)set_first.size()).first;
+        set_first.push_back(i);
+      }
+      rkey[i] = it->second;
+    }
+    if (set_first.empty() || set_first.size() * W * 4 > ROLE_ROW_BYTES || set_first.size() >= 0xFFFF) return;
+    B.role_bits.assign(set_first.size() * W, 0u);
+    for (size_t k = 0; k < set_first.size(); ++k) {
+      const uint32_t i = set_first[k];
+      Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
+      for (uint32_t w = 0; w < W; ++w) r[w] &= valid[w];
+      sets_need_policies(r);
+      std::copy(r.begin(), r.end(), B.role_bits.begin() + k * W);
+    }
+    B.role_key = std::move(rkey);
+    B.role_rows = (uint32_t)set_first.size();
+    return;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ batch driver + C ABI
+namespace {
+
+std::vector<std::pair<const char*, const char*>> array_items(const char* p, const char* e) {
+  auto ws = [&] {
+    while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  };
+  std::vector<std::pair<const char*, const char*>> out;
+  ws();
+  if (p >= e || *p != '[') throw ParseError{"requests: expected a JSON array"};
+  ++p;
+  ws();
+  if (p < e && *p == ']') {
+    ++p;
+  } else {
+    for (;;) {
+      ws();
+      const char* b = p;
+      p = skip_value(p, e);
+      out.push_back({b, p});
+      ws();
+      if (p < e && *p == ',') {
+        ++p;
+        continue;
+      }
+      if (p < e && *p == ']') {
+        ++p;
+        break;
+      }
+      throw ParseError{"requests: expected ',' or ']'"};
+    }
+  }
+  ws();
+  if (p != e) throw ParseError{"requests: trailing text"};
+  return out;
+}
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int threads) {
+  const double t0 = now_s();
+  auto B = std::make_unique<acs_codec_batch>();
+  B->codec = c;
+  const auto items = array_items(json, json + len);
+  const uint32_t n = (uint32_t)items.size();
+  if (items.size() > 0xFFFFFFFull) throw ParseError{"requests: batch too large"};
+  B->n = n;
+  B->hdr.assign(n, ReqHdr{});
+  B->res.assign((size_t)QMAX * n, ReqRes{});
+  B->subj.assign((size_t)SMAX * n, Pair{});
+  B->act.assign((size_t)AMAX * n, Pair{});
+  B->roles.assign((size_t)RMAX * n, 0u);
+  B->reason.assign(n, nullptr);
+  int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  if ((uint32_t)T > n / 64 + 1) T = (int)(n / 64 + 1);
+  B->strings.resize(T);
+  for (int t = 0; t < T; ++t) B->strings[t].base = c->n_dict + ((uint32_t)t << LOCAL_BITS);
+  Shared sh;
+  std::vector<std::vector<uint32_t>> arenas(T);
+  std::vector<std::string> errs(T);
+  std::atomic<uint64_t> hits{0}, misses{0};
+  auto work = [&](int t) {
+    const uint32_t lo = (uint32_t)((uint64_t)n * t / T), hi = (uint32_t)((uint64_t)n * (t + 1) / T);
+    try {
+      Encoder enc(*c, *B, sh, (uint32_t)t);
+      for (uint32_t i = lo; i < hi; ++i) enc.encode(i, items[i].first, items[i].second);
+      arenas[t] = std::move(enc.arena);
+      hits += enc.hits;
+      misses += enc.misses;
+    } catch (const ParseError& e) {
+      errs[t] = std::string("requests: ") + e.what;
+    } catch (const std::exception& e) {
+      errs[t] = e.what();
+    }
+  };
+  {
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+  }
+  for (auto& e : errs)
+    if (!e.empty()) throw std::runtime_error(e);
+  B->hr_hits = hits;
+  B->hr_misses = misses;
+  // one arena: shift each thread's offsets
+  size_t total = 0;
+  for (auto& a : arenas) total += a.size();
+  B->arena.reserve(total);
+  for (int t = 0; t < T; ++t) {
+    const uint32_t base = (uint32_t)B->arena.size();
+    const uint32_t lo = (uint32_t)((uint64_t)n * t / T), hi = (uint32_t)((uint64_t)n * (t + 1) / T);
+    for (uint32_t i = lo; i < hi; ++i) B->hdr[i].arena_off += base;
+    B->arena.insert(B->arena.end(), arenas[t].begin(), arenas[t].end());
+  }
+  // regex-matrix columns in first-use order (request, attribute), as encoder.py numbers them
+  std::vector<uint32_t> order(sh.cols.size()), remap(sh.cols.size());
+  for (size_t k = 0; k < order.size(); ++k) order[k] = (uint32_t)k;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sh.cols[a].first < sh.cols[b].first; });
+  for (size_t k = 0; k < order.size(); ++k) remap[order[k]] = (uint32_t)k;
+  for (uint32_t j = 0; j < (uint32_t)QMAX; ++j)
+    for (uint32_t i = 0; i < n; ++i) {
+      ReqRes& q = B->res[(size_t)j * n + i];
+      if ((q.kind & K_ENT_LOOSE) && j < B->hdr[i].nres) q.col = (uint16_t)remap[q.col];
+    }
+  const double t1 = now_s();
+  // regex matrix: one cached column of cells per distinct entity value
+  const uint32_t n_rx = (uint32_t)c->rx_pat.size();
+  B->rx_cols = order.empty() ? 1u : (uint32_t)order.size();
+  B->rx_rows = n_rx ? n_rx : 1u;
+  B->rx.assign((size_t)B->rx_cols * B->rx_rows, 0);
+  std::vector<std::string> keys(B->rx_cols);
+  for (size_t k = 0; k < order.size(); ++k) keys[k] = sh.cols[order[k]].key;
+  {
+    std::atomic<size_t> next{0};
+    auto cells = [&] {
+      for (;;) {
+        const size_t k = next.fetch_add(1);
+        if (k >= order.size()) return;
+        std::shared_ptr<const std::vector<uint8_t>> col;
+        {
+          std::lock_guard<std::mutex> lock(c->col_mu);
+          auto it = c->rx_cols.find(keys[k]);
+          if (it != c->rx_cols.end()) col = it->second;
+        }
+        if (!col) {
+          auto v = std::make_shared<std::vector<uint8_t>>(n_rx);
+          const bool nul = keys[k][0] != 's';
+          const std::string_view q = nul ? std::string_view() : std::string_view(keys[k]).substr(1);
+          for (uint32_t r = 0; r < n_rx; ++r) (*v)[r] = rx_cell(c->rx_pat[r], nul, q);
+          std::lock_guard<std::mutex> lock(c->col_mu);
+          if (c->rx_cols.size() > 65536) c->rx_cols.clear();
+          c->rx_cols.emplace(keys[k], v);
+          col = v;
+        }
+        std::copy(col->begin(), col->end(), B->rx.begin() + k * B->rx_rows);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T && (size_t)t < order.size(); ++t) pool.emplace_back(cells);
+    cells();
+    for (auto& th : pool) th.join();
+  }
+  const double t2 = now_s();
+  Classes cl(*c, *B, T);
+  cl.col_keys = keys;  // padding column: ''
+  cl.run();
+  const double t3 = now_s();
+  B->seconds[0] = t1 - t0;
+  B->seconds[1] = t2 - t1;
+  B->seconds[2] = t3 - t2;
+  B->seconds[3] = t3 - t0;
+  return B.release();
+}
+
+thread_local std::string g_codec_err;
+
+}  // namespace
+
+extern "C" {
+
+acs_codec* acs_codec_create(const void* blob, size_t n_bytes) {
+  auto c = std::make_unique<acs_codec>();
+  std::string err;
+  try {
+    if (!codec_load(c.get(), blob, n_bytes, err)) {
+      g_codec_err = "acs_codec_create: " + err;
+      acs_internal_set_error(g_codec_err.c_str());
+      return nullptr;
+    }
+  } catch (const std::exception& e) {
+    g_codec_err = std::string("acs_codec_create: ") + e.what();
+    acs_internal_set_error(g_codec_err.c_str());
+    return nullptr;
+  }
+  return c.release();
+}
+
+void acs_codec_free(acs_codec* c) { delete c; }
+
+int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, const char* json, size_t len) {
+  if (!c || !key || (!json && len)) {
+    acs_internal_set_error("acs_codec_set_subject_scopes: null argument");
+    return -1;
+  }
+  auto F = std::make_shared<HrForest>();
+  try {
+    Arena ar;
+    Parser p(ar);
+    const JV* v = p.parse(json, json + len);
+    build_forest(*F, v);
+  } catch (const ParseError& e) {
+    g_codec_err = std::string("acs_codec_set_subject_scopes: ") + e.what;
+    acs_internal_set_error(g_codec_err.c_str());
+    return -1;
+  }
+  std::unique_lock<std::shared_mutex> lock(c->hr_mu);
+  c->hr_subject[std::string(key, key_len)] = F;
+  return 0;
+}
+
+int acs_codec_evict_subject(acs_codec* c, const char* key, size_t key_len) {
+  if (!c || !key) {
+    acs_internal_set_error("acs_codec_evict_subject: null argument");
+    return -1;
+  }
+  std::unique_lock<std::shared_mutex> lock(c->hr_mu);
+  return c->hr_subject.erase(std::string(key, key_len)) ? 1 : 0;
+}
+
+acs_codec_batch* acs_codec_encode(acs_codec* c, const char* json, size_t len, int threads) {
+  if (!c || (!json && len)) {
+    acs_internal_set_error("acs_codec_encode: null argument");
+    return nullptr;
+  }
+  try {
+    return encode_batch(c, json, len, threads);
+  } catch (const ParseError& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what;
+  } catch (const Unsup& u) {
+    g_codec_err = std::string("acs_codec_encode: ") + u.why;
+  } catch (const std::exception& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what();
+  }
+  acs_internal_set_error(g_codec_err.c_str());
+  return nullptr;
+}
+
+void acs_codec_batch_free(acs_codec_batch* b) { delete b; }
+
+int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
+  if (!b || !out) {
+    acs_internal_set_error("acs_codec_batch_view: null argument");
+    return -1;
+  }
+  acs_req_batch v{};
+  v.n = b->n;
+  v.hdr = b->hdr.data();
+  v.res = b->res.data();
+  v.subj = b->subj.data();
+  v.act = b->act.data();
+  v.roles = b->roles.data();
+  v.arena = b->arena.data();
+  v.arena_words = b->arena.size();
+  v.rx = b->rx.data();
+  v.rx_cols = b->rx_cols;
+  v.rx_rows = b->rx_rows;
+  v.cand = b->cand.empty() ? nullptr : b->cand.data();
+  v.cand_words = b->cand_words;
+  v.cand_wp = b->cand_wp;
+  v.cand_wr = b->cand_wr;
+  v.cand_rows = b->cand_rows;
+  if (!b->role_key.empty()) {
+    v.role_key = b->role_key.data();
+    v.role_rows_bits = b->role_bits.data();
+    v.role_rows = b->role_rows;
+  }
+  *out = v;
+  return 0;
+}
+
+const char* acs_codec_batch_reason(const acs_codec_batch* b, uint32_t i) {
+  return b && i < b->n ? b->reason[i] : nullptr;
+}
+
+int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size_t* len) {
+  if (!b || !s || !len) return -1;
+  *s = nullptr;
+  *len = 0;
+  if (id == ID_UNDEF) return 0;
+  if (id == ID_NULL) return 1;
+  const acs_codec* c = b->codec;
+  if (id < c->n_dict) {
+    const std::string_view v = c->string_of(id);
+    *s = v.data();
+    *len = v.size();
+    return 2;
+  }
+  const uint32_t t = (id - c->n_dict) >> LOCAL_BITS, k = (id - c->n_dict) & ((1u << LOCAL_BITS) - 1);
+  if (t >= b->strings.size() || k >= b->strings[t].strs.size()) return -1;
+  *s = b->strings[t].strs[k].data();
+  *len = b->strings[t].strs[k].size();
+  return 2;
+}
+
+int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n) {
+  if (!b || !out) return -1;
+  const double v[6] = {b->seconds[0], b->seconds[1], b->seconds[2], b->seconds[3], (double)b->hr_hits,
+                       (double)b->hr_misses};
+  for (int k = 0; k < n && k < 6; ++k) out[k] = v[k];
+  return 6;
+}
+
+}  // extern "C"

@@ -52,10 +52,6 @@ enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET,
 #define PROF_ADD(k, v)
 #endif
 
-struct Pair {
-  uint32_t id, value;
-};
-
 // regex matrix cell bits (rule entity value row x request entity value column)
 enum RxBits : uint8_t { RX_HIT = 1, RX_RESET = 2, RX_THROW_TYPE = 4, RX_THROW_SYNTAX = 8, RX_HOST = 16 };
 

@@ -463,6 +463,9 @@ extern "C" {
 
 const char* acs_last_error(void) { return g_err.c_str(); }
 
+// The codec (acs_codec.cpp) reports through the same thread-local message.
+void acs_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
 #if defined(ACS_PHASE_PROF)
 // Profiling build only: read and reset the per-phase lane-cycle sums.
 int acs_phase_read(unsigned long long* out, int n) {

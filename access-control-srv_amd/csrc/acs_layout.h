@@ -100,6 +100,10 @@ struct NodeRec {
   uint8_t pad[3];
 };
 
+struct Pair {                // (id, value) of a subject / action attribute, interned
+  uint32_t id, value;
+};
+
 struct RuleResAttr {         // 16 B
   uint32_t value;
   uint32_t hash_sfx;         // id of value.substring(lastIndexOf('#')+1)  (K_PROP)

@@ -162,6 +162,44 @@ int acs_kernel_times(acs_tables* t, float* ms, int n);
  * its stream; -1 if none. */
 float acs_last_kernel_ms(const acs_tables* t);
 
+/* ------------------------------------------------------------------ native request codec
+ * Replaces: the per-request JS work the reference does before and around its matchers —
+ * unmarshallContext's JSON (accessControlService.ts:103-125), the request-only parts of
+ * resourceAttributesMatch / checkHierarchicalScope / verifyACLList (attribute kinds, lodash
+ * _.find context lookups, the verifyACL request loop, the HR-scope flattening of
+ * hierarchicalScope.ts:199-245) — for a whole batch, on host threads, producing the packed
+ * acs_req_batch the kernels read.  csrc/acs_codec.cpp restates acs_mi355x/encoder.py.
+ *
+ * acs_codec_create: from the same image acs_compile takes (its codec section, written by
+ *   acs_mi355x/compiler.store_blob: dictionary, URN ids, regex rows, candidate specs).
+ * acs_codec_encode: `json` = a JSON array of requests ({target, context}, the shape
+ *   AccessController.isAllowed receives); `threads` host threads.  NULL on a malformed
+ *   array (acs_last_error); a request the packed form cannot carry is encoded with
+ *   ACS_RQ_HOST and acs_codec_batch_reason(b, i) says why.  A subject's
+ *   `hierarchical_scopes` tree is cached per distinct JSON text; a subject may instead name
+ *   a forest registered with acs_codec_set_subject_scopes by a "$hrs": "<key>" member (the
+ *   per-subject cache createHRScope fills from Redis, accessController.ts:735-783;
+ *   acs_codec_evict_subject = evictHRScopes, :717-725).
+ * acs_codec_batch_view: the batch's host buffers as an acs_req_batch (valid until
+ *   acs_codec_batch_free), for acs_is_allowed / acs_what_is_allowed or a device upload.
+ *   A batch refers to its codec's dictionary: free batches before their codec.
+ * acs_codec_string: interned id -> string (0 undefined, 1 null, 2 string; -1 unknown), e.g.
+ *   for maskedProperty obligation ids. */
+typedef struct acs_codec acs_codec;
+typedef struct acs_codec_batch acs_codec_batch;
+#define ACS_RQ_HOST 0x2u
+acs_codec* acs_codec_create(const void* blob, size_t n_bytes);
+void acs_codec_free(acs_codec* c);
+int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, const char* json, size_t len);
+int acs_codec_evict_subject(acs_codec* c, const char* key, size_t key_len);
+acs_codec_batch* acs_codec_encode(acs_codec* c, const char* json, size_t len, int threads);
+int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out);
+const char* acs_codec_batch_reason(const acs_codec_batch* b, uint32_t i);
+int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size_t* len);
+/* out[0..5]: seconds parse+encode, regex matrix, candidate classes, total; HR cache hits, misses */
+int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n);
+void acs_codec_batch_free(acs_codec_batch* b);
+
 const char* acs_last_error(void);
 int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 5 packed structs, for host checks */
 int acs_device_count(void);

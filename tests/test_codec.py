@@ -1,0 +1,215 @@
+"""The native request codec (csrc/acs_codec.cpp) against the Python encoder + the oracle.
+
+For the same JSON requests the codec's batch must carry the same request-only facts as
+encoder.py's (flags, counts, attribute kinds, context slots, indexOf masks, regex-matrix
+columns and cells; ids compared as the strings they intern) and, evaluated by the CPU
+build of the evaluator core, give bit-identical decision records and reverse queries —
+which the oracle pins (tests/test_host_core_diff.py).  Also: regex cells vs V8, the HR
+forest cache (inline text, per-subject registration, eviction), multi-threaded encoding.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import host_core
+import randgen
+from diff_utils import build, gpu_outcome, oracle_outcome, norm_rq
+from kat_utils import load_kats, load_fixture, urns_for
+from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS, Oracle
+from oracle.jsval import OracleUnsupported
+from acs_mi355x import compiler, encoder, results, store, synth, layout as L
+from acs_mi355x.codec import NativeCodec
+from acs_mi355x.jsops import MISSING
+
+
+def _s(ov, i):
+    v = ov.string(int(i))
+    return ("m",) if v is MISSING else (("n",) if v is None else ("s", v))
+
+
+def compare_batches(pb, nb, check_cols=True):
+    """Request-only facts of the Python batch `pb` and the codec batch `nb`."""
+    assert pb.n == nb.n
+    n = pb.n
+    ph, nh = pb.hdr, nb.hdr
+    assert np.array_equal(ph["flags"] & 0xFFFF, nh["flags"] & 0xFFFF)
+    for f in ("nres", "nsubj", "nact", "nroles"):
+        assert np.array_equal(ph[f], nh[f]), f
+    host = (ph["flags"] & L.RQ_HOST) != 0
+    assert sorted(pb.host_reasons) == sorted(nb.host_reasons)
+    for i in range(n):
+        if host[i]:
+            continue
+        assert _s(pb.overlay, ph["subject_id"][i]) == _s(nb.overlay, nh["subject_id"][i]), i
+        for j in range(ph["nres"][i]):
+            p, q = pb.res[j, i], nb.res[j, i]
+            for f in ("contains", "kind", "slot_a", "slot_b"):
+                assert p[f] == q[f], (i, j, f)
+            if check_cols:
+                assert p["col"] == q["col"], (i, j)
+            assert _s(pb.overlay, p["value"]) == _s(nb.overlay, q["value"]), (i, j)
+            assert _s(pb.overlay, p["hash_sfx"]) == _s(nb.overlay, q["hash_sfx"]), (i, j)
+        for arr, cnt in ((("subj", "nsubj")), (("act", "nact"))):
+            for j in range(ph[cnt][i]):
+                a, b = getattr(pb, arr)[j, i], getattr(nb, arr)[j, i]
+                assert _s(pb.overlay, a["id"]) == _s(nb.overlay, b["id"])
+                assert _s(pb.overlay, a["value"]) == _s(nb.overlay, b["value"])
+        for j in range(ph["nroles"][i]):
+            assert _s(pb.overlay, pb.roles[j, i]) == _s(nb.overlay, nb.roles[j, i])
+        # context arena: same length per request (contents hold batch-local ids)
+    if check_cols:
+        assert pb.rx.shape == nb.rx.shape and np.array_equal(pb.rx, nb.rx)
+
+
+def decisions_equal(cs, pb, nb):
+    a, b = host_core.is_allowed(cs, pb), host_core.is_allowed(cs, nb)
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    return b
+
+
+@pytest.mark.parametrize("seed", range(0, 600, 25))
+def test_codec_random_stores(seed):
+    for s in range(seed, seed + 25):
+        urns, doc, reqs = randgen.rand_case(s)
+        o, cs = build(urns, doc)
+        pb = encoder.Encoder(cs).encode(reqs)
+        codec = NativeCodec(compiler.store_blob(cs))
+        nb = codec.encode(reqs)
+        compare_batches(pb, nb)
+        dec = decisions_equal(cs, pb, nb)
+        for i, req in enumerate(reqs):
+            got = gpu_outcome(cs, dec[i])
+            if got[0] == "HOST":
+                continue
+            try:
+                assert got == oracle_outcome(o, req), (s, i)
+            except OracleUnsupported:
+                pass
+        # whatIsAllowed: same reverse queries (obligation ids through each batch's strings)
+        pw, nw = host_core.what_is_allowed(cs, pb), host_core.what_is_allowed(cs, nb)
+        assert np.array_equal(pw[0], nw[0]) and np.array_equal(pw[2], nw[2])
+        for i in range(len(reqs)):
+            try:
+                a = norm_rq(results.reverse_query(cs, pb.overlay, pw[0][i], pw[1][i][:pw[2][i]], pw[3][i]))
+            except (results.HostPathRequired, results.EvaluationError) as e:
+                a = type(e).__name__
+            try:
+                b = norm_rq(results.reverse_query(cs, nb.overlay, nw[0][i], nw[1][i][:nw[2][i]], nw[3][i]))
+            except (results.HostPathRequired, results.EvaluationError) as e:
+                b = type(e).__name__
+            assert a == b, (s, i)
+        nb.close()
+        codec.close()
+
+
+def test_codec_kats():
+    by_fx = {}
+    for v in load_kats():
+        by_fx.setdefault((v["fixture"], v["urns"]), []).append(v)
+    checked = 0
+    for (fx, _), vecs in by_fx.items():
+        cs = compiler.compile_store(store.populate(load_fixture(fx)), urns_for(vecs[0]), DEFAULT_CAS)
+        reqs = [v["request"] for v in vecs]
+        pb = encoder.Encoder(cs).encode(reqs)
+        nb = NativeCodec(compiler.store_blob(cs)).encode(reqs)
+        compare_batches(pb, nb)
+        dec = decisions_equal(cs, pb, nb)
+        for v, d in zip(vecs, dec):
+            if v["op"] == "isAllowed":
+                oc = results.outcome(cs, d)
+                if oc[0] == "OK":
+                    assert oc[1] == v["expect"]["decision"], v["spec"]
+                    checked += 1
+    assert checked >= 70
+
+
+@pytest.mark.parametrize("kind,threads", [("c2", 1), ("c2", 4), ("c3", 3)])
+def test_codec_synthetic_threads(kind, threads):
+    doc = synth.c2_store() if kind == "c2" else synth.c3_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 1500 if kind == "c2" else 400, kind, seed=77)
+    reqs = [sb.decode(i) for i in range(sb.batch.n)]
+    pb = encoder.Encoder(cs).encode(reqs)
+    codec = NativeCodec(compiler.store_blob(cs))
+    nb = codec.encode(reqs, threads=threads)
+    compare_batches(pb, nb)
+    decisions_equal(cs, pb, nb)
+    # the synthetic packer and both encoders agree on the decisions
+    assert np.array_equal(host_core.is_allowed(cs, sb.batch).view(np.uint64),
+                          host_core.is_allowed(cs, nb).view(np.uint64))
+    if kind == "c3":  # one flatten per distinct forest (threads may race on a first sight)
+        st = nb.stats()
+        distinct = len(set(zip(sb.draws["scope"].tolist(), sb.draws["role"].tolist())))
+        assert st["hr_cache_hits"] + st["hr_cache_misses"] == sb.batch.n
+        assert st["hr_cache_misses"] <= distinct * threads
+        st2 = codec.encode(reqs, threads=threads).stats()
+        assert st2["hr_cache_misses"] == 0 and st2["hr_cache_hits"] == sb.batch.n
+
+
+def test_codec_subject_scope_registry():
+    """A request naming a registered forest ("$hrs") decides exactly as one carrying the
+    forest inline; eviction sends it to the host; replacing the forest changes it."""
+    doc = synth.c3_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 160, "c3", seed=5)
+    inline = [sb.decode(i) for i in range(sb.batch.n)]
+    codec = NativeCodec(compiler.store_blob(cs))
+    by_ref = []
+    for r in inline:
+        r = json.loads(json.dumps(r))
+        subj = r["context"]["subject"]
+        key = json.dumps(subj["hierarchical_scopes"], sort_keys=True)
+        codec.set_subject_scopes(key, subj.pop("hierarchical_scopes"))
+        subj["$hrs"] = key
+        by_ref.append(r)
+    a = host_core.is_allowed(cs, codec.encode(inline, threads=2))
+    b = host_core.is_allowed(cs, codec.encode(by_ref, threads=2))
+    assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    k0 = by_ref[0]["context"]["subject"]["$hrs"]
+    assert codec.evict_subject(k0) and not codec.evict_subject(k0)
+    nb = codec.encode(by_ref[:1])
+    assert nb.hdr["flags"][0] & L.RQ_HOST and "not in the codec cache" in nb.host_reasons[0]
+
+
+def test_codec_regex_cells_v8():
+    """Every non-host cell the codec computes equals V8's (the rows of a store whose rule
+    entity values are the fixture's patterns, the columns its request values)."""
+    with open(__file__.replace("test_codec.py", "golden/regex_cells.json")) as f:
+        pairs = json.load(f)["pairs"]
+    rules = sorted({p[0] for p in pairs if p[0] is not None})[:600]
+    rset = set(rules)
+    urn = FULL_URNS
+    doc = {"policy_sets": [{"id": "s", "combining_algorithm": DEFAULT_CAS[0]["urn"], "policies": [
+        {"id": "p", "combining_algorithm": DEFAULT_CAS[0]["urn"], "rules": [
+            {"id": f"r{k}", "effect": "PERMIT", "target": {"resources": [{"id": urn["entity"], "value": v}]}}
+            for k, v in enumerate(rules)]}]}]}
+    cs = compiler.compile_store(store.populate(doc), urn, DEFAULT_CAS)
+    reqv = sorted({p[1] for p in pairs if p[1] is not None})
+    reqs = [{"target": {"resources": [{"id": urn["entity"], "value": q}]}} for q in reqv]
+    nb = NativeCodec(compiler.store_blob(cs)).encode(reqs)
+    row = {v: r for r, v in enumerate(cs.rx_rows)}
+    col = {nb.overlay.string(nb.res[0, i]["value"]): nb.res[0, i]["col"] for i in range(nb.n)}
+    checked = 0
+    for rv, qv, want in pairs:
+        if rv not in rset or qv is None:
+            continue
+        got = int(nb.rx[col[qv], row[rv]])
+        if got & L.RX_HOST:
+            continue
+        if got & (L.RX_THROW_TYPE | L.RX_THROW_SYNTAX):
+            got &= L.RX_THROW_TYPE | L.RX_THROW_SYNTAX
+        assert got == want, (rv, qv, got, want)
+        checked += 1
+    assert checked > 5000
+
+
+def test_codec_rejects_malformed_array():
+    cs = compiler.compile_store(store.populate(synth.c2_store()), FULL_URNS, DEFAULT_CAS)
+    codec = NativeCodec(compiler.store_blob(cs))
+    for bad in (b"", b"{}", b"[1,", b"[{\"target\": }]", b"[] x"):
+        with pytest.raises(RuntimeError):
+            codec.encode(bad)
+    assert codec.encode(b"[]").n == 0
+    nb = codec.encode(b'[1, "x", null, {"target": 5}]')
+    assert (nb.hdr["flags"] & L.RQ_HOST).all() or (nb.hdr["flags"][2] & L.RQ_NO_TARGET)
