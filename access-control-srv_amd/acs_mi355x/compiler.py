@@ -495,6 +495,58 @@ def compile_store(policy_sets: dict, urns: dict, combining_algorithms: list) -> 
     return IncrementalCompiler(urns, combining_algorithms).compile(policy_sets)
 
 
+def snapshot_json(policy_sets: dict) -> bytes:
+    """The policySets Map as the JSON snapshot acs_store_compile reads: the Map's values in
+    order, each set's / policy's ``combinables`` the list of its Map's values (JSON.stringify
+    of Array.from(map.values()) at each level, as a Node host produces it)."""
+    import json
+
+    def clean(v):
+        if isinstance(v, dict):
+            return {k: clean(x) for k, x in v.items() if x is not MISSING}
+        if isinstance(v, list):
+            return [None if x is MISSING else clean(x) for x in v]
+        return v
+
+    def pol(p):
+        if p is None or p is MISSING:
+            return None
+        out = clean({k: v for k, v in p.items() if k != "combinables"})
+        out["combinables"] = [None if r is None or r is MISSING else clean(r) for r in p["combinables"].values()]
+        return out
+
+    sets = []
+    for ps in policy_sets.values():
+        if not isinstance(ps, dict):
+            sets.append(None)
+            continue
+        out = clean({k: v for k, v in ps.items() if k not in ("combinables", "policies")})
+        out["combinables"] = [pol(p) for p in ps["combinables"].values()]
+        sets.append(out)
+    return json.dumps(sets, ensure_ascii=False, separators=(",", ":")).encode("utf-8", "surrogatepass")
+
+
+def native_store_blob(policy_sets: dict, urns: dict, combining_algorithms: list) -> bytes:
+    """The store image compiled by the native compiler (acs_store_compile)."""
+    import ctypes as C
+    import json
+    from .native import last_error, load
+    lib = load()
+    lib.acs_store_compile.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t,
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    lib.acs_blob_free.argtypes = [C.c_void_p]
+    snap = snapshot_json(policy_sets)
+    u = json.dumps(urns).encode()
+    c = json.dumps(combining_algorithms).encode()
+    out, n = C.c_void_p(), C.c_size_t()
+    if lib.acs_store_compile(snap, len(snap), u, len(u), c, len(c), C.byref(out), C.byref(n)) != 0:
+        raise Unsupported(last_error(lib))
+    try:
+        return C.string_at(out.value, n.value)
+    finally:
+        lib.acs_blob_free(out)
+
+
 # URN config names the native request codec (csrc/acs_codec.cpp) reads, in this order.
 CODEC_URNS = ("entity", "property", "operation", "resourceID", "actionID", "role", "roleScopingEntity",
               "roleScopingInstance", "hierarchicalRoleScoping", "ownerEntity", "ownerInstance",

@@ -310,6 +310,61 @@ class SynthBatch:
         return req
 
 
+    def json_text(self, idx=None) -> bytes:
+        """JSON array text of requests ``idx`` (default: all), built from string templates —
+        millions per second's worth, for the end-to-end (JSON -> decision) measurement.  Equal,
+        request for request, to ``json.dumps(decode(i))`` except that at c3 the subject names
+        its HR forest by reference — ``"$hrs": hrs_key(i)`` in place of the inline
+        ``hierarchical_scopes`` tree (the per-subject forest cache of acs_codec; register
+        the forests with ``hrs_forests``)."""
+        d = self.draws
+        idx = np.arange(self.batch.n) if idx is None else np.asarray(idx)
+        u_ent, u_prop, u_rid = URN["entity"], URN["property"], URN["resourceID"]
+        ents = [f'{{"id":"{u_ent}","value":"{entity(k)}"}}' for k in range(N_ENT)]
+        props = [[f',{{"id":"{u_prop}","value":"{prop(k, p)}"}}' for p in range(N_PROPS)] for k in range(N_ENT)]
+        acts = [f'"actions":[{{"id":"{URN["actionID"]}","value":"{a}"}}]' for a in ACTIONS]
+        pre_s = f'{{"target":{{"subjects":[{{"id":"{URN["role"]}","value":"r'
+        mid_s = f'"}},{{"id":"{URN["subjectID"]}","value":"u'
+        out = []
+        ent, rol, act, usr, rid, npr, pr, pe = (d["ent"], d["role"], d["act"], d["user"], d["rid"], d["nprops"],
+                                                d["props"], d["prop_ent"])
+        c3 = self.kind != "c2"
+        if c3:
+            scope, owner = d["scope"], d["owner"]
+            rse, rsi, oe, oi = URN["rse"], URN["rsi"], URN["ownerEntity"], URN["ownerInstance"]
+        for i in idx.tolist():
+            e, r, u = int(ent[i]), int(rol[i]), int(usr[i])
+            res = ents[e] + f',{{"id":"{u_rid}","value":"res{int(rid[i])}"}}' + \
+                "".join(props[int(pe[i, k])][int(pr[i, k])] for k in range(int(npr[i])))
+            head = f'{pre_s}{r}{mid_s}{u}"}}],"resources":[{res}],{acts[int(act[i])]}}},'
+            if not c3:
+                ctx = (f'"context":{{"subject":{{"id":"u{u}","role_associations":[{{"role":"r{r}","attributes":[]}}],'
+                       f'"hierarchical_scopes":[]}},"resources":[]}}}}')
+            else:
+                sc = int(scope[i])
+                ctx = (f'"context":{{"subject":{{"id":"u{u}","role_associations":[{{"role":"r{r}","attributes":['
+                       f'{{"id":"{rse}","value":"{ORG_ENTITY}","attributes":[{{"id":"{rsi}","value":"org{sc}"}}]}}]}}],'
+                       f'"$hrs":"{self.hrs_key(i)}"}},"resources":[{{"id":"res{int(rid[i])}","meta":{{"owners":['
+                       f'{{"id":"{oe}","value":"{ORG_ENTITY}","attributes":[{{"id":"{oi}","value":"org{int(owner[i])}"}}]}}'
+                       f']}}}}]}}}}')
+            out.append(head + ctx)
+        return ("[" + ",".join(out) + "]").encode()
+
+    def hrs_key(self, i):
+        """The subject forest a c3 request names: its scope org and role."""
+        return f"s{int(self.draws['scope'][i])}:r{int(self.draws['role'][i])}"
+
+    def hrs_forests(self, idx=None):
+        """{hrs_key: hierarchical_scopes} of requests ``idx`` (the forests to register)."""
+        out = {}
+        idx = np.arange(self.batch.n) if idx is None else np.asarray(idx)
+        for i in idx.tolist():
+            k = self.hrs_key(i)
+            if k not in out:
+                out[k] = [self.tree.subtree_json(int(self.draws["scope"][i]), role(int(self.draws["role"][i])))]
+        return out
+
+
 class SharedValues:
     """Values shared by many decoded requests, referenced as {"$shared": k}."""
 

@@ -1,0 +1,530 @@
+// acs_compiler.cpp — native policy-store compiler (C ABI: acs_store_compile, include/acs_mi355x.h).
+//
+// The `policySets` Map of AccessController (accessController.ts:32; nested combinables
+// Maps, interfaces.ts:12-18) as a JSON snapshot -> the store image acs_compile and
+// acs_codec_create take.  It restates acs_mi355x/compiler.py (compile_store + store_blob)
+// step for step, interning strings in the same order, so the image is byte-identical to
+// the Python compiler's (tests/test_codec.py).  Everything that depends on a rule / policy
+// / set alone is evaluated here once:
+//
+//   target subject scan (role, roleScopingEntity, hierarchicalRoleScoping, skipACL)
+//                                  accessController.ts:797-806, hierarchicalScope.ts:25-42, verifyACL.ts:13-25
+//   policyEffect prefix (pe_at)    accessController.ts:136-148
+//   evaluation_cacheable prefix    accessController.ts:202-211
+//   effect / CA codes              accessController.ts:299-312, 832-838
+//   candidate specs                acs_mi355x/candidates.py
+//
+// Snapshot format: a JSON array of the Map's values in Map order; a set's `combinables` is
+// the array of its policies (Map order, null entries kept), a policy's `combinables` the
+// array of its rules — JSON.stringify of Array.from(map.values()) at each level.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/acs_mi355x.h"
+#include "acs_json.h"
+#include "acs_layout.h"
+
+extern "C" void acs_internal_set_error(const char* msg);
+
+using namespace acs;
+using namespace acs_json;
+
+namespace {
+
+struct CompileError {
+  std::string why;
+};
+[[noreturn]] void fail(const std::string& why) { throw CompileError{why}; }
+
+const char* const kCodecUrns[] = {"entity", "property", "operation", "resourceID", "actionID", "role",
+                                  "roleScopingEntity", "roleScopingInstance", "hierarchicalRoleScoping",
+                                  "ownerEntity", "ownerInstance", "aclIndicatoryEntity", "aclInstance", "create",
+                                  "read", "modify", "delete", "user", "skipACL", "maskedProperty"};
+constexpr int N_CODEC_URNS = 20;
+
+// Object.prototype members: an effect string naming one resolves to a function in
+// Response_Decision[effect] (accessController.ts:312) — not restated, refused.
+const char* const kProtoKeys[] = {"constructor", "__proto__", "toString", "toLocaleString", "valueOf",
+                                  "hasOwnProperty", "isPrototypeOf", "propertyIsEnumerable", "__defineGetter__",
+                                  "__defineSetter__", "__lookupGetter__", "__lookupSetter__"};
+
+struct Builder {
+  // dictionary (compiler.Dictionary: 0 undefined, 1 null, 2 '')
+  std::vector<std::string> strings{"", "", ""};
+  std::unordered_map<std::string, uint32_t> ids{{"", ID_EMPTY}};
+  // URN config
+  std::vector<std::pair<std::string, const JV*>> urns;  // config order
+  std::unordered_map<std::string, const JV*> urn;
+  // combining algorithms: urn key -> code
+  std::vector<std::pair<std::string, uint8_t>> ca_map;  // key: 's'+urn / 'm' undefined / 'n' null
+  // pools
+  std::vector<RuleResAttr> rres;
+  std::vector<Pair> pairs;
+  std::vector<uint32_t> u32pool;
+  std::vector<uint32_t> rx_rows;  // row -> dictionary id of the value (0 undefined, 1 null)
+  std::unordered_map<uint32_t, uint32_t> rx_index;
+  // evaluation_cacheable values: kind (0 undefined 1 null 2 false 3 true 4 number 5 string 6 object)
+  struct Ec {
+    int kind;
+    double num;
+    std::string s;
+    bool truthy;
+  };
+  std::vector<Ec> ec{{0, 0, "", false}, {1, 0, "", false}, {2, 0, "", false}, {3, 0, "", true}};
+  // node tables + candidate specs (kind 0 never, 1 always, 2 rows)
+  std::vector<NodeRec> sets, pols, rules;
+  std::vector<uint8_t> spec_kind[3];
+  std::vector<std::vector<uint32_t>> spec_rows[3];
+
+  uint32_t intern(const JV* v) {
+    if (v->t == J_UNDEF) return ID_UNDEF;
+    if (v->t == J_NULL) return ID_NULL;
+    if (v->t != J_STR) fail("non-string value");
+    return intern_sv(v->str());
+  }
+  uint32_t intern_sv(std::string_view s) {
+    auto it = ids.find(std::string(s));
+    if (it != ids.end()) return it->second;
+    const uint32_t i = (uint32_t)strings.size();
+    strings.emplace_back(s);
+    ids.emplace(std::string(s), i);
+    return i;
+  }
+  const JV* U(const char* name) const {
+    auto it = urn.find(name);
+    return it == urn.end() ? &kUndef : it->second;
+  }
+  static bool strict_eq(const JV* a, const JV* b) {
+    if (a->t == J_UNDEF || b->t == J_UNDEF || a->t == J_NULL || b->t == J_NULL) return a->t == b->t;
+    if (a->t == J_STR || b->t == J_STR) return a->t == J_STR && b->t == J_STR && a->str() == b->str();
+    if ((a->t == J_TRUE || a->t == J_FALSE) || (b->t == J_TRUE || b->t == J_FALSE)) return a->t == b->t;
+    if (a->t == J_NUM && b->t == J_NUM) return a->num == b->num;
+    return a == b;
+  }
+  static void check_scalar(const JV* v) {
+    if (!(v->t == J_UNDEF || v->t == J_NULL || v->t == J_STR)) fail("non-string attribute scalar");
+  }
+  uint8_t ca_code(const JV* urn_v) const {
+    std::string key;
+    if (urn_v->t == J_UNDEF) key = "m";
+    else if (urn_v->t == J_NULL) key = "n";
+    else if (urn_v->t == J_STR) key = "s" + std::string(urn_v->str());
+    else return CA_INVALID;  // a non-string combining_algorithm matches no configured URN
+    for (auto& kv : ca_map)
+      if (kv.first == key) return kv.second;
+    return CA_INVALID;
+  }
+  static uint8_t effect_code(const JV* e) {
+    if (e->t == J_UNDEF) return EFF_UNDEF;
+    if (e->t == J_NULL) return EFF_NULL;
+    if (e->t == J_STR) {
+      const std::string_view s = e->str();
+      for (const char* k : kProtoKeys)
+        if (s == k) fail("effect resolves to an Object.prototype member");
+      if (s == "PERMIT") return EFF_PERMIT;
+      if (s == "DENY") return EFF_DENY;
+      if (s == "NOT_APPLICABLE") return EFF_NOT_APPLICABLE;
+      if (s == "INDETERMINATE") return EFF_INDETERMINATE;
+      if (s == "UNRECOGNIZED") return EFF_UNRECOGNIZED;
+    }
+    return truthy(e) ? EFF_OTHER_TRUTHY : EFF_OTHER_FALSY;
+  }
+  uint8_t ec_code(const JV* v) {
+    Ec x{6, 0, "", true};
+    switch (v->t) {
+      case J_UNDEF: return EC_UNDEF;
+      case J_NULL: return EC_NULL;
+      case J_FALSE: return EC_FALSE;
+      case J_TRUE: return EC_TRUE;
+      case J_NUM: x = {4, v->num, "", v->num == v->num && v->num != 0}; break;
+      case J_STR: x = {5, 0, std::string(v->str()), v->n != 0}; break;
+      default: break;  // objects / arrays: each value its own entry (identity)
+    }
+    if (x.kind != 6)
+      for (size_t k = 4; k < ec.size(); ++k)
+        if (ec[k].kind == x.kind && (x.kind == 4 ? ec[k].num == x.num : ec[k].s == x.s)) return (uint8_t)k;
+    if (ec.size() >= 255) fail("too many distinct evaluation_cacheable values");
+    ec.push_back(x);
+    return (uint8_t)(ec.size() - 1);
+  }
+  uint32_t rx_row(const JV* v) {
+    const uint32_t id = intern(v);
+    auto it = rx_index.find(id);
+    if (it != rx_index.end()) return it->second;
+    const uint32_t r = (uint32_t)rx_rows.size();
+    if (r >= 0xFFFF) fail("too many distinct rule entity values");
+    rx_index.emplace(id, r);
+    rx_rows.push_back(id);
+    return r;
+  }
+  static const JV* attrs(const JV* v, const char* what) {  // _attrs of `v || []`
+    if (!truthy(v)) return nullptr;
+    if (v->t != J_ARR) fail(std::string("target ") + what + " is not an array");
+    for (uint32_t k = 0; k < v->n; ++k) {
+      if (v->a[k].t != J_OBJ) fail(std::string("non-object entry in target ") + what);
+      check_scalar(get(&v->a[k], "id"));
+      check_scalar(get(&v->a[k], "value"));
+    }
+    return v;
+  }
+  uint32_t add_pairs(const JV* lst) {
+    const uint32_t off = (uint32_t)pairs.size();
+    if (lst)
+      for (uint32_t k = 0; k < lst->n; ++k)
+        pairs.push_back(Pair{intern(get(&lst->a[k], "id")), intern(get(&lst->a[k], "value"))});
+    return off;
+  }
+
+  struct Target {
+    bool present = false;
+    NodeRec rec{};
+    int spec_kind = 1;  // 1 always, 2 rows
+    std::vector<uint32_t> rows;
+  };
+
+  // compiler._Builder.target: inline target fields of a node record
+  Target target(const JV* t) {
+    Target T;
+    if (!truthy(t)) return T;
+    if (t->t != J_OBJ) fail("target is not an object");
+    T.present = true;
+    const JV* subs = attrs(get(t, "subjects"), "subjects");
+    const JV* acts = attrs(get(t, "actions"), "actions");
+    const JV* res = attrs(get(t, "resources"), "resources");
+    const JV* sj = get(t, "subjects");
+    if (sj->t != J_UNDEF && sj->t != J_ARR) fail("subjects");
+    const uint32_t ns = subs ? subs->n : 0, na = acts ? acts->n : 0, nr = res ? res->n : 0;
+    NodeRec& R = T.rec;
+    uint32_t flags = 0;
+    const JV* role = &kUndef;
+    for (uint32_t k = 0; k < ns; ++k)
+      if (strict_eq(get(&subs->a[k], "id"), U("role"))) role = get(&subs->a[k], "value");
+    if (ns == 0) flags |= TF_SUBJ_EMPTY;
+    else if (truthy(role)) flags |= TF_SUBJ_ROLE;
+    if (ns > 0) flags |= TF_HAS_SUBJECTS;
+    R.role = intern(role);
+    R.subj_off = add_pairs(subs);
+    R.subj_n = (uint16_t)ns;
+    R.act_off = add_pairs(acts);
+    R.act_n = (uint16_t)na;
+    // checkHierarchicalScope subject scan (if / else-if chain, hierarchicalScope.ts:29-37)
+    static const JV kTrue = [] {
+      JV v;
+      v.t = J_STR;
+      v.s = "true";
+      v.n = 4;
+      return v;
+    }();
+    const JV* hr_check = &kTrue;
+    const JV* se = &kUndef;
+    for (uint32_t k = 0; k < ns; ++k) {
+      const JV* i = get(&subs->a[k], "id");
+      if (strict_eq(i, U("role"))) {
+      } else if (strict_eq(i, U("hierarchicalRoleScoping"))) {
+        hr_check = get(&subs->a[k], "value");
+      } else if (strict_eq(i, U("roleScopingEntity"))) {
+        se = get(&subs->a[k], "value");
+      }
+    }
+    if (ns == 0 || !truthy(se)) flags |= TF_HR_TRIVIAL;
+    if (hr_check->t == J_STR && hr_check->str() == "true") flags |= TF_HR_CHECK;
+    R.se = intern(se);
+    // verifyACLList subject scan (verifyACL.ts:17-25)
+    std::vector<uint32_t> scoped;
+    for (uint32_t k = 0; k < ns; ++k) {
+      const JV* i = get(&subs->a[k], "id");
+      if (strict_eq(i, U("role"))) {
+        scoped.push_back(intern(get(&subs->a[k], "value")));
+      } else if (strict_eq(i, U("skipACL"))) {
+        flags |= TF_ACL_SKIP;
+        break;
+      }
+    }
+    R.acl_roles_off = (uint32_t)u32pool.size();
+    R.acl_roles_n = (uint16_t)scoped.size();
+    u32pool.insert(u32pool.end(), scoped.begin(), scoped.end());
+    // resources
+    if (nr == 0) flags |= TF_RES_EMPTY;
+    R.res_off = (uint32_t)rres.size();
+    R.res_n = (uint16_t)nr;
+    const JV* last_prop = &kUndef;
+    const JV* uent = U("entity");
+    for (uint32_t k = 0; k < nr; ++k) {
+      const JV* i = get(&res->a[k], "id");
+      const JV* v = get(&res->a[k], "value");
+      uint8_t kind = 0;
+      if (strict_eq(i, uent)) kind |= K_ENT;
+      if ((nullish(i) && nullish(uent)) || strict_eq(i, uent)) kind |= K_ENT_LOOSE;
+      if (strict_eq(i, U("operation"))) kind |= K_OP;
+      if (strict_eq(i, U("property"))) {
+        kind |= K_PROP;
+        flags |= TF_RULE_PROPS;
+        last_prop = v;
+      }
+      uint32_t hs = ID_UNDEF;
+      if ((kind & K_PROP) && v->t == J_STR) {
+        const std::string_view s = v->str();
+        const size_t h = s.rfind('#');
+        hs = intern_sv(h == std::string_view::npos ? s : s.substr(h + 1));
+      }
+      const uint32_t row = (kind & K_ENT_LOOSE) ? rx_row(v) : 0;
+      RuleResAttr a{};
+      a.value = intern(v);
+      a.hash_sfx = hs;
+      a.row = (uint16_t)row;
+      a.kind = kind;
+      rres.push_back(a);
+    }
+    R.last_prop_value = intern(last_prop);
+    bool has_op = false, prop_or_op = false;
+    for (uint32_t k = 0; k < nr; ++k) {
+      const JV* i = get(&res->a[k], "id");
+      has_op = has_op || strict_eq(i, U("operation"));
+      prop_or_op = prop_or_op || strict_eq(i, U("property")) || strict_eq(i, U("operation"));
+    }
+    if (nr == 0 || has_op) {
+      T.spec_kind = 1;
+    } else {
+      T.spec_kind = 2;
+      for (uint32_t k = 0; k < nr; ++k)
+        if (strict_eq(get(&res->a[k], "id"), uent)) T.rows.push_back(rx_row(get(&res->a[k], "value")));
+    }
+    if (nr > 0 && !prop_or_op) flags |= TF_RES_ENT_ONLY;
+    if (last_prop->t == J_STR) {
+      flags |= TF_LASTPROP_STR;
+      if (last_prop->str().find('#') != std::string_view::npos) flags |= TF_LASTPROP_HASH;
+    }
+    R.tflags = flags;
+    return T;
+  }
+
+  void push_spec(int sec, bool has_target, const Target& T, bool null_rule) {
+    if (has_target) {  // rows listed but none (no entity attribute): never a candidate
+      spec_kind[sec].push_back((uint8_t)(T.spec_kind == 2 && T.rows.empty() ? 0 : T.spec_kind));
+      spec_rows[sec].push_back(T.spec_kind == 2 ? T.rows : std::vector<uint32_t>{});
+    } else {
+      spec_kind[sec].push_back(null_rule ? 0 : 1);
+      spec_rows[sec].push_back({});
+    }
+  }
+
+  // compiler._compile_set + _assemble (global offsets from the start)
+  void compile_set(const JV* ps) {
+    if (ps->t != J_OBJ) fail("null policy set");
+    Target st = target(get(ps, "target"));
+    NodeRec S = st.rec;
+    S.nflags = st.present ? NF_HAS_TARGET : 0;
+    S.child_begin = (uint32_t)pols.size();
+    const JV* combin = get(ps, "combinables");
+    if (combin->t != J_ARR) fail("policy set without combinables");
+    uint8_t pe_at = EFF_UNDEF;
+    std::vector<NodeRec> my_pols;  // set record goes first in the Python order of node appends
+    for (uint32_t k = 0; k < combin->n; ++k) {
+      const JV* pol = &combin->a[k];
+      if (pol->t == J_NULL) {
+        NodeRec P{};
+        P.nflags = NF_NULL;
+        P.child_begin = P.child_end = P.fe = (uint32_t)rules.size();
+        P.pe_at = pe_at;
+        pols.push_back(P);
+        push_spec(1, false, Target{}, false);
+        continue;
+      }
+      if (pol->t != J_OBJ) fail("policy is not an object");
+      Target pt = target(get(pol, "target"));
+      NodeRec P = pt.rec;
+      uint8_t nf = pt.present ? NF_HAS_TARGET : 0;
+      if (truthy(get(pol, "effect"))) {
+        nf |= NF_EFFECT_TRUTHY;
+        pe_at = effect_code(get(pol, "effect"));  // accessController.ts:138-140
+      }
+      P.nflags = nf;
+      P.child_begin = (uint32_t)rules.size();
+      P.effect = effect_code(get(pol, "effect"));
+      P.ec = ec_code(get(pol, "evaluation_cacheable"));
+      P.ca = ca_code(get(pol, "combining_algorithm"));
+      P.pe_at = pe_at;
+      const JV* rcomb = get(pol, "combinables");
+      if (rcomb->t != J_ARR) fail("policy without combinables");
+      uint32_t fe = NONE32;
+      for (uint32_t r = 0; r < rcomb->n; ++r) {
+        const JV* rule = &rcomb->a[r];
+        if (rule->t == J_NULL) {
+          NodeRec Q{};
+          Q.nflags = NF_NULL;
+          rules.push_back(Q);
+          push_spec(2, false, Target{}, true);
+          continue;
+        }
+        if (rule->t != J_OBJ) fail("rule is not an object");
+        Target rt = target(get(rule, "target"));
+        NodeRec Q = rt.rec;
+        uint8_t rf = rt.present ? NF_HAS_TARGET : 0;
+        const JV* cond = get(rule, "condition");
+        const JV* clen_v = &kUndef;
+        bool clen = false;
+        if (cond->t == J_STR || cond->t == J_ARR) clen = cond->n > 0;
+        else {
+          clen_v = get(cond, "length");
+          clen = truthy(clen_v);
+        }
+        if (clen) rf |= NF_HAS_CONDITION;
+        const uint8_t ec = ec_code(get(rule, "evaluation_cacheable"));
+        if (this->ec[ec].truthy) rf |= NF_EC_TRUTHY;
+        else if (fe == NONE32) fe = (uint32_t)rules.size();
+        Q.nflags = rf;
+        Q.effect = effect_code(get(rule, "effect"));
+        Q.ec = ec;
+        rules.push_back(Q);
+        push_spec(2, rt.present, rt, false);
+      }
+      P.child_end = (uint32_t)rules.size();
+      P.map_size = rcomb->n;
+      P.fe = fe == NONE32 ? (uint32_t)rules.size() : fe;
+      pols.push_back(P);
+      push_spec(1, pt.present, pt, false);
+    }
+    S.child_end = (uint32_t)pols.size();
+    S.ca = ca_code(get(ps, "combining_algorithm"));
+    S.pe_at = pe_at;
+    sets.push_back(S);
+    push_spec(0, st.present, st, false);
+  }
+};
+
+
+template <class T>
+void put(std::string& out, const T* p, size_t n, size_t align) {
+  out.append((const char*)p, n * sizeof(T));
+  out.append((align - (n * sizeof(T)) % align) % align, '\0');
+}
+
+std::string build_image(Builder& b) {
+  // codec section (compiler.codec_section)
+  std::string sec;
+  const uint32_t n_str = (uint32_t)b.strings.size();
+  std::vector<uint32_t> urn_ids(N_CODEC_URNS);
+  for (int k = 0; k < N_CODEC_URNS; ++k) {
+    const JV* v = b.U(kCodecUrns[k]);
+    urn_ids[k] = v->t == J_STR ? b.intern(v) : ID_UNDEF;
+  }
+  std::vector<uint8_t> kind;
+  std::vector<uint32_t> ptr{0}, idx;
+  for (int s = 0; s < 3; ++s)
+    for (size_t k = 0; k < b.spec_kind[s].size(); ++k) {
+      kind.push_back(b.spec_kind[s][k]);
+      if (b.spec_kind[s][k] == 2) idx.insert(idx.end(), b.spec_rows[s][k].begin(), b.spec_rows[s][k].end());
+      ptr.push_back((uint32_t)idx.size());
+    }
+  std::vector<uint32_t> offs{0};
+  std::string sbytes;
+  for (uint32_t i = 0; i < n_str; ++i) {
+    if (i > ID_EMPTY) sbytes += b.strings[i];
+    offs.push_back((uint32_t)sbytes.size());
+  }
+  const uint32_t hd[8] = {0x43534341u, 1u, n_str, (uint32_t)N_CODEC_URNS, (uint32_t)b.rx_rows.size(),
+                          (uint32_t)kind.size(), (uint32_t)idx.size(), (uint32_t)sbytes.size()};
+  put(sec, hd, 8, 4);
+  put(sec, urn_ids.data(), urn_ids.size(), 4);
+  put(sec, b.rx_rows.data(), b.rx_rows.size(), 4);
+  put(sec, kind.data(), kind.size(), 4);
+  put(sec, ptr.data(), ptr.size(), 4);
+  put(sec, idx.data(), idx.size(), 4);
+  put(sec, offs.data(), offs.size(), 4);
+  put(sec, sbytes.data(), sbytes.size(), 4);
+  // node tables + pools (compiler.store_blob)
+  std::string body;
+  put(body, b.sets.data(), b.sets.size(), 16);
+  put(body, b.pols.data(), b.pols.size(), 16);
+  put(body, b.rules.data(), b.rules.size(), 16);
+  put(body, b.rres.data(), b.rres.size(), 16);
+  put(body, b.pairs.data(), b.pairs.size(), 16);
+  put(body, b.u32pool.data(), b.u32pool.size(), 16);
+  const JV* user = b.U("user");
+  const uint32_t id_user = user->t == J_UNDEF ? ID_UNDEF : b.intern(user);
+  const uint32_t hdr[16] = {ACS_BLOB_MAGIC, ACS_ABI_VERSION, (uint32_t)b.sets.size(), (uint32_t)b.pols.size(),
+                            (uint32_t)b.rules.size(), (uint32_t)b.rres.size(), (uint32_t)b.pairs.size(),
+                            (uint32_t)b.u32pool.size(), id_user, (uint32_t)(64 + body.size()), (uint32_t)sec.size(),
+                            0, 0, 0, 0, 0};
+  std::string out((const char*)hdr, sizeof hdr);
+  out += body;
+  out += sec;
+  return out;
+}
+
+thread_local std::string g_compile_err;
+
+}  // namespace
+
+extern "C" {
+
+int acs_store_compile(const char* store_json, size_t store_len, const char* urns_json, size_t urns_len,
+                      const char* cas_json, size_t cas_len, void** blob_out, size_t* blob_len) {
+  if (!store_json || !urns_json || !cas_json || !blob_out || !blob_len) {
+    acs_internal_set_error("acs_store_compile: null argument");
+    return -1;
+  }
+  *blob_out = nullptr;
+  *blob_len = 0;
+  try {
+    Arena ar;
+    Parser p1(ar), p2(ar), p3(ar);
+    const JV* urns = p1.parse(urns_json, urns_json + urns_len);
+    const JV* cas = p2.parse(cas_json, cas_json + cas_len);
+    const JV* st = p3.parse(store_json, store_json + store_len);
+    if (urns->t != J_OBJ) fail("urns: expected a JSON object");
+    if (cas->t != J_ARR) fail("combining algorithms: expected a JSON array");
+    if (st->t != J_ARR) fail("store: expected a JSON array of policy sets (Map values in order)");
+    Builder b;
+    for (uint32_t k = 0; k < cas->n; ++k) {  // accessController.ts:51-62
+      const JV* m = get(&cas->a[k], "method");
+      uint8_t code;
+      if (m->t == J_STR && m->str() == "denyOverrides") code = CA_DENY_OVERRIDES;
+      else if (m->t == J_STR && m->str() == "permitOverrides") code = CA_PERMIT_OVERRIDES;
+      else if (m->t == J_STR && m->str() == "firstApplicable") code = CA_FIRST_APPLICABLE;
+      else fail("combining algorithm method");
+      const JV* u = get(&cas->a[k], "urn");
+      std::string key = u->t == J_UNDEF ? "m" : u->t == J_NULL ? "n" : u->t == J_STR ? "s" + std::string(u->str()) : "x";
+      bool found = false;
+      for (auto& kv : b.ca_map)
+        if (kv.first == key) {
+          kv.second = code;
+          found = true;
+        }
+      if (!found) b.ca_map.push_back({key, code});
+    }
+    for (uint32_t k = 0; k < urns->n; ++k) {  // URN ids first, in config order
+      const std::string name(urns->o[k].k);
+      const JV* v = &urns->o[k].v;
+      if (b.urn.count(name)) {
+        b.urn[name] = v;
+      } else {
+        b.urn.emplace(name, v);
+        b.urns.push_back({name, v});
+      }
+    }
+    for (auto& kv : b.urns) b.intern(b.urn[kv.first]);
+    for (uint32_t k = 0; k < st->n; ++k) b.compile_set(&st->a[k]);
+    const std::string img = build_image(b);
+    void* mem = malloc(img.size());
+    if (!mem) fail("out of memory");
+    memcpy(mem, img.data(), img.size());
+    *blob_out = mem;
+    *blob_len = img.size();
+    return 0;
+  } catch (const CompileError& e) {
+    g_compile_err = "acs_store_compile: " + e.why;
+  } catch (const ParseError& e) {
+    g_compile_err = std::string("acs_store_compile: ") + e.what;
+  }
+  acs_internal_set_error(g_compile_err.c_str());
+  return -1;
+}
+
+void acs_blob_free(void* blob) { free(blob); }
+
+}  // extern "C"

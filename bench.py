@@ -255,6 +255,50 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
     return cb, par
 
 
+def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
+    """JSON -> decision: the native codec (csrc/acs_codec.cpp) encodes the JSON text of the
+    first n_e2e requests of the timed batch on `threads` host threads, then acs_is_allowed
+    (H2D + sort + K1 + D2H) decides them.  c3 subjects name their HR forests by reference
+    ("$hrs": the per-subject cache of acs_codec, registered once before timing, as the
+    reference's Redis HR cache is warm in steady state).  The records must equal those of
+    the resident (synthetic-packed) path bit for bit."""
+    from acs_mi355x import compiler
+    from acs_mi355x.codec import NativeCodec
+    idx = np.arange(min(n_e2e, sb.batch.n))
+    t0 = time.perf_counter()
+    text = sb.json_text(idx)
+    gen_s = time.perf_counter() - t0
+    codec = NativeCodec(compiler.store_blob(cs))
+    registered = 0
+    if kind != "c2":
+        for k, v in sb.hrs_forests(idx).items():
+            codec.set_subject_scopes(k, v)
+            registered += 1
+    codec.encode(text, threads=threads).close()  # warm: arenas, regex / entity / action caches
+    t0 = time.perf_counter()
+    b = codec.encode(text, threads=threads)
+    t1 = time.perf_counter()
+    dec = tables.is_allowed(b)
+    t2 = time.perf_counter()
+    st = b.stats()
+    same = bool(np.array_equal(dec.view(np.uint64), dec_resident[idx].view(np.uint64)))
+    host = int(((dec["flags"] & 0x04) != 0).sum())
+    b.close()
+    codec.close()
+    n = len(idx)
+    return {"requests": n, "json_bytes": len(text), "json_bytes_per_request": len(text) / n,
+            "json_generation_s": gen_s,
+            "encode": {"requests_per_s": n / (t1 - t0), "cores": threads, "seconds": t1 - t0,
+                       "parts_s": {k: st[k] for k in ("encode_s", "regex_s", "classes_s")},
+                       "hr_forests_registered": registered, "hr_cache_hits": st["hr_cache_hits"],
+                       "hr_cache_misses": st["hr_cache_misses"]},
+            "gpu_host_buffers_s": t2 - t1,
+            "end_to_end": {"requests_per_s": n / (t2 - t0),
+                           "what": "JSON text -> acs_codec_encode -> acs_is_allowed (H2D, sort, K1, D2H) -> "
+                                   "decision records in host memory, sequential (no overlap)"},
+            "host_path_requests": host, "identical_to_resident_path": same}
+
+
 def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist):
     """c4: one step = K2 over a resident batch of whatIsAllowed requests (c3 store and request
     generator); outputs: per-request inclusion bitset over (sets | policies | rules), the
@@ -380,6 +424,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=90.0, help="bound on the oracle's evaluation time")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle parity + CPU baseline leg")
     ap.add_argument("--selftest", action="store_true", help="launcher / collective check on CPU (gloo), no GPU")
+    ap.add_argument("--e2e-requests", type=int, default=1_000_000,
+                    help="requests of the JSON -> decision measurement (0: skip)")
     ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--lib", default=None, help="evaluate with another build of libacs_mi355x (experiments)")
@@ -546,6 +592,10 @@ def main():
             line["pcie_inclusive"] = pcie
         if shard_check:
             line["rule_shard"] = shard_check
+        if world == 1 and args.e2e_requests and not args.rule_shard:
+            log("end to end: JSON -> native codec -> GPU -> decisions")
+            line["end_to_end"] = end_to_end(kind, cs, sb, tables, dec, args.e2e_requests,
+                                            max(1, min(16, os.cpu_count() or 1)))
         if REHEARSAL:
             line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:

@@ -185,6 +185,16 @@ float acs_last_kernel_ms(const acs_tables* t);
  *   A batch refers to its codec's dictionary: free batches before their codec.
  * acs_codec_string: interned id -> string (0 undefined, 1 null, 2 string; -1 unknown), e.g.
  *   for maskedProperty obligation ids. */
+/* Replaces: the Map -> table snapshot step (acs_mi355x/compiler.py, in C++: csrc/acs_compiler.cpp)
+ * for a host without Python.  store_json: the policySets Map as JSON — an array of the Map's
+ * values in order, each set's / policy's `combinables` the array of its Map's values
+ * (null entries kept); urns_json: policies.options.urns (cfg/config.json:270-307);
+ * cas_json: policies.options.combiningAlgorithms.  *blob_out (free with acs_blob_free) is
+ * the image for acs_compile / acs_codec_create, byte-identical to compiler.store_blob. */
+int acs_store_compile(const char* store_json, size_t store_len, const char* urns_json, size_t urns_len,
+                      const char* cas_json, size_t cas_len, void** blob_out, size_t* blob_len);
+void acs_blob_free(void* blob);
+
 typedef struct acs_codec acs_codec;
 typedef struct acs_codec_batch acs_codec_batch;
 #define ACS_RQ_HOST 0x2u

@@ -213,3 +213,36 @@ def test_codec_rejects_malformed_array():
     assert codec.encode(b"[]").n == 0
     nb = codec.encode(b'[1, "x", null, {"target": 5}]')
     assert (nb.hdr["flags"] & L.RQ_HOST).all() or (nb.hdr["flags"][2] & L.RQ_NO_TARGET)
+
+
+# ---------------------------------------------------------------- the native store compiler
+def _both(m, urns):
+    from acs_mi355x.jsops import Unsupported
+    try:
+        a = compiler.store_blob(compiler.compile_store(m, urns, DEFAULT_CAS))
+    except Unsupported:
+        a = "Unsupported"
+    try:
+        b = compiler.native_store_blob(m, urns, DEFAULT_CAS)
+    except Unsupported:
+        b = "Unsupported"
+    return a, b
+
+
+@pytest.mark.parametrize("seed", range(0, 600, 100))
+def test_native_compiler_random_stores_byte_identical(seed):
+    for s in range(seed, seed + 100):
+        urns, doc, _ = randgen.rand_case(s)
+        a, b = _both(store.populate(doc), urns)
+        assert a == b, s
+
+
+def test_native_compiler_fixtures_and_configs_byte_identical():
+    fx = sorted({(v["fixture"], v["urns"]) for v in load_kats()})
+    for name, u in fx:
+        v = next(x for x in load_kats() if x["fixture"] == name and x["urns"] == u)
+        a, b = _both(store.populate(load_fixture(name)), urns_for(v))
+        assert a == b and a != "Unsupported", name
+    for doc in (synth.c2_store(), synth.c3_store()):
+        a, b = _both(store.populate(doc), FULL_URNS)
+        assert a == b
