@@ -552,7 +552,7 @@ CODEC_URNS = ("entity", "property", "operation", "resourceID", "actionID", "role
               "roleScopingInstance", "hierarchicalRoleScoping", "ownerEntity", "ownerInstance",
               "aclIndicatoryEntity", "aclInstance", "create", "read", "modify", "delete", "user", "skipACL",
               "maskedProperty")
-CODEC_MAGIC, CODEC_VERSION = 0x43534341, 1  # "ACSC"
+CODEC_MAGIC, CODEC_VERSION = 0x43534341, 2  # "ACSC"
 
 
 def codec_section(cs: CompiledStore) -> bytes:
@@ -581,9 +581,12 @@ def codec_section(cs: CompiledStore) -> bytes:
         return b + b"\0" * ((-len(b)) % 4)
     hdr = struct.pack("<8I", CODEC_MAGIC, CODEC_VERSION, len(enc), len(CODEC_URNS), len(rx), len(spec), len(idx),
                       len(sbytes))
+    # evaluation_cacheable values beyond undefined / null / false / true (codes 4..), as JSON
+    import json
+    ec = json.dumps(list(cs.ec_values[4:]), ensure_ascii=False, separators=(",", ":")).encode("utf-8", "surrogatepass")
     return b"".join([hdr, np.array(urn_ids, np.uint32).tobytes(), np.array(rx, np.uint32).tobytes(),
                      pad4(kind.tobytes()), ptr.tobytes(), np.array(idx, np.uint32).tobytes(), offs.tobytes(),
-                     pad4(sbytes)])
+                     pad4(sbytes), struct.pack("<I", len(ec)), pad4(ec)])
 
 
 def store_blob(cs: CompiledStore, codec: bool = True) -> bytes:

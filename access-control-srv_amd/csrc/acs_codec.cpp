@@ -57,7 +57,7 @@ enum UrnName {
   U_READ, U_MODIFY, U_DELETE, U_USER, U_SKIPACL, U_MASKED, U_COUNT
 };
 
-constexpr uint32_t CODEC_MAGIC = 0x43534341u, CODEC_VERSION = 1u;
+constexpr uint32_t CODEC_MAGIC = 0x43534341u, CODEC_VERSION = 2u;
 constexpr uint8_t HIT_LIKE = 1 | 4 | 8 | 16;  // RX_HIT | RX_THROW_TYPE | RX_THROW_SYNTAX | RX_HOST
 constexpr uint8_t C_RX_HIT = 1, C_RX_RESET = 2, C_RX_THROW_TYPE = 4, C_RX_THROW_SYNTAX = 8, C_RX_HOST = 16;
 constexpr uint32_t LOCAL_BITS = 24;  // per-thread batch-local id range
@@ -293,6 +293,7 @@ struct acs_codec {
   uint32_t n_dict = 0;
   uint32_t urn[U_COUNT] = {};
   std::string_view urn_s[U_COUNT];
+  std::string ec_json;  // JSON array of the evaluation_cacheable values with codes 4..
   // regex rows
   std::vector<uint32_t> rx_row_id;
   std::vector<RxPattern> rx_pat;
@@ -398,6 +399,13 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     return err = "truncated codec section", false;
   if ((size_t)(e - p) < n_sb || c->soff.back() != n_sb) return err = "bad codec string table", false;
   c->sbytes.assign((const char*)p, n_sb);
+  p += (n_sb + 3) / 4 * 4;
+  uint32_t ecn = 0;
+  if ((size_t)(e - p) < 4) return err = "truncated codec section", false;
+  memcpy(&ecn, p, 4);
+  p += 4;
+  if ((size_t)(e - p) < ecn) return err = "truncated codec section", false;
+  c->ec_json.assign((const char*)p, ecn);
   c->n_dict = n_str;
   c->dict.reserve(n_str * 2);
   for (uint32_t i = ID_EMPTY; i < n_str; ++i) c->dict.emplace(c->string_of(i), i);
@@ -1638,6 +1646,13 @@ int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size
   *s = b->strings[t].strs[k].data();
   *len = b->strings[t].strs[k].size();
   return 2;
+}
+
+int acs_codec_ec_values(const acs_codec* c, const char** json, size_t* len) {
+  if (!c || !json || !len) return -1;
+  *json = c->ec_json.data();
+  *len = c->ec_json.size();
+  return 0;
 }
 
 int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n) {

@@ -17,7 +17,9 @@
 // Snapshot format: a JSON array of the Map's values in Map order; a set's `combinables` is
 // the array of its policies (Map order, null entries kept), a policy's `combinables` the
 // array of its rules — JSON.stringify of Array.from(map.values()) at each level.
+#include <charconv>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -73,6 +75,7 @@ struct Builder {
     double num;
     std::string s;
     bool truthy;
+    const JV* v = nullptr;  // the value itself (JSON for the codec section)
   };
   std::vector<Ec> ec{{0, 0, "", false}, {1, 0, "", false}, {2, 0, "", false}, {3, 0, "", true}};
   // node tables + candidate specs (kind 0 never, 1 always, 2 rows)
@@ -148,6 +151,7 @@ struct Builder {
       for (size_t k = 4; k < ec.size(); ++k)
         if (ec[k].kind == x.kind && (x.kind == 4 ? ec[k].num == x.num : ec[k].s == x.s)) return (uint8_t)k;
     if (ec.size() >= 255) fail("too many distinct evaluation_cacheable values");
+    x.v = v;
     ec.push_back(x);
     return (uint8_t)(ec.size() - 1);
   }
@@ -397,6 +401,74 @@ struct Builder {
 };
 
 
+// JSON text as Python's json.dumps(v, ensure_ascii=False, separators=(",", ":")) writes it
+void json_write(std::string& o, const JV* v) {
+  switch (v->t) {
+    case J_NULL: case J_UNDEF: o += "null"; return;
+    case J_TRUE: o += "true"; return;
+    case J_FALSE: o += "false"; return;
+    case J_NUM: {
+      char buf[64];
+      const double d = v->num;
+      if (d == std::floor(d) && std::fabs(d) < 9007199254740992.0) {
+        snprintf(buf, sizeof buf, "%lld", (long long)d);
+      } else {
+        auto r = std::to_chars(buf, buf + sizeof buf, d);
+        *r.ptr = 0;
+      }
+      o += buf;
+      return;
+    }
+    case J_STR: {
+      o += '"';
+      for (unsigned char c : v->str()) {
+        switch (c) {
+          case '"': o += "\\\""; break;
+          case '\\': o += "\\\\"; break;
+          case '\n': o += "\\n"; break;
+          case '\r': o += "\\r"; break;
+          case '\t': o += "\\t"; break;
+          case '\b': o += "\\b"; break;
+          case '\f': o += "\\f"; break;
+          default:
+            if (c < 0x20) {
+              char buf[8];
+              snprintf(buf, sizeof buf, "\\u%04x", c);
+              o += buf;
+            } else {
+              o += (char)c;
+            }
+        }
+      }
+      o += '"';
+      return;
+    }
+    case J_ARR:
+      o += '[';
+      for (uint32_t k = 0; k < v->n; ++k) {
+        if (k) o += ',';
+        json_write(o, &v->a[k]);
+      }
+      o += ']';
+      return;
+    case J_OBJ:
+      o += '{';
+      for (uint32_t k = 0; k < v->n; ++k) {
+        if (k) o += ',';
+        JV key;
+        key.t = J_STR;
+        key.s = v->o[k].k.data();
+        key.n = (uint32_t)v->o[k].k.size();
+        json_write(o, &key);
+        o += ':';
+        json_write(o, &v->o[k].v);
+      }
+      o += '}';
+      return;
+    default: o += "null"; return;
+  }
+}
+
 template <class T>
 void put(std::string& out, const T* p, size_t n, size_t align) {
   out.append((const char*)p, n * sizeof(T));
@@ -426,7 +498,7 @@ std::string build_image(Builder& b) {
     if (i > ID_EMPTY) sbytes += b.strings[i];
     offs.push_back((uint32_t)sbytes.size());
   }
-  const uint32_t hd[8] = {0x43534341u, 1u, n_str, (uint32_t)N_CODEC_URNS, (uint32_t)b.rx_rows.size(),
+  const uint32_t hd[8] = {0x43534341u, 2u, n_str, (uint32_t)N_CODEC_URNS, (uint32_t)b.rx_rows.size(),
                           (uint32_t)kind.size(), (uint32_t)idx.size(), (uint32_t)sbytes.size()};
   put(sec, hd, 8, 4);
   put(sec, urn_ids.data(), urn_ids.size(), 4);
@@ -436,6 +508,15 @@ std::string build_image(Builder& b) {
   put(sec, idx.data(), idx.size(), 4);
   put(sec, offs.data(), offs.size(), 4);
   put(sec, sbytes.data(), sbytes.size(), 4);
+  std::string ecj = "[";
+  for (size_t k = 4; k < b.ec.size(); ++k) {
+    if (k > 4) ecj += ',';
+    json_write(ecj, b.ec[k].v);
+  }
+  ecj += ']';
+  const uint32_t ecn = (uint32_t)ecj.size();
+  put(sec, &ecn, 1, 4);
+  put(sec, ecj.data(), ecj.size(), 4);
   // node tables + pools (compiler.store_blob)
   std::string body;
   put(body, b.sets.data(), b.sets.size(), 16);

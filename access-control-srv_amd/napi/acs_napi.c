@@ -1,21 +1,38 @@
 /* acs_napi.c — N-API addon over the C ABI of libacs_mi355x.so (include/acs_mi355x.h).
  *
- * The binding a TypeScript host (src/core/accessController.ts) loads to hand
- * packed request batches to the MI355X evaluator; see INTEGRATION.md for the
- * TS side.  Plain C over node_api.h (N-API 8, Node >= 12.22): no V8 headers, no
- * node-gyp needed — access-control-srv_amd/acs_mi355x/build.py compiles it with gcc.
+ * The binding a TypeScript host (src/core/accessController.ts) loads to compile its
+ * policySets Map, encode JSON requests and evaluate them on the MI355X; gpuCodec.js (next
+ * to this file) is the JS layer over it and INTEGRATION.md the TS side.  Plain C over
+ * node_api.h (N-API 8, Node >= 12.22): no V8 headers, no node-gyp —
+ * access-control-srv_amd/acs_mi355x/build.py compiles it with gcc.
  *
  * JS surface:
- *   compile(blob: Uint8Array, device: number) -> handle      acs_compile
- *   free(handle)                                             acs_free
- *   isAllowed(handle, batch) -> Uint8Array(8 n)              acs_is_allowed (sync)
- *   isAllowedAsync(handle, batch) -> Promise<Uint8Array>     same, on the libuv pool
- *   whatIsAllowed(handle, batch) -> {bits, obl, oblN, out}   acs_what_is_allowed
- *   wordsPerRequest(handle), layoutSizes(), deviceCount(), lastError()
- * `batch` = {n, hdr, res, subj, act, roles, arena, rx, rxCols, rxRows,
- *            cand, candWords, candWp, candWr, candRows[, roleKey, roleRowsBits, roleRows]}:
- *            typed arrays / Buffers in the
- * layout of csrc/acs_layout.h (what acs_mi355x/encoder.py produces).
+ *   compileStore(storeJson, urnsJson, casJson) -> Uint8Array   acs_store_compile
+ *   compile(blob: Uint8Array, device?) -> tables                acs_compile
+ *   free(tables)                                                acs_free (deferred past in-flight work)
+ *   codecCreate(blob) -> codec                                  acs_codec_create
+ *   codecSetSubjectScopes(codec, key, scopesJson)               acs_codec_set_subject_scopes
+ *   codecEvictSubject(codec, key) -> bool                       acs_codec_evict_subject
+ *   codecEcValues(codec) -> string (JSON array)                 acs_codec_ec_values
+ *   encode(codec, json, threads?) -> batch                      acs_codec_encode
+ *   batchInfo(batch) -> {n, host: {index: reason}}
+ *   batchString(batch, id) -> string | null | undefined         acs_codec_string
+ *   decideAsync(tables, codec, json, threads?) -> Promise<{records, host}>
+ *                                    encode + acs_is_allowed on the libuv pool, one step
+ *   isAllowed(tables, batch) -> Uint8Array(8 n)                 acs_is_allowed (sync)
+ *   isAllowedAsync(tables, batch) -> Promise<Uint8Array>        same, on the libuv pool
+ *   whatIsAllowed(tables, batch) -> {bits, obl, oblN, out}      acs_what_is_allowed
+ *   whatIsAllowedObl(tables, batch, idx, chunks, cap) -> {obl, oblN}
+ *   wordsPerRequest(tables), layoutSizes(), deviceCount(), lastError()
+ * `batch` = an encode() handle, or a plain object {n, hdr, res, subj, act, roles, arena,
+ * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, roleKey, roleRowsBits,
+ * roleRows]} of typed arrays in the layout of csrc/acs_layout.h; every array is checked
+ * against the sizes `n` and the counts imply before the library reads it.
+ *
+ * Handles are externals with finalizers: a garbage-collected handle releases its GPU
+ * tables / codec / batch.  free() on tables with async work in flight defers the release
+ * until that work completes; any call on a freed handle throws.  A batch keeps its codec
+ * alive (a reference), the codec's dictionary being part of the batch's meaning.
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
@@ -34,6 +51,9 @@
     }                                                                 \
   } while (0)
 
+/* csrc/acs_layout.h sizes (checked against acs_layout_sizes by tests/test_napi.py) */
+enum { HDR_B = 16, RES_B = 16, PAIR_B = 8, QMAX = 16, SMAX = 8, AMAX = 4, RMAX = 8 };
+
 static napi_value throw_acs(napi_env env, const char* what) {
   char msg[512];
   const char* e = acs_last_error();
@@ -42,6 +62,107 @@ static napi_value throw_acs(napi_env env, const char* what) {
   return NULL;
 }
 
+/* ------------------------------------------------------------------ handles */
+enum { H_TABLES = 0x54424c31, H_CODEC = 0x434f4431, H_BATCH = 0x42415431 };
+
+typedef struct {
+  int magic;
+  acs_tables* t;
+  int closed;   /* free() called */
+  int inflight; /* async work items using t */
+  int refs;     /* the external + in-flight work: the struct outlives both */
+} tables_h;
+
+typedef struct {
+  int magic;
+  acs_codec* c;
+  int refs; /* the external + live batches + in-flight work (finalizers run in any order at exit) */
+} codec_h;
+
+typedef struct {
+  int magic;
+  acs_codec_batch* b;
+  codec_h* codec;
+  napi_ref codec_ref;
+} batch_h;
+
+static void tables_release(tables_h* h) {
+  if (h->t) acs_free(h->t);
+  h->t = NULL;
+}
+
+static void tables_unref(tables_h* h) {
+  if (--h->refs == 0) {
+    tables_release(h);
+    h->magic = 0;
+    free(h);
+  }
+}
+
+static void codec_unref(codec_h* h) {
+  if (--h->refs == 0) {
+    if (h->c) acs_codec_free(h->c);
+    h->magic = 0;
+    free(h);
+  }
+}
+
+static void fin_tables(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  tables_h* h = (tables_h*)data;
+  h->closed = 1;
+  if (h->inflight == 0) tables_release(h);
+  tables_unref(h);
+}
+
+static void fin_codec(napi_env env, void* data, void* hint) {
+  (void)env;
+  (void)hint;
+  codec_unref((codec_h*)data);
+}
+
+static void fin_batch(napi_env env, void* data, void* hint) {
+  batch_h* h = (batch_h*)data;
+  (void)hint;
+  if (h->b) acs_codec_batch_free(h->b); /* before its codec */
+  if (h->codec_ref) napi_delete_reference(env, h->codec_ref);
+  if (h->codec) codec_unref(h->codec);
+  h->magic = 0;
+  free(h);
+}
+
+static void* get_ext(napi_env env, napi_value v, int magic) {
+  napi_valuetype t;
+  void* p = NULL;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_external) return NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) return NULL;
+  return *(int*)p == magic ? p : NULL;
+}
+
+static tables_h* get_tables(napi_env env, napi_value v) {
+  tables_h* h = (tables_h*)get_ext(env, v, H_TABLES);
+  if (!h) {
+    napi_throw_type_error(env, NULL, "expected a tables handle (compile())");
+    return NULL;
+  }
+  if (h->closed || !h->t) {
+    napi_throw_error(env, NULL, "tables handle already freed");
+    return NULL;
+  }
+  return h;
+}
+
+static codec_h* get_codec(napi_env env, napi_value v) {
+  codec_h* h = (codec_h*)get_ext(env, v, H_CODEC);
+  if (!h || !h->c) {
+    napi_throw_type_error(env, NULL, "expected a codec handle (codecCreate())");
+    return NULL;
+  }
+  return h;
+}
+
+/* ------------------------------------------------------------------ buffers */
 /* Bytes of a typed array / Buffer / ArrayBuffer (NULL for null / undefined). */
 static int get_bytes(napi_env env, napi_value v, void** data, size_t* len) {
   napi_valuetype t;
@@ -70,6 +191,33 @@ static int get_bytes(napi_env env, napi_value v, void** data, size_t* len) {
   return -1;
 }
 
+/* A JS string (UTF-8, malloc'd copy in *out) or bytes (borrowed).  *owned: free it. */
+static int get_text(napi_env env, napi_value v, char** out, size_t* len, int* owned) {
+  napi_valuetype t;
+  *out = NULL;
+  *len = 0;
+  *owned = 0;
+  if (napi_typeof(env, v, &t) != napi_ok) return -1;
+  if (t == napi_string) {
+    size_t n = 0;
+    if (napi_get_value_string_utf8(env, v, NULL, 0, &n) != napi_ok) return -1;
+    char* s = (char*)malloc(n + 1);
+    if (!s) return -1;
+    if (napi_get_value_string_utf8(env, v, s, n + 1, &n) != napi_ok) {
+      free(s);
+      return -1;
+    }
+    *out = s;
+    *len = n;
+    *owned = 1;
+    return 0;
+  }
+  void* p;
+  if (get_bytes(env, v, &p, len) || !p) return -1;
+  *out = (char*)p;
+  return 0;
+}
+
 static int prop_bytes(napi_env env, napi_value obj, const char* key, void** data, size_t* len) {
   napi_value v;
   if (napi_get_named_property(env, obj, key, &v) != napi_ok) return -1;
@@ -86,47 +234,100 @@ static int prop_u32(napi_env env, napi_value obj, const char* key, uint32_t* out
   return napi_get_value_uint32(env, v, out) == napi_ok ? 0 : -1;
 }
 
-/* JS batch object -> acs_req_batch (pointers into the JS buffers; caller keeps them alive). */
-static int read_batch(napi_env env, napi_value obj, acs_req_batch* b) {
-  size_t len;
+/* one typed-array field of a plain batch object, required to hold at least `need` bytes */
+static int field(napi_env env, napi_value obj, const char* key, size_t need, int required, const void** out,
+                 size_t* len_out, const char** bad) {
   void* p;
-  memset(b, 0, sizeof *b);
-  if (prop_u32(env, obj, "n", &b->n)) return -1;
-  if (prop_bytes(env, obj, "hdr", &p, &len)) return -1;
-  b->hdr = p;
-  if (prop_bytes(env, obj, "res", &p, &len)) return -1;
-  b->res = p;
-  if (prop_bytes(env, obj, "subj", &p, &len)) return -1;
-  b->subj = p;
-  if (prop_bytes(env, obj, "act", &p, &len)) return -1;
-  b->act = p;
-  if (prop_bytes(env, obj, "roles", &p, &len)) return -1;
-  b->roles = (const uint32_t*)p;
-  if (prop_bytes(env, obj, "arena", &p, &len)) return -1;
-  b->arena = (const uint32_t*)p;
-  b->arena_words = len / 4;
-  if (prop_bytes(env, obj, "rx", &p, &len)) return -1;
-  b->rx = (const uint8_t*)p;
-  if (prop_u32(env, obj, "rxCols", &b->rx_cols) || prop_u32(env, obj, "rxRows", &b->rx_rows)) return -1;
-  if (prop_bytes(env, obj, "cand", &p, &len)) return -1;
-  b->cand = (const uint32_t*)p;
-  if (prop_u32(env, obj, "candWords", &b->cand_words) || prop_u32(env, obj, "candWp", &b->cand_wp) ||
-      prop_u32(env, obj, "candWr", &b->cand_wr) || prop_u32(env, obj, "candRows", &b->cand_rows))
+  size_t len;
+  if (prop_bytes(env, obj, key, &p, &len)) {
+    *bad = key;
     return -1;
-  /* optional role factor (large stores): roleKey [n] u32, roleRowsBits, roleRows */
-  if (prop_bytes(env, obj, "roleKey", &p, &len)) return -1;
-  b->role_key = (const uint32_t*)p;
-  if (prop_bytes(env, obj, "roleRowsBits", &p, &len)) return -1;
-  b->role_rows_bits = (const uint32_t*)p;
-  if (prop_u32(env, obj, "roleRows", &b->role_rows)) return -1;
-  if (!b->role_key) b->role_rows = 0;
+  }
+  if ((required && need && !p) || len < need) {
+    *bad = key;
+    return -1;
+  }
+  *out = p;
+  if (len_out) *len_out = len;
   return 0;
 }
 
-static acs_tables* get_handle(napi_env env, napi_value v) {
-  void* h = NULL;
-  if (napi_get_value_external(env, v, &h) != napi_ok) return NULL;
-  return (acs_tables*)h;
+/* JS batch (encode() handle or plain object) -> acs_req_batch with every buffer checked
+ * against the sizes its counts imply (pointers into JS buffers; the caller keeps them alive). */
+static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
+  memset(b, 0, sizeof *b);
+  batch_h* bh = (batch_h*)get_ext(env, v, H_BATCH);
+  if (bh) return acs_codec_batch_view(bh->b, b) == 0 ? 0 : -1;
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_object) return -1;
+  const char* bad = NULL;
+  size_t len = 0;
+  if (prop_u32(env, v, "n", &b->n)) return -1;
+  const size_t n = b->n;
+  const void* p;
+  if (prop_u32(env, v, "rxCols", &b->rx_cols) || prop_u32(env, v, "rxRows", &b->rx_rows) ||
+      prop_u32(env, v, "candWords", &b->cand_words) || prop_u32(env, v, "candWp", &b->cand_wp) ||
+      prop_u32(env, v, "candWr", &b->cand_wr) || prop_u32(env, v, "candRows", &b->cand_rows) ||
+      prop_u32(env, v, "roleRows", &b->role_rows))
+    return -1;
+  if (field(env, v, "hdr", n * HDR_B, n > 0, &b->hdr, NULL, &bad) ||
+      field(env, v, "res", n * QMAX * RES_B, n > 0, &b->res, NULL, &bad) ||
+      field(env, v, "subj", n * SMAX * PAIR_B, n > 0, &b->subj, NULL, &bad) ||
+      field(env, v, "act", n * AMAX * PAIR_B, n > 0, &b->act, NULL, &bad) ||
+      field(env, v, "roles", n * RMAX * 4, n > 0, &p, NULL, &bad))
+    goto fail;
+  b->roles = (const uint32_t*)p;
+  if (field(env, v, "arena", 0, 0, &p, &len, &bad)) goto fail;
+  b->arena = (const uint32_t*)p;
+  b->arena_words = len / 4;
+  if (n > 0 && (!p || len < 8)) {
+    bad = "arena";
+    goto fail;
+  }
+  if (field(env, v, "rx", (size_t)b->rx_cols * b->rx_rows, n > 0, &p, NULL, &bad)) goto fail;
+  b->rx = (const uint8_t*)p;
+  if (field(env, v, "cand", (size_t)b->cand_rows * b->cand_words * 4, 0, &p, &len, &bad)) goto fail;
+  b->cand = (const uint32_t*)p;
+  if (b->cand && (b->cand_wp > b->cand_words || b->cand_wr > b->cand_words)) {
+    bad = "candWp / candWr";
+    goto fail;
+  }
+  if (field(env, v, "roleKey", 0, 0, &p, &len, &bad)) goto fail;
+  b->role_key = (const uint32_t*)p;
+  if (b->role_key) {
+    if (len < n * 4) {
+      bad = "roleKey";
+      goto fail;
+    }
+    if (field(env, v, "roleRowsBits", (size_t)b->role_rows * b->cand_words * 4, 1, &p, NULL, &bad)) goto fail;
+    b->role_rows_bits = (const uint32_t*)p;
+  } else {
+    b->role_rows = 0;
+  }
+  /* per-request offsets the kernels follow */
+  {
+    const uint8_t* hdr = (const uint8_t*)b->hdr;
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t arena_off;
+      memcpy(&arena_off, hdr + i * HDR_B + 8, 4);
+      if ((size_t)arena_off + 2 > b->arena_words) {
+        bad = "hdr.arena_off";
+        goto fail;
+      }
+      if (hdr[i * HDR_B + 4] > QMAX || hdr[i * HDR_B + 5] > SMAX || hdr[i * HDR_B + 6] > AMAX ||
+          hdr[i * HDR_B + 7] > RMAX) {
+        bad = "hdr counts";
+        goto fail;
+      }
+    }
+  }
+  return 0;
+fail : {
+  char msg[160];
+  snprintf(msg, sizeof msg, "batch.%s is missing or shorter than its counts require", bad ? bad : "?");
+  napi_throw_range_error(env, NULL, msg);
+  return -2;
+}
 }
 
 static napi_value new_u8(napi_env env, size_t n, void** data) {
@@ -143,7 +344,46 @@ static napi_value new_u32(napi_env env, size_t n, void** data) {
   return arr;
 }
 
-/* ------------------------------------------------------------------ compile / free */
+static int batch_arg(napi_env env, napi_value v, acs_req_batch* b, const char* usage) {
+  const int rc = read_batch(env, v, b);
+  if (rc == -1) napi_throw_type_error(env, NULL, usage);
+  return rc;
+}
+
+/* ------------------------------------------------------------------ store compile */
+static napi_value js_compile_store(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  char* s[3] = {NULL, NULL, NULL};
+  size_t n[3] = {0, 0, 0};
+  int own[3] = {0, 0, 0};
+  int ok = argc == 3;
+  for (int k = 0; k < 3 && ok; ++k) ok = get_text(env, argv[k], &s[k], &n[k], &own[k]) == 0;
+  napi_value ret = NULL;
+  if (!ok) {
+    napi_throw_type_error(env, NULL, "compileStore(storeJson, urnsJson, casJson)");
+  } else {
+    void* blob = NULL;
+    size_t len = 0;
+    if (acs_store_compile(s[0], n[0], s[1], n[1], s[2], n[2], &blob, &len) != 0) {
+      throw_acs(env, "acs_store_compile");
+    } else {
+      void* d;
+      out = new_u8(env, len, &d);
+      if (out) {
+        memcpy(d, blob, len);
+        ret = out;
+      }
+      acs_blob_free(blob);
+    }
+  }
+  for (int k = 0; k < 3; ++k)
+    if (own[k]) free(s[k]);
+  return ret;
+}
+
+/* ------------------------------------------------------------------ tables */
 static napi_value js_compile(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2], out;
@@ -158,7 +398,16 @@ static napi_value js_compile(napi_env env, napi_callback_info info) {
   if (argc > 1) CHECK(env, napi_get_value_int32(env, argv[1], &device));
   acs_tables* t = acs_compile(blob, len, device);
   if (!t) return throw_acs(env, "acs_compile");
-  CHECK(env, napi_create_external(env, t, NULL, NULL, &out));
+  tables_h* h = (tables_h*)calloc(1, sizeof *h);
+  if (!h) {
+    acs_free(t);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  h->magic = H_TABLES;
+  h->t = t;
+  h->refs = 1;
+  CHECK(env, napi_create_external(env, h, fin_tables, NULL, &out));
   return out;
 }
 
@@ -166,44 +415,67 @@ static napi_value js_free(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  if (argc > 0) acs_free(get_handle(env, argv[0]));
+  tables_h* h = argc > 0 ? (tables_h*)get_ext(env, argv[0], H_TABLES) : NULL;
+  if (!h) {
+    napi_throw_type_error(env, NULL, "free(tables)");
+    return NULL;
+  }
+  if (!h->closed) {
+    h->closed = 1;
+    if (h->inflight == 0) tables_release(h);  /* else: the last completing work item releases */
+  }
   return NULL;
 }
 
-/* ------------------------------------------------------------------ isAllowed (sync) */
 static napi_value js_is_allowed(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   acs_req_batch b;
   void* out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  acs_tables* t = argc == 2 ? get_handle(env, argv[0]) : NULL;
-  if (!t || read_batch(env, argv[1], &b)) {
-    napi_throw_type_error(env, NULL, "isAllowed(handle, batch)");
+  if (argc != 2) {
+    napi_throw_type_error(env, NULL, "isAllowed(tables, batch)");
     return NULL;
   }
+  /* the batch first: its checks need no device */
+  if (batch_arg(env, argv[1], &b, "isAllowed(tables, batch)")) return NULL;
+  tables_h* h = get_tables(env, argv[0]);
+  if (!h) return NULL;
   napi_value arr = new_u8(env, (size_t)b.n * sizeof(acs_decision), &out);
   if (!arr) return NULL;
-  if (acs_is_allowed(t, &b, (acs_decision*)out) != 0) return throw_acs(env, "acs_is_allowed");
+  if (acs_is_allowed(h->t, &b, (acs_decision*)out) != 0) return throw_acs(env, "acs_is_allowed");
   return arr;
 }
 
-/* ------------------------------------------------------------------ isAllowed (async) */
+/* ------------------------------------------------------------------ async work */
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
-  napi_ref keep_batch, keep_out;
-  acs_tables* t;
+  napi_ref keep_tables, keep_batch, keep_out, keep_codec;
+  tables_h* th;
+  codec_h* ch;
   acs_req_batch b;
   acs_decision* out;
+  /* decideAsync: encode on the pool too */
+  char* text;
+  size_t text_len;
+  int text_owned;
+  int threads;
+  acs_codec_batch* enc;
   int rc;
-  char err[256];
+  char err[512];
 } async_req;
+
+static void work_done_tables(async_req* r) {
+  r->th->inflight--;
+  if (r->th->closed && r->th->inflight == 0) tables_release(r->th);
+  tables_unref(r->th);
+}
 
 static void exec_is_allowed(napi_env env, void* data) {
   (void)env;
   async_req* r = (async_req*)data;
-  r->rc = acs_is_allowed(r->t, &r->b, r->out);
+  r->rc = acs_is_allowed(r->th->t, &r->b, r->out);
   if (r->rc) snprintf(r->err, sizeof r->err, "acs_is_allowed: %s", acs_last_error());
 }
 
@@ -211,6 +483,7 @@ static void done_is_allowed(napi_env env, napi_status status, void* data) {
   async_req* r = (async_req*)data;
   napi_value out;
   napi_get_reference_value(env, r->keep_out, &out);
+  work_done_tables(r);
   if (status == napi_ok && r->rc == 0) {
     napi_resolve_deferred(env, r->deferred, out);
   } else {
@@ -219,6 +492,7 @@ static void done_is_allowed(napi_env env, napi_status status, void* data) {
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, r->deferred, err);
   }
+  napi_delete_reference(env, r->keep_tables);
   napi_delete_reference(env, r->keep_batch);
   napi_delete_reference(env, r->keep_out);
   napi_delete_async_work(env, r->work);
@@ -230,15 +504,20 @@ static napi_value js_is_allowed_async(napi_env env, napi_callback_info info) {
   napi_value argv[2], promise, name;
   void* out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc != 2) {
+    napi_throw_type_error(env, NULL, "isAllowedAsync(tables, batch)");
+    return NULL;
+  }
+  tables_h* th = get_tables(env, argv[0]);
+  if (!th) return NULL;
   async_req* r = (async_req*)calloc(1, sizeof *r);
   if (!r) {
     napi_throw_error(env, NULL, "out of memory");
     return NULL;
   }
-  r->t = argc == 2 ? get_handle(env, argv[0]) : NULL;
-  if (!r->t || read_batch(env, argv[1], &r->b)) {
+  r->th = th;
+  if (batch_arg(env, argv[1], &r->b, "isAllowedAsync(tables, batch)")) {
     free(r);
-    napi_throw_type_error(env, NULL, "isAllowedAsync(handle, batch)");
     return NULL;
   }
   napi_value arr = new_u8(env, (size_t)r->b.n * sizeof(acs_decision), &out);
@@ -247,13 +526,288 @@ static napi_value js_is_allowed_async(napi_env env, napi_callback_info info) {
     return NULL;
   }
   r->out = (acs_decision*)out;
+  CHECK(env, napi_create_reference(env, argv[0], 1, &r->keep_tables));
   CHECK(env, napi_create_reference(env, argv[1], 1, &r->keep_batch));
   CHECK(env, napi_create_reference(env, arr, 1, &r->keep_out));
   CHECK(env, napi_create_promise(env, &r->deferred, &promise));
   CHECK(env, napi_create_string_utf8(env, "acs_is_allowed", NAPI_AUTO_LENGTH, &name));
   CHECK(env, napi_create_async_work(env, NULL, name, exec_is_allowed, done_is_allowed, r, &r->work));
+  th->inflight++;
+  th->refs++;
   CHECK(env, napi_queue_async_work(env, r->work));
   return promise;
+}
+
+/* decideAsync: JSON text -> acs_codec_encode -> acs_is_allowed, all on the libuv pool */
+static void exec_decide(napi_env env, void* data) {
+  (void)env;
+  async_req* r = (async_req*)data;
+  r->enc = acs_codec_encode(r->ch->c, r->text, r->text_len, r->threads);
+  if (!r->enc) {
+    r->rc = -1;
+    snprintf(r->err, sizeof r->err, "%s", acs_last_error());
+    return;
+  }
+  if (acs_codec_batch_view(r->enc, &r->b) != 0) {
+    r->rc = -1;
+    snprintf(r->err, sizeof r->err, "%s", acs_last_error());
+    return;
+  }
+  r->out = (acs_decision*)malloc((size_t)r->b.n * sizeof(acs_decision) + 1);
+  if (!r->out) {
+    r->rc = -1;
+    snprintf(r->err, sizeof r->err, "out of memory");
+    return;
+  }
+  r->rc = acs_is_allowed(r->th->t, &r->b, r->out);
+  if (r->rc) snprintf(r->err, sizeof r->err, "acs_is_allowed: %s", acs_last_error());
+}
+
+static napi_value host_map(napi_env env, acs_codec_batch* b, uint32_t n) {
+  napi_value host, v;
+  if (napi_create_object(env, &host) != napi_ok) return NULL;
+  acs_req_batch view;
+  if (acs_codec_batch_view(b, &view) != 0) return host;
+  const uint8_t* hdr = (const uint8_t*)view.hdr;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t flags;
+    memcpy(&flags, hdr + (size_t)i * HDR_B, 4);
+    if (!(flags & ACS_RQ_HOST)) continue;
+    const char* why = acs_codec_batch_reason(b, i);
+    char key[16];
+    snprintf(key, sizeof key, "%u", i);
+    napi_create_string_utf8(env, why ? why : "host path", NAPI_AUTO_LENGTH, &v);
+    napi_set_named_property(env, host, key, v);
+  }
+  return host;
+}
+
+static void done_decide(napi_env env, napi_status status, void* data) {
+  async_req* r = (async_req*)data;
+  work_done_tables(r);
+  if (status == napi_ok && r->rc == 0) {
+    napi_value res, rec;
+    void* d;
+    napi_create_object(env, &res);
+    rec = new_u8(env, (size_t)r->b.n * sizeof(acs_decision), &d);
+    if (rec) memcpy(d, r->out, (size_t)r->b.n * sizeof(acs_decision));
+    napi_set_named_property(env, res, "records", rec);
+    napi_set_named_property(env, res, "host", host_map(env, r->enc, r->b.n));
+    napi_resolve_deferred(env, r->deferred, res);
+  } else {
+    napi_value msg, err;
+    napi_create_string_utf8(env, r->rc ? r->err : "async work cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, r->deferred, err);
+  }
+  if (r->enc) acs_codec_batch_free(r->enc);
+  codec_unref(r->ch);
+  free(r->out);
+  if (r->text_owned) free(r->text);
+  napi_delete_reference(env, r->keep_tables);
+  napi_delete_reference(env, r->keep_codec);
+  if (r->keep_batch) napi_delete_reference(env, r->keep_batch);
+  napi_delete_async_work(env, r->work);
+  free(r);
+}
+
+static napi_value js_decide_async(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4], promise, name;
+  int32_t threads = 4;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 3) {
+    napi_throw_type_error(env, NULL, "decideAsync(tables, codec, json, threads?)");
+    return NULL;
+  }
+  tables_h* th = get_tables(env, argv[0]);
+  codec_h* ch = th ? get_codec(env, argv[1]) : NULL;
+  if (!th || !ch) return NULL;
+  if (argc > 3) CHECK(env, napi_get_value_int32(env, argv[3], &threads));
+  async_req* r = (async_req*)calloc(1, sizeof *r);
+  if (!r) {
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  r->th = th;
+  r->ch = ch;
+  r->threads = threads;
+  if (get_text(env, argv[2], &r->text, &r->text_len, &r->text_owned)) {
+    free(r);
+    napi_throw_type_error(env, NULL, "decideAsync: json must be a string or bytes");
+    return NULL;
+  }
+  if (!r->text_owned) CHECK(env, napi_create_reference(env, argv[2], 1, &r->keep_batch));  /* borrowed bytes */
+  CHECK(env, napi_create_reference(env, argv[0], 1, &r->keep_tables));
+  CHECK(env, napi_create_reference(env, argv[1], 1, &r->keep_codec));
+  CHECK(env, napi_create_promise(env, &r->deferred, &promise));
+  CHECK(env, napi_create_string_utf8(env, "acs_decide", NAPI_AUTO_LENGTH, &name));
+  CHECK(env, napi_create_async_work(env, NULL, name, exec_decide, done_decide, r, &r->work));
+  th->inflight++;
+  th->refs++;
+  ch->refs++;
+  CHECK(env, napi_queue_async_work(env, r->work));
+  return promise;
+}
+
+/* ------------------------------------------------------------------ codec */
+static napi_value js_codec_create(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  void* blob;
+  size_t len;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 1 || get_bytes(env, argv[0], &blob, &len) || !blob) {
+    napi_throw_type_error(env, NULL, "codecCreate(blob: Uint8Array)");
+    return NULL;
+  }
+  acs_codec* c = acs_codec_create(blob, len);
+  if (!c) return throw_acs(env, "acs_codec_create");
+  codec_h* h = (codec_h*)calloc(1, sizeof *h);
+  if (!h) {
+    acs_codec_free(c);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  h->magic = H_CODEC;
+  h->c = c;
+  h->refs = 1;
+  CHECK(env, napi_create_external(env, h, fin_codec, NULL, &out));
+  return out;
+}
+
+static napi_value js_codec_set_scopes(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  codec_h* h = argc == 3 ? get_codec(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  char *k, *j;
+  size_t kn, jn;
+  int ko, jo;
+  if (get_text(env, argv[1], &k, &kn, &ko)) {
+    napi_throw_type_error(env, NULL, "codecSetSubjectScopes(codec, key: string, scopesJson)");
+    return NULL;
+  }
+  if (get_text(env, argv[2], &j, &jn, &jo)) {
+    if (ko) free(k);
+    napi_throw_type_error(env, NULL, "codecSetSubjectScopes(codec, key: string, scopesJson)");
+    return NULL;
+  }
+  const int rc = acs_codec_set_subject_scopes(h->c, k, kn, j, jn);
+  if (ko) free(k);
+  if (jo) free(j);
+  if (rc != 0) return throw_acs(env, "acs_codec_set_subject_scopes");
+  return NULL;
+}
+
+static napi_value js_codec_evict(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  codec_h* h = argc == 2 ? get_codec(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  char* k;
+  size_t kn;
+  int ko;
+  if (get_text(env, argv[1], &k, &kn, &ko)) {
+    napi_throw_type_error(env, NULL, "codecEvictSubject(codec, key: string)");
+    return NULL;
+  }
+  const int rc = acs_codec_evict_subject(h->c, k, kn);
+  if (ko) free(k);
+  CHECK(env, napi_get_boolean(env, rc == 1, &v));
+  return v;
+}
+
+static napi_value js_codec_ec_values(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  codec_h* h = argc == 1 ? get_codec(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  const char* j;
+  size_t n;
+  if (acs_codec_ec_values(h->c, &j, &n) != 0) return throw_acs(env, "acs_codec_ec_values");
+  CHECK(env, napi_create_string_utf8(env, j, n, &v));
+  return v;
+}
+
+static napi_value js_encode(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], out;
+  int32_t threads = 1;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  codec_h* h = argc >= 2 ? get_codec(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  if (argc > 2) CHECK(env, napi_get_value_int32(env, argv[2], &threads));
+  char* s;
+  size_t n;
+  int own;
+  if (get_text(env, argv[1], &s, &n, &own)) {
+    napi_throw_type_error(env, NULL, "encode(codec, json: string | Uint8Array, threads?)");
+    return NULL;
+  }
+  acs_codec_batch* b = acs_codec_encode(h->c, s, n, threads);
+  if (own) free(s);
+  if (!b) return throw_acs(env, "acs_codec_encode");
+  batch_h* bh = (batch_h*)calloc(1, sizeof *bh);
+  if (!bh) {
+    acs_codec_batch_free(b);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  bh->magic = H_BATCH;
+  bh->b = b;
+  bh->codec = h;
+  h->refs++;
+  CHECK(env, napi_create_reference(env, argv[0], 1, &bh->codec_ref));
+  CHECK(env, napi_create_external(env, bh, fin_batch, NULL, &out));
+  return out;
+}
+
+static napi_value js_batch_info(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], res, v;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  batch_h* bh = argc == 1 ? (batch_h*)get_ext(env, argv[0], H_BATCH) : NULL;
+  if (!bh) {
+    napi_throw_type_error(env, NULL, "batchInfo(batch)");
+    return NULL;
+  }
+  acs_req_batch view;
+  acs_codec_batch_view(bh->b, &view);
+  CHECK(env, napi_create_object(env, &res));
+  CHECK(env, napi_create_uint32(env, view.n, &v));
+  CHECK(env, napi_set_named_property(env, res, "n", v));
+  CHECK(env, napi_set_named_property(env, res, "host", host_map(env, bh->b, view.n)));
+  return res;
+}
+
+static napi_value js_batch_string(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], v;
+  uint32_t id;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  batch_h* bh = argc == 2 ? (batch_h*)get_ext(env, argv[0], H_BATCH) : NULL;
+  if (!bh || napi_get_value_uint32(env, argv[1], &id) != napi_ok) {
+    napi_throw_type_error(env, NULL, "batchString(batch, id)");
+    return NULL;
+  }
+  const char* s;
+  size_t n;
+  const int k = acs_codec_string(bh->b, id, &s, &n);
+  if (k == 0) {
+    CHECK(env, napi_get_undefined(env, &v));
+  } else if (k == 1) {
+    CHECK(env, napi_get_null(env, &v));
+  } else if (k == 2) {
+    CHECK(env, napi_create_string_utf8(env, s, n, &v));
+  } else {
+    napi_throw_range_error(env, NULL, "batchString: unknown id");
+    return NULL;
+  }
+  return v;
 }
 
 /* ------------------------------------------------------------------ whatIsAllowed */
@@ -263,18 +817,20 @@ static napi_value js_what_is_allowed(napi_env env, napi_callback_info info) {
   acs_req_batch b;
   void *bits, *obl, *obl_n, *out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  acs_tables* t = argc == 2 ? get_handle(env, argv[0]) : NULL;
-  if (!t || read_batch(env, argv[1], &b)) {
-    napi_throw_type_error(env, NULL, "whatIsAllowed(handle, batch)");
+  if (argc != 2) {
+    napi_throw_type_error(env, NULL, "whatIsAllowed(tables, batch)");
     return NULL;
   }
-  const size_t w = acs_wia_words_per_request(t);
+  if (batch_arg(env, argv[1], &b, "whatIsAllowed(tables, batch)")) return NULL;
+  tables_h* h = get_tables(env, argv[0]);
+  if (!h) return NULL;
+  const size_t w = acs_wia_words_per_request(h->t);
   napi_value a_bits = new_u32(env, (size_t)b.n * w, &bits);
   napi_value a_obl = new_u32(env, (size_t)b.n * ACS_OBL_MAX * 2, &obl);
   napi_value a_obl_n = new_u32(env, b.n, &obl_n);
   napi_value a_out = new_u8(env, (size_t)b.n * sizeof(acs_decision), &out);
   if (!a_bits || !a_obl || !a_obl_n || !a_out) return NULL;
-  if (acs_what_is_allowed(t, &b, (uint32_t*)bits, (uint32_t*)obl, (uint32_t*)obl_n, (acs_decision*)out) != 0)
+  if (acs_what_is_allowed(h->t, &b, (uint32_t*)bits, (uint32_t*)obl, (uint32_t*)obl_n, (acs_decision*)out) != 0)
     return throw_acs(env, "acs_what_is_allowed");
   CHECK(env, napi_create_object(env, &res));
   CHECK(env, napi_set_named_property(env, res, "bits", a_bits));
@@ -284,7 +840,7 @@ static napi_value js_what_is_allowed(napi_env env, napi_callback_info info) {
   return res;
 }
 
-/* whatIsAllowedObl(handle, batch, idx: Uint32Array, chunks, cap) -> {obl, oblN}: the
+/* whatIsAllowedObl(tables, batch, idx: Uint32Array, chunks, cap) -> {obl, oblN}: the
  * obligation-only pass (acs_what_is_allowed_obl) for requests whose whatIsAllowed record
  * carries ACS_OF_OBL_OVERFLOW; obl [chunks][m][cap][2], oblN [chunks][m]. */
 static napi_value js_what_is_allowed_obl(napi_env env, napi_callback_info info) {
@@ -295,18 +851,24 @@ static napi_value js_what_is_allowed_obl(napi_env env, napi_callback_info info) 
   size_t idx_len;
   uint32_t chunks = 0, cap = 0;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  acs_tables* t = argc == 5 ? get_handle(env, argv[0]) : NULL;
-  if (!t || read_batch(env, argv[1], &b) || get_bytes(env, argv[2], &idx, &idx_len) || idx_len % 4 ||
+  const char* usage = "whatIsAllowedObl(tables, batch, idx: Uint32Array, chunks 1..64, cap 1..2^20)";
+  if (argc != 5) {
+    napi_throw_type_error(env, NULL, usage);
+    return NULL;
+  }
+  tables_h* h = get_tables(env, argv[0]);
+  if (!h || batch_arg(env, argv[1], &b, usage)) return NULL;
+  if (get_bytes(env, argv[2], &idx, &idx_len) || idx_len % 4 ||
       napi_get_value_uint32(env, argv[3], &chunks) != napi_ok || napi_get_value_uint32(env, argv[4], &cap) != napi_ok ||
       chunks == 0 || chunks > 64 || cap == 0 || cap > (1u << 20)) {
-    napi_throw_type_error(env, NULL, "whatIsAllowedObl(handle, batch, idx: Uint32Array, chunks 1..64, cap 1..2^20)");
+    napi_throw_type_error(env, NULL, usage);
     return NULL;
   }
   const size_t m = idx_len / 4;
   napi_value a_obl = new_u32(env, m * chunks * (size_t)cap * 2, &obl);
   napi_value a_obl_n = new_u32(env, m * chunks, &obl_n);
   if (!a_obl || !a_obl_n) return NULL;
-  if (acs_what_is_allowed_obl(t, &b, (const uint32_t*)idx, m, chunks, cap, (uint32_t*)obl, (uint32_t*)obl_n) != 0)
+  if (acs_what_is_allowed_obl(h->t, &b, (const uint32_t*)idx, m, chunks, cap, (uint32_t*)obl, (uint32_t*)obl_n) != 0)
     return throw_acs(env, "acs_what_is_allowed_obl");
   CHECK(env, napi_create_object(env, &res));
   CHECK(env, napi_set_named_property(env, res, "obl", a_obl));
@@ -319,8 +881,9 @@ static napi_value js_words(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], v;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  acs_tables* t = argc ? get_handle(env, argv[0]) : NULL;
-  CHECK(env, napi_create_uint32(env, t ? acs_wia_words_per_request(t) : 0, &v));
+  tables_h* h = argc ? get_tables(env, argv[0]) : NULL;
+  if (!h) return NULL;
+  CHECK(env, napi_create_uint32(env, acs_wia_words_per_request(h->t), &v));
   return v;
 }
 
@@ -354,8 +917,17 @@ static napi_value js_last_error(napi_env env, napi_callback_info info) {
 
 static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
+      {"compileStore", NULL, js_compile_store, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},
       {"free", NULL, js_free, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codecCreate", NULL, js_codec_create, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codecSetSubjectScopes", NULL, js_codec_set_scopes, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codecEvictSubject", NULL, js_codec_evict, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codecEcValues", NULL, js_codec_ec_values, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"encode", NULL, js_encode, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"batchInfo", NULL, js_batch_info, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"batchString", NULL, js_batch_string, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"decideAsync", NULL, js_decide_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isAllowed", NULL, js_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isAllowedAsync", NULL, js_is_allowed_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"whatIsAllowed", NULL, js_what_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -1,0 +1,376 @@
+// gpuCodec.js — the JS side of the drop-in for a TypeScript access-control-srv host.
+//
+// GpuAccessController evaluates batches of the reference's isAllowed / whatIsAllowed requests
+// (src/core/accessController.ts:88-324, :326-427) on the MI355X through lib/acs_mi355x.node
+// (napi/acs_napi.c) and returns the reference's Response / ReverseQuery objects:
+//
+//   const { GpuAccessController } = require('.../napi/gpuCodec.js');
+//   const gpu = new GpuAccessController(accessController.policySets, urnsConfig, casConfig,
+//                                       { hostEvaluator: (op, req) => accessController[op](req) });
+//   const responses = await gpu.isAllowedBatch(requests);        // Response | Error per request
+//   const queries = await gpu.whatIsAllowedBatch(requests);      // ReverseQuery | Error
+//   gpu.refresh(accessController.policySets);                    // after a policy CRUD event
+//
+// The policySets Map is snapshotted (snapshotStore) and compiled natively (acs_store_compile,
+// byte-identical to acs_mi355x/compiler.py); requests go to the native codec as one JSON
+// text (acs_codec_encode on the libuv pool) and straight on to the kernels (decideAsync).
+// Requests the packed form cannot carry (a JS rule condition, a subject token to resolve, a
+// RegExp outside the precomputed subset) go to
+// `hostEvaluator` — normally the reference's own AccessController — or, without one, come
+// back as HostPathRequired errors.  Node >= 12: no optional chaining, no structuredClone.
+'use strict';
+
+const path = require('path');
+
+const addon = require(process.env.ACS_MI355X_ADDON ||
+  path.join(__dirname, '..', 'lib', 'acs_mi355x.node'));
+
+// csrc/acs_layout.h
+const DECISIONS = [undefined, undefined, 'PERMIT', 'DENY', 'NOT_APPLICABLE', 'INDETERMINATE', 'UNRECOGNIZED'];
+const OF_ERR = 0x01, OF_HOST_COND = 0x02, OF_HOST_REQ = 0x04, OF_NO_TARGET = 0x08, OF_OBL_OVERFLOW = 0x20;
+const ERR_KINDS = { 1: 'TypeError', 2: 'InvalidCombiningAlgorithm', 3: 'SyntaxError', 4: 'RegexHost' };
+const ERR_REGEX_HOST = 4;
+const REC_BYTES = 8;
+const OBL_MAX = 64; // ACS_OBL_MAX: (entity, mask) pairs per request in the whatIsAllowed log
+const OVERFLOW_CAP = 1024, OVERFLOW_CHUNKS = 8;
+
+class HostPathRequired extends Error {
+  constructor(reason, ruleIndex) {
+    super(reason);
+    this.name = 'HostPathRequired';
+    this.reason = reason;
+    this.ruleIndex = ruleIndex;
+  }
+}
+
+// The reference's promise would reject with this kind of error (TypeError from a null
+// policy / malformed target, errors.InvalidCombiningAlgorithm, RegExp SyntaxError).
+class GpuEvaluationError extends Error {
+  constructor(kind) {
+    super(kind);
+    this.name = kind;
+    this.kind = kind;
+  }
+}
+
+function mapValues(m) {
+  if (m instanceof Map) return Array.from(m.values());
+  return Array.isArray(m) ? m : [];
+}
+
+function without(o, drop) {
+  const out = {};
+  for (const k of Object.keys(o)) if (drop.indexOf(k) < 0 && o[k] !== undefined) out[k] = o[k];
+  return out;
+}
+
+// The policySets Map as the JSON text acs_store_compile reads: the Map's values in order,
+// each set's / policy's `combinables` the array of its Map's values (null entries kept).
+function snapshotStore(policySets) {
+  const sets = mapValues(policySets).map((ps) => {
+    if (!ps || typeof ps !== 'object') return null;
+    const s = without(ps, ['combinables', 'policies']);
+    s.combinables = mapValues(ps.combinables).map((p) => {
+      if (!p || typeof p !== 'object') return null;
+      const po = without(p, ['combinables']);
+      po.combinables = mapValues(p.combinables).map((r) => (r && typeof r === 'object' ? r : null));
+      return po;
+    });
+    return s;
+  });
+  return JSON.stringify(sets);
+}
+
+// The node order of the compiled image (acs_mi355x/compiler.py _compile_set/_assemble):
+// sets in Map order, their policies flattened (null entries keep a slot), then rules.
+function nodeIndex(policySets) {
+  const sets = [], pols = [], rules = [], setPols = [], polRules = [];
+  for (const ps of mapValues(policySets)) {
+    const p0 = pols.length;
+    for (const p of mapValues(ps && ps.combinables)) {
+      const r0 = rules.length;
+      pols.push(p || null);
+      if (p) for (const r of mapValues(p.combinables)) rules.push(r || null);
+      polRules.push([r0, rules.length]);
+    }
+    sets.push(ps);
+    setPols.push([p0, pols.length]);
+  }
+  return { sets, pols, rules, setPols, polRules };
+}
+
+function parseRequests(requests) {
+  if (Array.isArray(requests)) return requests;
+  return JSON.parse(typeof requests === 'string' ? requests : Buffer.from(requests).toString('utf8'));
+}
+
+const clone = (v) => (v === undefined || v === null || typeof v !== 'object' ? v : JSON.parse(JSON.stringify(v)));
+
+function pick(obj, keys, into) {
+  for (const k of keys) if (k in obj) into[k] = clone(obj[k]);
+  return into;
+}
+
+function ecDecoder(codec) {
+  const extra = JSON.parse(addon.codecEcValues(codec));
+  const table = [undefined, null, false, true].concat(extra);
+  return (code) => (code < table.length ? table[code] : undefined);
+}
+
+class GpuAccessController {
+  // urns: policies.options.urns (cfg/config.json:270-307) as an object or Map;
+  // combiningAlgorithms: policies.options.combiningAlgorithms (array of {urn, method}).
+  constructor(policySets, urns, combiningAlgorithms, options) {
+    const o = options || {};
+    this.device = o.device || 0;
+    this.threads = o.threads || 4;
+    this.hostEvaluator = o.hostEvaluator || null;
+    this.urns = urns instanceof Map ? Object.fromEntries(urns) : urns;
+    this.cas = combiningAlgorithms;
+    this.stats = { requests: 0, host: 0, compiles: 0 };
+    this.tables = null;
+    this.codec = null;
+    this.refresh(policySets);
+  }
+
+  // Recompile from the (mutated) policySets Map; the reference re-reads its Map on every
+  // request, so call this after each policy CRUD event (before the next batch).
+  refresh(policySets) {
+    const blob = addon.compileStore(snapshotStore(policySets), JSON.stringify(this.urns), JSON.stringify(this.cas));
+    const tables = addon.compile(blob, this.device);
+    const codec = addon.codecCreate(blob);
+    if (this.tables) addon.free(this.tables); // deferred past batches still in flight
+    this.tables = tables;
+    this.codec = codec;
+    this.ec = ecDecoder(codec);
+    this.index = nodeIndex(policySets);
+    this.scopes = this.scopes || new Map();
+    for (const [k, v] of this.scopes) addon.codecSetSubjectScopes(codec, k, v);
+    this.stats.compiles += 1;
+  }
+
+  // The per-subject HR-scope cache (createHRScope / evictHRScopes, accessController.ts:717-783):
+  // a request whose context.subject has "$hrs": key uses this forest.
+  setSubjectScopes(key, hierarchicalScopes) {
+    const text = typeof hierarchicalScopes === 'string' ? hierarchicalScopes : JSON.stringify(hierarchicalScopes);
+    addon.codecSetSubjectScopes(this.codec, key, text);
+    this.scopes.set(key, text);
+  }
+
+  evictSubject(key) {
+    this.scopes.delete(key);
+    return addon.codecEvictSubject(this.codec, key);
+  }
+
+  close() {
+    if (this.tables) addon.free(this.tables);
+    this.tables = null;
+    this.codec = null;
+  }
+
+  _host(op, request, err) {
+    this.stats.host += 1;
+    if (!this.hostEvaluator) return Promise.resolve(err);
+    return Promise.resolve().then(() => this.hostEvaluator(op, request)).catch((e) => e);
+  }
+
+  // record i of `rec` -> Response, or the error the reference would reject with
+  _response(rec, i, hostReason) {
+    const flags = rec[i * REC_BYTES + 2];
+    if (flags & OF_HOST_REQ) return new HostPathRequired(hostReason || 'request flagged for the host path');
+    const aux = rec[i * REC_BYTES + 4] | (rec[i * REC_BYTES + 5] << 8) | (rec[i * REC_BYTES + 6] << 16) |
+      (rec[i * REC_BYTES + 7] << 24);
+    if (flags & OF_HOST_COND) return new HostPathRequired('rule condition (JS eval)', aux >>> 0);
+    if (flags & OF_ERR) {
+      const err = rec[i * REC_BYTES + 3];
+      if (err === ERR_REGEX_HOST) return new HostPathRequired('entity RegExp outside the precomputed subset');
+      return new GpuEvaluationError(ERR_KINDS[err] || 'Error');
+    }
+    if (flags & OF_NO_TARGET) {
+      return { decision: 'DENY', evaluation_cacheable: false, obligations: [],
+               operation_status: { code: 400, message: 'Access request had no target. Skipping request' } };
+    }
+    return { decision: DECISIONS[rec[i * REC_BYTES]], obligations: [],
+             evaluation_cacheable: this.ec(rec[i * REC_BYTES + 1]),
+             operation_status: { code: 200, message: 'success' } };
+  }
+
+  // requests: an array of Request objects, or their JSON text.  Resolves to one entry per
+  // request: a Response, or an Error (per request, as the reference's promises would reject).
+  async isAllowedBatch(requests) {
+    const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
+    const r = await addon.decideAsync(this.tables, this.codec, text, this.threads);
+    const n = r.records.length / REC_BYTES;
+    this.stats.requests += n;
+    const out = new Array(n);
+    const pending = [];
+    let parsed = null;
+    for (let i = 0; i < n; ++i) {
+      const v = this._response(r.records, i, r.host[i]);
+      if (v instanceof HostPathRequired) {
+        if (parsed === null) parsed = parseRequests(requests);
+        pending.push(this._host('isAllowed', parsed[i], v).then((x) => { out[i] = x; }));
+      } else {
+        out[i] = v;
+      }
+    }
+    await Promise.all(pending);
+    return out;
+  }
+
+  async isAllowed(request) {
+    const r = (await this.isAllowedBatch([request]))[0];
+    if (r instanceof Error) throw r;
+    return r;
+  }
+
+  // maskedProperty push log -> obligations (find by entity value, else append;
+  // accessController.ts:599-613, 624-638)
+  _obligations(batch, log, k) {
+    const out = [];
+    const ent = this.urns.entity, masked = this.urns.maskedProperty;
+    for (let j = 0; j < k; ++j) {
+      const ev = addon.batchString(batch, log[2 * j]);
+      const mv = addon.batchString(batch, log[2 * j + 1]);
+      const entry = { id: masked, value: mv, attributes: [] };
+      let hit = null;
+      for (const m of out) if (m.value === ev) { hit = m; break; }
+      if (hit === null) out.push({ id: ent, value: ev, attributes: [entry] });
+      else hit.attributes.push(entry);
+    }
+    return out;
+  }
+
+  // Full maskedProperty logs of the requests whose 64-entry log overflowed: the
+  // obligation-only pass over 8 policy-set ranges with 1024-entry logs, then once more at the
+  // exact count for any range still truncated (INTEGRATION.md §4; native.resolve_overflow).
+  _resolveOverflow(batch, flagged) {
+    const logs = new Map();
+    const chunks = OVERFLOW_CHUNKS;
+    let idx = Uint32Array.from(flagged), cap = OVERFLOW_CAP;
+    while (idx.length) {
+      const r = addon.whatIsAllowedObl(this.tables, batch, idx, chunks, cap);
+      const m = idx.length, left = [];
+      let need = cap;
+      for (let j = 0; j < m; ++j) {
+        const parts = [];
+        let total = 0, truncated = false;
+        for (let c = 0; c < chunks; ++c) {
+          const n = r.oblN[c * m + j];
+          if (n > cap) {
+            truncated = true;
+            need = Math.max(need, n);
+            continue;
+          }
+          const base = (c * m + j) * cap * 2;
+          parts.push(r.obl.subarray(base, base + 2 * n));
+          total += n;
+        }
+        if (truncated) {
+          left.push(idx[j]);
+          continue;
+        }
+        const log = new Uint32Array(2 * total);
+        let at = 0;
+        for (const p of parts) {
+          log.set(p, at);
+          at += p.length;
+        }
+        logs.set(idx[j], log);
+      }
+      idx = Uint32Array.from(left);
+      cap = need;
+    }
+    return logs;
+  }
+
+  // inclusion bitset row -> the reference's PolicySetRQ list (accessController.ts:342-420)
+  _reverseQuery(bits, row, words, wp, wr) {
+    const ix = this.index;
+    const has = (sec, i) => (bits[row * words + sec + (i >>> 5)] >>> (i & 31)) & 1;
+    const policySets = [];
+    for (let s = 0; s < ix.sets.length; ++s) {
+      if (!has(0, s)) continue;
+      const ps = ix.sets[s];
+      const rq = pick(ps, ['id', 'target', 'effect'], { combining_algorithm: ps.combining_algorithm });
+      rq.policies = [];
+      for (let p = ix.setPols[s][0]; p < ix.setPols[s][1]; ++p) {
+        if (!has(wp, p)) continue;
+        const po = ix.pols[p];
+        const prq = pick(po, ['id', 'target', 'effect', 'evaluation_cacheable'],
+                         { combining_algorithm: po.combining_algorithm });
+        prq.rules = [];
+        prq.has_rules = !!po.combinables && mapValues(po.combinables).length > 0;
+        for (let r = ix.polRules[p][0]; r < ix.polRules[p][1]; ++r) {
+          if (!has(wr, r)) continue;
+          const ro = ix.rules[r];
+          prq.rules.push(pick(ro, ['id', 'target', 'effect', 'condition', 'evaluation_cacheable'],
+                              { context_query: clone(ro.context_query) }));
+        }
+        rq.policies.push(prq);
+      }
+      policySets.push(rq);
+    }
+    return policySets;
+  }
+
+  // Batch whatIsAllowed (encode + kernels on the calling thread; host-path requests then go
+  // to the host evaluator).  Resolves to one entry per request: a ReverseQuery or an Error.
+  async whatIsAllowedBatch(requests) {
+    const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
+    const batch = addon.encode(this.codec, text, this.threads);
+    const info = addon.batchInfo(batch);
+    const w = addon.whatIsAllowed(this.tables, batch);
+    const words = addon.wordsPerRequest(this.tables);
+    const ns = this.index.sets.length, np = this.index.pols.length;
+    const up4 = (x) => (x + 3) & ~3;
+    const wp = up4((ns + 31) >>> 5), wr = wp + up4((np + 31) >>> 5);
+    const flagged = [];
+    for (let i = 0; i < info.n; ++i) {
+      const f = w.out[i * REC_BYTES + 2];
+      if ((f & OF_OBL_OVERFLOW) && !(f & (OF_HOST_REQ | OF_ERR))) flagged.push(i);
+    }
+    const long = flagged.length ? this._resolveOverflow(batch, flagged) : new Map();
+    const out = new Array(info.n);
+    const pending = [];
+    let parsed = null;
+    for (let i = 0; i < info.n; ++i) {
+      const flags = w.out[i * REC_BYTES + 2] & (long.has(i) ? ~OF_OBL_OVERFLOW : 0xff);
+      let err = null;
+      if (flags & OF_HOST_REQ) err = new HostPathRequired(info.host[i] || 'request flagged for the host path');
+      else if (flags & OF_ERR) {
+        const e = w.out[i * REC_BYTES + 3];
+        err = e === ERR_REGEX_HOST ? new HostPathRequired('entity RegExp outside the precomputed subset')
+          : new GpuEvaluationError(ERR_KINDS[e] || 'Error');
+      } else if (flags & OF_OBL_OVERFLOW) err = new HostPathRequired('maskedProperty log overflow');
+      if (err instanceof HostPathRequired) {
+        if (parsed === null) parsed = parseRequests(requests);
+        const at = i;
+        pending.push(this._host('whatIsAllowed', parsed[i], err).then((x) => { out[at] = x; }));
+        continue;
+      }
+      if (err) {
+        out[i] = err;
+        continue;
+      }
+      const log = long.has(i) ? long.get(i)
+        : w.obl.subarray(i * 2 * OBL_MAX, i * 2 * OBL_MAX + 2 * Math.min(w.oblN[i], OBL_MAX));
+      out[i] = {
+        policy_sets: this._reverseQuery(w.bits, i, words, wp, wr),
+        obligations: this._obligations(batch, log, log.length / 2),
+        operation_status: { code: 200, message: 'success' },
+      };
+    }
+    this.stats.requests += info.n;
+    await Promise.all(pending);
+    return out;
+  }
+
+  async whatIsAllowed(request) {
+    const r = (await this.whatIsAllowedBatch([request]))[0];
+    if (r instanceof Error) throw r;
+    return r;
+  }
+}
+
+module.exports = { GpuAccessController, HostPathRequired, GpuEvaluationError, snapshotStore, nodeIndex, addon };

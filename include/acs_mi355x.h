@@ -206,6 +206,9 @@ acs_codec_batch* acs_codec_encode(acs_codec* c, const char* json, size_t len, in
 int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out);
 const char* acs_codec_batch_reason(const acs_codec_batch* b, uint32_t i);
 int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size_t* len);
+/* The evaluation_cacheable values of the store beyond codes 0..3 (undefined, null, false,
+ * true), as a JSON array: code k >= 4 is element k - 4 (acs_decision.ec). */
+int acs_codec_ec_values(const acs_codec* c, const char** json, size_t* len);
 /* out[0..5]: seconds parse+encode, regex matrix, candidate classes, total; HR cache hits, misses */
 int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n);
 void acs_codec_batch_free(acs_codec_batch* b);

@@ -31,7 +31,9 @@ def test_addon_loads_with_surface():
     r = subprocess.run([NODE, "-e", js, p], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     info = json.loads(r.stdout.splitlines()[0])
-    assert info["keys"] == sorted(["compile", "free", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
+    assert info["keys"] == sorted(["compileStore", "compile", "free", "codecCreate", "codecSetSubjectScopes",
+                                   "codecEvictSubject", "codecEcValues", "encode", "batchInfo", "batchString",
+                                   "decideAsync", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
                                    "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
     assert info["sizes"] == [64, 16, 16, 16, 8]
     assert "magic" in r.stdout.splitlines()[1]  # a bad image is rejected with acs_last_error's message
@@ -76,3 +78,31 @@ def test_node_batch_matches_c_abi(tmp_path):
     assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_bits.bin").read_bytes(), np.uint32),
                           bits.reshape(-1))
     assert np.array_equal(np.frombuffer(tmp_path.joinpath("wia_obl_n.bin").read_bytes(), np.uint32), obl_n)
+
+
+def test_addon_checks_batch_sizes():
+    """A plain-object batch whose arrays are shorter than n and its counts imply is refused
+    (RangeError naming the field) before anything reads it; handles are type-checked."""
+    p = _addon()
+    js = r"""
+const a = require(process.argv[1]);
+const n = 4, ok = () => ({n, hdr: new Uint8Array(16*n), res: new Uint8Array(16*16*n), subj: new Uint8Array(8*8*n),
+  act: new Uint8Array(8*4*n), roles: new Uint32Array(8*n), arena: new Uint32Array(8), rx: new Uint8Array(0)});
+const out = [];
+const tryit = (f) => { try { f(); out.push('ok'); } catch (e) { out.push(e.constructor.name + ':' + e.message); } };
+for (const k of ['hdr', 'res', 'subj', 'act', 'roles']) { const b = ok(); b[k] = b[k].subarray(0, b[k].length - 1); tryit(() => a.isAllowed(null, b)); }
+{ const b = ok(); b.rxCols = 3; b.rxRows = 2; tryit(() => a.isAllowed(null, b)); }
+{ const b = ok(); b.cand = new Uint32Array(10); b.candRows = 3; b.candWords = 4; tryit(() => a.whatIsAllowed(null, b)); }
+{ const b = ok(); const h = new Uint32Array(b.hdr.buffer); h[2] = 1000; tryit(() => a.isAllowed(null, b)); }
+{ const b = ok(); b.hdr[4] = 17; tryit(() => a.isAllowed(null, b)); }
+tryit(() => a.isAllowed(null, ok()));
+tryit(() => a.encode({}, '[]'));
+console.log(JSON.stringify(out));
+"""
+    r = subprocess.run([NODE, "-e", js, p], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    for k, msg in zip(["hdr", "res", "subj", "act", "roles", "rx", "cand", "hdr.arena_off", "hdr counts"], out):
+        assert msg.startswith("RangeError") and f"batch.{k} " in msg, (k, msg)
+    assert out[9].startswith("TypeError") and "tables handle" in out[9]
+    assert out[10].startswith("TypeError") and "codec handle" in out[10]

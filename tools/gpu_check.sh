@@ -28,28 +28,8 @@ for s in $STEPS; do
     quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
-    abtest) for v in ${VARIANTS:-scalar_tables}; do
-          ACS_MI355X_LIB=access-control-srv_amd/lib/variants/$v.so step "pytest_gpu_$v" 600 \
-            python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-        done ;;
-    ab) for v in ${VARIANTS:-scalar_tables}; do
-          step "bench_$v" 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pcie \
-            --lib access-control-srv_amd/lib/variants/$v.so
-        done ;;
-    ab3) for v in ${VARIANTS:-scalar_tables}; do
-          step "bench_c3_$v" 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie \
-            --lib access-control-srv_amd/lib/variants/$v.so
-        done ;;
     quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
-    ab5) for v in ${VARIANTS:-scalar_tables}; do
-          step "bench_c5_$v" 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie \
-            --lib access-control-srv_amd/lib/variants/$v.so
-        done ;;
     quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
-    ab4) for v in ${VARIANTS:-scalar_tables}; do
-          step "bench_c4_$v" 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie \
-            --lib access-control-srv_amd/lib/variants/$v.so
-        done ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
     c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
     c5shard) step bench_c5_rule_shard 1200 python bench.py --config c5 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
