@@ -24,7 +24,7 @@ ARCH = "gfx950"
 _HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h", "acs_json.h")] + \
     [os.path.join(ROOT, "include", "acs_mi355x.h")]
 # host-only C++ of the product library: the native request codec and its JSON reader
-_HOST_SRCS = [os.path.join(CSRC, f) for f in ("acs_codec.cpp", "acs_compiler.cpp", "acs_json.cpp")]
+_HOST_SRCS = [os.path.join(CSRC, f) for f in ("acs_codec.cpp", "acs_compiler.cpp", "acs_json.cpp", "acs_validate.cpp")]
 
 
 def _stale(out, srcs):

@@ -457,7 +457,17 @@ struct acs_tables {
   // host-buffer entry points (internal stream, events, workspace) may be called from
   // several host threads at once (e.g. the N-API addon's libuv pool): one at a time
   std::mutex mu;
+  uint32_t rx_rows_min = 0;  // regex-matrix rows the rule resource attributes read
 };
+
+// csrc/acs_validate.cpp
+extern "C" int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_min);
+extern "C" int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
+                                        uint32_t rx_rows_min);
+
+static int check_batch(const acs_tables* t, const acs_req_batch* b) {
+  return acs_internal_check_batch(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min);
+}
 
 extern "C" {
 
@@ -513,8 +523,11 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     fail("acs_compile: blob shorter than its header declares");
     return nullptr;
   }
+  uint32_t rx_rows_min = 0;
+  if (acs_internal_check_blob(blob, n_bytes, &rx_rows_min)) return nullptr;
   auto* t = new acs_tables();
   t->device = device;
+  t->rx_rows_min = rx_rows_min;
   const size_t alloc = total + 64;  // clamp window [base, base + total] for 64-B record loads
   if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
       hipMemcpy(t->dev, (const char*)blob + src, total, hipMemcpyHostToDevice) != hipSuccess ||
@@ -791,8 +804,9 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
 }  // namespace
 
 int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
-  if (!t || !b || !out) return fail("acs_is_allowed: null argument");
+  if (!t || !b || (b && b->n && !out)) return fail("acs_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;
@@ -810,8 +824,9 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
 
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl, uint32_t* obl_n,
                         acs_decision* out) {
-  if (!t || !b || !bits || !obl || !obl_n || !out) return fail("acs_what_is_allowed: null argument");
+  if (!t || !b || (b->n && (!bits || !obl || !obl_n || !out))) return fail("acs_what_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;
@@ -844,6 +859,7 @@ int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_
   if (m == 0) return 0;
   for (size_t k = 0; k < m; ++k)
     if (idx[k] >= b->n) return fail("acs_what_is_allowed_obl: request index outside the batch");
+  if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
   DevBatch D;

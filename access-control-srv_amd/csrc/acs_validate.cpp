@@ -1,0 +1,137 @@
+// acs_validate.cpp — host-side structural checks of what the kernels dereference.
+//
+// The kernels index the compiled tables and the request batch without bounds checks (every
+// record load is on the hot path).  A malformed image or batch handed to the host-buffer
+// entry points (acs_compile, acs_is_allowed, acs_what_is_allowed, acs_what_is_allowed_obl)
+// would turn into out-of-bounds device reads, so they are walked here first, once, on the
+// host copy: every child range, pool offset, arena offset and regex-matrix coordinate the
+// device code follows must land inside its buffer.  The *_device entry points take
+// device-resident batches (normally from acs_codec_encode, which writes them consistent)
+// and are not walked.
+#include <stdio.h>
+#include <string.h>
+
+#include <cstddef>
+
+#include "../../include/acs_mi355x.h"
+#include "acs_layout.h"
+
+using namespace acs;
+
+extern "C" void acs_internal_set_error(const char* msg);
+
+namespace {
+
+int bad(const char* what, size_t at) {
+  char msg[192];
+  snprintf(msg, sizeof msg, "malformed %s (at %zu)", what, at);
+  acs_internal_set_error(msg);
+  return -1;
+}
+
+size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+uint32_t words32(uint32_t n) { return (n + 31) >> 5; }
+
+}  // namespace
+
+extern "C" {
+
+// Image checks for acs_compile; *rx_rows_min = 1 + the largest regex-matrix row any rule
+// resource attribute reads (0: none).
+int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_min) {
+  acs_blob_header h;
+  memcpy(&h, blob, sizeof h);
+  const char* p = (const char*)blob + align16(sizeof h);
+  const NodeRec* sets = (const NodeRec*)p;
+  p += align16((size_t)h.n_sets * sizeof(NodeRec));
+  const NodeRec* pols = (const NodeRec*)p;
+  p += align16((size_t)h.n_pols * sizeof(NodeRec));
+  const NodeRec* rules = (const NodeRec*)p;
+  p += align16((size_t)h.n_rules * sizeof(NodeRec));
+  const RuleResAttr* rres = (const RuleResAttr*)p;
+  (void)n_bytes;  // the caller checked that every section lies inside the blob
+  auto node_ok = [&](const NodeRec& t) {
+    return (uint64_t)t.subj_off + t.subj_n <= h.n_pairs && (uint64_t)t.act_off + t.act_n <= h.n_pairs &&
+           (uint64_t)t.res_off + t.res_n <= h.n_rres && (uint64_t)t.acl_roles_off + t.acl_roles_n <= h.n_u32pool;
+  };
+  for (uint32_t s = 0; s < h.n_sets; ++s) {
+    const NodeRec t = sets[s];
+    if (!node_ok(t) || t.child_begin > t.child_end || t.child_end > h.n_pols) return bad("image: policy set", s);
+  }
+  for (uint32_t q = 0; q < h.n_pols; ++q) {
+    const NodeRec t = pols[q];
+    if (!node_ok(t) || t.child_begin > t.child_end || t.child_end > h.n_rules || t.fe < t.child_begin ||
+        t.fe > t.child_end)
+      return bad("image: policy", q);
+  }
+  for (uint32_t r = 0; r < h.n_rules; ++r)
+    if (!node_ok(rules[r])) return bad("image: rule", r);
+  uint32_t rows = 0;
+  for (uint32_t k = 0; k < h.n_rres; ++k)
+    if ((rres[k].kind & K_ENT_LOOSE) && (uint32_t)rres[k].row + 1 > rows) rows = (uint32_t)rres[k].row + 1;
+  *rx_rows_min = rows;
+  return 0;
+}
+
+// Batch checks for the host-buffer entry points.
+int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
+                             uint32_t rx_rows_min) {
+  const size_t n = b->n;
+  if (n == 0) return 0;
+  if (!b->hdr || !b->res || !b->subj || !b->act || !b->roles || !b->arena)
+    return bad("batch: null request buffer", 0);
+  if (rx_rows_min && (!b->rx || b->rx_rows < rx_rows_min)) return bad("batch: regex matrix rows", b->rx_rows);
+  if (b->cand) {
+    if (b->cand_wp < words32(n_sets) || b->cand_wr < b->cand_wp + words32(n_pols) ||
+        b->cand_words < b->cand_wr + words32(n_rules))
+      return bad("batch: candidate row layout", b->cand_words);
+    if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
+  }
+  const ReqHdr* hdr = (const ReqHdr*)b->hdr;
+  const ReqRes* res = (const ReqRes*)b->res;
+  const size_t W = b->arena_words;
+  for (size_t i = 0; i < n; ++i) {
+    const ReqHdr hd = hdr[i];
+    if (hd.nres > QMAX || hd.nsubj > SMAX || hd.nact > AMAX || hd.nroles > RMAX) return bad("batch: counts", i);
+    const size_t o = hd.arena_off;
+    if (o + 2 > W) return bad("batch: arena offset", i);
+    const uint32_t* ar = b->arena + o;
+    const size_t room = W - o;
+    const uint32_t c0 = ar[0], c1 = ar[1];
+    const uint32_t ng = c0 & 0xFF, nre = (c0 >> 8) & 0xFF, ns = (c0 >> 16) & 0xFF, nro = c0 >> 24;
+    const uint32_t nt = c1 & 0xFF, nh = (c1 >> 8) & 0xFF;
+    if (nro > MAX_ROOTS || nh > MAX_HRKEYS || ns > MAX_SLOTS) return bad("batch: arena header", i);
+    const size_t head = 2 + 3 * (size_t)ng + 2 * (size_t)nre + nro + nh + ns + 3 * (size_t)nt;
+    if (head > room) return bad("batch: arena header", i);
+    const uint32_t* slotoff = ar + 2 + 3 * ng + 2 * nre + nro + nh;
+    const uint32_t* tse = slotoff + ns;
+    for (uint32_t s = 0; s < ns; ++s) {  // [owners_empty, n_owners, owner...]
+      size_t at = slotoff[s];
+      if (at + 2 > room) return bad("batch: arena slot record", i);
+      const uint32_t no = ar[at + 1];
+      at += 2;
+      for (uint32_t k = 0; k < no; ++k) {  // [is_oe | n_attrs << 8, value, n_attrs x 3]
+        if (at + 2 > room) return bad("batch: arena owner record", i);
+        at += 2 + 3 * (size_t)(ar[at] >> 8);
+        if (at > room) return bad("batch: arena owner record", i);
+      }
+    }
+    for (uint32_t e = 0; e < nt; ++e) {  // (se, n_inst, inst_rel_off) -> n_inst x 2
+      const uint32_t ni = tse[3 * e + 1];
+      if (ni > 32 || (size_t)tse[3 * e + 2] + 2 * (size_t)ni > room) return bad("batch: arena instance list", i);
+    }
+    const uint32_t ent = (hd.flags >> RQ_ENT_SHIFT) & 7u;
+    const uint32_t e0 = ent >= 1 && ent <= 6 ? ent - 1 : (uint32_t)QMAX;  // the lone entity attr's slot
+    for (uint32_t j = 0; j < QMAX; ++j) {
+      if (j >= hd.nres && j != e0) continue;
+      const ReqRes q = res[(size_t)j * n + i];
+      if (rx_rows_min && ((q.kind & K_ENT_LOOSE) || j == e0) && q.col >= b->rx_cols)
+        return bad("batch: regex matrix column", i);
+      if ((q.slot_a != NONE8 && q.slot_a >= ns) || (q.slot_b != NONE8 && q.slot_b >= ns))
+        return bad("batch: context resource slot", i);
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"
