@@ -12,8 +12,10 @@ import pytest
 
 import host_core
 import randgen
+from diff_utils import controller_outcome, norm_rq, oracle_from_store, oracle_outcome, gpu_outcome
 from oracle.acs_oracle import DEFAULT_CAS, FULL_URNS
-from acs_mi355x import compiler, encoder, store as pstore, synth, layout as L
+from oracle.jsval import JSError, OracleUnsupported
+from acs_mi355x import compiler, encoder, results, store as pstore, synth, layout as L
 from acs_mi355x.controller import AccessController
 
 ID_FIELDS = ("role", "se", "last_prop_value")
@@ -116,6 +118,14 @@ def test_incremental_matches_fresh_compile(seed):
         fresh.policySets = pstore.populate({"policy_sets": []}) if not ctl.policySets else dict(ctl.policySets)
         want = fresh.isAllowed_batch(reqs)
         assert [repr(x) for x in got] == [repr(x) for x in want], (seed, step, op)
+        o = oracle_from_store(urns, ctl.policySets)  # and the mutated Map through the oracle
+        for i, req in enumerate(reqs):
+            g = controller_outcome(got[i])
+            if g[0] != "HOST":
+                try:
+                    assert g == oracle_outcome(o, req), (seed, step, op, i)
+                except OracleUnsupported:
+                    pass
 
 
 def test_incremental_recompiles_only_touched_sets():
@@ -178,6 +188,7 @@ def test_incremental_gpu(seed):
     ctl = AccessController(opts)
     ctl.policySets = base
     ctl.isAllowed_batch(reqs[:1])
+    compared = 0
     for step in range(5):
         op = _mutate(rng, ctl, donors)
         try:
@@ -190,4 +201,27 @@ def test_incremental_gpu(seed):
         assert [repr(x) for x in got] == [repr(x) for x in fresh.isAllowed_batch(reqs)], (seed, step, op)
         assert [repr(x) for x in got_w] == [repr(x) for x in fresh.whatIsAllowed_batch(reqs)], (seed, step, op)
         fresh.close()
+        # the mutated Map, loaded into the oracle, decides every request the same way
+        o = oracle_from_store(urns, ctl.policySets)
+        for i, req in enumerate(reqs):
+            g = controller_outcome(got[i])
+            if g[0] == "HOST":
+                continue
+            try:
+                assert g == oracle_outcome(o, req), (seed, step, op, i)
+            except OracleUnsupported:
+                continue
+            try:
+                want = ("OK", norm_rq(o.what_is_allowed(req)))
+            except JSError as e:
+                want = ("ERR", e.kind)
+            except OracleUnsupported:
+                continue
+            w = got_w[i]
+            if isinstance(w, results.HostPathRequired):
+                continue
+            gw = ("ERR", w.kind) if isinstance(w, results.EvaluationError) else ("OK", norm_rq(w))
+            assert gw == want, (seed, step, op, i)
+            compared += 1
     ctl.close()
+    assert compared > 0 or not reqs
