@@ -148,12 +148,37 @@ struct Filter {
   }
 };
 
+// The filter forms the GPU kernels are instantiated with (the evaluation core takes any
+// type with wp, wr and word(w)); each keeps only the state its form reads, so the wave's
+// long-lived scalar state stays small.
+// FilterAll: the batch carries no candidate rows — every node is a candidate.
+struct FilterAll {
+  uint32_t wp, wr;
+  ACS_FN uint32_t word(uint32_t) const { return ~0u; }
+};
+
+// FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
+// kernel before any lane diverges (all ones for a wave holding an unfiltered request).
+struct FilterLds {
+  const uint32_t* lds;
+  uint32_t wp, wr;
+  ACS_FN uint32_t word(uint32_t w) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    return wave_uniform(((lds_u32*)lds)[w]);
+#else
+    return lds[w];
+#endif
+  }
+};
+
 // Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
 // lane that is still inside the loop holds the same iterator state.
+template <class FL>
 struct CandRange {
-  const Filter& F;
+  const FL& F;
   uint32_t off, base, e, bits;
-  ACS_FN CandRange(const Filter& f, uint32_t section_off, uint32_t b, uint32_t e_)
+  ACS_FN CandRange(const FL& f, uint32_t section_off, uint32_t b, uint32_t e_)
       : F(f), off(section_off), base(b & ~31u), e(e_), bits(0) {
     if (b < e) bits = F.word(off + (b >> 5)) & (~0u << (b & 31));
   }
@@ -689,19 +714,19 @@ ACS_FN Decision make_err(tri e, uint32_t at = 0) {
   return d;
 }
 
-template <class RQ>
-ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F);
+template <class RQ, class FL>
+ACS_FN Decision is_allowed_body(const RQ& R, const FL& F);
 
-template <class RQ>
-ACS_FN Decision is_allowed_t(const RQ& R, const Filter& F) {
+template <class RQ, class FL>
+ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
   PROF_T0(t_total);
   const Decision d = is_allowed_body(R, F);
   PROF_ADD(PH_TOTAL, t_total);
   return d;
 }
 
-template <class RQ>
-ACS_FN Decision is_allowed_body(const RQ& R, const Filter& F) {
+template <class RQ, class FL>
+ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   const Tables& T = R.T;
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
@@ -937,8 +962,8 @@ struct ChunkSink {
 
 // [s_begin, s_end): the policy sets evaluated (whatIsAllowed keeps no state across sets but the
 // push log, so a request's log is the concatenation of the logs of consecutive set ranges).
-template <class RQ, class Sink>
-ACS_FN Decision what_is_allowed_t(const RQ& R, const Filter& F, const BitsLayout& BL, Sink& bits, OblLog& obl,
+template <class RQ, class Sink, class FL>
+ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL, Sink& bits, OblLog& obl,
                                   uint32_t s_begin = 0, uint32_t s_end = NONE32) {
   const Tables& T = R.T;
   Decision out{};

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -265,6 +266,53 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   return F;
 }
 
+// The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
+// W-word LDS region, all ones when the wave holds an unfiltered request.
+__device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
+  FilterLds F{lds, B.cand_wp, B.cand_wr};
+  const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
+  const uint32_t nroles = B.role_key ? B.role_rows : 0u;
+  const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
+  bool all = false;
+  for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
+  uint64_t pending = __ballot(valid);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader), c = k >> 16, r = k & 0xFFFFu;
+    if (c == PCOL_ALL || c >= B.cand_rows) {
+      all = true;
+      break;
+    }
+    const uint32_t* row = B.cand + (size_t)c * W;
+    const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : nullptr;
+    for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
+    pending &= ~__ballot(valid && key == k);
+  }
+  if (all)
+    for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
+  return F;
+}
+
+__device__ inline FilterAll wave_filter_all(const Batch& B) { return FilterAll{B.cand_wp, B.cand_wr}; }
+
+// One maker per filter form, selected by the kernel's template argument.
+template <class FL> struct FilterMaker;
+template <> struct FilterMaker<Filter> {
+  static __device__ Filter make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds, uint32_t* list) {
+    return wave_filter(B, valid, cls, rk, lds, list);
+  }
+};
+template <> struct FilterMaker<FilterLds> {
+  static __device__ FilterLds make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds, uint32_t*) {
+    return wave_filter_lds(B, valid, cls, rk, lds);
+  }
+};
+template <> struct FilterMaker<FilterAll> {
+  static __device__ FilterAll make(const Batch& B, bool, uint32_t, uint32_t, uint32_t*, uint32_t*) {
+    return wave_filter_all(B);
+  }
+};
+
 extern __shared__ uint32_t acs_dyn_lds[];
 
 __device__ inline uint32_t lds_wave_words(const Batch& B) {
@@ -293,8 +341,9 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 #ifndef ACS_K1_WAVES_PER_EU
 #define ACS_K1_WAVES_PER_EU 4  // measured: 4 waves/SIMD (VGPR <= 128) beats 3 (+12% c2, +13% c3), 5+ spill
 #endif
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
-                                                           Decision* __restrict__ out) {
+template <class FL>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
+    Tables T, Batch B, const uint32_t* __restrict__ perm, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
@@ -304,8 +353,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
-  const Filter F = wave_filter(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu, wave_lds_row(B),
-                               wave_lds_list(B));
+  const FL F = FilterMaker<FL>::make(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                                     wave_lds_row(B), wave_lds_list(B));
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
@@ -339,6 +388,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
+template <class FL>
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                                 BitsLayout BL, uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
@@ -351,8 +401,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                               wave_lds_row(B), wave_lds_list(B));
+  const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                                     wave_lds_row(B), wave_lds_list(B));
   if (!in) return;
   ChunkSink sink(bits + (size_t)i * BL.words, BL);
   OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
@@ -379,6 +429,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
 // obl[c][j] / obl_n[c][j]: range c's log and total push count (> cap: re-run with that
 // cap); a request's log is the concatenation over c.  An index outside the batch writes
 // 0xFFFFFFFF and reads nothing.
+template <class FL>
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Batch B, const uint32_t* __restrict__ idx,
                                                                     uint32_t m, uint32_t chunks, uint32_t cap,
                                                                     uint32_t* __restrict__ obl,
@@ -396,8 +447,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
   ReqHdr h{};
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
-  const Filter F = wave_filter(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                               wave_lds_row(B), wave_lds_list(B));
+  const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                                     wave_lds_row(B), wave_lds_list(B));
   if (!live) return;
   if (!in) {
     obl_n[k] = 0xFFFFFFFFu;
@@ -435,6 +486,28 @@ size_t filter_lds_bytes(const Batch& B) {
   if (!B.cand) return 0;
   return (size_t)(BLOCK / 64) * (B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_PREFIX_WORDS + LDS_LIST_WORDS) * 4;
 }
+
+// Which filter form a batch's kernels are instantiated with.  ACS_FILTER_GENERAL=1 forces the
+// general form everywhere (A/B runs of the specialisation).
+enum class FilterForm { All, Lds, General };
+FilterForm filter_form(const Batch& B) {
+  static const bool general = [] {
+    const char* e = getenv("ACS_FILTER_GENERAL");
+    return e && *e == '1';
+  }();
+  if (general) return FilterForm::General;
+  if (!B.cand) return FilterForm::All;
+  return B.cand_words <= LDS_FILTER_WORDS ? FilterForm::Lds : FilterForm::General;
+}
+
+#define ACS_LAUNCH_FILTERED(kernel, grid, lds, stream, form, ...)                                       \
+  do {                                                                                                  \
+    switch (form) {                                                                                     \
+      case FilterForm::All: hipLaunchKernelGGL(kernel<FilterAll>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+      case FilterForm::Lds: hipLaunchKernelGGL(kernel<FilterLds>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+      default: hipLaunchKernelGGL(kernel<Filter>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+    }                                                                                                   \
+  } while (0)
 
 }  // namespace
 
@@ -674,7 +747,7 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  hipLaunchKernelGGL(is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, (Decision*)out);
+  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
@@ -708,8 +781,8 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  hipLaunchKernelGGL(what_is_allowed_kernel, grid, dim3(BLOCK), filter_lds_bytes(B), s, t->view, B, perm, BL, bits,
-                     obl, obl_n, (Decision*)out);
+  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, BL, bits,
+                      obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
@@ -729,8 +802,8 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const 
   if (m == 0 || b->n == 0) return 0;
   Batch B = to_batch(b);
   const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
-  hipLaunchKernelGGL(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), dim3(BLOCK),
-                     filter_lds_bytes(B), (hipStream_t)stream, t->view, B, idx, (uint32_t)m, chunks, cap, obl, obl_n);
+  ACS_LAUNCH_FILTERED(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), filter_lds_bytes(B),
+                      (hipStream_t)stream, filter_form(B), t->view, B, idx, (uint32_t)m, chunks, cap, obl, obl_n);
   HIP_OK(hipGetLastError());
   return 0;
 }

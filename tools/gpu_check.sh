@@ -29,6 +29,17 @@ for s in $STEPS; do
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
+    ab) for cfg in ${AB_CONFIGS:-c2 c3}; do
+          st=20; [ "$cfg" = c3 ] && st=5
+          for rep in 1 2; do
+            step "ab_${cfg}_product_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
+            step "ab_${cfg}_general_$rep" 900 env ACS_FILTER_GENERAL=1 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
+            for v in ${VARIANTS:-}; do
+              step "ab_${cfg}_${v}_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 \
+                --lib access-control-srv_amd/lib/variants/$v.so
+            done
+          done
+        done ;;
     quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
     c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
