@@ -21,9 +21,23 @@ AND of the two node filters; a set is kept only if one of its policies is.
 visited (the compiler's ``pe_at`` / ``fe`` prefixes), so the kernel may iterate
 only the class's candidates, in table order.
 
-Layout: ``cand[class][W]`` u32 words, W = ws + wp + wr (set, policy, rule
-sections).  The class id sits in the request header's flags (``RQ_PCOL_SHIFT``);
-``PCOL_ALL`` means "evaluate every node" (several distinct entity columns).
+Useful sections (isAllowed only).  Most candidate sets and policies cannot change an
+isAllowed result: a policy contributes only when one of its rules can match (a candidate
+rule), when it is an effect-only policy (no rules, truthy effect: accessController.ts:
+159-163), or when its own target evaluation can throw (a RegExp cell that throws or needs
+the host for the class's entity column; a subjects list, whose checkHierarchicalScope can
+throw; a target-bearing policy without an entity filter).  A set contributes only through
+such a policy, or by throwing in loop 2a (a null policy).  Visiting anything else leaves
+the decision, evaluation_cacheable and the error state exactly as they were, so K1 walks
+the *useful* sets, scans loop 2a over the candidate policies (they decide `exact` and
+`policyEffect`) and walks loop 2b over the useful policies only.  whatIsAllowed keeps the
+candidate sections (its obligations are pushed by any matching target).
+
+Layout: ``cand[class][W]`` u32 words, sections in this order: candidate sets (ws words),
+candidate policies (wp), useful sets (ws), useful policies (wp), candidate rules (wr);
+W = 2 ws + 2 wp + wr.  The class id sits in the request header's flags
+(``RQ_PCOL_SHIFT``); ``PCOL_ALL`` means "evaluate every node" (several distinct entity
+columns).
 """
 from __future__ import annotations
 
@@ -43,12 +57,77 @@ _ROLE_ROW_BYTES = 256 << 20  # role-factor rows per batch
 FORCE_LEVEL = None  # tests: pin the class key level (and with it the role factor)
 
 
+_THROW_LIKE = L.RX_THROW_TYPE | L.RX_THROW_SYNTAX | L.RX_HOST
+
+
 def words(n):
     return (n + 31) // 32
 
 
 def section_words(cs):
     return words(cs.n_sets), words(cs.n_pols), words(cs.n_rules)
+
+
+def row_layout(cs):
+    """Word offsets of a class row's sections: (wp, wsu, wpu, wr, W) — candidate policies,
+    useful sets, useful policies, candidate rules, row length (candidate sets start at 0)."""
+    ws, wp, wr = section_words(cs)
+    return ws, ws + wp, 2 * ws + wp, 2 * ws + 2 * wp, 2 * ws + 2 * wp + wr
+
+
+def _assemble(s, p, us, up, r, cs):
+    ws, wp, wr = section_words(cs)
+    return np.concatenate([_pack(s, ws), _pack(p, wp), _pack(us, ws), _pack(up, wp), _pack(r, wr)], axis=1)
+
+
+def useful_static(cs):
+    """(policies useful for every class that has them as candidates, sets holding a null
+    policy) — see the module docstring."""
+    P = cs.pols
+    nf, tf = P["nflags"], P["tflags"]
+    always = np.array([x is None for x in cs.cand_spec[1]], bool) if cs.n_pols else np.zeros(0, bool)
+    pol = ((nf & L.NF_EFFECT_TRUTHY) != 0) & (P["map_size"] == 0)
+    pol |= ((nf & L.NF_HAS_TARGET) != 0) & (((tf & L.TF_HAS_SUBJECTS) != 0) | always)
+    null = (nf & L.NF_NULL) != 0
+    cum = np.concatenate([[0], np.cumsum(null, dtype=np.int64)])
+    b_s = cs.sets["child_begin"].astype(np.int64)
+    e_s = cs.sets["child_end"].astype(np.int64)
+    return pol, (cum[e_s] - cum[b_s]) > 0
+
+
+def throw_policies(cs, col_values, rx):
+    """bool [ncols + 1, P]: policies whose target reads a RegExp cell that throws (or needs
+    the host) for a request entity value of that column (row ncols: no entity attr)."""
+    nrows = len(cs.rx_rows)
+    ncols = len(col_values)
+    out = np.zeros((ncols + 1, cs.n_pols), bool)
+    if not (nrows and ncols and cs.n_pols):
+        return out
+    real = np.array([v is MISSING or v is None or isinstance(v, str) for v in col_values], bool)
+    rowmask = ((rx[:ncols, :nrows] & _THROW_LIKE) != 0) & real[:, None]
+    if rowmask.any():
+        _, A = _spec_matrix(cs.cand_spec[1], nrows)
+        if A.nnz:
+            out[:ncols] = (sparse.csr_matrix(rowmask.astype(np.int32)) @ A.T).toarray() > 0
+    return out
+
+
+def _useful(cs, s, p, r, thr_rows, pol_static, set_null):
+    """Useful sets / policies of a chunk of class rows (bool [C, S], [C, P])."""
+    C = s.shape[0]
+    if cs.n_pols and cs.n_rules:
+        cr = np.concatenate([np.zeros((C, 1), np.int64), np.cumsum(r, axis=1)], axis=1)
+        has_rule = (cr[:, cs.pols["child_end"].astype(np.int64)] - cr[:, cs.pols["child_begin"].astype(np.int64)]) > 0
+    else:
+        has_rule = np.zeros((C, cs.n_pols), bool)
+    up = p & (has_rule | pol_static[None, :] | thr_rows)
+    if cs.n_pols:
+        cu = np.concatenate([np.zeros((C, 1), np.int64), np.cumsum(up, axis=1)], axis=1)
+        any_up = (cu[:, cs.sets["child_end"].astype(np.int64)] - cu[:, cs.sets["child_begin"].astype(np.int64)]) > 0
+    else:
+        any_up = np.zeros((C, cs.n_sets), bool)
+    us = s & (any_up | set_null[None, :])
+    return us, up
 
 
 def _key(v):
@@ -210,7 +289,7 @@ def action_candidates(cs, pairs):
     return tuple(out)
 
 
-def classes(cs, hdr, roles, pcol, ent, act=None):
+def classes(cs, hdr, roles, pcol, ent, act=None, thr=None):
     """Class id per request (u32, PCOL_ALL = unfiltered) and the class rows [C, W] u32.
 
     A class row is the AND of three node filters — entity column, role associations,
@@ -222,8 +301,7 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
     n = len(hdr)
     active = (pcol != L.PCOL_ALL) & ((hdr["flags"] & (L.RQ_HOST | L.RQ_NO_TARGET)) == 0)
     cls = np.full(n, L.PCOL_ALL, np.uint32)
-    ws, wp, wr = section_words(cs)
-    W = ws + wp + wr
+    W = row_layout(cs)[4]
     if not active.any():
         return cls, np.zeros((1, W), np.uint32), None, None
     if act is not None:
@@ -239,6 +317,9 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
     b_s = cs.sets["child_begin"].astype(np.int64)
     e_s = cs.sets["child_end"].astype(np.int64)
     nonempty = e_s > b_s
+    pol_static, set_null = useful_static(cs)
+    if thr is None:
+        thr = np.zeros((int(pcol[pcol != L.PCOL_ALL].max(initial=0)) + 1, cs.n_pols), bool)
     levels = ("entity+roles+action", "entity+action", "entity")
     for level in (levels if FORCE_LEVEL is None else (FORCE_LEVEL,)):
         cols = [pcol.astype(np.int64)[:, None]]
@@ -280,7 +361,8 @@ def classes(cs, hdr, roles, pcol, ent, act=None):
             else:
                 pol_any = np.zeros((len(ck), cs.n_sets), bool)
             s &= pol_any & nonempty[None, :]
-            out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+            us, up = _useful(cs, s, p, r, thr[np.minimum(pc, len(thr) - 1)], pol_static, set_null)
+            out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs)
         # requests whose rows are identical share one class
         urows, rinv = _unique_rows(out)
         if len(urows) <= MAX_CLASSES or level == "entity":
@@ -306,8 +388,7 @@ def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty):
     through checkSubjectMatches (accessController.ts:797-806) — and each request's row
     index (0xFFFF: no role filtering).  The kernel ANDs it with the class row; both are
     supersets of the joint filter, so their AND is too."""
-    ws, wp, wr = section_words(cs)
-    W = ws + wp + wr
+    W = row_layout(cs)[4]
     n = len(rs)
     rkey = np.full(n, 0xFFFF, np.uint32)
     keys, inv = _unique_rows(rs[active])
@@ -332,7 +413,10 @@ def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty):
         if cs.n_pols:
             cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
             s = s & ((cum[:, e_s] - cum[:, b_s]) > 0) & nonempty[None, :]
-        out[c0:c0 + len(ck)] = np.concatenate([_pack(s, ws), _pack(p, wp), _pack(r, wr)], axis=1)
+        # the useful sections are computed per class without role filtering: no factor there
+        ones_s = np.ones((len(ck), cs.n_sets), bool)
+        ones_p = np.ones((len(ck), cs.n_pols), bool)
+        out[c0:c0 + len(ck)] = _assemble(s, p, ones_s, ones_p, r, cs)
     return rkey, out
 
 

@@ -553,6 +553,7 @@ CODEC_URNS = ("entity", "property", "operation", "resourceID", "actionID", "role
               "aclIndicatoryEntity", "aclInstance", "create", "read", "modify", "delete", "user", "skipACL",
               "maskedProperty")
 CODEC_MAGIC, CODEC_VERSION = 0x43534341, 2  # "ACSC"
+ABI_VERSION = 5  # include/acs_mi355x.h ACS_ABI_VERSION (store image header)
 
 
 def codec_section(cs: CompiledStore) -> bytes:
@@ -600,6 +601,6 @@ def store_blob(cs: CompiledStore, codec: bool = True) -> bytes:
     body = b"".join(parts)
     sec = codec_section(cs) if codec else b""
     off = 64 + len(body) if sec else 0
-    hdr = struct.pack("<16I", 0x31534341, 4, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
+    hdr = struct.pack("<16I", 0x31534341, ABI_VERSION, cs.n_sets, cs.n_pols, cs.n_rules, len(cs.rres),
                       len(cs.pairs), len(cs.u32pool), cs.id_user, off, len(sec), 0, 0, 0, 0, 0)
     return hdr + body + sec

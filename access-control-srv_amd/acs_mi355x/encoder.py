@@ -49,6 +49,8 @@ class RequestBatch:
     cand: np.ndarray | None = None   # [rx_cols + 1, W] candidate bitsets (candidates.py)
     cand_wp: int = 0
     cand_wr: int = 0
+    cand_wsu: int = 0                # useful sets / policies sections (candidates.py); 0: absent
+    cand_wpu: int = 0
     role_key: np.ndarray | None = None   # [n] u32 role-factor row per request (large stores)
     role_bits: np.ndarray | None = None  # [role rows, W] u32
 
@@ -447,9 +449,9 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     # pad: columns without a value (an all-empty batch) get no candidates beyond the "always" nodes
     vals = list(col_values) + [object()] * (ncols - len(col_values))
     ent = candidates.entity_candidates(cs, vals, b.rx)
-    ws, wp, _ = candidates.section_words(cs)
-    b.cand_wp, b.cand_wr = ws, ws + wp
+    thr = candidates.throw_policies(cs, vals, b.rx)
+    b.cand_wp, b.cand_wsu, b.cand_wpu, b.cand_wr, _ = candidates.row_layout(cs)
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
     roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
-    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act)
+    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

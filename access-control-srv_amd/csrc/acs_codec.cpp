@@ -307,6 +307,10 @@ struct acs_codec {
   std::vector<uint32_t> norole_bits;          // [W]
   std::vector<std::vector<uint32_t>> role_node_list;  // per role row: node indices
   std::vector<uint8_t> node_need_act;
+  // useful sections (candidates.useful_static): policies useful wherever they are candidates,
+  // sets holding a null policy; output row layout [S | P | useful S | useful P | R]
+  std::vector<uint8_t> pol_static, set_null;
+  uint32_t W2 = 0;
   // caches
   std::shared_mutex hr_mu;
   std::unordered_map<uint64_t, std::vector<std::shared_ptr<const HrForest>>> hr_inline;
@@ -433,6 +437,21 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     c->row_ptr[r + 1] = c->row_ptr[r] + (uint32_t)per_row[r].size();
     c->row_nodes.insert(c->row_nodes.end(), per_row[r].begin(), per_row[r].end());
   }
+  // useful-section statics (candidates.useful_static)
+  c->W2 = 2 * c->ws + 2 * c->wp + c->wr;
+  c->pol_static.assign(c->P, 0);
+  c->set_null.assign(c->S, 0);
+  for (uint32_t q = 0; q < c->P; ++q) {
+    const NodeRec& N = c->nodes[c->S + q];
+    const bool eff_only = (N.nflags & NF_EFFECT_TRUTHY) && N.map_size == 0;
+    const bool tgt = (N.nflags & NF_HAS_TARGET) && ((N.tflags & TF_HAS_SUBJECTS) || kind[c->S + q] == 1);
+    c->pol_static[q] = eff_only || tgt;
+  }
+  for (uint32_t s = 0; s < c->S; ++s) {
+    const NodeRec& N = c->nodes[s];
+    for (uint32_t q = N.child_begin; q < N.child_end && q < c->P; ++q)
+      if (c->nodes[c->S + q].nflags & NF_NULL) c->set_null[s] = 1;
+  }
   // role requirements (candidates.role_requirements) and action requirements
   c->node_role.assign(nn, -1);
   c->node_need_act.assign(nn, 0);
@@ -480,7 +499,7 @@ struct acs_codec_batch {
   std::vector<uint8_t> rx;  // [rx_cols][rx_rows]
   uint32_t rx_cols = 1, rx_rows = 1;
   std::vector<uint32_t> cand;
-  uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0;
+  uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0;
   std::vector<uint32_t> role_key, role_bits;
   uint32_t role_rows = 0;
   std::vector<const char*> reason;  // per request: why it goes to the host (nullptr: it does not)
@@ -1134,6 +1153,42 @@ struct Classes {
     }
   }
 
+  static bool bit(const Row& r, uint32_t off, uint32_t i) { return (r[off + (i >> 5)] >> (i & 31)) & 1u; }
+
+  // [S | P | R] row -> [S | P | useful S | useful P | R] (candidates._useful / _assemble);
+  // thr: the column's throwing policies (P bits), or nullptr
+  Row assemble(const Row& r, const Row* thr) const {
+    Row out(C.W2, 0u);
+    std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
+    std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
+    const uint32_t wsu = C.ws + C.wp, wpu = 2 * C.ws + C.wp, rr = C.ws + C.wp;
+    for (uint32_t q = 0; q < C.P; ++q) {
+      if (!bit(r, C.ws, q)) continue;
+      bool use = C.pol_static[q] || (thr && bit(*thr, 0, q));
+      const NodeRec& N = C.nodes[C.S + q];
+      for (uint32_t k = N.child_begin; k < N.child_end && !use; ++k) use = bit(r, rr, k);
+      if (use) out[wpu + (q >> 5)] |= 1u << (q & 31);
+    }
+    for (uint32_t s = 0; s < C.S; ++s) {
+      if (!bit(r, 0, s)) continue;
+      bool use = C.set_null[s];
+      const NodeRec& N = C.nodes[s];
+      for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(out, wpu, q);
+      if (use) out[wsu + (s >> 5)] |= 1u << (s & 31);
+    }
+    return out;
+  }
+
+  // role-factor row: the useful sections are not role-factored (all nodes)
+  Row assemble_role(const Row& r) const {
+    Row out(C.W2, 0u);
+    std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
+    std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
+    for (uint32_t s = 0; s < C.S; ++s) out[C.ws + C.wp + (s >> 5)] |= 1u << (s & 31);
+    for (uint32_t q = 0; q < C.P; ++q) out[2 * C.ws + C.wp + (q >> 5)] |= 1u << (q & 31);
+    return out;
+  }
+
   Row class_row(uint32_t pc, uint32_t a, const int32_t* roles, int nroles, bool role_filter,
                 const std::vector<std::shared_ptr<const Row>>& ent,
                 const std::vector<std::shared_ptr<const Row>>& arow) const {
@@ -1154,11 +1209,13 @@ struct Classes {
 uint64_t row_hash(const uint32_t* r, size_t n) { return hash_bytes((const char*)r, n * 4); }
 
 void Classes::run() {
-  const uint32_t n = B.n, W = C.W;
+  const uint32_t n = B.n, W = C.W2;  // output rows: [S | P | useful S | useful P | R]
   const uint32_t ncols = B.rx_cols;
   B.cand_words = W;
   B.cand_wp = C.ws;
-  B.cand_wr = C.ws + C.wp;
+  B.cand_wsu = C.ws + C.wp;
+  B.cand_wpu = 2 * C.ws + C.wp;
+  B.cand_wr = 2 * C.ws + 2 * C.wp;
   // primary column per request (candidates.primary_columns)
   std::vector<uint32_t> pcol(n, ncols);
   std::vector<uint8_t> active(n, 0);
@@ -1199,6 +1256,21 @@ void Classes::run() {
       ent[c] = entity_row(keys[c], cells);
     }
     ent[ncols] = std::make_shared<Row>(C.always_bits);
+  }
+  // per column: policies whose target reads a throwing (or host) RegExp cell (candidates.throw_policies)
+  std::vector<std::unique_ptr<Row>> thr(ncols + 1);
+  for (uint32_t c = 0; c < ncols; ++c) {
+    if (col_keys[c].empty()) continue;
+    const uint8_t* cells = B.rx.data() + (size_t)c * B.rx_rows;
+    for (uint32_t r = 0; r < (uint32_t)C.rx_pat.size(); ++r) {
+      if (!(cells[r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST))) continue;
+      for (uint32_t k = C.row_ptr[r]; k < C.row_ptr[r + 1]; ++k) {
+        const uint32_t g = C.row_nodes[k];
+        if (g < C.S || g >= C.S + C.P) continue;
+        if (!thr[c]) thr[c] = std::make_unique<Row>(C.wp ? C.wp : 1, 0u);
+        (*thr[c])[(g - C.S) >> 5] |= 1u << ((g - C.S) & 31);
+      }
+    }
   }
   // action keys (candidates.action_keys): 0 none, 1 several / unfiltered, 2 + k a single pair
   std::vector<uint32_t> ak(n, 0);
@@ -1282,7 +1354,9 @@ void Classes::run() {
         const size_t k = next.fetch_add(1);
         if (k >= nk) return;
         const uint32_t i = key_first[k];
-        rows[k] = class_row(pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter, ent, arow);
+        rows[k] = assemble(class_row(pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter, ent,
+                                     arow),
+                           pcol[i] < ncols ? thr[pcol[i]].get() : nullptr);
       }
     };
     std::vector<std::thread> pool;
@@ -1349,9 +1423,10 @@ void Classes::run() {
     for (size_t k = 0; k < set_first.size(); ++k) {
       const uint32_t i = set_first[k];
       Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
-      for (uint32_t w = 0; w < W; ++w) r[w] &= valid[w];
+      for (uint32_t w = 0; w < C.W; ++w) r[w] &= valid[w];
       sets_need_policies(r);
-      std::copy(r.begin(), r.end(), B.role_bits.begin() + k * W);
+      const Row o = assemble_role(r);
+      std::copy(o.begin(), o.end(), B.role_bits.begin() + k * W);
     }
     B.role_key = std::move(rkey);
     B.role_rows = (uint32_t)set_first.size();
@@ -1614,6 +1689,8 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
   v.cand_words = b->cand_words;
   v.cand_wp = b->cand_wp;
   v.cand_wr = b->cand_wr;
+  v.cand_wsu = b->cand_wsu;
+  v.cand_wpu = b->cand_wpu;
   v.cand_rows = b->cand_rows;
   if (!b->role_key.empty()) {
     v.role_key = b->role_key.data();

@@ -74,7 +74,20 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   (void)T;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_NO_VLR)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(ACS_SLOAD)
+  // Scalar loads: the address is wave-uniform, so through the constant address space the
+  // compiler emits s_load_dwordxN.  Scalar loads ignore the exec mask, so every address must
+  // be valid even where no lane is active: node indices are clamped to their table
+  // (node_at), and every other table address is an offset taken from such a record, which
+  // acs_compile has validated against its pool (csrc/acs_validate.cpp).
+  typedef __attribute__((address_space(4))) const uint32_t const_u32;
+  const uint64_t a = (uint64_t)(uintptr_t)w;
+  const uint64_t ua = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
+                      ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
+  const const_u32* c = (const const_u32*)(uintptr_t)ua;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = c[k];
+#elif defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_NO_VLR)
   // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
   // the wave-uniform record moves to SGPRs: its fields feed scalar compares and branches and
   // free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself proves
@@ -90,6 +103,17 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   return out;
 }
 
+// Node record `x` of a table section of `n` records (x clamped into the section; see
+// load_words — only the scalar-load build needs the clamp).
+ACS_FN NodeRec node_at(const Tables& T, const NodeRec* sec, uint32_t x, uint32_t n) {
+#if defined(ACS_SLOAD)
+  x = x < n ? x : n - 1;
+#else
+  (void)n;
+#endif
+  return load_words(T, sec + x);
+}
+
 struct Batch {
   uint32_t n;
   const ReqHdr* hdr;      // [n]
@@ -103,6 +127,7 @@ struct Batch {
   const uint32_t* cand;   // [cand_rows][cand_words] candidate bitsets (sets | policies | rules) per class
   uint32_t cand_words, cand_wp, cand_wr;  // row length, word offsets of the policy / rule sections
   uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
+  uint32_t cand_wsu, cand_wpu;  // isAllowed's useful sets / policies sections (0: absent)
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
@@ -120,6 +145,7 @@ struct Filter {
   const uint32_t* rbits;
   uint32_t nlist, W, nroles, lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
+  uint32_t wsu, wpu;       // isAllowed: useful sets / loop-2b policies (0 / wp without them)
   bool all;                // no filtering
   ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
     uint32_t x = cand[(size_t)c * W + w];
@@ -153,7 +179,7 @@ struct Filter {
 // long-lived scalar state stays small.
 // FilterAll: the batch carries no candidate rows — every node is a candidate.
 struct FilterAll {
-  uint32_t wp, wr;
+  uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
 };
 
@@ -161,7 +187,7 @@ struct FilterAll {
 // kernel before any lane diverges (all ones for a wave holding an unfiltered request).
 struct FilterLds {
   const uint32_t* lds;
-  uint32_t wp, wr;
+  uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
@@ -237,6 +263,9 @@ struct ReqCtx {
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
+#if defined(ACS_ROLE_REGS)
+  uint32_t rl[RMAX];  // role_associations roles, NONE32 past nroles (branch-free role test)
+#endif
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
 #endif
@@ -258,6 +287,10 @@ struct ReqCtx {
     s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
     role0 = h.nroles > 0 ? B.roles[i] : 0u;
     role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
+#if defined(ACS_ROLE_REGS)
+#pragma unroll
+    for (int k = 0; k < RMAX; ++k) rl[k] = k < (int)h.nroles ? B.roles[(size_t)k * B.n + i] : NONE32;
+#endif
   }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
@@ -347,9 +380,16 @@ ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
   if (t.tflags & TF_SUBJ_EMPTY) return true;
   if (t.tflags & TF_SUBJ_ROLE) {
     if (!R.flag(RQ_RA_TRUTHY)) return false;
+#if defined(ACS_ROLE_REGS)
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < RMAX; ++k) hit |= R.rl[k] == t.role;
+    return hit;
+#else
     for (uint32_t k = 0; k < R.h.nroles; ++k)
       if (R.role(k) == t.role) return true;
     return false;
+#endif
   }
   return attrs_match(R.T.pairs + t.subj_off, t.subj_n, R, true);
 }
@@ -689,7 +729,7 @@ ACS_FN tri multiple_entities(const NodeRec& S, const RQ& R) {
     if (!(q.kind & K_ENT)) continue;
     bool multi = false;
     for (uint32_t p = S.child_begin; p < S.child_end; ++p) {
-      const NodeRec P = load_words(R.T, R.T.pols + p);
+      const NodeRec P = node_at(R.T, R.T.pols, p, R.T.n_pols);
       if (P.nflags & NF_NULL) return -(tri)ERR_TYPE;  // policy.effect of null
       if (!(P.nflags & NF_HAS_TARGET) || P.res_n == 0) continue;
       const uint8_t pe = (P.nflags & NF_EFFECT_TRUTHY) ? P.effect : (uint8_t)EFF_UNDEF;  // no PERMIT default
@@ -731,10 +771,10 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;
-  CandRange sets(F, 0, 0, T.n_sets);
+  CandRange sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py)
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = load_words(T, T.sets + s);
+    const NodeRec S = node_at(T, T.sets, s, T.n_sets);
     if (S.nflags & NF_HAS_TARGET) {
       PROF_T0(t0);
       const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
@@ -750,7 +790,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = load_words(T, T.pols + p);
+        const NodeRec P = node_at(T, T.pols, p, T.n_pols);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
@@ -772,10 +812,10 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       exact = m != 0;
     }
     Fold sf(S.ca);
-    CandRange pols(F, F.wp, S.child_begin, S.child_end);
+    CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = load_words(T, T.pols + p);
+      const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) continue;
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
@@ -801,7 +841,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = load_words(T, T.rules + r);
+        const NodeRec Q = node_at(T, T.rules, r, T.n_rules);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
@@ -877,6 +917,8 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
+  F.wsu = B.cand_wsu;
+  F.wpu = B.cand_wpu ? B.cand_wpu : B.cand_wp;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
   F.row[0] = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
@@ -970,7 +1012,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
   CandRange sets(F, 0, s_begin, s_end < T.n_sets ? s_end : T.n_sets);
   uint32_t s;
   while (sets.next(s)) {
-    const NodeRec S = load_words(T, T.sets + s);
+    const NodeRec S = node_at(T, T.sets, s, T.n_sets);
     if (S.nflags & NF_HAS_TARGET) {
       const tri m = target_match(S, R, EFF_PERMIT, false, true, &obl);
       if (m < 0) return make_err(m, s + 1);
@@ -982,7 +1024,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       CandRange pols(F, F.wp, S.child_begin, S.child_end);
       uint32_t p;
       while (pols.next(p)) {
-        const NodeRec P = load_words(T, T.pols + p);
+        const NodeRec P = node_at(T, T.pols, p, T.n_pols);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           const tri m = target_match(P, R, P.pe_at, false, true, &obl);
@@ -1004,7 +1046,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
-      const NodeRec P = load_words(T, T.pols + p);
+      const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
         const tri m = target_match(P, R, pe, !exact, true, &obl);
@@ -1015,7 +1057,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = load_words(T, T.rules + r);
+        const NodeRec Q = node_at(T, T.rules, r, T.n_rules);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {

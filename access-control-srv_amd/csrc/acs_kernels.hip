@@ -220,6 +220,8 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
+  F.wsu = B.cand_wsu;
+  F.wpu = B.cand_wpu ? B.cand_wpu : B.cand_wp;
   F.cand = B.cand;
   F.rbits = B.role_bits;
   F.nroles = B.role_key ? B.role_rows : 0u;
@@ -269,7 +271,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
 // The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
 // W-word LDS region, all ones when the wave holds an unfiltered request.
 __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-  FilterLds F{lds, B.cand_wp, B.cand_wr};
+  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
@@ -293,7 +295,9 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
   return F;
 }
 
-__device__ inline FilterAll wave_filter_all(const Batch& B) { return FilterAll{B.cand_wp, B.cand_wr}; }
+__device__ inline FilterAll wave_filter_all(const Batch& B) {
+  return FilterAll{B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp};
+}
 
 // One maker per filter form, selected by the kernel's template argument.
 template <class FL> struct FilterMaker;
@@ -658,6 +662,13 @@ static Batch to_batch(const acs_req_batch* b) {
   B.cand_words = b->cand_words;
   B.cand_wp = b->cand_wp;
   B.cand_wr = b->cand_wr;
+  B.cand_wsu = b->cand_wsu;
+  B.cand_wpu = b->cand_wpu;
+  static const bool no_useful = [] {  // A/B runs: ACS_NO_USEFUL=1 walks the candidate sections
+    const char* e = getenv("ACS_NO_USEFUL");
+    return e && *e == '1';
+  }();
+  if (no_useful) B.cand_wsu = B.cand_wpu = 0;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;

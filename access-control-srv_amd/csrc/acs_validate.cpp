@@ -85,6 +85,9 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
     if (b->cand_wp < words32(n_sets) || b->cand_wr < b->cand_wp + words32(n_pols) ||
         b->cand_words < b->cand_wr + words32(n_rules))
       return bad("batch: candidate row layout", b->cand_words);
+    if ((b->cand_wsu && b->cand_wsu + words32(n_sets) > b->cand_words) ||
+        (b->cand_wpu && b->cand_wpu + words32(n_pols) > b->cand_words))
+      return bad("batch: candidate row layout", b->cand_words);
     if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
   }
   const ReqHdr* hdr = (const ReqHdr*)b->hdr;

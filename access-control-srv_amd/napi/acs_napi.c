@@ -25,7 +25,7 @@
  *   whatIsAllowedObl(tables, batch, idx, chunks, cap) -> {obl, oblN}
  *   wordsPerRequest(tables), layoutSizes(), deviceCount(), lastError()
  * `batch` = an encode() handle, or a plain object {n, hdr, res, subj, act, roles, arena,
- * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, roleKey, roleRowsBits,
+ * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, candWsu, candWpu, roleKey, roleRowsBits,
  * roleRows]} of typed arrays in the layout of csrc/acs_layout.h; every array is checked
  * against the sizes `n` and the counts imply before the library reads it.
  *
@@ -268,7 +268,8 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
   if (prop_u32(env, v, "rxCols", &b->rx_cols) || prop_u32(env, v, "rxRows", &b->rx_rows) ||
       prop_u32(env, v, "candWords", &b->cand_words) || prop_u32(env, v, "candWp", &b->cand_wp) ||
       prop_u32(env, v, "candWr", &b->cand_wr) || prop_u32(env, v, "candRows", &b->cand_rows) ||
-      prop_u32(env, v, "roleRows", &b->role_rows))
+      prop_u32(env, v, "roleRows", &b->role_rows) || prop_u32(env, v, "candWsu", &b->cand_wsu) ||
+      prop_u32(env, v, "candWpu", &b->cand_wpu))
     return -1;
   if (field(env, v, "hdr", n * HDR_B, n > 0, &b->hdr, NULL, &bad) ||
       field(env, v, "res", n * QMAX * RES_B, n > 0, &b->res, NULL, &bad) ||
@@ -288,8 +289,9 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
   b->rx = (const uint8_t*)p;
   if (field(env, v, "cand", (size_t)b->cand_rows * b->cand_words * 4, 0, &p, &len, &bad)) goto fail;
   b->cand = (const uint32_t*)p;
-  if (b->cand && (b->cand_wp > b->cand_words || b->cand_wr > b->cand_words)) {
-    bad = "candWp / candWr";
+  if (b->cand && (b->cand_wp > b->cand_words || b->cand_wr > b->cand_words || b->cand_wsu > b->cand_words ||
+                  b->cand_wpu > b->cand_words)) {
+    bad = "candWp / candWr / candWsu / candWpu";
     goto fail;
   }
   if (field(env, v, "roleKey", 0, 0, &p, &len, &bad)) goto fail;

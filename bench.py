@@ -73,11 +73,13 @@ def _node_bytes(nodes):
 
 
 def scan_bytes(cs, batch, wave=64):
-    """Table bytes the K1 waves visit, counted from the same candidate rows the kernel uses:
+    """Table bytes the K1 waves visit, counted from the same class rows the kernel uses:
     requests in coherence-sort order, 64 per wave, the union of the wave's (class row AND
-    role-factor row) filters (an unfiltered class: the whole table); a policy is visited only
-    inside a visited set, a rule only inside a visited policy.  Returns total bytes."""
-    from acs_mi355x import layout as L
+    role-factor row) filters (an unfiltered class: the whole table).  K1 walks the useful
+    sets; inside one, loop 2a scans the candidate policies and loop 2b the useful ones; a
+    rule is visited only inside a loop-2b policy.  Each record counts once per wave (a policy
+    read by both loops, once).  Returns total bytes."""
+    from acs_mi355x import layout as L, candidates
     n = batch.n
     cand = batch.cand
     R = 0 if cand is None else cand.shape[0]
@@ -99,8 +101,8 @@ def scan_bytes(cs, batch, wave=64):
     par_p = np.repeat(np.arange(ns), (cs.sets["child_end"] - cs.sets["child_begin"]).astype(np.int64))
     par_r = np.repeat(np.arange(npol), (cs.pols["child_end"] - cs.pols["child_begin"]).astype(np.int64))
     full = int(bs.sum() + bp.sum() + br.sum())
-    ws = (ns + 31) // 32
-    wp = (npol + 31) // 32
+    wp, wsu, wpu, wr, _ = candidates.row_layout(cs)
+    useful = getattr(batch, "cand_wsu", 0) != 0
     cache = {}
 
     def union_bytes(key):
@@ -117,10 +119,11 @@ def scan_bytes(cs, batch, wave=64):
                 x = x & batch.role_bits[k & 0xFFFF]
             row |= x
         bits = np.unpackbits(row.view(np.uint8), bitorder="little").astype(bool)
-        s = bits[:ns]
-        p = bits[32 * ws:32 * ws + npol] & s[par_p]
-        r = bits[32 * (ws + wp):32 * (ws + wp) + nr] & p[par_r]
-        v = int(bs[s].sum() + bp[p].sum() + br[r].sum())
+        s = bits[32 * wsu:32 * wsu + ns] if useful else bits[:ns]
+        p2a = bits[32 * wp:32 * wp + npol] & s[par_p]
+        p2b = (bits[32 * wpu:32 * wpu + npol] if useful else bits[32 * wp:32 * wp + npol]) & s[par_p]
+        r = bits[32 * wr:32 * wr + nr] & p2b[par_r]
+        v = int(bs[s].sum() + bp[p2a | p2b].sum() + br[r].sum())
         cache[key] = v
         return v
 

@@ -24,7 +24,7 @@ extern "C" {
 #endif
 
 #define ACS_BLOB_MAGIC 0x31534341u /* "ACS1" */
-#define ACS_ABI_VERSION 4u
+#define ACS_ABI_VERSION 5u
 
 /* Compiled policy-store image (host compiler output, see csrc/acs_layout.h).
  * Header followed by 16-byte aligned sections in this order: set / policy / rule
@@ -53,12 +53,15 @@ typedef struct {
   size_t arena_words;
   const uint8_t* rx;      /* [rx_cols][rx_rows] regex matrix   */
   uint32_t rx_cols, rx_rows;
-  /* [cand_rows][cand_words] candidate bitsets over (sets | policies | rules), one row per
-   * request class (entity column x required roles, acs_mi355x/candidates.py); the class id
-   * is in ReqHdr.flags >> 16.  NULL = evaluate every node. */
+  /* [cand_rows][cand_words] candidate bitsets, one row per request class (entity column x
+   * required roles x action, acs_mi355x/candidates.py); the class id is in ReqHdr.flags >> 16.
+   * Sections (word offsets): candidate sets at 0, candidate policies at cand_wp, candidate
+   * rules at cand_wr, and — isAllowed only, 0 when absent — the sets / policies that can
+   * change an isAllowed result at cand_wsu / cand_wpu.  NULL = evaluate every node. */
   const uint32_t* cand;
   uint32_t cand_words, cand_wp, cand_wr;
   uint32_t cand_rows;
+  uint32_t cand_wsu, cand_wpu;
   /* Optional role factor (large stores, where class rows keyed by roles would not fit):
    * [role_rows][cand_words] bitsets of the nodes a request with that role-association set
    * can reach (checkSubjectMatches, accessController.ts:793-823), AND-ed with the class

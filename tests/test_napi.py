@@ -45,7 +45,7 @@ def _dump(tmp, cs, b):
         tmp.joinpath(k + ".bin").write_bytes(np.ascontiguousarray(getattr(b, k)).tobytes())
     tmp.joinpath("meta.json").write_text(json.dumps({
         "n": b.n, "rxCols": int(b.rx.shape[0]), "rxRows": int(b.rx_rows), "candWords": int(b.cand.shape[1]),
-        "candWp": int(b.cand_wp), "candWr": int(b.cand_wr),
+        "candWp": int(b.cand_wp), "candWr": int(b.cand_wr), "candWsu": int(b.cand_wsu), "candWpu": int(b.cand_wpu),
         "candRows": int(b.cand.shape[0])}))
 
 

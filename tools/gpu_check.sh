@@ -31,14 +31,20 @@ for s in $STEPS; do
     quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
     ab) for cfg in ${AB_CONFIGS:-c2 c3}; do
           st=20; [ "$cfg" = c3 ] && st=5
-          for rep in 1 2; do
+          for rep in $(seq 1 ${AB_REPS:-2}); do
             step "ab_${cfg}_product_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
-            step "ab_${cfg}_general_$rep" 900 env ACS_FILTER_GENERAL=1 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
+            for ev in ${AB_ENVS:-ACS_FILTER_GENERAL}; do
+              step "ab_${cfg}_${ev}_$rep" 900 env $ev=1 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
+            done
             for v in ${VARIANTS:-}; do
               step "ab_${cfg}_${v}_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 \
                 --lib access-control-srv_amd/lib/variants/$v.so
             done
           done
+        done ;;
+    abtest) for v in ${VARIANTS:-}; do
+          step "pytest_gpu_$v" 600 env ACS_MI355X_LIB=access-control-srv_amd/lib/variants/$v.so \
+            python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "kats or random_diff or synthetic_config"
         done ;;
     quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
