@@ -4,8 +4,9 @@
 traffic = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes, averaged over dispatches:
 rocprofv3 reports both in KiB, and on gfx950 FETCH_SIZE counts half the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM section).  Writes/updates
-<out>[config][kernel] = {bytes_per_launch, fetch_kib, write_kib, dispatches, source}.
-usage: pmc_traffic.py <pmc dir> <config> <out.json> [kernel-substring]
+<out>[key][kernel] = {bytes_per_launch, fetch_kib, write_kib, dispatches, source}, key = the run
+shape the passes measured (bench.traffic_key: config/n<requests>/w<ranks>/<requests|rules>).
+usage: pmc_traffic.py <pmc dir> <key> <out.json> [kernel-substring]
 """
 import csv
 import json
@@ -24,7 +25,7 @@ def read(path, kernel):
 
 
 def main():
-    pmc, config, out = sys.argv[1:4]
+    pmc, key, out = sys.argv[1:4]
     kernel = sys.argv[4] if len(sys.argv) > 4 else "is_allowed_kernel"
     fetch = read(os.path.join(pmc, "g3", "pmc_counter_collection.csv"), kernel)["FETCH_SIZE"]
     write = read(os.path.join(pmc, "g4", "pmc_counter_collection.csv"), kernel)["WRITE_SIZE"]
@@ -33,11 +34,11 @@ def main():
     f = sum(fetch) / len(fetch)
     w = sum(write) / len(write)
     d = json.load(open(out)) if os.path.exists(out) else {}
-    d.setdefault(config, {})[kernel.split("(")[0]] = {
+    d.setdefault(key, {})[kernel.split("(")[0]] = {
         "bytes_per_launch": (2 * f + w) * 1024, "fetch_kib": f, "write_kib": w, "dispatches": len(fetch),
         "source": os.environ.get("TRAFFIC_SOURCE", pmc)}
     json.dump(d, open(out, "w"), indent=1, sort_keys=True)
-    print(json.dumps(d[config]))
+    print(json.dumps(d[key]))
 
 
 if __name__ == "__main__":
