@@ -378,16 +378,17 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None):
     cls[active] = rank[rinv[inv]].astype(np.uint32)
     if role_filter or nrr == 0:
         return cls, urows, None, None
-    rkey, rbits = _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty)
+    rkey, rbits = _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr.any(axis=0), pol_static, set_null)
     return cls, urows, rkey, rbits
 
 
-def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty):
+def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr_any, pol_static, set_null):
     """Role factor for class rows keyed without roles (large stores): one row per distinct
     role-association set of the batch — the nodes a request holding those roles can reach
-    through checkSubjectMatches (accessController.ts:797-806) — and each request's row
-    index (0xFFFF: no role filtering).  The kernel ANDs it with the class row; both are
-    supersets of the joint filter, so their AND is too."""
+    through checkSubjectMatches (accessController.ts:797-806), and the sets / policies
+    useful through those nodes — and each request's row index (0xFFFF: no role filtering).
+    The kernel ANDs it with the class row; both are supersets of the joint filter, so their
+    AND is too."""
     W = row_layout(cs)[4]
     n = len(rs)
     rkey = np.full(n, 0xFFFF, np.uint32)
@@ -413,10 +414,11 @@ def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty):
         if cs.n_pols:
             cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
             s = s & ((cum[:, e_s] - cum[:, b_s]) > 0) & nonempty[None, :]
-        # the useful sections are computed per class without role filtering: no factor there
-        ones_s = np.ones((len(ck), cs.n_sets), bool)
-        ones_p = np.ones((len(ck), cs.n_pols), bool)
-        out[c0:c0 + len(ck)] = _assemble(s, p, ones_s, ones_p, r, cs)
+        # useful sections from the role side alone (rules the roles reach; a policy that may
+        # throw for any column of the batch stays): AND-ed with the class row's useful
+        # sections (entity + action side) the kernel keeps a superset of the joint ones
+        us, up = _useful(cs, s, p, r, thr_any[None, :], pol_static, set_null)
+        out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs)
     return rkey, out
 
 

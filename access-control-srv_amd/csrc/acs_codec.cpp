@@ -1179,16 +1179,6 @@ struct Classes {
     return out;
   }
 
-  // role-factor row: the useful sections are not role-factored (all nodes)
-  Row assemble_role(const Row& r) const {
-    Row out(C.W2, 0u);
-    std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
-    std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
-    for (uint32_t s = 0; s < C.S; ++s) out[C.ws + C.wp + (s >> 5)] |= 1u << (s & 31);
-    for (uint32_t q = 0; q < C.P; ++q) out[2 * C.ws + C.wp + (q >> 5)] |= 1u << (q & 31);
-    return out;
-  }
-
   Row class_row(uint32_t pc, uint32_t a, const int32_t* roles, int nroles, bool role_filter,
                 const std::vector<std::shared_ptr<const Row>>& ent,
                 const std::vector<std::shared_ptr<const Row>>& arow) const {
@@ -1326,7 +1316,11 @@ void Classes::run() {
   }
   const size_t KEY_ROW_BYTES = size_t(512) << 20, ROLE_ROW_BYTES = size_t(256) << 20;
   const uint32_t MAX_CLASSES = PCOL_ALL;
-  for (int level = 0; level < 3; ++level) {
+  // tests: ACS_CODEC_FORCE_LEVEL=0|1|2 pins the key level (candidates.FORCE_LEVEL)
+  const char* force = getenv("ACS_CODEC_FORCE_LEVEL");
+  const int first_level = force && *force >= '0' && *force <= '2' ? *force - '0' : 0;
+  const int last_level = force && *force >= '0' && *force <= '2' ? first_level + 1 : 3;
+  for (int level = first_level; level < last_level; ++level) {
     const bool role_filter = level == 0 && have_roles;
     const bool action_filter = level < 2;
     // distinct keys of the active requests
@@ -1420,12 +1414,17 @@ void Classes::run() {
     }
     if (set_first.empty() || set_first.size() * W * 4 > ROLE_ROW_BYTES || set_first.size() >= 0xFFFF) return;
     B.role_bits.assign(set_first.size() * W, 0u);
+    // the role side's useful sections keep every policy that may throw for some column
+    Row thr_any(C.wp ? C.wp : 1, 0u);
+    for (const auto& t : thr)
+      if (t)
+        for (uint32_t w = 0; w < thr_any.size(); ++w) thr_any[w] |= (*t)[w];
     for (size_t k = 0; k < set_first.size(); ++k) {
       const uint32_t i = set_first[k];
       Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
       for (uint32_t w = 0; w < C.W; ++w) r[w] &= valid[w];
       sets_need_policies(r);
-      const Row o = assemble_role(r);
+      const Row o = assemble(r, &thr_any);
       std::copy(o.begin(), o.end(), B.role_bits.begin() + k * W);
     }
     B.role_key = std::move(rkey);

@@ -246,3 +246,46 @@ def test_native_compiler_fixtures_and_configs_byte_identical():
     for doc in (synth.c2_store(), synth.c3_store()):
         a, b = _both(store.populate(doc), FULL_URNS)
         assert a == b
+
+
+def _request_rows(b):
+    """Per request: (class row bytes or None, role-factor row bytes or None)."""
+    cls = (b.hdr["flags"] >> np.uint32(16)).astype(np.int64)
+    out = []
+    for i in range(b.n):
+        c = b.cand[cls[i]].tobytes() if b.cand is not None and cls[i] < b.cand.shape[0] else None
+        r = None
+        if b.role_key is not None and b.role_key[i] < b.role_bits.shape[0]:
+            r = b.role_bits[b.role_key[i]].tobytes()
+        out.append((c, r))
+    return out
+
+
+@pytest.mark.parametrize("level", [0, 1, 2])
+def test_codec_class_rows_match_python_at_every_level(level, monkeypatch):
+    """The codec's class rows (with the useful sections) and role-factor rows equal the Python
+    candidates' for every request, at each key level (level 1 and 2 carry a role factor)."""
+    from acs_mi355x import candidates
+    names = ["entity+roles+action", "entity+action", "entity"]
+    cases = [(FULL_URNS, store.populate(synth.c3_store(n_sets=40)), None)]
+    for s in range(0, 60, 6):
+        urns, doc, reqs = randgen.rand_case(s)
+        cases.append((urns, store.populate(doc), reqs))
+    checked = 0
+    for urns, m, reqs in cases:
+        try:
+            cs = compiler.compile_store(m, urns, DEFAULT_CAS)
+        except Exception:
+            continue
+        if reqs is None:
+            sb = synth.requests(cs, 3000, "c3", seed=11, tree=synth.OrgTree(fanout=3, depth=5))
+            reqs = [sb.decode(i) for i in range(sb.batch.n)]
+        monkeypatch.setattr(candidates, "FORCE_LEVEL", names[level])
+        pb = encoder.Encoder(cs).encode(reqs)
+        monkeypatch.setenv("ACS_CODEC_FORCE_LEVEL", str(level))
+        nb = NativeCodec(compiler.store_blob(cs)).encode(reqs, threads=2)
+        assert (pb.cand_wp, pb.cand_wsu, pb.cand_wpu, pb.cand_wr) == (nb.cand_wp, nb.cand_wsu, nb.cand_wpu, nb.cand_wr)
+        assert (pb.role_key is None) == (nb.role_key is None)
+        assert _request_rows(pb) == _request_rows(nb)
+        checked += 1
+    assert checked >= 8
