@@ -70,14 +70,117 @@ def section_words(cs):
 
 def row_layout(cs):
     """Word offsets of a class row's sections: (wp, wsu, wpu, wr, W) — candidate policies,
-    useful sets, useful policies, candidate rules, row length (candidate sets start at 0)."""
+    useful sets, useful policies, candidate rules, row length (candidate sets start at 0;
+    the target verdicts follow the rules at verdict_offset)."""
     ws, wp, wr = section_words(cs)
-    return ws, ws + wp, 2 * ws + wp, 2 * ws + 2 * wp, 2 * ws + 2 * wp + wr
+    return ws, ws + wp, 2 * ws + wp, 2 * ws + 2 * wp, 2 * ws + 6 * wp + 2 * wr
 
 
-def _assemble(s, p, us, up, r, cs):
+def verdict_offset(cs):
+    """Word offset of the target-verdict sections: policies known exact-true, exact-false,
+    RegExp-true, RegExp-false (wp words each), then rules whose retried match is known true
+    (wr words)."""
     ws, wp, wr = section_words(cs)
-    return np.concatenate([_pack(s, ws), _pack(p, wp), _pack(us, ws), _pack(up, wp), _pack(r, wr)], axis=1)
+    return 2 * ws + 2 * wp + wr
+
+
+def _assemble(s, p, us, up, r, cs, verdicts=None):
+    ws, wp, wr = section_words(cs)
+    parts = [_pack(s, ws), _pack(p, wp), _pack(us, ws), _pack(up, wp), _pack(r, wr)]
+    if verdicts is None:
+        parts.append(np.zeros((s.shape[0], 4 * wp + wr), np.uint32))
+    else:
+        pxt, pxf, prt, prf, qt = verdicts
+        parts += [_pack(pxt, wp), _pack(pxf, wp), _pack(prt, wp), _pack(prf, wp), _pack(qt, wr)]
+    return np.concatenate(parts, axis=1)
+
+
+# ------------------------------------------------------------------ target verdicts
+# For a request class, a target whose subjects are empty or a role test, whose actions are
+# none or a single pair the class fixes, and whose resources are empty or entity-only has
+# the same targetMatches result for every request of the class: checkSubjectMatches is role
+# membership (the class holds the request's required roles), attributesMatch on actions
+# compares against the class's single action pair, and an entity-only
+# resourceAttributesMatch depends only on the entity value of the class's column — exactly
+# (===), or through the RegExp cells in the rule attribute order (the last cell that resets
+# or hits decides; a throwing cell leaves the verdict unknown).  K1 reads these bits for a
+# wave whose lanes share one class and skips the matching (accessController.ts:661-672).
+
+def resource_verdicts(cs, col_values, rx, sec):
+    """Per column (ncols + 1 rows; the last = no entity attribute) and node of section `sec`
+    (1 policies, 2 rules): (exact true, exact false, RegExp true, RegExp false) of an empty or
+    entity-only resourceAttributesMatch; all False where unknown."""
+    nodes = (cs.sets, cs.pols, cs.rules)[sec]
+    spec = cs.cand_spec[sec]
+    n = len(nodes)
+    ncols = len(col_values)
+    out = [np.zeros((ncols + 1, n), bool) for _ in range(4)]
+    if n == 0:
+        return out
+    tf = nodes["tflags"]
+    empty = (tf & L.TF_RES_EMPTY) != 0
+    ent = ((tf & L.TF_RES_ENT_ONLY) != 0) & ~empty
+    for k in (0, 2):
+        out[k][:, empty] = True
+    real = np.array([v is MISSING or v is None or isinstance(v, str) for v in col_values] + [True], bool)
+    # no entity attribute: an entity-only match never sets entityMatch
+    out[1][ncols, ent] = True
+    out[3][ncols, ent] = True
+    idx = np.flatnonzero(ent)
+    if len(idx) == 0 or ncols == 0:
+        return out
+    K = max((len(spec[i]) for i in idx), default=0)
+    rows = np.full((len(idx), max(K, 1)), -1, np.int64)
+    for j, i in enumerate(idx):
+        sp = spec[i]
+        rows[j, :len(sp)] = sp
+    nrows = len(cs.rx_rows)
+    row_of = {_key(v): r for r, v in enumerate(cs.rx_rows)}
+    exact_row = np.array([row_of.get(_key(v), -1) if real[c] else -1 for c, v in enumerate(col_values)], np.int64)
+    cells = np.zeros((ncols, max(nrows, 1)), np.uint8)
+    if nrows:
+        cells[:, :nrows] = rx[:ncols, :nrows]
+    xt = np.zeros((ncols, len(idx)), bool)
+    em = np.zeros((ncols, len(idx)), bool)
+    thrown = np.zeros((ncols, len(idx)), bool)
+    for k in range(rows.shape[1]):
+        rk = rows[:, k]
+        valid = rk >= 0
+        xt |= valid[None, :] & (rk[None, :] == exact_row[:, None]) & (exact_row[:, None] >= 0)
+        c = np.where(valid[None, :], cells[:, np.maximum(rk, 0)], 0)
+        thrown |= (c & _THROW_LIKE) != 0
+        em = np.where((c & L.RX_HIT) != 0, True, np.where((c & L.RX_RESET) != 0, False, em))
+    ok = real[:ncols, None]
+    out[0][:ncols, idx] = xt & ok
+    out[1][:ncols, idx] = ~xt & ok
+    out[2][:ncols, idx] = em & ~thrown & ok
+    out[3][:ncols, idx] = ~em & ~thrown & ok
+    return out
+
+
+def _verdicts(cs, sec, pc, a, A_sec, role_ok_sec, role_filter, action_filter, res):
+    """(known true, known false) of targetMatches in exact and RegExp mode for section `sec`
+    of a chunk of classes: four bool [C, n] arrays (xt, xf, rt, rf)."""
+    nodes = (cs.sets, cs.pols, cs.rules)[sec]
+    nf, tf = nodes["nflags"], nodes["tflags"]
+    tgt = ((nf & L.NF_HAS_TARGET) != 0)[None, :]
+    sub_empty = ((tf & L.TF_SUBJ_EMPTY) != 0)[None, :]
+    sub_role = (((tf & L.TF_SUBJ_ROLE) != 0) & ((tf & L.TF_SUBJ_EMPTY) == 0))[None, :]
+    if role_filter:
+        subj_t = sub_empty | (sub_role & role_ok_sec)
+        subj_f = sub_role & ~role_ok_sec
+    else:
+        subj_t = np.broadcast_to(sub_empty, (len(pc), len(nodes)))
+        subj_f = np.zeros((len(pc), len(nodes)), bool)
+    need = (((nf & L.NF_HAS_TARGET) != 0) & (nodes["act_n"] > 0))[None, :]
+    fixed = (a != 1)[:, None] if action_filter else np.zeros((len(pc), 1), bool)
+    act = A_sec[a]
+    act_t = ~need | (fixed & act)
+    act_f = need & fixed & ~act
+    xt_r, xf_r, rt_r, rf_r = (v[pc] for v in res)
+    both_t = subj_t & act_t
+    any_f = subj_f | act_f
+    return (tgt & both_t & xt_r, tgt & (any_f | xf_r), tgt & both_t & rt_r, tgt & (any_f | rf_r))
 
 
 def useful_static(cs):
@@ -289,7 +392,7 @@ def action_candidates(cs, pairs):
     return tuple(out)
 
 
-def classes(cs, hdr, roles, pcol, ent, act=None, thr=None):
+def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
     """Class id per request (u32, PCOL_ALL = unfiltered) and the class rows [C, W] u32.
 
     A class row is the AND of three node filters — entity column, role associations,
@@ -362,7 +465,14 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None):
                 pol_any = np.zeros((len(ck), cs.n_sets), bool)
             s &= pol_any & nonempty[None, :]
             us, up = _useful(cs, s, p, r, thr[np.minimum(pc, len(thr) - 1)], pol_static, set_null)
-            out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs)
+            verdicts = None
+            if res is not None:
+                pxt, pxf, prt, prf = _verdicts(cs, 1, pc, a, A_p, role_ok(req_rows[1]), role_filter, action_filter,
+                                               res[0])
+                rxt, rxf, rrt, _ = _verdicts(cs, 2, pc, a, A_r, role_ok(req_rows[2]), role_filter, action_filter,
+                                             res[1])
+                verdicts = (pxt, pxf, prt, prf, rxt | (rxf & rrt))
+            out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs, verdicts)
         # requests whose rows are identical share one class
         urows, rinv = _unique_rows(out)
         if len(urows) <= MAX_CLASSES or level == "entity":
@@ -418,7 +528,10 @@ def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr_any, pol
         # throw for any column of the batch stays): AND-ed with the class row's useful
         # sections (entity + action side) the kernel keeps a superset of the joint ones
         us, up = _useful(cs, s, p, r, thr_any[None, :], pol_static, set_null)
-        out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs)
+        # the verdict sections are the class row's: the role side keeps them (all nodes)
+        ap = np.ones((len(ck), cs.n_pols), bool)
+        ar = np.ones((len(ck), cs.n_rules), bool)
+        out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs, (ap, ap, ap, ap, ar))
     return rkey, out
 
 

@@ -90,6 +90,7 @@ class CodecBatch:
         self.cand = _view(s.cand, np.uint32, s.cand_rows * W).reshape(s.cand_rows, W) if s.cand else None
         self.cand_wp, self.cand_wr = int(s.cand_wp), int(s.cand_wr)
         self.cand_wsu, self.cand_wpu = int(s.cand_wsu), int(s.cand_wpu)
+        self.cand_wv = int(s.cand_wv)
         self.role_key = _view(s.role_key, np.uint32, n) if s.role_key else None
         self.role_bits = (_view(s.role_rows_bits, np.uint32, s.role_rows * W).reshape(s.role_rows, W)
                           if s.role_key else None)

@@ -51,6 +51,7 @@ class RequestBatch:
     cand_wr: int = 0
     cand_wsu: int = 0                # useful sets / policies sections (candidates.py); 0: absent
     cand_wpu: int = 0
+    cand_wv: int = 0                 # target-verdict sections (candidates.verdict_offset); 0: absent
     role_key: np.ndarray | None = None   # [n] u32 role-factor row per request (large stores)
     role_bits: np.ndarray | None = None  # [role rows, W] u32
 
@@ -450,8 +451,10 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     vals = list(col_values) + [object()] * (ncols - len(col_values))
     ent = candidates.entity_candidates(cs, vals, b.rx)
     thr = candidates.throw_policies(cs, vals, b.rx)
+    res = (candidates.resource_verdicts(cs, vals, b.rx, 1), candidates.resource_verdicts(cs, vals, b.rx, 2))
     b.cand_wp, b.cand_wsu, b.cand_wpu, b.cand_wr, _ = candidates.row_layout(cs)
+    b.cand_wv = candidates.verdict_offset(cs)
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
     roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
-    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr)
+    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr, res)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))

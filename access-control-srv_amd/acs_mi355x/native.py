@@ -23,6 +23,7 @@ class ReqBatchC(C.Structure):
                 ("rx", C.c_void_p), ("rx_cols", C.c_uint32), ("rx_rows", C.c_uint32),
                 ("cand", C.c_void_p), ("cand_words", C.c_uint32), ("cand_wp", C.c_uint32), ("cand_wr", C.c_uint32),
                 ("cand_rows", C.c_uint32), ("cand_wsu", C.c_uint32), ("cand_wpu", C.c_uint32),
+                ("cand_wv", C.c_uint32),
                 ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
                 ("role_rows", C.c_uint32)]
 
@@ -112,6 +113,7 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
         s.cand_words, s.cand_wp, s.cand_wr = b.cand.shape[1], b.cand_wp, b.cand_wr
         s.cand_rows = b.cand.shape[0]
         s.cand_wsu, s.cand_wpu = getattr(b, "cand_wsu", 0), getattr(b, "cand_wpu", 0)
+        s.cand_wv = getattr(b, "cand_wv", 0)
     if b.role_key is not None:
         s.role_rows = b.role_bits.shape[0]
     return s

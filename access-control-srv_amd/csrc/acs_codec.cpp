@@ -310,7 +310,9 @@ struct acs_codec {
   // useful sections (candidates.useful_static): policies useful wherever they are candidates,
   // sets holding a null policy; output row layout [S | P | useful S | useful P | R]
   std::vector<uint8_t> pol_static, set_null;
-  uint32_t W2 = 0;
+  uint32_t W2 = 0, WV = 0;  // row length; offset of the target-verdict sections
+  std::vector<uint8_t> spec_kind;              // per node: 0 rows list (maybe empty), 1 always, 2 rows list
+  std::vector<uint32_t> spec_ptr, spec_idx;    // per node: its entity rows, in attribute order
   // caches
   std::shared_mutex hr_mu;
   std::unordered_map<uint64_t, std::vector<std::shared_ptr<const HrForest>>> hr_inline;
@@ -438,7 +440,11 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     c->row_nodes.insert(c->row_nodes.end(), per_row[r].begin(), per_row[r].end());
   }
   // useful-section statics (candidates.useful_static)
-  c->W2 = 2 * c->ws + 2 * c->wp + c->wr;
+  c->WV = 2 * c->ws + 2 * c->wp + c->wr;
+  c->W2 = c->WV + 4 * c->wp + c->wr;
+  c->spec_kind = kind;
+  c->spec_ptr = spec_ptr;
+  c->spec_idx = spec_idx;
   c->pol_static.assign(c->P, 0);
   c->set_null.assign(c->S, 0);
   for (uint32_t q = 0; q < c->P; ++q) {
@@ -499,7 +505,7 @@ struct acs_codec_batch {
   std::vector<uint8_t> rx;  // [rx_cols][rx_rows]
   uint32_t rx_cols = 1, rx_rows = 1;
   std::vector<uint32_t> cand;
-  uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0;
+  uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0, cand_wv = 0;
   std::vector<uint32_t> role_key, role_bits;
   uint32_t role_rows = 0;
   std::vector<const char*> reason;  // per request: why it goes to the host (nullptr: it does not)
@@ -1157,6 +1163,109 @@ struct Classes {
 
   // [S | P | R] row -> [S | P | useful S | useful P | R] (candidates._useful / _assemble);
   // thr: the column's throwing policies (P bits), or nullptr
+  // candidates.resource_verdicts for one column: exact true / false, RegExp true / false of
+  // an empty or entity-only target, per policy (P bits) and rule (R bits)
+  struct ResV {
+    Row p[4], r[4];
+  };
+  std::vector<std::unique_ptr<ResV>> resv;  // per column + the no-entity column
+
+  void build_resv(uint32_t ncols) {
+    resv.clear();
+    resv.resize(ncols + 1);
+    for (uint32_t c = 0; c <= ncols; ++c) {
+      auto v = std::make_unique<ResV>();
+      for (int k = 0; k < 4; ++k) {
+        v->p[k].assign(C.wp ? C.wp : 1, 0u);
+        v->r[k].assign(C.wr ? C.wr : 1, 0u);
+      }
+      const bool none = c == ncols, real = none || !col_keys[c].empty();
+      uint32_t exact_row = NONE32;
+      const uint8_t* cells = nullptr;
+      if (!none && real) {
+        const std::string& key = col_keys[c];
+        uint32_t id = key[0] == 'm' ? ID_UNDEF : key[0] == 'n' ? ID_NULL : C.lookup(std::string_view(key).substr(1));
+        if (id != NONE32) {
+          auto it = C.row_of_id.find(id);
+          if (it != C.row_of_id.end()) exact_row = it->second;
+        }
+        cells = B.rx.data() + (size_t)c * B.rx_rows;
+      }
+      const uint32_t nn = C.S + C.P + C.R;
+      for (uint32_t g = C.S; g < nn; ++g) {
+        const bool pol = g < C.S + C.P;
+        const uint32_t l = pol ? g - C.S : g - C.S - C.P;
+        Row* out = pol ? v->p : v->r;
+        const uint16_t tf = (uint16_t)C.nodes[g].tflags;
+        auto set = [&](int k) { out[k][l >> 5] |= 1u << (l & 31); };
+        if (tf & TF_RES_EMPTY) {
+          set(0);
+          set(2);
+          continue;
+        }
+        if (!(tf & TF_RES_ENT_ONLY) || !real) continue;
+        if (none) {
+          set(1);
+          set(3);
+          continue;
+        }
+        bool xt = false, em = false, thrown = false;
+        if (C.spec_kind[g] != 1)
+          for (uint32_t k = C.spec_ptr[g]; k < C.spec_ptr[g + 1]; ++k) {
+            const uint32_t row = C.spec_idx[k];
+            if (row == exact_row) xt = true;
+            const uint8_t cell = row < C.rx_pat.size() ? cells[row] : 0;
+            if (cell & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST)) thrown = true;
+            if (cell & C_RX_HIT) em = true;
+            else if (cell & C_RX_RESET) em = false;
+          }
+        set(xt ? 0 : 1);
+        if (!thrown) set(em ? 2 : 3);
+      }
+      resv[c] = std::move(v);
+    }
+  }
+
+  // the verdict sections of one class (candidates._verdicts): pc column, a action key,
+  // roles / nroles the class's sorted role rows
+  void verdicts(Row& out, uint32_t pc, uint32_t a, const int32_t* roles, int nroles, bool role_filter,
+                bool action_filter, const std::vector<std::shared_ptr<const Row>>& arow) const {
+    const ResV& rv = *resv[pc];
+    const Row& A = *arow[action_filter ? a : 1u];
+    const bool fixed = action_filter && a != 1;
+    const uint32_t nn = C.S + C.P + C.R;
+    for (uint32_t g = C.S; g < nn; ++g) {
+      const NodeRec& N = C.nodes[g];
+      if (!(N.nflags & NF_HAS_TARGET)) continue;
+      const bool pol = g < C.S + C.P;
+      const uint32_t l = pol ? g - C.S : g - C.S - C.P;
+      const Row* res = pol ? rv.p : rv.r;
+      auto rb = [&](int k) { return (res[k][l >> 5] >> (l & 31)) & 1u; };
+      const bool sub_empty = N.tflags & TF_SUBJ_EMPTY;
+      const bool sub_role = (N.tflags & TF_SUBJ_ROLE) && !sub_empty;
+      bool in = false;
+      if (sub_role && role_filter && C.node_role[g] >= 0)
+        for (int k = 0; k < nroles && !in; ++k) in = roles[k] == C.node_role[g];
+      const bool subj_t = sub_empty || (sub_role && role_filter && in);
+      const bool subj_f = sub_role && role_filter && !in;
+      const bool need = C.node_need_act[g];
+      const bool abit = (A[C.node_word(g)] & C.node_bit(g)) != 0;
+      const bool act_t = !need || (fixed && abit);
+      const bool act_f = need && fixed && !abit;
+      const bool both_t = subj_t && act_t, any_f = subj_f || act_f;
+      const bool xt = both_t && rb(0), xf = any_f || rb(1), rt = both_t && rb(2), rf = any_f || rb(3);
+      auto put = [&](uint32_t sec) { out[C.WV + sec + (l >> 5)] |= 1u << (l & 31); };
+      if (pol) {
+        if (xt) put(0);
+        if (xf) put(C.wp);
+        if (rt) put(2 * C.wp);
+        if (rf) put(3 * C.wp);
+      } else if (xt || (xf && rt)) {
+        put(4 * C.wp);
+      }
+    }
+  }
+
   Row assemble(const Row& r, const Row* thr) const {
     Row out(C.W2, 0u);
     std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
@@ -1206,6 +1315,7 @@ void Classes::run() {
   B.cand_wsu = C.ws + C.wp;
   B.cand_wpu = 2 * C.ws + C.wp;
   B.cand_wr = 2 * C.ws + 2 * C.wp;
+  B.cand_wv = C.WV;
   // primary column per request (candidates.primary_columns)
   std::vector<uint32_t> pcol(n, ncols);
   std::vector<uint8_t> active(n, 0);
@@ -1247,6 +1357,7 @@ void Classes::run() {
     }
     ent[ncols] = std::make_shared<Row>(C.always_bits);
   }
+  build_resv(ncols);
   // per column: policies whose target reads a throwing (or host) RegExp cell (candidates.throw_policies)
   std::vector<std::unique_ptr<Row>> thr(ncols + 1);
   for (uint32_t c = 0; c < ncols; ++c) {
@@ -1351,6 +1462,8 @@ void Classes::run() {
         rows[k] = assemble(class_row(pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter, ent,
                                      arow),
                            pcol[i] < ncols ? thr[pcol[i]].get() : nullptr);
+        verdicts(rows[k], pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter,
+                 action_filter, arow);
       }
     };
     std::vector<std::thread> pool;
@@ -1424,7 +1537,10 @@ void Classes::run() {
       Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
       for (uint32_t w = 0; w < C.W; ++w) r[w] &= valid[w];
       sets_need_policies(r);
-      const Row o = assemble(r, &thr_any);
+      Row o = assemble(r, &thr_any);
+      for (uint32_t q = 0; q < C.P; ++q)
+        for (int k = 0; k < 4; ++k) o[C.WV + k * C.wp + (q >> 5)] |= 1u << (q & 31);
+      for (uint32_t x = 0; x < C.R; ++x) o[C.WV + 4 * C.wp + (x >> 5)] |= 1u << (x & 31);
       std::copy(o.begin(), o.end(), B.role_bits.begin() + k * W);
     }
     B.role_key = std::move(rkey);
@@ -1690,6 +1806,7 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
   v.cand_wr = b->cand_wr;
   v.cand_wsu = b->cand_wsu;
   v.cand_wpu = b->cand_wpu;
+  v.cand_wv = b->cand_wv;
   v.cand_rows = b->cand_rows;
   if (!b->role_key.empty()) {
     v.role_key = b->role_key.data();

@@ -128,6 +128,7 @@ struct Batch {
   uint32_t cand_words, cand_wp, cand_wr;  // row length, word offsets of the policy / rule sections
   uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
   uint32_t cand_wsu, cand_wpu;  // isAllowed's useful sets / policies sections (0: absent)
+  uint32_t cand_wv;             // target-verdict sections (0: absent)
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
@@ -146,6 +147,8 @@ struct Filter {
   uint32_t nlist, W, nroles, lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   uint32_t wsu, wpu;       // isAllowed: useful sets / loop-2b policies (0 / wp without them)
+  uint32_t wv;             // target-verdict sections (candidates.verdict_offset)
+  bool vok;                // the verdicts apply: the row is this request's own class row
   bool all;                // no filtering
   ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
     uint32_t x = cand[(size_t)c * W + w];
@@ -179,7 +182,8 @@ struct Filter {
 // long-lived scalar state stays small.
 // FilterAll: the batch carries no candidate rows — every node is a candidate.
 struct FilterAll {
-  uint32_t wp, wr, wsu, wpu;
+  uint32_t wp, wr, wsu, wpu, wv;
+  bool vok;  // always false: no class rows
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
 };
 
@@ -187,7 +191,8 @@ struct FilterAll {
 // kernel before any lane diverges (all ones for a wave holding an unfiltered request).
 struct FilterLds {
   const uint32_t* lds;
-  uint32_t wp, wr, wsu, wpu;
+  uint32_t wp, wr, wsu, wpu, wv;
+  bool vok;  // every lane of the wave has the same class: the row's verdicts are each lane's
   ACS_FN uint32_t word(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
@@ -225,6 +230,14 @@ struct CandRange {
 };
 
 ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
+
+// Bit i of the target-verdict section at word `sec` past F.wv (candidates.verdict_offset):
+// policies known exact-true (sec 0), exact-false (WP), RegExp-true (2 WP), RegExp-false
+// (3 WP), rules whose retried match is known true (4 WP); WP = ceil(P / 32).
+template <class FL>
+ACS_FN bool verdict(const FL& F, uint32_t sec, uint32_t i) {
+  return (F.word(F.wv + sec + (i >> 5)) >> (i & 31)) & 1u;
+}
 
 // tri-state result: 1 true, 0 false, <0 -ErrKind (the reference throws)
 typedef int tri;
@@ -768,6 +781,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
 template <class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   const Tables& T = R.T;
+  const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;
@@ -793,7 +807,9 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
         const NodeRec P = node_at(T, T.pols, p, T.n_pols);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
-          const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
+          const tri m = (F.vok && verdict(F, 0, p)) ? 1
+                      : (F.vok && verdict(F, WP, p)) ? 0
+                      : target_match(P, R, P.pe_at, false, false, nullptr);
           if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
@@ -820,7 +836,12 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
         PROF_T0(tp);
-        const tri m = target_match(P, R, pe, !exact, false, nullptr);
+        bool kt = false, kf = false;  // the class's verdict for this lane's mode
+        if (F.vok) {
+          kt = exact ? verdict(F, 0, p) : verdict(F, 2 * WP, p);
+          kf = exact ? verdict(F, WP, p) : verdict(F, 3 * WP, p);
+        }
+        const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
         if (m < 0) return make_err(m, s + 1);
         if (!m) {
           PROF_ADD(PH_POL_TARGET, tp);
@@ -846,7 +867,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
           PROF_T0(tr);
-          m = target_match_retry(Q, R, Q.effect, false, nullptr);
+          m = (F.vok && verdict(F, 4 * WP, r)) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
           if (m < 0) return make_err(m, s + 1);
           PROF_ADD(PH_RULE_TARGET, tr);
           if (!m) continue;
@@ -919,9 +940,11 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   F.wr = B.cand_wr;
   F.wsu = B.cand_wsu;
   F.wpu = B.cand_wpu ? B.cand_wpu : B.cand_wp;
+  F.wv = B.cand_wv;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
   F.row[0] = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
+  F.vok = !F.all && B.cand_wv != 0;  // the request's own class row
   return F;
 }
 

@@ -222,6 +222,8 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   F.wr = B.cand_wr;
   F.wsu = B.cand_wsu;
   F.wpu = B.cand_wpu ? B.cand_wpu : B.cand_wp;
+  F.wv = B.cand_wv;
+  F.vok = false;  // the long-row form keeps no per-class verdicts
   F.cand = B.cand;
   F.rbits = B.role_bits;
   F.nroles = B.role_key ? B.role_rows : 0u;
@@ -271,11 +273,12 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
 // The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
 // W-word LDS region, all ones when the wave holds an unfiltered request.
 __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp};
+  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, false};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
   bool all = false;
+  uint32_t first_cls = PCOL_ALL, classes = 0;
   for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
   uint64_t pending = __ballot(valid);
   while (pending) {
@@ -288,15 +291,21 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : nullptr;
     for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
+    if (c != first_cls) {
+      first_cls = c;
+      ++classes;
+    }
     pending &= ~__ballot(valid && key == k);
   }
   if (all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
+  // one class in the wave (role keys may differ: role rows keep the verdict sections whole)
+  F.vok = !all && classes == 1 && B.cand_wv != 0;
   return F;
 }
 
 __device__ inline FilterAll wave_filter_all(const Batch& B) {
-  return FilterAll{B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp};
+  return FilterAll{B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, 0u, false};
 }
 
 // One maker per filter form, selected by the kernel's template argument.
@@ -664,6 +673,12 @@ static Batch to_batch(const acs_req_batch* b) {
   B.cand_wr = b->cand_wr;
   B.cand_wsu = b->cand_wsu;
   B.cand_wpu = b->cand_wpu;
+  B.cand_wv = b->cand_wv;
+  static const bool no_verdicts = [] {  // A/B runs: ACS_NO_VERDICTS=1 matches every target
+    const char* e = getenv("ACS_NO_VERDICTS");
+    return e && *e == '1';
+  }();
+  if (no_verdicts) B.cand_wv = 0;
   static const bool no_useful = [] {  // A/B runs: ACS_NO_USEFUL=1 walks the candidate sections
     const char* e = getenv("ACS_NO_USEFUL");
     return e && *e == '1';

@@ -86,7 +86,8 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
         b->cand_words < b->cand_wr + words32(n_rules))
       return bad("batch: candidate row layout", b->cand_words);
     if ((b->cand_wsu && b->cand_wsu + words32(n_sets) > b->cand_words) ||
-        (b->cand_wpu && b->cand_wpu + words32(n_pols) > b->cand_words))
+        (b->cand_wpu && b->cand_wpu + words32(n_pols) > b->cand_words) ||
+        (b->cand_wv && (uint64_t)b->cand_wv + 4ull * words32(n_pols) + words32(n_rules) > b->cand_words))
       return bad("batch: candidate row layout", b->cand_words);
     if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
   }

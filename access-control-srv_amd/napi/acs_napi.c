@@ -25,7 +25,7 @@
  *   whatIsAllowedObl(tables, batch, idx, chunks, cap) -> {obl, oblN}
  *   wordsPerRequest(tables), layoutSizes(), deviceCount(), lastError()
  * `batch` = an encode() handle, or a plain object {n, hdr, res, subj, act, roles, arena,
- * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, candWsu, candWpu, roleKey, roleRowsBits,
+ * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, candWsu, candWpu, candWv, roleKey, roleRowsBits,
  * roleRows]} of typed arrays in the layout of csrc/acs_layout.h; every array is checked
  * against the sizes `n` and the counts imply before the library reads it.
  *
@@ -269,7 +269,7 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
       prop_u32(env, v, "candWords", &b->cand_words) || prop_u32(env, v, "candWp", &b->cand_wp) ||
       prop_u32(env, v, "candWr", &b->cand_wr) || prop_u32(env, v, "candRows", &b->cand_rows) ||
       prop_u32(env, v, "roleRows", &b->role_rows) || prop_u32(env, v, "candWsu", &b->cand_wsu) ||
-      prop_u32(env, v, "candWpu", &b->cand_wpu))
+      prop_u32(env, v, "candWpu", &b->cand_wpu) || prop_u32(env, v, "candWv", &b->cand_wv))
     return -1;
   if (field(env, v, "hdr", n * HDR_B, n > 0, &b->hdr, NULL, &bad) ||
       field(env, v, "res", n * QMAX * RES_B, n > 0, &b->res, NULL, &bad) ||
@@ -290,8 +290,8 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
   if (field(env, v, "cand", (size_t)b->cand_rows * b->cand_words * 4, 0, &p, &len, &bad)) goto fail;
   b->cand = (const uint32_t*)p;
   if (b->cand && (b->cand_wp > b->cand_words || b->cand_wr > b->cand_words || b->cand_wsu > b->cand_words ||
-                  b->cand_wpu > b->cand_words)) {
-    bad = "candWp / candWr / candWsu / candWpu";
+                  b->cand_wpu > b->cand_words || b->cand_wv > b->cand_words)) {
+    bad = "candWp / candWr / candWsu / candWpu / candWv";
     goto fail;
   }
   if (field(env, v, "roleKey", 0, 0, &p, &len, &bad)) goto fail;

@@ -57,11 +57,14 @@ typedef struct {
    * required roles x action, acs_mi355x/candidates.py); the class id is in ReqHdr.flags >> 16.
    * Sections (word offsets): candidate sets at 0, candidate policies at cand_wp, candidate
    * rules at cand_wr, and — isAllowed only, 0 when absent — the sets / policies that can
-   * change an isAllowed result at cand_wsu / cand_wpu.  NULL = evaluate every node. */
+   * change an isAllowed result at cand_wsu / cand_wpu, and the class's target verdicts at
+   * cand_wv: policies whose exact / RegExp target match is known true / false (4 sections
+   * of ceil(P/32) words), then rules whose retried match is known true (ceil(R/32) words).
+   * NULL = evaluate every node. */
   const uint32_t* cand;
   uint32_t cand_words, cand_wp, cand_wr;
   uint32_t cand_rows;
-  uint32_t cand_wsu, cand_wpu;
+  uint32_t cand_wsu, cand_wpu, cand_wv;
   /* Optional role factor (large stores, where class rows keyed by roles would not fit):
    * [role_rows][cand_words] bitsets of the nodes a request with that role-association set
    * can reach (checkSubjectMatches, accessController.ts:793-823), AND-ed with the class

@@ -11,7 +11,7 @@ const rd = (f) => { const b = fs.readFileSync(path.join(dir, f)); return new Uin
 const meta = JSON.parse(fs.readFileSync(path.join(dir, 'meta.json'), 'utf8'));
 const batch = { n: meta.n, rxCols: meta.rxCols, rxRows: meta.rxRows, candWords: meta.candWords,
                 candWp: meta.candWp, candWr: meta.candWr, candRows: meta.candRows,
-                candWsu: meta.candWsu, candWpu: meta.candWpu };
+                candWsu: meta.candWsu, candWpu: meta.candWpu, candWv: meta.candWv };
 for (const k of ['hdr', 'res', 'subj', 'act', 'roles', 'arena', 'rx', 'cand']) batch[k] = rd(k + '.bin');
 
 (async () => {

@@ -55,6 +55,7 @@ static Batch host_batch(const acs_req_batch* b) {
   B.cand_wr = b->cand_wr;
   B.cand_wsu = b->cand_wsu;
   B.cand_wpu = b->cand_wpu;
+  B.cand_wv = b->cand_wv;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;

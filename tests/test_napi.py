@@ -46,6 +46,7 @@ def _dump(tmp, cs, b):
     tmp.joinpath("meta.json").write_text(json.dumps({
         "n": b.n, "rxCols": int(b.rx.shape[0]), "rxRows": int(b.rx_rows), "candWords": int(b.cand.shape[1]),
         "candWp": int(b.cand_wp), "candWr": int(b.cand_wr), "candWsu": int(b.cand_wsu), "candWpu": int(b.cand_wpu),
+        "candWv": int(b.cand_wv),
         "candRows": int(b.cand.shape[0])}))
 
 
