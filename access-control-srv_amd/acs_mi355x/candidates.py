@@ -473,8 +473,13 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
                                              res[1])
                 verdicts = (pxt, pxf, prt, prf, rxt | (rxf & rrt))
             out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs, verdicts)
-        # requests whose rows are identical share one class
-        urows, rinv = _unique_rows(out)
+        # requests whose filter sections are identical share one class; its verdicts are
+        # the ones every key of the class agrees on (AND), so verdicts never split a class
+        wv = verdict_offset(cs)
+        ubase, rinv = _unique_rows(out[:, :wv])
+        ver = np.full((len(ubase), W - wv), 0xFFFFFFFF, np.uint32)
+        np.bitwise_and.at(ver, rinv, out[:, wv:])
+        urows = np.concatenate([ubase, ver], axis=1)
         if len(urows) <= MAX_CLASSES or level == "entity":
             break
     if len(urows) > MAX_CLASSES:  # entity level: at most one class per entity column (< 0xFFFE)

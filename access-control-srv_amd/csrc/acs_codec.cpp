@@ -1470,15 +1470,17 @@ void Classes::run() {
     for (int t = 1; t < threads && (size_t)t < nk; ++t) pool.emplace_back(work);
     work();
     for (auto& th : pool) th.join();
-    // identical rows share a class; heaviest (most candidate nodes) first
+    // rows with identical filter sections share a class; its verdict sections are the AND
+    // over its keys (candidates.classes); heaviest (most candidate nodes) first
+    const uint32_t WV = C.WV;
     std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
     std::vector<uint32_t> urow_of_key(nk), urows;
     for (size_t k = 0; k < nk; ++k) {
-      const uint64_t h = row_hash(rows[k].data(), W);
+      const uint64_t h = row_hash(rows[k].data(), WV);
       auto& bucket = by_hash[h];
       uint32_t u = NONE32;
       for (uint32_t x : bucket)
-        if (rows[urows[x]] == rows[k]) {
+        if (std::equal(rows[urows[x]].begin(), rows[urows[x]].begin() + WV, rows[k].begin())) {
           u = x;
           break;
         }
@@ -1486,6 +1488,9 @@ void Classes::run() {
         u = (uint32_t)urows.size();
         urows.push_back((uint32_t)k);
         bucket.push_back(u);
+      } else {
+        Row& acc = rows[urows[u]];
+        for (uint32_t w = WV; w < W; ++w) acc[w] &= rows[k][w];
       }
       urow_of_key[k] = u;
     }
