@@ -129,6 +129,7 @@ struct Batch {
   uint32_t cand_rows;     // number of request classes (class ids >= cand_rows: unfiltered)
   uint32_t cand_wsu, cand_wpu;  // isAllowed's useful sets / policies sections (0: absent)
   uint32_t cand_wv;             // target-verdict sections (0: absent)
+  uint32_t no_verdicts;         // A/B runs (ACS_NO_VERDICTS=1): K1 ignores the verdicts
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
@@ -150,6 +151,10 @@ struct Filter {
   uint32_t wv;             // target-verdict sections (candidates.verdict_offset)
   bool vok;                // the verdicts apply: the row is this request's own class row
   bool all;                // no filtering
+  // bit i of the verdict section at word `sec` past wv (false when the verdicts do not apply)
+  ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
+    return vok && ((row[0][wv + sec + (i >> 5)] >> (i & 31)) & 1u);
+  }
   ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
     uint32_t x = cand[(size_t)c * W + w];
     if (rk < nroles) x &= rbits[(size_t)rk * W + w];
@@ -182,9 +187,9 @@ struct Filter {
 // long-lived scalar state stays small.
 // FilterAll: the batch carries no candidate rows — every node is a candidate.
 struct FilterAll {
-  uint32_t wp, wr, wsu, wpu, wv;
-  bool vok;  // always false: no class rows
+  uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
+  ACS_FN bool verdict(uint32_t, uint32_t) const { return false; }  // no class rows
 };
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
@@ -192,7 +197,6 @@ struct FilterAll {
 struct FilterLds {
   const uint32_t* lds;
   uint32_t wp, wr, wsu, wpu, wv;
-  bool vok;  // every lane of the wave has the same class: the row's verdicts are each lane's
   ACS_FN uint32_t word(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
@@ -201,6 +205,8 @@ struct FilterLds {
     return lds[w];
 #endif
   }
+  // the kernel zeroes the verdict sections of a wave that mixes classes
+  ACS_FN bool verdict(uint32_t sec, uint32_t i) const { return (word(wv + sec + (i >> 5)) >> (i & 31)) & 1u; }
 };
 
 // Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
@@ -231,13 +237,14 @@ struct CandRange {
 
 ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
 
-// Bit i of the target-verdict section at word `sec` past F.wv (candidates.verdict_offset):
-// policies known exact-true (sec 0), exact-false (WP), RegExp-true (2 WP), RegExp-false
-// (3 WP), rules whose retried match is known true (4 WP); WP = ceil(P / 32).
-template <class FL>
-ACS_FN bool verdict(const FL& F, uint32_t sec, uint32_t i) {
-  return (F.word(F.wv + sec + (i >> 5)) >> (i & 31)) & 1u;
-}
+#ifndef ACS_POLICY_VERDICTS
+#define ACS_POLICY_VERDICTS 1  // K1 also skips policy target matching on known verdicts
+#endif
+
+// Target verdicts, F.verdict(sec, i) (candidates.verdict_offset): bit i of the section at
+// word `sec` past the verdict base — policies known exact-true (sec 0), exact-false (WP),
+// RegExp-true (2 WP), RegExp-false (3 WP), rules whose retried match is known true (4 WP);
+// WP = ceil(P / 32).  False wherever the class's verdicts do not apply.
 
 // tri-state result: 1 true, 0 false, <0 -ErrKind (the reference throws)
 typedef int tri;
@@ -807,9 +814,11 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
         const NodeRec P = node_at(T, T.pols, p, T.n_pols);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
-          const tri m = (F.vok && verdict(F, 0, p)) ? 1
-                      : (F.vok && verdict(F, WP, p)) ? 0
-                      : target_match(P, R, P.pe_at, false, false, nullptr);
+#if ACS_POLICY_VERDICTS
+          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
+#else
+          const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
+#endif
           if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
@@ -836,11 +845,13 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       bool psm = true;
       if (P.nflags & NF_HAS_TARGET) {
         PROF_T0(tp);
-        bool kt = false, kf = false;  // the class's verdict for this lane's mode
-        if (F.vok) {
-          kt = exact ? verdict(F, 0, p) : verdict(F, 2 * WP, p);
-          kf = exact ? verdict(F, WP, p) : verdict(F, 3 * WP, p);
-        }
+        // the class's verdict for this lane's mode
+#if ACS_POLICY_VERDICTS
+        const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
+        const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
+#else
+        const bool kt = false, kf = false;
+#endif
         const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
         if (m < 0) return make_err(m, s + 1);
         if (!m) {
@@ -867,7 +878,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
           PROF_T0(tr);
-          m = (F.vok && verdict(F, 4 * WP, r)) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
+          m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
           if (m < 0) return make_err(m, s + 1);
           PROF_ADD(PH_RULE_TARGET, tr);
           if (!m) continue;

@@ -273,7 +273,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
 // The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
 // W-word LDS region, all ones when the wave holds an unfiltered request.
 __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, false};
+  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
@@ -299,13 +299,16 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
   }
   if (all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
-  // one class in the wave (role keys may differ: role rows keep the verdict sections whole)
-  F.vok = !all && classes == 1 && B.cand_wv != 0;
+  // the verdicts hold for a wave of one class (role keys may differ: role rows keep the
+  // verdict sections whole); any other wave reads zeros there (the LDS form is only chosen
+  // for batches that carry verdict sections)
+  if (all || classes != 1 || B.no_verdicts)
+    for (uint32_t w = B.cand_wv + lane; w < W; w += 64) lds[w] = 0u;
   return F;
 }
 
 __device__ inline FilterAll wave_filter_all(const Batch& B) {
-  return FilterAll{B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, 0u, false};
+  return FilterAll{B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp};
 }
 
 // One maker per filter form, selected by the kernel's template argument.
@@ -510,7 +513,7 @@ FilterForm filter_form(const Batch& B) {
   }();
   if (general) return FilterForm::General;
   if (!B.cand) return FilterForm::All;
-  return B.cand_words <= LDS_FILTER_WORDS ? FilterForm::Lds : FilterForm::General;
+  return B.cand_words <= LDS_FILTER_WORDS && B.cand_wv ? FilterForm::Lds : FilterForm::General;
 }
 
 #define ACS_LAUNCH_FILTERED(kernel, grid, lds, stream, form, ...)                                       \
@@ -678,7 +681,7 @@ static Batch to_batch(const acs_req_batch* b) {
     const char* e = getenv("ACS_NO_VERDICTS");
     return e && *e == '1';
   }();
-  if (no_verdicts) B.cand_wv = 0;
+  B.no_verdicts = no_verdicts ? 1u : 0u;
   static const bool no_useful = [] {  // A/B runs: ACS_NO_USEFUL=1 walks the candidate sections
     const char* e = getenv("ACS_NO_USEFUL");
     return e && *e == '1';
