@@ -486,7 +486,8 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
         raise ValueError("too many request classes")
     # heaviest classes first: the kernel's sort key orders waves by class id, so the longest
     # waves are dispatched first (longest-processing-time-first; no tail of heavy waves)
-    cost = np.unpackbits(urows.view(np.uint8), axis=1).sum(axis=1)
+    # (the filter sections only: the verdicts are not work)
+    cost = np.unpackbits(np.ascontiguousarray(urows[:, :verdict_offset(cs)]).view(np.uint8), axis=1).sum(axis=1)
     rank = np.empty(len(cost), np.int64)
     rank[np.argsort(-cost, kind="stable")] = np.arange(len(cost))
     urows = np.ascontiguousarray(urows[np.argsort(rank)])

@@ -1502,7 +1502,7 @@ void Classes::run() {
     std::vector<uint32_t> cost(urows.size()), order(urows.size()), rank(urows.size());
     for (size_t u = 0; u < urows.size(); ++u) {
       uint32_t c = 0;
-      for (uint32_t w = 0; w < W; ++w) c += (uint32_t)__builtin_popcount(rows[urows[u]][w]);
+      for (uint32_t w = 0; w < WV; ++w) c += (uint32_t)__builtin_popcount(rows[urows[u]][w]);  // filter sections
       cost[u] = c;
       order[u] = (uint32_t)u;
     }

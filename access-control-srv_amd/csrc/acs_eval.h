@@ -206,7 +206,15 @@ struct FilterLds {
 #endif
   }
   // the kernel zeroes the verdict sections of a wave that mixes classes
-  ACS_FN bool verdict(uint32_t sec, uint32_t i) const { return (word(wv + sec + (i >> 5)) >> (i & 31)) & 1u; }
+  ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
+#if defined(ACS_NO_VERDICT_CODE)  // A/B builds: the traversal without any verdict lookup
+    (void)sec;
+    (void)i;
+    return false;
+#else
+    return (word(wv + sec + (i >> 5)) >> (i & 31)) & 1u;
+#endif
+  }
 };
 
 // Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
