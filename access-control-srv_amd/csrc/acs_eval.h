@@ -1050,6 +1050,7 @@ template <class RQ, class Sink, class FL>
 ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL, Sink& bits, OblLog& obl,
                                   uint32_t s_begin = 0, uint32_t s_end = NONE32) {
   const Tables& T = R.T;
+  const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
   Decision out{};
   CandRange sets(F, 0, s_begin, s_end < T.n_sets ? s_end : T.n_sets);
   uint32_t s;
@@ -1069,7 +1070,8 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         const NodeRec P = node_at(T, T.pols, p, T.n_pols);
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
-          const tri m = target_match(P, R, P.pe_at, false, true, &obl);
+          // a verdict-known target has no property attribute, so it pushes no obligation
+          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, true, &obl);
           if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
@@ -1091,7 +1093,9 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
-        const tri m = target_match(P, R, pe, !exact, true, &obl);
+        const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
+        const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
+        const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, true, &obl);
         if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
       }
@@ -1103,7 +1107,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
-          m = target_match_retry(Q, R, Q.effect, true, &obl);
+          m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, true, &obl);
           if (m < 0) return make_err(m, s + 1);
         }
         if (m) {
