@@ -344,7 +344,9 @@ struct ReqCtx {
 // Resource attributes staged in LDS by the kernel (slots < LDS_SLOTS, column = lane,
 // stride = block size): dynamic indexing without scratch, one ds_read_b128 per use.
 #ifndef ACS_LDS_SLOTS
-#define ACS_LDS_SLOTS 8
+// 6 x 16 B x 256 lanes = 24 KB: with a c3 filter row (832 words x 4 waves, 13 KB) a block
+// fits 4 times into the CU's 160 KB of LDS (8 slots: 3 blocks; A/B c3 20.6 -> 17.6 ms)
+#define ACS_LDS_SLOTS 6
 #endif
 constexpr int LDS_SLOTS = ACS_LDS_SLOTS;
 
