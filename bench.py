@@ -78,7 +78,8 @@ def scan_bytes(cs, batch, wave=64):
     role-factor row) filters (an unfiltered class: the whole table).  K1 walks the useful
     sets; inside one, loop 2a scans the candidate policies and loop 2b the useful ones; a
     rule is visited only inside a loop-2b policy.  Each record counts once per wave (a policy
-    read by both loops, once).  Returns total bytes."""
+    read by both loops, once); a node whose target verdict the class row carries (one-class
+    waves) counts its record only, its pairs and attributes are not read.  Returns total bytes."""
     from acs_mi355x import layout as L, candidates
     n = batch.n
     cand = batch.cand
@@ -103,6 +104,9 @@ def scan_bytes(cs, batch, wave=64):
     full = int(bs.sum() + bp.sum() + br.sum())
     wp, wsu, wpu, wr, _ = candidates.row_layout(cs)
     useful = getattr(batch, "cand_wsu", 0) != 0
+    wv = getattr(batch, "cand_wv", 0)
+    WP = (npol + 31) // 32
+    rec = 64  # a verdict-known target is not matched: only its record is read
     cache = {}
 
     def union_bytes(key):
@@ -123,7 +127,14 @@ def scan_bytes(cs, batch, wave=64):
         p2a = bits[32 * wp:32 * wp + npol] & s[par_p]
         p2b = (bits[32 * wpu:32 * wpu + npol] if useful else bits[32 * wp:32 * wp + npol]) & s[par_p]
         r = bits[32 * wr:32 * wr + nr] & p2b[par_r]
-        v = int(bs[s].sum() + bp[p2a | p2b].sum() + br[r].sum())
+        pk = np.zeros(npol, bool)
+        rk = np.zeros(nr, bool)
+        if wv and len({k >> 16 for k in key}) == 1:  # K1 reads the class's verdicts (one-class waves)
+            pv = [bits[32 * (wv + k * WP):32 * (wv + k * WP) + npol] for k in range(4)]
+            pk = (pv[0] | pv[1]) & (pv[2] | pv[3])
+            rk = bits[32 * (wv + 4 * WP):32 * (wv + 4 * WP) + nr]
+        pp = p2a | p2b
+        v = int(bs[s].sum() + np.where(pk, rec, bp)[pp].sum() + np.where(rk, rec, br)[r].sum())
         cache[key] = v
         return v
 
