@@ -130,22 +130,40 @@ struct Batch {
   uint32_t cand_wsu, cand_wpu;  // isAllowed's useful sets / policies sections (0: absent)
   uint32_t cand_wv;             // target-verdict sections (0: absent)
   uint32_t no_verdicts;         // A/B runs (ACS_NO_VERDICTS=1): K1 ignores the verdicts
+  uint32_t lds_pref;            // long rows (> LDS row capacity): words of the wave's LDS union prefix
+  uint32_t role_major;          // coherence sort key [role key | class] instead of [class | role key]
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
 };
 
-// Candidate filter of a wave (GPU: the union of its lanes' class rows, gathered with
-// ballots; host build: the request's own row).  Wave-uniform by construction; the rows
-// are explicit pointers (no dynamically indexed array, so the filter stays in SGPRs).
+// OR of x over the wave's ACTIVE lanes, returned in an SGPR.  A lane drops out once its bits
+// are covered, so the loop runs once per lane that still adds bits (lanes sharing a row
+// share the value: a few rounds).  Host build: x itself (one request).
+ACS_FN uint32_t wave_or(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t acc = 0;
+  uint64_t pend = __ballot(x != 0u);
+  while (pend) {
+    acc |= __builtin_amdgcn_readlane(x, __builtin_ctzll(pend));
+    pend &= ~__ballot((x & ~acc) == 0u);
+  }
+  return acc;
+#else
+  return x;
+#endif
+}
+
+// General candidate filter (rows longer than the LDS row form takes, and the host build).
+// Each lane holds pointers to its own request's rows.  GPU: words below lds_n come from the
+// wave's OR row in LDS (built before any lane diverges); a later word is the OR of the
+// ACTIVE lanes' own words — the lanes still inside the loop that asks for it, which is all
+// the iteration needs (lanes that returned or skipped the enclosing policy read nothing).
 struct Filter {
-  const uint32_t* row[4];  // class rows (nullptr: unused)
-  const uint32_t* rrow[4]; // role-factor rows AND-ed with row[k] (nullptr: none)
-  const uint32_t* lds;     // GPU: the wave's OR of all its (class & role) rows, words [0, lds_n), in LDS
-  const uint32_t* list;    // GPU, rows too long for LDS: the wave's > 4 (class, role key) pairs, in LDS
-  const uint32_t* cand;    // ... and the row tables they index ([C][W], [role_rows][W])
-  const uint32_t* rbits;
-  uint32_t nlist, W, nroles, lds_n;
+  const uint32_t* row;     // this request's class row
+  const uint32_t* rrow;    // its role-factor row (== row when the batch has no role factor)
+  const uint32_t* lds;     // GPU: the wave's OR of its (class & role) rows, words [0, lds_n)
+  uint32_t lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   uint32_t wsu, wpu;       // isAllowed: useful sets / loop-2b policies (0 / wp without them)
   uint32_t wv;             // target-verdict sections (candidates.verdict_offset)
@@ -153,32 +171,15 @@ struct Filter {
   bool all;                // no filtering
   // bit i of the verdict section at word `sec` past wv (false when the verdicts do not apply)
   ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
-    return vok && ((row[0][wv + sec + (i >> 5)] >> (i & 31)) & 1u);
-  }
-  ACS_FN uint32_t pair_word(uint32_t c, uint32_t rk, uint32_t w) const {
-    uint32_t x = cand[(size_t)c * W + w];
-    if (rk < nroles) x &= rbits[(size_t)rk * W + w];
-    return x;
+    return vok && ((row[wv + sec + (i >> 5)] >> (i & 31)) & 1u);
   }
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
-    if (lds && w < lds_n) return wave_uniform(((lds_u32*)lds)[w]);
-    if (list) {  // OR of every (class & role) row of the wave, word by word (large stores, mixed waves)
-      uint32_t x = 0;
-      for (uint32_t k = 0; k < nlist; ++k) {
-        const uint32_t key = wave_uniform(((lds_u32*)list)[k]);
-        x |= pair_word(key >> 16, key & 0xFFFFu, w);
-      }
-      return wave_uniform(x);
-    }
+    if (w < lds_n) return wave_uniform(((lds_u32*)lds)[w]);
 #endif
-    uint32_t x = row[0][w] & (rrow[0] ? rrow[0][w] : ~0u);
-    if (row[1]) x |= row[1][w] & (rrow[1] ? rrow[1][w] : ~0u);
-    if (row[2]) x |= row[2][w] & (rrow[2] ? rrow[2][w] : ~0u);
-    if (row[3]) x |= row[3][w] & (rrow[3] ? rrow[3][w] : ~0u);
-    return wave_uniform(x);
+    return wave_or(row[w] & rrow[w]);
   }
 };
 
@@ -964,14 +965,14 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   F.wv = B.cand_wv;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
-  F.row[0] = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
+  F.row = F.rrow = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
   F.vok = !F.all && B.cand_wv != 0;  // the request's own class row
   return F;
 }
 
 ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h, uint32_t i) {
   Filter F = request_filter(B, h);
-  if (!F.all && B.role_key && B.role_key[i] < B.role_rows) F.rrow[0] = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
+  if (!F.all && B.role_key && B.role_key[i] < B.role_rows) F.rrow = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
   return F;
 }
 

@@ -48,8 +48,10 @@ constexpr int BLOCK = 256;
 // id.  The low field keeps `lowbits` bits (role keys are dense, so all of them; action and
 // entity ids are folded mod 2^lowbits): fewer key bits, fewer radix passes.  A fold
 // collision only merges two groups, which costs coherence, never correctness: results are
-// written to out[perm[k]], so any permutation gives the same records.
-__device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits) {
+// written to out[perm[k]], so any permutation gives the same records.  With a role factor
+// and B.role_major the fields swap ([role key | bucket], `cbits` bucket bits): a wave then
+// spans few role keys, and the role rows prune rules hardest (large stores).
+__device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits, uint32_t cbits) {
   const ReqHdr h = B.hdr[k];
   const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
   uint32_t low = B.role_key ? B.role_key[k] : (h.nact ? B.act[k].value : 0u), bucket = cls + 1;
@@ -63,7 +65,8 @@ __device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits
       }
     }
   }
-  return (bucket << lowbits) | (low & ((1u << lowbits) - 1u));
+  low &= (1u << lowbits) - 1u;
+  return B.role_major ? (low << cbits) | bucket : (bucket << lowbits) | low;
 }
 
 // ---------------------------------------------------------------- LSD radix sort
@@ -84,7 +87,7 @@ constexpr uint32_t RADIX = 256;
 constexpr uint32_t SCAN_GROUP = 64;                   // tiles per tile-scan group
 
 __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_null, const Batch* B,
-                                      uint32_t lowbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
+                                      uint32_t lowbits, uint32_t cbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
                                       uint32_t shift, uint32_t* counts) {
   hist[threadIdx.x] = 0;
   __syncthreads();
@@ -94,7 +97,7 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
     if (i >= n) break;
     uint32_t key;
     if (B) {
-      key = sort_key(*B, i, lowbits);
+      key = sort_key(*B, i, lowbits, cbits);
       keys_out[i] = key;
       idx_out[i] = i;
     } else {
@@ -106,16 +109,17 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
   counts[(size_t)blockIdx.x * RADIX + threadIdx.x] = hist[threadIdx.x];
 }
 
-__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t* __restrict__ keys,
-                                                          uint32_t* __restrict__ idx, uint32_t* __restrict__ counts) {
+__global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t cbits,
+                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ idx,
+                                                          uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[RADIX];
-  tile_histogram(hist, nullptr, &B, lowbits, keys, idx, B.n, 0, counts);
+  tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts);
 }
 
 __global__ __launch_bounds__(BLOCK) void radix_histogram_kernel(const uint32_t* __restrict__ keys, uint32_t n,
                                                                 uint32_t shift, uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[RADIX];
-  tile_histogram(hist, keys, nullptr, 0, nullptr, nullptr, n, shift, counts);
+  tile_histogram(hist, keys, nullptr, 0, 0, nullptr, nullptr, n, shift, counts);
 }
 
 __global__ __launch_bounds__(RADIX) void radix_tile_scan_kernel(uint32_t* __restrict__ counts, uint32_t nt,
@@ -201,44 +205,43 @@ __global__ __launch_bounds__(BLOCK) void radix_scatter_kernel(const uint32_t* __
   }
 }
 
-// Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS; for longer rows
-// (large stores) a LDS_PREFIX_WORDS union prefix (sets + policies at c5) and a 64-entry
-// (class, role key) list for the rest — 8 KB per 256-thread block, so the block's LDS
-// (32 KB attribute staging + filter) still allows 4 blocks per CU.
+// Dynamic LDS per wave: one W-word union row when W <= LDS_FILTER_WORDS (the FilterLds
+// form); for longer rows (large stores) a B.lds_pref-word union prefix — the set and policy
+// sections, at most LDS_FILTER_WORDS — while rule words come from the lanes' own rows.
 constexpr uint32_t LDS_FILTER_WORDS = 1024;
-constexpr uint32_t LDS_PREFIX_WORDS = 448;
-constexpr uint32_t LDS_LIST_WORDS = 64;
+#ifndef ACS_SORT_ROLE_MAJOR_DEFAULT
+#define ACS_SORT_ROLE_MAJOR_DEFAULT 1  // c5 A/B: 269 ms class-major, 244 ms role-major (r02_h)
+#endif
 // Candidate filter of a wave, built with every lane present before any lane diverges.  A
 // request's row is its class row, AND-ed with its role-factor row when the batch has one.
-// With an LDS row (`lds` = this wave's W-word region, W <= LDS_FILTER_WORDS) the filter is
-// the OR of the rows of all the wave's active requests, however many (class, role key)
-// pairs the wave spans.  With rows too long for LDS (large stores) it keeps up to 4 row
-// pointer pairs, or — a more mixed wave — the pairs in this wave's LDS list, OR-ed word by
-// word.  An unfiltered request (PCOL_ALL) disables filtering for its wave.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds,
-                                     uint32_t* list) {
+// The LDS part is the OR of the rows of all the wave's active requests over the first
+// lds_n words, however many (class, role key) pairs the wave spans; Filter::word ORs the
+// active lanes' own rows past it.  An unfiltered request (PCOL_ALL) disables filtering for
+// its wave.
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
   F.wsu = B.cand_wsu;
   F.wpu = B.cand_wpu ? B.cand_wpu : B.cand_wp;
   F.wv = B.cand_wv;
-  F.vok = false;  // the long-row form keeps no per-class verdicts
-  F.cand = B.cand;
-  F.rbits = B.role_bits;
-  F.nroles = B.role_key ? B.role_rows : 0u;
-  F.W = B.cand_words;
+  F.vok = false;  // waves mix classes: the general form keeps no per-class verdicts
   F.all = B.cand == nullptr;
+  F.lds = lds;
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
-  // the LDS union covers the whole row, or (long rows) the set + policy prefix
-  const uint32_t LW = W <= LDS_FILTER_WORDS ? W : (W < LDS_PREFIX_WORDS ? W : LDS_PREFIX_WORDS);
+  const uint32_t nroles = B.role_key ? B.role_rows : 0u;
+  const uint32_t LW = W <= LDS_FILTER_WORDS ? W : B.lds_pref;
   F.lds_n = LW;
-  if (lds && !F.all)
-    for (uint32_t w = lane; w < LW; w += 64) lds[w] = 0u;
-  const uint32_t key = cls << 16 | (rk < F.nroles ? rk : 0xFFFFu);
-  uint32_t n = 0;
+  // this lane's own rows (any valid row for a lane that evaluates nothing)
+  const bool own = valid && cls < B.cand_rows;
+  F.row = B.cand ? B.cand + (size_t)(own ? cls : 0u) * W : nullptr;
+  F.rrow = own && rk < nroles ? B.role_bits + (size_t)rk * W : F.row;
+  if (F.all) return F;
+  for (uint32_t w = lane; w < LW; w += 64) lds[w] = 0u;
+  const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
   uint64_t pending = __ballot(valid);
-  while (pending && !F.all) {
+  if (!pending) F.all = true;  // no active lane: nothing is evaluated anyway
+  while (pending) {
     const int leader = __builtin_ctzll(pending);
     const uint32_t k = __builtin_amdgcn_readlane(key, leader), c = k >> 16, r = k & 0xFFFFu;
     if (c == PCOL_ALL || c >= B.cand_rows) {
@@ -246,26 +249,9 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
       break;
     }
     const uint32_t* row = B.cand + (size_t)c * W;
-    const uint32_t* rrow = r < F.nroles ? B.role_bits + (size_t)r * W : nullptr;
-    if (lds)
-      for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
-    if (list) {
-      if (lane == 0) list[n] = k;  // at most 64 distinct (class, role key) pairs per wave
-      if (n < 4) {
-        if (n == 0) { F.row[0] = row; F.rrow[0] = rrow; }
-        else if (n == 1) { F.row[1] = row; F.rrow[1] = rrow; }
-        else if (n == 2) { F.row[2] = row; F.rrow[2] = rrow; }
-        else { F.row[3] = row; F.rrow[3] = rrow; }
-      }
-    }
-    ++n;
+    const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : row;
+    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & rrow[w];
     pending &= ~__ballot(valid && key == k);
-  }
-  if (!F.all && n == 0) F.all = true;  // no active lane: nothing is evaluated anyway
-  if (!F.all && lds) F.lds = lds;
-  if (!F.all && list && n > 4) {
-    F.list = list;
-    F.nlist = n;
   }
   return F;
 }
@@ -314,35 +300,30 @@ __device__ inline FilterAll wave_filter_all(const Batch& B) {
 // One maker per filter form, selected by the kernel's template argument.
 template <class FL> struct FilterMaker;
 template <> struct FilterMaker<Filter> {
-  static __device__ Filter make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds, uint32_t* list) {
-    return wave_filter(B, valid, cls, rk, lds, list);
+  static __device__ Filter make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
+    return wave_filter(B, valid, cls, rk, lds);
   }
 };
 template <> struct FilterMaker<FilterLds> {
-  static __device__ FilterLds make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds, uint32_t*) {
+  static __device__ FilterLds make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
     return wave_filter_lds(B, valid, cls, rk, lds);
   }
 };
 template <> struct FilterMaker<FilterAll> {
-  static __device__ FilterAll make(const Batch& B, bool, uint32_t, uint32_t, uint32_t*, uint32_t*) {
+  static __device__ FilterAll make(const Batch& B, bool, uint32_t, uint32_t, uint32_t*) {
     return wave_filter_all(B);
   }
 };
 
 extern __shared__ uint32_t acs_dyn_lds[];
 
-__device__ inline uint32_t lds_wave_words(const Batch& B) {
-  return B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_PREFIX_WORDS + LDS_LIST_WORDS;
+__host__ __device__ inline uint32_t lds_wave_words(const Batch& B) {
+  return B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : B.lds_pref;
 }
 
 __device__ inline uint32_t* wave_lds_row(const Batch& B) {
   if (!B.cand) return nullptr;
   return acs_dyn_lds + (threadIdx.x >> 6) * lds_wave_words(B);
-}
-
-__device__ inline uint32_t* wave_lds_list(const Batch& B) {
-  if (!B.cand || B.cand_words <= LDS_FILTER_WORDS) return nullptr;
-  return acs_dyn_lds + (threadIdx.x >> 6) * lds_wave_words(B) + LDS_PREFIX_WORDS;
 }
 
 __device__ inline uint32_t request_pcol(const ReqHdr& h) {
@@ -370,7 +351,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   Decision d{};
   if (in) d = early_decision(h, &done);
   const FL F = FilterMaker<FL>::make(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B), wave_lds_list(B));
+                                     wave_lds_row(B));
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
@@ -418,7 +399,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B), wave_lds_list(B));
+                                     wave_lds_row(B));
   if (!in) return;
   ChunkSink sink(bits + (size_t)i * BL.words, BL);
   OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
@@ -464,7 +445,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
   if (in) h = B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B), wave_lds_list(B));
+                                     wave_lds_row(B));
   if (!live) return;
   if (!in) {
     obl_n[k] = 0xFFFFFFFFu;
@@ -500,7 +481,7 @@ size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 size_t filter_lds_bytes(const Batch& B) {
   if (!B.cand) return 0;
-  return (size_t)(BLOCK / 64) * (B.cand_words <= LDS_FILTER_WORDS ? B.cand_words : LDS_PREFIX_WORDS + LDS_LIST_WORDS) * 4;
+  return (size_t)(BLOCK / 64) * lds_wave_words(B) * 4;
 }
 
 // Which filter form a batch's kernels are instantiated with.  ACS_FILTER_GENERAL=1 forces the
@@ -687,6 +668,13 @@ static Batch to_batch(const acs_req_batch* b) {
     return e && *e == '1';
   }();
   if (no_useful) B.cand_wsu = B.cand_wpu = 0;
+  // long rows: the LDS union covers the set and policy sections (rule words: the lanes' rows)
+  B.lds_pref = b->cand_wr < LDS_FILTER_WORDS ? b->cand_wr : LDS_FILTER_WORDS;
+  static const int role_major = [] {  // A/B runs: ACS_SORT_ROLE_MAJOR=0/1 overrides the default
+    const char* e = getenv("ACS_SORT_ROLE_MAJOR");
+    return e && *e ? (*e == '1' ? 1 : 0) : ACS_SORT_ROLE_MAJOR_DEFAULT;
+  }();
+  B.role_major = b->role_key && role_major ? 1u : 0u;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
@@ -743,7 +731,7 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   uint32_t* v1 = v0 + n;
   uint32_t* counts = v1 + n;
   uint32_t* gsum = counts + (size_t)RADIX * nt;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, k0, v0, counts);
+  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
   HIP_OK(hipGetLastError());
   for (uint32_t p = 0; p < passes; ++p) {
     if (p > 0) {
