@@ -346,6 +346,7 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
         if not isinstance(combin, dict):
             raise Unsupported("policy set without combinables")
         pe_at = L.EFF_UNDEF
+        set_free = L.NF_COND_FREE  # no condition rule and no invalid combining algorithm below
         for pol in combin.values():
             if pol is None or pol is MISSING:
                 pols.append(_node({"nflags": L.NF_NULL, "child_begin": len(rules), "child_end": len(rules),
@@ -364,6 +365,7 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
             if not isinstance(rcomb, dict):
                 raise Unsupported("policy without combinables")
             fe = None
+            pol_free = L.NF_COND_FREE
             for rule in rcomb.values():
                 if rule is None or rule is MISSING:
                     rules.append(_node({"nflags": L.NF_NULL, "_rule": True}, spec_r))
@@ -375,6 +377,7 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
                 clen = len(cond) if isinstance(cond, (str, list)) else get(cond, "length")
                 if truthy(clen):
                     rf |= L.NF_HAS_CONDITION
+                    pol_free = 0
                 ec = b.ec_code(rule.get("evaluation_cacheable", MISSING))
                 if b.ec_truthy[ec]:
                     rf |= L.NF_EC_TRUTHY
@@ -383,10 +386,14 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
                 rn.update(nflags=rf, effect=effect_code(rule.get("effect", MISSING)), ec=ec)
                 rules.append(_node(rn, spec_r))
                 rule_objs.append(rule)
-            pn.update(child_end=len(rules), map_size=len(rcomb), fe=len(rules) if fe is None else fe)
+            pn.update(child_end=len(rules), map_size=len(rcomb), fe=len(rules) if fe is None else fe,
+                      nflags=pn["nflags"] | pol_free)
+            if not pol_free or pn["ca"] == L.CA_INVALID:
+                set_free = 0
             pols.append(_node(pn, spec_p))
             pol_objs.append(pol)
         sn.update(child_end=len(pols), ca=b.ca_code(ps.get("combining_algorithm", MISSING)),
+                  nflags=sn["nflags"] | set_free,
                   pe_at=pe_at)  # set: policyEffect after a full loop-2a scan
         sets = [_node(sn, spec_s)]
         return _Fragment(ps, _arr(sets, L.NODE_DT), _arr(pols, L.NODE_DT), _arr(rules, L.NODE_DT),

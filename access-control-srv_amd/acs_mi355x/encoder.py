@@ -443,8 +443,21 @@ class Encoder:
         return b
 
 
+def mark_rx_safe(b: RequestBatch):
+    """RES_RX_SAFE in ReqRes.pad of every entity attribute whose regex column holds no cell
+    that throws or needs the host: K1 may then end a combining loop once its result is final
+    (nothing left in it can throw).  acs_codec.cpp does the same."""
+    bad = (b.rx & np.uint8(L.RX_THROW_TYPE | L.RX_THROW_SYNTAX | L.RX_HOST)).any(axis=1)
+    j = np.arange(L.QMAX)[:, None]
+    col = b.res["col"].astype(np.int64)
+    ok = ((b.res["kind"] & L.K_ENT_LOOSE) != 0) & (j < b.hdr["nres"][None, :]) & (col < len(bad))
+    ok &= ~bad[np.minimum(col, len(bad) - 1)]
+    b.res["pad"] |= np.where(ok, np.uint8(L.RES_RX_SAFE), np.uint8(0))
+
+
 def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True):
     """Candidate rows for the batch's request classes + each request's class id in its flags."""
+    mark_rx_safe(b)
     ncols = b.rx.shape[0]
     assert len(col_values) <= ncols
     # pad: columns without a value (an all-empty batch) get no candidates beyond the "always" nodes

@@ -1701,6 +1701,19 @@ acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int th
     cells();
     for (auto& th : pool) th.join();
   }
+  // RES_RX_SAFE on every entity attribute whose column holds no throwing / host cell (K1 may
+  // then cut a combining loop short once its result is final: encoder.mark_rx_safe)
+  {
+    std::vector<uint8_t> safe(B->rx_cols, 1);
+    for (uint32_t k = 0; k < B->rx_cols; ++k)
+      for (uint32_t r = 0; r < B->rx_rows; ++r)
+        if (B->rx[(size_t)k * B->rx_rows + r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST)) safe[k] = 0;
+    for (uint32_t j = 0; j < (uint32_t)QMAX; ++j)
+      for (uint32_t i = 0; i < n; ++i) {
+        ReqRes& q = B->res[(size_t)j * n + i];
+        if ((q.kind & K_ENT_LOOSE) && j < B->hdr[i].nres && q.col < B->rx_cols && safe[q.col]) q.pad |= RES_RX_SAFE;
+      }
+  }
   const double t2 = now_s();
   Classes cl(*c, *B, T);
   cl.col_keys = keys;  // padding column: ''

@@ -326,6 +326,7 @@ struct Builder {
     const JV* combin = get(ps, "combinables");
     if (combin->t != J_ARR) fail("policy set without combinables");
     uint8_t pe_at = EFF_UNDEF;
+    uint8_t set_free = NF_COND_FREE;  // no condition rule and no invalid combining algorithm below
     std::vector<NodeRec> my_pols;  // set record goes first in the Python order of node appends
     for (uint32_t k = 0; k < combin->n; ++k) {
       const JV* pol = &combin->a[k];
@@ -355,6 +356,7 @@ struct Builder {
       const JV* rcomb = get(pol, "combinables");
       if (rcomb->t != J_ARR) fail("policy without combinables");
       uint32_t fe = NONE32;
+      uint8_t pol_free = NF_COND_FREE;
       for (uint32_t r = 0; r < rcomb->n; ++r) {
         const JV* rule = &rcomb->a[r];
         if (rule->t == J_NULL) {
@@ -376,7 +378,10 @@ struct Builder {
           clen_v = get(cond, "length");
           clen = truthy(clen_v);
         }
-        if (clen) rf |= NF_HAS_CONDITION;
+        if (clen) {
+          rf |= NF_HAS_CONDITION;
+          pol_free = 0;
+        }
         const uint8_t ec = ec_code(get(rule, "evaluation_cacheable"));
         if (this->ec[ec].truthy) rf |= NF_EC_TRUTHY;
         else if (fe == NONE32) fe = (uint32_t)rules.size();
@@ -389,12 +394,15 @@ struct Builder {
       P.child_end = (uint32_t)rules.size();
       P.map_size = rcomb->n;
       P.fe = fe == NONE32 ? (uint32_t)rules.size() : fe;
+      P.nflags |= pol_free;
+      if (!pol_free || P.ca == CA_INVALID) set_free = 0;
       pols.push_back(P);
       push_spec(1, pt.present, pt, false);
     }
     S.child_end = (uint32_t)pols.size();
     S.ca = ca_code(get(ps, "combining_algorithm"));
     S.pe_at = pe_at;
+    S.nflags |= set_free;
     sets.push_back(S);
     push_spec(0, st.present, st, false);
   }

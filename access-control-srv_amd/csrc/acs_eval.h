@@ -64,30 +64,18 @@ struct Tables {
   const uint32_t* u32pool;
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
+  uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
 };
 
-// Table records are read as whole dwords and unpacked in registers: with a wave-uniform
-// address this is one s_load_dwordx{2,4,8,16} (scalar loads have no byte / short forms).
+// Table records are read as whole dwords through wave-uniform addresses and unpacked in
+// registers (vector loads, then SGPRs: see below).
 template <class X, int NW = sizeof(X) / 4>
 ACS_FN X load_words(const Tables& T, const X* p) {
   static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
   (void)T;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
-#if defined(__HIP_DEVICE_COMPILE__) && defined(ACS_SLOAD)
-  // Scalar loads: the address is wave-uniform, so through the constant address space the
-  // compiler emits s_load_dwordxN.  Scalar loads ignore the exec mask, so every address must
-  // be valid even where no lane is active: node indices are clamped to their table
-  // (node_at), and every other table address is an offset taken from such a record, which
-  // acs_compile has validated against its pool (csrc/acs_validate.cpp).
-  typedef __attribute__((address_space(4))) const uint32_t const_u32;
-  const uint64_t a = (uint64_t)(uintptr_t)w;
-  const uint64_t ua = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)a) |
-                      ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32);
-  const const_u32* c = (const const_u32*)(uintptr_t)ua;
-#pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = c[k];
-#elif defined(__HIP_DEVICE_COMPILE__) && !defined(ACS_NO_VLR)
+#if defined(__HIP_DEVICE_COMPILE__)
   // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
   // the wave-uniform record moves to SGPRs: its fields feed scalar compares and branches and
   // free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself proves
@@ -103,15 +91,15 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   return out;
 }
 
-// Node record `x` of a table section of `n` records (x clamped into the section; see
-// load_words — only the scalar-load build needs the clamp).
+// Node record `x` of a table section of `n` records.
 ACS_FN NodeRec node_at(const Tables& T, const NodeRec* sec, uint32_t x, uint32_t n) {
-#if defined(ACS_SLOAD)
-  x = x < n ? x : n - 1;
-#else
   (void)n;
-#endif
   return load_words(T, sec + x);
+}
+
+// Rule r.  The device image stores each rule in a 128-B line (record + inline attributes).
+ACS_FN NodeRec rule_at(const Tables& T, uint32_t r) {
+  return node_at(T, T.rules, r * T.rstride, T.n_rules * T.rstride);
 }
 
 struct Batch {
@@ -132,6 +120,7 @@ struct Batch {
   uint32_t no_verdicts;         // A/B runs (ACS_NO_VERDICTS=1): K1 ignores the verdicts
   uint32_t lds_pref;            // long rows (> LDS row capacity): words of the wave's LDS union prefix
   uint32_t role_major;          // coherence sort key [role key | class] instead of [class | role key]
+  uint32_t no_cut;              // A/B runs (ACS_NO_CUT=1): combining loops always run to the end
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
@@ -271,6 +260,10 @@ struct Fold {  // streaming decide(): first X else last / first element
     }
     n = 1;
   }
+  // no later push can change eff / ec
+  ACS_FN bool final() const {
+    return n && ((ca != CA_DENY_OVERRIDES && ca != CA_PERMIT_OVERRIDES) || locked);
+  }
 };
 
 struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
@@ -292,9 +285,6 @@ struct ReqCtx {
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
-#if defined(ACS_ROLE_REGS)
-  uint32_t rl[RMAX];  // role_associations roles, NONE32 past nroles (branch-free role test)
-#endif
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
 #endif
@@ -316,10 +306,6 @@ struct ReqCtx {
     s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
     role0 = h.nroles > 0 ? B.roles[i] : 0u;
     role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
-#if defined(ACS_ROLE_REGS)
-#pragma unroll
-    for (int k = 0; k < RMAX; ++k) rl[k] = k < (int)h.nroles ? B.roles[(size_t)k * B.n + i] : NONE32;
-#endif
   }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
@@ -411,16 +397,9 @@ ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
   if (t.tflags & TF_SUBJ_EMPTY) return true;
   if (t.tflags & TF_SUBJ_ROLE) {
     if (!R.flag(RQ_RA_TRUTHY)) return false;
-#if defined(ACS_ROLE_REGS)
-    bool hit = false;
-#pragma unroll
-    for (int k = 0; k < RMAX; ++k) hit |= R.rl[k] == t.role;
-    return hit;
-#else
     for (uint32_t k = 0; k < R.h.nroles; ++k)
       if (R.role(k) == t.role) return true;
     return false;
-#endif
   }
   return attrs_match(R.T.pairs + t.subj_off, t.subj_n, R, true);
 }
@@ -436,11 +415,7 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
   if (t.tflags & TF_RES_EMPTY) return 1;
   const RuleResAttr* ra = R.T.rres + t.res_off;
   const uint32_t ent = (R.h.flags >> RQ_ENT_SHIFT) & 7u;
-#if defined(ACS_NO_ENT_FASTPATH)  // A/B builds only
-  if (false) {
-#else
   if ((t.tflags & TF_RES_ENT_ONLY) && ent != 7u && j0 == 0 && j1 == (int)R.h.nres) {
-#endif
     // Target without property / operation attributes and a request with at most one entity
     // attribute: every property / mask / skipDenyRule branch needs a rule property, so the
     // ordered double loop reduces to entityMatch over the rule's entity attributes (exact:
@@ -803,6 +778,17 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   Decision out{};
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;
+  // Cutting a combining loop short: once a fold's result is final (Fold::final), the rest of
+  // its loop can change the decision only by throwing or by reaching a rule condition.  A
+  // request cannot throw there when its hierarchical_scopes is an array, context.subject is
+  // present (checkHierarchicalScope / verifyACL TypeErrors) and no RegExp cell of its entity
+  // values throws or needs the host (RES_RX_SAFE); NF_COND_FREE rules out conditions (and,
+  // for a set, invalid combining algorithms).  Then the lane leaves the loop.
+  bool safe = !R.B.no_cut && R.flag(RQ_HRS_ITERABLE) && !R.flag(RQ_SUBJ_MISSING);
+  for (int j = 0; j < (int)R.h.nres && safe; ++j) {
+    const ReqRes q = R.res(j);
+    if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
+  }
   CandRange sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py)
   uint32_t s;
   while (sets.next(s)) {
@@ -848,6 +834,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       exact = m != 0;
     }
     Fold sf(S.ca);
+    const bool cut_p = safe && (S.nflags & NF_COND_FREE);
     CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
     uint32_t p;
     while (pols.next(p)) {
@@ -878,13 +865,15 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       }
       if (P.map_size == 0 && (P.nflags & NF_EFFECT_TRUTHY)) {
         sf.push(P.effect, P.ec);
+        if (cut_p && sf.final()) break;
         continue;
       }
       Fold rf(P.ca);
+      const bool cut_r = safe && (P.nflags & NF_COND_FREE);
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = node_at(T, T.rules, r, T.n_rules);
+        const NodeRec Q = rule_at(T, r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {
@@ -911,11 +900,15 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
           if (m < 0) return make_err(m, s + 1);
         }
         // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
-        if (m && psm) rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
+        if (m && psm) {
+          rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
+          if (cut_r && rf.final()) break;
+        }
       }
       if (rf.n) {
         if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA, s + 1);
         sf.push(rf.eff, rf.ec);
+        if (cut_p && sf.final()) break;
       }
     }
     if (sf.n) {
@@ -1106,7 +1099,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       CandRange rules(F, F.wr, P.child_begin, P.child_end);
       uint32_t r;
       while (rules.next(r)) {
-        const NodeRec Q = node_at(T, T.rules, r, T.n_rules);
+        const NodeRec Q = rule_at(T, r);
         if (Q.nflags & NF_NULL) continue;
         tri m = 1;
         if (Q.nflags & NF_HAS_TARGET) {

@@ -595,12 +595,79 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   }
   uint32_t rx_rows_min = 0;
   if (acs_internal_check_blob(blob, n_bytes, &rx_rows_min)) return nullptr;
+  // Device image: the blob's sections, except that each rule becomes a 128-B line (its 64-B
+  // record, then up to 3 resource attributes and 2 action pairs inline), so a rule visit's
+  // record, action and resource reads hit one cache line instead of three (large stores miss
+  // L2 on each).  The rres and pair pools follow the lines, and one base (the first line)
+  // addresses both: every node's res_off / act_off / subj_off is rebased, inline attributes
+  // point into their line.  ACS_RULE_LINES=0: the blob layout (A/B runs).
+  static const bool rule_lines = [] {
+    const char* e = getenv("ACS_RULE_LINES");
+    return !(e && *e == '0');
+  }();
+  const char* bsrc = (const char*)blob + src;
+  std::vector<char> img;
+  size_t doff[6];
+  uint32_t rstride = 1;
+  const void* up = bsrc;
+  size_t up_bytes = total;
+  const size_t lines = (size_t)h.n_rules * 128;
+  const size_t l0 = (align16(sz[0]) + align16(sz[1]) + 127) & ~size_t(127);
+  const size_t p_rel = lines + align16(sz[3]);  // pair pool, bytes past the first line
+  if (rule_lines && h.n_rules && (p_rel / 8 + h.n_pairs) < 0xFFFFFFFFull && (lines / 16 + h.n_rres) < 0xFFFFFFFFull) {
+    rstride = 2;
+    doff[0] = 0;
+    doff[1] = align16(sz[0]);
+    doff[2] = l0;
+    doff[3] = l0 + lines;
+    doff[4] = l0 + p_rel;
+    doff[5] = doff[4] + align16(sz[4]);
+    up_bytes = doff[5] + align16(sz[5]);
+    img.assign(up_bytes, 0);
+    char* d = img.data();
+    std::memcpy(d + doff[0], bsrc + off[0], sz[0]);
+    std::memcpy(d + doff[1], bsrc + off[1], sz[1]);
+    std::memcpy(d + doff[3], bsrc + off[3], sz[3]);
+    std::memcpy(d + doff[4], bsrc + off[4], sz[4]);
+    std::memcpy(d + doff[5], bsrc + off[5], sz[5]);
+    const uint32_t R0 = (uint32_t)(lines / 16), P0 = (uint32_t)(p_rel / 8);
+    auto rebase = [&](NodeRec& N) {
+      N.res_off += R0;
+      N.act_off += P0;
+      N.subj_off += P0;
+    };
+    for (uint32_t k = 0; k < h.n_sets + h.n_pols; ++k) {
+      NodeRec* N = (NodeRec*)(d + (k < h.n_sets ? doff[0] + (size_t)k * 64 : doff[1] + (size_t)(k - h.n_sets) * 64));
+      rebase(*N);
+    }
+    const RuleResAttr* rres = (const RuleResAttr*)(bsrc + off[3]);
+    const Pair* pairs = (const Pair*)(bsrc + off[4]);
+    for (uint32_t r = 0; r < h.n_rules; ++r) {
+      NodeRec N;
+      std::memcpy(&N, bsrc + off[2] + (size_t)r * 64, 64);
+      char* line = d + l0 + (size_t)r * 128;
+      const uint32_t res_off = N.res_off, act_off = N.act_off;
+      rebase(N);
+      if (N.res_n <= 3) {  // validated: [res_off, res_off + res_n) lies in the pool
+        std::memcpy(line + 64, rres + res_off, (size_t)N.res_n * sizeof(RuleResAttr));
+        N.res_off = r * 8 + 4;
+      }
+      if (N.act_n <= 2) {
+        std::memcpy(line + 112, pairs + act_off, (size_t)N.act_n * sizeof(Pair));
+        N.act_off = r * 16 + 14;
+      }
+      std::memcpy(line, &N, 64);
+    }
+    up = d;
+  } else {
+    for (int k = 0; k < 6; ++k) doff[k] = off[k];
+  }
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
-  const size_t alloc = total + 64;  // clamp window [base, base + total] for 64-B record loads
+  const size_t alloc = up_bytes + 128;
   if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
-      hipMemcpy(t->dev, (const char*)blob + src, total, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
     fail("acs_compile: device allocation / upload failed");
@@ -608,16 +675,18 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     return nullptr;
   }
   char* base = (char*)t->dev;
-  t->view.sets = (const NodeRec*)(base + off[0]);
-  t->view.pols = (const NodeRec*)(base + off[1]);
-  t->view.rules = (const NodeRec*)(base + off[2]);
-  t->view.rres = (const RuleResAttr*)(base + off[3]);
-  t->view.pairs = (const Pair*)(base + off[4]);
-  t->view.u32pool = (const uint32_t*)(base + off[5]);
+  t->view.sets = (const NodeRec*)(base + doff[0]);
+  t->view.pols = (const NodeRec*)(base + doff[1]);
+  t->view.rules = (const NodeRec*)(base + doff[2]);
+  // rule lines: one base for both attribute pools (offsets rebased above)
+  t->view.rres = (const RuleResAttr*)(base + (rstride == 2 ? doff[2] : doff[3]));
+  t->view.pairs = (const Pair*)(base + (rstride == 2 ? doff[2] : doff[4]));
+  t->view.u32pool = (const uint32_t*)(base + doff[5]);
   t->view.n_sets = h.n_sets;
   t->view.n_pols = h.n_pols;
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
+  t->view.rstride = rstride;
   return t;
 }
 
@@ -668,6 +737,9 @@ static Batch to_batch(const acs_req_batch* b) {
     return e && *e == '1';
   }();
   if (no_useful) B.cand_wsu = B.cand_wpu = 0;
+  // A/B runs and the cut-invariance tests: ACS_NO_CUT=1 runs every combining loop to its end
+  const char* no_cut = getenv("ACS_NO_CUT");
+  B.no_cut = no_cut && *no_cut == '1' ? 1u : 0u;
   // long rows: the LDS union covers the set and policy sections (rule words: the lanes' rows)
   B.lds_pref = b->cand_wr < LDS_FILTER_WORDS ? b->cand_wr : LDS_FILTER_WORDS;
   static const int role_major = [] {  // A/B runs: ACS_SORT_ROLE_MAJOR=0/1 overrides the default

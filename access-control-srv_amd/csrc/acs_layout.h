@@ -80,6 +80,9 @@ enum NodeFlags : uint8_t {
   NF_EFFECT_TRUTHY = 1u << 2,  // !!node.effect
   NF_HAS_CONDITION = 1u << 3,  // rule.condition?.length
   NF_EC_TRUTHY = 1u << 4,      // !!rule.evaluation_cacheable
+  NF_COND_FREE = 1u << 5,      // policy: no rule carries a condition; set: none of its policies'
+                               // rules does and no policy has an invalid combining algorithm
+                               // (absent: K1 never cuts the node's loop short)
 };
 
 struct NodeRec {
@@ -153,8 +156,9 @@ struct ReqRes {              // 16 B
   uint8_t kind;
   uint8_t slot_a;            // ctx resource via instance.id then id (NONE8: not found)
   uint8_t slot_b;            // ctx resource via id only (operation lookup)
-  uint8_t pad;
+  uint8_t pad;               // RES_RX_SAFE: no regex cell of this value's column throws or needs the host
 };
+constexpr uint32_t RES_RX_SAFE = 1;  // ReqRes.pad bit (absent: the request may throw in a RegExp test)
 
 // Context arena (u32 words), per request:
 //   [0] n_grants | n_rolese<<8 | n_slots<<16 | n_roots<<24

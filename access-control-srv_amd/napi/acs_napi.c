@@ -82,8 +82,8 @@ typedef struct {
 typedef struct {
   int magic;
   acs_codec_batch* b;
-  codec_h* codec;
-  napi_ref codec_ref;
+  codec_h* codec; /* counted reference: the codec outlives its batches (no napi_ref, which a
+                     finalizer may not delete once the environment is torn down at exit) */
 } batch_h;
 
 static void tables_release(tables_h* h) {
@@ -126,7 +126,6 @@ static void fin_batch(napi_env env, void* data, void* hint) {
   batch_h* h = (batch_h*)data;
   (void)hint;
   if (h->b) acs_codec_batch_free(h->b); /* before its codec */
-  if (h->codec_ref) napi_delete_reference(env, h->codec_ref);
   if (h->codec) codec_unref(h->codec);
   h->magic = 0;
   free(h);
@@ -763,7 +762,6 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
   bh->b = b;
   bh->codec = h;
   h->refs++;
-  CHECK(env, napi_create_reference(env, argv[0], 1, &bh->codec_ref));
   CHECK(env, napi_create_external(env, bh, fin_batch, NULL, &out));
   return out;
 }

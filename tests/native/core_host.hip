@@ -3,6 +3,7 @@
 // consume.  Lets the not-gpu test tier check the host compiler + encoder + core
 // logic against the oracle in a container without a GPU.  Never linked into the
 // product library (libacs_mi355x.so has no CPU path).
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/acs_mi355x.h"
@@ -35,6 +36,7 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   T->n_pols = h.n_pols;
   T->n_rules = h.n_rules;
   T->id_user = h.id_user;
+  T->rstride = 1;  // blob layout: 64-B rule records, separate pools
   return true;
 }
 
@@ -60,6 +62,8 @@ static Batch host_batch(const acs_req_batch* b) {
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
+  const char* no_cut = getenv("ACS_NO_CUT");  // as the product library (acs_kernels.hip: to_batch)
+  B.no_cut = no_cut && *no_cut == '1' ? 1u : 0u;
   return B;
 }
 

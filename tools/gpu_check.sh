@@ -33,8 +33,9 @@ for s in $STEPS; do
           st=20; [ "$cfg" = c3 ] && st=5
           for rep in $(seq 1 ${AB_REPS:-2}); do
             step "ab_${cfg}_product_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
-            for ev in ${AB_ENVS:-ACS_FILTER_GENERAL}; do
-              step "ab_${cfg}_${ev}_$rep" 900 env $ev=1 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
+            for ev in ${AB_ENVS:-ACS_FILTER_GENERAL}; do  # NAME (=1) or NAME=VALUE
+              case $ev in *=*) kv=$ev ;; *) kv=$ev=1 ;; esac
+              step "ab_${cfg}_${kv}_$rep" 900 env $kv python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
             done
             for v in ${VARIANTS:-}; do
               step "ab_${cfg}_${v}_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 \
@@ -46,6 +47,8 @@ for s in $STEPS; do
           step "pytest_gpu_$v" 600 env ACS_MI355X_LIB=access-control-srv_amd/lib/variants/$v.so \
             python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "kats or random_diff or synthetic_config"
         done ;;
+    phase5) step phase_c5 900 python tools/phase_prof.py c5 1000000 ;;
+    phase3) step phase_c3 900 python tools/phase_prof.py c3 2000000 ;;
     quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
     c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
