@@ -63,16 +63,29 @@ def what_is_allowed_device(tables, db: DeviceBatch, bufs=None, stream=None):
     return bufs
 
 
-def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int = 1024, chunks: int = 8, stream=None):
+# lanes of one obligation pass that keep the GPU busy (256 CUs x 16 waves x 64 lanes)
+OBL_PASS_LANES = 1 << 18
+
+
+def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int | None = None, chunks: int | None = None,
+                            stream=None):
     """Obligation-only passes for the requests whose K2 log overflowed (record flag
     OF_OBL_OVERFLOW in ``bufs[3]``): the policy sets cut into ``chunks`` ranges with ``cap``
-    entries each, then the still-truncated requests once more at their exact count.  Returns
+    entries each, then the still-truncated requests once more at their exact count.  By
+    default the ranges are as many (8..64, a power of two) as keep about OBL_PASS_LANES lanes
+    busy, so a few overflowed requests take 1/64 of a traversal, not 1/8.  Returns
     [(idx [m], cap, obl [chunks][m][cap][2], obl_n [chunks][m])] per pass (int32 tensors; later
     passes supersede earlier ones).  Syncs the stream to size each pass."""
     st = stream or torch.cuda.current_stream(db.dev)
     with torch.cuda.stream(st):
         flags = bufs[3][:, 2]
         idx = torch.nonzero(flags & L.OF_OBL_OVERFLOW).flatten()
+        if chunks is None:
+            chunks = 8
+            while chunks < 64 and chunks * 2 * max(idx.numel(), 1) <= OBL_PASS_LANES:
+                chunks *= 2
+        if cap is None:
+            cap = max(128, 8192 // chunks)
         # request-class order, as K2's coherence sort: a wave then shares its candidate row
         cls = (db.t["hdr"].view(torch.int32).view(-1, 4)[idx, 0] >> L.RQ_PCOL_SHIFT) & 0xFFFF
         idx = idx[torch.sort(cls, stable=True).indices].to(torch.int32)

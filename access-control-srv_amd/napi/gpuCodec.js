@@ -31,7 +31,7 @@ const OF_ERR = 0x01, OF_HOST_COND = 0x02, OF_HOST_REQ = 0x04, OF_NO_TARGET = 0x0
 const ERR_KINDS = { 1: 'TypeError', 2: 'InvalidCombiningAlgorithm', 3: 'SyntaxError', 4: 'RegexHost' };
 const ERR_REGEX_HOST = 4;
 const REC_BYTES = 8;
-const OBL_MAX = 64; // ACS_OBL_MAX: (entity, mask) pairs per request in the whatIsAllowed log
+const OBL_MAX = 128; // ACS_OBL_MAX: (entity, mask) pairs per request in the whatIsAllowed log
 const OVERFLOW_CAP = 1024, OVERFLOW_CHUNKS = 8;
 
 class HostPathRequired extends Error {
@@ -241,7 +241,7 @@ class GpuAccessController {
     return out;
   }
 
-  // Full maskedProperty logs of the requests whose 64-entry log overflowed: the
+  // Full maskedProperty logs of the requests whose 128-entry log overflowed: the
   // obligation-only pass over 8 policy-set ranges with 1024-entry logs, then once more at the
   // exact count for any range still truncated (INTEGRATION.md §4; native.resolve_overflow).
   _resolveOverflow(batch, flagged) {
