@@ -404,6 +404,21 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
         b.rres, b.pairs, b.u32pool = saved
 
 
+def mark_clean_below(sets, pols):
+    """NF_CLEAN_BELOW on every set all of whose predecessors are clean: NF_COND_FREE (no
+    condition rule, no invalid policy combining algorithm), a valid set combining algorithm
+    and no null policy (loop 2a's TypeError).  Depends on the Map order, so it is set on the
+    assembled tables (acs_compiler.cpp does the same after its last set)."""
+    if not len(sets):
+        return
+    owner = np.repeat(np.arange(len(sets)), (sets["child_end"] - sets["child_begin"]).astype(np.int64))
+    has_null = np.zeros(len(sets), bool)
+    has_null[owner[(pols["nflags"] & L.NF_NULL) != 0]] = True
+    clean = ((sets["nflags"] & L.NF_COND_FREE) != 0) & (sets["ca"] != L.CA_INVALID) & ~has_null
+    below = np.concatenate([[True], np.logical_and.accumulate(clean)[:-1]])
+    sets["nflags"] |= np.where(below, np.uint8(L.NF_CLEAN_BELOW), np.uint8(0))
+
+
 def _assemble(b: _Builder, frags: list) -> CompiledStore:
     """Concatenate fragments in Map order, shifting child ranges and pool offsets."""
     ns = [len(f.pols) for f in frags]
@@ -433,6 +448,7 @@ def _assemble(b: _Builder, frags: list) -> CompiledStore:
     sets = cat("sets", [("child_begin", pol0), ("child_end", pol0)])
     pols = cat("pols", [("child_begin", rule0), ("child_end", rule0), ("fe", rule0)])
     rules = cat("rules", [])
+    mark_clean_below(sets, pols)
 
     def pool(key, dt):
         return np.concatenate([getattr(f, key) for f in frags]) if frags else np.zeros(0, dt)

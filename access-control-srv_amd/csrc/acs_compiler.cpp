@@ -598,6 +598,15 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
     }
     for (auto& kv : b.urns) b.intern(b.urn[kv.first]);
     for (uint32_t k = 0; k < st->n; ++k) b.compile_set(&st->a[k]);
+    // compiler.mark_clean_below: every earlier set clean (NF_COND_FREE, valid CA, no null policy)
+    bool clean_so_far = true;
+    for (NodeRec& S : b.sets) {
+      if (clean_so_far) S.nflags |= NF_CLEAN_BELOW;
+      bool clean = (S.nflags & NF_COND_FREE) && S.ca != CA_INVALID;
+      for (uint32_t p = S.child_begin; p < S.child_end && clean; ++p)
+        if (b.pols[p].nflags & NF_NULL) clean = false;
+      clean_so_far = clean_so_far && clean;
+    }
     const std::string img = build_image(b);
     void* mem = malloc(img.size());
     if (!mem) fail("out of memory");

@@ -233,6 +233,36 @@ struct CandRange {
   }
 };
 
+// Descending iteration over the candidate indices in [b, e) of one bitset section.
+template <class FL>
+struct CandRangeRev {
+  const FL& F;
+  uint32_t off, b, lo, base, bits;  // lo: base of the word holding index b (the last word read)
+  ACS_FN CandRangeRev(const FL& f, uint32_t section_off, uint32_t b_, uint32_t e)
+      : F(f), off(section_off), b(b_), lo(b_ & ~31u), base(b_ & ~31u), bits(0) {
+    if (b < e) {
+      base = (e - 1) & ~31u;
+      const uint32_t top = (e - 1) & 31u;
+      bits = F.word(off + (base >> 5)) & (top == 31u ? ~0u : ((1u << (top + 1)) - 1u));
+    }
+  }
+  ACS_FN bool next(uint32_t& out) {
+    for (;;) {
+      if (bits) {
+        const uint32_t hi = 31u - (uint32_t)__builtin_clz(bits);
+        const uint32_t x = wave_uniform(base + hi);
+        bits &= ~(1u << hi);
+        if (x < b) return false;
+        out = x;
+        return true;
+      }
+      if (base <= lo) return false;
+      base -= 32;
+      bits = F.word(off + (base >> 5));
+    }
+  }
+};
+
 ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
 
 #ifndef ACS_POLICY_VERDICTS
@@ -771,13 +801,152 @@ ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
   return d;
 }
 
+// One policy set of isAllowed (the body of accessController.ts:125-295's set loop): no
+// effect, an effect (sf's eff / ec), or an event that ends the request there (an error the
+// reference throws, or a reached rule condition: the record in *ev).
+enum SetOutcome { SET_NONE = 0, SET_EFFECT = 1, SET_EVENT = 2 };
+
+template <class RQ, class FL>
+ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool safe, uint8_t* eff, uint8_t* ec,
+                    Decision* ev) {
+  const Tables& T = R.T;
+  const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
+  if (S.nflags & NF_HAS_TARGET) {
+    PROF_T0(t0);
+    const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
+    PROF_ADD(PH_SET_TARGET, t0);
+    if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+    if (!m) return SET_NONE;
+  }
+  // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
+  bool exact = false;
+  uint8_t pe = S.pe_at;  // after a full scan
+  PROF_T0(t2a);
+  {
+    CandRange pols(F, F.wp, S.child_begin, S.child_end);
+    uint32_t p;
+    while (pols.next(p)) {
+      const NodeRec P = node_at(T, T.pols, p, T.n_pols);
+      if (P.nflags & NF_NULL) return *ev = make_err(-(tri)ERR_TYPE, s + 1), SET_EVENT;
+      if (P.nflags & NF_HAS_TARGET) {
+#if ACS_POLICY_VERDICTS
+        const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
+#else
+        const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
+#endif
+        if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+        if (m) {
+          exact = true;
+          pe = P.pe_at;
+          break;
+        }
+      }
+    }
+  }
+  PROF_ADD(PH_POL_EXACT, t2a);
+  if (exact && R.flag(RQ_MULTI_ENT)) {
+    PROF_T0(tm);
+    const tri m = multiple_entities(S, R);
+    PROF_ADD(PH_MULTI, tm);
+    if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+    exact = m != 0;
+  }
+  Fold sf(S.ca);
+  const bool cut_p = safe && (S.nflags & NF_COND_FREE);
+  CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
+  uint32_t p;
+  while (pols.next(p)) {
+    const NodeRec P = node_at(T, T.pols, p, T.n_pols);
+    if (P.nflags & NF_NULL) continue;
+    bool psm = true;
+    if (P.nflags & NF_HAS_TARGET) {
+      PROF_T0(tp);
+      // the class's verdict for this lane's mode
+#if ACS_POLICY_VERDICTS
+      const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
+      const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
+#else
+      const bool kt = false, kf = false;
+#endif
+      const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
+      if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+      if (!m) {
+        PROF_ADD(PH_POL_TARGET, tp);
+        continue;
+      }
+      if (P.tflags & TF_HAS_SUBJECTS) {
+        const tri h = hierarchical_scope(P, R);
+        if (h < 0) return *ev = make_err(h, s + 1), SET_EVENT;
+        psm = h != 0;
+      }
+      PROF_ADD(PH_POL_TARGET, tp);
+    }
+    if (P.map_size == 0 && (P.nflags & NF_EFFECT_TRUTHY)) {
+      sf.push(P.effect, P.ec);
+      if (cut_p && sf.final()) break;
+      continue;
+    }
+    Fold rf(P.ca);
+    const bool cut_r = safe && (P.nflags & NF_COND_FREE);
+    CandRange rules(F, F.wr, P.child_begin, P.child_end);
+    uint32_t r;
+    while (rules.next(r)) {
+      const NodeRec Q = rule_at(T, r);
+      if (Q.nflags & NF_NULL) continue;
+      tri m = 1;
+      if (Q.nflags & NF_HAS_TARGET) {
+        PROF_T0(tr);
+        m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
+        if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+        PROF_ADD(PH_RULE_TARGET, tr);
+        if (!m) continue;
+        PROF_T0(th);
+        m = hierarchical_scope(Q, R);
+        PROF_ADD(PH_RULE_HR, th);
+        if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+      }
+      if (m && (Q.nflags & NF_HAS_CONDITION)) {
+        Decision d{};
+        d.decision = DEC_INDETERMINATE;
+        d.flags = OF_HOST_COND;
+        d.aux = r;
+        return *ev = d, SET_EVENT;
+      }
+      if (m && (Q.nflags & NF_HAS_TARGET)) {
+        PROF_T0(ta);
+        m = verify_acl(Q, R);
+        PROF_ADD(PH_RULE_ACL, ta);
+        if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
+      }
+      // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
+      if (m && psm) {
+        rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
+        if (cut_r && rf.final()) break;
+      }
+    }
+    if (rf.n) {
+      if (rf.ca == CA_INVALID) return *ev = make_err(-(tri)ERR_INVALID_CA, s + 1), SET_EVENT;
+      sf.push(rf.eff, rf.ec);
+      if (cut_p && sf.final()) break;
+    }
+  }
+  if (!sf.n) return SET_NONE;
+  if (sf.ca == CA_INVALID) return *ev = make_err(-(tri)ERR_INVALID_CA, s + 1), SET_EVENT;
+  *eff = sf.eff;
+  *ec = sf.ec;
+  return SET_EFFECT;
+}
+
+// isAllowed over the sets LAST TO FIRST.  Forward, the reference lets the last set with an
+// effect decide (`effect` is overwritten per set, :293-295) unless an earlier set ends the
+// request (the first error / reached condition).  So walking backwards, the first effect
+// found is the answer unless a set below it has an event, and the lowest event found wins
+// over everything.  Once something was found and every set below is clean (NF_CLEAN_BELOW)
+// and the request safe (nothing of it can throw there: see `safe`), no set below can change
+// the record and the lane stops; otherwise it walks on to set 0.
 template <class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   const Tables& T = R.T;
-  const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
-  Decision out{};
-  uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
-  uint32_t last_set = 0;
   // Cutting a combining loop short: once a fold's result is final (Fold::final), the rest of
   // its loop can change the decision only by throwing or by reaching a rule condition.  A
   // request cannot throw there when its hierarchical_scopes is an array, context.subject is
@@ -789,135 +958,29 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     const ReqRes q = R.res(j);
     if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
   }
-  CandRange sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py)
+  uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
+  uint32_t last_set = 0;  // 1 + the last set with an effect (0: none yet)
+  Decision ev{};
+  bool have_ev = false;
+  CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
   while (sets.next(s)) {
     const NodeRec S = node_at(T, T.sets, s, T.n_sets);
-    if (S.nflags & NF_HAS_TARGET) {
-      PROF_T0(t0);
-      const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
-      PROF_ADD(PH_SET_TARGET, t0);
-      if (m < 0) return make_err(m, s + 1);
-      if (!m) continue;
-    }
-    // loop 2a: first exact policy match; policyEffect = precomputed prefix (accessController.ts:136-157)
-    bool exact = false;
-    uint8_t pe = S.pe_at;  // after a full scan
-    PROF_T0(t2a);
-    {
-      CandRange pols(F, F.wp, S.child_begin, S.child_end);
-      uint32_t p;
-      while (pols.next(p)) {
-        const NodeRec P = node_at(T, T.pols, p, T.n_pols);
-        if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
-        if (P.nflags & NF_HAS_TARGET) {
-#if ACS_POLICY_VERDICTS
-          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
-#else
-          const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
-#endif
-          if (m < 0) return make_err(m, s + 1);
-          if (m) {
-            exact = true;
-            pe = P.pe_at;
-            break;
-          }
-        }
-      }
-    }
-    PROF_ADD(PH_POL_EXACT, t2a);
-    if (exact && R.flag(RQ_MULTI_ENT)) {
-      PROF_T0(tm);
-      const tri m = multiple_entities(S, R);
-      PROF_ADD(PH_MULTI, tm);
-      if (m < 0) return make_err(m, s + 1);
-      exact = m != 0;
-    }
-    Fold sf(S.ca);
-    const bool cut_p = safe && (S.nflags & NF_COND_FREE);
-    CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
-    uint32_t p;
-    while (pols.next(p)) {
-      const NodeRec P = node_at(T, T.pols, p, T.n_pols);
-      if (P.nflags & NF_NULL) continue;
-      bool psm = true;
-      if (P.nflags & NF_HAS_TARGET) {
-        PROF_T0(tp);
-        // the class's verdict for this lane's mode
-#if ACS_POLICY_VERDICTS
-        const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
-        const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
-#else
-        const bool kt = false, kf = false;
-#endif
-        const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
-        if (m < 0) return make_err(m, s + 1);
-        if (!m) {
-          PROF_ADD(PH_POL_TARGET, tp);
-          continue;
-        }
-        if (P.tflags & TF_HAS_SUBJECTS) {
-          const tri h = hierarchical_scope(P, R);
-          if (h < 0) return make_err(h, s + 1);
-          psm = h != 0;
-        }
-        PROF_ADD(PH_POL_TARGET, tp);
-      }
-      if (P.map_size == 0 && (P.nflags & NF_EFFECT_TRUTHY)) {
-        sf.push(P.effect, P.ec);
-        if (cut_p && sf.final()) break;
-        continue;
-      }
-      Fold rf(P.ca);
-      const bool cut_r = safe && (P.nflags & NF_COND_FREE);
-      CandRange rules(F, F.wr, P.child_begin, P.child_end);
-      uint32_t r;
-      while (rules.next(r)) {
-        const NodeRec Q = rule_at(T, r);
-        if (Q.nflags & NF_NULL) continue;
-        tri m = 1;
-        if (Q.nflags & NF_HAS_TARGET) {
-          PROF_T0(tr);
-          m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
-          if (m < 0) return make_err(m, s + 1);
-          PROF_ADD(PH_RULE_TARGET, tr);
-          if (!m) continue;
-          PROF_T0(th);
-          m = hierarchical_scope(Q, R);
-          PROF_ADD(PH_RULE_HR, th);
-          if (m < 0) return make_err(m, s + 1);
-        }
-        if (m && (Q.nflags & NF_HAS_CONDITION)) {
-          out.decision = DEC_INDETERMINATE;
-          out.flags = OF_HOST_COND;
-          out.aux = r;
-          return out;
-        }
-        if (m && (Q.nflags & NF_HAS_TARGET)) {
-          PROF_T0(ta);
-          m = verify_acl(Q, R);
-          PROF_ADD(PH_RULE_ACL, ta);
-          if (m < 0) return make_err(m, s + 1);
-        }
-        // evaluation_cacheable: the rule's own value while every non-null rule up to it was truthy
-        if (m && psm) {
-          rf.push(Q.effect, r < P.fe ? Q.ec : (uint8_t)EC_FALSE);
-          if (cut_r && rf.final()) break;
-        }
-      }
-      if (rf.n) {
-        if (rf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA, s + 1);
-        sf.push(rf.eff, rf.ec);
-        if (cut_p && sf.final()) break;
-      }
-    }
-    if (sf.n) {
-      if (sf.ca == CA_INVALID) return make_err(-(tri)ERR_INVALID_CA, s + 1);
-      eff = sf.eff;
-      ec = sf.ec;
+    uint8_t e2 = EFF_UNDEF, c2 = EC_UNDEF;
+    Decision d2{};
+    const int o = eval_set(R, F, s, S, safe, &e2, &c2, &d2);
+    if (o == SET_EVENT) {
+      ev = d2;  // lower than any event found so far
+      have_ev = true;
+    } else if (o == SET_EFFECT && !last_set) {
+      eff = e2;
+      ec = c2;
       last_set = s + 1;
     }
+    if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN_BELOW)) break;
   }
+  if (have_ev) return ev;
+  Decision out{};
   if (!last_set) {
     out.decision = DEC_INDETERMINATE;
     out.ec = EC_UNDEF;

@@ -83,6 +83,10 @@ enum NodeFlags : uint8_t {
   NF_COND_FREE = 1u << 5,      // policy: no rule carries a condition; set: none of its policies'
                                // rules does and no policy has an invalid combining algorithm
                                // (absent: K1 never cuts the node's loop short)
+  NF_CLEAN_BELOW = 1u << 6,    // set: every set before it is "clean" — NF_COND_FREE, a valid
+                               // combining algorithm, no null policy — so nothing there can
+                               // throw or reach a condition for a safe request (K1 walks the
+                               // sets last to first and stops at the deciding one)
 };
 
 struct NodeRec {

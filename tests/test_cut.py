@@ -1,5 +1,5 @@
-"""Cutting a combining loop short (acs_eval.h: is_allowed_body, Fold::final) never changes a
-record.  Random stores with injected rule conditions, RegExp SyntaxErrors in rule entities and
+"""Cutting a combining loop short (acs_eval.h: eval_set, Fold::final) and stopping the
+last-to-first walk over the sets (is_allowed_body, NF_CLEAN_BELOW) never change a record.  Random stores with injected rule conditions, RegExp SyntaxErrors in rule entities and
 invalid combining algorithms — the only things that can still matter after a fold's result
 is final — are evaluated with the cut (default) and with ACS_NO_CUT=1; the records must be
 bit-identical (decision, ec, flags, error kind and aux: set index / condition rule index)."""
@@ -34,6 +34,9 @@ def cut_case(seed):
             p["rules"].append({"id": p["id"] + "x", "target": tgt, "effect": r.choice(["PERMIT", "DENY"])})
         elif x < 0.6:
             p["combining_algorithm"] = "urn:bogus:ca"
+    for ps in doc["policy_sets"]:  # invalid set combining algorithms end requests where sets decide
+        if r.random() < 0.15:
+            ps["combining_algorithm"] = "urn:bogus:ca"
     return urns, doc, reqs
 
 
