@@ -72,6 +72,18 @@ def build_prof(force=False):
     return PROF_LIB
 
 
+SCAN_LIB = os.path.join(PKG, "lib", "libacs_mi355x_scan.so")
+
+
+def build_scan(force=False):
+    """Counting variant of the product library (-DACS_SCAN_COUNT): every table read a wave
+    issues adds its bytes to a device counter (bench.py's measured B_scan)."""
+    src = os.path.join(CSRC, "acs_kernels.hip")
+    if force or _stale(SCAN_LIB, [src] + _HEADERS + _HOST_SRCS):
+        _hipcc(src, SCAN_LIB, ("-DACS_SCAN_COUNT",), host_srcs=_HOST_SRCS)
+    return SCAN_LIB
+
+
 def build_variant(name, defines, force=False):
     """Experimental build of the product library with extra -D flags (lib/variants/<name>.so)."""
     out = os.path.join(PKG, "lib", "variants", name + ".so")
@@ -108,7 +120,7 @@ def build_host_core(force=False):
 
 
 def build_all(force=False):
-    return build_product(force), build_host_core(force), build_napi(force)
+    return build_product(force), build_host_core(force), build_napi(force), build_scan(force)
 
 
 if __name__ == "__main__":

@@ -86,9 +86,29 @@ constexpr uint32_t SORT_TILE = BLOCK * SORT_ITEMS;    // 2048
 constexpr uint32_t RADIX = 256;
 constexpr uint32_t SCAN_GROUP = 64;                   // tiles per tile-scan group
 
+// Request i's ReqLine (acs_eval.h) from the SoA rows; the arena head only for requests K1
+// evaluates (host / target-less requests may carry no arena record).
+__device__ inline void build_line(const Batch& B, uint32_t i, ReqLine* out) {
+  ReqLine L{};
+  L.h = B.hdr[i];
+  const uint32_t nq = L.h.nres < LINE_RES ? L.h.nres : LINE_RES;
+  for (uint32_t j = 0; j < nq; ++j) L.res[j] = B.res[(size_t)j * B.n + i];
+  if (L.h.nsubj > 0) L.s0 = B.subj[i];
+  if (L.h.nsubj > 1) L.s1 = B.subj[(size_t)B.n + i];
+  if (L.h.nact > 0) L.a0 = B.act[i];
+  if (L.h.nroles > 0) L.r0 = B.roles[i];
+  if (L.h.nroles > 1) L.r1 = B.roles[(size_t)B.n + i];
+  if (!(L.h.flags & (RQ_HOST | RQ_NO_TARGET))) {
+    const uint32_t* ar = B.arena + L.h.arena_off;
+    L.ar0 = ar[0];
+    L.ar1 = ar[1];
+  }
+  out[i] = L;
+}
+
 __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_null, const Batch* B,
                                       uint32_t lowbits, uint32_t cbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
-                                      uint32_t shift, uint32_t* counts) {
+                                      uint32_t shift, uint32_t* counts, ReqLine* lines = nullptr) {
   hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t t0 = blockIdx.x * SORT_TILE;
@@ -100,6 +120,7 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
       key = sort_key(*B, i, lowbits, cbits);
       keys_out[i] = key;
       idx_out[i] = i;
+      if (lines) build_line(*B, i, lines);
     } else {
       key = keys_or_null[i];
     }
@@ -111,9 +132,9 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
 
 __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t cbits,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ idx,
-                                                          uint32_t* __restrict__ counts) {
+                                                          uint32_t* __restrict__ counts, ReqLine* __restrict__ lines) {
   __shared__ uint32_t hist[RADIX];
-  tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts);
+  tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts, lines);
 }
 
 __global__ __launch_bounds__(BLOCK) void radix_histogram_kernel(const uint32_t* __restrict__ keys, uint32_t n,
@@ -251,6 +272,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : row;
     for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & rrow[w];
+    ACS_SCAN(LW * (rrow == row ? 4u : 8u));
     pending &= ~__ballot(valid && key == k);
   }
   return F;
@@ -277,6 +299,7 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : nullptr;
     for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
+    ACS_SCAN(W * (rrow ? 8u : 4u));
     if (c != first_cls) {
       first_cls = c;
       ++classes;
@@ -340,13 +363,15 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 template <class FL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
-    Tables T, Batch B, const uint32_t* __restrict__ perm, Decision* __restrict__ out) {
+    Tables T, Batch B, const uint32_t* __restrict__ perm, const ReqLine* __restrict__ lines,
+    Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  const ReqLine* ln = in && lines ? lines + i : nullptr;  // the request's packed line (sorted batches)
   ReqHdr h{};
-  if (in) h = B.hdr[i];
+  if (in) h = ln ? ln->h : B.hdr[i];
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
@@ -361,13 +386,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
 #if defined(ACS_PHASE_PROF)
-    const ReqLds R(T, B, i, h, col, BLOCK);
+    const ReqLds R(T, B, i, h, col, BLOCK, ln);
     d = is_allowed_t(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -545,6 +570,17 @@ const char* acs_last_error(void) { return g_err.c_str(); }
 
 // The codec (acs_codec.cpp) reports through the same thread-local message.
 void acs_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
+#if defined(ACS_SCAN_COUNT)
+// Counting build only: read and reset the table bytes the waves read (bench.py B_scan).
+int acs_scan_read(unsigned long long* out) {
+  unsigned long long z = 0;
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(acs_scan_bytes), sizeof *out));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_scan_bytes), &z, sizeof z));
+  return 0;
+}
+#endif
 
 #if defined(ACS_PHASE_PROF)
 // Profiling build only: read and reset the per-phase lane-cycle sums.
@@ -773,8 +809,11 @@ int acs_set_option(acs_tables* t, int option, int value) {
 }
 
 // Coherence sort: permutation of request indices ordered by (class, low field).
-static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
+// lines != nullptr: the key kernel also packs every request's ReqLine (K1's request reads).
+static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm,
+                          const ReqLine** lines = nullptr) {
   *perm = nullptr;
+  if (lines) *lines = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
   // Low field: the dense role key with a role factor; otherwise none — a class row already
@@ -789,7 +828,8 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   const uint32_t passes = end_bit ? (end_bit + 7) / 8 : 1;
   const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
   const uint32_t ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
-  const size_t need = 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
+  const size_t sort_bytes = (4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t) + 127) & ~size_t(127);
+  const size_t need = sort_bytes + (lines ? n * sizeof(ReqLine) : 0);
   if (need > t->ws_bytes) {
     if (t->ws) HIP_OK(hipFree(t->ws));
     t->ws = nullptr;
@@ -803,7 +843,8 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   uint32_t* v1 = v0 + n;
   uint32_t* counts = v1 + n;
   uint32_t* gsum = counts + (size_t)RADIX * nt;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
+  ReqLine* ln = lines ? (ReqLine*)((char*)t->ws + sort_bytes) : nullptr;
+  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts, ln);
   HIP_OK(hipGetLastError());
   for (uint32_t p = 0; p < passes; ++p) {
     if (p > 0) {
@@ -823,6 +864,7 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
     std::swap(v0, v1);
   }
   *perm = v0;
+  if (lines) *lines = ln;
   return 0;
 }
 
@@ -832,11 +874,14 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
   hipStream_t s = (hipStream_t)stream;
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  if (coherence_perm(t, B, s, &perm)) return -1;
+  const ReqLine* lines = nullptr;
+  const char* no_lines = getenv("ACS_NO_LINES");  // A/B runs: K1 reads the SoA rows
+  if (coherence_perm(t, B, s, &perm, no_lines && *no_lines == '1' ? nullptr : &lines)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, (Decision*)out);
+  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, lines,
+                      (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));

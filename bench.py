@@ -72,81 +72,50 @@ def _node_bytes(nodes):
             + 4 * nodes["acl_roles_n"].astype(np.int64))
 
 
-def scan_bytes(cs, batch, wave=64):
-    """Table bytes the K1 waves visit, counted from the same class rows the kernel uses:
-    requests in coherence-sort order, 64 per wave, the union of the wave's (class row AND
-    role-factor row) filters (an unfiltered class: the whole table).  K1 walks the useful
-    sets; inside one, loop 2a scans the candidate policies and loop 2b the useful ones; a
-    rule is visited only inside a loop-2b policy.  Each record counts once per wave (a policy
-    read by both loops, once); a node whose target verdict the class row carries (one-class
-    waves) counts its record only, its pairs and attributes are not read.  Returns total bytes."""
-    from acs_mi355x import layout as L, candidates
-    n = batch.n
-    cand = batch.cand
-    R = 0 if cand is None else cand.shape[0]
-    h = batch.hdr
-    cls = (h["flags"] >> np.uint32(L.RQ_PCOL_SHIFT)).astype(np.int64)
-    cls = np.where(cls >= R, R, cls)
-    rk_all = batch.role_key.astype(np.int64) if batch.role_key is not None else np.full(n, 0xFFFF, np.int64)
-    nrk = 0 if batch.role_bits is None else batch.role_bits.shape[0]
-    if batch.role_key is not None:
-        low = rk_all & 0xFFFF
-    else:
-        low = np.where(h["nact"] > 0, batch.act["value"][0], 0).astype(np.int64) & 0xFFFF
-    bucket = np.where(cls >= R, 0, cls + 1)  # sort_keys_kernel: unfiltered first, then class ids
-    order = np.argsort((bucket << 16) | low, kind="stable")
-    pair = (cls << 16) | np.where(rk_all < nrk, rk_all, 0xFFFF)
-    pw = pair[order]
-    ns, npol, nr = cs.n_sets, cs.n_pols, cs.n_rules
-    bs, bp, br = _node_bytes(cs.sets), _node_bytes(cs.pols), _node_bytes(cs.rules)
-    par_p = np.repeat(np.arange(ns), (cs.sets["child_end"] - cs.sets["child_begin"]).astype(np.int64))
-    par_r = np.repeat(np.arange(npol), (cs.pols["child_end"] - cs.pols["child_begin"]).astype(np.int64))
-    full = int(bs.sum() + bp.sum() + br.sum())
-    wp, wsu, wpu, wr, _ = candidates.row_layout(cs)
-    useful = getattr(batch, "cand_wsu", 0) != 0
-    wv = getattr(batch, "cand_wv", 0)
-    WP = (npol + 31) // 32
-    rec = 64  # a verdict-known target is not matched: only its record is read
-    cache = {}
+def measured_scan_bytes(blob, db, local, what="is_allowed"):
+    """B_scan of the whole launch, measured: the counting build of the library
+    (lib/libacs_mi355x_scan.so, -DACS_SCAN_COUNT) runs the same kernel once on the same device
+    batch; every table read a wave issues (node records, pairs, resource attributes, class-row
+    words) adds its bytes once per wave.  The traversal is deterministic, so this is exactly
+    what the timed launches read from the tables, re-reads included."""
+    import ctypes as C
+    from acs_mi355x import build as B, native
+    from acs_mi355x.device import is_allowed_device, what_is_allowed_device
+    if not os.path.exists(B.SCAN_LIB):
+        raise SystemExit(f"bench.py: counting build missing: {B.SCAN_LIB} (run __graft_entry__.build())")
+    lib = native._declare(C.CDLL(B.SCAN_LIB))
+    lib.acs_scan_read.argtypes = [C.POINTER(C.c_ulonglong)]
 
-    def union_bytes(key):
-        if key in cache:
-            return cache[key]
-        # K1 ORs every (class & role) row of the wave (in LDS, or word by word for long rows)
-        if any((k >> 16) >= R for k in key):
-            cache[key] = full
-            return full
-        row = np.zeros(cand.shape[1], np.uint32)
-        for k in key:
-            x = cand[k >> 16]
-            if (k & 0xFFFF) < nrk:
-                x = x & batch.role_bits[k & 0xFFFF]
-            row |= x
-        bits = np.unpackbits(row.view(np.uint8), bitorder="little").astype(bool)
-        s = bits[32 * wsu:32 * wsu + ns] if useful else bits[:ns]
-        p2a = bits[32 * wp:32 * wp + npol] & s[par_p]
-        p2b = (bits[32 * wpu:32 * wpu + npol] if useful else bits[32 * wp:32 * wp + npol]) & s[par_p]
-        r = bits[32 * wr:32 * wr + nr] & p2b[par_r]
-        pk = np.zeros(npol, bool)
-        rk = np.zeros(nr, bool)
-        if wv and len({k >> 16 for k in key}) == 1:  # K1 reads the class's verdicts (one-class waves)
-            pv = [bits[32 * (wv + k * WP):32 * (wv + k * WP) + npol] for k in range(4)]
-            pk = (pv[0] | pv[1]) & (pv[2] | pv[3])
-            rk = bits[32 * (wv + 4 * WP):32 * (wv + 4 * WP) + nr]
-        pp = p2a | p2b
-        v = int(bs[s].sum() + np.where(pk, rec, bp)[pp].sum() + np.where(rk, rec, br)[r].sum())
-        cache[key] = v
-        return v
-
-    total = 0
-    for w0 in range(0, n, wave):
-        total += union_bytes(tuple(np.unique(pw[w0:w0 + wave]).tolist()))
-    return total, full
+    class _T:  # the duck-typed tables handle device.py's launchers take
+        pass
+    t = _T()
+    t.lib = lib
+    t.h = lib.acs_compile(blob, len(blob), local)
+    if not t.h:
+        raise RuntimeError("counting build: acs_compile failed: " + native.last_error(lib))
+    t.words = lib.acs_wia_words_per_request(t.h)
+    v = C.c_ulonglong(0)
+    try:
+        lib.acs_scan_read(C.byref(v))  # reset
+        if what == "is_allowed":
+            is_allowed_device(t, db)
+        else:
+            what_is_allowed_device(t, db)
+        torch.cuda.synchronize()
+        if lib.acs_scan_read(C.byref(v)) != 0:
+            raise RuntimeError("acs_scan_read: " + native.last_error(lib))
+    finally:
+        lib.acs_free(t.h)
+    return int(v.value)
 
 
-def algorithmic_bytes(cs, batch):
+def table_bytes_full(cs):
+    return int(_node_bytes(cs.sets).sum() + _node_bytes(cs.pols).sum() + _node_bytes(cs.rules).sum())
+
+
+def algorithmic_bytes(cs, batch, scan_total):
     """Per-decision algorithmic bytes: B_req + B_ctx + B_out + B_scan/T, with
-    B_scan the table bytes each 64-request tile actually visits (candidate rows, see scan_bytes)."""
+    B_scan the table bytes the 64-request tiles actually read (measured_scan_bytes)."""
     h = batch.hdr
     b_req = 16 + 16 * h["nres"].astype(np.float64) + 8 * h["nsubj"] + 8 * h["nact"] + 4 * h["nroles"]
     # context arena bytes each request reads (its own record; a shared record counts for every request)
@@ -154,7 +123,7 @@ def algorithmic_bytes(cs, batch):
     uo = np.unique(offs)
     size = np.diff(np.append(uo, batch.arena.size))
     ctx = float(4.0 * size[np.searchsorted(uo, offs)].mean()) if batch.n else 0.0
-    scan_total, full = scan_bytes(cs, batch)
+    full = table_bytes_full(cs)
     b_scan_per_dec = scan_total / max(batch.n, 1)
     per = float(b_req.mean()) + ctx + 8.0 + b_scan_per_dec
     return per, {"B_req": float(b_req.mean()), "B_ctx": ctx, "B_out": 8.0, "B_scan_per_decision": b_scan_per_dec,
@@ -326,7 +295,8 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
     sb = synth.requests(cs, n, "c3", seed=0xACC1004 + 17 * rank)
     log(f"compiled {cs.n_rules} rules; encoded {n} requests")
-    tables = native.Tables(compiler.store_blob(cs), local)
+    blob = compiler.store_blob(cs)
+    tables = native.Tables(blob, local)
     tables.set_timing(True)
     db = DeviceBatch(sb.batch, local)
     stream = torch.cuda.current_stream(dev)
@@ -366,7 +336,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
         obl_n = bufs[2].cpu().numpy().view(np.uint32)
         rec = bufs[3].cpu().numpy().reshape(-1).view(L.DECISION_DT)
         words = bits.shape[1]
-        per_req, parts = algorithmic_bytes(cs, sb.batch)
+        per_req, parts = algorithmic_bytes(cs, sb.batch, measured_scan_bytes(blob, db, local, "what_is_allowed"))
         # K2 writes the inclusion bitset, the log entries it pushes, the log length and the record
         out_b = 4 * words + 8 * float(obl_n.mean()) + 4 + 8
         per = per_req - 8.0 + out_b
@@ -503,7 +473,8 @@ def main():
     log(f"compiled {cs.n_rules} rules; encoded {n} requests ({sb.batch.cand.shape[0]} classes)")
     if args.lib:
         native.load(args.lib)
-    tables = native.Tables(compiler.store_blob(cs), local)
+    blob = compiler.store_blob(cs)
+    tables = native.Tables(blob, local)
     tables.set_sort(not args.no_sort)
     tables.set_timing(True)
     db = DeviceBatch(sb.batch, local)
@@ -570,7 +541,7 @@ def main():
                 "identical_to_device_path": bool(np.array_equal(host_dec.view(np.uint64), dec.view(np.uint64)))}
     if rank == 0:
         log("counting algorithmic bytes")
-        per_dec, parts = algorithmic_bytes(cs, sb.batch)
+        per_dec, parts = algorithmic_bytes(cs, sb.batch, measured_scan_bytes(blob, db, local))
         achieved = per_dec * n / (kern_ms * 1e-3) / 1e9
         mode = "rules" if args.rule_shard else "requests"
         traffic, traffic_src = measured_traffic(traffic_key(kind, n, world, mode))
