@@ -88,7 +88,7 @@ constexpr uint32_t SCAN_GROUP = 64;                   // tiles per tile-scan gro
 
 // Request i's ReqLine (acs_eval.h) from the SoA rows; the arena head only for requests K1
 // evaluates (host / target-less requests may carry no arena record).
-__device__ inline void build_line(const Batch& B, uint32_t i, ReqLine* out) {
+__device__ inline ReqLine make_line(const Batch& B, uint32_t i) {
   ReqLine L{};
   L.h = B.hdr[i];
   const uint32_t nq = L.h.nres < LINE_RES ? L.h.nres : LINE_RES;
@@ -103,12 +103,12 @@ __device__ inline void build_line(const Batch& B, uint32_t i, ReqLine* out) {
     L.ar0 = ar[0];
     L.ar1 = ar[1];
   }
-  out[i] = L;
+  return L;
 }
 
 __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_null, const Batch* B,
                                       uint32_t lowbits, uint32_t cbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
-                                      uint32_t shift, uint32_t* counts, ReqLine* lines = nullptr) {
+                                      uint32_t shift, uint32_t* counts) {
   hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t t0 = blockIdx.x * SORT_TILE;
@@ -120,7 +120,6 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
       key = sort_key(*B, i, lowbits, cbits);
       keys_out[i] = key;
       idx_out[i] = i;
-      if (lines) build_line(*B, i, lines);
     } else {
       key = keys_or_null[i];
     }
@@ -132,9 +131,33 @@ __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_nu
 
 __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowbits, uint32_t cbits,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ idx,
-                                                          uint32_t* __restrict__ counts, ReqLine* __restrict__ lines) {
+                                                          uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[RADIX];
-  tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts, lines);
+  tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts);
+}
+
+// Packs every request's ReqLine, one request per thread (streaming: the SoA rows are read
+// in request order).  The block's lines go through LDS so that the stores are coalesced
+// (consecutive lanes write consecutive 16-B chunks: whole lines per wave store, no partial
+// line writes).  Runs on the handle's second stream, overlapped with the sort.
+constexpr uint32_t LINE_Q = sizeof(ReqLine) / 16;  // 16-B chunks per line
+__global__ __launch_bounds__(BLOCK) void pack_lines_kernel(Batch B, ReqLine* __restrict__ lines) {
+  __shared__ uint4 st[BLOCK * (LINE_Q + 1)];  // +1 chunk per line: conflict-free staging
+  const uint32_t i0 = blockIdx.x * BLOCK, i = i0 + threadIdx.x;
+  if (i < B.n) {
+    const ReqLine L = make_line(B, i);
+    const uint4* q = reinterpret_cast<const uint4*>(&L);
+#pragma unroll
+    for (uint32_t c = 0; c < LINE_Q; ++c) st[threadIdx.x * (LINE_Q + 1) + c] = q[c];
+  }
+  __syncthreads();
+  const uint32_t m = B.n - i0 < BLOCK ? B.n - i0 : BLOCK;  // lines in this block
+  uint4* dst = reinterpret_cast<uint4*>(lines + i0);
+#pragma unroll
+  for (uint32_t r = 0; r < LINE_Q; ++r) {
+    const uint32_t c = r * BLOCK + threadIdx.x;  // chunk c of the block: line c / LINE_Q
+    if (c / LINE_Q < m) dst[c] = st[(c / LINE_Q) * (LINE_Q + 1) + c % LINE_Q];
+  }
 }
 
 __global__ __launch_bounds__(BLOCK) void radix_histogram_kernel(const uint32_t* __restrict__ keys, uint32_t n,
@@ -539,6 +562,8 @@ struct acs_tables {
   Tables view{};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipStream_t stream2 = nullptr;            // request-line packing, overlapped with the sort
+  hipEvent_t fork = nullptr, join = nullptr;
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
@@ -705,7 +730,10 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
       hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
+      hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess ||
+      hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess) {
     fail("acs_compile: device allocation / upload failed");
     acs_free(t);
     return nullptr;
@@ -733,6 +761,9 @@ void acs_free(acs_tables* t) {
   if (t->ev0) (void)hipEventDestroy(t->ev0);
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
+  if (t->stream2) (void)hipStreamDestroy(t->stream2);
+  if (t->fork) (void)hipEventDestroy(t->fork);
+  if (t->join) (void)hipEventDestroy(t->join);
   if (t->ws) (void)hipFree(t->ws);
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
@@ -844,7 +875,14 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   uint32_t* counts = v1 + n;
   uint32_t* gsum = counts + (size_t)RADIX * nt;
   ReqLine* ln = lines ? (ReqLine*)((char*)t->ws + sort_bytes) : nullptr;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts, ln);
+  if (ln) {  // fork: the lines are packed on the second stream while the sort runs on s
+    HIP_OK(hipEventRecord(t->fork, s));
+    HIP_OK(hipStreamWaitEvent(t->stream2, t->fork, 0));
+    hipLaunchKernelGGL(pack_lines_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, t->stream2, B, ln);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(t->join, t->stream2));
+  }
+  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
   HIP_OK(hipGetLastError());
   for (uint32_t p = 0; p < passes; ++p) {
     if (p > 0) {
@@ -864,7 +902,10 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
     std::swap(v0, v1);
   }
   *perm = v0;
-  if (lines) *lines = ln;
+  if (ln) {
+    HIP_OK(hipStreamWaitEvent(s, t->join, 0));  // join before K1 reads the lines
+    *lines = ln;
+  }
   return 0;
 }
 

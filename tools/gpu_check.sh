@@ -19,6 +19,7 @@ STEPS=${STEPS:-"tests smoke bench prof"}
 for s in $STEPS; do
   case $s in
     tests) step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ;;
+    tests_quick) step pytest_gpu_quick 600 python -u -m pytest tests/test_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread -k "kats or random_diff or synthetic_config or role_factor or large_store" ;;
     rehearse) step rehearse_launcher 600 env ACS_BENCH_REHEARSAL=1 python bench.py --gpus 2 --config c2 --steps 5 --warmup 1 --no-cpu-baseline ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 900 python bench.py --steps 20 --warmup 3 ;;
