@@ -321,21 +321,6 @@ struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
 };
 
 // ------------------------------------------------------------------ request views
-// One request's hot fields in a single 128-B line (GPU: built from the SoA rows by the
-// coherence sort's key kernel, in request order), so K1's first reads of a request gather
-// one line instead of one per SoA row (header, attributes, subjects, action, roles, arena
-// head: ~8 lines per request at c3).
-constexpr int LINE_RES = 4;
-struct ReqLine {
-  ReqHdr h;               // 16
-  ReqRes res[LINE_RES];   // resource attributes j < min(nres, LINE_RES)
-  Pair s0, s1, a0;        // first two subjects, first action (zero past the counts)
-  uint32_t r0, r1;        // first two roles
-  uint32_t ar0, ar1;      // the context arena's two count words
-  uint32_t pad[2];
-};
-static_assert(sizeof(ReqLine) == 128, "ReqLine is one 128-B line");
-
 // Context arena + headers shared by both request views.
 struct ReqCtx {
   const Tables& T;
@@ -350,26 +335,9 @@ struct ReqCtx {
   mutable uint64_t prof[PH_N] = {};
 #endif
 
-  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
-      : T(t), B(b), i(idx), h(hd) {
+  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : T(t), B(b), i(idx), h(hd) {
     ar = B.arena + h.arena_off;
-    if (ln) {  // one line holds the counts and the first subjects / action / roles
-      s0i = ln->s0.id; s0v = ln->s0.value; s1i = ln->s1.id; s1v = ln->s1.value;
-      a0i = ln->a0.id; a0v = ln->a0.value;
-      role0 = ln->r0;
-      role1 = ln->r1;
-      set_arena(ln->ar0, ln->ar1);
-      return;
-    }
-    set_arena(ar[0], ar[1]);
-    const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
-    const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
-    const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
-    s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
-    role0 = h.nroles > 0 ? B.roles[i] : 0u;
-    role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
-  }
-  ACS_FN void set_arena(uint32_t c0, uint32_t c1) {
+    uint32_t c0 = ar[0], c1 = ar[1];
     n_grants = c0 & 0xFF; n_rolese = (c0 >> 8) & 0xFF; n_slots = (c0 >> 16) & 0xFF; n_roots = c0 >> 24;
     n_tse = c1 & 0xFF; n_hrkeys = (c1 >> 8) & 0xFF;
     grants = ar + 2;
@@ -378,6 +346,12 @@ struct ReqCtx {
     hrkeys = roots + n_roots;
     slotoff = hrkeys + n_hrkeys;
     tse = slotoff + n_slots;
+    const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
+    const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
+    const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
+    s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
+    role0 = h.nroles > 0 ? B.roles[i] : 0u;
+    role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
   }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
@@ -413,9 +387,8 @@ struct ReqLds : ReqCtx {
   const ReqRes* col;  // this lane's LDS column
   uint32_t stride;
   uint32_t e0_val, e0_col;  // the request's only entity attribute (RQ_ENT_SHIFT field 1..6)
-  ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st,
-                const ReqLine* ln = nullptr)
-      : ReqCtx(t, b, idx, hd, ln), col(c), stride(st) {
+  ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st)
+      : ReqCtx(t, b, idx, hd), col(c), stride(st) {
     const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
     e0_val = e0_col = 0;
     if (e >= 1 && e <= 6) {

@@ -86,26 +86,6 @@ constexpr uint32_t SORT_TILE = BLOCK * SORT_ITEMS;    // 2048
 constexpr uint32_t RADIX = 256;
 constexpr uint32_t SCAN_GROUP = 64;                   // tiles per tile-scan group
 
-// Request i's ReqLine (acs_eval.h) from the SoA rows; the arena head only for requests K1
-// evaluates (host / target-less requests may carry no arena record).
-__device__ inline ReqLine make_line(const Batch& B, uint32_t i) {
-  ReqLine L{};
-  L.h = B.hdr[i];
-  const uint32_t nq = L.h.nres < LINE_RES ? L.h.nres : LINE_RES;
-  for (uint32_t j = 0; j < nq; ++j) L.res[j] = B.res[(size_t)j * B.n + i];
-  if (L.h.nsubj > 0) L.s0 = B.subj[i];
-  if (L.h.nsubj > 1) L.s1 = B.subj[(size_t)B.n + i];
-  if (L.h.nact > 0) L.a0 = B.act[i];
-  if (L.h.nroles > 0) L.r0 = B.roles[i];
-  if (L.h.nroles > 1) L.r1 = B.roles[(size_t)B.n + i];
-  if (!(L.h.flags & (RQ_HOST | RQ_NO_TARGET))) {
-    const uint32_t* ar = B.arena + L.h.arena_off;
-    L.ar0 = ar[0];
-    L.ar1 = ar[1];
-  }
-  return L;
-}
-
 __device__ inline void tile_histogram(uint32_t* hist, const uint32_t* keys_or_null, const Batch* B,
                                       uint32_t lowbits, uint32_t cbits, uint32_t* keys_out, uint32_t* idx_out, uint32_t n,
                                       uint32_t shift, uint32_t* counts) {
@@ -134,30 +114,6 @@ __global__ __launch_bounds__(BLOCK) void sort_keys_kernel(Batch B, uint32_t lowb
                                                           uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[RADIX];
   tile_histogram(hist, nullptr, &B, lowbits, cbits, keys, idx, B.n, 0, counts);
-}
-
-// Packs every request's ReqLine, one request per thread (streaming: the SoA rows are read
-// in request order).  The block's lines go through LDS so that the stores are coalesced
-// (consecutive lanes write consecutive 16-B chunks: whole lines per wave store, no partial
-// line writes).  Runs on the handle's second stream, overlapped with the sort.
-constexpr uint32_t LINE_Q = sizeof(ReqLine) / 16;  // 16-B chunks per line
-__global__ __launch_bounds__(BLOCK) void pack_lines_kernel(Batch B, ReqLine* __restrict__ lines) {
-  __shared__ uint4 st[BLOCK * (LINE_Q + 1)];  // +1 chunk per line: conflict-free staging
-  const uint32_t i0 = blockIdx.x * BLOCK, i = i0 + threadIdx.x;
-  if (i < B.n) {
-    const ReqLine L = make_line(B, i);
-    const uint4* q = reinterpret_cast<const uint4*>(&L);
-#pragma unroll
-    for (uint32_t c = 0; c < LINE_Q; ++c) st[threadIdx.x * (LINE_Q + 1) + c] = q[c];
-  }
-  __syncthreads();
-  const uint32_t m = B.n - i0 < BLOCK ? B.n - i0 : BLOCK;  // lines in this block
-  uint4* dst = reinterpret_cast<uint4*>(lines + i0);
-#pragma unroll
-  for (uint32_t r = 0; r < LINE_Q; ++r) {
-    const uint32_t c = r * BLOCK + threadIdx.x;  // chunk c of the block: line c / LINE_Q
-    if (c / LINE_Q < m) dst[c] = st[(c / LINE_Q) * (LINE_Q + 1) + c % LINE_Q];
-  }
 }
 
 __global__ __launch_bounds__(BLOCK) void radix_histogram_kernel(const uint32_t* __restrict__ keys, uint32_t n,
@@ -386,15 +342,13 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 template <class FL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
-    Tables T, Batch B, const uint32_t* __restrict__ perm, const ReqLine* __restrict__ lines,
-    Decision* __restrict__ out) {
+    Tables T, Batch B, const uint32_t* __restrict__ perm, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
-  const ReqLine* ln = in && lines ? lines + i : nullptr;  // the request's packed line (sorted batches)
   ReqHdr h{};
-  if (in) h = ln ? ln->h : B.hdr[i];
+  if (in) h = B.hdr[i];
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
@@ -409,13 +363,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
 #if defined(ACS_PHASE_PROF)
-    const ReqLds R(T, B, i, h, col, BLOCK, ln);
+    const ReqLds R(T, B, i, h, col, BLOCK);
     d = is_allowed_t(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln), F);
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -562,8 +516,6 @@ struct acs_tables {
   Tables view{};
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  hipStream_t stream2 = nullptr;            // request-line packing, overlapped with the sort
-  hipEvent_t fork = nullptr, join = nullptr;
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
@@ -730,10 +682,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
       hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) != hipSuccess ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess ||
-      hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&t->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&t->join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
     fail("acs_compile: device allocation / upload failed");
     acs_free(t);
     return nullptr;
@@ -761,9 +710,6 @@ void acs_free(acs_tables* t) {
   if (t->ev0) (void)hipEventDestroy(t->ev0);
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
-  if (t->stream2) (void)hipStreamDestroy(t->stream2);
-  if (t->fork) (void)hipEventDestroy(t->fork);
-  if (t->join) (void)hipEventDestroy(t->join);
   if (t->ws) (void)hipFree(t->ws);
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
@@ -840,11 +786,8 @@ int acs_set_option(acs_tables* t, int option, int value) {
 }
 
 // Coherence sort: permutation of request indices ordered by (class, low field).
-// lines != nullptr: the key kernel also packs every request's ReqLine (K1's request reads).
-static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm,
-                          const ReqLine** lines = nullptr) {
+static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
   *perm = nullptr;
-  if (lines) *lines = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
   // Low field: the dense role key with a role factor; otherwise none — a class row already
@@ -859,8 +802,7 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   const uint32_t passes = end_bit ? (end_bit + 7) / 8 : 1;
   const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
   const uint32_t ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
-  const size_t sort_bytes = (4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t) + 127) & ~size_t(127);
-  const size_t need = sort_bytes + (lines ? n * sizeof(ReqLine) : 0);
+  const size_t need = 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
   if (need > t->ws_bytes) {
     if (t->ws) HIP_OK(hipFree(t->ws));
     t->ws = nullptr;
@@ -874,14 +816,6 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   uint32_t* v1 = v0 + n;
   uint32_t* counts = v1 + n;
   uint32_t* gsum = counts + (size_t)RADIX * nt;
-  ReqLine* ln = lines ? (ReqLine*)((char*)t->ws + sort_bytes) : nullptr;
-  if (ln) {  // fork: the lines are packed on the second stream while the sort runs on s
-    HIP_OK(hipEventRecord(t->fork, s));
-    HIP_OK(hipStreamWaitEvent(t->stream2, t->fork, 0));
-    hipLaunchKernelGGL(pack_lines_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, t->stream2, B, ln);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(t->join, t->stream2));
-  }
   hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
   HIP_OK(hipGetLastError());
   for (uint32_t p = 0; p < passes; ++p) {
@@ -902,10 +836,6 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
     std::swap(v0, v1);
   }
   *perm = v0;
-  if (ln) {
-    HIP_OK(hipStreamWaitEvent(s, t->join, 0));  // join before K1 reads the lines
-    *lines = ln;
-  }
   return 0;
 }
 
@@ -915,14 +845,11 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
   hipStream_t s = (hipStream_t)stream;
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  const ReqLine* lines = nullptr;
-  const char* no_lines = getenv("ACS_NO_LINES");  // A/B runs: K1 reads the SoA rows
-  if (coherence_perm(t, B, s, &perm, no_lines && *no_lines == '1' ? nullptr : &lines)) return -1;
+  if (coherence_perm(t, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, lines,
-                      (Decision*)out);
+  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
