@@ -94,6 +94,7 @@ class CodecBatch:
         self.role_key = _view(s.role_key, np.uint32, n) if s.role_key else None
         self.role_bits = (_view(s.role_rows_bits, np.uint32, s.role_rows * W).reshape(s.role_rows, W)
                           if s.role_key else None)
+        self.lines = _view(s.lines, L.REQ_LINE_DT, n) if s.lines else None
         self.overlay = _Strings(self)
         self.host_reasons = {}
         for i in np.flatnonzero((self.hdr["flags"] & np.uint32(L.RQ_HOST)) != 0):
@@ -109,11 +110,12 @@ class CodecBatch:
     def nbytes(self):
         return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
             (self.cand.nbytes if self.cand is not None else 0) + \
-            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
+            (self.lines.nbytes if self.lines is not None else 0)
 
     def close(self):
         if self.h:
-            for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx", "cand", "role_key", "role_bits"):
+            for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx", "cand", "role_key", "role_bits", "lines"):
                 setattr(self, k, None)
             _lib().acs_codec_batch_free(self.h)
             self.h = None

@@ -31,6 +31,8 @@ class DeviceBatch:
         if batch.role_key is not None:
             self.t["role_key"] = _to_dev(batch.role_key, self.dev)
             self.t["role_bits"] = _to_dev(batch.role_bits, self.dev)
+        if getattr(batch, "lines", None) is not None and batch.n:
+            self.t["lines"] = _to_dev(batch.lines, self.dev)
         self.ptrs = {k: v.data_ptr() for k, v in self.t.items()}
         self.struct = batch_struct(batch, self.ptrs)
         self.nbytes = sum(v.numel() for v in self.t.values())

@@ -50,6 +50,10 @@ REQ_HDR_DT = np.dtype([("flags", u32), ("nres", u8), ("nsubj", u8), ("nact", u8)
 REQ_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("col", u16), ("contains", u16), ("kind", u8),
                        ("slot_a", u8), ("slot_b", u8), ("pad", u8)])
 DECISION_DT = np.dtype([("decision", u8), ("ec", u8), ("flags", u8), ("err", u8), ("aux", u32)])
+# acs_layout.h ReqLine: a request's first rows packed into one 128-B line
+REQ_LINE_DT = np.dtype([("h", REQ_HDR_DT), ("res", REQ_RES_DT, (4,)), ("s0", PAIR_DT), ("s1", PAIR_DT),
+                        ("a0", PAIR_DT), ("r0", u32), ("r1", u32), ("ar0", u32), ("ar1", u32), ("pad", u32, (2,))])
+assert REQ_LINE_DT.itemsize == 128
 
 SIZES = {"NodeRec": NODE_DT.itemsize, "RuleResAttr": RULE_RES_DT.itemsize, "ReqHdr": REQ_HDR_DT.itemsize,
          "ReqRes": REQ_RES_DT.itemsize, "Decision": DECISION_DT.itemsize}

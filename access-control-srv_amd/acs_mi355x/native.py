@@ -25,7 +25,7 @@ class ReqBatchC(C.Structure):
                 ("cand_rows", C.c_uint32), ("cand_wsu", C.c_uint32), ("cand_wpu", C.c_uint32),
                 ("cand_wv", C.c_uint32),
                 ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
-                ("role_rows", C.c_uint32)]
+                ("role_rows", C.c_uint32), ("lines", C.c_void_p)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -101,11 +101,14 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
         s.cand = b.cand.ctypes.data if b.cand is not None else None
         if b.role_key is not None:
             s.role_key, s.role_rows_bits = b.role_key.ctypes.data, b.role_bits.ctypes.data
+        if getattr(b, "lines", None) is not None:
+            s.lines = b.lines.ctypes.data
     else:
         for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx"):
             setattr(s, k, ptrs[k])
         s.cand = ptrs.get("cand")
         s.role_key, s.role_rows_bits = ptrs.get("role_key"), ptrs.get("role_bits")
+        s.lines = ptrs.get("lines")
     s.arena_words = int(b.arena.size)
     s.rx_cols = int(b.rx.shape[0])
     s.rx_rows = int(b.rx.shape[1])

@@ -508,6 +508,7 @@ struct acs_codec_batch {
   uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0, cand_wv = 0;
   std::vector<uint32_t> role_key, role_bits;
   uint32_t role_rows = 0;
+  std::vector<ReqLine> lines;  // [n] packed first rows (acs_layout.h ReqLine; encoder.pack_lines)
   std::vector<const char*> reason;  // per request: why it goes to the host (nullptr: it does not)
   std::vector<ThreadStrings> strings;
   double seconds[4] = {};  // parse+encode, regex matrix, candidate classes, total
@@ -1718,6 +1719,23 @@ acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int th
   Classes cl(*c, *B, T);
   cl.col_keys = keys;  // padding column: ''
   cl.run();
+  // packed first rows, after the class ids went into the headers (encoder.pack_lines)
+  B->lines.assign(n, ReqLine{});
+  for (uint32_t i = 0; i < n; ++i) {
+    ReqLine& L = B->lines[i];
+    const ReqHdr& hd = B->hdr[i];
+    L.h = hd;
+    for (uint32_t j = 0; j < hd.nres && j < (uint32_t)LINE_RES; ++j) L.res[j] = B->res[(size_t)j * n + i];
+    if (hd.nsubj > 0) L.s0 = B->subj[i];
+    if (hd.nsubj > 1) L.s1 = B->subj[(size_t)n + i];
+    if (hd.nact > 0) L.a0 = B->act[i];
+    if (hd.nroles > 0) L.r0 = B->roles[i];
+    if (hd.nroles > 1) L.r1 = B->roles[(size_t)n + i];
+    if (!(hd.flags & (RQ_HOST | RQ_NO_TARGET))) {
+      L.ar0 = B->arena[hd.arena_off];
+      L.ar1 = B->arena[hd.arena_off + 1];
+    }
+  }
   const double t3 = now_s();
   B->seconds[0] = t1 - t0;
   B->seconds[1] = t2 - t1;
@@ -1831,6 +1849,7 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
     v.role_rows_bits = b->role_bits.data();
     v.role_rows = b->role_rows;
   }
+  v.lines = b->lines.empty() ? nullptr : b->lines.data();
   *out = v;
   return 0;
 }

@@ -139,6 +139,7 @@ struct Batch {
   const uint32_t* role_key;   // [n] role-factor row per request (nullptr: no role factor)
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
+  const ReqLine* lines;       // [n] packed first rows (nullptr: read the SoA rows)
 };
 
 // OR of x over the wave's ACTIVE lanes, returned in an SGPR.  A lane drops out once its bits
@@ -335,9 +336,27 @@ struct ReqCtx {
   mutable uint64_t prof[PH_N] = {};
 #endif
 
-  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : T(t), B(b), i(idx), h(hd) {
+  // ln: the request's packed line (acs_layout.h ReqLine), nullptr: the SoA rows
+  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
+      : T(t), B(b), i(idx), h(hd) {
     ar = B.arena + h.arena_off;
-    uint32_t c0 = ar[0], c1 = ar[1];
+    if (ln) {
+      s0i = ln->s0.id; s0v = ln->s0.value; s1i = ln->s1.id; s1v = ln->s1.value;
+      a0i = ln->a0.id; a0v = ln->a0.value;
+      role0 = ln->r0;
+      role1 = ln->r1;
+      set_arena(ln->ar0, ln->ar1);
+      return;
+    }
+    set_arena(ar[0], ar[1]);
+    const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
+    const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
+    const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
+    s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
+    role0 = h.nroles > 0 ? B.roles[i] : 0u;
+    role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
+  }
+  ACS_FN void set_arena(uint32_t c0, uint32_t c1) {
     n_grants = c0 & 0xFF; n_rolese = (c0 >> 8) & 0xFF; n_slots = (c0 >> 16) & 0xFF; n_roots = c0 >> 24;
     n_tse = c1 & 0xFF; n_hrkeys = (c1 >> 8) & 0xFF;
     grants = ar + 2;
@@ -346,12 +365,6 @@ struct ReqCtx {
     hrkeys = roots + n_roots;
     slotoff = hrkeys + n_hrkeys;
     tse = slotoff + n_slots;
-    const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
-    const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
-    const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
-    s0i = s0.id; s0v = s0.value; s1i = s1.id; s1v = s1.value; a0i = a0.id; a0v = a0.value;
-    role0 = h.nroles > 0 ? B.roles[i] : 0u;
-    role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
   }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
@@ -387,8 +400,9 @@ struct ReqLds : ReqCtx {
   const ReqRes* col;  // this lane's LDS column
   uint32_t stride;
   uint32_t e0_val, e0_col;  // the request's only entity attribute (RQ_ENT_SHIFT field 1..6)
-  ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st)
-      : ReqCtx(t, b, idx, hd), col(c), stride(st) {
+  ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st,
+                const ReqLine* ln = nullptr)
+      : ReqCtx(t, b, idx, hd, ln), col(c), stride(st) {
     const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
     e0_val = e0_col = 0;
     if (e >= 1 && e <= 6) {

@@ -347,8 +347,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;  // one gather for the first rows
   ReqHdr h{};
-  if (in) h = B.hdr[i];
+  if (in) h = ln ? ln->h : B.hdr[i];
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
@@ -363,13 +364,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
 #if defined(ACS_PHASE_PROF)
-    const ReqLds R(T, B, i, h, col, BLOCK);
+    const ReqLds R(T, B, i, h, col, BLOCK, ln);
     d = is_allowed_t(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK), F);
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -764,6 +765,8 @@ static Batch to_batch(const acs_req_batch* b) {
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
+  const char* no_lines = getenv("ACS_NO_LINES");  // A/B runs: K1 reads the SoA rows
+  B.lines = no_lines && *no_lines == '1' ? nullptr : (const ReqLine*)b->lines;
   return B;
 }
 
@@ -969,6 +972,7 @@ int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
   if (b->cand && D.up(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t),
                       (const void**)&D.d.cand, s))
     return -1;
+  if (b->lines && D.up(b->lines, n * sizeof(ReqLine), &D.d.lines, s)) return -1;
   if (b->role_key && (D.up(b->role_key, n * sizeof(uint32_t), (const void**)&D.d.role_key, s) ||
                       D.up(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
                            (const void**)&D.d.role_rows_bits, s)))

@@ -164,6 +164,22 @@ struct ReqRes {              // 16 B
 };
 constexpr uint32_t RES_RX_SAFE = 1;  // ReqRes.pad bit (absent: the request may throw in a RegExp test)
 
+// One request's first rows packed into one 128-B line (acs_req_batch.lines, optional): K1
+// reads it with one gather instead of one per SoA row (header, 4 attributes, 2 subjects,
+// action, 2 roles, arena counts: ~8 lines per request).  Every field equals the SoA rows:
+// res[j] / s* / a0 / r* zero past the request's counts, ar0 / ar1 the arena's two count words
+// (0 for RQ_HOST / RQ_NO_TARGET requests).  Built by both encoders (encoder.pack_lines,
+// acs_codec.cpp) and checked against the SoA rows by the host entry points.
+constexpr int LINE_RES = 4;
+struct ReqLine {             // 128 B
+  ReqHdr h;
+  ReqRes res[LINE_RES];
+  Pair s0, s1, a0;
+  uint32_t r0, r1;
+  uint32_t ar0, ar1;
+  uint32_t pad[2];
+};
+
 // Context arena (u32 words), per request:
 //   [0] n_grants | n_rolese<<8 | n_slots<<16 | n_roots<<24
 //   [1] n_tse | n_hrkeys<<8

@@ -8,6 +8,7 @@
 // device code follows must land inside its buffer.  The *_device entry points take
 // device-resident batches (normally from acs_codec_encode, which writes them consistent)
 // and are not walked.
+#include <cstring>
 #include <stdio.h>
 #include <string.h>
 
@@ -94,6 +95,7 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
   const ReqHdr* hdr = (const ReqHdr*)b->hdr;
   const ReqRes* res = (const ReqRes*)b->res;
   const size_t W = b->arena_words;
+  const ReqLine* lines = (const ReqLine*)b->lines;
   for (size_t i = 0; i < n; ++i) {
     const ReqHdr hd = hdr[i];
     if (hd.nres > QMAX || hd.nsubj > SMAX || hd.nact > AMAX || hd.nroles > RMAX) return bad("batch: counts", i);
@@ -101,6 +103,23 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
     if (o + 2 > W) return bad("batch: arena offset", i);
     const uint32_t* ar = b->arena + o;
     const size_t room = W - o;
+    if (lines) {  // the packed line must equal the SoA rows (K1 trusts it for addressing)
+      ReqLine want{};
+      want.h = hd;
+      for (uint32_t j = 0; j < hd.nres && j < (uint32_t)LINE_RES; ++j) want.res[j] = res[j * n + i];
+      const Pair* subj = (const Pair*)b->subj;
+      const Pair* act = (const Pair*)b->act;
+      if (hd.nsubj > 0) want.s0 = subj[i];
+      if (hd.nsubj > 1) want.s1 = subj[n + i];
+      if (hd.nact > 0) want.a0 = act[i];
+      if (hd.nroles > 0) want.r0 = b->roles[i];
+      if (hd.nroles > 1) want.r1 = b->roles[n + i];
+      if (!(hd.flags & (RQ_HOST | RQ_NO_TARGET))) {
+        want.ar0 = ar[0];
+        want.ar1 = ar[1];
+      }
+      if (std::memcmp(&want, &lines[i], sizeof want) != 0) return bad("batch: request line differs from its rows", i);
+    }
     const uint32_t c0 = ar[0], c1 = ar[1];
     const uint32_t ng = c0 & 0xFF, nre = (c0 >> 8) & 0xFF, ns = (c0 >> 16) & 0xFF, nro = c0 >> 24;
     const uint32_t nt = c1 & 0xFF, nh = (c1 >> 8) & 0xFF;

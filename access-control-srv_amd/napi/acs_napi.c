@@ -107,9 +107,19 @@ static void codec_unref(codec_h* h) {
   }
 }
 
+/* Set by an environment cleanup hook when Node tears the environment down: the finalizers
+ * that run after it leave the native state to the process exit (the C++ runtime's statics
+ * and the HIP runtime may already be gone), instead of freeing into them. */
+static int g_env_exiting = 0;
+static void on_env_exit(void* arg) {
+  (void)arg;
+  g_env_exiting = 1;
+}
+
 static void fin_tables(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
+  if (g_env_exiting) return;
   tables_h* h = (tables_h*)data;
   h->closed = 1;
   if (h->inflight == 0) tables_release(h);
@@ -119,12 +129,14 @@ static void fin_tables(napi_env env, void* data, void* hint) {
 static void fin_codec(napi_env env, void* data, void* hint) {
   (void)env;
   (void)hint;
+  if (g_env_exiting) return;
   codec_unref((codec_h*)data);
 }
 
 static void fin_batch(napi_env env, void* data, void* hint) {
   batch_h* h = (batch_h*)data;
   (void)hint;
+  if (g_env_exiting) return;
   if (h->b) acs_codec_batch_free(h->b); /* before its codec */
   if (h->codec) codec_unref(h->codec);
   h->magic = 0;
@@ -916,6 +928,7 @@ static napi_value js_last_error(napi_env env, napi_callback_info info) {
 }
 
 static napi_value init(napi_env env, napi_value exports) {
+  napi_add_env_cleanup_hook(env, on_env_exit, NULL);
   const napi_property_descriptor d[] = {
       {"compileStore", NULL, js_compile_store, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -72,6 +72,11 @@ typedef struct {
   const uint32_t* role_key;
   const uint32_t* role_rows_bits;
   uint32_t role_rows;
+  /* Optional [n] 128-B ReqLine (csrc/acs_layout.h): each request's header, first 4 resource
+   * attributes, 2 subjects, action, 2 roles and arena counts in one line, equal to the SoA
+   * rows above (checked by the host entry points).  The evaluation kernel then reads a
+   * request with one gather instead of ~8.  NULL = read the SoA rows. */
+  const void* lines;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */
@@ -114,7 +119,7 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* dev_batch, acs_dec
  * bit (i & 31) of its word i >> 5.  The device form needs a 16-byte aligned `bits`.
  * obl: [n][ACS_OBL_MAX][2] maskedProperty push log (entity id, mask id), obl_n: [n]; log entries
  * past a request's count are unspecified. */
-#define ACS_OBL_MAX 64
+#define ACS_OBL_MAX 128
 uint32_t acs_wia_words_per_request(const acs_tables* t);
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* host_batch, uint32_t* bits, uint32_t* obl,
                         uint32_t* obl_n, acs_decision* out);

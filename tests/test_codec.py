@@ -60,6 +60,10 @@ def compare_batches(pb, nb, check_cols=True):
         # context arena: same length per request (contents hold batch-local ids)
     if check_cols:
         assert pb.rx.shape == nb.rx.shape and np.array_equal(pb.rx, nb.rx)
+    # packed request lines: both encoders emit exactly the lines of their own rows
+    for x in (pb, nb):
+        assert x.lines is not None
+        assert x.lines.tobytes() == encoder.pack_lines(x).tobytes()
 
 
 def decisions_equal(cs, pb, nb):

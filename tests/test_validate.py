@@ -76,7 +76,7 @@ def _mut(b, field, fn):
         pass
     c = B()
     for k in ("n", "hdr", "res", "subj", "act", "roles", "arena", "rx", "cand", "cand_wp", "cand_wr",
-              "role_key", "role_bits"):
+              "role_key", "role_bits", "lines"):
         v = getattr(b, k, None)
         setattr(c, k, v.copy() if isinstance(v, np.ndarray) else v)
     fn(getattr(c, field), c)
@@ -105,7 +105,10 @@ def test_corrupt_batches_refused(lib):
         "context slot": _mut(b, "res", lambda a, c: a["slot_a"].__setitem__((0, with_slots), 200)),
         "candidate layout": _mut(b, "cand", lambda a, c: setattr(c, "cand_wr", c.cand_wp)),
         "regex rows": _mut(b, "rx", lambda a, c: setattr(c, "rx", a[:, :max(_rows(cs) - 1, 0)].copy())),
+        "request line": _mut(b, "lines", lambda a, c: a["h"]["arena_off"].__setitem__(7, a["h"]["arena_off"][7] + 1)),
+        "request line attribute": _mut(b, "lines", lambda a, c: a["res"]["col"].__setitem__((2, 0), 7)),
     }
+    assert b.lines is not None
     for what, c in bad.items():
         c.n = b.n
         assert _check(lib, cs, c) != 0, what
