@@ -398,8 +398,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;  // one gather for the first rows
   ReqHdr h{};
-  if (in) h = B.hdr[i];
+  if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                      wave_lds_row(B));
@@ -412,8 +413,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   } else {
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = B.res[(size_t)j * B.n + i];
-    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, BL, sink, log);
+    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
+    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln), F, BL, sink, log);
   }
   sink.finish();
   obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
