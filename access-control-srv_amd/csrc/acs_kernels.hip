@@ -23,6 +23,11 @@
 
 using namespace acs;
 
+#if defined(ACS_SCAN_COUNT)  // the counting build's kernels carry their own names in traces / PMC passes
+#define is_allowed_kernel is_allowed_kernel_scan_count
+#define what_is_allowed_kernel what_is_allowed_kernel_scan_count
+#endif
+
 namespace {
 
 thread_local std::string g_err;

@@ -383,7 +383,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic(traffic_key("c4", n, world, "requests"),
                                                                                       "what_is_allowed_kernel")[0],
-                         "kernel": "what_is_allowed_kernel (+ bitset_transpose_kernel, timed together)",
+                         "kernel": "what_is_allowed_kernel",
                          "kernel_ms": kern_ms, "bytes_per_query": per,
                          "bytes_parts": parts, "output_GBps": (4 * words + 8 * float(obl_n.mean()) + 12) * n /
                          (kern_ms * 1e-3) / 1e9},

@@ -28,7 +28,7 @@ for s in $STEPS; do
     quick) step bench_quick 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline --no-pcie ;;
     quick3) step bench_c3_quick 900 python bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
-    prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie ;;
+    prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 ;;
     quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
     ab) for cfg in ${AB_CONFIGS:-c2 c3}; do
           st=20; [ "$cfg" = c3 ] && st=5
