@@ -390,9 +390,11 @@ struct ReqCtx {
 // Resource attributes staged in LDS by the kernel (slots < LDS_SLOTS, column = lane,
 // stride = block size): dynamic indexing without scratch, one ds_read_b128 per use.
 #ifndef ACS_LDS_SLOTS
-// 6 x 16 B x 256 lanes = 24 KB: with a c3 filter row (832 words x 4 waves, 13 KB) a block
-// fits 4 times into the CU's 160 KB of LDS (8 slots: 3 blocks; A/B c3 20.6 -> 17.6 ms)
-#define ACS_LDS_SLOTS 6
+// 4 x 16 B x 256 lanes = 16 KB: with a c3 filter row (832 words x 4 waves, 13 KB) a block
+// fits 5 times into the CU's 160 KB of LDS, for K1's 5 waves/SIMD (A/B r02_q: 6 slots 1.98,
+// 4 slots 1.95, 4 slots + 5 waves 1.87 ms at c3; 8 slots: 3 blocks/CU, round-2 A/B 20.6 vs
+// 17.6 ms with 6).  Attributes past the slots are read from HBM.
+#define ACS_LDS_SLOTS 4
 #endif
 constexpr int LDS_SLOTS = ACS_LDS_SLOTS;
 

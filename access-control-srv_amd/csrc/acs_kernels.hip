@@ -343,7 +343,9 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
-#define ACS_K1_WAVES_PER_EU 4  // measured: 4 waves/SIMD (VGPR <= 128) beats 3 (+12% c2, +13% c3), 5+ spill
+// 5 waves/SIMD (VGPR <= 96, with 4 LDS attribute slots so 5 blocks fit a CU's LDS): c3 K1
+// 1.98 -> 1.87 ms in a same-call A/B (r02_q; c2 0.180 -> 0.190 ms), 4 slots alone 1.95 ms
+#define ACS_K1_WAVES_PER_EU 5
 #endif
 template <class FL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
