@@ -780,6 +780,7 @@ static Batch to_batch(const acs_req_batch* b) {
 
 int acs_set_option(acs_tables* t, int option, int value) {
   if (!t) return fail("acs_set_option: null tables");
+  std::lock_guard<std::mutex> lock(t->mu);  // the host-buffer entry points read these under it
   if (option == ACS_OPT_SORT) {
     t->sort = value ? 1 : 0;
     return 0;

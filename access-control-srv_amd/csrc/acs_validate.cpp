@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <cstddef>
+#include <vector>
 
 #include "../../include/acs_mi355x.h"
 #include "acs_layout.h"
@@ -92,6 +93,19 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
       return bad("batch: candidate row layout", b->cand_words);
     if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
   }
+  // RES_RX_SAFE on an attribute lets K1 stop early (the clean-below set walk, the final-fold
+  // cuts): it claims that no cell of the value's regex-matrix column throws or needs the host.
+  // Checked per column once (RX_THROW_TYPE | RX_THROW_SYNTAX | RX_HOST = 4 | 8 | 16).
+  std::vector<uint8_t> col_unsafe;
+  if (rx_rows_min && b->rx) {
+    col_unsafe.assign(b->rx_cols, 0);
+    for (size_t c = 0; c < b->rx_cols; ++c)
+      for (size_t r = 0; r < b->rx_rows; ++r)
+        if (b->rx[c * b->rx_rows + r] & 0x1Cu) {
+          col_unsafe[c] = 1;
+          break;
+        }
+  }
   const ReqHdr* hdr = (const ReqHdr*)b->hdr;
   const ReqRes* res = (const ReqRes*)b->res;
   const size_t W = b->arena_words;
@@ -150,6 +164,8 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
       const ReqRes q = res[(size_t)j * n + i];
       if (rx_rows_min && ((q.kind & K_ENT_LOOSE) || j == e0) && q.col >= b->rx_cols)
         return bad("batch: regex matrix column", i);
+      if (!col_unsafe.empty() && (q.kind & K_ENT_LOOSE) && (q.pad & RES_RX_SAFE) && col_unsafe[q.col])
+        return bad("batch: RES_RX_SAFE on a regex column that throws or needs the host", i);
       if ((q.slot_a != NONE8 && q.slot_a >= ns) || (q.slot_b != NONE8 && q.slot_b >= ns))
         return bad("batch: context resource slot", i);
     }

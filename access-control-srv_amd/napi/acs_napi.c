@@ -11,6 +11,7 @@
  *   compile(blob: Uint8Array, device?) -> tables                acs_compile
  *   free(tables)                                                acs_free (deferred past in-flight work)
  *   codecCreate(blob) -> codec                                  acs_codec_create
+ *   codecFree(codec), batchFree(batch)                          acs_codec_free / acs_codec_batch_free
  *   codecSetSubjectScopes(codec, key, scopesJson)               acs_codec_set_subject_scopes
  *   codecEvictSubject(codec, key) -> bool                       acs_codec_evict_subject
  *   codecEcValues(codec) -> string (JSON array)                 acs_codec_ec_values
@@ -29,10 +30,12 @@
  * roleRows]} of typed arrays in the layout of csrc/acs_layout.h; every array is checked
  * against the sizes `n` and the counts imply before the library reads it.
  *
- * Handles are externals with finalizers: a garbage-collected handle releases its GPU
- * tables / codec / batch.  free() on tables with async work in flight defers the release
- * until that work completes; any call on a freed handle throws.  A batch keeps its codec
- * alive (a reference), the codec's dictionary being part of the batch's meaning.
+ * Handles are plain objects naming a per-environment registry slot (see "handles" below:
+ * no napi externals, whose weak references Node 12 can touch after freeing them at exit).
+ * They are released explicitly (free / codecFree / batchFree) or at environment teardown.
+ * free() on tables with async work in flight defers the release until that work completes;
+ * any call on a freed handle throws.  A batch keeps its codec alive (a counted reference), the
+ * codec's dictionary being part of the batch's meaning.
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
@@ -62,115 +65,213 @@ static napi_value throw_acs(napi_env env, const char* what) {
   return NULL;
 }
 
-/* ------------------------------------------------------------------ handles */
-enum { H_TABLES = 0x54424c31, H_CODEC = 0x434f4431, H_BATCH = 0x42415431 };
+/* ------------------------------------------------------------------ handles
+ * A handle is a plain JS object ({acsTables: id}, {acsCodec: id} or {acsBatch: id}) naming a
+ * slot of this environment's registry, not a napi external.  Node 12's environment teardown
+ * (napi_env__'s destructor, RefTracker::FinalizeAll) deletes every napi reference while V8 may
+ * still hold a queued second-pass phantom callback for an external collected just before
+ * exit; Environment::CleanupHandles then runs that callback on the deleted reference
+ * (SIGSEGV in v8::internal::GlobalHandles::PendingPhantomCallback::Invoke, reproduced with a
+ * backtrace: 22 of 128 runs of tests/js/gpu_codec_run.js under load).  A handle that holds no
+ * weak reference cannot be hit.  Lifetimes are therefore explicit — free(tables),
+ * codecFree(codec), batchFree(batch) — and whatever is still registered when the environment
+ * is torn down is released by its cleanup hook (objects with work in flight are left to the
+ * process exit).  Each environment (main thread, worker_threads) has its own registry. */
+enum { H_TABLES = 1, H_CODEC = 2, H_BATCH = 3 };
+static const char* const KIND_KEY[4] = {"", "acsTables", "acsCodec", "acsBatch"};
+
+typedef struct env_state env_state;
 
 typedef struct {
-  int magic;
+  int kind;
+  env_state* st;
+  uint32_t slot; /* registry slot while the JS handle is live, UINT32_MAX after free */
+  int refs;      /* the JS handle + in-flight work (+ live batches, for a codec) */
+} obj_base;
+
+typedef struct {
+  obj_base base;
   acs_tables* t;
-  int closed;   /* free() called */
   int inflight; /* async work items using t */
-  int refs;     /* the external + in-flight work: the struct outlives both */
 } tables_h;
 
 typedef struct {
-  int magic;
+  obj_base base;
   acs_codec* c;
-  int refs; /* the external + live batches + in-flight work (finalizers run in any order at exit) */
 } codec_h;
 
 typedef struct {
-  int magic;
+  obj_base base;
   acs_codec_batch* b;
-  codec_h* codec; /* counted reference: the codec outlives its batches (no napi_ref, which a
-                     finalizer may not delete once the environment is torn down at exit) */
+  codec_h* codec; /* counted reference: the codec outlives its batches */
 } batch_h;
 
-static void tables_release(tables_h* h) {
-  if (h->t) acs_free(h->t);
-  h->t = NULL;
-}
+typedef struct {
+  int kind; /* 0: never used */
+  uint32_t gen;
+  obj_base* obj; /* NULL: freed (slot reusable) */
+} slot_t;
 
-static void tables_unref(tables_h* h) {
-  if (--h->refs == 0) {
-    tables_release(h);
-    h->magic = 0;
-    free(h);
-  }
-}
+struct env_state {
+  slot_t* slots;
+  uint32_t n, cap;
+  int dead; /* the environment is being torn down */
+};
 
-static void codec_unref(codec_h* h) {
-  if (--h->refs == 0) {
+static void obj_unref(obj_base* o);
+
+static void obj_release(obj_base* o) {
+  if (o->kind == H_TABLES) {
+    tables_h* h = (tables_h*)o;
+    if (h->t) acs_free(h->t);
+    h->t = NULL;
+  } else if (o->kind == H_CODEC) {
+    codec_h* h = (codec_h*)o;
     if (h->c) acs_codec_free(h->c);
-    h->magic = 0;
-    free(h);
+    h->c = NULL;
+  } else if (o->kind == H_BATCH) {
+    batch_h* h = (batch_h*)o;
+    if (h->b) acs_codec_batch_free(h->b); /* before its codec */
+    h->b = NULL;
+    if (h->codec) obj_unref(&h->codec->base);
+    h->codec = NULL;
   }
+  o->kind = 0;
+  free(o);
 }
 
-/* Set by an environment cleanup hook when Node tears the environment down: the finalizers
- * that run after it leave the native state to the process exit (the C++ runtime's statics
- * and the HIP runtime may already be gone), instead of freeing into them. */
-static int g_env_exiting = 0;
+static void obj_unref(obj_base* o) {
+  if (--o->refs == 0) obj_release(o);
+}
+
 static void on_env_exit(void* arg) {
-  (void)arg;
-  g_env_exiting = 1;
+  env_state* st = (env_state*)arg;
+  st->dead = 1;
+  /* batches first (they hold their codec), then codecs and tables */
+  static const int order[3] = {H_BATCH, H_CODEC, H_TABLES};
+  for (int k = 0; k < 3; ++k)
+    for (uint32_t i = 0; i < st->n; ++i) {
+      slot_t* s = &st->slots[i];
+      if (!s->obj || s->obj->kind != order[k]) continue;
+      obj_base* o = s->obj;
+      s->obj = NULL;
+      o->slot = UINT32_MAX;
+      if (o->kind == H_TABLES && ((tables_h*)o)->inflight) continue; /* the pool still uses it */
+      obj_unref(o);
+    }
 }
 
-static void fin_tables(napi_env env, void* data, void* hint) {
-  (void)env;
-  (void)hint;
-  if (g_env_exiting) return;
-  tables_h* h = (tables_h*)data;
-  h->closed = 1;
-  if (h->inflight == 0) tables_release(h);
-  tables_unref(h);
+static env_state* get_state(napi_env env) {
+  void* d = NULL;
+  if (napi_get_instance_data(env, &d) == napi_ok && d) return (env_state*)d;
+  env_state* st = (env_state*)calloc(1, sizeof *st);
+  if (!st) return NULL;
+  /* no finalizer: the struct is tiny and may be read by work completing during teardown */
+  if (napi_set_instance_data(env, st, NULL, NULL) != napi_ok) {
+    free(st);
+    return NULL;
+  }
+  napi_add_env_cleanup_hook(env, on_env_exit, st);
+  return st;
 }
 
-static void fin_codec(napi_env env, void* data, void* hint) {
-  (void)env;
-  (void)hint;
-  if (g_env_exiting) return;
-  codec_unref((codec_h*)data);
+/* Register `o` (refs = 1, the JS handle) and return its handle object. */
+static napi_value make_handle(napi_env env, obj_base* o, int kind) {
+  env_state* st = get_state(env);
+  napi_value h, id;
+  o->kind = kind;
+  o->st = st;
+  o->refs = 1;
+  o->slot = UINT32_MAX;
+  if (!st) goto fail;
+  uint32_t i = 0;
+  while (i < st->n && st->slots[i].obj) ++i;
+  if (i == st->n) {
+    if (st->n == st->cap) {
+      const uint32_t cap = st->cap ? 2 * st->cap : 64;
+      slot_t* s = (slot_t*)realloc(st->slots, cap * sizeof *s);
+      if (!s) goto fail;
+      memset(s + st->cap, 0, (cap - st->cap) * sizeof *s);
+      st->slots = s;
+      st->cap = cap;
+    }
+    ++st->n;
+  }
+  slot_t* s = &st->slots[i];
+  s->kind = kind;
+  s->gen = (s->gen + 1) & 0x0FFFFFFFu;
+  s->obj = o;
+  o->slot = i;
+  const double v = (double)s->gen * 16777216.0 + (double)i; /* < 2^53 */
+  napi_property_descriptor d = {KIND_KEY[kind], NULL, NULL, NULL, NULL, NULL, napi_enumerable, NULL};
+  if (napi_create_double(env, v, &id) != napi_ok || napi_create_object(env, &h) != napi_ok) goto fail;
+  d.value = id;
+  if (napi_define_properties(env, h, 1, &d) != napi_ok) goto fail;
+  return h;
+fail:
+  if (o->slot != UINT32_MAX) st->slots[o->slot].obj = NULL;
+  o->slot = UINT32_MAX;
+  obj_unref(o);
+  napi_throw_error(env, NULL, "could not register a handle");
+  return NULL;
 }
 
-static void fin_batch(napi_env env, void* data, void* hint) {
-  batch_h* h = (batch_h*)data;
-  (void)hint;
-  if (g_env_exiting) return;
-  if (h->b) acs_codec_batch_free(h->b); /* before its codec */
-  if (h->codec) codec_unref(h->codec);
-  h->magic = 0;
-  free(h);
-}
-
-static void* get_ext(napi_env env, napi_value v, int magic) {
+/* The live object a handle names, or NULL: *freed = 1 when it names a handle of this kind
+ * that was already freed. */
+static obj_base* lookup(napi_env env, napi_value v, int kind, int* freed) {
   napi_valuetype t;
-  void* p = NULL;
-  if (napi_typeof(env, v, &t) != napi_ok || t != napi_external) return NULL;
-  if (napi_get_value_external(env, v, &p) != napi_ok || !p) return NULL;
-  return *(int*)p == magic ? p : NULL;
+  napi_value idv;
+  bool has = false;
+  double d = -1;
+  *freed = 0;
+  env_state* st = get_state(env);
+  if (!st || napi_typeof(env, v, &t) != napi_ok || t != napi_object) return NULL;
+  if (napi_has_named_property(env, v, KIND_KEY[kind], &has) != napi_ok || !has) return NULL;
+  if (napi_get_named_property(env, v, KIND_KEY[kind], &idv) != napi_ok ||
+      napi_get_value_double(env, idv, &d) != napi_ok || !(d >= 0) || d >= 9007199254740992.0)
+    return NULL;
+  const uint64_t id = (uint64_t)d;
+  const uint32_t i = (uint32_t)(id & 0xFFFFFFu), gen = (uint32_t)(id >> 24);
+  if (i >= st->n || st->slots[i].kind != kind || st->slots[i].gen != gen) return NULL;
+  if (!st->slots[i].obj) {
+    *freed = 1;
+    return NULL;
+  }
+  return st->slots[i].obj;
+}
+
+/* JS free of a handle: the slot is released now, the object when its last ref goes. */
+static void handle_free(obj_base* o) {
+  if (o->slot != UINT32_MAX && o->st) o->st->slots[o->slot].obj = NULL;
+  o->slot = UINT32_MAX;
+  obj_unref(o);
 }
 
 static tables_h* get_tables(napi_env env, napi_value v) {
-  tables_h* h = (tables_h*)get_ext(env, v, H_TABLES);
+  int freed;
+  tables_h* h = (tables_h*)lookup(env, v, H_TABLES, &freed);
   if (!h) {
-    napi_throw_type_error(env, NULL, "expected a tables handle (compile())");
-    return NULL;
-  }
-  if (h->closed || !h->t) {
-    napi_throw_error(env, NULL, "tables handle already freed");
+    if (freed) napi_throw_error(env, NULL, "tables handle already freed");
+    else napi_throw_type_error(env, NULL, "expected a tables handle (compile())");
     return NULL;
   }
   return h;
 }
 
 static codec_h* get_codec(napi_env env, napi_value v) {
-  codec_h* h = (codec_h*)get_ext(env, v, H_CODEC);
-  if (!h || !h->c) {
-    napi_throw_type_error(env, NULL, "expected a codec handle (codecCreate())");
+  int freed;
+  codec_h* h = (codec_h*)lookup(env, v, H_CODEC, &freed);
+  if (!h) {
+    if (freed) napi_throw_error(env, NULL, "codec handle already freed");
+    else napi_throw_type_error(env, NULL, "expected a codec handle (codecCreate())");
     return NULL;
   }
   return h;
+}
+
+static batch_h* find_batch(napi_env env, napi_value v) {
+  int freed;
+  return (batch_h*)lookup(env, v, H_BATCH, &freed);
 }
 
 /* ------------------------------------------------------------------ buffers */
@@ -267,7 +368,7 @@ static int field(napi_env env, napi_value obj, const char* key, size_t need, int
  * against the sizes its counts imply (pointers into JS buffers; the caller keeps them alive). */
 static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
   memset(b, 0, sizeof *b);
-  batch_h* bh = (batch_h*)get_ext(env, v, H_BATCH);
+  batch_h* bh = find_batch(env, v);
   if (bh) return acs_codec_batch_view(bh->b, b) == 0 ? 0 : -1;
   napi_valuetype t;
   if (napi_typeof(env, v, &t) != napi_ok || t != napi_object) return -1;
@@ -417,10 +518,8 @@ static napi_value js_compile(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "out of memory");
     return NULL;
   }
-  h->magic = H_TABLES;
   h->t = t;
-  h->refs = 1;
-  CHECK(env, napi_create_external(env, h, fin_tables, NULL, &out));
+  out = make_handle(env, &h->base, H_TABLES);
   return out;
 }
 
@@ -428,15 +527,13 @@ static napi_value js_free(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  tables_h* h = argc > 0 ? (tables_h*)get_ext(env, argv[0], H_TABLES) : NULL;
+  int freed = 0;
+  tables_h* h = argc > 0 ? (tables_h*)lookup(env, argv[0], H_TABLES, &freed) : NULL;
   if (!h) {
-    napi_throw_type_error(env, NULL, "free(tables)");
-    return NULL;
+    if (!freed) napi_throw_type_error(env, NULL, "free(tables)");
+    return NULL; /* freeing twice is a no-op */
   }
-  if (!h->closed) {
-    h->closed = 1;
-    if (h->inflight == 0) tables_release(h);  /* else: the last completing work item releases */
-  }
+  handle_free(&h->base); /* work in flight holds its own reference: the last one releases */
   return NULL;
 }
 
@@ -464,7 +561,7 @@ static napi_value js_is_allowed(napi_env env, napi_callback_info info) {
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
-  napi_ref keep_tables, keep_batch, keep_out, keep_codec;
+  napi_ref keep_batch, keep_out; /* strong references (no weak callbacks) */
   tables_h* th;
   codec_h* ch;
   acs_req_batch b;
@@ -481,8 +578,7 @@ typedef struct {
 
 static void work_done_tables(async_req* r) {
   r->th->inflight--;
-  if (r->th->closed && r->th->inflight == 0) tables_release(r->th);
-  tables_unref(r->th);
+  obj_unref(&r->th->base);
 }
 
 static void exec_is_allowed(napi_env env, void* data) {
@@ -505,7 +601,6 @@ static void done_is_allowed(napi_env env, napi_status status, void* data) {
     napi_create_error(env, NULL, msg, &err);
     napi_reject_deferred(env, r->deferred, err);
   }
-  napi_delete_reference(env, r->keep_tables);
   napi_delete_reference(env, r->keep_batch);
   napi_delete_reference(env, r->keep_out);
   napi_delete_async_work(env, r->work);
@@ -539,14 +634,13 @@ static napi_value js_is_allowed_async(napi_env env, napi_callback_info info) {
     return NULL;
   }
   r->out = (acs_decision*)out;
-  CHECK(env, napi_create_reference(env, argv[0], 1, &r->keep_tables));
   CHECK(env, napi_create_reference(env, argv[1], 1, &r->keep_batch));
   CHECK(env, napi_create_reference(env, arr, 1, &r->keep_out));
   CHECK(env, napi_create_promise(env, &r->deferred, &promise));
   CHECK(env, napi_create_string_utf8(env, "acs_is_allowed", NAPI_AUTO_LENGTH, &name));
   CHECK(env, napi_create_async_work(env, NULL, name, exec_is_allowed, done_is_allowed, r, &r->work));
   th->inflight++;
-  th->refs++;
+  th->base.refs++;
   CHECK(env, napi_queue_async_work(env, r->work));
   return promise;
 }
@@ -614,11 +708,9 @@ static void done_decide(napi_env env, napi_status status, void* data) {
     napi_reject_deferred(env, r->deferred, err);
   }
   if (r->enc) acs_codec_batch_free(r->enc);
-  codec_unref(r->ch);
+  obj_unref(&r->ch->base);
   free(r->out);
   if (r->text_owned) free(r->text);
-  napi_delete_reference(env, r->keep_tables);
-  napi_delete_reference(env, r->keep_codec);
   if (r->keep_batch) napi_delete_reference(env, r->keep_batch);
   napi_delete_async_work(env, r->work);
   free(r);
@@ -651,14 +743,12 @@ static napi_value js_decide_async(napi_env env, napi_callback_info info) {
     return NULL;
   }
   if (!r->text_owned) CHECK(env, napi_create_reference(env, argv[2], 1, &r->keep_batch));  /* borrowed bytes */
-  CHECK(env, napi_create_reference(env, argv[0], 1, &r->keep_tables));
-  CHECK(env, napi_create_reference(env, argv[1], 1, &r->keep_codec));
   CHECK(env, napi_create_promise(env, &r->deferred, &promise));
   CHECK(env, napi_create_string_utf8(env, "acs_decide", NAPI_AUTO_LENGTH, &name));
   CHECK(env, napi_create_async_work(env, NULL, name, exec_decide, done_decide, r, &r->work));
   th->inflight++;
-  th->refs++;
-  ch->refs++;
+  th->base.refs++;
+  ch->base.refs++;
   CHECK(env, napi_queue_async_work(env, r->work));
   return promise;
 }
@@ -682,11 +772,40 @@ static napi_value js_codec_create(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "out of memory");
     return NULL;
   }
-  h->magic = H_CODEC;
   h->c = c;
-  h->refs = 1;
-  CHECK(env, napi_create_external(env, h, fin_codec, NULL, &out));
+  out = make_handle(env, &h->base, H_CODEC);
   return out;
+}
+
+/* codecFree(codec): release the JS handle; the codec itself goes once its batches and any
+ * work in flight are done with it.  Freeing twice is a no-op. */
+static napi_value js_codec_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  int freed = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  codec_h* h = argc > 0 ? (codec_h*)lookup(env, argv[0], H_CODEC, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "codecFree(codec)");
+    return NULL;
+  }
+  handle_free(&h->base);
+  return NULL;
+}
+
+/* batchFree(batch): release an encode() batch (and its reference on the codec). */
+static napi_value js_batch_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  int freed = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  batch_h* h = argc > 0 ? (batch_h*)lookup(env, argv[0], H_BATCH, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "batchFree(batch)");
+    return NULL;
+  }
+  handle_free(&h->base);
+  return NULL;
 }
 
 static napi_value js_codec_set_scopes(napi_env env, napi_callback_info info) {
@@ -770,11 +889,10 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
     napi_throw_error(env, NULL, "out of memory");
     return NULL;
   }
-  bh->magic = H_BATCH;
   bh->b = b;
   bh->codec = h;
-  h->refs++;
-  CHECK(env, napi_create_external(env, bh, fin_batch, NULL, &out));
+  h->base.refs++;
+  out = make_handle(env, &bh->base, H_BATCH);
   return out;
 }
 
@@ -782,7 +900,7 @@ static napi_value js_batch_info(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], res, v;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  batch_h* bh = argc == 1 ? (batch_h*)get_ext(env, argv[0], H_BATCH) : NULL;
+  batch_h* bh = argc == 1 ? find_batch(env, argv[0]) : NULL;
   if (!bh) {
     napi_throw_type_error(env, NULL, "batchInfo(batch)");
     return NULL;
@@ -801,7 +919,7 @@ static napi_value js_batch_string(napi_env env, napi_callback_info info) {
   napi_value argv[2], v;
   uint32_t id;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
-  batch_h* bh = argc == 2 ? (batch_h*)get_ext(env, argv[0], H_BATCH) : NULL;
+  batch_h* bh = argc == 2 ? find_batch(env, argv[0]) : NULL;
   if (!bh || napi_get_value_uint32(env, argv[1], &id) != napi_ok) {
     napi_throw_type_error(env, NULL, "batchString(batch, id)");
     return NULL;
@@ -928,12 +1046,14 @@ static napi_value js_last_error(napi_env env, napi_callback_info info) {
 }
 
 static napi_value init(napi_env env, napi_value exports) {
-  napi_add_env_cleanup_hook(env, on_env_exit, NULL);
+  if (!get_state(env)) return NULL; /* this environment's handle registry + its cleanup hook */
   const napi_property_descriptor d[] = {
       {"compileStore", NULL, js_compile_store, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},
       {"free", NULL, js_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecCreate", NULL, js_codec_create, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"codecFree", NULL, js_codec_free, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"batchFree", NULL, js_batch_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecSetSubjectScopes", NULL, js_codec_set_scopes, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecEvictSubject", NULL, js_codec_evict, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecEcValues", NULL, js_codec_ec_values, NULL, NULL, NULL, napi_enumerable, NULL},

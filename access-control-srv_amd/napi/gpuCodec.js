@@ -139,7 +139,9 @@ class GpuAccessController {
     const blob = addon.compileStore(snapshotStore(policySets), JSON.stringify(this.urns), JSON.stringify(this.cas));
     const tables = addon.compile(blob, this.device);
     const codec = addon.codecCreate(blob);
-    if (this.tables) addon.free(this.tables); // deferred past batches still in flight
+    // the old handles: released once the batches still in flight are done with them
+    if (this.tables) addon.free(this.tables);
+    if (this.codec) addon.codecFree(this.codec);
     this.tables = tables;
     this.codec = codec;
     this.ec = ecDecoder(codec);
@@ -162,8 +164,10 @@ class GpuAccessController {
     return addon.codecEvictSubject(this.codec, key);
   }
 
+  // Releases the GPU tables and the codec (handles are freed explicitly, napi/acs_napi.c).
   close() {
     if (this.tables) addon.free(this.tables);
+    if (this.codec) addon.codecFree(this.codec);
     this.tables = null;
     this.codec = null;
   }
@@ -175,7 +179,7 @@ class GpuAccessController {
   }
 
   // record i of `rec` -> Response, or the error the reference would reject with
-  _response(rec, i, hostReason) {
+  _response(rec, i, hostReason, ec) {
     const flags = rec[i * REC_BYTES + 2];
     if (flags & OF_HOST_REQ) return new HostPathRequired(hostReason || 'request flagged for the host path');
     const aux = rec[i * REC_BYTES + 4] | (rec[i * REC_BYTES + 5] << 8) | (rec[i * REC_BYTES + 6] << 16) |
@@ -191,7 +195,7 @@ class GpuAccessController {
                operation_status: { code: 400, message: 'Access request had no target. Skipping request' } };
     }
     return { decision: DECISIONS[rec[i * REC_BYTES]], obligations: [],
-             evaluation_cacheable: this.ec(rec[i * REC_BYTES + 1]),
+             evaluation_cacheable: ec(rec[i * REC_BYTES + 1]),
              operation_status: { code: 200, message: 'success' } };
   }
 
@@ -199,6 +203,7 @@ class GpuAccessController {
   // request: a Response, or an Error (per request, as the reference's promises would reject).
   async isAllowedBatch(requests) {
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
+    const ec = this.ec; // the codec's table: refresh() may swap this.ec while the batch is in flight
     const r = await addon.decideAsync(this.tables, this.codec, text, this.threads);
     const n = r.records.length / REC_BYTES;
     this.stats.requests += n;
@@ -206,7 +211,7 @@ class GpuAccessController {
     const pending = [];
     let parsed = null;
     for (let i = 0; i < n; ++i) {
-      const v = this._response(r.records, i, r.host[i]);
+      const v = this._response(r.records, i, r.host[i], ec);
       if (v instanceof HostPathRequired) {
         if (parsed === null) parsed = parseRequests(requests);
         pending.push(this._host('isAllowed', parsed[i], v).then((x) => { out[i] = x; }));
@@ -319,6 +324,14 @@ class GpuAccessController {
   async whatIsAllowedBatch(requests) {
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
     const batch = addon.encode(this.codec, text, this.threads);
+    try {
+      return await this._whatIsAllowedEncoded(batch, requests);
+    } finally {
+      addon.batchFree(batch);
+    }
+  }
+
+  async _whatIsAllowedEncoded(batch, requests) {
     const info = addon.batchInfo(batch);
     const w = addon.whatIsAllowed(this.tables, batch);
     const words = addon.wordsPerRequest(this.tables);

@@ -50,6 +50,11 @@ const enc = (x) => (x instanceof Error ? { $error: x.name, reason: x.reason } : 
       const codec = g.addon.codecCreate(blob);
       const b = g.addon.encode(codec, JSON.stringify(c.isAllowed), 2);
       out.push({ info: g.addon.batchInfo(b), ec: JSON.parse(g.addon.codecEcValues(codec)) });
+      // half the handles are freed here, the rest by the environment's cleanup hook at exit
+      if (k % 2) {
+        g.addon.codecFree(codec); // the batch keeps the codec alive until it is freed
+        g.addon.batchFree(b);
+      }
       continue;
     }
     let ctl;

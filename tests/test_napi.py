@@ -31,7 +31,8 @@ def test_addon_loads_with_surface():
     r = subprocess.run([NODE, "-e", js, p], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     info = json.loads(r.stdout.splitlines()[0])
-    assert info["keys"] == sorted(["compileStore", "compile", "free", "codecCreate", "codecSetSubjectScopes",
+    assert info["keys"] == sorted(["compileStore", "compile", "free", "codecCreate", "codecFree", "batchFree",
+                                   "codecSetSubjectScopes",
                                    "codecEvictSubject", "codecEcValues", "encode", "batchInfo", "batchString",
                                    "decideAsync", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
                                    "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
@@ -107,3 +108,65 @@ console.log(JSON.stringify(out));
         assert msg.startswith("RangeError") and f"batch.{k} " in msg, (k, msg)
     assert out[9].startswith("TypeError") and "tables handle" in out[9]
     assert out[10].startswith("TypeError") and "codec handle" in out[10]
+
+
+def test_addon_handle_lifecycle(tmp_path):
+    """Handles are registry slots, not napi externals (napi/acs_napi.c "handles"): a freed
+    handle throws on use and frees twice as a no-op, a batch keeps its freed codec working, a
+    stale id does not reach a reused slot, and handles left live in the main thread and in
+    worker_threads are released by each environment's cleanup hook — every run exits 0
+    (Node 12's teardown use-after-free on externals, which this layout avoids, crashed ~1 in
+    6 loaded runs)."""
+    from acs_mi355x import compiler, store
+    from kat_utils import load_fixture
+    p = _addon()
+    cs = compiler.compile_store(store.populate(load_fixture("simple_policies.yml")), FULL_URNS, DEFAULT_CAS)
+    tmp_path.joinpath("blob.bin").write_bytes(compiler.store_blob(cs))
+    js = r"""
+const { Worker, isMainThread, parentPort, workerData } = require('worker_threads');
+const fs = require('fs');
+const a = require(workerData ? workerData.addon : process.argv[2]);
+const blob = new Uint8Array(fs.readFileSync(workerData ? workerData.blob : process.argv[3]));
+const req = JSON.stringify([{ target: { subjects: [], resources: [], actions: [] }, context: {} }]);
+function round(live) {
+  const out = [];
+  const tryit = (f) => { try { const v = f(); out.push(v === undefined ? 'ok' : v); } catch (e) { out.push(e.constructor.name + ':' + e.message); } };
+  const c = a.codecCreate(blob);
+  const b = a.encode(c, req, 1);
+  a.codecFree(c);
+  tryit(() => a.batchInfo(b).n);            // the batch keeps its codec alive
+  tryit(() => a.codecEcValues(c));          // the freed handle throws
+  tryit(() => a.codecFree(c));              // freeing twice: no-op
+  a.batchFree(b);
+  tryit(() => a.batchInfo(b));
+  const c2 = a.codecCreate(blob);           // may reuse the slot: the stale id must not name it
+  tryit(() => a.codecEcValues(c));
+  tryit(() => typeof a.codecEcValues(c2));
+  for (let k = 0; k < live; ++k) a.encode(a.codecCreate(blob), req, 1);  // left for the cleanup hook
+  return out;
+}
+if (isMainThread) {
+  const res = { main: round(50) };
+  let left = 2;
+  for (let w = 0; w < 2; ++w) {
+    const wk = new Worker(__filename, { workerData: { addon: process.argv[2], blob: process.argv[3] } });
+    wk.on('message', (m) => { res['w' + w] = m; if (--left === 0) console.log(JSON.stringify(res)); });
+  }
+} else {
+  parentPort.postMessage(round(20));
+}
+"""
+    f = tmp_path.joinpath("life.js")
+    f.write_text(js)
+    for _ in range(3):
+        r = subprocess.run([NODE, str(f), p, str(tmp_path.joinpath("blob.bin"))], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+        res = json.loads(r.stdout)
+        for k in ("main", "w0", "w1"):
+            o = res[k]
+            assert o[0] == 1, (k, o)
+            assert o[1] == "Error:codec handle already freed", (k, o)
+            assert o[2] == "ok" and o[3].startswith("TypeError:batchInfo"), (k, o)
+            assert o[4].startswith(("Error:codec handle already freed", "TypeError:expected a codec handle")), (k, o)
+            assert o[5] == "string", (k, o)

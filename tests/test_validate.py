@@ -93,6 +93,8 @@ def test_corrupt_batches_refused(lib):
     offs = b.hdr["arena_off"].astype(np.int64)
     with_slots = next(i for i in range(b.n) if (arena_words[offs[i]] >> 16) & 0xFF)
     ent = (b.res["kind"] & L.K_ENT_LOOSE) != 0
+    safe = ent & ((b.res["pad"] & L.RES_RX_SAFE) != 0)
+    safe_col = int(b.res["col"][tuple(np.argwhere(safe)[0])])
 
     bad = {
         "arena offset": _mut(b, "hdr", lambda a, c: a["arena_off"].__setitem__(7, len(arena_words) - 1)),
@@ -107,6 +109,8 @@ def test_corrupt_batches_refused(lib):
         "regex rows": _mut(b, "rx", lambda a, c: setattr(c, "rx", a[:, :max(_rows(cs) - 1, 0)].copy())),
         "request line": _mut(b, "lines", lambda a, c: a["h"]["arena_off"].__setitem__(7, a["h"]["arena_off"][7] + 1)),
         "request line attribute": _mut(b, "lines", lambda a, c: a["res"]["col"].__setitem__((2, 0), 7)),
+        # a column an RES_RX_SAFE attribute names must hold no throwing / host cell
+        "rx safe": _mut(b, "rx", lambda a, c: a.__setitem__((safe_col, 0), a[safe_col, 0] | 4)),
     }
     assert b.lines is not None
     for what, c in bad.items():
