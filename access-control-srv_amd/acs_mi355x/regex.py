@@ -1,4 +1,4 @@
-"""Entity namespace / RegExp test of the reference, precomputed on the host.
+r"""Entity namespace / RegExp test of the reference, precomputed on the host.
 
 For a rule entity value ``v_r`` and a request entity value ``v_q`` the
 reference (accessController.ts:528-566 and hierarchicalScope.ts:64-101)
@@ -36,7 +36,7 @@ def _split_entity(v: str):
 
 
 def _to_python(pattern: str) -> str:
-    """The safe-subset JS pattern as a Python ``re`` pattern with the same matches: an
+    r"""The safe-subset JS pattern as a Python ``re`` pattern with the same matches: an
     unescaped ``$`` outside a character class asserts end of input (V8, no multiline flag)
     -> ``\Z``.  ``[]`` / ``[^]`` (JS: empty / any-char classes) never reach here, so a
     ``]`` inside a class always closes it, in both engines."""

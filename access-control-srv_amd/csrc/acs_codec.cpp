@@ -323,6 +323,7 @@ struct acs_codec {
   std::unordered_map<std::string, std::shared_ptr<const std::vector<uint32_t>>> ent_rows;   // value key -> [W]
   std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint32_t>>> act_rows;      // pair -> [W]
   std::atomic<uint64_t> hr_hits{0}, hr_misses{0};
+  int force_level = -1;  // tests only (acs_internal_codec_force_level): pin the class key level
 
   // global node index -> (section word offset, bit)
   uint32_t node_word(uint32_t g) const {
@@ -1428,10 +1429,10 @@ void Classes::run() {
   }
   const size_t KEY_ROW_BYTES = size_t(512) << 20, ROLE_ROW_BYTES = size_t(256) << 20;
   const uint32_t MAX_CLASSES = PCOL_ALL;
-  // tests: ACS_CODEC_FORCE_LEVEL=0|1|2 pins the key level (candidates.FORCE_LEVEL)
-  const char* force = getenv("ACS_CODEC_FORCE_LEVEL");
-  const int first_level = force && *force >= '0' && *force <= '2' ? *force - '0' : 0;
-  const int last_level = force && *force >= '0' && *force <= '2' ? first_level + 1 : 3;
+  // tests pin the key level (candidates.FORCE_LEVEL) through acs_internal_codec_force_level
+  const int force = C.force_level;
+  const int first_level = force >= 0 && force <= 2 ? force : 0;
+  const int last_level = force >= 0 && force <= 2 ? first_level + 1 : 3;
   for (int level = first_level; level < last_level; ++level) {
     const bool role_filter = level == 0 && have_roles;
     const bool action_filter = level < 2;
@@ -1787,6 +1788,14 @@ int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, 
   }
   std::unique_lock<std::shared_mutex> lock(c->hr_mu);
   c->hr_subject[std::string(key, key_len)] = F;
+  return 0;
+}
+
+// Test hook (not in include/acs_mi355x.h): pin the candidate-class key level of every later
+// encode (0 entity+roles+action, 1 entity+action, 2 entity; -1 automatic).
+int acs_internal_codec_force_level(acs_codec* c, int level) {
+  if (!c) return -1;
+  c->force_level = level;
   return 0;
 }
 

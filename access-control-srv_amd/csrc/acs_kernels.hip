@@ -45,6 +45,28 @@ int fail(const std::string& msg) {
 
 constexpr int BLOCK = 256;
 
+// A/B switches of experiment builds (acs_mi355x/build.build_variant, `bench.py --lib`), fixed
+// at compile time: the product library defines none of them, so no environment variable can
+// change how a service evaluates.
+#ifndef ACS_AB_NO_CUT          // combining loops and the set walk always run to their end
+#define ACS_AB_NO_CUT 0
+#endif
+#ifndef ACS_AB_NO_USEFUL       // walk the candidate sections instead of the useful ones
+#define ACS_AB_NO_USEFUL 0
+#endif
+#ifndef ACS_AB_NO_VERDICTS     // ignore the per-class target verdicts
+#define ACS_AB_NO_VERDICTS 0
+#endif
+#ifndef ACS_AB_NO_LINES        // read the SoA rows instead of the packed request lines
+#define ACS_AB_NO_LINES 0
+#endif
+#ifndef ACS_AB_BLOB_RULES      // rule records in the blob layout instead of 128-B lines
+#define ACS_AB_BLOB_RULES 0
+#endif
+#ifndef ACS_AB_FILTER_GENERAL  // the general filter form for every batch
+#define ACS_AB_FILTER_GENERAL 0
+#endif
+
 // Sort key that makes a wave share its request class (one candidate row) and action — or,
 // with a role factor, its role key — so table-driven branches are wave-uniform:
 // [bucket | low field].  Class ids come heaviest-first from the host (most candidate
@@ -495,15 +517,11 @@ size_t filter_lds_bytes(const Batch& B) {
   return (size_t)(BLOCK / 64) * lds_wave_words(B) * 4;
 }
 
-// Which filter form a batch's kernels are instantiated with.  ACS_FILTER_GENERAL=1 forces the
-// general form everywhere (A/B runs of the specialisation).
+// Which filter form a batch's kernels are instantiated with (ACS_AB_FILTER_GENERAL: the
+// general form everywhere, A/B builds of the specialisation).
 enum class FilterForm { All, Lds, General };
 FilterForm filter_form(const Batch& B) {
-  static const bool general = [] {
-    const char* e = getenv("ACS_FILTER_GENERAL");
-    return e && *e == '1';
-  }();
-  if (general) return FilterForm::General;
+  if (ACS_AB_FILTER_GENERAL) return FilterForm::General;
   if (!B.cand) return FilterForm::All;
   return B.cand_words <= LDS_FILTER_WORDS && B.cand_wv ? FilterForm::Lds : FilterForm::General;
 }
@@ -622,11 +640,8 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   // record, action and resource reads hit one cache line instead of three (large stores miss
   // L2 on each).  The rres and pair pools follow the lines, and one base (the first line)
   // addresses both: every node's res_off / act_off / subj_off is rebased, inline attributes
-  // point into their line.  ACS_RULE_LINES=0: the blob layout (A/B runs).
-  static const bool rule_lines = [] {
-    const char* e = getenv("ACS_RULE_LINES");
-    return !(e && *e == '0');
-  }();
+  // point into their line.  ACS_AB_BLOB_RULES: the blob layout (A/B builds).
+  const bool rule_lines = !ACS_AB_BLOB_RULES;
   const char* bsrc = (const char*)blob + src;
   std::vector<char> img;
   size_t doff[6];
@@ -749,32 +764,17 @@ static Batch to_batch(const acs_req_batch* b) {
   B.cand_wsu = b->cand_wsu;
   B.cand_wpu = b->cand_wpu;
   B.cand_wv = b->cand_wv;
-  static const bool no_verdicts = [] {  // A/B runs: ACS_NO_VERDICTS=1 matches every target
-    const char* e = getenv("ACS_NO_VERDICTS");
-    return e && *e == '1';
-  }();
-  B.no_verdicts = no_verdicts ? 1u : 0u;
-  static const bool no_useful = [] {  // A/B runs: ACS_NO_USEFUL=1 walks the candidate sections
-    const char* e = getenv("ACS_NO_USEFUL");
-    return e && *e == '1';
-  }();
-  if (no_useful) B.cand_wsu = B.cand_wpu = 0;
-  // A/B runs and the cut-invariance tests: ACS_NO_CUT=1 runs every combining loop to its end
-  const char* no_cut = getenv("ACS_NO_CUT");
-  B.no_cut = no_cut && *no_cut == '1' ? 1u : 0u;
+  B.no_verdicts = ACS_AB_NO_VERDICTS ? 1u : 0u;
+  if (ACS_AB_NO_USEFUL) B.cand_wsu = B.cand_wpu = 0;
+  B.no_cut = ACS_AB_NO_CUT ? 1u : 0u;
   // long rows: the LDS union covers the set and policy sections (rule words: the lanes' rows)
   B.lds_pref = b->cand_wr < LDS_FILTER_WORDS ? b->cand_wr : LDS_FILTER_WORDS;
-  static const int role_major = [] {  // A/B runs: ACS_SORT_ROLE_MAJOR=0/1 overrides the default
-    const char* e = getenv("ACS_SORT_ROLE_MAJOR");
-    return e && *e ? (*e == '1' ? 1 : 0) : ACS_SORT_ROLE_MAJOR_DEFAULT;
-  }();
-  B.role_major = b->role_key && role_major ? 1u : 0u;
+  B.role_major = b->role_key && ACS_SORT_ROLE_MAJOR_DEFAULT ? 1u : 0u;
   B.cand_rows = b->cand ? b->cand_rows : 0u;
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
-  const char* no_lines = getenv("ACS_NO_LINES");  // A/B runs: K1 reads the SoA rows
-  B.lines = no_lines && *no_lines == '1' ? nullptr : (const ReqLine*)b->lines;
+  B.lines = ACS_AB_NO_LINES ? nullptr : (const ReqLine*)b->lines;
   return B;
 }
 

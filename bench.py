@@ -288,8 +288,9 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     maskedProperty push log, its length and the 8-B record.  Parity: a random sample vs
     the Python oracle's whatIsAllowed (rule sets bit-exact, obligations in push order)."""
     from acs_mi355x import compiler, native, results, synth, layout as L
+    from acs_mi355x.config import SERVICE_URNS as FULL_URNS, COMBINING_ALGORITHMS as DEFAULT_CAS
     from acs_mi355x.device import DeviceBatch, what_is_allowed_device, resolve_overflow_device, overflow_logs
-    from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS, Oracle
+    from oracle.acs_oracle import Oracle, FULL_URNS as ORACLE_URNS
     from diff_utils import norm_rq
     import torch.distributed as tdist
     cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
@@ -343,7 +344,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
         parts.update({"B_out": out_b, "bitset_bytes": 4 * words, "obligation_entries_mean": float(obl_n.mean())})
         achieved = per * n / (kern_ms * 1e-3) / 1e9
         # parity sample vs the oracle (bounded: the Python oracle scans 10k rules per request)
-        o = Oracle(FULL_URNS)
+        o = Oracle(ORACLE_URNS)
         o.load(doc)
         rng = np.random.default_rng(4321)
         long_logs = overflow_logs(passes)
@@ -449,8 +450,8 @@ def main():
         assert tdist.get_world_size() == args.gpus
 
     from acs_mi355x import compiler, native, shard, store, synth, layout as L
+    from acs_mi355x.config import SERVICE_URNS as FULL_URNS, COMBINING_ALGORITHMS as DEFAULT_CAS
     from acs_mi355x.device import DeviceBatch, is_allowed_device, decisions_from_tensor
-    from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
 
     kind = args.config
     desc, n_default = WORKLOADS[kind]

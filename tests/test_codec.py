@@ -7,6 +7,7 @@ build of the evaluator core, give bit-identical decision records and reverse que
 which the oracle pins (tests/test_host_core_diff.py).  Also: regex cells vs V8, the HR
 forest cache (inline text, per-subject registration, eviction), multi-threaded encoding.
 """
+import ctypes
 import json
 
 import numpy as np
@@ -18,7 +19,7 @@ from diff_utils import build, gpu_outcome, oracle_outcome, norm_rq
 from kat_utils import load_kats, load_fixture, urns_for
 from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS, Oracle
 from oracle.jsval import OracleUnsupported
-from acs_mi355x import compiler, encoder, results, store, synth, layout as L
+from acs_mi355x import compiler, encoder, native, results, store, synth, layout as L
 from acs_mi355x.codec import NativeCodec
 from acs_mi355x.jsops import MISSING
 
@@ -286,8 +287,9 @@ def test_codec_class_rows_match_python_at_every_level(level, monkeypatch):
             reqs = [sb.decode(i) for i in range(sb.batch.n)]
         monkeypatch.setattr(candidates, "FORCE_LEVEL", names[level])
         pb = encoder.Encoder(cs).encode(reqs)
-        monkeypatch.setenv("ACS_CODEC_FORCE_LEVEL", str(level))
-        nb = NativeCodec(compiler.store_blob(cs)).encode(reqs, threads=2)
+        codec = NativeCodec(compiler.store_blob(cs))
+        native.load().acs_internal_codec_force_level(ctypes.c_void_p(codec.h), level)  # test hook
+        nb = codec.encode(reqs, threads=2)
         assert (pb.cand_wp, pb.cand_wsu, pb.cand_wpu, pb.cand_wr) == (nb.cand_wp, nb.cand_wsu, nb.cand_wpu, nb.cand_wr)
         assert (pb.role_key is None) == (nb.role_key is None)
         assert _request_rows(pb) == _request_rows(nb)

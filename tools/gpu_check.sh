@@ -30,14 +30,11 @@ for s in $STEPS; do
     bench3) step bench_c3 900 python bench.py --config c3 --steps 5 --warmup 1 ;;
     prof3) step rocprof_c3 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 bench.py --config c3 --steps 5 --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 ;;
     quick5) step bench_c5_quick 1200 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-pcie ;;
-    ab) for cfg in ${AB_CONFIGS:-c2 c3}; do
+    ab) # VARIANTS: experiment builds (build.build_variant, compile-time ACS_AB_* flags) vs the product
+        for cfg in ${AB_CONFIGS:-c2 c3}; do
           st=20; [ "$cfg" = c3 ] && st=5
           for rep in $(seq 1 ${AB_REPS:-2}); do
             step "ab_${cfg}_product_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
-            for ev in ${AB_ENVS:-ACS_FILTER_GENERAL}; do  # NAME (=1) or NAME=VALUE
-              case $ev in *=*) kv=$ev ;; *) kv=$ev=1 ;; esac
-              step "ab_${cfg}_${kv}_$rep" 900 env $kv python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0
-            done
             for v in ${VARIANTS:-}; do
               step "ab_${cfg}_${v}_$rep" 900 python bench.py --config $cfg --steps $st --warmup 1 --no-cpu-baseline --no-pcie --e2e-requests 0 \
                 --lib access-control-srv_amd/lib/variants/$v.so
