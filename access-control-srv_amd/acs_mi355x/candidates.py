@@ -473,13 +473,10 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
                                              res[1])
                 verdicts = (pxt, pxf, prt, prf, rxt | (rxf & rrt))
             out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs, verdicts)
-        # requests whose filter sections are identical share one class; its verdicts are
-        # the ones every key of the class agrees on (AND), so verdicts never split a class
-        wv = verdict_offset(cs)
-        ubase, rinv = _unique_rows(out[:, :wv])
-        ver = np.full((len(ubase), W - wv), 0xFFFFFFFF, np.uint32)
-        np.bitwise_and.at(ver, rinv, out[:, wv:])
-        urows = np.concatenate([ubase, ver], axis=1)
+        # keys whose rows (filter + verdict sections) come out identical share one class; a
+        # row depends only on its key, so the native codec caches rows per key across batches
+        # (acs_codec.cpp ClassCache) and the classes of a batch are its distinct rows
+        urows, rinv = _unique_rows(out)
         if len(urows) <= MAX_CLASSES or level == "entity":
             break
     if len(urows) > MAX_CLASSES:  # entity level: at most one class per entity column (< 0xFFFE)

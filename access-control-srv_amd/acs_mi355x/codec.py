@@ -38,6 +38,7 @@ def _lib():
         lib.acs_codec_batch_stats.argtypes = [vp, C.POINTER(C.c_double), C.c_int]
         lib.acs_codec_batch_free.argtypes = [vp]
         lib.acs_codec_batch_free.restype = None
+        lib.acs_codec_batch_expand.argtypes = [vp]
         _DECLARED.add(id(lib))
     return lib
 
@@ -68,7 +69,15 @@ class _Strings:
 
 
 class CodecBatch:
-    """One encoded batch (owns the codec's buffers until close())."""
+    """One encoded batch (owns the codec's buffers until close()).
+
+    The codec's own form is compact (acs_layout.h): request lines + extension records +
+    arena + regex matrix + class rows, which is what ``struct`` describes and what
+    native.Tables ships to the device.  The SoA rows (hdr / res / subj / act / roles, the
+    attribute names of encoder.RequestBatch) are materialised on first access
+    (acs_codec_batch_expand), for the tests and the CPU build of the core."""
+
+    _SOA = ("hdr", "res", "subj", "act", "roles")
 
     def __init__(self, handle, codec):
         self.h = handle
@@ -78,11 +87,6 @@ class CodecBatch:
             raise RuntimeError(last_error())
         self.struct = s
         n = self.n = int(s.n)
-        self.hdr = _view(s.hdr, L.REQ_HDR_DT, n)
-        self.res = _view(s.res, L.REQ_RES_DT, L.QMAX * n).reshape(L.QMAX, n)
-        self.subj = _view(s.subj, L.PAIR_DT, L.SMAX * n).reshape(L.SMAX, n)
-        self.act = _view(s.act, L.PAIR_DT, L.AMAX * n).reshape(L.AMAX, n)
-        self.roles = _view(s.roles, np.uint32, L.RMAX * n).reshape(L.RMAX, n)
         self.arena = _view(s.arena, np.uint32, int(s.arena_words))
         self.rx = _view(s.rx, np.uint8, s.rx_cols * s.rx_rows).reshape(s.rx_cols, s.rx_rows)
         self.rx_rows = int(s.rx_rows)
@@ -94,29 +98,55 @@ class CodecBatch:
         self.role_key = _view(s.role_key, np.uint32, n) if s.role_key else None
         self.role_bits = (_view(s.role_rows_bits, np.uint32, s.role_rows * W).reshape(s.role_rows, W)
                           if s.role_key else None)
-        self.lines = _view(s.lines, L.REQ_LINE_DT, n) if s.lines else None
+        self.lines = _view(s.lines, L.REQ_LINE_DT, n) if s.lines else np.zeros(0, L.REQ_LINE_DT)
+        self.ext = _view(s.ext, np.uint32, int(s.ext_words)) if s.ext else np.zeros(0, np.uint32)
         self.overlay = _Strings(self)
         self.host_reasons = {}
-        for i in np.flatnonzero((self.hdr["flags"] & np.uint32(L.RQ_HOST)) != 0):
+        for i in np.flatnonzero((self.lines["h"]["flags"] & np.uint32(L.RQ_HOST)) != 0):
             r = _lib().acs_codec_batch_reason(handle, int(i))
             self.host_reasons[int(i)] = r.decode() if r else "host path"
+        self._soa = None
+
+    def __getattr__(self, name):
+        if name in CodecBatch._SOA:  # SoA rows on first use
+            return self.expand()[name]
+        raise AttributeError(name)
+
+    def expand(self):
+        """The SoA rows (acs_codec_batch_expand); the struct keeps the compact form."""
+        if self._soa is None:
+            if _lib().acs_codec_batch_expand(self.h) != 0:
+                raise RuntimeError(last_error())
+            s = ReqBatchC()
+            _lib().acs_codec_batch_view(self.h, C.byref(s))
+            n = self.n
+            self._soa = {"hdr": _view(s.hdr, L.REQ_HDR_DT, n),
+                         "res": _view(s.res, L.REQ_RES_DT, L.QMAX * n).reshape(L.QMAX, n),
+                         "subj": _view(s.subj, L.PAIR_DT, L.SMAX * n).reshape(L.SMAX, n),
+                         "act": _view(s.act, L.PAIR_DT, L.AMAX * n).reshape(L.AMAX, n),
+                         "roles": _view(s.roles, np.uint32, L.RMAX * n).reshape(L.RMAX, n)}
+        return self._soa
 
     def stats(self):
-        out = (C.c_double * 6)()
-        _lib().acs_codec_batch_stats(self.h, out, 6)
+        out = (C.c_double * 8)()
+        _lib().acs_codec_batch_stats(self.h, out, 8)
         return {"encode_s": out[0], "regex_s": out[1], "classes_s": out[2], "total_s": out[3],
-                "hr_cache_hits": int(out[4]), "hr_cache_misses": int(out[5])}
+                "hr_cache_hits": int(out[4]), "hr_cache_misses": int(out[5]), "classes_new": int(out[6]),
+                "classes": int(out[7])}
 
     def nbytes(self):
-        return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
+        """Bytes of the compact form (what the host-buffer path uploads)."""
+        return sum(a.nbytes for a in (self.lines, self.ext, self.arena, self.rx)) + \
             (self.cand.nbytes if self.cand is not None else 0) + \
-            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
-            (self.lines.nbytes if self.lines is not None else 0)
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
+
+    compact_nbytes = nbytes
 
     def close(self):
         if self.h:
-            for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx", "cand", "role_key", "role_bits", "lines"):
+            for k in ("arena", "rx", "cand", "role_key", "role_bits", "lines", "ext"):
                 setattr(self, k, None)
+            self._soa = None
             _lib().acs_codec_batch_free(self.h)
             self.h = None
 

@@ -21,11 +21,19 @@ def _to_dev(a: np.ndarray, dev):
 
 
 class DeviceBatch:
-    def __init__(self, batch, device: int = 0):
+    """compact=True (default for a native-codec batch): request lines + extension records +
+    arena + regex matrix + class rows, the product's device form (acs_layout.h); False: the
+    SoA rows as well (the kernels then read them instead of the extension records)."""
+
+    def __init__(self, batch, device: int = 0, compact: bool | None = None):
         self.batch = batch
         self.dev = torch.device("cuda", device)
+        if compact is None:
+            compact = hasattr(batch, "struct")
+        self.compact = compact
+        keys = ("arena", "rx") if compact else ("hdr", "res", "subj", "act", "roles", "arena", "rx")
         self.t = {k: _to_dev(getattr(batch, k) if getattr(batch, k).size else np.zeros(4, np.uint32), self.dev)
-                  for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx")}
+                  for k in keys}
         if batch.cand is not None:
             self.t["cand"] = _to_dev(batch.cand, self.dev)
         if batch.role_key is not None:
@@ -33,8 +41,11 @@ class DeviceBatch:
             self.t["role_bits"] = _to_dev(batch.role_bits, self.dev)
         if getattr(batch, "lines", None) is not None and batch.n:
             self.t["lines"] = _to_dev(batch.lines, self.dev)
+        if compact:
+            ext = getattr(batch, "ext", None)
+            self.t["ext"] = _to_dev(ext if ext is not None and ext.size else np.zeros(4, np.uint32), self.dev)
         self.ptrs = {k: v.data_ptr() for k, v in self.t.items()}
-        self.struct = batch_struct(batch, self.ptrs)
+        self.struct = batch_struct(batch, self.ptrs, compact=compact)
         self.nbytes = sum(v.numel() for v in self.t.values())
 
 

@@ -55,12 +55,21 @@ class RequestBatch:
     role_key: np.ndarray | None = None   # [n] u32 role-factor row per request (large stores)
     role_bits: np.ndarray | None = None  # [role rows, W] u32
     lines: np.ndarray | None = None      # [n] REQ_LINE_DT packed first rows (pack_lines)
+    ext: np.ndarray | None = None        # u32 extension records of the rows past each line (pack_ext)
 
     def nbytes(self):
         return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
             (self.cand.nbytes if self.cand is not None else 0) + \
             (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
-            (self.lines.nbytes if self.lines is not None else 0)
+            (self.lines.nbytes if self.lines is not None else 0) + \
+            (self.ext.nbytes if self.ext is not None else 0)
+
+    def compact_nbytes(self):
+        """Bytes of the compact form (acs_layout.h): lines + extension records + arena + regex
+        matrix + class / role-factor rows — what the host-buffer path uploads."""
+        return self.lines.nbytes + self.ext.nbytes + self.arena.nbytes + self.rx.nbytes + \
+            (self.cand.nbytes if self.cand is not None else 0) + \
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
 
 
 def _attr_list(v, what):
@@ -478,7 +487,37 @@ def pack_lines(b: RequestBatch) -> np.ndarray:
     if b.arena.size:
         ln["ar0"] = np.where(live, b.arena[np.minimum(off, b.arena.size - 1)], 0)
         ln["ar1"] = np.where(live, b.arena[np.minimum(off + 1, b.arena.size - 1)], 0)
+    words = L.ext_geom(h["nres"], h["nsubj"], h["nact"], h["nroles"])[4]
+    start = np.cumsum(words) - words
+    ln["ext"] = np.where(words > 0, start // 4 + 1, 0).astype(np.uint32)
     return ln
+
+
+def pack_ext(b: RequestBatch) -> np.ndarray:
+    """u32 extension records (acs_layout.h ext_geom): per request, in request order, the rows
+    its line cannot hold — resource attributes 4.., subjects 2.., actions 1.., roles 2.. —
+    padded to 4 words; ReqLine.ext = 1 + the record's offset in 16-B units (pack_lines).
+    With the lines, this is the compact batch (no SoA rows) the kernels read.  acs_codec.cpp
+    writes the same records."""
+    h = b.hdr
+    _, g_subj, g_act, g_roles, words = L.ext_geom(h["nres"], h["nsubj"], h["nact"], h["nroles"])
+    start = np.cumsum(words) - words
+    ext = np.zeros(int(words.sum()), np.uint32)
+    nres, nsubj, nact, nroles = (h[f].astype(np.int64) for f in ("nres", "nsubj", "nact", "nroles"))
+    rw = b.res.view(np.uint32).reshape(L.QMAX, b.n, 4)
+    for j in range(L.LINE_RES, L.QMAX):
+        i = np.flatnonzero(nres > j)
+        for k in range(4):
+            ext[start[i] + 4 * (j - L.LINE_RES) + k] = rw[j, i, k]
+    for rows, cnt, base, first in ((b.subj, nsubj, g_subj, L.LINE_SUBJ), (b.act, nact, g_act, L.LINE_ACT)):
+        for j in range(first, rows.shape[0]):
+            i = np.flatnonzero(cnt > j)
+            ext[start[i] + base[i] + 2 * (j - first)] = rows["id"][j, i]
+            ext[start[i] + base[i] + 2 * (j - first) + 1] = rows["value"][j, i]
+    for j in range(L.LINE_ROLES, b.roles.shape[0]):
+        i = np.flatnonzero(nroles > j)
+        ext[start[i] + g_roles[i] + (j - L.LINE_ROLES)] = b.roles[j, i]
+    return ext
 
 
 def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True):
@@ -498,3 +537,4 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr, res)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))
     b.lines = pack_lines(b)
+    b.ext = pack_ext(b)

@@ -52,8 +52,20 @@ REQ_RES_DT = np.dtype([("value", u32), ("hash_sfx", u32), ("col", u16), ("contai
 DECISION_DT = np.dtype([("decision", u8), ("ec", u8), ("flags", u8), ("err", u8), ("aux", u32)])
 # acs_layout.h ReqLine: a request's first rows packed into one 128-B line
 REQ_LINE_DT = np.dtype([("h", REQ_HDR_DT), ("res", REQ_RES_DT, (4,)), ("s0", PAIR_DT), ("s1", PAIR_DT),
-                        ("a0", PAIR_DT), ("r0", u32), ("r1", u32), ("ar0", u32), ("ar1", u32), ("pad", u32, (2,))])
+                        ("a0", PAIR_DT), ("r0", u32), ("r1", u32), ("ar0", u32), ("ar1", u32), ("ext", u32),
+                        ("pad", u32)])
 assert REQ_LINE_DT.itemsize == 128
+
+
+def ext_geom(nres, nsubj, nact, nroles):
+    """acs_layout.h ext_geom (vectorised): word offsets of the res / subj / act / roles parts
+    of each request's extension record and its padded size."""
+    z = np.zeros_like(np.asarray(nres, np.int64))
+    g_subj = 4 * np.maximum(np.asarray(nres, np.int64) - LINE_RES, z)
+    g_act = g_subj + 2 * np.maximum(np.asarray(nsubj, np.int64) - LINE_SUBJ, z)
+    g_roles = g_act + 2 * np.maximum(np.asarray(nact, np.int64) - LINE_ACT, z)
+    end = g_roles + np.maximum(np.asarray(nroles, np.int64) - LINE_ROLES, z)
+    return z, g_subj, g_act, g_roles, (end + 3) & ~3
 
 SIZES = {"NodeRec": NODE_DT.itemsize, "RuleResAttr": RULE_RES_DT.itemsize, "ReqHdr": REQ_HDR_DT.itemsize,
          "ReqRes": REQ_RES_DT.itemsize, "Decision": DECISION_DT.itemsize}

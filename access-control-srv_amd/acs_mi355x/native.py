@@ -25,7 +25,7 @@ class ReqBatchC(C.Structure):
                 ("cand_rows", C.c_uint32), ("cand_wsu", C.c_uint32), ("cand_wpu", C.c_uint32),
                 ("cand_wv", C.c_uint32),
                 ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
-                ("role_rows", C.c_uint32), ("lines", C.c_void_p)]
+                ("role_rows", C.c_uint32), ("lines", C.c_void_p), ("ext", C.c_void_p), ("ext_words", C.c_size_t)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -35,7 +35,7 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_what_is_allowed_obl_device", "acs_store_compile", "acs_blob_free", "acs_codec_create",
            "acs_codec_free", "acs_codec_set_subject_scopes", "acs_codec_evict_subject", "acs_codec_encode",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
-           "acs_codec_batch_stats", "acs_codec_batch_free"]
+           "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand"]
 
 
 class ShardC(C.Structure):
@@ -86,29 +86,41 @@ def last_error(lib=None):
     return (lib or load()).acs_last_error().decode()
 
 
-def batch_struct(b, ptrs=None) -> ReqBatchC:
-    """acs_req_batch over host numpy arrays (ptrs=None) or a dict of device pointers."""
+def batch_struct(b, ptrs=None, compact=False) -> ReqBatchC:
+    """acs_req_batch over host numpy arrays (ptrs=None) or a dict of device pointers.
+    compact: lines + extension records only, no SoA rows (acs_layout.h; the form the host
+    path uploads)."""
     s = ReqBatchC()
     s.n = b.n
+    if compact and (getattr(b, "lines", None) is None or getattr(b, "ext", None) is None):
+        raise ValueError("a compact batch needs its lines and extension records (encoder.pack_ext)")
     if ptrs is None:
-        s.hdr = b.hdr.ctypes.data
-        s.res = b.res.ctypes.data
-        s.subj = b.subj.ctypes.data
-        s.act = b.act.ctypes.data
-        s.roles = b.roles.ctypes.data
-        s.arena = b.arena.ctypes.data if b.arena.size else b.hdr.ctypes.data
+        if not compact:
+            s.hdr = b.hdr.ctypes.data
+            s.res = b.res.ctypes.data
+            s.subj = b.subj.ctypes.data
+            s.act = b.act.ctypes.data
+            s.roles = b.roles.ctypes.data
+        s.arena = b.arena.ctypes.data if b.arena.size else b.lines.ctypes.data if compact else b.hdr.ctypes.data
         s.rx = b.rx.ctypes.data
         s.cand = b.cand.ctypes.data if b.cand is not None else None
         if b.role_key is not None:
             s.role_key, s.role_rows_bits = b.role_key.ctypes.data, b.role_bits.ctypes.data
         if getattr(b, "lines", None) is not None:
             s.lines = b.lines.ctypes.data
+        if compact and b.ext.size:
+            s.ext = b.ext.ctypes.data
     else:
-        for k in ("hdr", "res", "subj", "act", "roles", "arena", "rx"):
-            setattr(s, k, ptrs[k])
+        for k in ("hdr", "res", "subj", "act", "roles"):
+            if not compact:
+                setattr(s, k, ptrs[k])
+        s.arena, s.rx = ptrs["arena"], ptrs["rx"]
         s.cand = ptrs.get("cand")
         s.role_key, s.role_rows_bits = ptrs.get("role_key"), ptrs.get("role_bits")
         s.lines = ptrs.get("lines")
+        s.ext = ptrs.get("ext") if compact else None
+    if compact:
+        s.ext_words = int(b.ext.size)
     s.arena_words = int(b.arena.size)
     s.rx_cols = int(b.rx.shape[0])
     s.rx_rows = int(b.rx.shape[1])
@@ -120,6 +132,15 @@ def batch_struct(b, ptrs=None) -> ReqBatchC:
     if b.role_key is not None:
         s.role_rows = b.role_bits.shape[0]
     return s
+
+
+def host_struct(batch, compact=False) -> ReqBatchC:
+    """The acs_req_batch a host-buffer entry point gets for `batch`: a CodecBatch's own view
+    (compact, plus SoA rows once expanded), else batch_struct over the numpy arrays."""
+    s = getattr(batch, "struct", None)
+    if s is not None:
+        return s
+    return batch_struct(batch, compact=compact)
 
 
 OVERFLOW_CAP = 1024  # first obligation-only pass: log entries per overflowed request and set range
@@ -181,29 +202,31 @@ class Tables:
         except Exception:
             pass
 
-    def is_allowed(self, batch) -> np.ndarray:
+    def is_allowed(self, batch, compact: bool = False) -> np.ndarray:
+        """acs_is_allowed on host buffers: a CodecBatch ships its own (compact) form; a
+        RequestBatch its SoA rows + lines, or with compact=True its lines + extension records."""
         out = np.zeros(batch.n, L.DECISION_DT)
         if batch.n:
-            s = batch_struct(batch)
+            s = host_struct(batch, compact)
             if self.lib.acs_is_allowed(self.h, C.byref(s), out.ctypes.data) != 0:
                 raise RuntimeError(f"acs_is_allowed: {last_error(self.lib)}")
         return out
 
-    def what_is_allowed(self, batch):
+    def what_is_allowed(self, batch, compact: bool = False):
         n = batch.n
         bits = np.zeros((n, self.words), np.uint32)
         obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)
         obl_n = np.zeros(n, np.uint32)
         out = np.zeros(n, L.DECISION_DT)
         if n:
-            s = batch_struct(batch)
+            s = host_struct(batch, compact)
             rc = self.lib.acs_what_is_allowed(self.h, C.byref(s), bits.ctypes.data, obl.ctypes.data,
                                               obl_n.ctypes.data, out.ctypes.data)
             if rc != 0:
                 raise RuntimeError(f"acs_what_is_allowed: {last_error(self.lib)}")
         return bits, obl, obl_n, out
 
-    def what_is_allowed_obl(self, batch, idx, cap: int, chunks: int = OVERFLOW_CHUNKS):
+    def what_is_allowed_obl(self, batch, idx, cap: int, chunks: int = OVERFLOW_CHUNKS, compact: bool = False):
         """Obligation-only pass over requests ``idx`` of ``batch``, the policy sets cut into
         ``chunks`` ranges: (obl [chunks][m][cap][2], obl_n [chunks][m] = pushes per range)."""
         idx = np.ascontiguousarray(idx, np.uint32)
@@ -211,7 +234,7 @@ class Tables:
         obl = np.zeros((chunks, m, cap, 2), np.uint32)
         obl_n = np.zeros((chunks, m), np.uint32)
         if m:
-            s = batch_struct(batch)
+            s = host_struct(batch, compact)
             rc = self.lib.acs_what_is_allowed_obl(self.h, C.byref(s), idx.ctypes.data, m, chunks, cap,
                                                   obl.ctypes.data, obl_n.ctypes.data)
             if rc != 0:

@@ -41,6 +41,9 @@
 #include "acs_layout.h"
 
 extern "C" void acs_internal_set_error(const char* msg);
+// acs_kernels.hip: page-locked (portable) host memory when a device is present, else malloc
+extern "C" void* acs_internal_host_alloc(size_t bytes, int* pinned);
+extern "C" void acs_internal_host_free(void* p, int pinned);
 
 using namespace acs;
 using namespace acs_json;
@@ -185,6 +188,105 @@ uint8_t rx_cell(const RxPattern& R, bool q_nullish, std::string_view q) {
   return bits;
 }
 
+// ------------------------------------------------------------------ string hashing
+// 8 bytes per multiply-xorshift step: the codec hashes ~25 URNs / ids per request, and
+// std::hash's bytewise loop over 40-60 byte URNs was a visible share of encode time.
+inline uint64_t fast_hash(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xC2B2AE3D27D4EB4Full);
+  size_t k = 0;
+  for (; k + 8 <= n; k += 8) {
+    uint64_t w;
+    memcpy(&w, p + k, 8);
+    h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 31;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p + k, n - k);
+  h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+  h ^= h >> 29;
+  return h;
+}
+struct FastHash {
+  size_t operator()(std::string_view s) const { return (size_t)fast_hash(s.data(), s.size()); }
+  size_t operator()(const std::string& s) const { return (size_t)fast_hash(s.data(), s.size()); }
+};
+
+// String -> V, open addressing with the hash stored in the slot: a lookup is one probe run
+// over a flat array (no node chasing, no allocation per insert).  Keys are views: their bytes
+// must outlive the map (the dictionary's bytes, a StrPool, or the request text of a batch).
+template <class V>
+class StrMap {
+ public:
+  struct Slot {
+    uint64_t h;
+    const char* p;
+    uint32_t n;  // 0xFFFFFFFF: empty
+    V v;
+  };
+  explicit StrMap(size_t expect = 16) { rehash(expect); }
+  const Slot* find(uint64_t h, std::string_view s) const {
+    for (size_t x = h & mask_;; x = (x + 1) & mask_) {
+      const Slot& e = t_[x];
+      if (e.n == EMPTY) return nullptr;
+      if (e.h == h && e.n == s.size() && memcmp(e.p, s.data(), s.size()) == 0) return &e;
+    }
+  }
+  const Slot* find(std::string_view s) const { return find(fast_hash(s.data(), s.size()), s); }
+  Slot* insert(uint64_t h, const char* p, uint32_t n, const V& v) {  // the key must be absent
+    if (2 * (size_ + 1) > t_.size()) rehash(size_ + 1);
+    size_t x = h & mask_;
+    while (t_[x].n != EMPTY) x = (x + 1) & mask_;
+    t_[x] = Slot{h, p, n, v};
+    ++size_;
+    return &t_[x];
+  }
+  size_t size() const { return size_; }
+  void clear() {
+    for (Slot& e : t_) e.n = EMPTY;
+    size_ = 0;
+  }
+
+ private:
+  static constexpr uint32_t EMPTY = 0xFFFFFFFFu;
+  void rehash(size_t expect) {
+    size_t cap = 16;
+    while (cap < 2 * expect) cap <<= 1;
+    std::vector<Slot> old(std::move(t_));
+    t_.assign(cap, Slot{0, nullptr, EMPTY, V{}});
+    mask_ = cap - 1;
+    size_ = 0;
+    for (const Slot& e : old)
+      if (e.n != EMPTY) insert(e.h, e.p, e.n, e.v);
+  }
+  std::vector<Slot> t_;
+  size_t mask_ = 0, size_ = 0;
+};
+
+// Stable bump storage for strings (chunks never move).
+class StrPool {
+ public:
+  const char* put(std::string_view s) {
+    if (s.size() > CHUNK) {
+      big_.emplace_back(s);
+      return big_.back().data();
+    }
+    if (chunks_.empty() || used_ + s.size() > CHUNK) {
+      chunks_.emplace_back(new char[CHUNK]);
+      used_ = 0;
+    }
+    char* d = chunks_.back().get() + used_;
+    memcpy(d, s.data(), s.size());
+    used_ += s.size();
+    return d;
+  }
+
+ private:
+  static constexpr size_t CHUNK = size_t(1) << 16;
+  std::vector<std::unique_ptr<char[]>> chunks_;
+  std::deque<std::string> big_;
+  size_t used_ = 0;
+};
+
 // ------------------------------------------------------------------ HR forests
 struct Scalar {
   uint8_t kind = 0;  // 0 undefined, 1 null, 2 string
@@ -196,9 +298,14 @@ struct HrForest {
   bool is_array = false;
   std::vector<Scalar> roots;  // hierarchical_scopes[i].role
   std::vector<Scalar> keys;   // verifyACL effective-role keys, first-seen order
-  std::unordered_map<std::string, uint64_t> masks;  // org id -> root bits | key bits << 32
+  std::deque<std::string> ids;  // storage of the org ids `masks` is keyed by
+  std::unordered_map<std::string_view, uint64_t, FastHash> masks;  // org id -> root bits | key bits << 32
   std::string text;           // inline forests: the exact JSON text they were built from
-  size_t bytes() const { return text.size() + masks.size() * 48 + 256; }
+  size_t bytes() const { return text.size() + masks.size() * 64 + 256; }
+  uint64_t mask(std::string_view id) const {
+    auto it = masks.find(id);
+    return it == masks.end() ? 0 : it->second;
+  }
 };
 
 Scalar scalar_of(const JV* v) {
@@ -261,7 +368,14 @@ void build_forest(HrForest& F, const JV* hrs) {
             val_key[vi] = (int)F.keys.size();
             F.keys.push_back(vals[vi]);
           }
-          if (hid->t == J_STR) F.masks[std::string(hid->s, hid->n)] |= (1ull << r) | (1ull << (32 + val_key[vi]));
+          if (hid->t == J_STR) {
+            auto it = F.masks.find(hid->str());
+            if (it == F.masks.end()) {
+              F.ids.emplace_back(hid->s, hid->n);
+              it = F.masks.emplace(std::string_view(F.ids.back()), 0ull).first;
+            }
+            it->second |= (1ull << r) | (1ull << (32 + val_key[vi]));
+          }
         }
         const JV* ch = get(h, "children");
         if (ch->t == J_ARR) {
@@ -280,6 +394,91 @@ void build_forest(HrForest& F, const JV* hrs) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ host buffers
+namespace {
+// The big arrays of an encoded batch (request lines, extension records, arena, class rows)
+// live in page-locked host memory, so acs_is_allowed's copies to the device run at full PCIe
+// speed without a staging copy.  Pinning is slow, so blocks are recycled across batches.
+struct HostBlock {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int pinned = 0;
+};
+
+class HostPool {
+ public:
+  ~HostPool() {
+    for (HostBlock& b : free_) acs_internal_host_free(b.p, b.pinned);
+  }
+  HostBlock acquire(size_t bytes) {
+    if (bytes < 256) bytes = 256;
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      size_t best = free_.size();
+      for (size_t k = 0; k < free_.size(); ++k)
+        if (free_[k].bytes >= bytes && free_[k].bytes <= 4 * bytes &&
+            (best == free_.size() || free_[k].bytes < free_[best].bytes))
+          best = k;
+      if (best < free_.size()) {
+        HostBlock b = free_[best];
+        free_.erase(free_.begin() + (ptrdiff_t)best);
+        held_ -= b.bytes;
+        return b;
+      }
+    }
+    HostBlock b;
+    b.bytes = ((bytes + bytes / 8) + 4095) & ~size_t(4095);  // headroom for the next, slightly larger batch
+    b.p = acs_internal_host_alloc(b.bytes, &b.pinned);
+    if (!b.p) throw std::bad_alloc();
+    return b;
+  }
+  void release(HostBlock& b) {
+    if (!b.p) return;
+    std::lock_guard<std::mutex> lock(mu_);
+    while (!free_.empty() && held_ + b.bytes > HOLD_MAX) {  // drop the oldest
+      acs_internal_host_free(free_.front().p, free_.front().pinned);
+      held_ -= free_.front().bytes;
+      free_.erase(free_.begin());
+    }
+    free_.push_back(b);
+    held_ += b.bytes;
+    b = HostBlock{};
+  }
+
+ private:
+  static constexpr size_t HOLD_MAX = size_t(8) << 30;
+  std::mutex mu_;
+  std::vector<HostBlock> free_;
+  size_t held_ = 0;
+};
+}  // namespace
+
+namespace {
+// Candidate-class rows, cached per codec (= per store version) across batches: a class row
+// is a pure function of its key (entity value, action, role-association set, key level) and
+// of the image, so a steady stream of requests computes each row once (c3: ~15k keys, each
+// ~200 us of bit work; per-batch recomputation was 0.39 s per 1M requests on 16 threads).
+// Rows are interned by content: keys whose rows coincide share one entry (one class).
+struct ClassEntry {
+  std::vector<uint32_t> row;
+  uint32_t cost = 0;  // candidate nodes in the filter sections (heaviest classes first)
+};
+struct ClassCache {
+  std::shared_mutex mu;
+  std::unordered_map<std::string, std::shared_ptr<const ClassEntry>> by_key;
+  std::unordered_map<uint64_t, std::vector<std::shared_ptr<const ClassEntry>>> by_row;
+  std::unordered_map<std::string, std::shared_ptr<const std::vector<uint32_t>>> role_rows;  // role factor
+  size_t bytes = 0;
+  static constexpr size_t MAX_BYTES = size_t(2) << 30;
+  void clear_locked() {  // batches hold their own references to the rows they use
+    by_key.clear();
+    by_row.clear();
+    role_rows.clear();
+    bytes = 0;
+  }
+};
+}  // namespace
+
 // ------------------------------------------------------------------ the codec (per store image)
 struct acs_codec {
   // store image
@@ -289,7 +488,7 @@ struct acs_codec {
   // dictionary
   std::string sbytes;
   std::vector<uint32_t> soff;
-  std::unordered_map<std::string_view, uint32_t> dict;
+  StrMap<uint32_t> dict;
   uint32_t n_dict = 0;
   uint32_t urn[U_COUNT] = {};
   std::string_view urn_s[U_COUNT];
@@ -316,7 +515,7 @@ struct acs_codec {
   // caches
   std::shared_mutex hr_mu;
   std::unordered_map<uint64_t, std::vector<std::shared_ptr<const HrForest>>> hr_inline;
-  std::unordered_map<std::string, std::shared_ptr<const HrForest>> hr_subject;
+  std::unordered_map<std::string, std::shared_ptr<const HrForest>, FastHash> hr_subject;
   size_t hr_bytes = 0;
   std::mutex col_mu;
   std::unordered_map<std::string, std::shared_ptr<const std::vector<uint8_t>>> rx_cols;     // value key -> cells
@@ -324,6 +523,10 @@ struct acs_codec {
   std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint32_t>>> act_rows;      // pair -> [W]
   std::atomic<uint64_t> hr_hits{0}, hr_misses{0};
   int force_level = -1;  // tests only (acs_internal_codec_force_level): pin the class key level
+  // recycled page-locked blocks of the batches' arrays (shared: a batch may be freed after its
+  // codec, e.g. by a garbage collector that finalises both in either order)
+  std::shared_ptr<HostPool> pool = std::make_shared<HostPool>();
+  ClassCache classes;    // candidate-class rows per key, across batches of this store version
 
   // global node index -> (section word offset, bit)
   uint32_t node_word(uint32_t g) const {
@@ -340,8 +543,8 @@ struct acs_codec {
     return std::string_view(sbytes.data() + soff[id], soff[id + 1] - soff[id]);
   }
   uint32_t lookup(std::string_view s) const {
-    auto it = dict.find(s);
-    return it == dict.end() ? NONE32 : it->second;
+    auto e = dict.find(s);
+    return e ? e->v : NONE32;
   }
 };
 
@@ -414,8 +617,12 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
   if ((size_t)(e - p) < ecn) return err = "truncated codec section", false;
   c->ec_json.assign((const char*)p, ecn);
   c->n_dict = n_str;
-  c->dict.reserve(n_str * 2);
-  for (uint32_t i = ID_EMPTY; i < n_str; ++i) c->dict.emplace(c->string_of(i), i);
+  c->dict = StrMap<uint32_t>(n_str);
+  for (uint32_t i = ID_EMPTY; i < n_str; ++i) {
+    const std::string_view v = c->string_of(i);
+    const uint64_t h = fast_hash(v.data(), v.size());
+    if (!c->dict.find(h, v)) c->dict.insert(h, v.data(), (uint32_t)v.size(), i);  // first id of a string
+  }
   for (int k = 0; k < U_COUNT; ++k) {
     c->urn[k] = urns[k];
     c->urn_s[k] = c->string_of(urns[k]);
@@ -493,27 +700,66 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
 // ------------------------------------------------------------------ encoded batch
 struct ThreadStrings {  // one encoder thread's batch-local strings (ids base + k)
   uint32_t base = 0;
-  std::vector<std::string> strs;
+  StrPool bytes;
+  std::vector<std::string_view> strs;  // views into `bytes`
 };
 
+// An encoded batch in the compact form (acs_layout.h): request lines, extension records,
+// context arena, regex matrix, class rows — the arrays the kernels read, in page-locked host
+// memory.  The SoA rows (hdr / res / subj / act / roles) are only materialised on request
+// (acs_codec_batch_expand: tests, the CPU build of the core).
 struct acs_codec_batch {
-  const acs_codec* codec = nullptr;
+  acs_codec* codec = nullptr;
+  std::shared_ptr<HostPool> pool;
   uint32_t n = 0;
-  std::vector<ReqHdr> hdr;
-  std::vector<ReqRes> res;  // [QMAX][n]
-  std::vector<Pair> subj, act;
-  std::vector<uint32_t> roles, arena;
+  HostBlock lines_b, ext_b, arena_b, cand_b;
+  ReqLine* lines = nullptr;   // [n]
+  uint32_t* ext = nullptr;    // extension records (ReqLine.ext)
+  size_t ext_words = 0;
+  uint32_t* arena = nullptr;  // context arena
+  size_t arena_words = 0;
   std::vector<uint8_t> rx;  // [rx_cols][rx_rows]
   uint32_t rx_cols = 1, rx_rows = 1;
-  std::vector<uint32_t> cand;
+  uint32_t* cand = nullptr;  // [cand_rows][cand_words]
   uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0, cand_wv = 0;
   std::vector<uint32_t> role_key, role_bits;
   uint32_t role_rows = 0;
-  std::vector<ReqLine> lines;  // [n] packed first rows (acs_layout.h ReqLine; encoder.pack_lines)
+  // SoA rows (acs_codec_batch_expand)
+  bool expanded = false;
+  std::vector<ReqHdr> hdr;
+  std::vector<ReqRes> res;  // [QMAX][n]
+  std::vector<Pair> subj, act;
+  std::vector<uint32_t> roles;
   std::vector<const char*> reason;  // per request: why it goes to the host (nullptr: it does not)
-  std::vector<ThreadStrings> strings;
+  std::deque<ThreadStrings> strings;  // (a deque: StrPool does not move)
   double seconds[4] = {};  // parse+encode, regex matrix, candidate classes, total
   uint64_t hr_hits = 0, hr_misses = 0;
+  uint32_t classes_new = 0;  // class keys computed by this batch (the rest came from the cache)
+  ~acs_codec_batch() {
+    if (!pool) return;
+    pool->release(lines_b);
+    pool->release(ext_b);
+    pool->release(arena_b);
+    pool->release(cand_b);
+  }
+  // request rows of the compact form
+  const ReqHdr& h(uint32_t i) const { return lines[i].h; }
+  ReqRes res_at(uint32_t i, uint32_t j) const {
+    if (j < (uint32_t)LINE_RES) return lines[i].res[j];
+    ReqRes q;
+    memcpy(&q, ext + (size_t)(lines[i].ext - 1) * 4 + 4 * (j - LINE_RES), sizeof q);
+    return q;
+  }
+  ReqRes* res_ptr(uint32_t i, uint32_t j) {
+    if (j < (uint32_t)LINE_RES) return &lines[i].res[j];
+    return (ReqRes*)(ext + (size_t)(lines[i].ext - 1) * 4 + 4 * (j - LINE_RES));
+  }
+  uint32_t role_at(uint32_t i, uint32_t k) const {
+    if (k == 0) return lines[i].r0;
+    if (k == 1) return lines[i].r1;
+    const ReqHdr& hd = lines[i].h;
+    return ext[(size_t)(lines[i].ext - 1) * 4 + ext_geom(hd.nres, hd.nsubj, hd.nact, hd.nroles).roles + (k - 2)];
+  }
 };
 
 namespace {
@@ -554,20 +800,39 @@ class Encoder {
   }
   void encode(uint32_t i, const char* p, const char* e);
   std::vector<uint32_t> arena;  // this thread's context arena words
+  std::vector<uint32_t> ext;    // this thread's extension records
   uint64_t hits = 0, misses = 0;
 
  private:
+  // String -> id: the store dictionary, else this thread's batch-local strings.  A
+  // direct-mapped cache of recent strings (hash, canonical bytes, id) in front of both: a
+  // request interns ~25 strings, most of them URNs every request repeats, and a miss in the
+  // node-based maps costs a few cache misses (~500 cycles measured) where a hit here costs
+  // one hash and one compare against bytes that are already in cache.
   uint32_t intern_sv(std::string_view s) {
-    const uint32_t id = C.lookup(s);
-    if (id != NONE32) return id;
-    auto it = local_.find(s);
-    if (it != local_.end()) return it->second;
-    if (strs_->strs.size() >= (1u << LOCAL_BITS)) unsup("too many batch-local strings");
-    strs_->strs.emplace_back(s);
-    const uint32_t v = strs_->base + (uint32_t)strs_->strs.size() - 1;
-    pool_.emplace_back(s);  // stable storage for the key view
-    local_.emplace(std::string_view(pool_.back()), v);
-    return v;
+    const uint64_t h = fast_hash(s.data(), s.size());
+    RecentString& x = recent_[h & (RECENT - 1)];
+    if (x.h == h && x.n == s.size() && memcmp(x.p, s.data(), s.size()) == 0) return x.id;
+    uint32_t id;
+    const char* canon;
+    if (auto d = C.dict.find(h, s)) {
+      id = d->v;
+      canon = d->p;
+    } else if (auto l = local_.find(h, s)) {
+      id = l->v;
+      canon = l->p;
+    } else {
+      if (strs_->strs.size() >= (1u << LOCAL_BITS)) unsup("too many batch-local strings");
+      canon = strs_->bytes.put(s);
+      strs_->strs.emplace_back(canon, s.size());
+      id = strs_->base + (uint32_t)strs_->strs.size() - 1;
+      local_.insert(h, canon, (uint32_t)s.size(), id);
+    }
+    x.h = h;
+    x.p = canon;
+    x.n = (uint32_t)s.size();
+    x.id = id;
+    return id;
   }
   uint32_t intern(const JV* v) {
     if (v->t == J_UNDEF) return ID_UNDEF;
@@ -622,11 +887,13 @@ class Encoder {
     return &kUndef;
   }
   uint32_t column(const JV* v, uint32_t i) {  // i: request index * QMAX + attribute index
-    std::string key = v->t == J_UNDEF ? std::string("m") : v->t == J_NULL ? std::string("n") : "s" + std::string(v->str());
-    auto it = cols_.find(key);
-    if (it != cols_.end()) {
-      return it->second;
+    uint32_t* memo = v->t == J_UNDEF ? &col_undef_ : v->t == J_NULL ? &col_null_ : nullptr;
+    if (memo && *memo != NONE32) return *memo;
+    if (!memo) {
+      auto it = cols_.find(v->str());
+      if (it != cols_.end()) return it->second;
     }
+    std::string key = v->t == J_UNDEF ? std::string("m") : v->t == J_NULL ? std::string("n") : "s" + std::string(v->str());
     std::lock_guard<std::mutex> lock(SH.mu);
     auto g = SH.col_index.find(key);
     uint32_t c;
@@ -639,11 +906,12 @@ class Encoder {
       c = g->second;
       if (i < SH.cols[c].first) SH.cols[c].first = i;
     }
-    cols_.emplace(std::move(key), c);
+    if (memo) *memo = c;
+    else cols_.emplace(v->str(), c);
     return c;
   }
   std::shared_ptr<const HrForest> inline_forest(const JV* raw);
-  std::shared_ptr<const HrForest> subject_forest(const JV* key);
+  const HrForest* subject_forest(const JV* key);
   void encode_one(uint32_t i, const JV* req);
 
   acs_codec& C;
@@ -652,9 +920,28 @@ class Encoder {
   ThreadStrings* strs_;
   Arena ar_, ar2_;
   Parser parser_;
-  std::unordered_map<std::string_view, uint32_t> local_;
-  std::deque<std::string> pool_;
-  std::unordered_map<std::string, uint32_t> cols_;
+  StrMap<uint32_t> local_{4096};  // batch-local strings of this thread (bytes: strs_->bytes)
+  struct RecentString {
+    uint64_t h = 0;
+    const char* p = nullptr;  // the dictionary's or pool_'s bytes (stable for the batch)
+    uint32_t n = 0xFFFFFFFFu, id = 0;
+  };
+  static constexpr size_t RECENT = 4096;
+  std::unique_ptr<RecentString[]> recent_{new RecentString[RECENT]};
+  // this thread's view of batch-wide state, keyed by views into the request text (valid for
+  // the batch): entity value -> regex-matrix column, "$hrs" subject key -> forest (the
+  // shared_ptrs in `held_` keep the forests alive), so the shared maps and their locks are
+  // touched once per distinct value per thread, not once per request
+  std::unordered_map<std::string_view, uint32_t, FastHash> cols_;
+  uint32_t col_undef_ = NONE32, col_null_ = NONE32;
+  std::unordered_map<std::string_view, const HrForest*, FastHash> forests_;
+  std::vector<std::shared_ptr<const HrForest>> held_;
+  // per-request scratch (cleared, never freed)
+  std::vector<const JV*> slot_objs_;
+  std::vector<std::pair<uint32_t, uint8_t>> keys_a_, keys_b_;
+  std::vector<uint32_t> rolese_, grants_, roots_, hr_keys_, w_;
+  std::vector<std::pair<uint32_t, std::vector<const JV*>>> tse_;
+  size_t tse_n_ = 0;
 };
 
 std::shared_ptr<const HrForest> Encoder::inline_forest(const JV* raw) {
@@ -686,38 +973,60 @@ std::shared_ptr<const HrForest> Encoder::inline_forest(const JV* raw) {
   return F;
 }
 
-std::shared_ptr<const HrForest> Encoder::subject_forest(const JV* key) {
+const HrForest* Encoder::subject_forest(const JV* key) {
   if (key->t != J_STR) unsup("$hrs subject key is not a string");
-  std::shared_lock<std::shared_mutex> lock(C.hr_mu);
-  auto it = C.hr_subject.find(std::string(key->str()));
-  if (it == C.hr_subject.end()) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+  auto mine = forests_.find(key->str());
+  if (mine != forests_.end()) {
+    if (!mine->second) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+    ++hits;
+    return mine->second;
+  }
+  std::shared_ptr<const HrForest> f;
+  {
+    std::shared_lock<std::shared_mutex> lock(C.hr_mu);
+    auto it = C.hr_subject.find(std::string(key->str()));
+    if (it != C.hr_subject.end()) f = it->second;
+  }
+  forests_.emplace(key->str(), f.get());
+  if (!f) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+  held_.push_back(f);
   ++hits;
-  return it->second;
+  return f.get();
 }
+
+#if defined(ACS_CODEC_TIMING)  // profiling harness only: cycles in parse / encode_one
+std::atomic<uint64_t> g_cyc_parse{0}, g_cyc_encode{0};
+#endif
 
 void Encoder::encode(uint32_t i, const char* p, const char* e) {
   ar_.reset();
+#if defined(ACS_CODEC_TIMING)
+  const uint64_t c0 = __builtin_ia32_rdtsc();
+#endif
   const JV* req = parser_.parse(p, e, "hierarchical_scopes");
+#if defined(ACS_CODEC_TIMING)
+  const uint64_t c1 = __builtin_ia32_rdtsc();
+  g_cyc_parse += c1 - c0;
+  struct Tail {
+    uint64_t t;
+    ~Tail() { g_cyc_encode += __builtin_ia32_rdtsc() - t; }
+  } tail{c1};
+#endif
   try {
     encode_one(i, req);
   } catch (const Unsup& u) {
-    ReqHdr& h = B.hdr[i];
-    h = ReqHdr{};
-    h.flags = RQ_HOST;
-    h.arena_off = (uint32_t)arena.size();
+    ReqLine& L = B.lines[i];
+    L = ReqLine{};
+    L.h.flags = RQ_HOST;
+    L.h.arena_off = (uint32_t)arena.size();  // (thread-local until the batch is assembled)
     arena.push_back(0);
     arena.push_back(0);
-    for (int j = 0; j < QMAX; ++j) B.res[(size_t)j * B.n + i] = ReqRes{};
-    for (int j = 0; j < SMAX; ++j) B.subj[(size_t)j * B.n + i] = Pair{};
-    for (int j = 0; j < AMAX; ++j) B.act[(size_t)j * B.n + i] = Pair{};
-    for (int j = 0; j < RMAX; ++j) B.roles[(size_t)j * B.n + i] = 0;
     B.reason[i] = u.why;
   }
 }
 
 // encoder.py Encoder._encode_one, restated.
 void Encoder::encode_one(uint32_t i, const JV* req) {
-  const uint32_t n = B.n;
   uint32_t flags = 0;
   if (req->t != J_OBJ) unsup("request is not an object");
   const JV* target = get(req, "target");
@@ -748,9 +1057,13 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   const JV* ras = truthy(ras_v) ? dict_list(ras_v, n_ras) : nullptr;
   if (n_ras > (uint32_t)RMAX) unsup("too many role associations");
   const JV* hrs = get(subj, "hierarchical_scopes");
-  std::shared_ptr<const HrForest> forest;
+  const HrForest* forest = nullptr;
+  std::shared_ptr<const HrForest> inl;  // an inline forest (the codec's cache may drop it)
   if (hrs->t == J_RAW) {
-    if (hrs->raw == J_ARR) forest = inline_forest(hrs);
+    if (hrs->raw == J_ARR) {
+      inl = inline_forest(hrs);
+      forest = inl.get();
+    }
     else if (hrs->raw != J_NULL) unsup("hierarchical_scopes is not an array");
   } else if (hrs->t == J_UNDEF) {
     const JV* key = get(subj, "$hrs");  // the subject's registered forest (createHRScope's cache)
@@ -807,7 +1120,8 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
       n_ctx = cr->n;
     }
   }
-  std::vector<const JV*> slot_objs;
+  std::vector<const JV*>& slot_objs = slot_objs_;
+  slot_objs.clear();
   auto slot_of = [&](const JV* obj) -> uint8_t {
     if (!truthy(obj)) return NONE8;
     for (size_t k = 0; k < slot_objs.size(); ++k)
@@ -822,7 +1136,10 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     return find_by(ctx_res, n_ctx, false, v);
   };
   ReqRes rows[QMAX] = {};
-  std::vector<std::pair<uint32_t, uint8_t>> keys_a, keys_b;  // first slot per interned value
+  auto& keys_a = keys_a_;  // first slot per interned value
+  auto& keys_b = keys_b_;
+  keys_a.clear();
+  keys_b.clear();
   for (uint32_t j = 0; j < nr; ++j) {
     const JV* v = get(&resources[j], "value");
     const uint8_t kind = kinds[j];
@@ -872,7 +1189,10 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
 
   // ---- role associations -> roles, (role, se) pairs, (role, se, inst) grants
   uint32_t roles[RMAX] = {};
-  std::vector<uint32_t> rolese, grants;
+  std::vector<uint32_t>& rolese = rolese_;
+  std::vector<uint32_t>& grants = grants_;
+  rolese.clear();
+  grants.clear();
   for (uint32_t k = 0; k < n_ras; ++k) {
     const JV* ra = &ras[k];
     const JV* role = get(ra, "role");
@@ -906,15 +1226,17 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   if (grants.size() / 3 > 255 || rolese.size() / 2 > 255) unsup("too many role scoping grants");
 
   // ---- hierarchical_scopes: roots and effective-role keys from the cached forest
-  std::vector<uint32_t> roots, hr_keys;
+  std::vector<uint32_t>& roots = roots_;
+  std::vector<uint32_t>& hr_keys = hr_keys_;
+  roots.clear();
+  hr_keys.clear();
   if (forest && forest->is_array) {
     for (const Scalar& r : forest->roots) roots.push_back(intern(r));
     for (const Scalar& k : forest->keys) hr_keys.push_back(intern(k));
   }
   auto masks_of = [&](const JV* v) -> uint64_t {
     if (!forest || v->t != J_STR) return 0;
-    auto it = forest->masks.find(std::string(v->str()));
-    return it == forest->masks.end() ? 0 : it->second;
+    return forest->mask(v->str());
   };
 
   // ---- verifyACL request loop (verifyACL.ts:37-88)
@@ -978,7 +1300,8 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   }
 
   // ---- arena
-  std::vector<uint32_t> w = {0, 0};
+  std::vector<uint32_t>& w = w_;
+  w.assign(2, 0u);
   w.insert(w.end(), grants.begin(), grants.end());
   w.insert(w.end(), rolese.begin(), rolese.end());
   w.insert(w.end(), roots.begin(), roots.end());
@@ -1044,14 +1367,35 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   Pair sp[SMAX] = {}, ap[AMAX] = {};
   for (uint32_t k = 0; k < ns; ++k) sp[k] = Pair{intern(get(&subjects[k], "id")), intern(get(&subjects[k], "value"))};
   for (uint32_t k = 0; k < na; ++k) ap[k] = Pair{intern(get(&actions[k], "id")), intern(get(&actions[k], "value"))};
-  // commit (nothing above wrote the batch: an Unsupported leaves no partial request)
+  // commit (nothing above wrote the batch: an Unsupported leaves no partial request): the
+  // request line, then the rows past it as this thread's extension record (offsets are
+  // thread-local until the batch is assembled)
   h.arena_off = (uint32_t)arena.size();
   arena.insert(arena.end(), w.begin(), w.end());
-  B.hdr[i] = h;
-  for (int j = 0; j < QMAX; ++j) B.res[(size_t)j * n + i] = rows[j];
-  for (int j = 0; j < SMAX; ++j) B.subj[(size_t)j * n + i] = sp[j];
-  for (int j = 0; j < AMAX; ++j) B.act[(size_t)j * n + i] = ap[j];
-  for (int j = 0; j < RMAX; ++j) B.roles[(size_t)j * n + i] = roles[j];
+  ReqLine& L = B.lines[i];
+  L = ReqLine{};
+  L.h = h;
+  for (uint32_t j = 0; j < nr && j < (uint32_t)LINE_RES; ++j) L.res[j] = rows[j];
+  L.s0 = sp[0];
+  L.s1 = sp[1];
+  L.a0 = ap[0];
+  L.r0 = roles[0];
+  L.r1 = roles[1];
+  if (!(flags & RQ_NO_TARGET)) {
+    L.ar0 = w[0];
+    L.ar1 = w[1];
+  }
+  const ExtGeom g = ext_geom(nr, ns, na, n_ras);
+  if (g.words) {
+    L.ext = 1u + (uint32_t)(ext.size() / 4);
+    const size_t x = ext.size();
+    ext.resize(x + g.words, 0u);
+    uint32_t* d = ext.data() + x;
+    for (uint32_t j = LINE_RES; j < nr; ++j) memcpy(d + 4 * (j - LINE_RES), &rows[j], 16);
+    for (uint32_t j = LINE_SUBJ; j < ns; ++j) memcpy(d + g.subj + 2 * (j - LINE_SUBJ), &sp[j], 8);
+    for (uint32_t j = LINE_ACT; j < na; ++j) memcpy(d + g.act + 2 * (j - LINE_ACT), &ap[j], 8);
+    for (uint32_t j = LINE_ROLES; j < n_ras; ++j) d[g.roles + (j - LINE_ROLES)] = roles[j];
+  }
 }
 
 }  // namespace
@@ -1268,6 +1612,24 @@ struct Classes {
     }
   }
 
+  // policies whose target reads a throwing (or host) RegExp cell of column c
+  // (candidates.throw_policies); nullptr when none
+  std::unique_ptr<Row> throw_row(uint32_t c) const {
+    if (col_keys[c].empty()) return nullptr;
+    std::unique_ptr<Row> out;
+    const uint8_t* cells = B.rx.data() + (size_t)c * B.rx_rows;
+    for (uint32_t r = 0; r < (uint32_t)C.rx_pat.size(); ++r) {
+      if (!(cells[r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST))) continue;
+      for (uint32_t k = C.row_ptr[r]; k < C.row_ptr[r + 1]; ++k) {
+        const uint32_t g = C.row_nodes[k];
+        if (g < C.S || g >= C.S + C.P) continue;
+        if (!out) out = std::make_unique<Row>(C.wp ? C.wp : 1, 0u);
+        (*out)[(g - C.S) >> 5] |= 1u << ((g - C.S) & 31);
+      }
+    }
+    return out;
+  }
+
   Row assemble(const Row& r, const Row* thr) const {
     Row out(C.W2, 0u);
     std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
@@ -1309,6 +1671,67 @@ struct Classes {
 
 uint64_t row_hash(const uint32_t* r, size_t n) { return hash_bytes((const char*)r, n * 4); }
 
+// Run f(t, lo, hi) over [0, n) cut into `threads` contiguous ranges (t = 0 on this thread).
+template <class F>
+void parallel_ranges(int threads, size_t n, F f) {
+  int T = threads < 1 ? 1 : threads;
+  if ((size_t)T > n / 4096 + 1) T = (int)(n / 4096 + 1);
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+  f(0, 0, n / T);
+  for (auto& th : pool) th.join();
+}
+
+// Open-addressing u64 -> u32 map (linear probing; key ~0 is reserved).
+class U64Map {
+ public:
+  explicit U64Map(size_t expect = 64) {
+    size_t cap = 64;
+    while (cap < 2 * expect) cap <<= 1;
+    k_.assign(cap, ~0ull);
+    v_.resize(cap);
+  }
+  // the value for key (inserting `fresh` if absent); *inserted: whether it was absent
+  uint32_t get_or_put(uint64_t key, uint32_t fresh, bool* inserted) {
+    if (2 * (n_ + 1) > k_.size()) grow();
+    size_t m = k_.size() - 1, x = (size_t)(mix(key) & m);
+    for (;; x = (x + 1) & m) {
+      if (k_[x] == key) {
+        *inserted = false;
+        return v_[x];
+      }
+      if (k_[x] == ~0ull) {
+        k_[x] = key;
+        v_[x] = fresh;
+        ++n_;
+        *inserted = true;
+        return fresh;
+      }
+    }
+  }
+
+ private:
+  static uint64_t mix(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    h ^= h >> 33;
+    return h;
+  }
+  void grow() {
+    std::vector<uint64_t> k(std::move(k_));
+    std::vector<uint32_t> v(std::move(v_));
+    k_.assign(k.size() * 2, ~0ull);
+    v_.resize(k.size() * 2);
+    n_ = 0;
+    bool ins;
+    for (size_t x = 0; x < k.size(); ++x)
+      if (k[x] != ~0ull) get_or_put(k[x], v[x], &ins);
+  }
+  std::vector<uint64_t> k_;
+  std::vector<uint32_t> v_;
+  size_t n_ = 0;
+};
+
 void Classes::run() {
   const uint32_t n = B.n, W = C.W2;  // output rows: [S | P | useful S | useful P | R]
   const uint32_t ncols = B.rx_cols;
@@ -1318,62 +1741,60 @@ void Classes::run() {
   B.cand_wpu = 2 * C.ws + C.wp;
   B.cand_wr = 2 * C.ws + 2 * C.wp;
   B.cand_wv = C.WV;
-  // primary column per request (candidates.primary_columns)
+  // per request: primary column (candidates.primary_columns), action key, sorted role rows
+  const bool have_roles = !C.role_ids.empty();
+  const int RW = RMAX;
   std::vector<uint32_t> pcol(n, ncols);
   std::vector<uint8_t> active(n, 0);
-  bool any_active = false;
-  for (uint32_t i = 0; i < n; ++i) {
-    bool seen = false;
-    for (uint32_t j = 0; j < B.hdr[i].nres; ++j) {
-      const ReqRes& q = B.res[(size_t)j * n + i];
-      if (!(q.kind & K_ENT)) continue;
-      if (!seen) pcol[i] = q.col;
-      else if (pcol[i] != q.col) pcol[i] = PCOL_ALL;
-      seen = true;
+  std::vector<int32_t> rs((size_t)n * RW, -1);
+  std::vector<uint8_t> nrs(n, 0);
+  std::atomic<bool> any_active{false};
+  parallel_ranges(threads, n, [&](int, size_t lo, size_t hi) {
+    bool any = false;
+    for (uint32_t i = (uint32_t)lo; i < hi; ++i) {
+      const ReqHdr& hd = B.h(i);
+      bool seen = false;
+      for (uint32_t j = 0; j < hd.nres; ++j) {
+        const ReqRes q = B.res_at(i, j);
+        if (!(q.kind & K_ENT)) continue;
+        if (!seen) pcol[i] = q.col;
+        else if (pcol[i] != q.col) pcol[i] = PCOL_ALL;
+        seen = true;
+      }
+      active[i] = pcol[i] != PCOL_ALL && !(hd.flags & (RQ_HOST | RQ_NO_TARGET));
+      any = any || active[i];
+      if (!have_roles || !(hd.flags & RQ_RA_TRUTHY)) continue;
+      int32_t* r = &rs[(size_t)i * RW];
+      int m = 0;
+      for (uint32_t k = 0; k < hd.nroles; ++k) {
+        const uint32_t v = B.role_at(i, k);
+        auto it = std::lower_bound(C.role_ids.begin(), C.role_ids.end(), v);
+        if (it != C.role_ids.end() && *it == v) r[m++] = (int32_t)(it - C.role_ids.begin());
+      }
+      std::sort(r, r + m);
+      m = (int)(std::unique(r, r + m) - r);
+      nrs[i] = (uint8_t)m;
     }
-    active[i] = pcol[i] != PCOL_ALL && !(B.hdr[i].flags & (RQ_HOST | RQ_NO_TARGET));
-    any_active = any_active || active[i];
-  }
-  std::vector<uint32_t> cls(n, PCOL_ALL);
-  auto finish = [&]() {
-    for (uint32_t i = 0; i < n; ++i) B.hdr[i].flags = (B.hdr[i].flags & 0xFFFFu) | cls[i] << RQ_PCOL_SHIFT;
+    if (any) any_active = true;
+  });
+  auto finish = [&](const std::vector<uint32_t>& cls) {
+    parallel_ranges(threads, n, [&](int, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        uint32_t& f = B.lines[i].h.flags;
+        f = (f & 0xFFFFu) | cls[i] << RQ_PCOL_SHIFT;
+      }
+    });
+  };
+  auto set_rows = [&](size_t rows) {
+    B.cand_b = C.pool->acquire(rows * W * sizeof(uint32_t));
+    B.cand = (uint32_t*)B.cand_b.p;
+    B.cand_rows = (uint32_t)rows;
   };
   if (!any_active) {
-    B.cand.assign(W ? W : 1, 0u);
-    B.cand_rows = 1;
-    finish();
+    set_rows(1);
+    memset(B.cand, 0, (size_t)W * 4);
+    finish(std::vector<uint32_t>(n, PCOL_ALL));
     return;
-  }
-  // entity rows per column (+ the no-entity column: always candidates)
-  std::vector<std::shared_ptr<const Row>> ent(ncols + 1);
-  {
-    const std::vector<std::string>& keys = col_keys;
-    for (uint32_t c = 0; c < ncols; ++c) {
-      if (keys[c].empty()) {
-        ent[c] = std::make_shared<Row>(C.always_bits);
-        continue;
-      }
-      std::vector<uint8_t> cells(B.rx.begin() + (size_t)c * B.rx_rows,
-                                 B.rx.begin() + (size_t)c * B.rx_rows + C.rx_pat.size());
-      ent[c] = entity_row(keys[c], cells);
-    }
-    ent[ncols] = std::make_shared<Row>(C.always_bits);
-  }
-  build_resv(ncols);
-  // per column: policies whose target reads a throwing (or host) RegExp cell (candidates.throw_policies)
-  std::vector<std::unique_ptr<Row>> thr(ncols + 1);
-  for (uint32_t c = 0; c < ncols; ++c) {
-    if (col_keys[c].empty()) continue;
-    const uint8_t* cells = B.rx.data() + (size_t)c * B.rx_rows;
-    for (uint32_t r = 0; r < (uint32_t)C.rx_pat.size(); ++r) {
-      if (!(cells[r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST))) continue;
-      for (uint32_t k = C.row_ptr[r]; k < C.row_ptr[r + 1]; ++k) {
-        const uint32_t g = C.row_nodes[k];
-        if (g < C.S || g >= C.S + C.P) continue;
-        if (!thr[c]) thr[c] = std::make_unique<Row>(C.wp ? C.wp : 1, 0u);
-        (*thr[c])[(g - C.S) >> 5] |= 1u << ((g - C.S) & 31);
-      }
-    }
   }
   // action keys (candidates.action_keys): 0 none, 1 several / unfiltered, 2 + k a single pair
   std::vector<uint32_t> ak(n, 0);
@@ -1381,7 +1802,7 @@ void Classes::run() {
   {
     std::unordered_map<uint64_t, uint32_t> cnt;
     for (uint32_t i = 0; i < n; ++i)
-      if (B.hdr[i].nact == 1) ++cnt[(uint64_t)B.act[i].id << 32 | B.act[i].value];
+      if (B.h(i).nact == 1) ++cnt[(uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value];
     std::vector<std::pair<uint64_t, uint32_t>> v(cnt.begin(), cnt.end());
     std::sort(v.begin(), v.end());
     if (v.size() > 62) {
@@ -1395,133 +1816,238 @@ void Classes::run() {
       pairs_k.push_back(v[k].first);
     }
     for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t na = B.hdr[i].nact;
+      const uint32_t na = B.h(i).nact;
       if (na == 0) ak[i] = 0;
       else if (na > 1) ak[i] = 1;
       else {
-        auto it = idx.find((uint64_t)B.act[i].id << 32 | B.act[i].value);
+        auto it = idx.find((uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value);
         ak[i] = it == idx.end() ? 1 : 2 + it->second;
       }
     }
   }
-  std::vector<std::shared_ptr<const Row>> arow(2 + pairs_k.size());
-  arow[0] = std::make_shared<Row>(no_action_row());
-  arow[1] = std::make_shared<Row>(valid);
-  for (size_t k = 0; k < pairs_k.size(); ++k)
-    arow[2 + k] = action_row((uint32_t)(pairs_k[k] >> 32), (uint32_t)pairs_k[k]);
-  // role sets: sorted distinct role rows some target requires
-  const int RW = RMAX;
-  std::vector<int32_t> rs((size_t)n * RW, -1);
-  std::vector<uint8_t> nrs(n, 0);
-  const bool have_roles = !C.role_ids.empty();
-  for (uint32_t i = 0; i < n && have_roles; ++i) {
-    if (!(B.hdr[i].flags & RQ_RA_TRUTHY)) continue;
-    int32_t* r = &rs[(size_t)i * RW];
-    int m = 0;
-    for (uint32_t k = 0; k < B.hdr[i].nroles; ++k) {
-      const uint32_t v = B.roles[(size_t)k * n + i];
-      auto it = std::lower_bound(C.role_ids.begin(), C.role_ids.end(), v);
-      if (it != C.role_ids.end() && *it == v) r[m++] = (int32_t)(it - C.role_ids.begin());
+  // per-batch inputs of a row computation, built only when some key misses the cache
+  std::vector<std::shared_ptr<const Row>> ent, arow;
+  std::vector<std::unique_ptr<Row>> thr;
+  bool prepared = false;
+  auto prepare = [&] {
+    if (prepared) return;
+    prepared = true;
+    ent.assign(ncols + 1, nullptr);
+    for (uint32_t c = 0; c < ncols; ++c) {
+      if (col_keys[c].empty()) {
+        ent[c] = std::make_shared<Row>(C.always_bits);
+        continue;
+      }
+      std::vector<uint8_t> cells(B.rx.begin() + (size_t)c * B.rx_rows,
+                                 B.rx.begin() + (size_t)c * B.rx_rows + C.rx_pat.size());
+      ent[c] = entity_row(col_keys[c], cells);
     }
-    std::sort(r, r + m);
-    m = (int)(std::unique(r, r + m) - r);
-    nrs[i] = (uint8_t)m;
-  }
+    ent[ncols] = std::make_shared<Row>(C.always_bits);
+    build_resv(ncols);
+    thr.clear();
+    thr.resize(ncols + 1);
+    for (uint32_t c = 0; c < ncols; ++c) thr[c] = throw_row(c);
+    arow.assign(2 + pairs_k.size(), nullptr);
+    arow[0] = std::make_shared<Row>(no_action_row());
+    arow[1] = std::make_shared<Row>(valid);
+    for (size_t k = 0; k < pairs_k.size(); ++k)
+      arow[2 + k] = action_row((uint32_t)(pairs_k[k] >> 32), (uint32_t)pairs_k[k]);
+  };
+  // the column part of a cache key: the entity value (a padding column: never a key)
+  auto col_key = [&](uint32_t c) -> std::string {
+    if (c >= ncols) return std::string("\x01", 1);  // no entity attribute
+    return "\x02" + col_keys[c];
+  };
   const size_t KEY_ROW_BYTES = size_t(512) << 20, ROLE_ROW_BYTES = size_t(256) << 20;
   const uint32_t MAX_CLASSES = PCOL_ALL;
   // tests pin the key level (candidates.FORCE_LEVEL) through acs_internal_codec_force_level
   const int force = C.force_level;
   const int first_level = force >= 0 && force <= 2 ? force : 0;
   const int last_level = force >= 0 && force <= 2 ? first_level + 1 : 3;
+  const bool packable = C.role_ids.size() < 512;
   for (int level = first_level; level < last_level; ++level) {
     const bool role_filter = level == 0 && have_roles;
     const bool action_filter = level < 2;
-    // distinct keys of the active requests
-    std::unordered_map<std::string, uint32_t> kidx;
-    std::vector<uint32_t> key_of(n, NONE32), key_first;
-    std::string kb;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (!active[i]) continue;
-      kb.assign((const char*)&pcol[i], 4);
+    // distinct keys of the active requests, numbered in order of first appearance: 64-bit
+    // packed keys deduplicated per thread range, then merged in range order
+    bool pack_ok = packable;
+    if (role_filter)
+      for (uint32_t i = 0; i < n && pack_ok; ++i) pack_ok = nrs[i] <= 4;
+    auto kv = [&](uint32_t i) -> uint64_t {  // pcol 16 | ak 6 | nrs 3 | 4 x 9-bit role rows
+      uint64_t k = (uint64_t)(pcol[i] & 0xFFFF) << 48 | (uint64_t)(action_filter ? ak[i] : 0) << 42;
+      if (role_filter) {
+        k |= (uint64_t)nrs[i] << 36;
+        for (int j = 0; j < nrs[i]; ++j) k |= (uint64_t)rs[(size_t)i * RW + j] << (9 * j);
+      }
+      return k;
+    };
+    auto ks = [&](uint32_t i) -> std::string {
+      std::string kb((const char*)&pcol[i], 4);
       if (action_filter) kb.append((const char*)&ak[i], 4);
       if (role_filter) kb.append((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
-      auto it = kidx.find(kb);
-      if (it == kidx.end()) {
-        it = kidx.emplace(kb, (uint32_t)key_first.size()).first;
-        key_first.push_back(i);
+      return kb;
+    };
+    std::vector<uint32_t> key_of(n, NONE32), key_first;
+    {
+      int T = threads < 1 ? 1 : threads;
+      if ((size_t)T > n / 4096 + 1) T = (int)(n / 4096 + 1);
+      std::vector<std::vector<uint32_t>> firsts(T);
+      parallel_ranges(T, n, [&](int t, size_t lo, size_t hi) {
+        if (pack_ok) {
+          U64Map m(1024);
+          bool ins;
+          for (uint32_t i = (uint32_t)lo; i < hi; ++i) {
+            if (!active[i]) continue;
+            key_of[i] = m.get_or_put(kv(i), (uint32_t)firsts[t].size(), &ins);
+            if (ins) firsts[t].push_back(i);
+          }
+        } else {
+          std::unordered_map<std::string, uint32_t> m;
+          for (uint32_t i = (uint32_t)lo; i < hi; ++i) {
+            if (!active[i]) continue;
+            auto it = m.emplace(ks(i), (uint32_t)firsts[t].size());
+            if (it.second) firsts[t].push_back(i);
+            key_of[i] = it.first->second;
+          }
+        }
+      });
+      // merge: thread-local key index -> global key index
+      std::vector<std::vector<uint32_t>> remap(T);
+      U64Map gm(4096);
+      std::unordered_map<std::string, uint32_t> gs;
+      for (int t = 0; t < T; ++t) {
+        remap[t].resize(firsts[t].size());
+        for (size_t k = 0; k < firsts[t].size(); ++k) {
+          const uint32_t i = firsts[t][k];
+          uint32_t g;
+          bool ins;
+          if (pack_ok) {
+            g = gm.get_or_put(kv(i), (uint32_t)key_first.size(), &ins);
+          } else {
+            auto it = gs.emplace(ks(i), (uint32_t)key_first.size());
+            g = it.first->second;
+            ins = it.second;
+          }
+          if (ins) key_first.push_back(i);
+          remap[t][k] = g;
+        }
       }
-      key_of[i] = it->second;
+      parallel_ranges(T, n, [&](int t, size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i)
+          if (key_of[i] != NONE32) key_of[i] = remap[t][key_of[i]];
+      });
     }
     const size_t nk = key_first.size();
     if (level < 2 && nk * W * 4 > KEY_ROW_BYTES) continue;
-    std::vector<Row> rows(nk);
-    std::atomic<size_t> next{0};
-    auto work = [&] {
-      for (;;) {
-        const size_t k = next.fetch_add(1);
-        if (k >= nk) return;
-        const uint32_t i = key_first[k];
-        rows[k] = assemble(class_row(pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter, ent,
-                                     arow),
-                           pcol[i] < ncols ? thr[pcol[i]].get() : nullptr);
-        verdicts(rows[k], pcol[i], action_filter ? ak[i] : 1u, &rs[(size_t)i * RW], nrs[i], role_filter,
-                 action_filter, arow);
-      }
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads && (size_t)t < nk; ++t) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-    // rows with identical filter sections share a class; its verdict sections are the AND
-    // over its keys (candidates.classes); heaviest (most candidate nodes) first
-    const uint32_t WV = C.WV;
-    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
-    std::vector<uint32_t> urow_of_key(nk), urows;
+    // cache lookup by (level, entity value, action, roles); compute the misses in parallel
+    std::vector<std::string> gkey(nk);
+    std::vector<std::shared_ptr<const ClassEntry>> entry(nk);
+    std::vector<uint32_t> miss;
     for (size_t k = 0; k < nk; ++k) {
-      const uint64_t h = row_hash(rows[k].data(), WV);
-      auto& bucket = by_hash[h];
-      uint32_t u = NONE32;
-      for (uint32_t x : bucket)
-        if (std::equal(rows[urows[x]].begin(), rows[urows[x]].begin() + WV, rows[k].begin())) {
-          u = x;
-          break;
-        }
-      if (u == NONE32) {
-        u = (uint32_t)urows.size();
-        urows.push_back((uint32_t)k);
-        bucket.push_back(u);
-      } else {
-        Row& acc = rows[urows[u]];
-        for (uint32_t w = WV; w < W; ++w) acc[w] &= rows[k][w];
+      const uint32_t i = key_first[k];
+      std::string g(1, (char)('0' + level));
+      g += col_key(pcol[i]);
+      g.push_back('\0');
+      if (action_filter) {
+        const uint32_t a = ak[i];
+        if (a < 2) g.push_back((char)a);
+        else g.append((const char*)&pairs_k[a - 2], 8);
       }
-      urow_of_key[k] = u;
+      g.push_back('|');
+      if (role_filter) g.append((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      gkey[k] = std::move(g);
     }
-    if (urows.size() > MAX_CLASSES && level < 2) continue;
-    if (urows.size() > MAX_CLASSES) {
+    {
+      std::shared_lock<std::shared_mutex> lock(C.classes.mu);
+      for (size_t k = 0; k < nk; ++k) {
+        auto it = C.classes.by_key.find(gkey[k]);
+        if (it != C.classes.by_key.end()) entry[k] = it->second;
+        else miss.push_back((uint32_t)k);
+      }
+    }
+    B.classes_new += (uint32_t)miss.size();
+    if (!miss.empty()) {
+      prepare();
+      std::vector<Row> rows(miss.size());
+      std::atomic<size_t> next{0};
+      auto work = [&] {
+        for (;;) {
+          const size_t m = next.fetch_add(1);
+          if (m >= miss.size()) return;
+          const uint32_t i = key_first[miss[m]];
+          const uint32_t a = action_filter ? ak[i] : 1u;
+          rows[m] = assemble(class_row(pcol[i], a, &rs[(size_t)i * RW], nrs[i], role_filter, ent, arow),
+                             pcol[i] < ncols ? thr[pcol[i]].get() : nullptr);
+          verdicts(rows[m], pcol[i], a, &rs[(size_t)i * RW], nrs[i], role_filter, action_filter, arow);
+        }
+      };
+      std::vector<std::thread> pool;
+      for (int t = 1; t < threads && (size_t)t < miss.size(); ++t) pool.emplace_back(work);
+      work();
+      for (auto& th : pool) th.join();
+      std::unique_lock<std::shared_mutex> lock(C.classes.mu);
+      ClassCache& K = C.classes;
+      if (K.bytes > ClassCache::MAX_BYTES) K.clear_locked();  // this batch holds its own references
+      for (size_t m = 0; m < miss.size(); ++m) {
+        const uint64_t h = row_hash(rows[m].data(), W);
+        std::shared_ptr<const ClassEntry> e;
+        for (const auto& x : K.by_row[h])
+          if (x->row == rows[m]) {
+            e = x;
+            break;
+          }
+        if (!e) {
+          auto ne = std::make_shared<ClassEntry>();
+          uint32_t c = 0;
+          for (uint32_t w = 0; w < C.WV; ++w) c += (uint32_t)__builtin_popcount(rows[m][w]);  // filter sections
+          ne->cost = c;
+          ne->row = std::move(rows[m]);
+          K.bytes += (size_t)W * 4 + 64;
+          K.by_row[h].push_back(ne);
+          e = ne;
+        }
+        K.by_key.emplace(gkey[miss[m]], e);
+        K.bytes += gkey[miss[m]].size() + 64;
+        entry[miss[m]] = e;
+      }
+    }
+    // the batch's classes: its distinct rows, heaviest first (candidate nodes in the filter
+    // sections; ties in order of first appearance), so the longest waves are dispatched first
+    std::unordered_map<const ClassEntry*, uint32_t> uidx;
+    std::vector<const ClassEntry*> uent;
+    std::vector<uint32_t> cls_of_key(nk);
+    for (size_t k = 0; k < nk; ++k) {
+      auto it = uidx.emplace(entry[k].get(), (uint32_t)uent.size());
+      if (it.second) uent.push_back(entry[k].get());
+      cls_of_key[k] = it.first->second;
+    }
+    if (uent.size() > MAX_CLASSES && level < 2) continue;
+    if (uent.size() > MAX_CLASSES) {
       acs_internal_set_error("acs_codec_encode: too many request classes");
       throw Unsup{"too many request classes"};
     }
-    std::vector<uint32_t> cost(urows.size()), order(urows.size()), rank(urows.size());
-    for (size_t u = 0; u < urows.size(); ++u) {
-      uint32_t c = 0;
-      for (uint32_t w = 0; w < WV; ++w) c += (uint32_t)__builtin_popcount(rows[urows[u]][w]);  // filter sections
-      cost[u] = c;
-      order[u] = (uint32_t)u;
-    }
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    std::vector<uint32_t> order(uent.size()), rank(uent.size());
+    for (size_t u = 0; u < uent.size(); ++u) order[u] = (uint32_t)u;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return uent[a]->cost > uent[b]->cost; });
     for (size_t k = 0; k < order.size(); ++k) rank[order[k]] = (uint32_t)k;
-    B.cand.assign((size_t)urows.size() * W, 0u);
-    for (size_t u = 0; u < urows.size(); ++u)
-      std::copy(rows[urows[u]].begin(), rows[urows[u]].end(), B.cand.begin() + (size_t)rank[u] * W);
-    B.cand_rows = (uint32_t)urows.size();
+    set_rows(uent.size());
+    parallel_ranges(threads, uent.size() * (size_t)W / 1024 + 1, [&](int, size_t lo, size_t hi) {
+      // rows split by bytes: chunk c covers classes [c * U / C, (c + 1) * U / C)
+      const size_t U = uent.size(), Cn = uent.size() * (size_t)W / 1024 + 1;
+      for (size_t u = U * lo / Cn; u < U * hi / Cn; ++u)
+        memcpy(B.cand + (size_t)rank[u] * W, uent[u]->row.data(), (size_t)W * 4);
+    });
+    std::vector<uint32_t> cls(n, PCOL_ALL);
     for (uint32_t i = 0; i < n; ++i)
-      if (active[i]) cls[i] = rank[urow_of_key[key_of[i]]];
-    finish();
+      if (active[i]) cls[i] = rank[cls_of_key[key_of[i]]];
+    finish(cls);
     if (role_filter || !have_roles) return;
-    // role factor (candidates._role_factor): one row per distinct role set of the active requests
+    // role factor (candidates._role_factor): one row per distinct role set of the active
+    // requests, cached by (role set, the batch's may-throw policies)
     std::unordered_map<std::string, uint32_t> sidx;
     std::vector<uint32_t> set_first;
     std::vector<uint32_t> rkey(n, 0xFFFFu);
+    std::string kb;
     for (uint32_t i = 0; i < n; ++i) {
       if (!active[i]) continue;
       kb.assign((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
@@ -1533,23 +2059,52 @@ void Classes::run() {
       rkey[i] = it->second;
     }
     if (set_first.empty() || set_first.size() * W * 4 > ROLE_ROW_BYTES || set_first.size() >= 0xFFFF) return;
-    B.role_bits.assign(set_first.size() * W, 0u);
     // the role side's useful sections keep every policy that may throw for some column
     Row thr_any(C.wp ? C.wp : 1, 0u);
-    for (const auto& t : thr)
-      if (t)
-        for (uint32_t w = 0; w < thr_any.size(); ++w) thr_any[w] |= (*t)[w];
-    for (size_t k = 0; k < set_first.size(); ++k) {
+    for (uint32_t c = 0; c < ncols; ++c) {
+      std::unique_ptr<Row> t = prepared ? nullptr : throw_row(c);
+      const Row* tr = prepared ? thr[c].get() : t.get();
+      if (tr)
+        for (uint32_t w = 0; w < thr_any.size(); ++w) thr_any[w] |= (*tr)[w];
+    }
+    const std::string thr_key((const char*)thr_any.data(), thr_any.size() * 4);
+    B.role_bits.assign(set_first.size() * W, 0u);
+    std::vector<std::shared_ptr<const std::vector<uint32_t>>> rrow(set_first.size());
+    std::vector<uint32_t> rmiss;
+    std::vector<std::string> rkeys(set_first.size());
+    {
+      std::shared_lock<std::shared_mutex> lock(C.classes.mu);
+      for (size_t k = 0; k < set_first.size(); ++k) {
+        const uint32_t i = set_first[k];
+        rkeys[k].assign((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+        rkeys[k] += '|';
+        rkeys[k] += thr_key;
+        auto it = C.classes.role_rows.find(rkeys[k]);
+        if (it != C.classes.role_rows.end()) rrow[k] = it->second;
+        else rmiss.push_back((uint32_t)k);
+      }
+    }
+    B.classes_new += (uint32_t)rmiss.size();
+    for (uint32_t k : rmiss) {
       const uint32_t i = set_first[k];
       Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
       for (uint32_t w = 0; w < C.W; ++w) r[w] &= valid[w];
       sets_need_policies(r);
       Row o = assemble(r, &thr_any);
       for (uint32_t q = 0; q < C.P; ++q)
-        for (int k = 0; k < 4; ++k) o[C.WV + k * C.wp + (q >> 5)] |= 1u << (q & 31);
+        for (int s = 0; s < 4; ++s) o[C.WV + s * C.wp + (q >> 5)] |= 1u << (q & 31);
       for (uint32_t x = 0; x < C.R; ++x) o[C.WV + 4 * C.wp + (x >> 5)] |= 1u << (x & 31);
-      std::copy(o.begin(), o.end(), B.role_bits.begin() + k * W);
+      rrow[k] = std::make_shared<const std::vector<uint32_t>>(std::move(o));
     }
+    if (!rmiss.empty()) {
+      std::unique_lock<std::shared_mutex> lock(C.classes.mu);
+      for (uint32_t k : rmiss) {
+        C.classes.role_rows.emplace(rkeys[k], rrow[k]);
+        C.classes.bytes += (size_t)W * 4 + rkeys[k].size() + 64;
+      }
+    }
+    for (size_t k = 0; k < set_first.size(); ++k)
+      std::copy(rrow[k]->begin(), rrow[k]->end(), B.role_bits.begin() + k * W);
     B.role_key = std::move(rkey);
     B.role_rows = (uint32_t)set_first.size();
     return;
@@ -1595,6 +2150,83 @@ std::vector<std::pair<const char*, const char*>> array_items(const char* p, cons
   return out;
 }
 
+inline bool is_ws(char c) { return c == ' ' || c == '\n' || c == '\r' || c == '\t'; }
+
+// The top-level array's items, delimited on `threads` threads: thread t starts at a guessed
+// item boundary (the first "},{" past t/T of the text) and delimits items until it reaches
+// thread t+1's start; the guesses are accepted only if every thread stops exactly where the
+// next one started (a guess inside a string or a nested list would not line up), otherwise
+// the text is delimited again on one thread.  Serial delimiting alone ran at ~2 GB/s, half
+// of the codec's time at 16 threads (1.2 GB of JSON per 1M c3 requests).
+std::vector<std::pair<const char*, const char*>> split_items(const char* p, const char* e, int threads) {
+  const char* b = p;
+  while (b < e && is_ws(*b)) ++b;
+  const char* z = e;
+  while (z > b && is_ws(z[-1])) --z;
+  const size_t len = (size_t)(z - b);
+  int T = threads < 1 ? 1 : threads;
+  if (len < (size_t(4) << 20) || T == 1 || *b != '[' || z[-1] != ']') return array_items(p, e);
+  const char* body = b + 1;
+  const char* end = z - 1;  // the closing ']'
+  std::vector<const char*> g(T + 1);
+  g[0] = body;
+  g[T] = end;
+  for (int t = 1; t < T; ++t) {
+    const char* from = body + (size_t)(end - body) * t / T;
+    if (from < g[t - 1]) from = g[t - 1];
+    const char* hit = end;
+    for (const char* q = from; q + 2 < end; ++q) {
+      q = (const char*)memchr(q, '}', (size_t)(end - q));
+      if (!q || q + 2 >= end) break;
+      if (q[1] == ',' && q[2] == '{') {
+        hit = q + 2;
+        break;
+      }
+    }
+    g[t] = hit;
+  }
+  std::vector<std::vector<std::pair<const char*, const char*>>> part(T);
+  std::vector<const char*> stop(T, nullptr);
+  std::vector<char> ok(T, 1);
+  auto work = [&](int t) {
+    try {
+      const char* q = g[t];
+      for (;;) {
+        while (q < end && is_ws(*q)) ++q;
+        if (q >= end || q >= g[t + 1]) break;
+        const char* s = q;
+        q = skip_value(q, end);
+        part[t].push_back({s, q});
+        while (q < end && is_ws(*q)) ++q;
+        if (q < end) {
+          if (*q != ',') throw ParseError{"x"};
+          ++q;
+          while (q < end && is_ws(*q)) ++q;
+          if (q >= end) throw ParseError{"x"};  // a trailing comma
+        }
+      }
+      stop[t] = q;
+    } catch (const ParseError&) {
+      ok[t] = 0;
+    }
+  };
+  {
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+  }
+  bool good = true;
+  for (int t = 0; t < T && good; ++t) good = ok[t] && stop[t] == (t + 1 < T ? (g[t + 1] < end ? g[t + 1] : end) : end);
+  if (!good) return array_items(p, e);
+  std::vector<std::pair<const char*, const char*>> out;
+  size_t total = 0;
+  for (auto& x : part) total += x.size();
+  out.reserve(total);
+  for (auto& x : part) out.insert(out.end(), x.begin(), x.end());
+  return out;
+}
+
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1603,30 +2235,34 @@ acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int th
   const double t0 = now_s();
   auto B = std::make_unique<acs_codec_batch>();
   B->codec = c;
-  const auto items = array_items(json, json + len);
+  B->pool = c->pool;
+  int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  const auto items = split_items(json, json + len, T);
   const uint32_t n = (uint32_t)items.size();
   if (items.size() > 0xFFFFFFFull) throw ParseError{"requests: batch too large"};
   B->n = n;
-  B->hdr.assign(n, ReqHdr{});
-  B->res.assign((size_t)QMAX * n, ReqRes{});
-  B->subj.assign((size_t)SMAX * n, Pair{});
-  B->act.assign((size_t)AMAX * n, Pair{});
-  B->roles.assign((size_t)RMAX * n, 0u);
+  B->lines_b = c->pool->acquire((size_t)n * sizeof(ReqLine));
+  B->lines = (ReqLine*)B->lines_b.p;
   B->reason.assign(n, nullptr);
-  int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
   if ((uint32_t)T > n / 64 + 1) T = (int)(n / 64 + 1);
   B->strings.resize(T);
   for (int t = 0; t < T; ++t) B->strings[t].base = c->n_dict + ((uint32_t)t << LOCAL_BITS);
   Shared sh;
-  std::vector<std::vector<uint32_t>> arenas(T);
+  std::vector<std::vector<uint32_t>> arenas(T), exts(T);
   std::vector<std::string> errs(T);
   std::atomic<uint64_t> hits{0}, misses{0};
+  auto range = [&](int t, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)((uint64_t)n * t / T);
+    hi = (uint32_t)((uint64_t)n * (t + 1) / T);
+  };
   auto work = [&](int t) {
-    const uint32_t lo = (uint32_t)((uint64_t)n * t / T), hi = (uint32_t)((uint64_t)n * (t + 1) / T);
+    uint32_t lo, hi;
+    range(t, lo, hi);
     try {
       Encoder enc(*c, *B, sh, (uint32_t)t);
       for (uint32_t i = lo; i < hi; ++i) enc.encode(i, items[i].first, items[i].second);
       arenas[t] = std::move(enc.arena);
+      exts[t] = std::move(enc.ext);
       hits += enc.hits;
       misses += enc.misses;
     } catch (const ParseError& e) {
@@ -1645,27 +2281,12 @@ acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int th
     if (!e.empty()) throw std::runtime_error(e);
   B->hr_hits = hits;
   B->hr_misses = misses;
-  // one arena: shift each thread's offsets
-  size_t total = 0;
-  for (auto& a : arenas) total += a.size();
-  B->arena.reserve(total);
-  for (int t = 0; t < T; ++t) {
-    const uint32_t base = (uint32_t)B->arena.size();
-    const uint32_t lo = (uint32_t)((uint64_t)n * t / T), hi = (uint32_t)((uint64_t)n * (t + 1) / T);
-    for (uint32_t i = lo; i < hi; ++i) B->hdr[i].arena_off += base;
-    B->arena.insert(B->arena.end(), arenas[t].begin(), arenas[t].end());
-  }
+  const double t1 = now_s();
   // regex-matrix columns in first-use order (request, attribute), as encoder.py numbers them
   std::vector<uint32_t> order(sh.cols.size()), remap(sh.cols.size());
   for (size_t k = 0; k < order.size(); ++k) order[k] = (uint32_t)k;
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sh.cols[a].first < sh.cols[b].first; });
   for (size_t k = 0; k < order.size(); ++k) remap[order[k]] = (uint32_t)k;
-  for (uint32_t j = 0; j < (uint32_t)QMAX; ++j)
-    for (uint32_t i = 0; i < n; ++i) {
-      ReqRes& q = B->res[(size_t)j * n + i];
-      if ((q.kind & K_ENT_LOOSE) && j < B->hdr[i].nres) q.col = (uint16_t)remap[q.col];
-    }
-  const double t1 = now_s();
   // regex matrix: one cached column of cells per distinct entity value
   const uint32_t n_rx = (uint32_t)c->rx_pat.size();
   B->rx_cols = order.empty() ? 1u : (uint32_t)order.size();
@@ -1705,44 +2326,82 @@ acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int th
   }
   // RES_RX_SAFE on every entity attribute whose column holds no throwing / host cell (K1 may
   // then cut a combining loop short once its result is final: encoder.mark_rx_safe)
+  std::vector<uint8_t> safe(B->rx_cols, 1);
+  for (uint32_t k = 0; k < B->rx_cols; ++k)
+    for (uint32_t r = 0; r < B->rx_rows; ++r)
+      if (B->rx[(size_t)k * B->rx_rows + r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST)) safe[k] = 0;
+  // one arena and one extension-record array: each thread copies its part into place and
+  // rebases its requests' offsets; column ids in first-use order; RES_RX_SAFE
+  std::vector<size_t> abase(T + 1, 0), ebase(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    abase[t + 1] = abase[t] + arenas[t].size();
+    ebase[t + 1] = ebase[t] + exts[t].size();
+  }
+  if (abase[T] > 0xFFFFFFFFull || ebase[T] / 4 >= 0xFFFFFFFFull) throw std::runtime_error("batch arena too large");
+  B->arena_b = c->pool->acquire(abase[T] * 4);
+  B->arena = (uint32_t*)B->arena_b.p;
+  B->arena_words = abase[T];
+  B->ext_b = c->pool->acquire(ebase[T] * 4);
+  B->ext = (uint32_t*)B->ext_b.p;
+  B->ext_words = ebase[T];
   {
-    std::vector<uint8_t> safe(B->rx_cols, 1);
-    for (uint32_t k = 0; k < B->rx_cols; ++k)
-      for (uint32_t r = 0; r < B->rx_rows; ++r)
-        if (B->rx[(size_t)k * B->rx_rows + r] & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST)) safe[k] = 0;
-    for (uint32_t j = 0; j < (uint32_t)QMAX; ++j)
-      for (uint32_t i = 0; i < n; ++i) {
-        ReqRes& q = B->res[(size_t)j * n + i];
-        if ((q.kind & K_ENT_LOOSE) && j < B->hdr[i].nres && q.col < B->rx_cols && safe[q.col]) q.pad |= RES_RX_SAFE;
+    std::vector<std::thread> pool;
+    auto fix = [&](int t) {
+      if (!arenas[t].empty()) memcpy(B->arena + abase[t], arenas[t].data(), arenas[t].size() * 4);
+      if (!exts[t].empty()) memcpy(B->ext + ebase[t], exts[t].data(), exts[t].size() * 4);
+      uint32_t lo, hi;
+      range(t, lo, hi);
+      for (uint32_t i = lo; i < hi; ++i) {
+        ReqLine& L = B->lines[i];
+        L.h.arena_off += (uint32_t)abase[t];
+        if (L.ext) L.ext += (uint32_t)(ebase[t] / 4);
+        for (uint32_t j = 0; j < L.h.nres; ++j) {
+          ReqRes* q = B->res_ptr(i, j);
+          if (!(q->kind & K_ENT_LOOSE)) continue;
+          q->col = (uint16_t)remap[q->col];
+          if (q->col < B->rx_cols && safe[q->col]) q->pad |= RES_RX_SAFE;
+        }
       }
+    };
+    for (int t = 1; t < T; ++t) pool.emplace_back(fix, t);
+    fix(0);
+    for (auto& th : pool) th.join();
   }
   const double t2 = now_s();
   Classes cl(*c, *B, T);
   cl.col_keys = keys;  // padding column: ''
   cl.run();
-  // packed first rows, after the class ids went into the headers (encoder.pack_lines)
-  B->lines.assign(n, ReqLine{});
-  for (uint32_t i = 0; i < n; ++i) {
-    ReqLine& L = B->lines[i];
-    const ReqHdr& hd = B->hdr[i];
-    L.h = hd;
-    for (uint32_t j = 0; j < hd.nres && j < (uint32_t)LINE_RES; ++j) L.res[j] = B->res[(size_t)j * n + i];
-    if (hd.nsubj > 0) L.s0 = B->subj[i];
-    if (hd.nsubj > 1) L.s1 = B->subj[(size_t)n + i];
-    if (hd.nact > 0) L.a0 = B->act[i];
-    if (hd.nroles > 0) L.r0 = B->roles[i];
-    if (hd.nroles > 1) L.r1 = B->roles[(size_t)n + i];
-    if (!(hd.flags & (RQ_HOST | RQ_NO_TARGET))) {
-      L.ar0 = B->arena[hd.arena_off];
-      L.ar1 = B->arena[hd.arena_off + 1];
-    }
-  }
   const double t3 = now_s();
   B->seconds[0] = t1 - t0;
   B->seconds[1] = t2 - t1;
   B->seconds[2] = t3 - t2;
   B->seconds[3] = t3 - t0;
   return B.release();
+}
+
+// SoA rows of a compact batch (acs_codec_batch_expand): tests and the CPU build of the core.
+void expand_soa(acs_codec_batch& B) {
+  if (B.expanded) return;
+  const uint32_t n = B.n;
+  B.hdr.assign(n, ReqHdr{});
+  B.res.assign((size_t)QMAX * n, ReqRes{});
+  B.subj.assign((size_t)SMAX * n, Pair{});
+  B.act.assign((size_t)AMAX * n, Pair{});
+  B.roles.assign((size_t)RMAX * n, 0u);
+  for (uint32_t i = 0; i < n; ++i) {
+    const ReqLine& L = B.lines[i];
+    const ReqHdr& h = L.h;
+    B.hdr[i] = h;
+    for (uint32_t j = 0; j < h.nres; ++j) B.res[(size_t)j * n + i] = B.res_at(i, j);
+    const ExtGeom g = ext_geom(h.nres, h.nsubj, h.nact, h.nroles);
+    const uint32_t* x = L.ext ? B.ext + (size_t)(L.ext - 1) * 4 : nullptr;
+    for (uint32_t j = 0; j < h.nsubj; ++j)
+      B.subj[(size_t)j * n + i] = j == 0 ? L.s0 : j == 1 ? L.s1 : Pair{x[g.subj + 2 * (j - 2)], x[g.subj + 2 * (j - 2) + 1]};
+    for (uint32_t j = 0; j < h.nact; ++j)
+      B.act[(size_t)j * n + i] = j == 0 ? L.a0 : Pair{x[g.act + 2 * (j - 1)], x[g.act + 2 * (j - 1) + 1]};
+    for (uint32_t j = 0; j < h.nroles; ++j) B.roles[(size_t)j * n + i] = B.role_at(i, j);
+  }
+  B.expanded = true;
 }
 
 thread_local std::string g_codec_err;
@@ -1791,6 +2450,14 @@ int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, 
   return 0;
 }
 
+#if defined(ACS_CODEC_TIMING)
+int acs_internal_codec_cycles(uint64_t* parse, uint64_t* encode) {
+  *parse = g_cyc_parse.exchange(0);
+  *encode = g_cyc_encode.exchange(0);
+  return 0;
+}
+#endif
+
 // Test hook (not in include/acs_mi355x.h): pin the candidate-class key level of every later
 // encode (0 entity+roles+action, 1 entity+action, 2 entity; -1 automatic).
 int acs_internal_codec_force_level(acs_codec* c, int level) {
@@ -1835,17 +2502,22 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
   }
   acs_req_batch v{};
   v.n = b->n;
-  v.hdr = b->hdr.data();
-  v.res = b->res.data();
-  v.subj = b->subj.data();
-  v.act = b->act.data();
-  v.roles = b->roles.data();
-  v.arena = b->arena.data();
-  v.arena_words = b->arena.size();
+  if (b->expanded) {
+    v.hdr = b->hdr.data();
+    v.res = b->res.data();
+    v.subj = b->subj.data();
+    v.act = b->act.data();
+    v.roles = b->roles.data();
+  }
+  v.lines = b->n ? b->lines : nullptr;
+  v.ext = b->ext_words ? b->ext : nullptr;
+  v.ext_words = b->ext_words;
+  v.arena = b->arena;
+  v.arena_words = b->arena_words;
   v.rx = b->rx.data();
   v.rx_cols = b->rx_cols;
   v.rx_rows = b->rx_rows;
-  v.cand = b->cand.empty() ? nullptr : b->cand.data();
+  v.cand = b->cand;
   v.cand_words = b->cand_words;
   v.cand_wp = b->cand_wp;
   v.cand_wr = b->cand_wr;
@@ -1858,8 +2530,22 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
     v.role_rows_bits = b->role_bits.data();
     v.role_rows = b->role_rows;
   }
-  v.lines = b->lines.empty() ? nullptr : b->lines.data();
   *out = v;
+  return 0;
+}
+
+int acs_codec_batch_expand(acs_codec_batch* b) {
+  if (!b) {
+    acs_internal_set_error("acs_codec_batch_expand: null argument");
+    return -1;
+  }
+  try {
+    expand_soa(*b);
+  } catch (const std::exception& e) {
+    g_codec_err = std::string("acs_codec_batch_expand: ") + e.what();
+    acs_internal_set_error(g_codec_err.c_str());
+    return -1;
+  }
   return 0;
 }
 
@@ -1883,7 +2569,7 @@ int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size
   const uint32_t t = (id - c->n_dict) >> LOCAL_BITS, k = (id - c->n_dict) & ((1u << LOCAL_BITS) - 1);
   if (t >= b->strings.size() || k >= b->strings[t].strs.size()) return -1;
   *s = b->strings[t].strs[k].data();
-  *len = b->strings[t].strs[k].size();
+  *len = b->strings[t].strs[k].size();  // (views into the thread's StrPool, alive with the batch)
   return 2;
 }
 
@@ -1896,10 +2582,10 @@ int acs_codec_ec_values(const acs_codec* c, const char** json, size_t* len) {
 
 int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n) {
   if (!b || !out) return -1;
-  const double v[6] = {b->seconds[0], b->seconds[1], b->seconds[2], b->seconds[3], (double)b->hr_hits,
-                       (double)b->hr_misses};
-  for (int k = 0; k < n && k < 6; ++k) out[k] = v[k];
-  return 6;
+  const double v[8] = {b->seconds[0], b->seconds[1], b->seconds[2], b->seconds[3], (double)b->hr_hits,
+                       (double)b->hr_misses, (double)b->classes_new, (double)b->cand_rows};
+  for (int k = 0; k < n && k < 8; ++k) out[k] = v[k];
+  return 8;
 }
 
 }  // extern "C"

@@ -465,8 +465,8 @@ void json_write(std::string& o, const JV* v) {
         if (k) o += ',';
         JV key;
         key.t = J_STR;
-        key.s = v->o[k].k.data();
-        key.n = (uint32_t)v->o[k].k.size();
+        key.s = v->o[k].k;
+        key.n = v->o[k].kn;
         json_write(o, &key);
         o += ':';
         json_write(o, &v->o[k].v);
@@ -587,7 +587,7 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
       if (!found) b.ca_map.push_back({key, code});
     }
     for (uint32_t k = 0; k < urns->n; ++k) {  // URN ids first, in config order
-      const std::string name(urns->o[k].k);
+      const std::string name(urns->o[k].key());
       const JV* v = &urns->o[k].v;
       if (b.urn.count(name)) {
         b.urn[name] = v;

@@ -140,6 +140,7 @@ struct Batch {
   const uint32_t* role_bits;  // [role_rows][cand_words]
   uint32_t role_rows;
   const ReqLine* lines;       // [n] packed first rows (nullptr: read the SoA rows)
+  const uint32_t* ext;        // compact batches (hdr == nullptr): extension records (ReqLine.ext)
 };
 
 // OR of x over the wave's ACTIVE lanes, returned in an SGPR.  A lane drops out once its bits
@@ -329,6 +330,7 @@ struct ReqCtx {
   uint32_t i;
   ReqHdr h;
   const uint32_t* ar;
+  const uint32_t* ex;  // compact batch: this request's extension record (acs_layout.h ext_geom)
   uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
   const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
@@ -340,6 +342,7 @@ struct ReqCtx {
   ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
       : T(t), B(b), i(idx), h(hd) {
     ar = B.arena + h.arena_off;
+    ex = ln && ln->ext ? B.ext + (size_t)(ln->ext - 1u) * 4u : nullptr;
     if (ln) {
       s0i = ln->s0.id; s0v = ln->s0.value; s1i = ln->s1.id; s1v = ln->s1.value;
       a0i = ln->a0.id; a0v = ln->a0.value;
@@ -368,21 +371,41 @@ struct ReqCtx {
   }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
+  // Rows past the line: the SoA rows, or a compact batch's extension record.
+  ACS_FN ExtGeom geom() const { return ext_geom(h.nres, h.nsubj, h.nact, h.nroles); }
+  ACS_FN ReqRes res_row(uint32_t j) const {
+    if (B.hdr) return B.res[(size_t)j * B.n + i];
+    const uint32_t* w = ex + 4u * (j - (uint32_t)LINE_RES);
+    ReqRes q;
+    __builtin_memcpy(&q, w, sizeof q);
+    return q;
+  }
   ACS_FN Pair subj(uint32_t j) const {
-    if (j >= 2) return B.subj[(size_t)j * B.n + i];
+    if (j >= 2) {
+      if (B.hdr) return B.subj[(size_t)j * B.n + i];
+      const uint32_t* w = ex + geom().subj + 2u * (j - 2u);
+      return Pair{w[0], w[1]};
+    }
     Pair p;
     p.id = j == 0 ? s0i : s1i;  // value selects (no address taken: stays in registers)
     p.value = j == 0 ? s0v : s1v;
     return p;
   }
   ACS_FN Pair act(uint32_t j) const {
-    if (j >= 1) return B.act[(size_t)j * B.n + i];
+    if (j >= 1) {
+      if (B.hdr) return B.act[(size_t)j * B.n + i];
+      const uint32_t* w = ex + geom().act + 2u * (j - 1u);
+      return Pair{w[0], w[1]};
+    }
     Pair p;
     p.id = a0i;
     p.value = a0v;
     return p;
   }
-  ACS_FN uint32_t role(uint32_t j) const { return j >= 2 ? B.roles[(size_t)j * B.n + i] : (j == 0 ? role0 : role1); }
+  ACS_FN uint32_t role(uint32_t j) const {
+    if (j < 2) return j == 0 ? role0 : role1;
+    return B.hdr ? B.roles[(size_t)j * B.n + i] : ex[geom().roles + (j - 2u)];
+  }
   ACS_FN uint8_t rx(uint32_t col, uint32_t row) const { return B.rx[(size_t)col * B.rx_rows + row]; }
   ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
 };
@@ -420,14 +443,17 @@ struct ReqLds : ReqCtx {
 #else
     if (j < LDS_SLOTS) return col[j * stride];
 #endif
-    return B.res[(size_t)j * B.n + i];
+    return res_row((uint32_t)j);
   }
 };
+static_assert(LDS_SLOTS <= LINE_RES, "the kernels stage LDS slots from the request line");
 
 // Resource attributes read from HBM on every use (host build of the core).
 struct ReqMem : ReqCtx {
   uint32_t e0_val, e0_col;
-  ACS_FN ReqMem(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd) : ReqCtx(t, b, idx, hd) {
+  const ReqLine* line;  // compact batch: the request's line (nullptr: SoA rows)
+  ACS_FN ReqMem(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
+      : ReqCtx(t, b, idx, hd, ln), line(ln) {
     const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
     e0_val = e0_col = 0;
     if (e >= 1 && e <= 6) {
@@ -436,8 +462,12 @@ struct ReqMem : ReqCtx {
       e0_col = q.col;
     }
   }
-  ACS_FN ReqRes res(int j) const { return B.res[(size_t)j * B.n + i]; }
+  ACS_FN ReqRes res(int j) const { return line && j < LINE_RES ? line->res[j] : res_row((uint32_t)j); }
 };
+
+// The request's header and (compact batches) its line.
+ACS_FN const ReqLine* req_line(const Batch& B, uint32_t i) { return B.hdr ? nullptr : B.lines + i; }
+ACS_FN ReqHdr req_hdr(const Batch& B, uint32_t i) { return B.hdr ? B.hdr[i] : B.lines[i].h; }
 
 // ------------------------------------------------------------------ attributesMatch (loose ==)
 ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const ReqCtx& R, bool subjects) {
@@ -1065,11 +1095,11 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h, uint32_t i) {
 }
 
 ACS_FN Decision is_allowed(const Tables& T, const Batch& B, uint32_t i) {
-  const ReqHdr h = B.hdr[i];
+  const ReqHdr h = req_hdr(B, i);
   bool done;
   Decision d = early_decision(h, &done);
   if (done) return d;
-  return is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i));
+  return is_allowed_t(ReqMem(T, B, i, h, req_line(B, i)), request_filter(B, h, i));
 }
 
 // ------------------------------------------------------------------ whatIsAllowed
@@ -1220,14 +1250,15 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
 // Host build: row = this request's zeroed BitsLayout row.
 ACS_FN Decision what_is_allowed(const Tables& T, const Batch& B, uint32_t i, uint32_t* row, uint32_t* obl_out,
                                 uint32_t* obl_n) {
-  const ReqHdr h = B.hdr[i];
+  const ReqHdr h = req_hdr(B, i);
   OblLog obl{obl_out, 0, false};
   Decision d{};
   if (h.flags & RQ_HOST) {
     d.flags = OF_HOST_REQ;
   } else {
     RowSink sink{row};
-    d = what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), bits_layout(T.n_sets, T.n_pols, T.n_rules),
+    d = what_is_allowed_t(ReqMem(T, B, i, h, req_line(B, i)), request_filter(B, h, i),
+                          bits_layout(T.n_sets, T.n_pols, T.n_rules),
                           sink, obl);
   }
   *obl_n = (d.flags & OF_ERR) ? 0u : obl.n;

@@ -78,19 +78,35 @@ static void utf8(std::string& out, uint32_t c) {
   }
 }
 
+// The next '"' or '\\' in [p, e): 8 bytes at a time (zero-byte test on the XOR with each
+// target byte), then the tail.
+static inline const char* find_quote_or_escape(const char* p, const char* e) {
+  constexpr uint64_t ONES = 0x0101010101010101ull, HIGH = 0x8080808080808080ull;
+  constexpr uint64_t QQ = ONES * (uint8_t)'"', BS = ONES * (uint8_t)'\\';
+  while (p + 8 <= e) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    const uint64_t a = w ^ QQ, b = w ^ BS;
+    const uint64_t hit = ((a - ONES) & ~a & HIGH) | ((b - ONES) & ~b & HIGH);
+    if (hit) return p + (__builtin_ctzll(hit) >> 3);
+    p += 8;
+  }
+  while (p < e && *p != '"' && *p != '\\') ++p;
+  return p;
+}
+
 void Parser::string(JV& out) {
   ++p_;  // opening quote
   const char* b = p_;
   bool esc = false;
-  while (p_ < e_ && *p_ != '"') {
-    if (*p_ == '\\') {
-      esc = true;
-      p_ += 2;
-    } else {
-      ++p_;
-    }
+  for (;;) {
+    p_ = find_quote_or_escape(p_, e_);
+    if (p_ >= e_) throw ParseError{"unterminated string"};
+    if (*p_ == '"') break;
+    esc = true;  // a backslash: skip it and the escaped byte
+    p_ += 2;
+    if (p_ > e_) throw ParseError{"unterminated string"};
   }
-  if (p_ >= e_) throw ParseError{"unterminated string"};
   out.t = J_STR;
   if (!esc) {
     out.s = b;
@@ -170,8 +186,9 @@ void Parser::value(JV& out) {
         if (p_ >= e_ || *p_ != ':') throw ParseError{"expected ':'"};
         ++p_;
         JKV kv;
-        kv.k = k.str();
-        if (!raw_key_.empty() && kv.k == raw_key_) {
+        kv.k = k.s;
+        kv.kn = k.n;
+        if (!raw_key_.empty() && kv.key() == raw_key_) {
           skip_ws();
           const char* b = p_;
           const char f = b < e_ ? *b : 0;
@@ -280,14 +297,6 @@ const JV* Parser::parse(const char* p, const char* e, std::string_view raw_key) 
   skip_ws();
   if (p_ != e_) throw ParseError{"trailing text"};
   return v;
-}
-
-const JV* get(const JV* v, std::string_view key) {
-  if (v->t != J_OBJ) return &kUndef;
-  const JV* hit = &kUndef;
-  for (uint32_t k = 0; k < v->n; ++k)
-    if (v->o[k].k == key) hit = &v->o[k].v;
-  return hit;
 }
 
 bool truthy(const JV* v) {

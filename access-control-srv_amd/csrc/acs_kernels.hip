@@ -79,13 +79,17 @@ constexpr int BLOCK = 256;
 // and B.role_major the fields swap ([role key | bucket], `cbits` bucket bits): a wave then
 // spans few role keys, and the role rows prune rules hardest (large stores).
 __device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits, uint32_t cbits) {
-  const ReqHdr h = B.hdr[k];
+  const ReqLine* ln = B.hdr ? nullptr : B.lines + k;  // compact batch: the line holds the rows read here
+  const ReqHdr h = ln ? ln->h : B.hdr[k];
   const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
-  uint32_t low = B.role_key ? B.role_key[k] : (h.nact ? B.act[k].value : 0u), bucket = cls + 1;
+  const uint32_t a0 = h.nact ? (ln ? ln->a0.value : B.act[k].value) : 0u;
+  uint32_t low = B.role_key ? B.role_key[k] : a0, bucket = cls + 1;
   if (cls >= B.cand_rows) {
     bucket = 0;
+    const uint32_t* ex = ln && ln->ext ? B.ext + (size_t)(ln->ext - 1u) * 4u : nullptr;
     for (uint32_t j = 0; j < h.nres; ++j) {
-      const ReqRes q = B.res[(size_t)j * B.n + k];
+      const ReqRes q = !ln ? B.res[(size_t)j * B.n + k]
+                       : j < (uint32_t)LINE_RES ? ln->res[j] : *(const ReqRes*)(ex + 4u * (j - LINE_RES));
       if (q.kind & K_ENT) {
         low = q.value;
         break;
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
     const ReqLds R(T, B, i, h, col, BLOCK, ln);
     d = is_allowed_t(R, F);
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   } else {
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln && j < LINE_RES ? ln->res[j] : B.res[(size_t)j * B.n + i];
+    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
     d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln), F, BL, sink, log);
   }
   sink.finish();
@@ -474,8 +478,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
   const uint64_t k = (uint64_t)c * m + j;  // output slot [c][j]
   const uint32_t i = live ? idx[j] : 0u;
   const bool in = live && i < B.n;
+  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;
   ReqHdr h{};
-  if (in) h = B.hdr[i];
+  if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                      wave_lds_row(B));
@@ -489,10 +494,10 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
     OblLog log{obl + k * 2 * cap, 0, false, cap, 0};
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = B.res[(size_t)q * B.n + i];
+    for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = ln ? ln->res[q] : B.res[(size_t)q * B.n + i];
     const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks), s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
     NullSink none;
-    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK), F, BitsLayout{}, none, log, s0, s1);
+    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln), F, BitsLayout{}, none, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
   }
   obl_n[k] = total;
@@ -537,6 +542,39 @@ FilterForm filter_form(const Batch& B) {
 
 }  // namespace
 
+namespace {
+// Grow-only device allocation: a steady state of equal-sized batches allocates nothing.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int reserve(size_t n) {
+    if (n <= bytes) return 0;
+    if (p) HIP_OK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+    const size_t want = n + n / 8;  // headroom: batches of slightly varying size reuse it
+    HIP_OK(hipMalloc(&p, want));
+    bytes = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+// The device memory one evaluation needs beyond the tables: the coherence sort's keys /
+// permutation, the uploaded request image and the outputs.
+struct Workspace {
+  DevBuf sort, img, out;
+  void release() {
+    sort.release();
+    img.release();
+    out.release();
+  }
+};
+}  // namespace
+
 struct acs_tables {
   int device = 0;
   void* dev = nullptr;  // one allocation holding every section
@@ -550,11 +588,11 @@ struct acs_tables {
   int timing = 0;
   hipEvent_t tev[2 * RING] = {};
   uint64_t launches = 0;
-  // sort workspace, grown on demand: keys/idx double buffers + per-tile digit counts
-  void* ws = nullptr;
-  size_t ws_bytes = 0;
-  // host-buffer entry points (internal stream, events, workspace) may be called from
-  // several host threads at once (e.g. the N-API addon's libuv pool): one at a time
+  // *_device entry points: the coherence sort's workspace (one stream at a time)
+  Workspace dws;
+  // host-buffer entry points (internal stream, events, their own workspace) may be called
+  // from several host threads at once (e.g. the N-API addon's libuv pool): one at a time
+  Workspace hws;
   std::mutex mu;
   uint32_t rx_rows_min = 0;  // regex-matrix rows the rule resource attributes read
 };
@@ -597,6 +635,29 @@ int acs_phase_read(unsigned long long* out, int n) {
   return PH_N;
 }
 #endif
+
+// Host memory for the codec's batch arrays (acs_codec.cpp HostPool): page-locked and portable
+// (every device can DMA from it) when a device is present, so acs_is_allowed's per-section
+// copies run at full PCIe speed; plain malloc on a machine without one.
+void* acs_internal_host_alloc(size_t bytes, int* pinned) {
+  static const bool have = [] {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+  }();
+  void* p = nullptr;
+  if (have && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess) {
+    *pinned = 1;
+    return p;
+  }
+  *pinned = 0;
+  return malloc(bytes);
+}
+
+void acs_internal_host_free(void* p, int pinned) {
+  if (!p) return;
+  if (pinned) (void)hipHostFree(p);
+  else free(p);
+}
 
 int acs_device_count(void) {
   int n = 0;
@@ -734,7 +795,8 @@ void acs_free(acs_tables* t) {
   if (t->ev0) (void)hipEventDestroy(t->ev0);
   if (t->ev1) (void)hipEventDestroy(t->ev1);
   if (t->stream) (void)hipStreamDestroy(t->stream);
-  if (t->ws) (void)hipFree(t->ws);
+  t->dws.release();
+  t->hws.release();
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
@@ -774,7 +836,9 @@ static Batch to_batch(const acs_req_batch* b) {
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
-  B.lines = ACS_AB_NO_LINES ? nullptr : (const ReqLine*)b->lines;
+  // compact batches (no SoA rows) always read their lines; SoA batches may skip them (A/B)
+  B.lines = (ACS_AB_NO_LINES && b->hdr) ? nullptr : (const ReqLine*)b->lines;
+  B.ext = b->ext;
   return B;
 }
 
@@ -798,7 +862,7 @@ int acs_set_option(acs_tables* t, int option, int value) {
 }
 
 // Coherence sort: permutation of request indices ordered by (class, low field).
-static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const uint32_t** perm) {
+static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream_t s, const uint32_t** perm) {
   *perm = nullptr;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
@@ -815,14 +879,8 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
   const uint32_t ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
   const size_t need = 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
-  if (need > t->ws_bytes) {
-    if (t->ws) HIP_OK(hipFree(t->ws));
-    t->ws = nullptr;
-    t->ws_bytes = 0;
-    HIP_OK(hipMalloc(&t->ws, need));
-    t->ws_bytes = need;
-  }
-  uint32_t* k0 = (uint32_t*)t->ws;
+  if (W.sort.reserve(need)) return -1;
+  uint32_t* k0 = (uint32_t*)W.sort.p;
   uint32_t* k1 = k0 + n;
   uint32_t* v0 = k1 + n;
   uint32_t* v1 = v0 + n;
@@ -851,13 +909,10 @@ static int coherence_perm(acs_tables* t, const Batch& B, hipStream_t s, const ui
   return 0;
 }
 
-int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* out, void* stream) {
-  if (!t || !b) return fail("acs_is_allowed_device: null argument");
-  if (b->n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
+static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  if (coherence_perm(t, B, s, &perm)) return -1;
+  if (coherence_perm(t, W, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
@@ -868,6 +923,12 @@ int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* o
     t->launches++;
   }
   return 0;
+}
+
+int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* out, void* stream) {
+  if (!t || !b) return fail("acs_is_allowed_device: null argument");
+  if (b->n == 0) return 0;
+  return is_allowed_launch(t, t->dws, b, out, (hipStream_t)stream);
 }
 
 int acs_kernel_times(acs_tables* t, float* ms, int n) {
@@ -882,14 +943,11 @@ int acs_kernel_times(acs_tables* t, float* ms, int n) {
   return m;
 }
 
-int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
-                               uint32_t* obl_n, acs_decision* out, void* stream) {
-  if (!t || !b) return fail("acs_what_is_allowed_device: null argument");
-  if (b->n == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
+static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
+                                  uint32_t* obl_n, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  if (coherence_perm(t, B, s, &perm)) return -1;
+  if (coherence_perm(t, W, B, s, &perm)) return -1;
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
@@ -903,6 +961,13 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
     t->launches++;
   }
   return 0;
+}
+
+int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
+                               uint32_t* obl_n, acs_decision* out, void* stream) {
+  if (!t || !b) return fail("acs_what_is_allowed_device: null argument");
+  if (b->n == 0) return 0;
+  return what_is_allowed_launch(t, t->dws, b, bits, obl, obl_n, out, (hipStream_t)stream);
 }
 
 constexpr uint32_t OBL_CAP_LIMIT = 1u << 20;
@@ -947,47 +1012,75 @@ int acs_shard_decode_device(const uint64_t* keys, size_t n, acs_decision* out, v
 // ---------------------------------------------------------------- host-buffer entry points
 namespace {
 
-struct DevBatch {
-  std::vector<void*> bufs;
+constexpr size_t IMG_ALIGN = 256;
+
+// The device image of a host batch: every section the kernels read, copied into one
+// grow-only device buffer (no per-call allocation) with one async copy per section — from
+// pinned memory (the native codec's buffers) these run at full PCIe speed.  A compact batch
+// ships request lines + extension records + arena + regex matrix + class rows (~220 B per
+// request at c3); an SoA batch its rows as well.
+struct Image {
   acs_req_batch d{};
-  ~DevBatch() {
-    for (void* p : bufs) (void)hipFree(p);
-  }
-  int up(const void* src, size_t n, const void** dst, hipStream_t s) {
-    void* p = nullptr;
-    HIP_OK(hipMalloc(&p, n ? n : 16));
-    bufs.push_back(p);
-    if (n) HIP_OK(hipMemcpyAsync(p, src, n, hipMemcpyHostToDevice, s));
-    *dst = p;
-    return 0;
-  }
-  void* alloc(size_t n) {
-    void* p = nullptr;
-    if (hipMalloc(&p, n ? n : 16) != hipSuccess) return nullptr;
-    bufs.push_back(p);
-    return p;
+  struct Sec {
+    const void* src;
+    size_t bytes;
+    const void** dst;
+  };
+  std::vector<Sec> secs;
+  size_t total = 0;
+  void add(const void* src, size_t bytes, const void** dst) {
+    if (!src) {
+      *dst = nullptr;
+      return;
+    }
+    secs.push_back({src, bytes, dst});
+    total += (bytes + IMG_ALIGN - 1) & ~(IMG_ALIGN - 1);
   }
 };
 
-int upload_batch(DevBatch& D, const acs_req_batch* b, hipStream_t s) {
-  D.d = *b;
+int upload_batch(Workspace& W, const acs_req_batch* b, acs_req_batch* dev, hipStream_t s) {
+  Image I;
+  I.d = *b;
   const size_t n = b->n;
-  if (D.up(b->hdr, n * sizeof(ReqHdr), &D.d.hdr, s) || D.up(b->res, n * QMAX * sizeof(ReqRes), &D.d.res, s) ||
-      D.up(b->subj, n * SMAX * sizeof(Pair), &D.d.subj, s) || D.up(b->act, n * AMAX * sizeof(Pair), &D.d.act, s) ||
-      D.up(b->roles, n * RMAX * sizeof(uint32_t), (const void**)&D.d.roles, s) ||
-      D.up(b->arena, b->arena_words * sizeof(uint32_t), (const void**)&D.d.arena, s) ||
-      D.up(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&D.d.rx, s))
-    return -1;
-  if (b->cand && D.up(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t),
-                      (const void**)&D.d.cand, s))
-    return -1;
-  if (b->lines && D.up(b->lines, n * sizeof(ReqLine), &D.d.lines, s)) return -1;
-  if (b->role_key && (D.up(b->role_key, n * sizeof(uint32_t), (const void**)&D.d.role_key, s) ||
-                      D.up(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
-                           (const void**)&D.d.role_rows_bits, s)))
-    return -1;
+  if (b->hdr) {
+    I.add(b->hdr, n * sizeof(ReqHdr), &I.d.hdr);
+    I.add(b->res, n * QMAX * sizeof(ReqRes), &I.d.res);
+    I.add(b->subj, n * SMAX * sizeof(Pair), &I.d.subj);
+    I.add(b->act, n * AMAX * sizeof(Pair), &I.d.act);
+    I.add(b->roles, n * RMAX * sizeof(uint32_t), (const void**)&I.d.roles);
+  }
+  I.add(b->lines, n * sizeof(ReqLine), &I.d.lines);
+  I.add(b->ext, b->ext_words * sizeof(uint32_t), (const void**)&I.d.ext);
+  I.add(b->arena, b->arena_words * sizeof(uint32_t), (const void**)&I.d.arena);
+  I.add(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&I.d.rx);
+  if (b->cand) I.add(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t), (const void**)&I.d.cand);
+  if (b->role_key) {
+    I.add(b->role_key, n * sizeof(uint32_t), (const void**)&I.d.role_key);
+    I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
+          (const void**)&I.d.role_rows_bits);
+  }
+  if (W.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
+  char* base = (char*)W.img.p;
+  size_t off = 0;
+  for (const Image::Sec& x : I.secs) {
+    if (x.bytes) HIP_OK(hipMemcpyAsync(base + off, x.src, x.bytes, hipMemcpyHostToDevice, s));
+    *x.dst = base + off;
+    off += (x.bytes + IMG_ALIGN - 1) & ~(IMG_ALIGN - 1);
+  }
+  *dev = I.d;
   return 0;
 }
+
+// Output regions of one call in the workspace's `out` buffer (256-B aligned).
+struct OutLayout {
+  size_t off[4] = {};
+  size_t total = 0;
+  size_t put(size_t bytes) {
+    const size_t o = total;
+    total += (bytes + IMG_ALIGN - 1) & ~(IMG_ALIGN - 1);
+    return o;
+  }
+};
 
 }  // namespace
 
@@ -997,12 +1090,12 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
-  DevBatch D;
-  if (upload_batch(D, b, t->stream)) return -1;
-  void* dout = D.alloc(b->n * sizeof(Decision));
-  if (!dout) return fail("acs_is_allowed: hipMalloc failed");
+  acs_req_batch d;
+  if (upload_batch(t->hws, b, &d, t->stream)) return -1;
+  if (t->hws.out.reserve(b->n * sizeof(Decision))) return -1;
+  void* dout = t->hws.out.p;
   HIP_OK(hipEventRecord(t->ev0, t->stream));
-  if (acs_is_allowed_device(t, &D.d, (acs_decision*)dout, t->stream)) return -1;
+  if (is_allowed_launch(t, t->hws, &d, (acs_decision*)dout, t->stream)) return -1;
   HIP_OK(hipEventRecord(t->ev1, t->stream));
   HIP_OK(hipMemcpyAsync(out, dout, b->n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
@@ -1017,23 +1110,23 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
-  DevBatch D;
-  if (upload_batch(D, b, t->stream)) return -1;
+  acs_req_batch d;
+  if (upload_batch(t->hws, b, &d, t->stream)) return -1;
   const size_t words = acs_wia_words_per_request(t);
-  void* dbits = D.alloc(b->n * words * sizeof(uint32_t));
-  void* dobl = D.alloc(b->n * 2 * OBL_MAX * sizeof(uint32_t));
-  void* dobln = D.alloc(b->n * sizeof(uint32_t));
-  void* dout = D.alloc(b->n * sizeof(Decision));
-  if (!dbits || !dobl || !dobln || !dout) return fail("acs_what_is_allowed: hipMalloc failed");
+  OutLayout O;
+  const size_t o_bits = O.put(b->n * words * sizeof(uint32_t)), o_obl = O.put(b->n * 2 * OBL_MAX * sizeof(uint32_t));
+  const size_t o_n = O.put(b->n * sizeof(uint32_t)), o_out = O.put(b->n * sizeof(Decision));
+  if (t->hws.out.reserve(O.total)) return -1;
+  char* ob = (char*)t->hws.out.p;
   HIP_OK(hipEventRecord(t->ev0, t->stream));
-  if (acs_what_is_allowed_device(t, &D.d, (uint32_t*)dbits, (uint32_t*)dobl, (uint32_t*)dobln,
-                                 (acs_decision*)dout, t->stream))
+  if (what_is_allowed_launch(t, t->hws, &d, (uint32_t*)(ob + o_bits), (uint32_t*)(ob + o_obl), (uint32_t*)(ob + o_n),
+                             (acs_decision*)(ob + o_out), t->stream))
     return -1;
   HIP_OK(hipEventRecord(t->ev1, t->stream));
-  HIP_OK(hipMemcpyAsync(bits, dbits, b->n * words * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl, dobl, b->n * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl_n, dobln, b->n * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(out, dout, b->n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(bits, ob + o_bits, b->n * words * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl, ob + o_obl, b->n * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl_n, ob + o_n, b->n * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(out, ob + o_out, b->n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
   HIP_OK(hipEventElapsedTime(&t->last_ms, t->ev0, t->ev1));
   return 0;
@@ -1050,19 +1143,21 @@ int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
-  DevBatch D;
-  if (upload_batch(D, b, t->stream)) return -1;
+  acs_req_batch d;
+  if (upload_batch(t->hws, b, &d, t->stream)) return -1;
   const size_t lanes = m * chunks;
-  void* didx = D.alloc(m * sizeof(uint32_t));
-  void* dobl = D.alloc(lanes * 2 * (size_t)cap * sizeof(uint32_t));
-  void* dobln = D.alloc(lanes * sizeof(uint32_t));
-  if (!didx || !dobl || !dobln) return fail("acs_what_is_allowed_obl: hipMalloc failed");
-  HIP_OK(hipMemcpyAsync(didx, idx, m * sizeof(uint32_t), hipMemcpyHostToDevice, t->stream));
-  if (acs_what_is_allowed_obl_device(t, &D.d, (const uint32_t*)didx, m, chunks, cap, (uint32_t*)dobl,
-                                     (uint32_t*)dobln, t->stream))
+  OutLayout O;
+  const size_t o_idx = O.put(m * sizeof(uint32_t)), o_obl = O.put(lanes * 2 * (size_t)cap * sizeof(uint32_t));
+  const size_t o_n = O.put(lanes * sizeof(uint32_t));
+  if (t->hws.out.reserve(O.total)) return -1;
+  char* ob = (char*)t->hws.out.p;
+  HIP_OK(hipMemcpyAsync(ob + o_idx, idx, m * sizeof(uint32_t), hipMemcpyHostToDevice, t->stream));
+  if (acs_what_is_allowed_obl_device(t, &d, (const uint32_t*)(ob + o_idx), m, chunks, cap, (uint32_t*)(ob + o_obl),
+                                     (uint32_t*)(ob + o_n), t->stream))
     return -1;
-  HIP_OK(hipMemcpyAsync(obl, dobl, lanes * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl_n, dobln, lanes * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl, ob + o_obl, lanes * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                        t->stream));
+  HIP_OK(hipMemcpyAsync(obl_n, ob + o_n, lanes * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
   return 0;
 }

@@ -9,6 +9,15 @@
 #pragma once
 #include <stdint.h>
 
+#ifndef __HIPCC__  // plain C++ (g++) translation units: the host codec, compiler, validator
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
 namespace acs {
 
 // ---------------------------------------------------------------- interned ids
@@ -164,21 +173,43 @@ struct ReqRes {              // 16 B
 };
 constexpr uint32_t RES_RX_SAFE = 1;  // ReqRes.pad bit (absent: the request may throw in a RegExp test)
 
-// One request's first rows packed into one 128-B line (acs_req_batch.lines, optional): K1
-// reads it with one gather instead of one per SoA row (header, 4 attributes, 2 subjects,
-// action, 2 roles, arena counts: ~8 lines per request).  Every field equals the SoA rows:
-// res[j] / s* / a0 / r* zero past the request's counts, ar0 / ar1 the arena's two count words
-// (0 for RQ_HOST / RQ_NO_TARGET requests).  Built by both encoders (encoder.pack_lines,
-// acs_codec.cpp) and checked against the SoA rows by the host entry points.
-constexpr int LINE_RES = 4;
+// One request's first rows packed into one 128-B line (acs_req_batch.lines): K1 reads it with
+// one gather instead of one per SoA row (header, 4 attributes, 2 subjects, action, 2 roles,
+// arena counts: ~8 lines per request).  res[j] / s* / a0 / r* are zero past the request's
+// counts, ar0 / ar1 the arena's two count words (0 for RQ_HOST / RQ_NO_TARGET requests).
+// The rows that do not fit (attributes 4.., subjects 2.., actions 1.., roles 2..) live in the
+// request's extension record in acs_req_batch.ext (ReqLine.ext = 1 + its offset in 16-B
+// units; 0 = none):
+//   ReqRes res[LINE_RES..nres) | Pair subj[2..nsubj) | Pair act[1..nact) | u32 roles[2..nroles)
+// padded to a multiple of 4 words.  A batch is either SoA rows (+ optional lines, equal to
+// them) or compact: lines + ext only (hdr / res / subj / act / roles NULL), the form the
+// native codec emits and the host-buffer entry points upload.  Built by both encoders
+// (encoder.pack_lines, acs_codec.cpp) and checked by the host entry points.
+constexpr int LINE_RES = 4, LINE_SUBJ = 2, LINE_ACT = 1, LINE_ROLES = 2;
 struct ReqLine {             // 128 B
   ReqHdr h;
   ReqRes res[LINE_RES];
   Pair s0, s1, a0;
   uint32_t r0, r1;
   uint32_t ar0, ar1;
-  uint32_t pad[2];
+  uint32_t ext;              // 1 + 16-B unit offset of the extension record (0: none)
+  uint32_t pad;
 };
+
+// Extension record geometry (u32 words) of a request with the given counts.
+struct ExtGeom {
+  uint32_t res, subj, act, roles, words;  // word offsets of each part, total padded size
+};
+__host__ __device__ inline ExtGeom ext_geom(uint32_t nres, uint32_t nsubj, uint32_t nact, uint32_t nroles) {
+  ExtGeom g;
+  g.res = 0;
+  g.subj = 4u * (nres > (uint32_t)LINE_RES ? nres - LINE_RES : 0u);
+  g.act = g.subj + 2u * (nsubj > (uint32_t)LINE_SUBJ ? nsubj - LINE_SUBJ : 0u);
+  g.roles = g.act + 2u * (nact > (uint32_t)LINE_ACT ? nact - LINE_ACT : 0u);
+  const uint32_t end = g.roles + (nroles > (uint32_t)LINE_ROLES ? nroles - LINE_ROLES : 0u);
+  g.words = (end + 3u) & ~3u;
+  return g;
+}
 
 // Context arena (u32 words), per request:
 //   [0] n_grants | n_rolese<<8 | n_slots<<16 | n_roots<<24

@@ -75,13 +75,20 @@ int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_
   return 0;
 }
 
-// Batch checks for the host-buffer entry points.
+// Batch checks for the host-buffer entry points.  SoA batches (+ optional lines equal to
+// their rows) and compact batches (lines + extension records) alike.
 int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
                              uint32_t rx_rows_min) {
   const size_t n = b->n;
   if (n == 0) return 0;
-  if (!b->hdr || !b->res || !b->subj || !b->act || !b->roles || !b->arena)
+  const bool compact = b->hdr == nullptr;
+  if (compact) {
+    if (b->res || b->subj || b->act || b->roles) return bad("batch: partial SoA rows", 0);
+    if (!b->lines) return bad("batch: compact batch without request lines", 0);
+  } else if (!b->res || !b->subj || !b->act || !b->roles) {
     return bad("batch: null request buffer", 0);
+  }
+  if (!b->arena) return bad("batch: null request buffer", 0);
   if (rx_rows_min && (!b->rx || b->rx_rows < rx_rows_min)) return bad("batch: regex matrix rows", b->rx_rows);
   if (b->cand) {
     if (b->cand_wp < words32(n_sets) || b->cand_wr < b->cand_wp + words32(n_pols) ||
@@ -111,13 +118,25 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
   const size_t W = b->arena_words;
   const ReqLine* lines = (const ReqLine*)b->lines;
   for (size_t i = 0; i < n; ++i) {
-    const ReqHdr hd = hdr[i];
+    const ReqHdr hd = compact ? lines[i].h : hdr[i];
     if (hd.nres > QMAX || hd.nsubj > SMAX || hd.nact > AMAX || hd.nroles > RMAX) return bad("batch: counts", i);
     const size_t o = hd.arena_off;
     if (o + 2 > W) return bad("batch: arena offset", i);
     const uint32_t* ar = b->arena + o;
     const size_t room = W - o;
-    if (lines) {  // the packed line must equal the SoA rows (K1 trusts it for addressing)
+    const bool live = !(hd.flags & (RQ_HOST | RQ_NO_TARGET));
+    // the rows past the line: extension record of a compact batch
+    const uint32_t* ex = nullptr;
+    if (compact) {
+      const ExtGeom g = ext_geom(hd.nres, hd.nsubj, hd.nact, hd.nroles);
+      if (g.words) {
+        const uint32_t e = lines[i].ext;
+        if (!e || !b->ext || ((size_t)e - 1) * 4 + g.words > b->ext_words) return bad("batch: extension record", i);
+        ex = b->ext + ((size_t)e - 1) * 4;
+      }
+      if (lines[i].ar0 != (live ? ar[0] : 0u) || lines[i].ar1 != (live ? ar[1] : 0u))
+        return bad("batch: request line arena counts", i);
+    } else if (lines) {  // the packed line must equal the SoA rows (K1 trusts it for addressing)
       ReqLine want{};
       want.h = hd;
       for (uint32_t j = 0; j < hd.nres && j < (uint32_t)LINE_RES; ++j) want.res[j] = res[j * n + i];
@@ -128,12 +147,20 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
       if (hd.nact > 0) want.a0 = act[i];
       if (hd.nroles > 0) want.r0 = b->roles[i];
       if (hd.nroles > 1) want.r1 = b->roles[n + i];
-      if (!(hd.flags & (RQ_HOST | RQ_NO_TARGET))) {
+      if (live) {
         want.ar0 = ar[0];
         want.ar1 = ar[1];
       }
+      want.ext = lines[i].ext;  // (an SoA batch reads its rows, not extension records)
       if (std::memcmp(&want, &lines[i], sizeof want) != 0) return bad("batch: request line differs from its rows", i);
     }
+    auto res_at = [&](uint32_t j) -> ReqRes {
+      if (!compact) return res[(size_t)j * n + i];
+      if (j < (uint32_t)LINE_RES) return lines[i].res[j];
+      ReqRes q;
+      std::memcpy(&q, ex + 4 * (j - LINE_RES), sizeof q);
+      return q;
+    };
     const uint32_t c0 = ar[0], c1 = ar[1];
     const uint32_t ng = c0 & 0xFF, nre = (c0 >> 8) & 0xFF, ns = (c0 >> 16) & 0xFF, nro = c0 >> 24;
     const uint32_t nt = c1 & 0xFF, nh = (c1 >> 8) & 0xFF;
@@ -159,9 +186,10 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
     }
     const uint32_t ent = (hd.flags >> RQ_ENT_SHIFT) & 7u;
     const uint32_t e0 = ent >= 1 && ent <= 6 ? ent - 1 : (uint32_t)QMAX;  // the lone entity attr's slot
+    if (compact && e0 < QMAX && e0 >= hd.nres) return bad("batch: entity slot", i);
     for (uint32_t j = 0; j < QMAX; ++j) {
       if (j >= hd.nres && j != e0) continue;
-      const ReqRes q = res[(size_t)j * n + i];
+      const ReqRes q = res_at(j);
       if (rx_rows_min && ((q.kind & K_ENT_LOOSE) || j == e0) && q.col >= b->rx_cols)
         return bad("batch: regex matrix column", i);
       if (!col_unsafe.empty() && (q.kind & K_ENT_LOOSE) && (q.pad & RES_RX_SAFE) && col_unsafe[q.col])

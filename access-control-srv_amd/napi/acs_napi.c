@@ -27,8 +27,9 @@
  *   wordsPerRequest(tables), layoutSizes(), deviceCount(), lastError()
  * `batch` = an encode() handle, or a plain object {n, hdr, res, subj, act, roles, arena,
  * rx, rxCols, rxRows, cand, candWords, candWp, candWr, candRows[, candWsu, candWpu, candWv, roleKey, roleRowsBits,
- * roleRows]} of typed arrays in the layout of csrc/acs_layout.h; every array is checked
- * against the sizes `n` and the counts imply before the library reads it.
+ * roleRows, lines]} of typed arrays in the layout of csrc/acs_layout.h — or, compact, {n, lines,
+ * ext, arena, rx, ...} without the SoA rows; every array is checked against the sizes `n` and
+ * the counts imply before the library reads it.
  *
  * Handles are plain objects naming a per-environment registry slot (see "handles" below:
  * no napi externals, whose weak references Node 12 can touch after freeing them at exit).
@@ -55,7 +56,7 @@
   } while (0)
 
 /* csrc/acs_layout.h sizes (checked against acs_layout_sizes by tests/test_napi.py) */
-enum { HDR_B = 16, RES_B = 16, PAIR_B = 8, QMAX = 16, SMAX = 8, AMAX = 4, RMAX = 8 };
+enum { HDR_B = 16, RES_B = 16, PAIR_B = 8, LINE_B = 128, QMAX = 16, SMAX = 8, AMAX = 4, RMAX = 8 };
 
 static napi_value throw_acs(napi_env env, const char* what) {
   char msg[512];
@@ -355,7 +356,7 @@ static int field(napi_env env, napi_value obj, const char* key, size_t need, int
     *bad = key;
     return -1;
   }
-  if ((required && need && !p) || len < need) {
+  if ((required && need && !p) || (p && len < need)) {  /* an absent optional field is fine */
     *bad = key;
     return -1;
   }
@@ -383,13 +384,27 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
       prop_u32(env, v, "roleRows", &b->role_rows) || prop_u32(env, v, "candWsu", &b->cand_wsu) ||
       prop_u32(env, v, "candWpu", &b->cand_wpu) || prop_u32(env, v, "candWv", &b->cand_wv))
     return -1;
-  if (field(env, v, "hdr", n * HDR_B, n > 0, &b->hdr, NULL, &bad) ||
-      field(env, v, "res", n * QMAX * RES_B, n > 0, &b->res, NULL, &bad) ||
-      field(env, v, "subj", n * SMAX * PAIR_B, n > 0, &b->subj, NULL, &bad) ||
-      field(env, v, "act", n * AMAX * PAIR_B, n > 0, &b->act, NULL, &bad) ||
-      field(env, v, "roles", n * RMAX * 4, n > 0, &p, NULL, &bad))
-    goto fail;
-  b->roles = (const uint32_t*)p;
+  /* compact batch (csrc/acs_layout.h): lines + ext, no SoA rows */
+  if (field(env, v, "lines", n * LINE_B, 0, &b->lines, NULL, &bad)) goto fail;
+  {
+    napi_value hv;
+    napi_valuetype ht;
+    const int compact = napi_get_named_property(env, v, "hdr", &hv) == napi_ok && napi_typeof(env, hv, &ht) == napi_ok &&
+                        (ht == napi_undefined || ht == napi_null) && b->lines;
+    if (compact) {
+      if (field(env, v, "ext", 0, 0, &p, &len, &bad)) goto fail;
+      b->ext = (const uint32_t*)p;
+      b->ext_words = len / 4;
+    } else {
+      if (field(env, v, "hdr", n * HDR_B, n > 0, &b->hdr, NULL, &bad) ||
+          field(env, v, "res", n * QMAX * RES_B, n > 0, &b->res, NULL, &bad) ||
+          field(env, v, "subj", n * SMAX * PAIR_B, n > 0, &b->subj, NULL, &bad) ||
+          field(env, v, "act", n * AMAX * PAIR_B, n > 0, &b->act, NULL, &bad) ||
+          field(env, v, "roles", n * RMAX * 4, n > 0, &p, NULL, &bad))
+        goto fail;
+      b->roles = (const uint32_t*)p;
+    }
+  }
   if (field(env, v, "arena", 0, 0, &p, &len, &bad)) goto fail;
   b->arena = (const uint32_t*)p;
   b->arena_words = len / 4;
@@ -418,18 +433,19 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
   } else {
     b->role_rows = 0;
   }
-  /* per-request offsets the kernels follow */
+  /* per-request offsets the kernels follow (the library checks everything again) */
   {
-    const uint8_t* hdr = (const uint8_t*)b->hdr;
+    const uint8_t* hdr = b->hdr ? (const uint8_t*)b->hdr : (const uint8_t*)b->lines;
+    const size_t stride = b->hdr ? HDR_B : LINE_B;
     for (size_t i = 0; i < n; ++i) {
       uint32_t arena_off;
-      memcpy(&arena_off, hdr + i * HDR_B + 8, 4);
+      memcpy(&arena_off, hdr + i * stride + 8, 4);
       if ((size_t)arena_off + 2 > b->arena_words) {
         bad = "hdr.arena_off";
         goto fail;
       }
-      if (hdr[i * HDR_B + 4] > QMAX || hdr[i * HDR_B + 5] > SMAX || hdr[i * HDR_B + 6] > AMAX ||
-          hdr[i * HDR_B + 7] > RMAX) {
+      if (hdr[i * stride + 4] > QMAX || hdr[i * stride + 5] > SMAX || hdr[i * stride + 6] > AMAX ||
+          hdr[i * stride + 7] > RMAX) {
         bad = "hdr counts";
         goto fail;
       }
@@ -675,10 +691,12 @@ static napi_value host_map(napi_env env, acs_codec_batch* b, uint32_t n) {
   if (napi_create_object(env, &host) != napi_ok) return NULL;
   acs_req_batch view;
   if (acs_codec_batch_view(b, &view) != 0) return host;
-  const uint8_t* hdr = (const uint8_t*)view.hdr;
+  /* the header is the first 16 B of each 128-B request line (csrc/acs_layout.h ReqLine) */
+  const uint8_t* hdr = view.hdr ? (const uint8_t*)view.hdr : (const uint8_t*)view.lines;
+  const size_t stride = view.hdr ? HDR_B : LINE_B;
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t flags;
-    memcpy(&flags, hdr + (size_t)i * HDR_B, 4);
+    memcpy(&flags, hdr + (size_t)i * stride, 4);
     if (!(flags & ACS_RQ_HOST)) continue;
     const char* why = acs_codec_batch_reason(b, i);
     char key[16];

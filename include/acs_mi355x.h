@@ -39,9 +39,10 @@ typedef struct {
 
 typedef struct acs_tables acs_tables; /* device-resident tables, immutable once built */
 
-/* One request batch in the packed SoA layout of csrc/acs_layout.h.  The same
- * struct describes host buffers (acs_is_allowed) or device buffers
- * (acs_is_allowed_device). */
+/* One request batch in the packed layout of csrc/acs_layout.h: SoA rows (+ optional request
+ * lines), or compact (request lines + extension records, the native codec's form: about
+ * 220 B per request instead of 620).  The same struct describes host buffers
+ * (acs_is_allowed) or device buffers (acs_is_allowed_device). */
 typedef struct {
   uint32_t n;
   const void* hdr;     /* [n] ReqHdr                         */
@@ -72,11 +73,16 @@ typedef struct {
   const uint32_t* role_key;
   const uint32_t* role_rows_bits;
   uint32_t role_rows;
-  /* Optional [n] 128-B ReqLine (csrc/acs_layout.h): each request's header, first 4 resource
-   * attributes, 2 subjects, action, 2 roles and arena counts in one line, equal to the SoA
-   * rows above (checked by the host entry points).  The evaluation kernel then reads a
-   * request with one gather instead of ~8.  NULL = read the SoA rows. */
+  /* [n] 128-B ReqLine (csrc/acs_layout.h): each request's header, first 4 resource
+   * attributes, 2 subjects, action, 2 roles and arena counts in one line, so the evaluation
+   * kernel reads a request with one gather instead of ~8.  With the SoA rows above: optional,
+   * equal to them (checked by the host entry points).  Compact batch (hdr, res, subj, act,
+   * roles all NULL): required, and the rows past the line live in `ext`. */
   const void* lines;
+  /* Compact batches: the requests' extension records (ReqLine.ext; acs_layout.h ext_geom),
+   * u32 words.  May be NULL when no request needs one. */
+  const uint32_t* ext;
+  size_t ext_words;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */
@@ -192,8 +198,13 @@ float acs_last_kernel_ms(const acs_tables* t);
  *   per-subject cache createHRScope fills from Redis, accessController.ts:735-783;
  *   acs_codec_evict_subject = evictHRScopes, :717-725).
  * acs_codec_batch_view: the batch's host buffers as an acs_req_batch (valid until
- *   acs_codec_batch_free), for acs_is_allowed / acs_what_is_allowed or a device upload.
- *   A batch refers to its codec's dictionary: free batches before their codec.
+ *   acs_codec_batch_free), for acs_is_allowed / acs_what_is_allowed or a device upload: the
+ *   compact form (request lines + extension records + arena + regex matrix + class rows, in
+ *   page-locked memory when a device is present), plus the SoA rows once
+ *   acs_codec_batch_expand materialised them.  A batch refers to its codec's dictionary and
+ *   buffer pool: free batches before their codec.
+ * Candidate-class rows are cached per codec across batches (a steady request stream computes
+ *   each class row once).
  * acs_codec_string: interned id -> string (0 undefined, 1 null, 2 string; -1 unknown), e.g.
  *   for maskedProperty obligation ids. */
 /* Replaces: the Map -> table snapshot step (acs_mi355x/compiler.py, in C++: csrc/acs_compiler.cpp)
@@ -215,12 +226,17 @@ int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, 
 int acs_codec_evict_subject(acs_codec* c, const char* key, size_t key_len);
 acs_codec_batch* acs_codec_encode(acs_codec* c, const char* json, size_t len, int threads);
 int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out);
+/* Materialise the SoA rows (hdr / res / subj / act / roles) of an encoded batch, for consumers
+ * of that layout (the CPU build of the evaluator core, tests); acs_codec_batch_view then
+ * returns them beside the compact arrays. */
+int acs_codec_batch_expand(acs_codec_batch* b);
 const char* acs_codec_batch_reason(const acs_codec_batch* b, uint32_t i);
 int acs_codec_string(const acs_codec_batch* b, uint32_t id, const char** s, size_t* len);
 /* The evaluation_cacheable values of the store beyond codes 0..3 (undefined, null, false,
  * true), as a JSON array: code k >= 4 is element k - 4 (acs_decision.ec). */
 int acs_codec_ec_values(const acs_codec* c, const char** json, size_t* len);
-/* out[0..5]: seconds parse+encode, regex matrix, candidate classes, total; HR cache hits, misses */
+/* out[0..7]: seconds parse+encode, regex matrix + assembly, candidate classes, total; HR cache
+ * hits, misses; class rows computed by this batch (not served by the codec's cache), classes */
 int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n);
 void acs_codec_batch_free(acs_codec_batch* b);
 

@@ -8,7 +8,7 @@ import numpy as np
 from acs_mi355x import layout as L
 from acs_mi355x.build import build_host_core
 from acs_mi355x.compiler import store_blob
-from acs_mi355x.native import ReqBatchC, ShardC, batch_struct
+from acs_mi355x.native import ReqBatchC, ShardC, batch_struct, host_struct
 
 _LIB = None
 
@@ -45,15 +45,21 @@ def shard_decode(keys):
     return out
 
 
-def is_allowed(cs, batch):
+def _struct(batch, compact):
+    """compact: the batch's compact form (a CodecBatch's own view; a RequestBatch's lines +
+    extension records), else its SoA rows (+ lines)."""
+    return host_struct(batch, True) if compact else batch_struct(batch)
+
+
+def is_allowed(cs, batch, compact=False):
     blob = store_blob(cs)
     out = np.zeros(batch.n, L.DECISION_DT)
-    s = batch_struct(batch)
+    s = _struct(batch, compact)
     assert lib().acs_host_is_allowed(blob, len(blob), C.byref(s), out.ctypes.data) == 0
     return out
 
 
-def what_is_allowed(cs, batch):
+def what_is_allowed(cs, batch, compact=False):
     from acs_mi355x.results import bits_layout
     blob = store_blob(cs)
     words = bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)[2]
@@ -62,7 +68,7 @@ def what_is_allowed(cs, batch):
     obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)
     obl_n = np.zeros(n, np.uint32)
     out = np.zeros(n, L.DECISION_DT)
-    s = batch_struct(batch)
+    s = _struct(batch, compact)
     assert lib().acs_host_what_is_allowed(blob, len(blob), C.byref(s), bits.ctypes.data, obl.ctypes.data,
                                           obl_n.ctypes.data, out.ctypes.data) == 0
     return bits, obl, obl_n, out

@@ -62,7 +62,11 @@ static Batch host_batch(const acs_req_batch* b) {
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
-  const char* no_cut = getenv("ACS_NO_CUT");  // as the product library (acs_kernels.hip: to_batch)
+  B.lines = (const ReqLine*)b->lines;  // a compact batch reads its lines + extension records
+  B.ext = b->ext;
+  // cut-invariance tests (tests/test_cut.py): ACS_NO_CUT=1 in this test build only; the product
+  // library fixes it at compile time (ACS_AB_NO_CUT)
+  const char* no_cut = getenv("ACS_NO_CUT");
   B.no_cut = no_cut && *no_cut == '1' ? 1u : 0u;
   return B;
 }
@@ -129,7 +133,7 @@ extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const ac
       const uint32_t i = idx[j];
       if (i >= B.n) return -1;
       const size_t k = (size_t)c * m + j;
-      const ReqHdr h = B.hdr[i];
+      const ReqHdr h = req_hdr(B, i);
       OblLog log{obl + k * 2 * (size_t)cap, 0, false, cap, 0};
       uint32_t total = 0;
       if (!(h.flags & RQ_HOST)) {
@@ -137,7 +141,8 @@ extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const ac
         const uint32_t s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
         NullSink none;
         const Decision d =
-            what_is_allowed_t(ReqMem(T, B, i, h), request_filter(B, h, i), BitsLayout{}, none, log, s0, s1);
+            what_is_allowed_t(ReqMem(T, B, i, h, req_line(B, i)), request_filter(B, h, i), BitsLayout{}, none, log, s0,
+                              s1);
         total = (d.flags & OF_ERR) ? 0u : log.total;
       }
       obl_n[k] = total;

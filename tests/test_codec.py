@@ -61,15 +61,20 @@ def compare_batches(pb, nb, check_cols=True):
         # context arena: same length per request (contents hold batch-local ids)
     if check_cols:
         assert pb.rx.shape == nb.rx.shape and np.array_equal(pb.rx, nb.rx)
-    # packed request lines: both encoders emit exactly the lines of their own rows
+    # packed request lines + extension records: both encoders emit exactly those of their own rows
     for x in (pb, nb):
         assert x.lines is not None
         assert x.lines.tobytes() == encoder.pack_lines(x).tobytes()
+        assert x.ext.tobytes() == encoder.pack_ext(x).tobytes()
 
 
 def decisions_equal(cs, pb, nb):
-    a, b = host_core.is_allowed(cs, pb), host_core.is_allowed(cs, nb)
+    """The Python batch (SoA and compact) and the codec batch (its own compact form and its
+    expanded SoA rows) decide identically on the CPU build of the core."""
+    a, b = host_core.is_allowed(cs, pb), host_core.is_allowed(cs, nb, compact=True)
     assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    assert np.array_equal(a.view(np.uint64), host_core.is_allowed(cs, pb, compact=True).view(np.uint64))
+    assert np.array_equal(a.view(np.uint64), host_core.is_allowed(cs, nb).view(np.uint64))
     return b
 
 
