@@ -201,3 +201,50 @@ class NativeCodec:
             self.close()
         except Exception:
             pass
+
+
+class PipelineStats(C.Structure):
+    _fields_ = [("encode_s", C.c_double), ("wait_s", C.c_double), ("total_s", C.c_double), ("gpu_ms", C.c_double),
+                ("upload_bytes", C.c_double), ("requests", C.c_uint64), ("chunks", C.c_uint64),
+                ("host_requests", C.c_uint64)]
+
+
+class Pipeline:
+    """acs_pipeline (include/acs_mi355x.h): JSON request text -> decision records, encode of
+    chunk k+1 overlapped with the device work of chunk k (two streams, page-locked buffers)."""
+
+    def __init__(self, tables, codec: NativeCodec, threads: int = 16, chunk: int = 131072):
+        lib = tables.lib
+        lib.acs_pipeline_create.restype = C.c_void_p
+        lib.acs_pipeline_create.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_uint32]
+        lib.acs_pipeline_free.argtypes = [C.c_void_p]
+        lib.acs_pipeline_free.restype = None
+        lib.acs_pipeline_is_allowed.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                                C.POINTER(C.c_size_t), C.POINTER(PipelineStats)]
+        self.lib, self._tables, self._codec = lib, tables, codec  # both must outlive the pipeline
+        self.h = lib.acs_pipeline_create(tables.h, codec.h, int(threads), int(chunk))
+        if not self.h:
+            raise RuntimeError(last_error(lib))
+
+    def is_allowed(self, text: bytes, capacity: int):
+        """(records [n] DECISION_DT, stats dict) for the JSON array `text` (at most `capacity`
+        requests)."""
+        out = np.zeros(capacity, L.DECISION_DT)
+        n = C.c_size_t(0)
+        st = PipelineStats()
+        if self.lib.acs_pipeline_is_allowed(self.h, text, len(text), out.ctypes.data, capacity, C.byref(n),
+                                            C.byref(st)) != 0:
+            raise RuntimeError(last_error(self.lib))
+        stats = {k: getattr(st, k) for k, _ in PipelineStats._fields_}
+        return out[:n.value], stats
+
+    def close(self):
+        if self.h:
+            self.lib.acs_pipeline_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -2231,15 +2231,27 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+using Items = std::vector<std::pair<const char*, const char*>>;
+
+acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const char*>* items, size_t count,
+                              int threads, double t0);
+
 acs_codec_batch* encode_batch(acs_codec* c, const char* json, size_t len, int threads) {
   const double t0 = now_s();
+  const int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+  const Items items = split_items(json, json + len, T);
+  return encode_items(c, items.data(), items.size(), T, t0);
+}
+
+// Encode the requests items[0..count) (delimited JSON values) into one batch.
+acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const char*>* items, size_t count,
+                              int threads, double t0) {
   auto B = std::make_unique<acs_codec_batch>();
   B->codec = c;
   B->pool = c->pool;
   int T = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
-  const auto items = split_items(json, json + len, T);
-  const uint32_t n = (uint32_t)items.size();
-  if (items.size() > 0xFFFFFFFull) throw ParseError{"requests: batch too large"};
+  const uint32_t n = (uint32_t)count;
+  if (count > 0xFFFFFFFull) throw ParseError{"requests: batch too large"};
   B->n = n;
   B->lines_b = c->pool->acquire((size_t)n * sizeof(ReqLine));
   B->lines = (ReqLine*)B->lines_b.p;
@@ -2457,6 +2469,41 @@ int acs_internal_codec_cycles(uint64_t* parse, uint64_t* encode) {
   return 0;
 }
 #endif
+
+// Pipeline support (acs_kernels.hip acs_pipeline_*, not in include/acs_mi355x.h): delimit the
+// request array once, then encode it chunk by chunk.
+struct acs_internal_items {
+  std::vector<std::pair<const char*, const char*>> v;
+};
+acs_internal_items* acs_internal_split(const char* json, size_t len, int threads, size_t* n) {
+  try {
+    auto it = std::make_unique<acs_internal_items>();
+    it->v = split_items(json, json + len, threads < 1 ? 1 : (threads > 64 ? 64 : threads));
+    *n = it->v.size();
+    return it.release();
+  } catch (const ParseError& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what;
+  } catch (const std::exception& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what();
+  }
+  acs_internal_set_error(g_codec_err.c_str());
+  return nullptr;
+}
+void acs_internal_items_free(acs_internal_items* it) { delete it; }
+acs_codec_batch* acs_internal_encode_range(acs_codec* c, const acs_internal_items* it, size_t lo, size_t hi,
+                                           int threads) {
+  try {
+    return encode_items(c, it->v.data() + lo, hi - lo, threads, now_s());
+  } catch (const ParseError& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what;
+  } catch (const Unsup& u) {
+    g_codec_err = std::string("acs_codec_encode: ") + u.why;
+  } catch (const std::exception& e) {
+    g_codec_err = std::string("acs_codec_encode: ") + e.what();
+  }
+  acs_internal_set_error(g_codec_err.c_str());
+  return nullptr;
+}
 
 // Test hook (not in include/acs_mi355x.h): pin the candidate-class key level of every later
 // encode (0 entity+roles+action, 1 entity+action, 2 entity; -1 automatic).

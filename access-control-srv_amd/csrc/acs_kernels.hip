@@ -10,6 +10,7 @@
 //                             (class, low) keys -> the permutation K1 / K2 run in.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1161,5 +1162,178 @@ int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_
   HIP_OK(hipStreamSynchronize(t->stream));
   return 0;
 }
+
+// ---------------------------------------------------------------- decision pipeline
+// JSON text -> decision records with encode and device work overlapped: the request array is
+// delimited once, then cut into chunks; chunk k+1 is encoded on the host threads while chunk
+// k's upload (from the codec's page-locked blocks), coherence sort, K1 and download run on
+// one of two streams, each with its own device workspace and page-locked output staging.
+struct acs_internal_items;
+acs_internal_items* acs_internal_split(const char* json, size_t len, int threads, size_t* n);
+void acs_internal_items_free(acs_internal_items* it);
+acs_codec_batch* acs_internal_encode_range(acs_codec* c, const acs_internal_items* it, size_t lo, size_t hi,
+                                           int threads);
+
+}  // extern "C"
+
+struct acs_pipeline {
+  acs_tables* t = nullptr;
+  acs_codec* c = nullptr;
+  int threads = 1;
+  uint32_t chunk = 131072;
+  struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
+    Workspace ws;
+    acs_decision* stage = nullptr;  // page-locked output staging
+    size_t stage_n = 0;
+    acs_codec_batch* batch = nullptr;  // in flight
+    size_t lo = 0, n = 0;              // its requests
+    bool busy = false;
+  } slot[2];
+  std::mutex mu;  // one run at a time per pipeline
+};
+
+namespace {
+
+// Finish slot S: wait for its chunk, copy its records out, free its batch.
+int pipeline_retire(acs_pipeline* p, acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats* st) {
+  if (!S.busy) return 0;
+  const double w0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  HIP_OK(hipEventSynchronize(S.done));
+  const double w1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+  std::memcpy(out + S.lo, S.stage, S.n * sizeof(acs_decision));
+  if (st) {
+    st->wait_s += w1 - w0;
+    st->gpu_ms += ms;
+    for (size_t i = 0; i < S.n; ++i) st->host_requests += (S.stage[i].flags & ACS_OF_HOST_REQ) ? 1u : 0u;
+  }
+  acs_codec_batch_free(S.batch);
+  S.batch = nullptr;
+  S.busy = false;
+  (void)p;
+  return 0;
+}
+
+double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+extern "C" {
+
+acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint32_t chunk) {
+  if (!t || !c) {
+    fail("acs_pipeline_create: null argument");
+    return nullptr;
+  }
+  auto p = new acs_pipeline();
+  p->t = t;
+  p->c = c;
+  p->threads = threads < 1 ? 1 : threads;
+  p->chunk = chunk ? chunk : 131072;
+  if (hipSetDevice(t->device) != hipSuccess) {
+    fail("acs_pipeline_create: hipSetDevice failed");
+    delete p;
+    return nullptr;
+  }
+  for (auto& S : p->slot)
+    if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&S.ev0) != hipSuccess || hipEventCreate(&S.ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
+      fail("acs_pipeline_create: stream / event creation failed");
+      acs_pipeline_free(p);
+      return nullptr;
+    }
+  return p;
+}
+
+void acs_pipeline_free(acs_pipeline* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->t->device);
+  for (auto& S : p->slot) {
+    if (S.busy) (void)hipEventSynchronize(S.done);
+    if (S.batch) acs_codec_batch_free(S.batch);
+    S.ws.release();
+    if (S.stage) (void)hipHostFree(S.stage);
+    if (S.ev0) (void)hipEventDestroy(S.ev0);
+    if (S.ev1) (void)hipEventDestroy(S.ev1);
+    if (S.done) (void)hipEventDestroy(S.done);
+    if (S.stream) (void)hipStreamDestroy(S.stream);
+  }
+  delete p;
+}
+
+int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_decision* out, size_t out_cap,
+                            size_t* n_out, acs_pipeline_stats* st) {
+  if (!p || (!json && len) || !n_out) return fail("acs_pipeline_is_allowed: null argument");
+  std::lock_guard<std::mutex> lock(p->mu);
+  if (st) *st = acs_pipeline_stats{};
+  const double t0 = steady_s();
+  size_t n = 0;
+  acs_internal_items* items = acs_internal_split(json, len, p->threads, &n);
+  if (!items) return -1;
+  *n_out = n;
+  struct Free {
+    acs_internal_items* it;
+    ~Free() { acs_internal_items_free(it); }
+  } free_items{items};
+  if (n > out_cap || (n && !out)) return fail("acs_pipeline_is_allowed: output holds fewer records than the requests");
+  HIP_OK(hipSetDevice(p->t->device));
+  int k = 0;
+  for (size_t lo = 0; lo < n; lo += p->chunk, ++k) {
+    const size_t hi = lo + p->chunk < n ? lo + p->chunk : n;
+    const double e0 = steady_s();
+    acs_codec_batch* b = acs_internal_encode_range(p->c, items, lo, hi, p->threads);
+    if (!b) return -1;
+    if (st) st->encode_s += steady_s() - e0;
+    acs_pipeline::Slot& S = p->slot[k & 1];
+    if (pipeline_retire(p, S, out, st)) {  // the chunk two back
+      acs_codec_batch_free(b);
+      return -1;
+    }
+    S.batch = b;
+    S.lo = lo;
+    S.n = hi - lo;
+    acs_req_batch view;
+    if (acs_codec_batch_view(b, &view) || check_batch(p->t, &view)) return -1;
+    if (S.stage_n < S.n) {
+      if (S.stage) HIP_OK(hipHostFree(S.stage));
+      S.stage = nullptr;
+      S.stage_n = 0;
+      HIP_OK(hipHostMalloc((void**)&S.stage, S.n * sizeof(acs_decision), hipHostMallocPortable));
+      S.stage_n = S.n;
+    }
+    {
+      std::lock_guard<std::mutex> tl(p->t->mu);  // the handle's launch bookkeeping
+      acs_req_batch d;
+      HIP_OK(hipEventRecord(S.ev0, S.stream));
+      if (upload_batch(S.ws, &view, &d, S.stream)) return -1;
+      if (S.ws.out.reserve(S.n * sizeof(Decision))) return -1;
+      if (is_allowed_launch(p->t, S.ws, &d, (acs_decision*)S.ws.out.p, S.stream)) return -1;
+      HIP_OK(hipMemcpyAsync(S.stage, S.ws.out.p, S.n * sizeof(Decision), hipMemcpyDeviceToHost, S.stream));
+      HIP_OK(hipEventRecord(S.ev1, S.stream));
+      HIP_OK(hipEventRecord(S.done, S.stream));
+    }
+    S.busy = true;
+    if (st) {
+      st->chunks += 1;
+      st->upload_bytes += (double)(S.n * sizeof(ReqLine) + view.ext_words * 4 + view.arena_words * 4 +
+                                   (size_t)view.rx_cols * view.rx_rows +
+                                   (size_t)view.cand_rows * view.cand_words * 4);
+    }
+  }
+  for (auto& S : p->slot)
+    if (pipeline_retire(p, S, out, st)) return -1;
+  if (st) {
+    st->requests = n;
+    st->total_s = steady_s() - t0;
+  }
+  return 0;
+}
+
 
 }  // extern "C"

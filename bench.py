@@ -239,15 +239,21 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
 
 
 def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
-    """JSON -> decision: the native codec (csrc/acs_codec.cpp) encodes the JSON text of the
-    first n_e2e requests of the timed batch on `threads` host threads, then acs_is_allowed
-    (H2D + sort + K1 + D2H) decides them.  c3 subjects name their HR forests by reference
-    ("$hrs": the per-subject cache of acs_codec, registered once before timing, as the
-    reference's Redis HR cache is warm in steady state).  The records must equal those of
-    the resident (synthetic-packed) path bit for bit."""
+    """JSON -> decision, the product path: the JSON text of the first n_e2e requests of the
+    timed batch through acs_pipeline (csrc/acs_kernels.hip) — the request array delimited on
+    `threads` host threads, then chunk k+1 encoded by the native codec (csrc/acs_codec.cpp) on
+    those threads while chunk k is uploaded from the codec's page-locked blocks, sorted, decided
+    by K1 and downloaded on a second stream.  c3 subjects name their HR forests by reference
+    ("$hrs": the per-subject cache, registered once before timing, as the reference's Redis HR
+    cache is warm in steady state); one untimed run warms the codec's caches (HR forests,
+    candidate-class rows, page-locked blocks), as a service's steady state has them.  The
+    records must equal those of the resident (synthetic-packed) path bit for bit.  Also
+    reported: the same requests encoded in one call, then decided (no overlap), and the share
+    of a steady-state encode spent on candidate classes."""
     from acs_mi355x import compiler
-    from acs_mi355x.codec import NativeCodec
+    from acs_mi355x.codec import NativeCodec, Pipeline
     idx = np.arange(min(n_e2e, sb.batch.n))
+    n = len(idx)
     t0 = time.perf_counter()
     text = sb.json_text(idx)
     gen_s = time.perf_counter() - t0
@@ -257,29 +263,62 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
         for k, v in sb.hrs_forests(idx).items():
             codec.set_subject_scopes(k, v)
             registered += 1
-    codec.encode(text, threads=threads).close()  # warm: arenas, regex / entity / action caches
+    pipe = Pipeline(tables, codec, threads=threads, chunk=131072)
+    pipe.is_allowed(text, n)  # warm: HR forests, class rows, regex columns, page-locked blocks
+    dec, st = pipe.is_allowed(text, n)
+    same = bool(np.array_equal(dec.view(np.uint64), dec_resident[idx].view(np.uint64)))
+    pipe.close()
+    # sequential: one encode call, then acs_is_allowed on its (compact, page-locked) buffers
     t0 = time.perf_counter()
     b = codec.encode(text, threads=threads)
     t1 = time.perf_counter()
-    dec = tables.is_allowed(b)
+    dec2 = tables.is_allowed(b)
     t2 = time.perf_counter()
-    st = b.stats()
-    same = bool(np.array_equal(dec.view(np.uint64), dec_resident[idx].view(np.uint64)))
-    host = int(((dec["flags"] & 0x04) != 0).sum())
+    bst = b.stats()
+    wire = b.nbytes()
+    same = same and bool(np.array_equal(dec2.view(np.uint64), dec_resident[idx].view(np.uint64)))
     b.close()
     codec.close()
-    n = len(idx)
     return {"requests": n, "json_bytes": len(text), "json_bytes_per_request": len(text) / n,
-            "json_generation_s": gen_s,
-            "encode": {"requests_per_s": n / (t1 - t0), "cores": threads, "seconds": t1 - t0,
-                       "parts_s": {k: st[k] for k in ("encode_s", "regex_s", "classes_s")},
-                       "hr_forests_registered": registered, "hr_cache_hits": st["hr_cache_hits"],
-                       "hr_cache_misses": st["hr_cache_misses"]},
-            "gpu_host_buffers_s": t2 - t1,
-            "end_to_end": {"requests_per_s": n / (t2 - t0),
-                           "what": "JSON text -> acs_codec_encode -> acs_is_allowed (H2D, sort, K1, D2H) -> "
-                                   "decision records in host memory, sequential (no overlap)"},
-            "host_path_requests": host, "identical_to_resident_path": same}
+            "json_generation_s": gen_s, "threads": threads,
+            "requests_per_s": n / st["total_s"],
+            "what": "JSON text -> acs_pipeline (delimit; per 131072-request chunk: native encode into page-locked "
+                    "blocks || upload + coherence sort + K1 + download of the previous chunk on a second stream) -> "
+                    "decision records in host memory; codec caches warm (steady state)",
+            "stages": {"total_s": st["total_s"], "encode_s": st["encode_s"], "device_wait_s": st["wait_s"],
+                       "device_ms": st["gpu_ms"], "chunks": int(st["chunks"]),
+                       "upload_bytes_per_request": st["upload_bytes"] / n,
+                       "host_path_requests": int(st["host_requests"])},
+            "sequential": {"requests_per_s": n / (t2 - t0), "encode_s": t1 - t0, "decide_s": t2 - t1,
+                           "encode_parts_s": {k: bst[k] for k in ("encode_s", "regex_s", "classes_s")},
+                           "class_share_of_encode": bst["classes_s"] / max(bst["total_s"], 1e-9),
+                           "classes": bst["classes"], "classes_computed": bst["classes_new"],
+                           "wire_bytes_per_request": wire / n,
+                           "hr_forests_registered": registered, "hr_cache_hits": bst["hr_cache_hits"],
+                           "hr_cache_misses": bst["hr_cache_misses"]},
+            "identical_to_resident_path": same}
+
+
+def pinned_compact(batch):
+    """The batch's compact arrays (lines, extension records, arena, regex matrix, class rows)
+    copied into page-locked host memory (torch pin_memory), as the native codec leaves them:
+    what a service hands to acs_is_allowed."""
+    import types
+    out = types.SimpleNamespace(n=batch.n, rx_rows=batch.rx_rows, cand_wp=batch.cand_wp, cand_wr=batch.cand_wr,
+                                cand_wsu=batch.cand_wsu, cand_wpu=batch.cand_wpu, cand_wv=batch.cand_wv)
+    keep = []
+    for k in ("lines", "ext", "arena", "rx", "cand", "role_key", "role_bits"):
+        a = getattr(batch, k)
+        if a is None:
+            setattr(out, k, None)
+            continue
+        t = torch.empty(max(a.nbytes, 16), dtype=torch.uint8, pin_memory=True)
+        v = t.numpy()[:a.nbytes].view(a.dtype).reshape(a.shape)
+        v[...] = a
+        keep.append(t)
+        setattr(out, k, v)
+    out._keep = keep
+    return out
 
 
 def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev, dist):
@@ -299,7 +338,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     blob = compiler.store_blob(cs)
     tables = native.Tables(blob, local)
     tables.set_timing(True)
-    db = DeviceBatch(sb.batch, local)
+    db = DeviceBatch(sb.batch, local, compact=True)  # the product form: request lines + extension records
     stream = torch.cuda.current_stream(dev)
     bufs = what_is_allowed_device(tables, db, None, stream)
 
@@ -478,7 +517,7 @@ def main():
     tables = native.Tables(blob, local)
     tables.set_sort(not args.no_sort)
     tables.set_timing(True)
-    db = DeviceBatch(sb.batch, local)
+    db = DeviceBatch(sb.batch, local, compact=True)  # the product form: request lines + extension records
     out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     if args.rule_shard:
@@ -533,13 +572,19 @@ def main():
                        "identical_to_unsharded": bool(np.array_equal(want.view(np.uint64), dec.view(np.uint64)))}
     pcie = None
     if rank == 0 and not args.no_pcie and not args.rule_shard:
-        # host buffers through acs_is_allowed: H2D + sort + K1 + D2H (reported beside, never `value`)
-        tables.is_allowed(sb.batch)
+        # host buffers through acs_is_allowed: H2D + sort + K1 + D2H (reported beside, never
+        # `value`), from the compact form in page-locked memory, as the codec leaves a batch
+        hb = pinned_compact(sb.batch)
+        tables.is_allowed(hb, compact=True)
         t1 = time.perf_counter()
-        host_dec = tables.is_allowed(sb.batch)
+        host_dec = tables.is_allowed(hb, compact=True)
         pcie_s = time.perf_counter() - t1
-        pcie = {"value": n / pcie_s, "unit": "decisions/s", "ms": pcie_s * 1e3, "input_bytes": int(sb.batch.nbytes()),
+        pcie = {"value": n / pcie_s, "unit": "decisions/s", "ms": pcie_s * 1e3,
+                "input_bytes": int(sb.batch.compact_nbytes()),
+                "input": "compact batch (request lines + extension records + arena + regex matrix + class rows) "
+                         "in page-locked host memory",
                 "identical_to_device_path": bool(np.array_equal(host_dec.view(np.uint64), dec.view(np.uint64)))}
+        del hb
     if rank == 0:
         log("counting algorithmic bytes")
         per_dec, parts = algorithmic_bytes(cs, sb.batch, measured_scan_bytes(blob, db, local))

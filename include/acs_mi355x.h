@@ -240,6 +240,30 @@ int acs_codec_ec_values(const acs_codec* c, const char** json, size_t* len);
 int acs_codec_batch_stats(const acs_codec_batch* b, double* out, int n);
 void acs_codec_batch_free(acs_codec_batch* b);
 
+/* ------------------------------------------------------------------ decision pipeline
+ * Replaces: the reference's per-request evaluation behind AccessControlService.isAllowed
+ * (accessControlService.ts:62-81 -> accessController.ts:88-324) for a micro-batch of requests
+ * arriving as JSON text, end to end: the request array is delimited once and cut into chunks
+ * of `chunk` requests; chunk k+1 is encoded (acs_codec) on `threads` host threads while chunk
+ * k is uploaded from the codec's page-locked blocks, sorted and decided (K1) and its records
+ * downloaded, on one of the pipeline's two streams (each with its own device workspace).
+ * out[0..n) receives the records in request order (out_cap >= n, else an error with *n_out set).
+ * Requests flagged for the host path carry ACS_OF_HOST_REQ (acs_codec_encode of that request
+ * gives the reason).  One run at a time per pipeline; the tables and codec must outlive it. */
+typedef struct acs_pipeline acs_pipeline;
+typedef struct {
+  double encode_s;      /* host time encoding (all chunks) */
+  double wait_s;        /* host time blocked on the device */
+  double total_s;       /* wall time of the call */
+  double gpu_ms;        /* device time (upload + sort + K1 + download), summed over chunks */
+  double upload_bytes;  /* bytes copied to the device */
+  uint64_t requests, chunks, host_requests;
+} acs_pipeline_stats;
+acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint32_t chunk);
+void acs_pipeline_free(acs_pipeline* p);
+int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_decision* out, size_t out_cap,
+                            size_t* n_out, acs_pipeline_stats* st);
+
 const char* acs_last_error(void);
 int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 5 packed structs, for host checks */
 int acs_device_count(void);
