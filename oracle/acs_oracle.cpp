@@ -23,7 +23,9 @@
 //   formatTarget                          src/core/utils.ts:35-45
 //   populate (store loader of the tests)  test/utils.ts:345-383
 //
-// Scope: isAllowed.  Inputs the restatement cannot decide exactly report "unsupported"
+// Scope: isAllowed and whatIsAllowed (rule sets + maskedProperty pushes,
+// accessController.ts:326-427, :592-640).  Inputs the restatement cannot decide exactly
+// report "unsupported"
 // (rule `condition` — JS eval —, subject `token` I/O, RegExp patterns outside the
 // restated subset, non-ASCII case mapping), exactly where oracle/acs_oracle.py raises
 // OracleUnsupported.  tests/test_oracle_c.py checks it against the golden vectors and
@@ -574,6 +576,11 @@ struct OrderedMap {  // JS Map: insertion order, re-set keeps the position
 struct Target {
   bool present = false;  // formatTarget(null) -> null
   VP subjects = &kEmptyArr, resources = &kEmptyArr, actions = &kEmptyArr;
+  // checkSubjectMatches' rule side (accessController.ts:797-806), a pure function of the
+  // immutable store: subjects empty, and ruleRole (the last role-URN subject value); set by
+  // Oracle::load once the URN config is known
+  bool subj_empty = true;
+  VP rule_role = nullptr;
 };
 
 Target format_target(VP t) {  // utils.ts:35-45
@@ -637,12 +644,15 @@ struct Oracle {
   }
 
   VP u(UrnName k) const { return U[k]; }
+  VP S_EMPTY = nullptr;  // ''
+
 
   void init_urns(VP cfg) {
     for (int k = 0; k < U_COUNT; ++k) U[k] = get(cfg, kUrnNames[k]);
     S_PERMIT = str_val("PERMIT");
     S_DENY = str_val("DENY");
     S_TRUE = str_val("true");
+    S_EMPTY = str_val("");
   }
 
   void init_cas(VP list) {  // accessController.ts:51-62
@@ -663,15 +673,18 @@ struct Oracle {
       PolicySet s;
       s.raw = ps;
       s.target = format_target(get(ps, "target"));
+      prepare_target(s.target);
       for (VP py : iterate(prop(ps, "policies"))) {
         Policy p;
         p.raw = py;
         p.target = format_target(get(py, "target"));
+        prepare_target(p.target);
         VP rules = get(py, "rules");
         for (VP ry : or_empty(rules)) {
           Rule r;
           r.raw = ry;
           r.target = format_target(get(ry, "target"));
+          prepare_target(r.target);
           p.rules.set(map_key(get(ry, "id")), r);
         }
         s.policies.set(map_key(get(py, "id")), std::move(p));
@@ -725,6 +738,62 @@ struct Oracle {
     return false;
   }
 
+  // The request side of checkSubjectMatches, per request (the request is not mutated on the
+  // supported paths): whether context.subject.role_associations is truthy and the string
+  // `role` values it holds (any non-string role: the general path above).
+  struct RoleSet {
+    VP request = nullptr;
+    bool truthy_ras = false, strings_only = true;
+    std::unordered_set<std::string_view> roles;
+  };
+  static RoleSet& role_set_slot() {
+    thread_local RoleSet rs;
+    return rs;
+  }
+  // called at the start of every request evaluation (a later request may reuse an address)
+  static void role_set_reset() { role_set_slot().request = nullptr; }
+  static RoleSet& role_set(VP request) {
+    RoleSet& rs = role_set_slot();
+    if (rs.request == request) return rs;
+    rs.request = request;
+    rs.roles.clear();
+    rs.strings_only = true;
+    VP ras = get(get(get(request, "context"), "subject"), "role_associations");
+    rs.truthy_ras = truthy(ras);
+    if (rs.truthy_ras) {
+      if (ras->t != T::Arr) {
+        rs.strings_only = false;
+      } else {
+        for (VP r : ras->a) {
+          VP role = get(r, "role");
+          if (role->t == T::Str) rs.roles.insert(std::string_view(role->s));
+          else if (role->t != T::Undef && role->t != T::Null) rs.strings_only = false;
+        }
+      }
+    }
+    return rs;
+  }
+
+  // checkSubjectMatches with the rule side precomputed (Target::rule_role): the same result
+  // as subject_matches(t.subjects, ...), one hash probe for a role-scoped target
+  bool target_subject_matches(const Target& t, VP req_subs, VP request) const {
+    if (t.subj_empty) return true;
+    if (!t.rule_role || !truthy(t.rule_role)) return subject_matches(t.subjects, req_subs, request);
+    const RoleSet& rs = role_set(request);
+    if (!rs.truthy_ras) return false;
+    if (!rs.strings_only || t.rule_role->t != T::Str) return subject_matches(t.subjects, req_subs, request);
+    return rs.roles.count(std::string_view(t.rule_role->s)) > 0;
+  }
+
+  void prepare_target(Target& t) const {  // the rule side of :797-806
+    t.subj_empty = nullish(t.subjects) || length_of(t.subjects) == 0;
+    if (t.subj_empty) return;
+    VP rule_role = UNDEF;
+    for (VP s : iterate(t.subjects))
+      if (strict_eq(get(s, "id"), u(U_role))) rule_role = get(s, "value");
+    t.rule_role = rule_role;
+  }
+
   // namespace / RegExp entity test (:528-566, hierarchicalScope.ts:64-101) -> (reset, hit)
   std::pair<bool, bool> regex_entity(VP rule_value, VP req_value) const {
     if (nullish(rule_value)) type_error();  // nsEntityArray[0] of undefined
@@ -758,12 +827,30 @@ struct Oracle {
     return {reset, hit};
   }
 
-  bool resource_attrs_match(VP rule_attrs, const std::vector<VP>& req_list, VP effect, bool regex) const {
-    // :465-654, operation 'isAllowed'
+  // whatIsAllowed's maskedProperty pushes, in evaluation order: (requestEntityURN, maskProperty)
+  // per push (:599-613, 624-638); the obligations list groups them by entity value.
+  using Pushes = std::vector<std::pair<VP, VP>>;
+
+  // :597-614 / :622-639: returns true where the reference `continue`s (no push)
+  bool push_mask(Pushes* masks, VP qa, bool req_props, VP req_entity_urn, VP rule_prop_value) const {
+    VP qval = get(qa, "value");
+    VP mask = UNDEF;
+    if (req_props && truthy(qval)) mask = qval;
+    else if (!req_props) mask = rule_prop_value;
+    if (!nullish(mask) && str_of(mask).find('#') == std::string::npos) return true;  // indexOf('#') <= -1
+    masks->push_back({req_entity_urn ? req_entity_urn : S_EMPTY, mask});
+    return false;
+  }
+
+  bool resource_attrs_match(VP rule_attrs, const std::vector<VP>& req_list, VP effect, bool regex,
+                            Pushes* masks = nullptr) const {
+    // :465-654; masks != nullptr: operation 'whatIsAllowed' (pushes into *masks)
+    const bool wia = masks != nullptr;
     VP ent = u(U_entity), prop_urn = u(U_property), op_urn = u(U_operation);
     bool entity_match = false, property_match = false, rule_props = false, req_props = false;
     bool operation_match = false, skip_deny = true;
     VP req_entity_urn = nullptr;  // '' initially
+    VP rule_prop_value = S_EMPTY;  // rulePropertyValue = ''
     if (lodash_is_empty(rule_attrs)) return true;
     for (VP ra : req_list)
       if (strict_eq(prop(ra, "id"), prop_urn)) req_props = true;
@@ -773,7 +860,10 @@ struct Oracle {
       for (VP r : or_empty(rule_attrs)) {
         VP rid = get(r, "id"), rval = get(r, "value");
         VP qid = get(qa, "id"), qval = get(qa, "value");
-        if (strict_eq(prop(r, "id"), prop_urn)) rule_props = true;
+        if (strict_eq(prop(r, "id"), prop_urn)) {
+          rule_props = true;
+          rule_prop_value = prop(r, "value");
+        }
         if (!regex) {
           if (strict_eq(qid, ent) && strict_eq(rid, ent) && strict_eq(qval, rval)) {
             entity_match = true;
@@ -814,21 +904,32 @@ struct Oracle {
       }
       VP qid = get(qa, "id");
       const bool scope = strict_eq(qid, prop_urn) || !req_props;
-      if (eff_deny && scope && entity_match && rule_props && property_match) skip_deny = false;
-      if (eff_permit && scope && entity_match && rule_props && !property_match) return false;
+      if (!wia) {
+        if (eff_deny && scope && entity_match && rule_props && property_match) skip_deny = false;
+        if (eff_permit && scope && entity_match && rule_props && !property_match) return false;
+        continue;
+      }
+      if (eff_permit && scope && entity_match && rule_props && !property_match) {  // :592-614
+        if (!req_props) return false;
+        if (push_mask(masks, qa, req_props, req_entity_urn, rule_prop_value)) continue;
+      }
+      if (eff_deny && scope && entity_match && rule_props && (property_match || !req_props)) {  // :619-639
+        if (push_mask(masks, qa, req_props, req_entity_urn, rule_prop_value)) continue;
+      }
     }
-    if (skip_deny && rule_props && req_props && eff_deny && !property_match) return false;
+    if (!wia && skip_deny && rule_props && req_props && eff_deny && !property_match) return false;
     if (!entity_match && !operation_match) return false;
     return true;
   }
 
-  bool target_matches(const Target& t, VP request, VP effect, bool regex) const {  // :661-672
+  bool target_matches(const Target& t, VP request, VP effect, bool regex, Pushes* masks = nullptr) const {
+    // :661-672 (masks: operation 'whatIsAllowed')
     if (effect->t == T::Undef) effect = S_PERMIT;
     VP req_target = prop(request, "target");
-    if (!subject_matches(t.subjects, prop(req_target, "subjects"), request)) return false;
+    if (!target_subject_matches(t, prop(req_target, "subjects"), request)) return false;
     if (!attributes_match(t.actions, prop(req_target, "actions"))) return false;
     VP res = prop(req_target, "resources");
-    return resource_attrs_match(t.resources, or_empty(res), effect, regex);
+    return resource_attrs_match(t.resources, or_empty(res), effect, regex, masks);
   }
 
   bool multiple_entities_match(const PolicySet& ps, VP request) const {  // :429-463
@@ -1217,6 +1318,7 @@ struct Oracle {
   }
 
   Outcome is_allowed(VP request, SharedIds* cache = nullptr) const {
+    role_set_reset();
     Outcome out;
     if (!truthy(get(request, "target"))) {  // :91-102
       out.decision = 3;
@@ -1297,7 +1399,121 @@ struct Oracle {
     out.ec = ec_code(effect.ec);
     return out;
   }
+
+  // ---------------------------------------------------------------- whatIsAllowed (:326-427)
+  // The included sets / policies / rules as global node indices (sets in Map order, then every
+  // set's policies in order, then every policy's rules in order; null entries keep their
+  // slot: the numbering of the product's compiled image) and the maskedProperty push log.
+  struct ReverseQuery {
+    std::vector<uint32_t> sets, pols, rules;
+    Pushes pushes;
+  };
+
+  ReverseQuery what_is_allowed(VP request) const {
+    role_set_reset();
+    ReverseQuery rq;
+    VP ctx = get(request, "context");
+    if (truthy(get(get(ctx, "subject"), "token"))) unsupported("subject token (identity-srv / Redis I/O)");
+    Pushes* masks = &rq.pushes;
+    uint32_t si = 0, pbase = 0, rbase = 0;
+    for (auto& skv : sets.items) {
+      const PolicySet& pset = skv.second;
+      const uint32_t p0 = pbase;
+      uint32_t rcount = 0;  // rules of this set's policies (null policies hold none)
+      std::vector<uint32_t> rule_base(pset.policies.items.size());
+      for (size_t q = 0; q < pset.policies.items.size(); ++q) {
+        rule_base[q] = rbase + rcount;
+        rcount += (uint32_t)pset.policies.items[q].second.rules.size();
+      }
+      pbase += (uint32_t)pset.policies.items.size();
+      rbase += rcount;
+      const uint32_t s_idx = si++;
+      // set gate: _.isEmpty(target) || targetMatches(target, request, 'whatIsAllowed') (:344-347)
+      if (pset.target.present && !target_matches(pset.target, request, UNDEF, false, masks)) continue;
+      bool exact = false;
+      VP pe = UNDEF;
+      for (auto& pkv : pset.policies.items) {  // :353-368 (the CA branch never fires, as in isAllowed)
+        const Policy& pol = pkv.second;
+        VP eff = prop(pol.raw, "effect");
+        if (truthy(eff)) pe = eff;
+        if (pol.target.present && target_matches(pol.target, request, pe, false, masks)) {
+          exact = true;
+          break;
+        }
+      }
+      if (exact) {  // :373-376
+        long n_ent = 0;
+        for (VP a : or_empty(get(get(request, "target"), "resources")))
+          if (strict_eq(get(a, "id"), u(U_entity))) ++n_ent;
+        if (n_ent > 1) exact = multiple_entities_match(pset, request);
+      }
+      std::vector<uint32_t> pols, rules;
+      for (size_t q = 0; q < pset.policies.items.size(); ++q) {  // :378-414
+        const Policy& pol = pset.policies.items[q].second;
+        if (!truthy(pol.raw)) continue;
+        const bool gate = !pol.target.present || (exact && target_matches(pol.target, request, pe, false, masks)) ||
+                          (!exact && target_matches(pol.target, request, pe, true, masks));
+        if (!gate) continue;
+        std::vector<uint32_t> prules;
+        for (size_t r = 0; r < pol.rules.items.size(); ++r) {
+          const Rule& rule = pol.rules.items[r].second;
+          if (!truthy(rule.raw)) continue;
+          VP re = get(rule.raw, "effect");
+          bool m = !rule.target.present || target_matches(rule.target, request, re, false, masks);
+          if (!m) m = target_matches(rule.target, request, re, true, masks);
+          if (!rule.target.present || m) prules.push_back(rule_base[q] + (uint32_t)r);
+        }
+        if (truthy(get(pol.raw, "effect")) || !prules.empty()) {  // :411-413
+          pols.push_back(p0 + (uint32_t)q);
+          rules.insert(rules.end(), prules.begin(), prules.end());
+        }
+      }
+      if (!pols.empty()) {  // :416-418
+        rq.sets.push_back(s_idx);
+        rq.pols.insert(rq.pols.end(), pols.begin(), pols.end());
+        rq.rules.insert(rq.rules.end(), rules.begin(), rules.end());
+      }
+    }
+    return rq;
+  }
 };
+
+void json_string(std::string& o, const std::string& s) {
+  o += '"';
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += (char)c;
+    } else if (c < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", c);
+      o += b;
+    } else {
+      o += (char)c;
+    }
+  }
+  o += '"';
+}
+
+// A JS value of the push log as JSON: strings as strings, null as null, undefined as
+// {"$undef":1}, anything else as {"$other":1} (never compared: the product sends such values
+// to the host).
+void json_value(std::string& o, VP v) {
+  if (v->t == T::Str) json_string(o, v->s);
+  else if (v->t == T::Null) o += "null";
+  else if (v->t == T::Undef) o += "{\"$undef\":1}";
+  else o += "{\"$other\":1}";
+}
+
+template <class V>
+void json_ints(std::string& o, const V& v) {
+  o += '[';
+  for (size_t k = 0; k < v.size(); ++k) {
+    if (k) o += ',';
+    o += std::to_string(v[k]);
+  }
+  o += ']';
+}
 
 thread_local std::string g_err;
 
@@ -1421,5 +1637,100 @@ int acs_oracle_is_allowed_shared(void* h, const char* shared_json, const char* r
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return 0;
 }
+
+// whatIsAllowed (accessController.ts:326-427) of n requests (a JSON array; shared_json as in
+// acs_oracle_is_allowed_shared), evaluated on `threads` std::threads.  *out_json (free with
+// acs_oracle_free_text): a JSON array with one element per request:
+//   {"k":0,"s":[set idx],"p":[policy idx],"r":[rule idx],"o":[[entity, mask], ...]}  (global
+//   node indices in the compiled image's numbering; "o" the maskedProperty pushes in order)
+//   {"k":1,"e":kind}  the reference rejects (1 TypeError, 2 InvalidCombiningAlgorithm, 3 SyntaxError)
+//   {"k":2}           outside the restatement (token I/O, RegExp outside the subset, ...)
+int acs_oracle_what_is_allowed_shared(void* h, const char* shared_json, const char* requests, size_t n, int threads,
+                                      char** out_json, double* seconds) {
+  auto* o = (Oracle*)h;
+  Arena arena;
+  VP arr;
+  std::vector<VP> shared;
+  try {
+    if (shared_json) {
+      Parser ps(shared_json, strlen(shared_json), arena);
+      VP sv = ps.value();
+      if (sv->t != T::Arr) throw std::runtime_error("shared: expected a JSON array");
+      shared = sv->a;
+    }
+    Parser p(requests, strlen(requests), arena);
+    if (shared_json) p.shared = &shared;
+    arr = p.value();
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+  if (arr->t != T::Arr || arr->a.size() != n) {
+    g_err = "requests: expected a JSON array of n requests";
+    return -1;
+  }
+  if (threads < 1) threads = 1;
+  std::vector<std::string> parts(n);
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (;;) {
+      const size_t i = next.fetch_add(16);
+      if (i >= n) return;
+      const size_t e = std::min(n, i + 16);
+      for (size_t k = i; k < e; ++k) {
+        std::string& s = parts[k];
+        try {
+          const Oracle::ReverseQuery rq = o->what_is_allowed(arr->a[k]);
+          s = "{\"k\":0,\"s\":";
+          json_ints(s, rq.sets);
+          s += ",\"p\":";
+          json_ints(s, rq.pols);
+          s += ",\"r\":";
+          json_ints(s, rq.rules);
+          s += ",\"o\":[";
+          for (size_t x = 0; x < rq.pushes.size(); ++x) {
+            if (x) s += ',';
+            s += '[';
+            json_value(s, rq.pushes[x].first);
+            s += ',';
+            json_value(s, rq.pushes[x].second);
+            s += ']';
+          }
+          s += "]}";
+        } catch (const JSError& err) {
+          s = "{\"k\":1,\"e\":" + std::to_string(err.kind) + "}";
+        } catch (const Unsupported&) {
+          s = "{\"k\":2}";
+        }
+      }
+    }
+  };
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  size_t total = 2;
+  for (auto& x : parts) total += x.size() + 1;
+  char* buf = (char*)malloc(total + 1);
+  if (!buf) {
+    g_err = "out of memory";
+    return -1;
+  }
+  size_t at = 0;
+  buf[at++] = '[';
+  for (size_t k = 0; k < n; ++k) {
+    if (k) buf[at++] = ',';
+    memcpy(buf + at, parts[k].data(), parts[k].size());
+    at += parts[k].size();
+  }
+  buf[at++] = ']';
+  buf[at] = 0;
+  *out_json = buf;
+  return 0;
+}
+
+void acs_oracle_free_text(char* p) { free(p); }
 
 }  // extern "C"

@@ -49,6 +49,10 @@ def lib():
                                                C.POINTER(C.c_double)]
         _LIB.acs_oracle_is_allowed_shared.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, C.c_int,
                                                       C.c_void_p, C.POINTER(C.c_double)]
+        _LIB.acs_oracle_what_is_allowed_shared.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_size_t, C.c_int,
+                                                           C.POINTER(C.c_void_p), C.POINTER(C.c_double)]
+        _LIB.acs_oracle_free_text.argtypes = [C.c_void_p]
+        _LIB.acs_oracle_free_text.restype = None
         _LIB.acs_oracle_last_error.restype = C.c_char_p
         _LIB.acs_oracle_regex_cell.argtypes = [C.c_char_p, C.c_char_p]
     return _LIB
@@ -60,7 +64,8 @@ def _json(v):
 
 
 class COracle:
-    """isAllowed of the reference on one policy store, evaluated by the C++ restatement."""
+    """isAllowed / whatIsAllowed of the reference on one policy store, evaluated by the C++
+    restatement."""
 
     def __init__(self, urns: dict, combining_algorithms: list, doc: dict):
         self.h = lib().acs_oracle_create(_json(urns), _json(combining_algorithms), _json(doc))
@@ -93,6 +98,26 @@ class COracle:
         if rc != 0:
             raise RuntimeError(f"acs_oracle_is_allowed: {lib().acs_oracle_last_error().decode()}")
         return out, sec.value
+
+    def what_is_allowed(self, requests, threads=1, shared=None):
+        """(results, evaluation seconds) of whatIsAllowed (accessController.ts:326-427) per
+        request: {"k": 0, "s": [set idx], "p": [policy idx], "r": [rule idx], "o": [[entity,
+        mask], ...]} (global node indices of the compiled image; the maskedProperty pushes in
+        order, undefined as {"$undef": 1}), {"k": 1, "e": kind} (the reference rejects) or
+        {"k": 2} (outside the restatement)."""
+        n = len(requests)
+        text = b"[" + b",".join(_json(r) for r in requests) + b"]"
+        stext = None if shared is None else b"[" + b",".join(_json(v) for v in shared) + b"]"
+        out = C.c_void_p()
+        sec = C.c_double(0.0)
+        rc = lib().acs_oracle_what_is_allowed_shared(self.h, stext, text, n, int(threads), C.byref(out), C.byref(sec))
+        if rc != 0:
+            raise RuntimeError(f"acs_oracle_what_is_allowed: {lib().acs_oracle_last_error().decode()}")
+        try:
+            res = json.loads(C.string_at(out.value).decode("utf-8", "surrogatepass"))
+        finally:
+            lib().acs_oracle_free_text(out)
+        return res, sec.value
 
     def outcomes(self, requests, threads=1):
         """Normalised outcomes as tests/diff_utils.oracle_outcome builds them:

@@ -77,3 +77,68 @@ def controller_outcome(r):
     if isinstance(r, Exception):
         return ("EXC", repr(r))
     return ("OK", r["decision"], _norm(r["evaluation_cacheable"]), r["operation_status"]["code"])
+
+
+def gpu_reverse_query_compact(cs, overlay, bits_row, log, rec):
+    """A whatIsAllowed result of the evaluator (inclusion bitset row, maskedProperty log of
+    (entity id, mask id) pairs, decision record) in the C++ oracle's compact form
+    (oracle/acs_oracle_c.COracle.what_is_allowed), or None for a host-path request."""
+    from acs_mi355x import layout as L
+    from acs_mi355x.results import bits_layout
+    import numpy as np
+    f = int(rec["flags"])
+    if f & (L.OF_HOST_REQ | L.OF_HOST_COND | L.OF_OBL_OVERFLOW):
+        return None
+    if f & L.OF_ERR:
+        if int(rec["err"]) == L.ERR_REGEX_HOST:
+            return None
+        return {"k": 1, "e": int(rec["err"])}
+    wp, wr, _ = bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)
+    row = np.asarray(bits_row, np.uint32)
+
+    def members(off, count):
+        words = row[off:off + (count + 31) // 32]
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:count]
+        return [int(i) for i in np.flatnonzero(bits)]
+
+    def val(i):
+        v = overlay.string(int(i))
+        if v is MISSING:
+            return {"$undef": 1}
+        return v
+
+    return {"k": 0, "s": members(0, cs.n_sets), "p": members(wp, cs.n_pols), "r": members(wr, cs.n_rules),
+            "o": [[val(e), val(m)] for e, m in np.asarray(log).reshape(-1, 2)]}
+
+
+class _ListOverlay:
+    """id -> value over a plain list (MISSING for {"$undef": 1})."""
+
+    def __init__(self, values):
+        self.values = values
+
+    def string(self, i):
+        v = self.values[int(i)]
+        return MISSING if isinstance(v, dict) and "$undef" in v else v
+
+
+def compact_reverse_query(cs, c):
+    """The C++ oracle's compact whatIsAllowed result -> the reference's ReverseQuery shape
+    (results.reverse_query over the same inclusion sets and push log), or ('ERR', kind) /
+    None (unsupported)."""
+    import numpy as np
+    from acs_mi355x import layout as L
+    from acs_mi355x.results import bits_layout
+    if c["k"] == 2:
+        return None
+    if c["k"] == 1:
+        return ("ERR", {1: "TypeError", 2: "InvalidCombiningAlgorithm", 3: "SyntaxError"}.get(c["e"], "Error"))
+    wp, wr, words = bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)
+    row = np.zeros(max(words, 1), np.uint32)
+    for off, idx in ((0, c["s"]), (wp, c["p"]), (wr, c["r"])):
+        for i in idx:
+            row[off + (i >> 5)] |= np.uint32(1 << (i & 31))
+    vals = [x for pair in c["o"] for x in pair]
+    pairs = [(2 * k, 2 * k + 1) for k in range(len(c["o"]))]
+    rec = np.zeros(1, L.DECISION_DT)[0]
+    return norm_rq(results.reverse_query(cs, _ListOverlay(vals), row, pairs, rec))

@@ -70,3 +70,68 @@ def test_synthetic_vs_python_oracle(kind):
     co = acs_oracle_c.COracle(FULL_URNS, DEFAULT_CAS, doc)
     got = co.outcomes(reqs, threads=4)
     assert got == [oracle_outcome(po, r) for r in reqs]
+
+
+# ---------------------------------------------------------------- whatIsAllowed
+def _wia_python(po, req):
+    from diff_utils import norm_rq
+    from oracle.jsval import JSError
+    try:
+        return norm_rq(po.what_is_allowed(req))
+    except JSError as e:
+        return ("ERR", e.kind)
+
+
+def test_kats_what_is_allowed():
+    """The C++ whatIsAllowed (rule sets + maskedProperty pushes) meets every whatIsAllowed
+    golden vector of the reference's specs and equals the Python oracle on them."""
+    from diff_utils import compact_reverse_query
+    from kat_utils import check_asserts
+    by_fx = {}
+    for v in KATS:
+        if v["op"] == "whatIsAllowed":
+            by_fx.setdefault((v["fixture"], v["urns"]), []).append(v)
+    checked = 0
+    for (fx, _), vecs in by_fx.items():
+        doc = load_fixture(fx)
+        urns = urns_for(vecs[0])
+        cs = compiler.compile_store(store.populate(doc), urns, DEFAULT_CAS)
+        co = acs_oracle_c.COracle(urns, DEFAULT_CAS, doc)
+        po = Oracle(urns=urns)
+        po.load(doc)
+        res, _ = co.what_is_allowed([v["request"] for v in vecs])
+        for v, c in zip(vecs, res):
+            got = compact_reverse_query(cs, c)
+            assert got is not None, v["spec"]
+            assert check_asserts(got, v["expect"]["asserts"]) == [], v["spec"]
+            assert got == _wia_python(po, v["request"]), v["spec"]
+            checked += 1
+    assert checked >= 19
+
+
+@pytest.mark.parametrize("seed", range(0, 600, 30))
+def test_random_what_is_allowed_vs_python_oracle(seed):
+    from diff_utils import compact_reverse_query
+    from acs_mi355x.jsops import Unsupported
+    agree = 0
+    for s in range(seed, seed + 30):
+        urns, doc, reqs = randgen.rand_case(s)
+        try:
+            cs = compiler.compile_store(store.populate(doc), urns, DEFAULT_CAS)
+        except Unsupported:
+            continue
+        po = Oracle(urns=urns)
+        po.load(doc)
+        co = acs_oracle_c.COracle(urns, DEFAULT_CAS, doc)
+        res, _ = co.what_is_allowed(reqs, threads=2)
+        for req, c in zip(reqs, res):
+            got = compact_reverse_query(cs, c)
+            if got is None:
+                continue
+            try:
+                want = _wia_python(po, req)
+            except OracleUnsupported:
+                continue
+            assert got == want, (s, req)
+            agree += 1
+    assert agree > 150
