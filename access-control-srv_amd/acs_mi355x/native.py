@@ -36,7 +36,7 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_codec_free", "acs_codec_set_subject_scopes", "acs_codec_evict_subject", "acs_codec_encode",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",
-           "acs_pipeline_free", "acs_pipeline_is_allowed"]
+           "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_device_list"]
 
 
 class ShardC(C.Structure):
@@ -48,6 +48,9 @@ def _declare(lib):
     pb = C.POINTER(ReqBatchC)
     lib.acs_compile.restype = vp
     lib.acs_compile.argtypes = [vp, C.c_size_t, C.c_int]
+    lib.acs_compile_multi.restype = vp
+    lib.acs_compile_multi.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    lib.acs_device_list.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     lib.acs_free.argtypes = [vp]
     lib.acs_free.restype = None
     lib.acs_is_allowed.argtypes = [vp, pb, vp]
@@ -181,16 +184,32 @@ def resolve_overflow(tables, batch, out, cap: int = OVERFLOW_CAP, chunks: int = 
 
 
 class Tables:
-    """Device-resident compiled store on one GPU (wraps an acs_tables handle)."""
+    """Device-resident compiled store (wraps an acs_tables handle): on one GPU, or with
+    ``devices=[d0, d1, ...]`` replicated over several (acs_compile_multi) so that large
+    compact host batches and the pipeline split across them; the *_device entry points and
+    ``device`` name d0."""
 
-    def __init__(self, blob: bytes, device: int = 0, lib=None):
+    def __init__(self, blob: bytes, device: int = 0, lib=None, devices=None):
         self.lib = lib or load()
         self._blob = blob
-        self.h = self.lib.acs_compile(blob, len(blob), device)
+        if devices:
+            arr = (C.c_int * len(devices))(*devices)
+            self.h = self.lib.acs_compile_multi(blob, len(blob), arr, len(devices))
+            device = int(devices[0])
+        else:
+            self.h = self.lib.acs_compile(blob, len(blob), device)
         if not self.h:
             raise RuntimeError(f"acs_compile failed: {last_error(self.lib)}")
         self.device = device
         self.words = int(self.lib.acs_wia_words_per_request(self.h))
+
+    def devices(self):
+        """The handle's devices (acs_device_list), primary first."""
+        arr = (C.c_int * 64)()
+        m = self.lib.acs_device_list(self.h, arr, 64)
+        if m < 0:
+            raise RuntimeError(last_error(self.lib))
+        return list(arr[:m])
 
     def close(self):
         if self.h:

@@ -596,12 +596,20 @@ struct acs_tables {
   Workspace hws;
   std::mutex mu;
   uint32_t rx_rows_min = 0;  // regex-matrix rows the rule resource attributes read
+  // acs_compile_multi: replicas of the same image on further devices (C0); the host-buffer
+  // entry points split a compact batch across this handle and its replicas
+  std::vector<acs_tables*> peers;
+  size_t image_bytes = 0;
 };
 
 // csrc/acs_validate.cpp
 extern "C" int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_min);
 extern "C" int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
                                         uint32_t rx_rows_min);
+extern "C" void acs_internal_shard_plan(const acs_req_batch* b, size_t lo, size_t hi, const uint32_t* arena_end,
+                                        size_t plan[4]);
+extern "C" int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
+                                         uint32_t rx_rows_min, uint32_t* arena_end);
 
 static int check_batch(const acs_tables* t, const acs_req_batch* b) {
   return acs_internal_check_batch(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min);
@@ -786,11 +794,14 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
+  t->image_bytes = up_bytes;
   return t;
 }
 
 void acs_free(acs_tables* t) {
   if (!t) return;
+  for (acs_tables* p : t->peers) acs_free(p);
+  t->peers.clear();
   (void)hipSetDevice(t->device);
   if (t->dev) (void)hipFree(t->dev);
   if (t->ev0) (void)hipEventDestroy(t->ev0);
@@ -801,6 +812,52 @@ void acs_free(acs_tables* t) {
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
+}
+
+acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devices, int n_devices) {
+  if (!devices || n_devices < 1) {
+    fail("acs_compile_multi: no devices");
+    return nullptr;
+  }
+  acs_tables* t = acs_compile(blob, n_bytes, devices[0]);
+  if (!t) return nullptr;
+  for (int k = 1; k < n_devices; ++k) {
+    // C0: the replica's image comes from the primary's over the device interconnect (xGMI
+    // peer copy), not again from the host
+    auto* r = new acs_tables();
+    r->device = devices[k];
+    r->rx_rows_min = t->rx_rows_min;
+    r->view = t->view;
+    r->image_bytes = t->image_bytes;
+    if (hipSetDevice(r->device) != hipSuccess || hipMalloc(&r->dev, t->image_bytes + 128) != hipSuccess ||
+        hipMemcpyPeer(r->dev, r->device, t->dev, t->device, t->image_bytes) != hipSuccess ||
+        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&r->ev0) != hipSuccess || hipEventCreate(&r->ev1) != hipSuccess) {
+      fail("acs_compile_multi: replica allocation / peer copy failed");
+      acs_free(r);
+      acs_free(t);
+      return nullptr;
+    }
+    // rebase the view's pointers from the primary's image onto the replica's
+    auto rebase = [&](const void* p) -> const void* { return (const char*)r->dev + ((const char*)p - (const char*)t->dev); };
+    r->view.sets = (const NodeRec*)rebase(t->view.sets);
+    r->view.pols = (const NodeRec*)rebase(t->view.pols);
+    r->view.rules = (const NodeRec*)rebase(t->view.rules);
+    r->view.rres = (const RuleResAttr*)rebase(t->view.rres);
+    r->view.pairs = (const Pair*)rebase(t->view.pairs);
+    r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
+    r->sort = t->sort;
+    t->peers.push_back(r);
+  }
+  (void)hipSetDevice(t->device);
+  return t;
+}
+
+int acs_device_list(const acs_tables* t, int* devices, int n) {
+  if (!t) return fail("acs_device_list: null tables");
+  const int m = 1 + (int)t->peers.size();
+  for (int k = 0; k < n && k < m; ++k) devices[k] = k == 0 ? t->device : t->peers[k - 1]->device;
+  return m;
 }
 
 uint32_t acs_wia_words_per_request(const acs_tables* t) {
@@ -1072,6 +1129,47 @@ int upload_batch(Workspace& W, const acs_req_batch* b, acs_req_batch* dev, hipSt
   return 0;
 }
 
+// Requests [lo, hi) of a compact batch on one device: their lines, extension records and
+// arena words only (the shard's slices, uploaded so that the batch's absolute offsets still
+// index them: the device pointers are based one slice-start below the copy), plus the whole
+// regex matrix and class rows.  arena_end: per request, one past its last arena word.
+int upload_shard(Workspace& W, const acs_req_batch* b, size_t lo, size_t hi, const uint32_t* arena_end,
+                 acs_req_batch* dev, hipStream_t s) {
+  size_t plan[4];
+  acs_internal_shard_plan(b, lo, hi, arena_end, plan);
+  const size_t a0 = plan[0], a1 = plan[1], e0 = plan[2], e1 = plan[3];
+  const size_t m = hi - lo;
+  Image I;
+  I.d = *b;
+  I.d.n = (uint32_t)m;
+  I.add((const ReqLine*)b->lines + lo, m * sizeof(ReqLine), &I.d.lines);
+  const void* ext_dst = nullptr;
+  const void* arena_dst = nullptr;
+  I.add(b->ext ? b->ext + e0 : (const uint32_t*)b->lines, (e1 - e0) * 4, &ext_dst);
+  I.add(b->arena + a0, (a1 - a0) * 4, &arena_dst);
+  I.add(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&I.d.rx);
+  if (b->cand) I.add(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t), (const void**)&I.d.cand);
+  if (b->role_key) {
+    I.add(b->role_key + lo, m * sizeof(uint32_t), (const void**)&I.d.role_key);
+    I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
+          (const void**)&I.d.role_rows_bits);
+  }
+  if (W.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
+  char* base = (char*)W.img.p;
+  size_t off = 0;
+  for (const Image::Sec& x : I.secs) {
+    if (x.bytes) HIP_OK(hipMemcpyAsync(base + off, x.src, x.bytes, hipMemcpyHostToDevice, s));
+    *x.dst = base + off;
+    off += (x.bytes + IMG_ALIGN - 1) & ~(IMG_ALIGN - 1);
+  }
+  // absolute offsets: the device pointers sit one slice-start below the copies (only
+  // [start, end) is ever dereferenced)
+  I.d.arena = (const uint32_t*)arena_dst - a0;
+  I.d.ext = b->ext ? (const uint32_t*)ext_dst - e0 : nullptr;
+  *dev = I.d;
+  return 0;
+}
+
 // Output regions of one call in the workspace's `out` buffer (256-B aligned).
 struct OutLayout {
   size_t off[4] = {};
@@ -1085,9 +1183,50 @@ struct OutLayout {
 
 }  // namespace
 
+// A compact batch split over the handle and its replicas (acs_compile_multi): contiguous
+// request shards, one per device, each uploaded (its slices only), sorted, decided and
+// downloaded on that device's stream; all devices run concurrently.
+static constexpr size_t MULTI_MIN_PER_DEVICE = 4096;
+
+static bool split_across_devices(const acs_tables* t, const acs_req_batch* b) {
+  return !t->peers.empty() && !b->hdr && b->lines && b->n >= 2 * MULTI_MIN_PER_DEVICE;
+}
+
+static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out, const uint32_t* arena_end) {
+  std::vector<acs_tables*> dev{t};
+  dev.insert(dev.end(), t->peers.begin(), t->peers.end());
+  size_t D = dev.size();
+  if (b->n / D < MULTI_MIN_PER_DEVICE) D = b->n / MULTI_MIN_PER_DEVICE;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
+  for (size_t k = 0; k < D; ++k) {
+    acs_tables* T = dev[k];
+    const size_t lo = b->n * k / D, hi = b->n * (k + 1) / D;
+    HIP_OK(hipSetDevice(T->device));
+    acs_req_batch d;
+    if (upload_shard(T->hws, b, lo, hi, arena_end, &d, T->stream)) return -1;
+    if (T->hws.out.reserve((hi - lo) * sizeof(Decision))) return -1;
+    if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return -1;
+    HIP_OK(hipMemcpyAsync(out + lo, T->hws.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, T->stream));
+  }
+  for (size_t k = 0; k < D; ++k) {
+    HIP_OK(hipSetDevice(dev[k]->device));
+    HIP_OK(hipStreamSynchronize(dev[k]->stream));
+  }
+  HIP_OK(hipSetDevice(t->device));
+  return 0;
+}
+
 int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
   if (!t || !b || (b && b->n && !out)) return fail("acs_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (split_across_devices(t, b)) {
+    std::vector<uint32_t> arena_end(b->n);
+    if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
+                                  arena_end.data()))
+      return -1;
+    return multi_is_allowed(t, b, out, arena_end.data());
+  }
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
@@ -1182,6 +1321,7 @@ struct acs_pipeline {
   int threads = 1;
   uint32_t chunk = 131072;
   struct Slot {
+    acs_tables* T = nullptr;  // the device this slot runs on (the handle or one of its replicas)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, done = nullptr;
     Workspace ws;
@@ -1190,18 +1330,23 @@ struct acs_pipeline {
     acs_codec_batch* batch = nullptr;  // in flight
     size_t lo = 0, n = 0;              // its requests
     bool busy = false;
-  } slot[2];
-  std::mutex mu;  // one run at a time per pipeline
+  };
+  std::vector<Slot> slot;  // two per device: chunk k -> device k % D, slot (k / D) % 2
+  std::mutex mu;           // one run at a time per pipeline
 };
 
 namespace {
 
+double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // Finish slot S: wait for its chunk, copy its records out, free its batch.
-int pipeline_retire(acs_pipeline* p, acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats* st) {
+int pipeline_retire(acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats* st) {
   if (!S.busy) return 0;
-  const double w0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  const double w0 = steady_s();
   HIP_OK(hipEventSynchronize(S.done));
-  const double w1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  const double w1 = steady_s();
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, S.ev0, S.ev1));
   std::memcpy(out + S.lo, S.stage, S.n * sizeof(acs_decision));
@@ -1213,12 +1358,7 @@ int pipeline_retire(acs_pipeline* p, acs_pipeline::Slot& S, acs_decision* out, a
   acs_codec_batch_free(S.batch);
   S.batch = nullptr;
   S.busy = false;
-  (void)p;
   return 0;
-}
-
-double steady_s() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 }  // namespace
@@ -1235,26 +1375,28 @@ acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint
   p->c = c;
   p->threads = threads < 1 ? 1 : threads;
   p->chunk = chunk ? chunk : 131072;
-  if (hipSetDevice(t->device) != hipSuccess) {
-    fail("acs_pipeline_create: hipSetDevice failed");
-    delete p;
-    return nullptr;
-  }
-  for (auto& S : p->slot)
-    if (hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
+  std::vector<acs_tables*> dev{t};
+  dev.insert(dev.end(), t->peers.begin(), t->peers.end());
+  p->slot.resize(2 * dev.size());
+  for (size_t k = 0; k < p->slot.size(); ++k) {
+    acs_pipeline::Slot& S = p->slot[k];
+    S.T = dev[k / 2];
+    if (hipSetDevice(S.T->device) != hipSuccess || hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&S.ev0) != hipSuccess || hipEventCreate(&S.ev1) != hipSuccess ||
         hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
       fail("acs_pipeline_create: stream / event creation failed");
       acs_pipeline_free(p);
       return nullptr;
     }
+  }
+  (void)hipSetDevice(t->device);
   return p;
 }
 
 void acs_pipeline_free(acs_pipeline* p) {
   if (!p) return;
-  (void)hipSetDevice(p->t->device);
   for (auto& S : p->slot) {
+    if (S.T) (void)hipSetDevice(S.T->device);
     if (S.busy) (void)hipEventSynchronize(S.done);
     if (S.batch) acs_codec_batch_free(S.batch);
     S.ws.release();
@@ -1264,6 +1406,7 @@ void acs_pipeline_free(acs_pipeline* p) {
     if (S.done) (void)hipEventDestroy(S.done);
     if (S.stream) (void)hipStreamDestroy(S.stream);
   }
+  (void)hipSetDevice(p->t->device);
   delete p;
 }
 
@@ -1282,24 +1425,26 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     ~Free() { acs_internal_items_free(it); }
   } free_items{items};
   if (n > out_cap || (n && !out)) return fail("acs_pipeline_is_allowed: output holds fewer records than the requests");
-  HIP_OK(hipSetDevice(p->t->device));
-  int k = 0;
+  const size_t D = p->slot.size() / 2;
+  size_t k = 0;
   for (size_t lo = 0; lo < n; lo += p->chunk, ++k) {
     const size_t hi = lo + p->chunk < n ? lo + p->chunk : n;
     const double e0 = steady_s();
     acs_codec_batch* b = acs_internal_encode_range(p->c, items, lo, hi, p->threads);
     if (!b) return -1;
     if (st) st->encode_s += steady_s() - e0;
-    acs_pipeline::Slot& S = p->slot[k & 1];
-    if (pipeline_retire(p, S, out, st)) {  // the chunk two back
+    acs_pipeline::Slot& S = p->slot[2 * (k % D) + (k / D) % 2];
+    if (pipeline_retire(S, out, st)) {  // this slot's previous chunk
       acs_codec_batch_free(b);
       return -1;
     }
     S.batch = b;
     S.lo = lo;
     S.n = hi - lo;
+    acs_tables* T = S.T;
     acs_req_batch view;
-    if (acs_codec_batch_view(b, &view) || check_batch(p->t, &view)) return -1;
+    if (acs_codec_batch_view(b, &view) || check_batch(T, &view)) return -1;
+    HIP_OK(hipSetDevice(T->device));
     if (S.stage_n < S.n) {
       if (S.stage) HIP_OK(hipHostFree(S.stage));
       S.stage = nullptr;
@@ -1308,12 +1453,12 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
       S.stage_n = S.n;
     }
     {
-      std::lock_guard<std::mutex> tl(p->t->mu);  // the handle's launch bookkeeping
+      std::lock_guard<std::mutex> tl(T->mu);  // the device handle's launch bookkeeping
       acs_req_batch d;
       HIP_OK(hipEventRecord(S.ev0, S.stream));
       if (upload_batch(S.ws, &view, &d, S.stream)) return -1;
       if (S.ws.out.reserve(S.n * sizeof(Decision))) return -1;
-      if (is_allowed_launch(p->t, S.ws, &d, (acs_decision*)S.ws.out.p, S.stream)) return -1;
+      if (is_allowed_launch(T, S.ws, &d, (acs_decision*)S.ws.out.p, S.stream)) return -1;
       HIP_OK(hipMemcpyAsync(S.stage, S.ws.out.p, S.n * sizeof(Decision), hipMemcpyDeviceToHost, S.stream));
       HIP_OK(hipEventRecord(S.ev1, S.stream));
       HIP_OK(hipEventRecord(S.done, S.stream));
@@ -1327,13 +1472,13 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     }
   }
   for (auto& S : p->slot)
-    if (pipeline_retire(p, S, out, st)) return -1;
+    if (pipeline_retire(S, out, st)) return -1;
+  HIP_OK(hipSetDevice(p->t->device));
   if (st) {
     st->requests = n;
     st->total_s = steady_s() - t0;
   }
   return 0;
 }
-
 
 }  // extern "C"

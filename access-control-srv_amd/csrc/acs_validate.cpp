@@ -77,8 +77,18 @@ int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_
 
 // Batch checks for the host-buffer entry points.  SoA batches (+ optional lines equal to
 // their rows) and compact batches (lines + extension records) alike.
+int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
+                              uint32_t rx_rows_min, uint32_t* arena_end);
+
 int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
                              uint32_t rx_rows_min) {
+  return acs_internal_check_batch2(b, n_sets, n_pols, n_rules, rx_rows_min, nullptr);
+}
+
+// arena_end (optional, [n]): one past the last arena word request i's records occupy (the
+// multi-device split uploads each shard's arena words only).
+int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
+                              uint32_t rx_rows_min, uint32_t* arena_end) {
   const size_t n = b->n;
   if (n == 0) return 0;
   const bool compact = b->hdr == nullptr;
@@ -167,6 +177,7 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
     if (nro > MAX_ROOTS || nh > MAX_HRKEYS || ns > MAX_SLOTS) return bad("batch: arena header", i);
     const size_t head = 2 + 3 * (size_t)ng + 2 * (size_t)nre + nro + nh + ns + 3 * (size_t)nt;
     if (head > room) return bad("batch: arena header", i);
+    size_t used = head;  // words of this request's records past its offset
     const uint32_t* slotoff = ar + 2 + 3 * ng + 2 * nre + nro + nh;
     const uint32_t* tse = slotoff + ns;
     for (uint32_t s = 0; s < ns; ++s) {  // [owners_empty, n_owners, owner...]
@@ -179,11 +190,14 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
         at += 2 + 3 * (size_t)(ar[at] >> 8);
         if (at > room) return bad("batch: arena owner record", i);
       }
+      if (at > used) used = at;
     }
     for (uint32_t e = 0; e < nt; ++e) {  // (se, n_inst, inst_rel_off) -> n_inst x 2
       const uint32_t ni = tse[3 * e + 1];
       if (ni > 32 || (size_t)tse[3 * e + 2] + 2 * (size_t)ni > room) return bad("batch: arena instance list", i);
+      if ((size_t)tse[3 * e + 2] + 2 * (size_t)ni > used) used = (size_t)tse[3 * e + 2] + 2 * (size_t)ni;
     }
+    if (arena_end) arena_end[i] = (uint32_t)(o + used);
     const uint32_t ent = (hd.flags >> RQ_ENT_SHIFT) & 7u;
     const uint32_t e0 = ent >= 1 && ent <= 6 ? ent - 1 : (uint32_t)QMAX;  // the lone entity attr's slot
     if (compact && e0 < QMAX && e0 >= hd.nres) return bad("batch: entity slot", i);
@@ -199,6 +213,32 @@ int acs_internal_check_batch(const acs_req_batch* b, uint32_t n_sets, uint32_t n
     }
   }
   return 0;
+}
+
+// The slices of a compact batch that requests [lo, hi) read (the multi-device split uploads
+// only these): plan[0..1] = arena words [a0, a1), plan[2..3] = extension words [e0, e1).
+// arena_end from acs_internal_check_batch2.  Empty ranges are [0, 0).
+void acs_internal_shard_plan(const acs_req_batch* b, size_t lo, size_t hi, const uint32_t* arena_end, size_t plan[4]) {
+  const ReqLine* L = (const ReqLine*)b->lines;
+  size_t a0 = ~size_t(0), a1 = 0, e0 = ~size_t(0), e1 = 0;
+  for (size_t i = lo; i < hi; ++i) {
+    const ReqHdr& h = L[i].h;
+    if (arena_end[i] > h.arena_off) {
+      a0 = h.arena_off < a0 ? h.arena_off : a0;
+      a1 = arena_end[i] > a1 ? arena_end[i] : a1;
+    }
+    if (L[i].ext) {
+      const size_t x = (size_t)(L[i].ext - 1) * 4, w = ext_geom(h.nres, h.nsubj, h.nact, h.nroles).words;
+      e0 = x < e0 ? x : e0;
+      e1 = x + w > e1 ? x + w : e1;
+    }
+  }
+  if (a0 > a1) a0 = a1 = 0;
+  if (e0 > e1) e0 = e1 = 0;
+  plan[0] = a0;
+  plan[1] = a1;
+  plan[2] = e0;
+  plan[3] = e1;
 }
 
 }  // extern "C"

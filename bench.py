@@ -207,7 +207,7 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
     n = sb.batch.n
     want_n = max(1, int(round(fraction * n)))
     idx = np.random.default_rng(1234).permutation(n)[:want_n]
-    chunk = {"c2": 50_000, "c3": 10_000}.get(kind, 16)
+    chunk = {"c2": 50_000, "c3": 10_000}.get(kind, 256)
     done = busy = mism = unsup = host = 0
     wall0 = time.perf_counter()
     while done < len(idx) and busy < seconds and time.perf_counter() - wall0 < 2 * seconds + 30:
@@ -651,7 +651,7 @@ def main():
             line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:
             log("oracle parity + CPU baseline (C++ oracle)")
-            frac = args.parity_fraction if kind in ("c2", "c3") else 64 / n  # c5: 1M rules, a bounded sample
+            frac = args.parity_fraction if kind in ("c2", "c3") else 1000 / n  # c5: 1M rules, 1000 requests
             cb, par = oracle_parity(kind, doc, sb, dec, cs, frac, args.cpu_seconds)
             line["cpu_baseline"] = cb
             line["parity"] = par

@@ -794,8 +794,34 @@ struct Oracle {
     t.rule_role = rule_role;
   }
 
-  // namespace / RegExp entity test (:528-566, hierarchicalScope.ts:64-101) -> (reset, hit)
+  // namespace / RegExp entity test (:528-566, hierarchicalScope.ts:64-101) -> (reset, hit).
+  // A pure function of the two strings: memoised per thread by their contents (a 1M-rule
+  // store asks for the same (rule value, request value) pairs again and again).
   std::pair<bool, bool> regex_entity(VP rule_value, VP req_value) const {
+    if (rule_value->t != T::Str || req_value->t != T::Str) return regex_entity_eval(rule_value, req_value);
+    thread_local std::unordered_map<std::string, int> memo;  // 0..3: reset<<1 | hit; 4: unsupported
+    std::string key;
+    key.reserve(rule_value->s.size() + req_value->s.size() + 1);
+    key += rule_value->s;
+    key += '\0';
+    key += req_value->s;
+    auto it = memo.find(key);
+    if (it == memo.end()) {
+      int code;
+      try {
+        const auto rh = regex_entity_eval(rule_value, req_value);
+        code = (rh.first ? 2 : 0) | (rh.second ? 1 : 0);
+      } catch (const Unsupported&) {
+        code = 4;
+      }
+      if (memo.size() > (1u << 20)) memo.clear();
+      it = memo.emplace(std::move(key), code).first;
+    }
+    if (it->second == 4) unsupported("RegExp pattern outside the restated subset");
+    return {(it->second & 2) != 0, (it->second & 1) != 0};
+  }
+
+  std::pair<bool, bool> regex_entity_eval(VP rule_value, VP req_value) const {
     if (nullish(rule_value)) type_error();  // nsEntityArray[0] of undefined
     const std::string& rv = str_of(rule_value);
     const std::string pattern = rv.substr(last_index_of(rv, ':') + 1);

@@ -60,7 +60,10 @@ def lib():
 
 def _json(v):
     from .acs_oracle import _to_json
-    return json.dumps(_to_json(v), separators=(",", ":")).encode()
+    try:  # plain JSON values (no UNDEF inside): serialised directly (a 1M-rule store: seconds)
+        return json.dumps(v, separators=(",", ":")).encode()
+    except TypeError:
+        return json.dumps(_to_json(v), separators=(",", ":")).encode()
 
 
 class COracle:

@@ -49,7 +49,7 @@ for s in $STEPS; do
     phase3) step phase_c3 900 python tools/phase_prof.py c3 2000000 ;;
     quick4) step bench_c4_quick 900 python bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-pcie ;;
     c4) step bench_c4 900 python bench.py --config c4 --steps 10 --warmup 2 ;;
-    c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 10 --no-pcie ;;
+    c5) step bench_c5 1200 python bench.py --config c5 --steps 5 --warmup 1 --cpu-seconds 150 --no-pcie ;;
     c5shard) step bench_c5_rule_shard 1200 python bench.py --config c5 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
     shard) step bench_rule_shard 600 python bench.py --rule-shard --steps 20 --warmup 3 --no-cpu-baseline ;;
     shard3) step bench_c3_rule_shard 900 python bench.py --config c3 --rule-shard --steps 5 --warmup 1 --no-cpu-baseline ;;
