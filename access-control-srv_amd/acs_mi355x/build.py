@@ -104,7 +104,7 @@ def build_napi(force=False):
         return None
     lib = build_product()
     if force or _stale(NAPI_OUT, [NAPI_SRC, lib, os.path.join(ROOT, "include", "acs_mi355x.h")]):
-        cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+        cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra", "-Wno-unused-parameter",
                "-I", NODE_INC, NAPI_SRC, "-o", NAPI_OUT + ".tmp", "-L", os.path.dirname(lib), "-lacs_mi355x",
                "-Wl,-rpath,$ORIGIN"]
         subprocess.run(cmd, check=True)

@@ -221,6 +221,8 @@ class Pipeline:
         lib.acs_pipeline_free.restype = None
         lib.acs_pipeline_is_allowed.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t,
                                                 C.POINTER(C.c_size_t), C.POINTER(PipelineStats)]
+        lib.acs_pipeline_host_reason.restype = C.c_char_p
+        lib.acs_pipeline_host_reason.argtypes = [C.c_void_p, C.c_size_t]
         self.lib, self._tables, self._codec = lib, tables, codec  # both must outlive the pipeline
         self.h = lib.acs_pipeline_create(tables.h, codec.h, int(threads), int(chunk))
         if not self.h:
@@ -236,7 +238,12 @@ class Pipeline:
                                             C.byref(st)) != 0:
             raise RuntimeError(last_error(self.lib))
         stats = {k: getattr(st, k) for k, _ in PipelineStats._fields_}
-        return out[:n.value], stats
+        out = out[:n.value]
+        self.host_reasons = {}
+        for i in np.flatnonzero((out["flags"] & np.uint8(L.OF_HOST_REQ)) != 0):
+            r = self.lib.acs_pipeline_host_reason(self.h, int(i))
+            self.host_reasons[int(i)] = r.decode() if r else None
+        return out, stats
 
     def close(self):
         if self.h:

@@ -36,7 +36,8 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_codec_free", "acs_codec_set_subject_scopes", "acs_codec_evict_subject", "acs_codec_encode",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",
-           "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_device_list"]
+           "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_device_list",
+           "acs_pipeline_host_reason"]
 
 
 class ShardC(C.Structure):

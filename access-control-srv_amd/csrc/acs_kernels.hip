@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -1333,6 +1334,7 @@ struct acs_pipeline {
   };
   std::vector<Slot> slot;  // two per device: chunk k -> device k % D, slot (k / D) % 2
   std::mutex mu;           // one run at a time per pipeline
+  std::unordered_map<size_t, std::string> reasons;  // host-path requests of the last run
 };
 
 namespace {
@@ -1342,7 +1344,7 @@ double steady_s() {
 }
 
 // Finish slot S: wait for its chunk, copy its records out, free its batch.
-int pipeline_retire(acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats* st) {
+int pipeline_retire(acs_pipeline* p, acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats* st) {
   if (!S.busy) return 0;
   const double w0 = steady_s();
   HIP_OK(hipEventSynchronize(S.done));
@@ -1350,10 +1352,14 @@ int pipeline_retire(acs_pipeline::Slot& S, acs_decision* out, acs_pipeline_stats
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, S.ev0, S.ev1));
   std::memcpy(out + S.lo, S.stage, S.n * sizeof(acs_decision));
+  for (size_t i = 0; i < S.n; ++i)
+    if (S.stage[i].flags & ACS_OF_HOST_REQ) {
+      const char* why = acs_codec_batch_reason(S.batch, (uint32_t)i);
+      p->reasons[S.lo + i] = why ? why : "host path";
+    }
   if (st) {
     st->wait_s += w1 - w0;
     st->gpu_ms += ms;
-    for (size_t i = 0; i < S.n; ++i) st->host_requests += (S.stage[i].flags & ACS_OF_HOST_REQ) ? 1u : 0u;
   }
   acs_codec_batch_free(S.batch);
   S.batch = nullptr;
@@ -1415,6 +1421,7 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
   if (!p || (!json && len) || !n_out) return fail("acs_pipeline_is_allowed: null argument");
   std::lock_guard<std::mutex> lock(p->mu);
   if (st) *st = acs_pipeline_stats{};
+  p->reasons.clear();
   const double t0 = steady_s();
   size_t n = 0;
   acs_internal_items* items = acs_internal_split(json, len, p->threads, &n);
@@ -1434,7 +1441,7 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     if (!b) return -1;
     if (st) st->encode_s += steady_s() - e0;
     acs_pipeline::Slot& S = p->slot[2 * (k % D) + (k / D) % 2];
-    if (pipeline_retire(S, out, st)) {  // this slot's previous chunk
+    if (pipeline_retire(p, S, out, st)) {  // this slot's previous chunk
       acs_codec_batch_free(b);
       return -1;
     }
@@ -1472,13 +1479,20 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     }
   }
   for (auto& S : p->slot)
-    if (pipeline_retire(S, out, st)) return -1;
+    if (pipeline_retire(p, S, out, st)) return -1;
   HIP_OK(hipSetDevice(p->t->device));
   if (st) {
     st->requests = n;
+    st->host_requests = p->reasons.size();
     st->total_s = steady_s() - t0;
   }
   return 0;
+}
+
+const char* acs_pipeline_host_reason(acs_pipeline* p, size_t i) {
+  if (!p) return nullptr;
+  auto it = p->reasons.find(i);
+  return it == p->reasons.end() ? nullptr : it->second.c_str();
 }
 
 }  // extern "C"

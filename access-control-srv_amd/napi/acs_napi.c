@@ -9,6 +9,8 @@
  * JS surface:
  *   compileStore(storeJson, urnsJson, casJson) -> Uint8Array   acs_store_compile
  *   compile(blob: Uint8Array, device?) -> tables                acs_compile
+ *     (device = [d0, d1, ...]: one image per device, acs_compile_multi)
+ *   devices(tables) -> number[]                                 acs_device_list
  *   free(tables)                                                acs_free (deferred past in-flight work)
  *   codecCreate(blob) -> codec                                  acs_codec_create
  *   codecFree(codec), batchFree(batch)                          acs_codec_free / acs_codec_batch_free
@@ -20,6 +22,11 @@
  *   batchString(batch, id) -> string | null | undefined         acs_codec_string
  *   decideAsync(tables, codec, json, threads?) -> Promise<{records, host}>
  *                                    encode + acs_is_allowed on the libuv pool, one step
+ *   pipelineCreate(tables, codec, threads?, chunk?) -> pipeline acs_pipeline_create
+ *   pipelineFree(pipeline)                                      acs_pipeline_free (after in-flight work)
+ *   pipelineDecideAsync(pipeline, json) -> Promise<{records, host, stats}>
+ *                                    acs_pipeline_is_allowed on the libuv pool: encode of
+ *                                    chunk k+1 overlapped with the device work of chunk k
  *   isAllowed(tables, batch) -> Uint8Array(8 n)                 acs_is_allowed (sync)
  *   isAllowedAsync(tables, batch) -> Promise<Uint8Array>        same, on the libuv pool
  *   whatIsAllowed(tables, batch) -> {bits, obl, oblN, out}      acs_what_is_allowed
@@ -40,6 +47,7 @@
  */
 #define NAPI_VERSION 8
 #include <node_api.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -78,8 +86,8 @@ static napi_value throw_acs(napi_env env, const char* what) {
  * codecFree(codec), batchFree(batch) — and whatever is still registered when the environment
  * is torn down is released by its cleanup hook (objects with work in flight are left to the
  * process exit).  Each environment (main thread, worker_threads) has its own registry. */
-enum { H_TABLES = 1, H_CODEC = 2, H_BATCH = 3 };
-static const char* const KIND_KEY[4] = {"", "acsTables", "acsCodec", "acsBatch"};
+enum { H_TABLES = 1, H_CODEC = 2, H_BATCH = 3, H_PIPELINE = 4 };
+static const char* const KIND_KEY[5] = {"", "acsTables", "acsCodec", "acsBatch", "acsPipeline"};
 
 typedef struct env_state env_state;
 
@@ -108,6 +116,15 @@ typedef struct {
 } batch_h;
 
 typedef struct {
+  obj_base base;
+  acs_pipeline* p;
+  tables_h* tables; /* counted references: both outlive the pipeline */
+  codec_h* codec;
+  int inflight;      /* queued / running pipelineDecideAsync work */
+  pthread_mutex_t mu; /* a run and the reading of its host reasons, together */
+} pipeline_h;
+
+typedef struct {
   int kind; /* 0: never used */
   uint32_t gen;
   obj_base* obj; /* NULL: freed (slot reusable) */
@@ -130,6 +147,15 @@ static void obj_release(obj_base* o) {
     codec_h* h = (codec_h*)o;
     if (h->c) acs_codec_free(h->c);
     h->c = NULL;
+  } else if (o->kind == H_PIPELINE) {
+    pipeline_h* h = (pipeline_h*)o;
+    if (h->p) acs_pipeline_free(h->p); /* before its tables and codec */
+    h->p = NULL;
+    pthread_mutex_destroy(&h->mu);
+    if (h->tables) obj_unref(&h->tables->base);
+    if (h->codec) obj_unref(&h->codec->base);
+    h->tables = NULL;
+    h->codec = NULL;
   } else if (o->kind == H_BATCH) {
     batch_h* h = (batch_h*)o;
     if (h->b) acs_codec_batch_free(h->b); /* before its codec */
@@ -148,9 +174,9 @@ static void obj_unref(obj_base* o) {
 static void on_env_exit(void* arg) {
   env_state* st = (env_state*)arg;
   st->dead = 1;
-  /* batches first (they hold their codec), then codecs and tables */
-  static const int order[3] = {H_BATCH, H_CODEC, H_TABLES};
-  for (int k = 0; k < 3; ++k)
+  /* pipelines and batches first (they hold their codec / tables), then codecs and tables */
+  static const int order[4] = {H_PIPELINE, H_BATCH, H_CODEC, H_TABLES};
+  for (int k = 0; k < 4; ++k)
     for (uint32_t i = 0; i < st->n; ++i) {
       slot_t* s = &st->slots[i];
       if (!s->obj || s->obj->kind != order[k]) continue;
@@ -158,6 +184,7 @@ static void on_env_exit(void* arg) {
       s->obj = NULL;
       o->slot = UINT32_MAX;
       if (o->kind == H_TABLES && ((tables_h*)o)->inflight) continue; /* the pool still uses it */
+      if (o->kind == H_PIPELINE && ((pipeline_h*)o)->inflight) continue;
       obj_unref(o);
     }
 }
@@ -519,14 +546,35 @@ static napi_value js_compile(napi_env env, napi_callback_info info) {
   napi_value argv[2], out;
   void* blob;
   size_t len;
-  int32_t device = 0;
+  int32_t device = 0, devs[64];
+  uint32_t n_devs = 0;
+  bool is_array = false;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   if (argc < 1 || get_bytes(env, argv[0], &blob, &len) || !blob) {
-    napi_throw_type_error(env, NULL, "compile(blob: Uint8Array, device?: number)");
+    napi_throw_type_error(env, NULL, "compile(blob: Uint8Array, device?: number | number[])");
     return NULL;
   }
-  if (argc > 1) CHECK(env, napi_get_value_int32(env, argv[1], &device));
-  acs_tables* t = acs_compile(blob, len, device);
+  if (argc > 1) {
+    CHECK(env, napi_is_array(env, argv[1], &is_array));
+    if (is_array) {
+      CHECK(env, napi_get_array_length(env, argv[1], &n_devs));
+      if (n_devs < 1 || n_devs > 64) {
+        napi_throw_range_error(env, NULL, "compile: 1..64 devices");
+        return NULL;
+      }
+      for (uint32_t k = 0; k < n_devs; ++k) {
+        napi_value e;
+        CHECK(env, napi_get_element(env, argv[1], k, &e));
+        if (napi_get_value_int32(env, e, &devs[k]) != napi_ok) {
+          napi_throw_type_error(env, NULL, "compile: device ids must be numbers");
+          return NULL;
+        }
+      }
+    } else {
+      CHECK(env, napi_get_value_int32(env, argv[1], &device));
+    }
+  }
+  acs_tables* t = is_array ? acs_compile_multi(blob, len, devs, (int)n_devs) : acs_compile(blob, len, device);
   if (!t) return throw_acs(env, "acs_compile");
   tables_h* h = (tables_h*)calloc(1, sizeof *h);
   if (!h) {
@@ -536,6 +584,28 @@ static napi_value js_compile(napi_env env, napi_callback_info info) {
   }
   h->t = t;
   out = make_handle(env, &h->base, H_TABLES);
+  return out;
+}
+
+static napi_value js_devices(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int freed = 0;
+  tables_h* h = argc > 0 ? (tables_h*)lookup(env, argv[0], H_TABLES, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "devices(tables)");
+    return NULL;
+  }
+  int devs[64];
+  const int m = acs_device_list(h->t, devs, 64);
+  if (m < 0) return throw_acs(env, "acs_device_list");
+  CHECK(env, napi_create_array_with_length(env, (size_t)m, &out));
+  for (int k = 0; k < m && k < 64; ++k) {
+    napi_value e;
+    CHECK(env, napi_create_int32(env, devs[k], &e));
+    CHECK(env, napi_set_element(env, out, (uint32_t)k, e));
+  }
   return out;
 }
 
@@ -767,6 +837,197 @@ static napi_value js_decide_async(napi_env env, napi_callback_info info) {
   th->inflight++;
   th->base.refs++;
   ch->base.refs++;
+  CHECK(env, napi_queue_async_work(env, r->work));
+  return promise;
+}
+
+/* ------------------------------------------------------------------ pipeline */
+static napi_value js_pipeline_create(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  int32_t threads = 4;
+  uint32_t chunk = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  if (argc < 2) {
+    napi_throw_type_error(env, NULL, "pipelineCreate(tables, codec, threads?, chunk?)");
+    return NULL;
+  }
+  tables_h* th = get_tables(env, argv[0]);
+  codec_h* ch = th ? get_codec(env, argv[1]) : NULL;
+  if (!th || !ch) return NULL;
+  if (argc > 2) CHECK(env, napi_get_value_int32(env, argv[2], &threads));
+  if (argc > 3) CHECK(env, napi_get_value_uint32(env, argv[3], &chunk));
+  acs_pipeline* p = acs_pipeline_create(th->t, ch->c, threads, chunk);
+  if (!p) return throw_acs(env, "acs_pipeline_create");
+  pipeline_h* h = (pipeline_h*)calloc(1, sizeof *h);
+  if (!h || pthread_mutex_init(&h->mu, NULL) != 0) {
+    free(h);
+    acs_pipeline_free(p);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  h->p = p;
+  h->tables = th;
+  h->codec = ch;
+  th->base.refs++;
+  ch->base.refs++;
+  return make_handle(env, &h->base, H_PIPELINE);
+}
+
+static napi_value js_pipeline_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int freed = 0;
+  obj_base* h = argc > 0 ? lookup(env, argv[0], H_PIPELINE, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "pipelineFree(pipeline)");
+    return NULL;
+  }
+  handle_free(h);
+  return NULL;
+}
+
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref keep_text;
+  pipeline_h* ph;
+  char* text;
+  size_t text_len;
+  int text_owned;
+  acs_decision* out;
+  size_t n;
+  size_t n_host;
+  uint32_t* host_idx;
+  char** host_why;
+  acs_pipeline_stats st;
+  int rc;
+  char err[512];
+} pipe_req;
+
+static void exec_pipeline(napi_env env, void* data) {
+  (void)env;
+  pipe_req* r = (pipe_req*)data;
+  pthread_mutex_lock(&r->ph->mu);
+  /* the request count is known only once the array is delimited: a first guess, then (an
+   * error before any encoding, with the count) the exact size */
+  size_t cap = r->text_len / 32 + 16;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    r->out = (acs_decision*)malloc(cap * sizeof(acs_decision) + 1);
+    if (!r->out) {
+      r->rc = -1;
+      snprintf(r->err, sizeof r->err, "out of memory");
+      break;
+    }
+    size_t n = 0;
+    r->rc = acs_pipeline_is_allowed(r->ph->p, r->text, r->text_len, r->out, cap, &n, &r->st);
+    if (r->rc == 0) {
+      r->n = n;
+      break;
+    }
+    snprintf(r->err, sizeof r->err, "acs_pipeline_is_allowed: %s", acs_last_error());
+    free(r->out);
+    r->out = NULL;
+    if (n <= cap) break;
+    cap = n;
+  }
+  if (r->rc == 0) {
+    for (size_t i = 0; i < r->n; ++i) r->n_host += (r->out[i].flags & ACS_OF_HOST_REQ) ? 1 : 0;
+    if (r->n_host) {
+      r->host_idx = (uint32_t*)calloc(r->n_host, sizeof *r->host_idx);
+      r->host_why = (char**)calloc(r->n_host, sizeof *r->host_why);
+      size_t k = 0;
+      for (size_t i = 0; i < r->n && r->host_idx && r->host_why; ++i) {
+        if (!(r->out[i].flags & ACS_OF_HOST_REQ)) continue;
+        const char* why = acs_pipeline_host_reason(r->ph->p, i);
+        r->host_idx[k] = (uint32_t)i;
+        const char* w = why ? why : "host path";
+        const size_t wl = strlen(w);
+        r->host_why[k] = (char*)malloc(wl + 1);
+        if (r->host_why[k]) memcpy(r->host_why[k], w, wl + 1);
+        ++k;
+      }
+      if (!r->host_idx || !r->host_why) r->n_host = 0;
+    }
+  }
+  pthread_mutex_unlock(&r->ph->mu);
+}
+
+static void done_pipeline(napi_env env, napi_status status, void* data) {
+  pipe_req* r = (pipe_req*)data;
+  if (status == napi_ok && r->rc == 0) {
+    napi_value res, rec, host, stats, v;
+    void* d;
+    napi_create_object(env, &res);
+    rec = new_u8(env, r->n * sizeof(acs_decision), &d);
+    if (rec && r->n) memcpy(d, r->out, r->n * sizeof(acs_decision));
+    napi_set_named_property(env, res, "records", rec);
+    napi_create_object(env, &host);
+    for (size_t k = 0; k < r->n_host; ++k) {
+      char key[16];
+      snprintf(key, sizeof key, "%u", r->host_idx[k]);
+      napi_create_string_utf8(env, r->host_why[k] ? r->host_why[k] : "host path", NAPI_AUTO_LENGTH, &v);
+      napi_set_named_property(env, host, key, v);
+    }
+    napi_set_named_property(env, res, "host", host);
+    napi_create_object(env, &stats);
+    const double sv[8] = {r->st.encode_s, r->st.wait_s, r->st.total_s, r->st.gpu_ms, r->st.upload_bytes,
+                          (double)r->st.requests, (double)r->st.chunks, (double)r->st.host_requests};
+    static const char* const sk[8] = {"encodeS", "waitS", "totalS", "gpuMs", "uploadBytes", "requests", "chunks",
+                                      "hostRequests"};
+    for (int k = 0; k < 8; ++k) {
+      napi_create_double(env, sv[k], &v);
+      napi_set_named_property(env, stats, sk[k], v);
+    }
+    napi_set_named_property(env, res, "stats", stats);
+    napi_resolve_deferred(env, r->deferred, res);
+  } else {
+    napi_value msg, err;
+    napi_create_string_utf8(env, r->rc ? r->err : "async work cancelled", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, r->deferred, err);
+  }
+  r->ph->inflight--;
+  obj_unref(&r->ph->base);
+  for (size_t k = 0; k < r->n_host; ++k) free(r->host_why[k]);
+  free(r->host_why);
+  free(r->host_idx);
+  free(r->out);
+  if (r->text_owned) free(r->text);
+  if (r->keep_text) napi_delete_reference(env, r->keep_text);
+  napi_delete_async_work(env, r->work);
+  free(r);
+}
+
+static napi_value js_pipeline_decide_async(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], promise, name;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int freed = 0;
+  pipeline_h* ph = argc == 2 ? (pipeline_h*)lookup(env, argv[0], H_PIPELINE, &freed) : NULL;
+  if (!ph) {
+    if (freed) napi_throw_error(env, NULL, "pipeline handle already freed");
+    else napi_throw_type_error(env, NULL, "pipelineDecideAsync(pipeline, json)");
+    return NULL;
+  }
+  pipe_req* r = (pipe_req*)calloc(1, sizeof *r);
+  if (!r) {
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  r->ph = ph;
+  if (get_text(env, argv[1], &r->text, &r->text_len, &r->text_owned)) {
+    free(r);
+    napi_throw_type_error(env, NULL, "pipelineDecideAsync: json must be a string or bytes");
+    return NULL;
+  }
+  if (!r->text_owned) CHECK(env, napi_create_reference(env, argv[1], 1, &r->keep_text)); /* borrowed bytes */
+  CHECK(env, napi_create_promise(env, &r->deferred, &promise));
+  CHECK(env, napi_create_string_utf8(env, "acs_pipeline", NAPI_AUTO_LENGTH, &name));
+  CHECK(env, napi_create_async_work(env, NULL, name, exec_pipeline, done_pipeline, r, &r->work));
+  ph->inflight++;
+  ph->base.refs++;
   CHECK(env, napi_queue_async_work(env, r->work));
   return promise;
 }
@@ -1079,6 +1340,10 @@ static napi_value init(napi_env env, napi_value exports) {
       {"batchInfo", NULL, js_batch_info, NULL, NULL, NULL, napi_enumerable, NULL},
       {"batchString", NULL, js_batch_string, NULL, NULL, NULL, napi_enumerable, NULL},
       {"decideAsync", NULL, js_decide_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pipelineCreate", NULL, js_pipeline_create, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pipelineFree", NULL, js_pipeline_free, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"pipelineDecideAsync", NULL, js_pipeline_decide_async, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"devices", NULL, js_devices, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isAllowed", NULL, js_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},
       {"isAllowedAsync", NULL, js_is_allowed_async, NULL, NULL, NULL, napi_enumerable, NULL},
       {"whatIsAllowed", NULL, js_what_is_allowed, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -13,7 +13,11 @@
 //
 // The policySets Map is snapshotted (snapshotStore) and compiled natively (acs_store_compile,
 // byte-identical to acs_mi355x/compiler.py); requests go to the native codec as one JSON
-// text (acs_codec_encode on the libuv pool) and straight on to the kernels (decideAsync).
+// text (acs_codec_encode on the libuv pool) and straight on to the kernels (decideAsync);
+// a batch of at least `pipelineBytes` of JSON goes through the decision pipeline instead
+// (pipelineDecideAsync: encode of chunk k+1 overlapped with the device work of chunk k).
+// `device` may be an array of device ids: one image per device, large batches split
+// across them (acs_compile_multi).
 // Requests the packed form cannot carry (a JS rule condition, a subject token to resolve, a
 // RegExp outside the precomputed subset) go to
 // `hostEvaluator` — normally the reference's own AccessController — or, without one, come
@@ -122,8 +126,11 @@ class GpuAccessController {
   // combiningAlgorithms: policies.options.combiningAlgorithms (array of {urn, method}).
   constructor(policySets, urns, combiningAlgorithms, options) {
     const o = options || {};
-    this.device = o.device || 0;
+    this.device = o.device || 0; // a device id, or an array of them
     this.threads = o.threads || 4;
+    this.chunk = o.chunk || 0; // pipeline chunk (requests); 0: the library's default
+    this.pipelineBytes = o.pipelineBytes === undefined ? (1 << 20) : o.pipelineBytes; // null: never
+    this.pipeline = null;
     this.hostEvaluator = o.hostEvaluator || null;
     this.urns = urns instanceof Map ? Object.fromEntries(urns) : urns;
     this.cas = combiningAlgorithms;
@@ -139,11 +146,14 @@ class GpuAccessController {
     const blob = addon.compileStore(snapshotStore(policySets), JSON.stringify(this.urns), JSON.stringify(this.cas));
     const tables = addon.compile(blob, this.device);
     const codec = addon.codecCreate(blob);
+    const pipeline = this.pipelineBytes === null ? null : addon.pipelineCreate(tables, codec, this.threads, this.chunk);
     // the old handles: released once the batches still in flight are done with them
+    if (this.pipeline) addon.pipelineFree(this.pipeline);
     if (this.tables) addon.free(this.tables);
     if (this.codec) addon.codecFree(this.codec);
     this.tables = tables;
     this.codec = codec;
+    this.pipeline = pipeline;
     this.ec = ecDecoder(codec);
     this.index = nodeIndex(policySets);
     this.scopes = this.scopes || new Map();
@@ -166,10 +176,17 @@ class GpuAccessController {
 
   // Releases the GPU tables and the codec (handles are freed explicitly, napi/acs_napi.c).
   close() {
+    if (this.pipeline) addon.pipelineFree(this.pipeline);
     if (this.tables) addon.free(this.tables);
     if (this.codec) addon.codecFree(this.codec);
+    this.pipeline = null;
     this.tables = null;
     this.codec = null;
+  }
+
+  // The devices the tables live on (primary first).
+  devices() {
+    return addon.devices(this.tables);
   }
 
   _host(op, request, err) {
@@ -204,7 +221,10 @@ class GpuAccessController {
   async isAllowedBatch(requests) {
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
     const ec = this.ec; // the codec's table: refresh() may swap this.ec while the batch is in flight
-    const r = await addon.decideAsync(this.tables, this.codec, text, this.threads);
+    const bytes = typeof text === 'string' ? text.length : text.byteLength;
+    const r = this.pipeline && bytes >= this.pipelineBytes
+      ? await addon.pipelineDecideAsync(this.pipeline, text)
+      : await addon.decideAsync(this.tables, this.codec, text, this.threads);
     const n = r.records.length / REC_BYTES;
     this.stats.requests += n;
     const out = new Array(n);

@@ -256,10 +256,13 @@ void acs_codec_batch_free(acs_codec_batch* b);
  * arriving as JSON text, end to end: the request array is delimited once and cut into chunks
  * of `chunk` requests; chunk k+1 is encoded (acs_codec) on `threads` host threads while chunk
  * k is uploaded from the codec's page-locked blocks, sorted and decided (K1) and its records
- * downloaded, on one of the pipeline's two streams (each with its own device workspace).
- * out[0..n) receives the records in request order (out_cap >= n, else an error with *n_out set).
- * Requests flagged for the host path carry ACS_OF_HOST_REQ (acs_codec_encode of that request
- * gives the reason).  One run at a time per pipeline; the tables and codec must outlive it. */
+ * downloaded, on one of the pipeline's two streams per device (each with its own device
+ * workspace; a multi-device handle's chunks go round the devices).
+ * out[0..n) receives the records in request order (out_cap >= n, else an error with *n_out set,
+ * before any encoding).  Requests flagged for the host path carry ACS_OF_HOST_REQ;
+ * acs_pipeline_host_reason gives the codec's reason for request i of the last run (NULL for a
+ * request that is not one), valid until the next run.  One run at a time per pipeline; the
+ * tables and codec must outlive it. */
 typedef struct acs_pipeline acs_pipeline;
 typedef struct {
   double encode_s;      /* host time encoding (all chunks) */
@@ -273,6 +276,7 @@ acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint
 void acs_pipeline_free(acs_pipeline* p);
 int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_decision* out, size_t out_cap,
                             size_t* n_out, acs_pipeline_stats* st);
+const char* acs_pipeline_host_reason(acs_pipeline* p, size_t i);
 
 const char* acs_last_error(void);
 int acs_layout_sizes(uint32_t* out, int n); /* sizeof of the 5 packed structs, for host checks */

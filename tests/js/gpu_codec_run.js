@@ -70,6 +70,16 @@ const enc = (x) => (x instanceof Error ? { $error: x.name, reason: x.reason } : 
     const ia = await ctl.isAllowedBatch(c.isAllowed);
     const wa = await ctl.whatIsAllowedBatch(c.whatIsAllowed);
     const res = { isAllowed: ia.map(enc), whatIsAllowed: wa.map(enc), stats: ctl.stats };
+    {  // the same requests through the decision pipeline (3-request chunks) on a handle
+       // replicated twice on device 0: the same answers
+      const opts2 = Object.assign({}, opts, { pipelineBytes: 0, chunk: 3, device: [0, 0] });
+      const ctl2 = new g.GpuAccessController(maps, c.urns, c.cas, opts2);
+      for (const key of Object.keys(c.scopes || {})) ctl2.setSubjectScopes(key, c.scopes[key]);
+      const ia2 = await ctl2.isAllowedBatch(c.isAllowed);
+      res.pipelineSame = JSON.stringify(ia2.map(enc)) === JSON.stringify(res.isAllowed);
+      res.devices = ctl2.devices();
+      ctl2.close();
+    }
     if (c.evict) {
       res.evicted = c.evict.map((key) => ctl.evictSubject(key));
       res.afterEvict = (await ctl.isAllowedBatch(c.isAllowed)).map(enc);

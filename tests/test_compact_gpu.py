@@ -113,6 +113,8 @@ def test_pipeline_errors_and_host_requests_gpu():
     got, st = p.is_allowed(json.dumps(reqs).encode(), 3)
     assert (got["flags"][0] & L.OF_HOST_REQ) and st["host_requests"] == 1
     assert got["flags"][2] & L.OF_NO_TARGET
+    want = codec.encode(json.dumps(reqs).encode()).host_reasons
+    assert p.host_reasons == want and list(want) == [0] and want[0]
     got, _ = p.is_allowed(b"[]", 0)
     assert len(got) == 0
     p.close()

@@ -50,7 +50,11 @@ def _run(tmp, cases, mode, timeout=600):
     tmp.joinpath("cases.json").write_text(json.dumps(cases))
     r = subprocess.run([NODE, RUNNER, str(tmp), mode], capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, (r.returncode, r.stderr[-4000:])
-    return json.loads(tmp.joinpath("out.json").read_text())
+    out = json.loads(tmp.joinpath("out.json").read_text())
+    if mode == "decide":  # every case also ran through the pipeline on a two-replica handle
+        for k, res in enumerate(out):
+            assert "compileError" in res or (res["pipelineSame"] and res["devices"] == [0, 0]), k
+    return out
 
 
 def _kat_groups():

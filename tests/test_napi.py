@@ -34,7 +34,8 @@ def test_addon_loads_with_surface():
     assert info["keys"] == sorted(["compileStore", "compile", "free", "codecCreate", "codecFree", "batchFree",
                                    "codecSetSubjectScopes",
                                    "codecEvictSubject", "codecEcValues", "encode", "batchInfo", "batchString",
-                                   "decideAsync", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
+                                   "decideAsync", "pipelineCreate", "pipelineFree", "pipelineDecideAsync",
+                                   "devices", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
                                    "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
     assert info["sizes"] == [64, 16, 16, 16, 8]
     assert "magic" in r.stdout.splitlines()[1]  # a bad image is rejected with acs_last_error's message
