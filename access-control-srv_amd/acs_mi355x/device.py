@@ -86,37 +86,43 @@ def resolve_overflow_device(tables, db: DeviceBatch, bufs, cap: int | None = Non
     OF_OBL_OVERFLOW in ``bufs[3]``): the policy sets cut into ``chunks`` ranges with ``cap``
     entries each, then the still-truncated requests once more at their exact count.  By
     default the ranges are as many (8..64, a power of two) as keep about OBL_PASS_LANES lanes
-    busy, so a few overflowed requests take 1/64 of a traversal, not 1/8.  Returns
-    [(idx [m], cap, obl [chunks][m][cap][2], obl_n [chunks][m])] per pass (int32 tensors; later
-    passes supersede earlier ones).  Syncs the stream to size each pass."""
+    busy, so a few overflowed requests take 1/64 of a traversal, not 1/8.  The index lists
+    come from the library's selection kernels (acs_overflow_index_device: K2's coherence
+    order; acs_overflow_repass_device), each syncing the stream once to size its pass.
+    Returns [(idx [m], cap, obl [chunks][m][cap][2], obl_n [chunks][m])] per pass (int32
+    tensors; later passes supersede earlier ones)."""
     st = stream or torch.cuda.current_stream(db.dev)
+    s = C.c_void_p(st.cuda_stream)
+    lib, n = tables.lib, db.batch.n
     with torch.cuda.stream(st):
-        flags = bufs[3][:, 2]
-        idx = torch.nonzero(flags & L.OF_OBL_OVERFLOW).flatten()
+        idx = torch.empty(max(n, 1), dtype=torch.int32, device=db.dev)
+        m = C.c_size_t(0)
+        if lib.acs_overflow_index_device(tables.h, C.byref(db.struct), bufs[3].data_ptr(), idx.data_ptr(), C.byref(m),
+                                         s) != 0:
+            raise RuntimeError(f"acs_overflow_index_device: {last_error(lib)}")
+        m = int(m.value)
         if chunks is None:
             chunks = 8
-            while chunks < 64 and chunks * 2 * max(idx.numel(), 1) <= OBL_PASS_LANES:
+            while chunks < 64 and chunks * 2 * max(m, 1) <= OBL_PASS_LANES:
                 chunks *= 2
         if cap is None:
             cap = max(128, 8192 // chunks)
-        # request-class order, as K2's coherence sort: a wave then shares its candidate row
-        cls = (db.t["hdr"].view(torch.int32).view(-1, 4)[idx, 0] >> L.RQ_PCOL_SHIFT) & 0xFFFF
-        idx = idx[torch.sort(cls, stable=True).indices].to(torch.int32)
+        idx = idx[:m]
         passes = []
-        while idx.numel():
-            m = idx.numel()
+        while m:
             obl = torch.empty((chunks, m, cap, 2), dtype=torch.int32, device=db.dev)
             obl_n = torch.empty((chunks, m), dtype=torch.int32, device=db.dev)
-            rc = tables.lib.acs_what_is_allowed_obl_device(tables.h, C.byref(db.struct), idx.data_ptr(), m, chunks,
-                                                           cap, obl.data_ptr(), obl_n.data_ptr(),
-                                                           C.c_void_p(st.cuda_stream))
+            rc = lib.acs_what_is_allowed_obl_device(tables.h, C.byref(db.struct), idx.data_ptr(), m, chunks, cap,
+                                                    obl.data_ptr(), obl_n.data_ptr(), s)
             if rc != 0:
-                raise RuntimeError(f"acs_what_is_allowed_obl_device: {last_error(tables.lib)}")
+                raise RuntimeError(f"acs_what_is_allowed_obl_device: {last_error(lib)}")
             passes.append((idx, cap, obl, obl_n))
-            more = (obl_n > cap).any(dim=0)
-            if not bool(more.any()):
-                break
-            idx, cap = idx[more], int(obl_n[:, more].max())
+            nxt = torch.empty(m, dtype=torch.int32, device=db.dev)
+            m2, cap2 = C.c_size_t(0), C.c_uint32(0)
+            if lib.acs_overflow_repass_device(tables.h, obl_n.data_ptr(), idx.data_ptr(), m, chunks, cap,
+                                              nxt.data_ptr(), C.byref(m2), C.byref(cap2), s) != 0:
+                raise RuntimeError(f"acs_overflow_repass_device: {last_error(lib)}")
+            m, cap, idx = int(m2.value), int(cap2.value), nxt[:int(m2.value)]
     return passes
 
 

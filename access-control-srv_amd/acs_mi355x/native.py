@@ -37,7 +37,7 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",
            "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_device_list",
-           "acs_pipeline_host_reason"]
+           "acs_pipeline_host_reason", "acs_overflow_index_device", "acs_overflow_repass_device"]
 
 
 class ShardC(C.Structure):
@@ -68,6 +68,9 @@ def _declare(lib):
     lib.acs_layout_sizes.argtypes = [C.POINTER(u32), C.c_int]
     lib.acs_set_option.argtypes = [vp, C.c_int, C.c_int]
     lib.acs_kernel_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+    lib.acs_overflow_index_device.argtypes = [vp, pb, vp, vp, C.POINTER(C.c_size_t), vp]
+    lib.acs_overflow_repass_device.argtypes = [vp, vp, vp, C.c_size_t, u32, u32, vp, C.POINTER(C.c_size_t),
+                                               C.POINTER(u32), vp]
     lib.acs_shard_keys_device.argtypes = [vp, vp, C.c_size_t, C.POINTER(ShardC), vp, vp]
     lib.acs_shard_decode_device.argtypes = [vp, C.c_size_t, vp, vp]
     return lib

@@ -517,6 +517,141 @@ __global__ __launch_bounds__(BLOCK) void shard_decode_kernel(const uint64_t* __r
   if (i < n) out[i] = shard_decode(keys[i]);
 }
 
+// ---------------------------------------------------------------- stable selection
+// The overflowed-log bookkeeping of the device path: the indices i < n a predicate selects,
+// in index order (count per 2048-item tile -> one-block exclusive scan -> per-tile write,
+// ranked with wave ballots: deterministic, no atomics), plus the largest value of the
+// selected items.
+struct FlaggedRecords {  // decision records carrying `mask`
+  const Decision* d;
+  uint32_t mask;
+  __device__ bool sel(uint32_t i) const { return (d[i].flags & mask) != 0; }
+  __device__ uint32_t val(uint32_t) const { return 0; }
+};
+
+struct TruncatedLogs {  // a pass's obl_n [chunks][m]: some range pushed more than cap
+  const uint32_t* obl_n;
+  uint32_t m, chunks, cap;
+  __device__ uint32_t val(uint32_t j) const {
+    uint32_t v = 0;
+    for (uint32_t c = 0; c < chunks; ++c) {
+      const uint32_t x = obl_n[(size_t)c * m + j];
+      v = x != 0xFFFFFFFFu && x > v ? x : v;  // 0xFFFFFFFF: an index outside the batch
+    }
+    return v;
+  }
+  __device__ bool sel(uint32_t j) const { return val(j) > cap; }
+};
+
+template <class P>
+__global__ __launch_bounds__(BLOCK) void select_count_kernel(P p, uint32_t n, uint32_t* __restrict__ tile_cnt,
+                                                             uint32_t* __restrict__ tile_max) {
+  __shared__ uint32_t sc[BLOCK / 64], sm[BLOCK / 64];
+  uint32_t c = 0, mx = 0;
+  const uint32_t t0 = blockIdx.x * SORT_TILE;
+  for (uint32_t r = 0; r < SORT_ITEMS; ++r) {
+    const uint32_t i = t0 + r * BLOCK + threadIdx.x;
+    if (i < n && p.sel(i)) {
+      ++c;
+      const uint32_t v = p.val(i);
+      mx = v > mx ? v : mx;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    c += __shfl_xor(c, off);
+    const uint32_t o = __shfl_xor(mx, off);
+    mx = o > mx ? o : mx;
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    sc[threadIdx.x >> 6] = c;
+    sm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t tc = 0, tm = 0;
+    for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+      tc += sc[w];
+      tm = sm[w] > tm ? sm[w] : tm;
+    }
+    tile_cnt[blockIdx.x] = tc;
+    tile_max[blockIdx.x] = tm;
+  }
+}
+
+// one block: tile_cnt -> exclusive offsets (in place); total[0] = selected, total[1] = max
+__global__ __launch_bounds__(BLOCK) void select_scan_kernel(uint32_t* __restrict__ tile_cnt,
+                                                            const uint32_t* __restrict__ tile_max, uint32_t nt,
+                                                            uint32_t* __restrict__ total) {
+  __shared__ uint32_t sv[BLOCK];
+  uint32_t carry = 0, mx = 0;
+  for (uint32_t b0 = 0; b0 < nt; b0 += BLOCK) {
+    const uint32_t k = b0 + threadIdx.x;
+    const uint32_t v = k < nt ? tile_cnt[k] : 0u;
+    if (k < nt) mx = tile_max[k] > mx ? tile_max[k] : mx;
+    sv[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t off = 1; off < BLOCK; off <<= 1) {
+      const uint32_t x = threadIdx.x >= off ? sv[threadIdx.x - off] : 0u;
+      __syncthreads();
+      sv[threadIdx.x] += x;
+      __syncthreads();
+    }
+    if (k < nt) tile_cnt[k] = carry + sv[threadIdx.x] - v;
+    carry += sv[BLOCK - 1];
+    __syncthreads();
+  }
+  sv[threadIdx.x] = mx;
+  __syncthreads();
+  for (uint32_t off = BLOCK / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off && sv[threadIdx.x + off] > sv[threadIdx.x]) sv[threadIdx.x] = sv[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    total[0] = carry;
+    total[1] = sv[0];
+  }
+}
+
+// out[offset + rank] = map ? map[i] : i for the selected i, in index order
+template <class P>
+__global__ __launch_bounds__(BLOCK) void select_write_kernel(P p, uint32_t n, const uint32_t* __restrict__ tile_off,
+                                                             const uint32_t* __restrict__ map,
+                                                             uint32_t* __restrict__ out) {
+  __shared__ uint32_t wc[BLOCK / 64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t base = tile_off[blockIdx.x];
+  const uint32_t t0 = blockIdx.x * SORT_TILE;
+  for (uint32_t r = 0; r < SORT_ITEMS; ++r) {
+    if (t0 + r * BLOCK >= n) break;  // block-uniform
+    const uint32_t i = t0 + r * BLOCK + threadIdx.x;
+    const bool s = i < n && p.sel(i);
+    const uint64_t bal = __ballot(s);
+    if (lane == 0) wc[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pos = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+      pos += w < wave ? wc[w] : 0u;
+      tot += wc[w];
+    }
+    if (s) out[pos] = map ? map[i] : i;
+    base += tot;
+    __syncthreads();  // wc is rewritten by the next round
+  }
+}
+
+// keys of the selected requests for the coherence order (sort_key), values = their indices
+__global__ __launch_bounds__(BLOCK) void gather_sort_keys_kernel(Batch B, const uint32_t* __restrict__ idx, uint32_t m,
+                                                                 uint32_t lowbits, uint32_t cbits,
+                                                                 uint32_t* __restrict__ keys,
+                                                                 uint32_t* __restrict__ vals) {
+  const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t i = idx[j];
+  keys[j] = sort_key(B, i, lowbits, cbits);
+  vals[j] = i;
+}
+
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 size_t filter_lds_bytes(const Batch& B) {
@@ -595,6 +730,7 @@ struct acs_tables {
   // host-buffer entry points (internal stream, events, their own workspace) may be called
   // from several host threads at once (e.g. the N-API addon's libuv pool): one at a time
   Workspace hws;
+  Workspace ows;  // acs_overflow_*_device: selection scratch (.out) and the sort (.sort)
   std::mutex mu;
   uint32_t rx_rows_min = 0;  // regex-matrix rows the rule resource attributes read
   // acs_compile_multi: replicas of the same image on further devices (C0); the host-buffer
@@ -810,6 +946,7 @@ void acs_free(acs_tables* t) {
   if (t->stream) (void)hipStreamDestroy(t->stream);
   t->dws.release();
   t->hws.release();
+  t->ows.release();
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
@@ -920,11 +1057,8 @@ int acs_set_option(acs_tables* t, int option, int value) {
   return fail("acs_set_option: unknown option");
 }
 
-// Coherence sort: permutation of request indices ordered by (class, low field).
-static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream_t s, const uint32_t** perm) {
-  *perm = nullptr;
-  if (!t->sort || B.n < 2 * BLOCK) return 0;
-  const size_t n = B.n;
+// Sort-key geometry of a batch: low field bits and the key's end bit.
+static void sort_bits(const Batch& B, uint32_t* lowbits_out, uint32_t* end_bit_out) {
   // Low field: the dense role key with a role factor; otherwise none — a class row already
   // folds in the action filter (measured: 0 low bits time the same as 4 or 8, r01_sort).
   uint32_t lowbits = 0;
@@ -934,21 +1068,29 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
   }
   uint32_t end_bit = lowbits;  // keys < (cand_rows + 1) << lowbits
   while (end_bit < 32 && (uint64_t(B.cand_rows) >> (end_bit - lowbits)) != 0) ++end_bit;
+  *lowbits_out = lowbits;
+  *end_bit_out = end_bit;
+}
+
+static size_t radix_scratch_bytes(size_t n) {
+  const size_t nt = (n + SORT_TILE - 1) / SORT_TILE, ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
+  return 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
+}
+
+// LSD passes over (k0, v0) of n pairs in the scratch `base` (radix_scratch_bytes(n)): pass 0's
+// histogram already written by the caller when hist0; returns the sorted values.
+static int radix_passes(uint32_t* base, size_t n, uint32_t end_bit, bool hist0, hipStream_t s, const uint32_t** vals) {
   const uint32_t passes = end_bit ? (end_bit + 7) / 8 : 1;
   const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
   const uint32_t ng = (nt + SCAN_GROUP - 1) / SCAN_GROUP;
-  const size_t need = 4 * n * sizeof(uint32_t) + (size_t)RADIX * (nt + ng) * sizeof(uint32_t);
-  if (W.sort.reserve(need)) return -1;
-  uint32_t* k0 = (uint32_t*)W.sort.p;
+  uint32_t* k0 = base;
   uint32_t* k1 = k0 + n;
   uint32_t* v0 = k1 + n;
   uint32_t* v1 = v0 + n;
   uint32_t* counts = v1 + n;
   uint32_t* gsum = counts + (size_t)RADIX * nt;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
-  HIP_OK(hipGetLastError());
   for (uint32_t p = 0; p < passes; ++p) {
-    if (p > 0) {
+    if (p > 0 || !hist0) {
       hipLaunchKernelGGL(radix_histogram_kernel, dim3(nt), dim3(BLOCK), 0, s, (const uint32_t*)k0, (uint32_t)n,
                          8 * p, counts);
       HIP_OK(hipGetLastError());
@@ -964,8 +1106,25 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
     std::swap(k0, k1);
     std::swap(v0, v1);
   }
-  *perm = v0;
+  *vals = v0;
   return 0;
+}
+
+// Coherence sort: permutation of request indices ordered by (class, low field).
+static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream_t s, const uint32_t** perm) {
+  *perm = nullptr;
+  if (!t->sort || B.n < 2 * BLOCK) return 0;
+  const size_t n = B.n;
+  uint32_t lowbits, end_bit;
+  sort_bits(B, &lowbits, &end_bit);
+  const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
+  if (W.sort.reserve(radix_scratch_bytes(n))) return -1;
+  uint32_t* k0 = (uint32_t*)W.sort.p;
+  uint32_t* v0 = k0 + 2 * n;
+  uint32_t* counts = k0 + 4 * n;
+  hipLaunchKernelGGL(sort_keys_kernel, dim3(nt), dim3(BLOCK), 0, s, B, lowbits, end_bit - lowbits, k0, v0, counts);
+  HIP_OK(hipGetLastError());
+  return radix_passes(k0, n, end_bit, true, s, perm);
 }
 
 static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
@@ -1044,6 +1203,73 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const 
                       (hipStream_t)stream, filter_form(B), t->view, B, idx, (uint32_t)m, chunks, cap, obl, obl_n);
   HIP_OK(hipGetLastError());
   return 0;
+}
+
+}  // extern "C"
+
+// idx[0..*m) <- the items of p (n of them) selected, in index order (map[i] when map); syncs s.
+// *vmax <- the largest value of a selected item.
+template <class P>
+static int select_device(Workspace& W, const P& p, size_t n, const uint32_t* map, uint32_t* idx, size_t* m,
+                         uint32_t* vmax, hipStream_t s) {
+  const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
+  if (W.out.reserve((2 * (size_t)nt + 4) * sizeof(uint32_t))) return -1;
+  uint32_t* cnt = (uint32_t*)W.out.p;
+  uint32_t* mx = cnt + nt;
+  uint32_t* total = mx + nt;
+  hipLaunchKernelGGL(select_count_kernel<P>, dim3(nt), dim3(BLOCK), 0, s, p, (uint32_t)n, cnt, mx);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(BLOCK), 0, s, cnt, (const uint32_t*)mx, nt, total);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(select_write_kernel<P>, dim3(nt), dim3(BLOCK), 0, s, p, (uint32_t)n, (const uint32_t*)cnt, map,
+                     idx);
+  HIP_OK(hipGetLastError());
+  uint32_t h[2] = {0, 0};
+  HIP_OK(hipMemcpyAsync(h, total, sizeof h, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  *m = h[0];
+  if (vmax) *vmax = h[1];
+  return 0;
+}
+
+extern "C" {
+
+int acs_overflow_index_device(acs_tables* t, const acs_req_batch* b, const acs_decision* out, uint32_t* idx, size_t* m,
+                              void* stream) {
+  if (!t || !b || !m || (b->n && (!out || !idx))) return fail("acs_overflow_index_device: null argument");
+  *m = 0;
+  if (b->n == 0) return 0;
+  const hipStream_t s = (hipStream_t)stream;
+  const Batch B = to_batch(b);
+  const FlaggedRecords p{(const Decision*)out, OF_OBL_OVERFLOW};
+  if (select_device(t->ows, p, B.n, nullptr, idx, m, nullptr, s)) return -1;
+  // the coherence order of K2 (class, low field; stable: request order within a key), so
+  // that a wave of the obligation pass shares its candidate rows
+  if (!t->sort || *m < 2 || !B.cand) return 0;
+  uint32_t lowbits, end_bit;
+  sort_bits(B, &lowbits, &end_bit);
+  if (t->ows.sort.reserve(radix_scratch_bytes(*m))) return -1;
+  uint32_t* k0 = (uint32_t*)t->ows.sort.p;
+  hipLaunchKernelGGL(gather_sort_keys_kernel, dim3((unsigned)((*m + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, B,
+                     (const uint32_t*)idx, (uint32_t)*m, lowbits, end_bit - lowbits, k0, k0 + 2 * *m);
+  HIP_OK(hipGetLastError());
+  const uint32_t* sorted = nullptr;
+  if (radix_passes(k0, *m, end_bit, false, s, &sorted)) return -1;
+  HIP_OK(hipMemcpyAsync(idx, sorted, *m * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+int acs_overflow_repass_device(acs_tables* t, const uint32_t* obl_n, const uint32_t* idx, size_t m, uint32_t chunks,
+                               uint32_t cap, uint32_t* idx_out, size_t* m_out, uint32_t* cap_out, void* stream) {
+  if (!t || !m_out || !cap_out || (m && (!obl_n || !idx || !idx_out)))
+    return fail("acs_overflow_repass_device: null argument");
+  if (chunks == 0 || chunks > 64) return fail("acs_overflow_repass_device: chunks must be in [1, 64]");
+  if (m > 0xFFFFFFFFull) return fail("acs_overflow_repass_device: too many requests");
+  *m_out = 0;
+  *cap_out = 0;
+  if (m == 0) return 0;
+  const TruncatedLogs p{obl_n, (uint32_t)m, chunks, cap};
+  return select_device(t->ows, p, m, idx, idx_out, m_out, cap_out, (hipStream_t)stream);
 }
 
 int acs_shard_keys_device(acs_tables* t, const acs_decision* dec, size_t n, const acs_shard* shard, uint64_t* keys,

@@ -157,6 +157,22 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* dev_batch
                                    uint32_t chunks, uint32_t cap, uint32_t* dev_obl, uint32_t* dev_obl_n,
                                    void* stream);
 
+/* The device path's bookkeeping around the obligation-only pass, on the GPU (stable
+ * selection: per-tile counts, one-block scan, ballot-ranked writes; no atomics).
+ * acs_overflow_index_device: dev_idx[0..*m) <- the requests of dev_batch whose record in
+ * dev_out (an acs_what_is_allowed_device output) carries ACS_OF_OBL_OVERFLOW, in K2's
+ * coherence order (class / role key, then request index); dev_idx holds dev_batch->n entries.
+ * acs_overflow_repass_device: after a pass over dev_idx[0..m) with `chunks` ranges of cap
+ * `cap` (dev_obl_n [chunks][m]), dev_idx_out[0..*m_out) <- the requests some range still
+ * truncated (order kept) and *cap_out <- their largest range count, the next pass's cap.
+ * Both synchronise `stream` (the count sizes the next pass) and share one scratch per handle:
+ * one stream at a time. */
+int acs_overflow_index_device(acs_tables* t, const acs_req_batch* dev_batch, const acs_decision* dev_out,
+                              uint32_t* dev_idx, size_t* m, void* stream);
+int acs_overflow_repass_device(acs_tables* t, const uint32_t* dev_obl_n, const uint32_t* dev_idx, size_t m,
+                               uint32_t chunks, uint32_t cap, uint32_t* dev_idx_out, size_t* m_out,
+                               uint32_t* cap_out, void* stream);
+
 /* Rule-sharded isAllowed (configs[4] variant ii).  A rank compiles only the
  * policy sets [set_base, set_base + n_sets) of the store (whole sets, Map order) and
  * evaluates every request against them with acs_is_allowed_device.  acs_shard_keys_device

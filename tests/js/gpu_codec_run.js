@@ -58,8 +58,8 @@ const enc = (x) => (x instanceof Error ? { $error: x.name, reason: x.reason } : 
       continue;
     }
     let ctl;
+    const opts = { threads: 2 };
     try {
-      const opts = { threads: 2 };
       if (c.hostEvaluator) opts.hostEvaluator = (op, req) => ({ host: op, keys: Object.keys(req).sort() });
       ctl = new g.GpuAccessController(maps, c.urns, c.cas, opts);
     } catch (e) {

@@ -258,6 +258,50 @@ def test_what_is_allowed_overflow_pass_gpu(cap):
     t.close()
 
 
+@pytest.mark.parametrize("compact", [True, False])
+def test_overflow_resolution_on_device_gpu(compact):
+    """The device path's overflow bookkeeping (acs_overflow_index_device /
+    acs_overflow_repass_device, no torch kernels): the index list is the overflowed
+    requests, every one once, in a deterministic order; cap=70 forces the exact-count
+    re-pass, whose list and cap equal a numpy restatement; the joined logs equal the host
+    form's."""
+    import ctypes as C
+    from acs_mi355x.device import resolve_overflow_device, overflow_logs, what_is_allowed_device
+    doc, cs, sb = _synth("c3", 8_000)
+    t = gpu_tables(cs)
+    _, _, _, out = t.what_is_allowed(sb.batch)
+    want = t.resolve_overflow(sb.batch, out.copy(), cap=1024)
+    db = DeviceBatch(sb.batch, 0, compact=compact)
+    bufs = what_is_allowed_device(t, db)
+    passes = resolve_overflow_device(t, db, bufs, cap=70, chunks=4)
+    assert len(passes) >= 2
+    idx0 = passes[0][0].cpu().numpy()
+    assert sorted(idx0.tolist()) == sorted(want)
+    again = resolve_overflow_device(t, db, bufs, cap=70, chunks=4)
+    assert np.array_equal(again[0][0].cpu().numpy(), idx0)  # deterministic order
+    for (idx, cap, obl, obl_n), nxt in zip(passes, passes[1:] + [None]):
+        n = obl_n.cpu().numpy().view(np.uint32).astype(np.int64)
+        more = (n > cap).any(axis=0)
+        exp = idx.cpu().numpy()[more]
+        if nxt is None:
+            assert not more.any()
+        else:
+            assert np.array_equal(nxt[0].cpu().numpy(), exp) and nxt[1] == int(n[:, more].max())
+    logs = overflow_logs(passes)
+    assert sorted(logs) == sorted(want)
+    for i, lg in want.items():
+        assert np.array_equal(logs[i], lg), i
+    # none overflowed: an empty list and no pass
+    clean = bufs[3].clone()
+    clean[:, 2] &= ~L.OF_OBL_OVERFLOW
+    assert resolve_overflow_device(t, db, (bufs[0], bufs[1], bufs[2], clean)) == []
+    m = C.c_size_t(7)
+    idx = torch.empty(sb.batch.n, dtype=torch.int32, device="cuda")
+    assert t.lib.acs_overflow_index_device(t.h, C.byref(db.struct), clean.data_ptr(), idx.data_ptr(), C.byref(m),
+                                           None) == 0 and m.value == 0
+    t.close()
+
+
 def _shard_reduce_gpu(urns, full_map, world, make_batch):
     """Evaluate `world` policy-set shards one after another on this GPU and reduce their
     keys with MAX, as the RCCL all-reduce of the rule-sharded bench does across GPUs."""
