@@ -329,10 +329,10 @@ struct ReqCtx {
   const Batch& B;
   uint32_t i;
   ReqHdr h;
-  const uint32_t* ar;
-  const uint32_t* ex;  // compact batch: this request's extension record (acs_layout.h ext_geom)
-  uint32_t n_grants, n_rolese, n_slots, n_roots, n_tse, n_hrkeys;
-  const uint32_t *grants, *rolese, *roots, *hrkeys, *slotoff, *tse;
+  // The arena view is recomputed from two packed count words at each use (HR / ACL only)
+  // instead of being held as six pointers and six counts: K1's per-lane state stays small.
+  uint32_t c0, c1;  // arena counts: [0] grants | rolese<<8 | slots<<16 | roots<<24, [1] tse | hrkeys<<8
+  uint32_t ext;     // compact batch: 1 + 16-B unit offset of the extension record (0: none)
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
@@ -341,17 +341,20 @@ struct ReqCtx {
   // ln: the request's packed line (acs_layout.h ReqLine), nullptr: the SoA rows
   ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
       : T(t), B(b), i(idx), h(hd) {
-    ar = B.arena + h.arena_off;
-    ex = ln && ln->ext ? B.ext + (size_t)(ln->ext - 1u) * 4u : nullptr;
     if (ln) {
+      ext = ln->ext;
       s0i = ln->s0.id; s0v = ln->s0.value; s1i = ln->s1.id; s1v = ln->s1.value;
       a0i = ln->a0.id; a0v = ln->a0.value;
       role0 = ln->r0;
       role1 = ln->r1;
-      set_arena(ln->ar0, ln->ar1);
+      c0 = ln->ar0;
+      c1 = ln->ar1;
       return;
     }
-    set_arena(ar[0], ar[1]);
+    ext = 0;
+    const uint32_t* a = B.arena + h.arena_off;
+    c0 = a[0];
+    c1 = a[1];
     const Pair s0 = h.nsubj > 0 ? B.subj[i] : Pair{};
     const Pair s1 = h.nsubj > 1 ? B.subj[(size_t)B.n + i] : Pair{};
     const Pair a0 = h.nact > 0 ? B.act[i] : Pair{};
@@ -359,23 +362,27 @@ struct ReqCtx {
     role0 = h.nroles > 0 ? B.roles[i] : 0u;
     role1 = h.nroles > 1 ? B.roles[(size_t)B.n + i] : 0u;
   }
-  ACS_FN void set_arena(uint32_t c0, uint32_t c1) {
-    n_grants = c0 & 0xFF; n_rolese = (c0 >> 8) & 0xFF; n_slots = (c0 >> 16) & 0xFF; n_roots = c0 >> 24;
-    n_tse = c1 & 0xFF; n_hrkeys = (c1 >> 8) & 0xFF;
-    grants = ar + 2;
-    rolese = grants + 3 * n_grants;
-    roots = rolese + 2 * n_rolese;
-    hrkeys = roots + n_roots;
-    slotoff = hrkeys + n_hrkeys;
-    tse = slotoff + n_slots;
-  }
+  ACS_FN const uint32_t* ar() const { return B.arena + h.arena_off; }
+  ACS_FN const uint32_t* ex() const { return B.ext + (size_t)(ext - 1u) * 4u; }
+  ACS_FN uint32_t n_grants() const { return c0 & 0xFFu; }
+  ACS_FN uint32_t n_rolese() const { return (c0 >> 8) & 0xFFu; }
+  ACS_FN uint32_t n_slots() const { return (c0 >> 16) & 0xFFu; }
+  ACS_FN uint32_t n_roots() const { return c0 >> 24; }
+  ACS_FN uint32_t n_tse() const { return c1 & 0xFFu; }
+  ACS_FN uint32_t n_hrkeys() const { return (c1 >> 8) & 0xFFu; }
+  ACS_FN const uint32_t* grants() const { return ar() + 2; }
+  ACS_FN const uint32_t* rolese() const { return grants() + 3 * n_grants(); }
+  ACS_FN const uint32_t* roots() const { return rolese() + 2 * n_rolese(); }
+  ACS_FN const uint32_t* hrkeys() const { return roots() + n_roots(); }
+  ACS_FN const uint32_t* slotoff() const { return hrkeys() + n_hrkeys(); }
+  ACS_FN const uint32_t* tse() const { return slotoff() + n_slots(); }
   // The first subject / action / role attributes live in registers: target matching reads
   // them for every visited node, and the rows are gathered in sort order (uncoalesced).
   // Rows past the line: the SoA rows, or a compact batch's extension record.
   ACS_FN ExtGeom geom() const { return ext_geom(h.nres, h.nsubj, h.nact, h.nroles); }
   ACS_FN ReqRes res_row(uint32_t j) const {
     if (B.hdr) return B.res[(size_t)j * B.n + i];
-    const uint32_t* w = ex + 4u * (j - (uint32_t)LINE_RES);
+    const uint32_t* w = ex() + 4u * (j - (uint32_t)LINE_RES);
     ReqRes q;
     __builtin_memcpy(&q, w, sizeof q);
     return q;
@@ -383,7 +390,7 @@ struct ReqCtx {
   ACS_FN Pair subj(uint32_t j) const {
     if (j >= 2) {
       if (B.hdr) return B.subj[(size_t)j * B.n + i];
-      const uint32_t* w = ex + geom().subj + 2u * (j - 2u);
+      const uint32_t* w = ex() + geom().subj + 2u * (j - 2u);
       return Pair{w[0], w[1]};
     }
     Pair p;
@@ -394,7 +401,7 @@ struct ReqCtx {
   ACS_FN Pair act(uint32_t j) const {
     if (j >= 1) {
       if (B.hdr) return B.act[(size_t)j * B.n + i];
-      const uint32_t* w = ex + geom().act + 2u * (j - 1u);
+      const uint32_t* w = ex() + geom().act + 2u * (j - 1u);
       return Pair{w[0], w[1]};
     }
     Pair p;
@@ -404,7 +411,7 @@ struct ReqCtx {
   }
   ACS_FN uint32_t role(uint32_t j) const {
     if (j < 2) return j == 0 ? role0 : role1;
-    return B.hdr ? B.roles[(size_t)j * B.n + i] : ex[geom().roles + (j - 2u)];
+    return B.hdr ? B.roles[(size_t)j * B.n + i] : ex()[geom().roles + (j - 2u)];
   }
   ACS_FN uint8_t rx(uint32_t col, uint32_t row) const { return B.rx[(size_t)col * B.rx_rows + row]; }
   ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
@@ -651,7 +658,7 @@ ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, boo
 }
 
 // ------------------------------------------------------------------ checkHierarchicalScope
-ACS_FN const uint32_t* slot_rec(const ReqCtx& R, uint32_t slot) { return R.ar + R.slotoff[slot]; }
+ACS_FN const uint32_t* slot_rec(const ReqCtx& R, uint32_t slot) { return R.ar() + R.slotoff()[slot]; }
 
 ACS_FN bool hr_direct(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   const uint32_t* rec = slot_rec(R, slot);
@@ -661,8 +668,8 @@ ACS_FN bool hr_direct(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se
     const uint32_t w = p[0], val = p[1], na = w >> 8;
     const uint32_t* at = p + 2;
     if ((w & 1u) && val == se) {
-      for (uint32_t g = 0; g < R.n_grants; ++g) {
-        const uint32_t* gr = R.grants + 3 * g;
+      for (uint32_t g = 0; g < R.n_grants(); ++g) {
+        const uint32_t* gr = R.grants() + 3 * g;
         if (gr[0] == role && gr[1] == se)
           for (uint32_t a = 0; a < na; ++a)
             if (at[3 * a] == gr[2]) return true;
@@ -675,11 +682,11 @@ ACS_FN bool hr_direct(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se
 
 ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   bool rse = false;
-  for (uint32_t k = 0; k < R.n_rolese && !rse; ++k) rse = R.rolese[2 * k] == role && R.rolese[2 * k + 1] == se;
+  for (uint32_t k = 0; k < R.n_rolese() && !rse; ++k) rse = R.rolese()[2 * k] == role && R.rolese()[2 * k + 1] == se;
   if (!rse) return false;
   uint32_t mask = 0;
-  for (uint32_t r = 0; r < R.n_roots; ++r)
-    if (R.roots[r] == role) mask |= 1u << r;
+  for (uint32_t r = 0; r < R.n_roots(); ++r)
+    if (R.roots()[r] == role) mask |= 1u << r;
   if (!mask) return false;
   const uint32_t* rec = slot_rec(R, slot);
   const uint32_t n_owners = rec[1];
@@ -765,22 +772,22 @@ ACS_FN tri verify_acl(const NodeRec& t, const ReqCtx& R) {
   const uint32_t* roles = R.T.u32pool + t.acl_roles_off;
   const uint32_t nr = t.acl_roles_n;
   if (R.flag(RQ_ACT_CREATE)) {
-    if (R.n_tse == 0) return 1;
+    if (R.n_tse() == 0) return 1;
     bool valid = false;
-    for (uint32_t e = 0; e < R.n_tse; ++e) {
-      const uint32_t se = R.tse[3 * e], ni = R.tse[3 * e + 1];
-      const uint32_t* inst = R.ar + R.tse[3 * e + 2];
+    for (uint32_t e = 0; e < R.n_tse(); ++e) {
+      const uint32_t se = R.tse()[3 * e], ni = R.tse()[3 * e + 1];
+      const uint32_t* inst = R.ar() + R.tse()[3 * e + 2];
       if (se == R.T.id_user) {
         valid = true;
         continue;
       }
       bool present = false;
-      for (uint32_t k = 0; k < R.n_rolese && !present; ++k)
-        present = R.rolese[2 * k + 1] == se && in_list(roles, nr, R.rolese[2 * k]);
+      for (uint32_t k = 0; k < R.n_rolese() && !present; ++k)
+        present = R.rolese()[2 * k + 1] == se && in_list(roles, nr, R.rolese()[2 * k]);
       if (!present) return 0;
       uint32_t validated = 0;  // bitmask over inst indices
-      for (uint32_t kk = 0; kk < R.n_hrkeys; ++kk) {
-        if (!in_list(roles, nr, R.hrkeys[kk])) continue;
+      for (uint32_t kk = 0; kk < R.n_hrkeys(); ++kk) {
+        if (!in_list(roles, nr, R.hrkeys()[kk])) continue;
         for (uint32_t x = 0; x < ni; ++x) {
           if ((inst[2 * x + 1] >> kk) & 1u) {
             valid = true;
@@ -800,15 +807,15 @@ ACS_FN tri verify_acl(const NodeRec& t, const ReqCtx& R) {
     return valid ? 1 : 0;
   }
   if (R.flag(RQ_ACT_RMD)) {
-    if (R.n_tse == 0) return 1;
-    for (uint32_t e = 0; e < R.n_tse; ++e) {
-      const uint32_t se = R.tse[3 * e], ni = R.tse[3 * e + 1];
-      const uint32_t* inst = R.ar + R.tse[3 * e + 2];
+    if (R.n_tse() == 0) return 1;
+    for (uint32_t e = 0; e < R.n_tse(); ++e) {
+      const uint32_t se = R.tse()[3 * e], ni = R.tse()[3 * e + 1];
+      const uint32_t* inst = R.ar() + R.tse()[3 * e + 2];
       if (se == R.T.id_user)
         for (uint32_t x = 0; x < ni; ++x)
           if (inst[2 * x] == R.h.subject_id) return 1;
-      for (uint32_t g = 0; g < R.n_grants; ++g) {
-        const uint32_t* gr = R.grants + 3 * g;
+      for (uint32_t g = 0; g < R.n_grants(); ++g) {
+        const uint32_t* gr = R.grants() + 3 * g;
         if (gr[1] != se || !in_list(roles, nr, gr[0])) continue;
         for (uint32_t x = 0; x < ni; ++x)
           if (inst[2 * x] == gr[2]) return 1;

@@ -65,6 +65,12 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_BLOB_RULES      // rule records in the blob layout instead of 128-B lines
 #define ACS_AB_BLOB_RULES 0
 #endif
+#ifndef ACS_AB_NO_SCATTER      // timing only: K1 writes records in sort order (out[k])
+#define ACS_AB_NO_SCATTER 0
+#endif
+#ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
+#define ACS_AB_PROLOGUE_ONLY 0
+#endif
 #ifndef ACS_AB_FILTER_GENERAL  // the general filter form for every batch
 #define ACS_AB_FILTER_GENERAL 0
 #endif
@@ -84,8 +90,11 @@ __device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits
   const ReqLine* ln = B.hdr ? nullptr : B.lines + k;  // compact batch: the line holds the rows read here
   const ReqHdr h = ln ? ln->h : B.hdr[k];
   const uint32_t cls = h.flags >> RQ_PCOL_SHIFT;
-  const uint32_t a0 = h.nact ? (ln ? ln->a0.value : B.act[k].value) : 0u;
-  uint32_t low = B.role_key ? B.role_key[k] : a0, bucket = cls + 1;
+  // the action is read only when it is the low field (a 4-B read of a 128-B line still
+  // moves a sector: with lowbits == 0 the key kernel reads the header alone)
+  uint32_t low = 0, bucket = cls + 1;
+  if (B.role_key) low = B.role_key[k];
+  else if (lowbits && h.nact) low = ln ? ln->a0.value : B.act[k].value;
   if (cls >= B.cand_rows) {
     bucket = 0;
     const uint32_t* ex = ln && ln->ext ? B.ext + (size_t)(ln->ext - 1u) * 4u : nullptr;
@@ -396,6 +405,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #else
   if (!in) return;
 #endif
+  if (ACS_AB_PROLOGUE_ONLY) done = true;  // A/B timing only: filter build + line read, no walk
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
@@ -409,7 +419,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
+#if ACS_AB_NO_SCATTER
+  out[k] = d;  // A/B timing only: records in sort order (wrong order for the caller)
+#else
   out[i] = d;
+#endif
 #else
   if (in) out[i] = d;
   for (int k = 0; k < PH_N; ++k) {  // lane-cycles per phase, one atomic per wave
