@@ -51,6 +51,9 @@ def populate(doc: dict, store: dict | None = None) -> dict:
     for ps in doc.get("policy_sets") or []:
         policies = {}
         for py in ps.get("policies") or []:
+            if isinstance(py, dict) and py.get("$null"):  # a null Map entry under this id (fixture form:
+                policies[py.get("id", MISSING)] = None  # resourceManager re-reads, accessController.ts:138)
+                continue
             rules = {}
             for ry in py.get("rules") or []:
                 r = make_rule(ry)

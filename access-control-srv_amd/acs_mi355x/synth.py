@@ -35,6 +35,8 @@ URN = {
     "hrs": "urn:restorecommerce:acs:names:hierarchicalRoleScoping",
     "ownerEntity": "urn:restorecommerce:acs:names:ownerIndicatoryEntity",
     "ownerInstance": "urn:restorecommerce:acs:names:ownerInstance",
+    "aclEntity": "urn:restorecommerce:acs:names:aclIndicatoryEntity",
+    "aclInstance": "urn:restorecommerce:acs:names:aclInstance",
 }
 ACTIONS = ["urn:restorecommerce:acs:names:action:read", "urn:restorecommerce:acs:names:action:modify",
            "urn:restorecommerce:acs:names:action:create", "urn:restorecommerce:acs:names:action:delete",
@@ -203,6 +205,26 @@ def c3_store(seed=0xACC0003, n_sets=200, n_pols=5, n_rules=10):
     return {"policy_sets": sets}
 
 
+def c3_adverse_store(seed=0xACC0006, n_cond=50, early_sets=20, null_set=7):
+    """c3-adverse: the c3 store made hostile to the kernel's early stops (NF_CLEAN_BELOW fails
+    below the top sets): ``n_cond`` rules (0.5 %) of the first ``early_sets`` sets carry a
+    `condition` (utils.ts:47-56: the request goes to the host when one is reached), and set
+    ``null_set`` holds a null policy entry (accessController.ts:138: the TypeError of loop 2a),
+    behind a set target of a rare role so that only its requests throw."""
+    doc = c3_store()
+    rng = np.random.default_rng(seed)
+    sets = doc["policy_sets"]
+    early = [(s, p, q) for s in range(early_sets) for p in range(len(sets[s]["policies"]))
+             for q in range(len(sets[s]["policies"][p]["rules"]))]
+    for k in rng.choice(len(early), size=n_cond, replace=False):
+        s, p, q = early[int(k)]
+        sets[s]["policies"][p]["rules"][q]["condition"] = "context.subject.id === 'u0'"
+    sets[null_set]["target"] = {"subjects": [{"id": URN["role"], "value": role(50)}]}
+    pols = sets[null_set]["policies"]
+    pols[2] = {"id": pols[2]["id"], "$null": True}
+    return doc
+
+
 def c5_store(seed=0xACC0005, n_sets=1000, n_pols=10, n_rules=100):
     """c5: 1,000 sets x 10 policies x 100 rules = 1M rules, the c3 rule mix (roles, 50%
     organization-scoped with 25% of those hierarchicalRoleScoping 'false', 30% with
@@ -299,14 +321,27 @@ class SynthBatch:
             subj["role_associations"] = [{"role": role(r), "attributes": [
                 {"id": URN["rse"], "value": ORG_ENTITY,
                  "attributes": [{"id": URN["rsi"], "value": t.name(scope)}]}]}]
-            tree = t.subtree_json(scope, role(r))
-            if shared is not None and "children" in tree:  # one shared children list per scope org
-                tree = dict(tree, children=shared.ref(scope, tree["children"]))
-            subj["hierarchical_scopes"] = [tree]
+            r2 = int(d.get("role2", -1))
+            scopes = [(scope, r)]
+            if r2 >= 0:  # a second role association, scoped to its own org
+                sc2 = int(d["scope2"])
+                subj["role_associations"].append({"role": role(r2), "attributes": [
+                    {"id": URN["rse"], "value": ORG_ENTITY,
+                     "attributes": [{"id": URN["rsi"], "value": t.name(sc2)}]}]})
+                scopes.append((sc2, r2))
+            subj["hierarchical_scopes"] = []
+            for sc, rr in scopes:
+                tree = t.subtree_json(sc, role(rr))
+                if shared is not None and "children" in tree:  # one shared children list per scope org
+                    tree = dict(tree, children=shared.ref(sc, tree["children"]))
+                subj["hierarchical_scopes"].append(tree)
             owner = int(d["owner"])
-            req["context"] = {"subject": subj, "resources": [{"id": f"res{int(d['rid'])}", "meta": {"owners": [
-                {"id": URN["ownerEntity"], "value": ORG_ENTITY,
-                 "attributes": [{"id": URN["ownerInstance"], "value": t.name(owner)}]}]}}]}
+            meta = {"owners": [{"id": URN["ownerEntity"], "value": ORG_ENTITY,
+                                "attributes": [{"id": URN["ownerInstance"], "value": t.name(owner)}]}]}
+            if int(d.get("acl", -1)) >= 0:  # c3-adverse: an ACL on the resource (verifyACL.ts:37-88)
+                meta["acls"] = [{"id": URN["aclEntity"], "value": ORG_ENTITY,
+                                 "attributes": [{"id": URN["aclInstance"], "value": t.name(int(d["acl"]))}]}]
+            req["context"] = {"subject": subj, "resources": [{"id": f"res{int(d['rid'])}", "meta": meta}]}
         return req
 
 
@@ -331,6 +366,10 @@ class SynthBatch:
         c3 = self.kind != "c2"
         if c3:
             scope, owner = d["scope"], d["owner"]
+            role2 = d.get("role2", np.full(len(ent), -1))
+            scope2 = d.get("scope2", np.zeros(len(ent), np.int64))
+            acl = d.get("acl", np.full(len(ent), -1))
+            ae, ai = URN["aclEntity"], URN["aclInstance"]
             rse, rsi, oe, oi = URN["rse"], URN["rsi"], URN["ownerEntity"], URN["ownerInstance"]
         for i in idx.tolist():
             e, r, u = int(ent[i]), int(rol[i]), int(usr[i])
@@ -341,18 +380,25 @@ class SynthBatch:
                 ctx = (f'"context":{{"subject":{{"id":"u{u}","role_associations":[{{"role":"r{r}","attributes":[]}}],'
                        f'"hierarchical_scopes":[]}},"resources":[]}}}}')
             else:
-                sc = int(scope[i])
+                sc, r2 = int(scope[i]), int(role2[i])
+                ra2 = (f',{{"role":"r{r2}","attributes":[{{"id":"{rse}","value":"{ORG_ENTITY}","attributes":'
+                       f'[{{"id":"{rsi}","value":"org{int(scope2[i])}"}}]}}]}}') if r2 >= 0 else ""
                 ctx = (f'"context":{{"subject":{{"id":"u{u}","role_associations":[{{"role":"r{r}","attributes":['
-                       f'{{"id":"{rse}","value":"{ORG_ENTITY}","attributes":[{{"id":"{rsi}","value":"org{sc}"}}]}}]}}],'
+                       f'{{"id":"{rse}","value":"{ORG_ENTITY}","attributes":[{{"id":"{rsi}","value":"org{sc}"}}]}}]}}{ra2}],'
                        f'"$hrs":"{self.hrs_key(i)}"}},"resources":[{{"id":"res{int(rid[i])}","meta":{{"owners":['
                        f'{{"id":"{oe}","value":"{ORG_ENTITY}","attributes":[{{"id":"{oi}","value":"org{int(owner[i])}"}}]}}'
+                       + (f'],"acls":[{{"id":"{ae}","value":"{ORG_ENTITY}","attributes":[{{"id":"{ai}",'
+                          f'"value":"org{int(acl[i])}"}}]}}' if int(acl[i]) >= 0 else '') +
                        f']}}}}]}}}}')
             out.append(head + ctx)
         return ("[" + ",".join(out) + "]").encode()
 
     def hrs_key(self, i):
-        """The subject forest a c3 request names: its scope org and role."""
-        return f"s{int(self.draws['scope'][i])}:r{int(self.draws['role'][i])}"
+        """The subject forest a c3 request names: its scope org and role (and the second
+        association's, when it has one)."""
+        k = f"s{int(self.draws['scope'][i])}:r{int(self.draws['role'][i])}"
+        r2 = int(self.draws["role2"][i]) if "role2" in self.draws else -1
+        return k if r2 < 0 else f"{k}:s{int(self.draws['scope2'][i])}:r{r2}"
 
     def hrs_forests(self, idx=None):
         """{hrs_key: hierarchical_scopes} of requests ``idx`` (the forests to register)."""
@@ -362,6 +408,9 @@ class SynthBatch:
             k = self.hrs_key(i)
             if k not in out:
                 out[k] = [self.tree.subtree_json(int(self.draws["scope"][i]), role(int(self.draws["role"][i])))]
+                r2 = int(self.draws["role2"][i]) if "role2" in self.draws else -1
+                if r2 >= 0:
+                    out[k].append(self.tree.subtree_json(int(self.draws["scope2"][i]), role(r2)))
         return out
 
 
@@ -393,8 +442,15 @@ def _vocab(cs: CompiledStore, ov: Overlay):
     }
 
 
-def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree | None = None) -> SynthBatch:
-    """Generate n packed requests for config ``kind`` ('c2' or 'c3') against store ``cs``."""
+def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree | None = None,
+             second_role=0.0, acl=0.0, classes=True) -> SynthBatch:
+    """Generate n packed requests for config ``kind`` ('c2' or 'c3') against store ``cs``.
+    c3: a fraction ``second_role`` of the subjects carries a second role association (SURVEY
+    §8(d): 1-2 per request), drawn like the first and distinct from it, scoped to its own random
+    org of depth 0-3, with its subtree as a second hierarchical_scopes root.
+    c3-adverse: a fraction ``acl`` of the context resources carries an ACL (an org inside the
+    subject's scope with p = 0.5); the packed batch flags those requests RQ_HOST (it packs no
+    ACL maps) — their batches come from an encoder (the native codec) instead."""
     rng = np.random.default_rng(seed)
     ov = Overlay(cs.dictionary)
     V = _vocab(cs, ov)
@@ -454,6 +510,15 @@ def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree
     hdr["nact"] = 1
     hdr["nroles"] = 1
     hdr["subject_id"] = V["user"][usr]
+    r2 = np.full(n, -1, np.int32)
+    if kind != "c2" and second_role > 0:
+        r2 = rng.choice(N_ROLES, size=n, p=zipf_p(N_ROLES)).astype(np.int32)
+        r2 = np.where(r2 == rol, (r2 + 1) % N_ROLES, r2)
+        r2 = np.where(rng.random(n) < second_role, r2, -1).astype(np.int32)
+        draws["role2"] = r2
+    has2 = r2 >= 0
+    hdr["nroles"] = np.where(has2, 2, 1)
+    roles[1] = np.where(has2, V["role"][np.maximum(r2, 0)], 0)
 
     if kind == "c2":
         # no context resources: the first resource-id lookup finds no ACLs -> verifyACL true
@@ -462,40 +527,75 @@ def requests(cs: CompiledStore, n: int, kind="c2", seed=0xACC1002, tree: OrgTree
         hdr["arena_off"] = 0
     else:
         tree = tree or OrgTree()
+
+        def draw_scope():  # a random org of depth 0..3
+            lv = rng.integers(0, 4, size=n)
+            sc = np.zeros(n, np.int64)
+            for d in range(4):
+                nodes = np.flatnonzero(tree.level == d)
+                m = lv == d
+                sc[m] = nodes[rng.integers(len(nodes), size=int(m.sum()))]
+            return sc
+
         # subject scoped at a random org of depth 0..3, owner inside its subtree with p=0.6
-        lv = rng.integers(0, 4, size=n)
-        scope = np.zeros(n, np.int64)
-        for d in range(4):
-            nodes = np.flatnonzero(tree.level == d)
-            m = lv == d
-            scope[m] = nodes[rng.integers(len(nodes), size=int(m.sum()))]
+        scope = draw_scope()
         inside = rng.random(n) < 0.6
         off = (rng.random(n) * tree.size[scope]).astype(np.int64)
         owner = np.where(inside, scope + off, rng.integers(0, tree.n, size=n))
         draws.update({"scope": scope, "owner": owner})
+        scope2 = np.zeros(n, np.int64)
+        if has2.any():
+            scope2 = np.where(has2, draw_scope(), 0)
+            draws["scope2"] = scope2
         org_id = np.array([ov.intern(tree.name(k)) for k in range(tree.n)], np.uint32)
         urn_org = ov.intern(ORG_ENTITY)
-        # arena per request (22 words): counts, 1 grant, 1 rolese, 1 root, 1 hrkey, 1 slot, owner record
-        W = 22
-        ar = np.zeros((n, W), np.uint32)
-        ar[:, 0] = 1 | (1 << 8) | (1 << 16) | (1 << 24)
-        ar[:, 1] = 0 | (1 << 8)
-        ar[:, 2], ar[:, 3], ar[:, 4] = V["role"][rol], urn_org, org_id[scope]        # grant
-        ar[:, 5], ar[:, 6] = V["role"][rol], urn_org                                 # rolese
-        ar[:, 7] = V["role"][rol]                                                    # root raw role
-        ar[:, 8] = V["role"][rol]                                                    # hr key
-        ar[:, 9] = 10                                                                # slot 0 offset
-        ar[:, 10], ar[:, 11] = 0, 1                                                  # owners_empty, n_owners
-        ar[:, 12], ar[:, 13] = 1 | (1 << 8), urn_org                                 # is_oe | 1 attr, value
         in_sub = (owner >= scope) & (owner < scope + tree.size[scope])
-        ar[:, 14], ar[:, 15], ar[:, 16] = org_id[owner], L.K_OI, in_sub.astype(np.uint32)
+        in_sub2 = has2 & (owner >= scope2) & (owner < scope2 + tree.size[scope2])
+        # arena per request (acs_layout.h, the encoder's order): counts, grants, rolese, roots,
+        # HR keys, 1 slot offset, the owner record.  One role: 17 words; two: 24.
+        W = 24 if has2.any() else 22
+        ar = np.zeros((n, W), np.uint32)
+        R1, R2 = V["role"][rol], V["role"][np.maximum(r2, 0)]
+        one, two = ~has2, has2
+        ar[one, 0] = 1 | (1 << 8) | (1 << 16) | (1 << 24)
+        ar[one, 1] = 0 | (1 << 8)
+        ar[one, 2], ar[one, 3], ar[one, 4] = R1[one], urn_org, org_id[scope[one]]   # grant
+        ar[one, 5], ar[one, 6] = R1[one], urn_org                                   # rolese
+        ar[one, 7] = R1[one]                                                        # root raw role
+        ar[one, 8] = R1[one]                                                        # hr key
+        ar[one, 9] = 10                                                             # slot 0 offset
+        slot1 = 10
+        if not has2.any():
+            two = np.zeros(0, np.int64)  # no two-role request (W = 22: the two-role columns do not exist)
+        ar[two, 0] = 2 | (2 << 8) | (1 << 16) | (2 << 24)
+        ar[two, 1] = 0 | (2 << 8)
+        ar[two, 2], ar[two, 3], ar[two, 4] = R1[two], urn_org, org_id[scope[two]]   # grants
+        ar[two, 5], ar[two, 6], ar[two, 7] = R2[two], urn_org, org_id[scope2[two]]
+        ar[two, 8], ar[two, 9] = R1[two], urn_org                                   # rolese
+        ar[two, 10], ar[two, 11] = R2[two], urn_org
+        ar[two, 12], ar[two, 13] = R1[two], R2[two]                                 # roots
+        ar[two, 14], ar[two, 15] = R1[two], R2[two]                                 # hr keys
+        ar[two, 16] = 17                                                            # slot 0 offset
+        for sel, base in ((one, slot1), (two, 17)) if has2.any() else ((one, slot1),):
+            ar[sel, base], ar[sel, base + 1] = 0, 1                                 # owners_empty, n_owners
+            ar[sel, base + 2], ar[sel, base + 3] = 1 | (1 << 8), urn_org            # is_oe | 1 attr, value
+            ar[sel, base + 4], ar[sel, base + 5] = org_id[owner[sel]], L.K_OI
+            ar[sel, base + 6] = in_sub[sel].astype(np.uint32) | (in_sub2[sel].astype(np.uint32) << 1)
         arena = ar.reshape(-1)
         hdr["arena_off"] = (np.arange(n, dtype=np.int64) * W).astype(np.uint32)
         res["slot_a"][1] = 0
         flags |= np.uint32(L.ACL_RET_TRUE << L.RQ_ACL_SHIFT)  # owners-only meta: no ACLs
+        if acl > 0:
+            has_acl = rng.random(n) < acl
+            near = rng.random(n) < 0.5
+            a_org = np.where(near, scope + (rng.random(n) * tree.size[scope]).astype(np.int64),
+                             rng.integers(0, tree.n, size=n))
+            draws["acl"] = np.where(has_acl, a_org, -1)
+            flags |= np.where(has_acl, L.RQ_HOST, 0).astype(np.uint32)  # not packed here: encode the JSON
     hdr["flags"] = flags
     b = RequestBatch(n=n, hdr=hdr, res=res, subj=subj, act=actp, roles=roles, arena=arena, rx=rx,
                      rx_rows=rx.shape[1], overlay=ov)
-    from .encoder import attach_candidates
-    attach_candidates(cs, b, [entity(k) for k in range(N_ENT)])
+    if classes:  # (False: the caller re-encodes the JSON, e.g. c3-adverse through the codec)
+        from .encoder import attach_candidates
+        attach_candidates(cs, b, [entity(k) for k in range(N_ENT)])
     return SynthBatch(batch=b, draws=draws, kind=kind, tree=tree if kind != "c2" else None)

@@ -179,6 +179,7 @@ struct Filter {
   ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
     return vok && ((row[wv + sec + (i >> 5)] >> (i & 31)) & 1u);
   }
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w) const { return vok ? row[wv + sec + w] : 0u; }
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -198,6 +199,7 @@ struct FilterAll {
   uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
   ACS_FN bool verdict(uint32_t, uint32_t) const { return false; }  // no class rows
+  ACS_FN uint32_t vword(uint32_t, uint32_t) const { return 0u; }
 };
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
@@ -221,6 +223,16 @@ struct FilterLds {
     return false;
 #else
     return (word(wv + sec + (i >> 5)) >> (i & 31)) & 1u;
+#endif
+  }
+  // word w of the verdict section at `sec` (wave-uniform)
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w) const {
+#if defined(ACS_NO_VERDICT_CODE)
+    (void)sec;
+    (void)w;
+    return 0u;
+#else
+    return word(wv + sec + w);
 #endif
   }
 };
@@ -1227,20 +1239,37 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
       }
+      // Rules a word at a time: the candidates whose retried target match the class already
+      // knows to be true (verdict section 4 WP: targets without properties, so they push no
+      // obligation) are included as a whole word, unread; only the rest are visited
+      // (accessController.ts:389-418).
       bool any_rule = false;
-      CandRange rules(F, F.wr, P.child_begin, P.child_end);
-      uint32_t r;
-      while (rules.next(r)) {
-        const NodeRec Q = rule_at(T, r);
-        if (Q.nflags & NF_NULL) continue;
-        tri m = 1;
-        if (Q.nflags & NF_HAS_TARGET) {
-          m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, true, &obl);
-          if (m < 0) return make_err(m, s + 1);
-        }
-        if (m) {
-          bits.template set<2>(BL.wr + (r >> 5), 1u << (r & 31));
+      const uint32_t rb = P.child_begin, re = P.child_end;
+      for (uint32_t base = rb & ~31u; base < re; base += 32) {
+        const uint32_t w = base >> 5;
+        uint32_t m = F.word(F.wr + w);
+        if (base < rb) m &= ~0u << (rb & 31u);
+        if (re - base < 32u) m &= (1u << (re - base)) - 1u;
+        const uint32_t known = m & F.vword(4 * WP, w);
+        if (known) {
+          bits.template set<2>(BL.wr + w, known);
           any_rule = true;
+        }
+        uint32_t rest = m & ~known;
+        while (rest) {
+          const uint32_t r = wave_uniform(base + (uint32_t)__builtin_ctz(rest));
+          rest &= rest - 1u;
+          const NodeRec Q = rule_at(T, r);
+          if (Q.nflags & NF_NULL) continue;
+          tri mt = 1;
+          if (Q.nflags & NF_HAS_TARGET) {
+            mt = target_match_retry(Q, R, Q.effect, true, &obl);
+            if (mt < 0) return make_err(mt, s + 1);
+          }
+          if (mt) {
+            bits.template set<2>(BL.wr + w, 1u << (r & 31u));
+            any_rule = true;
+          }
         }
       }
       if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {

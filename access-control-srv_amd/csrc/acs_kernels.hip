@@ -71,6 +71,9 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
 #define ACS_AB_PROLOGUE_ONLY 0
 #endif
+#ifndef ACS_AB_RADIX_ONLY      // the coherence sort always takes the radix passes
+#define ACS_AB_RADIX_ONLY 0
+#endif
 #ifndef ACS_AB_FILTER_GENERAL  // the general filter form for every batch
 #define ACS_AB_FILTER_GENERAL 0
 #endif
@@ -244,6 +247,109 @@ __global__ __launch_bounds__(BLOCK) void radix_scatter_kernel(const uint32_t* __
       if (write_keys) kout[pos] = key;
     }
     __syncthreads();  // wcnt is cleared by the next round
+  }
+}
+
+// ---------------------------------------------------------------- class counting sort
+// The coherence sort only has to GROUP equal keys (any permutation gives the same records),
+// and a batch's key space is small (c3: 31k classes), so when it has at most CS_BINS keys one
+// counting pass replaces the radix passes:
+//   count    block b takes a contiguous chunk (< 2^16 keys) of the batch: extracts each key
+//            from the request line (written to keys[] for the scatter), counts it in LDS
+//            (16-bit counters, two per word: 64k bins in 128 KB) and writes its count row
+//            counts[b][0..K) whole (no memset);
+//   columns  per bin: exclusive prefix over the blocks (in place) and the bin total;
+//   bases    one block: exclusive scan of the K bin totals;
+//   scatter  block b again: a key's LDS atomic returns its rank inside the block, and
+//            perm[base[key] + counts[b][key] + rank] = i.  Ranks follow the LDS atomic order,
+//            so equal keys are grouped but not kept in index order (not needed).
+// Traffic: the line headers once, 4 B of key written and read back, K x blocks count words
+// twice, 4 B of perm per request — against ~8 passes of 8-B keys + values for the radix sort.
+constexpr uint32_t CS_BINS = 65536;
+constexpr uint32_t CS_THREADS = 1024;
+constexpr uint32_t CS_MAX_CHUNK = 65535;  // per-block counts fit 16 bits
+
+__device__ inline void cs_zero(uint32_t* h, uint32_t K) {
+  for (uint32_t w = threadIdx.x; w < (K + 1) / 2; w += CS_THREADS) h[w] = 0;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(CS_THREADS) void class_count_kernel(Batch B, uint32_t lowbits, uint32_t cbits,
+                                                                 uint32_t chunk, uint32_t K,
+                                                                 uint32_t* __restrict__ keys,
+                                                                 uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[CS_BINS / 2];
+  cs_zero(h, K);
+  const uint32_t i0 = blockIdx.x * chunk, i1 = i0 + chunk < B.n ? i0 + chunk : B.n;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += CS_THREADS) {
+    const uint32_t key = sort_key(B, i, lowbits, cbits);
+    keys[i] = key;
+    atomicAdd(&h[key >> 1], 1u << ((key & 1u) * 16u));
+  }
+  __syncthreads();
+  uint32_t* row = counts + (size_t)blockIdx.x * K;
+  for (uint32_t k = threadIdx.x; k < K; k += CS_THREADS) row[k] = (h[k >> 1] >> ((k & 1u) * 16u)) & 0xFFFFu;
+}
+
+__global__ __launch_bounds__(BLOCK) void class_columns_kernel(uint32_t* __restrict__ counts, uint32_t nb, uint32_t K,
+                                                              uint32_t* __restrict__ tot) {
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= K) return;
+  uint32_t run = 0;
+  constexpr uint32_t G = 32;  // rows loaded per round, all in flight (a serial load per row is latency-bound)
+  for (uint32_t b0 = 0; b0 < nb; b0 += G) {
+    uint32_t c[G];
+#pragma unroll
+    for (uint32_t j = 0; j < G; ++j) c[j] = b0 + j < nb ? counts[(size_t)(b0 + j) * K + k] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < G; ++j) {
+      if (b0 + j < nb) counts[(size_t)(b0 + j) * K + k] = run;
+      run += c[j];
+    }
+  }
+  tot[k] = run;
+}
+
+__global__ __launch_bounds__(CS_THREADS) void class_bases_kernel(uint32_t* __restrict__ tot, uint32_t K) {
+  __shared__ uint32_t part[CS_THREADS];
+  constexpr uint32_t PER_MAX = CS_BINS / CS_THREADS;  // 64: this thread's bins, loaded at once
+  const uint32_t per = (K + CS_THREADS - 1) / CS_THREADS, k0 = threadIdx.x * per;
+  uint32_t v[PER_MAX];
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < PER_MAX; ++j) {
+    v[j] = j < per && k0 + j < K ? tot[k0 + j] : 0u;
+    s += v[j];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < CS_THREADS; off <<= 1) {  // inclusive scan of the thread sums
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;
+#pragma unroll
+  for (uint32_t j = 0; j < PER_MAX; ++j) {
+    if (j < per && k0 + j < K) tot[k0 + j] = run;
+    run += v[j];
+  }
+}
+
+__global__ __launch_bounds__(CS_THREADS) void class_scatter_kernel(const uint32_t* __restrict__ keys, uint32_t n,
+                                                                   uint32_t chunk, uint32_t K,
+                                                                   const uint32_t* __restrict__ counts,
+                                                                   const uint32_t* __restrict__ base,
+                                                                   uint32_t* __restrict__ perm) {
+  __shared__ uint32_t h[CS_BINS / 2];
+  cs_zero(h, K);
+  const uint32_t i0 = blockIdx.x * chunk, i1 = i0 + chunk < n ? i0 + chunk : n;
+  const uint32_t* row = counts + (size_t)blockIdx.x * K;
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += CS_THREADS) {
+    const uint32_t key = keys[i], sh = (key & 1u) * 16u;
+    const uint32_t rank = (atomicAdd(&h[key >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    perm[base[key] + row[key] + rank] = i;
   }
 }
 
@@ -1131,6 +1237,36 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
   const size_t n = B.n;
   uint32_t lowbits, end_bit;
   sort_bits(B, &lowbits, &end_bit);
+  // key space: class-major keys are < (cand_rows + 1) << lowbits, role-major ones < 2^end_bit
+  const uint64_t K = B.role_major ? (1ull << end_bit) : ((uint64_t)B.cand_rows + 1u) << lowbits;
+  if (K <= CS_BINS && !ACS_AB_RADIX_ONLY) {  // one counting pass (class_count_kernel)
+    uint32_t nb = (uint32_t)((n + 1023) / 1024);
+    if (nb > 256) nb = 256;  // one block per CU
+    uint32_t chunk = (uint32_t)((n + nb - 1) / nb);
+    if (chunk > CS_MAX_CHUNK) {
+      chunk = CS_MAX_CHUNK;
+      nb = (uint32_t)((n + chunk - 1) / chunk);
+    }
+    const size_t words = 2 * n + (size_t)nb * K + K;
+    if (W.sort.reserve(words * sizeof(uint32_t))) return -1;
+    uint32_t* keys = (uint32_t*)W.sort.p;
+    uint32_t* out = keys + n;
+    uint32_t* counts = out + n;
+    uint32_t* tot = counts + (size_t)nb * K;
+    hipLaunchKernelGGL(class_count_kernel, dim3(nb), dim3(CS_THREADS), 0, s, B, lowbits, end_bit - lowbits, chunk,
+                       (uint32_t)K, keys, counts);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(class_columns_kernel, dim3((unsigned)((K + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, counts, nb,
+                       (uint32_t)K, tot);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(class_bases_kernel, dim3(1), dim3(CS_THREADS), 0, s, tot, (uint32_t)K);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(class_scatter_kernel, dim3(nb), dim3(CS_THREADS), 0, s, (const uint32_t*)keys, (uint32_t)n,
+                       chunk, (uint32_t)K, (const uint32_t*)counts, (const uint32_t*)tot, out);
+    HIP_OK(hipGetLastError());
+    *perm = out;
+    return 0;
+  }
   const uint32_t nt = (uint32_t)((n + SORT_TILE - 1) / SORT_TILE);
   if (W.sort.reserve(radix_scratch_bytes(n))) return -1;
   uint32_t* k0 = (uint32_t*)W.sort.p;

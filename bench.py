@@ -29,6 +29,11 @@ import torch  # noqa: E402
 WORKLOADS = {
     "c2": ("c2: isAllowed, 1M requests/GPU vs 100 policy sets / 200 policies / 1k rules, flat roles", 1_000_000),
     "c3": ("c3: isAllowed, 10M requests/GPU vs 10k rules, mixed CAs + HR role scoping (depth-8 org tree)", 10_000_000),
+    "c3adv": ("c3adv: c3-adverse, 1M requests/GPU vs the c3 store with 0.5 % condition rules in the first 20 sets, a "
+              "null policy behind a rare set target and ACLs on 10 % of the context resources (no early stop below "
+              "the top sets); requests encoded from JSON by the native codec", 1_000_000),
+    "c3r2": ("c3r2: the c3 workload with a second org-scoped role association (and HR subtree) on half of the "
+             "subjects (SURVEY §8(d): 1-2 role associations)", 10_000_000),
     "c4": ("c4: whatIsAllowed, 1M reverse queries/GPU vs 10k rules (c3 store, 30% of rules with properties), "
            "inclusion bitsets over sets|policies|rules + maskedProperty logs", 1_000_000),
     "c5": ("c5: isAllowed, 1M-request batches/GPU vs 1M rules (1,000 sets x 10 policies x 100 rules, c3 rule mix "
@@ -38,11 +43,16 @@ WORKLOADS = {
 
 def make_store(kind):
     from acs_mi355x import synth
-    return {"c2": synth.c2_store, "c3": synth.c3_store, "c4": synth.c3_store, "c5": synth.c5_store}[kind]()
+    return {"c2": synth.c2_store, "c3": synth.c3_store, "c3r2": synth.c3_store, "c3adv": synth.c3_adverse_store,
+            "c4": synth.c3_store,
+            "c5": synth.c5_store}[kind]()
 
 
 def request_kind(kind):
     return "c2" if kind == "c2" else "c3"  # c4 / c5 draw c3-shaped requests (HR context)
+# c3-shaped requests: share of subjects with a second org-scoped role association (§8(d): 1-2);
+# set per config in main() (c3r2: 0.5, the others 0) unless --second-role is given
+SECOND_ROLE = 0.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 _T0 = time.time()
 
@@ -200,6 +210,7 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
     from oracle import acs_oracle_c
     from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
     from diff_utils import gpu_outcome
+    from acs_mi355x import layout as L
     from acs_mi355x.synth import SharedValues
     acs_oracle_c.build()
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -207,8 +218,8 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
     n = sb.batch.n
     want_n = max(1, int(round(fraction * n)))
     idx = np.random.default_rng(1234).permutation(n)[:want_n]
-    chunk = {"c2": 50_000, "c3": 10_000}.get(kind, 256)
-    done = busy = mism = unsup = host = 0
+    chunk = {"c2": 50_000, "c3": 10_000, "c3r2": 10_000, "c3adv": 10_000}.get(kind, 256)
+    done = busy = mism = unsup = host = host_both = 0
     wall0 = time.perf_counter()
     while done < len(idx) and busy < seconds and time.perf_counter() - wall0 < 2 * seconds + 30:
         part = idx[done:done + chunk]
@@ -219,8 +230,14 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
         for i, r in zip(part, out):
             want = acs_oracle_c.outcome(r)
             got = gpu_outcome(cs, gpu_dec[i])
-            if want[0] == "UNSUPPORTED":
-                unsup += 1
+            cond = bool(gpu_dec[i]["flags"] & L.OF_HOST_COND)
+            if want[0] == "UNSUPPORTED":  # the oracle met a rule condition (JS eval) or a subject token
+                if got[0] == "HOST":
+                    host_both += 1
+                else:
+                    unsup += 1
+            elif cond:  # the GPU stopped at a condition the oracle's forward walk never reached
+                mism += 1
             elif got[0] == "HOST":
                 host += 1
             elif got != want:
@@ -234,8 +251,27 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
                     f"memoised, so faster than the reference's own loop), std::thread x {threads}, "
                     f"{busy:.1f}s of evaluation wall time (requests decoded and parsed beforehand)"}
     par = {"oracle_sample": done, "sample_fraction": done / n, "mismatches": mism,
-           "oracle_unsupported": unsup, "gpu_host_path": host, "checker": "oracle/acs_oracle.cpp"}
+           "oracle_unsupported": unsup, "gpu_host_path": host, "host_path_both": host_both,
+           "checker": "oracle/acs_oracle.cpp"}
     return cb, par
+
+
+def codec_batch(cs, sb):
+    """The batch of ``sb``'s JSON text through the native codec (the product encoder), its HR
+    forests registered first (the per-subject cache)."""
+    from acs_mi355x.codec import NativeCodec
+    codec = NativeCodec(compiler_blob(cs))
+    for k, v in sb.hrs_forests().items():
+        codec.set_subject_scopes(k, v)
+    b = codec.encode(sb.json_text(), threads=max(1, min(16, os.cpu_count() or 1)))
+    if b.host_reasons:
+        raise SystemExit(f"codec sent {len(b.host_reasons)} requests to the host: {next(iter(b.host_reasons.values()))}")
+    return b
+
+
+def compiler_blob(cs):
+    from acs_mi355x import compiler
+    return compiler.store_blob(cs)
 
 
 def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
@@ -333,7 +369,7 @@ def bench_what_is_allowed(args, desc, n, doc, full_map, world, rank, local, dev,
     from diff_utils import norm_rq
     import torch.distributed as tdist
     cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
-    sb = synth.requests(cs, n, "c3", seed=0xACC1004 + 17 * rank)
+    sb = synth.requests(cs, n, "c3", seed=0xACC1004 + 17 * rank, second_role=SECOND_ROLE)
     log(f"compiled {cs.n_rules} rules; encoded {n} requests")
     blob = compiler.store_blob(cs)
     tables = native.Tables(blob, local)
@@ -470,6 +506,8 @@ def main():
     ap.add_argument("--selftest", action="store_true", help="launcher / collective check on CPU (gloo), no GPU")
     ap.add_argument("--e2e-requests", type=int, default=1_000_000,
                     help="requests of the JSON -> decision measurement (0: skip)")
+    ap.add_argument("--second-role", type=float, default=None,
+                    help="c3-shaped requests: fraction with a second role association (SURVEY §8(d): 1-2)")
     ap.add_argument("--no-sort", action="store_true", help="disable the (class, action) coherence sort")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--lib", default=None, help="evaluate with another build of libacs_mi355x (experiments)")
@@ -488,6 +526,7 @@ def main():
                          f"{args.gpus}, or run without a torch.distributed environment)")
     if args.selftest:
         return selftest(world, rank)
+    globals()["SECOND_ROLE"] = args.second_role if args.second_role is not None else (0.5 if args.config == "c3r2" else 0.0)
     dist = world > 1
     global REHEARSAL
     # ACS_BENCH_REHEARSAL=1: several ranks on ONE GPU over gloo (collectives through host
@@ -526,10 +565,13 @@ def main():
         set_lo, set_hi = shard.partition(full_map, world)[rank]
         sbase = shard.base(full_map, set_lo)
         cs = compiler.compile_store(shard.slice_store(full_map, set_lo, set_hi), FULL_URNS, DEFAULT_CAS)
-        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000)
+        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000, second_role=SECOND_ROLE)
     else:
         cs = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
-        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000 + 17 * rank)
+        sb = synth.requests(cs, n, request_kind(kind), seed=0xACC1000 + 17 * rank, second_role=SECOND_ROLE,
+                            acl=0.1 if kind == "c3adv" else 0.0, classes=kind != "c3adv")
+        if kind == "c3adv":  # ACL maps are not packed by synth: the product codec encodes the JSON
+            sb.batch = codec_batch(cs, sb)
     log(f"compiled {cs.n_rules} rules; encoded {n} requests ({sb.batch.cand.shape[0]} classes)")
     if args.lib:
         native.load(args.lib)
@@ -584,7 +626,7 @@ def main():
         # size-independent property: the set-sharded + all-reduced records equal an
         # unsharded evaluation of the whole store on the same requests, bit for bit
         cs_full = compiler.compile_store(full_map, FULL_URNS, DEFAULT_CAS)
-        sb_full = synth.requests(cs_full, n, request_kind(kind), seed=0xACC1000)
+        sb_full = synth.requests(cs_full, n, request_kind(kind), seed=0xACC1000, second_role=SECOND_ROLE)
         t_full = native.Tables(compiler.store_blob(cs_full), local)
         want = decisions_from_tensor(is_allowed_device(t_full, DeviceBatch(sb_full.batch, local)))
         t_full.close()
@@ -629,6 +671,9 @@ def main():
                        "parallelism": f"policy-set shards x{world}" if args.rule_shard else f"requests dp{world}",
                        "decision_mix": {"PERMIT": int(mix[2]), "DENY": int(mix[3]), "INDETERMINATE": int(mix[5])},
                        "host_fallback_fraction": host / n, "request_classes": int(sb.batch.cand.shape[0]),
+                       "role_factor_rows": (int(sb.batch.role_bits.shape[0])
+                                            if getattr(sb.batch, "role_key", None) is not None else 0),
+                       "second_role_fraction": SECOND_ROLE if request_kind(kind) == "c3" else 0.0,
                        "ranks_confirmed": world},
             "coherence_sort": not args.no_sort,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -643,7 +688,9 @@ def main():
             line["pcie_inclusive"] = pcie
         if shard_check:
             line["rule_shard"] = shard_check
-        if world == 1 and args.e2e_requests and not args.rule_shard:
+        if kind == "c3r2":  # each request's (scope, role) x (scope2, role2) forest is its own: no codec forest cache
+            line["end_to_end"] = "not run for c3r2 (see the c3 line)"
+        elif world == 1 and args.e2e_requests and not args.rule_shard:
             log("end to end: JSON -> native codec -> GPU -> decisions")
             line["end_to_end"] = end_to_end(kind, cs, sb, tables, dec, args.e2e_requests,
                                             max(1, min(16, os.cpu_count() or 1)))
@@ -651,7 +698,7 @@ def main():
             line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:
             log("oracle parity + CPU baseline (C++ oracle)")
-            frac = args.parity_fraction if kind in ("c2", "c3") else 1000 / n  # c5: 1M rules, 1000 requests
+            frac = args.parity_fraction if kind in ("c2", "c3", "c3r2", "c3adv") else 1000 / n  # c5: 1M rules, 1000 requests
             cb, par = oracle_parity(kind, doc, sb, dec, cs, frac, args.cpu_seconds)
             line["cpu_baseline"] = cb
             line["parity"] = par

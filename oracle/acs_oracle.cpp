@@ -602,6 +602,7 @@ struct Policy {
   VP raw;
   Target target;
   OrderedMap<Rule> rules;
+  bool null = false;  // a null Map entry (resourceManager re-reads, accessController.ts:138): {"id", "$null": true}
 };
 struct PolicySet {
   VP raw;
@@ -677,6 +678,11 @@ struct Oracle {
       for (VP py : iterate(prop(ps, "policies"))) {
         Policy p;
         p.raw = py;
+        if (truthy(get(py, "$null"))) {  // the fixture form of a null entry under this id
+          p.null = true;
+          s.policies.set(map_key(get(py, "id")), std::move(p));
+          continue;
+        }
         p.target = format_target(get(py, "target"));
         prepare_target(p.target);
         VP rules = get(py, "rules");
@@ -965,6 +971,7 @@ struct Oracle {
       bool multi = false;
       for (auto& kv : ps.policies.items) {
         const Policy& pol = kv.second;
+        if (pol.null) throw JSError{1};  // policy.effect of null (:439)
         VP pe = UNDEF;
         if (truthy(prop(pol.raw, "effect"))) pe = get(pol.raw, "effect");
         if (pol.target.present && length_gt0(pol.target.resources)) {
@@ -1366,6 +1373,7 @@ struct Oracle {
       VP pe = UNDEF;
       for (auto& pkv : pset.policies.items) {  // loop 2a (:136-157)
         const Policy& pol = pkv.second;
+        if (pol.null) throw JSError{1};  // policy.effect of null (:138)
         VP eff = prop(pol.raw, "effect");
         if (truthy(eff)) pe = eff;
         if (pol.target.present && target_matches(pol.target, request, pe, false)) {
@@ -1381,6 +1389,7 @@ struct Oracle {
       }
       for (auto& pkv : pset.policies.items) {  // loop 2b (:167-290)
         const Policy& pol = pkv.second;
+        if (pol.null) continue;  // if (!policy) continue
         std::vector<Effect> rule_effects;
         const bool gate = !pol.target.present || (exact && target_matches(pol.target, request, pe, false)) ||
                           (!exact && target_matches(pol.target, request, pe, true));
@@ -1460,6 +1469,7 @@ struct Oracle {
       VP pe = UNDEF;
       for (auto& pkv : pset.policies.items) {  // :353-368 (the CA branch never fires, as in isAllowed)
         const Policy& pol = pkv.second;
+        if (pol.null) throw JSError{1};  // policy.effect of null
         VP eff = prop(pol.raw, "effect");
         if (truthy(eff)) pe = eff;
         if (pol.target.present && target_matches(pol.target, request, pe, false, masks)) {
@@ -1476,7 +1486,7 @@ struct Oracle {
       std::vector<uint32_t> pols, rules;
       for (size_t q = 0; q < pset.policies.items.size(); ++q) {  // :378-414
         const Policy& pol = pset.policies.items[q].second;
-        if (!truthy(pol.raw)) continue;
+        if (pol.null || !truthy(pol.raw)) continue;
         const bool gate = !pol.target.present || (exact && target_matches(pol.target, request, pe, false, masks)) ||
                           (!exact && target_matches(pol.target, request, pe, true, masks));
         if (!gate) continue;

@@ -144,6 +144,9 @@ def populate_store(doc):
     for ps in doc["policy_sets"]:
         policies = {}
         for py in iterate(ps["policies"]):
+            if isinstance(py, dict) and py.get("$null"):  # a null Map entry under this id (fixture form)
+                policies[_Key(py.get("id", UNDEF))] = None
+                continue
             rules = {}
             for ry in (py.get("rules") or []):
                 rule = _from_partial(ry, _RULE_KEYS)
