@@ -206,7 +206,7 @@ class NativeCodec:
 class PipelineStats(C.Structure):
     _fields_ = [("encode_s", C.c_double), ("wait_s", C.c_double), ("total_s", C.c_double), ("gpu_ms", C.c_double),
                 ("upload_bytes", C.c_double), ("requests", C.c_uint64), ("chunks", C.c_uint64),
-                ("host_requests", C.c_uint64)]
+                ("host_requests", C.c_uint64), ("split_s", C.c_double), ("check_s", C.c_double)]
 
 
 class Pipeline:

@@ -203,10 +203,15 @@ struct FilterAll {
 };
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
-// kernel before any lane diverges (all ones for a wave holding an unfiltered request).
+// kernel before any lane diverges (all ones for a wave holding an unfiltered request).  The
+// target verdicts are class facts: a wave of one class reads them from its LDS row (`single`);
+// in a wave that mixes classes each lane reads its own class row (`own`, L2-resident; nullptr
+// for an unfiltered lane: no verdicts).
 struct FilterLds {
   const uint32_t* lds;
   uint32_t wp, wr, wsu, wpu, wv;
+  const uint32_t* own;
+  bool single;
   ACS_FN uint32_t word(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
@@ -215,26 +220,18 @@ struct FilterLds {
     return lds[w];
 #endif
   }
-  // the kernel zeroes the verdict sections of a wave that mixes classes
-  ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
-#if defined(ACS_NO_VERDICT_CODE)  // A/B builds: the traversal without any verdict lookup
-    (void)sec;
-    (void)i;
-    return false;
-#else
-    return (word(wv + sec + (i >> 5)) >> (i & 31)) & 1u;
-#endif
-  }
-  // word w of the verdict section at `sec` (wave-uniform)
+  // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane)
   ACS_FN uint32_t vword(uint32_t sec, uint32_t w) const {
-#if defined(ACS_NO_VERDICT_CODE)
+#if defined(ACS_NO_VERDICT_CODE)  // A/B builds: the traversal without any verdict lookup
     (void)sec;
     (void)w;
     return 0u;
 #else
-    return word(wv + sec + w);
+    if (single) return word(wv + sec + w);
+    return own ? own[wv + sec + w] : 0u;
 #endif
   }
+  ACS_FN bool verdict(uint32_t sec, uint32_t i) const { return (vword(sec, i >> 5) >> (i & 31)) & 1u; }
 };
 
 // Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
@@ -1239,10 +1236,10 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
       }
-      // Rules a word at a time: the candidates whose retried target match the class already
-      // knows to be true (verdict section 4 WP: targets without properties, so they push no
-      // obligation) are included as a whole word, unread; only the rest are visited
-      // (accessController.ts:389-418).
+      // Rules a word at a time: the candidates whose retried target match the lane's class
+      // already knows to be true (verdict section 4 WP: targets without properties, so they
+      // push no obligation) are included as a whole word, unread; the wave visits only the
+      // rules some lane does not know (accessController.ts:389-418).
       bool any_rule = false;
       const uint32_t rb = P.child_begin, re = P.child_end;
       for (uint32_t base = rb & ~31u; base < re; base += 32) {
@@ -1250,15 +1247,16 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         uint32_t m = F.word(F.wr + w);
         if (base < rb) m &= ~0u << (rb & 31u);
         if (re - base < 32u) m &= (1u << (re - base)) - 1u;
-        const uint32_t known = m & F.vword(4 * WP, w);
+        const uint32_t known = m & F.vword(4 * WP, w);  // this lane's
         if (known) {
           bits.template set<2>(BL.wr + w, known);
           any_rule = true;
         }
-        uint32_t rest = m & ~known;
+        uint32_t rest = wave_or(m & ~known);
         while (rest) {
           const uint32_t r = wave_uniform(base + (uint32_t)__builtin_ctz(rest));
           rest &= rest - 1u;
+          if ((known >> (r & 31u)) & 1u) continue;  // included above
           const NodeRec Q = rule_at(T, r);
           if (Q.nflags & NF_NULL) continue;
           tri mt = 1;

@@ -71,6 +71,9 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
 #define ACS_AB_PROLOGUE_ONLY 0
 #endif
+#ifndef ACS_AB_WAVE_VERDICTS   // verdicts only in one-class waves (no per-lane class-row reads)
+#define ACS_AB_WAVE_VERDICTS 0
+#endif
 #ifndef ACS_AB_RADIX_ONLY      // the coherence sort always takes the radix passes
 #define ACS_AB_RADIX_ONLY 0
 #endif
@@ -268,6 +271,7 @@ __global__ __launch_bounds__(BLOCK) void radix_scatter_kernel(const uint32_t* __
 constexpr uint32_t CS_BINS = 65536;
 constexpr uint32_t CS_THREADS = 1024;
 constexpr uint32_t CS_MAX_CHUNK = 65535;  // per-block counts fit 16 bits
+constexpr uint32_t CS_ITEMS = 8;          // keys per thread per round
 
 __device__ inline void cs_zero(uint32_t* h, uint32_t K) {
   for (uint32_t w = threadIdx.x; w < (K + 1) / 2; w += CS_THREADS) h[w] = 0;
@@ -281,10 +285,22 @@ __global__ __launch_bounds__(CS_THREADS) void class_count_kernel(Batch B, uint32
   __shared__ uint32_t h[CS_BINS / 2];
   cs_zero(h, K);
   const uint32_t i0 = blockIdx.x * chunk, i1 = i0 + chunk < B.n ? i0 + chunk : B.n;
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += CS_THREADS) {
-    const uint32_t key = sort_key(B, i, lowbits, cbits);
-    keys[i] = key;
-    atomicAdd(&h[key >> 1], 1u << ((key & 1u) * 16u));
+  // CS_ITEMS keys per thread per round, their header reads all in flight before the atomics
+  for (uint32_t r0 = i0; r0 < i1; r0 += CS_ITEMS * CS_THREADS) {
+    uint32_t key[CS_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < CS_ITEMS; ++j) {
+      const uint32_t i = r0 + j * CS_THREADS + threadIdx.x;
+      key[j] = i < i1 ? sort_key(B, i, lowbits, cbits) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < CS_ITEMS; ++j) {
+      const uint32_t i = r0 + j * CS_THREADS + threadIdx.x;
+      if (i < i1) {
+        keys[i] = key[j];
+        atomicAdd(&h[key[j] >> 1], 1u << ((key[j] & 1u) * 16u));
+      }
+    }
   }
   __syncthreads();
   uint32_t* row = counts + (size_t)blockIdx.x * K;
@@ -346,10 +362,24 @@ __global__ __launch_bounds__(CS_THREADS) void class_scatter_kernel(const uint32_
   cs_zero(h, K);
   const uint32_t i0 = blockIdx.x * chunk, i1 = i0 + chunk < n ? i0 + chunk : n;
   const uint32_t* row = counts + (size_t)blockIdx.x * K;
-  for (uint32_t i = i0 + threadIdx.x; i < i1; i += CS_THREADS) {
-    const uint32_t key = keys[i], sh = (key & 1u) * 16u;
-    const uint32_t rank = (atomicAdd(&h[key >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    perm[base[key] + row[key] + rank] = i;
+  for (uint32_t r0 = i0; r0 < i1; r0 += CS_ITEMS * CS_THREADS) {
+    uint32_t key[CS_ITEMS], at[CS_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < CS_ITEMS; ++j) {
+      const uint32_t i = r0 + j * CS_THREADS + threadIdx.x;
+      key[j] = i < i1 ? keys[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < CS_ITEMS; ++j) at[j] = base[key[j]] + row[key[j]];  // all in flight
+#pragma unroll
+    for (uint32_t j = 0; j < CS_ITEMS; ++j) {
+      const uint32_t i = r0 + j * CS_THREADS + threadIdx.x;
+      if (i < i1) {
+        const uint32_t sh = (key[j] & 1u) * 16u;
+        const uint32_t rank = (atomicAdd(&h[key[j] >> 1], 1u << sh) >> sh) & 0xFFFFu;
+        perm[at[j] + rank] = i;
+      }
+    }
   }
 }
 
@@ -408,7 +438,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
 // The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
 // W-word LDS region, all ones when the wave holds an unfiltered request.
 __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv};
+  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, nullptr, false};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
@@ -435,11 +465,11 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
   }
   if (all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
-  // the verdicts hold for a wave of one class (role keys may differ: role rows keep the
-  // verdict sections whole); any other wave reads zeros there (the LDS form is only chosen
-  // for batches that carry verdict sections)
-  if (all || classes != 1 || B.no_verdicts)
-    for (uint32_t w = B.cand_wv + lane; w < W; w += 64) lds[w] = 0u;
+  // the verdicts are the class's (role keys may differ: role rows keep the verdict sections
+  // whole): a wave of one class reads them from LDS, any other lane from its own class row
+  // (the LDS form is only chosen for batches that carry verdict sections)
+  F.single = !all && classes == 1 && !B.no_verdicts;
+  F.own = valid && cls < B.cand_rows && !B.no_verdicts && !ACS_AB_WAVE_VERDICTS ? B.cand + (size_t)cls * W : nullptr;
   return F;
 }
 
@@ -1802,6 +1832,7 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
   size_t n = 0;
   acs_internal_items* items = acs_internal_split(json, len, p->threads, &n);
   if (!items) return -1;
+  if (st) st->split_s = steady_s() - t0;
   *n_out = n;
   struct Free {
     acs_internal_items* it;
@@ -1826,7 +1857,9 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     S.n = hi - lo;
     acs_tables* T = S.T;
     acs_req_batch view;
+    const double c0 = steady_s();
     if (acs_codec_batch_view(b, &view) || check_batch(T, &view)) return -1;
+    if (st) st->check_s += steady_s() - c0;
     HIP_OK(hipSetDevice(T->device));
     if (S.stage_n < S.n) {
       if (S.stage) HIP_OK(hipHostFree(S.stage));

@@ -321,7 +321,8 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
             "what": "JSON text -> acs_pipeline (delimit; per 131072-request chunk: native encode into page-locked "
                     "blocks || upload + coherence sort + K1 + download of the previous chunk on a second stream) -> "
                     "decision records in host memory; codec caches warm (steady state)",
-            "stages": {"total_s": st["total_s"], "encode_s": st["encode_s"], "device_wait_s": st["wait_s"],
+            "stages": {"total_s": st["total_s"], "split_s": st["split_s"], "encode_s": st["encode_s"],
+                       "check_s": st["check_s"], "device_wait_s": st["wait_s"],
                        "device_ms": st["gpu_ms"], "chunks": int(st["chunks"]),
                        "upload_bytes_per_request": st["upload_bytes"] / n,
                        "host_path_requests": int(st["host_requests"])},

@@ -287,6 +287,8 @@ typedef struct {
   double gpu_ms;        /* device time (upload + sort + K1 + download), summed over chunks */
   double upload_bytes;  /* bytes copied to the device */
   uint64_t requests, chunks, host_requests;
+  double split_s;       /* host time delimiting the request array */
+  double check_s;       /* host time validating the encoded chunks (acs_is_allowed's batch checks) */
 } acs_pipeline_stats;
 acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint32_t chunk);
 void acs_pipeline_free(acs_pipeline* p);

@@ -1640,14 +1640,16 @@ int acs_oracle_is_allowed_shared(void* h, const char* shared_json, const char* r
   }
   if (threads < 1) threads = 1;
   std::atomic<size_t> next{0};
+  // requests per grab: 64 for large calls, down to 1 so that every thread has work in a small one
+  const size_t grain = std::max<size_t>(1, std::min<size_t>(64, n / (4 * (size_t)threads)));
   const std::unordered_set<VP> shared_set(shared.begin(), shared.end());
   auto work = [&] {
     Oracle::SharedIds cache;
     cache.shared_values = &shared_set;
     for (;;) {
-      const size_t i = next.fetch_add(64);
+      const size_t i = next.fetch_add(grain);
       if (i >= n) return;
-      const size_t e = std::min(n, i + 64);
+      const size_t e = std::min(n, i + grain);
       for (size_t k = i; k < e; ++k) {
         Outcome r;
         try {
@@ -1708,11 +1710,13 @@ int acs_oracle_what_is_allowed_shared(void* h, const char* shared_json, const ch
   if (threads < 1) threads = 1;
   std::vector<std::string> parts(n);
   std::atomic<size_t> next{0};
+  // requests per grab: 64 for large calls, down to 1 so that every thread has work in a small one
+  const size_t grain = std::max<size_t>(1, std::min<size_t>(64, n / (4 * (size_t)threads)));
   auto work = [&] {
     for (;;) {
-      const size_t i = next.fetch_add(16);
+      const size_t i = next.fetch_add(grain);
       if (i >= n) return;
-      const size_t e = std::min(n, i + 16);
+      const size_t e = std::min(n, i + grain);
       for (size_t k = i; k < e; ++k) {
         std::string& s = parts[k];
         try {
