@@ -549,6 +549,59 @@ def snapshot_json(policy_sets: dict) -> bytes:
     return json.dumps(sets, ensure_ascii=False, separators=(",", ":")).encode("utf-8", "surrogatepass")
 
 
+def set_texts(policy_sets: dict) -> list:
+    """Each policy set's element of snapshot_json (the JSON text acs_store_builder_compile keys
+    its fragments by), in Map order."""
+    import json
+    snap = json.loads(snapshot_json(policy_sets))
+    return [json.dumps(x, ensure_ascii=False, separators=(",", ":")).encode("utf-8", "surrogatepass") for x in snap]
+
+
+class NativeStoreBuilder:
+    """acs_store_builder (include/acs_mi355x.h): the native compiler keeping one compiled
+    fragment per policy set, so a compile after a mutation recompiles only the changed sets."""
+
+    def __init__(self, urns: dict, combining_algorithms: list):
+        import ctypes as C
+        import json
+        from .native import last_error, load
+        self.C, self._err = C, last_error
+        self.lib = lib = load()
+        lib.acs_store_builder_create.restype = C.c_void_p
+        lib.acs_store_builder_create.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        lib.acs_store_builder_compile.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t,
+                                                  C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        lib.acs_store_builder_free.argtypes = [C.c_void_p]
+        lib.acs_blob_free.argtypes = [C.c_void_p]
+        u, c = json.dumps(urns).encode(), json.dumps(combining_algorithms).encode()
+        self.h = lib.acs_store_builder_create(u, len(u), c, len(c))
+        if not self.h:
+            raise Unsupported(last_error(lib))
+        self.recompiled = 0
+
+    def compile_texts(self, texts) -> bytes:
+        C = self.C
+        n = len(texts)
+        arr = (C.c_char_p * n)(*texts)
+        lens = (C.c_size_t * n)(*[len(t) for t in texts])
+        out, nb, rec = C.c_void_p(), C.c_size_t(), C.c_size_t()
+        if self.lib.acs_store_builder_compile(self.h, arr, lens, n, C.byref(out), C.byref(nb), C.byref(rec)) != 0:
+            raise Unsupported(self._err(self.lib))
+        self.recompiled = rec.value
+        try:
+            return C.string_at(out.value, nb.value)
+        finally:
+            self.lib.acs_blob_free(out)
+
+    def compile(self, policy_sets: dict) -> bytes:
+        return self.compile_texts(set_texts(policy_sets))
+
+    def close(self):
+        if self.h:
+            self.lib.acs_store_builder_free(self.h)
+            self.h = None
+
+
 def native_store_blob(policy_sets: dict, urns: dict, combining_algorithms: list) -> bytes:
     """The store image compiled by the native compiler (acs_store_compile)."""
     import ctypes as C

@@ -54,6 +54,8 @@ const char* const kProtoKeys[] = {"constructor", "__proto__", "toString", "toLoc
                                   "hasOwnProperty", "isPrototypeOf", "propertyIsEnumerable", "__defineGetter__",
                                   "__defineSetter__", "__lookupGetter__", "__lookupSetter__"};
 
+void json_write(std::string& o, const JV* v);
+
 struct Builder {
   // dictionary (compiler.Dictionary: 0 undefined, 1 null, 2 '')
   std::vector<std::string> strings{"", "", ""};
@@ -75,7 +77,7 @@ struct Builder {
     double num;
     std::string s;
     bool truthy;
-    const JV* v = nullptr;  // the value itself (JSON for the codec section)
+    std::string json;  // the value as JSON text (the codec section; outlives the parsed store)
   };
   std::vector<Ec> ec{{0, 0, "", false}, {1, 0, "", false}, {2, 0, "", false}, {3, 0, "", true}};
   // node tables + candidate specs (kind 0 never, 1 always, 2 rows)
@@ -151,7 +153,7 @@ struct Builder {
       for (size_t k = 4; k < ec.size(); ++k)
         if (ec[k].kind == x.kind && (x.kind == 4 ? ec[k].num == x.num : ec[k].s == x.s)) return (uint8_t)k;
     if (ec.size() >= 255) fail("too many distinct evaluation_cacheable values");
-    x.v = v;
+    json_write(x.json, v);
     ec.push_back(x);
     return (uint8_t)(ec.size() - 1);
   }
@@ -519,7 +521,7 @@ std::string build_image(Builder& b) {
   std::string ecj = "[";
   for (size_t k = 4; k < b.ec.size(); ++k) {
     if (k > 4) ecj += ',';
-    json_write(ecj, b.ec[k].v);
+    ecj += b.ec[k].json;
   }
   ecj += ']';
   const uint32_t ecn = (uint32_t)ecj.size();
@@ -545,9 +547,162 @@ std::string build_image(Builder& b) {
   return out;
 }
 
+// Combining algorithms (accessController.ts:51-62) and the URN config, URN ids interned first
+// in config order (compiler.compile_store).
+void configure(Builder& b, const JV* urns, const JV* cas) {
+  if (urns->t != J_OBJ) fail("urns: expected a JSON object");
+  if (cas->t != J_ARR) fail("combining algorithms: expected a JSON array");
+  for (uint32_t k = 0; k < cas->n; ++k) {
+    const JV* m = get(&cas->a[k], "method");
+    uint8_t code;
+    if (m->t == J_STR && m->str() == "denyOverrides") code = CA_DENY_OVERRIDES;
+    else if (m->t == J_STR && m->str() == "permitOverrides") code = CA_PERMIT_OVERRIDES;
+    else if (m->t == J_STR && m->str() == "firstApplicable") code = CA_FIRST_APPLICABLE;
+    else fail("combining algorithm method");
+    const JV* u = get(&cas->a[k], "urn");
+    std::string key = u->t == J_UNDEF ? "m" : u->t == J_NULL ? "n" : u->t == J_STR ? "s" + std::string(u->str()) : "x";
+    bool found = false;
+    for (auto& kv : b.ca_map)
+      if (kv.first == key) {
+        kv.second = code;
+        found = true;
+      }
+    if (!found) b.ca_map.push_back({key, code});
+  }
+  for (uint32_t k = 0; k < urns->n; ++k) {
+    const std::string name(urns->o[k].key());
+    const JV* v = &urns->o[k].v;
+    if (b.urn.count(name)) {
+      b.urn[name] = v;
+    } else {
+      b.urn.emplace(name, v);
+      b.urns.push_back({name, v});
+    }
+  }
+  for (auto& kv : b.urns) b.intern(b.urn[kv.first]);
+}
+
+// compiler.mark_clean_below: NF_CLEAN_BELOW on a set when every earlier set is clean
+// (NF_COND_FREE, valid combining algorithm, no null policy)
+void mark_clean_below(Builder& b) {
+  bool clean_so_far = true;
+  for (NodeRec& S : b.sets) {
+    if (clean_so_far) S.nflags |= NF_CLEAN_BELOW;
+    bool clean = (S.nflags & NF_COND_FREE) && S.ca != CA_INVALID;
+    for (uint32_t p = S.child_begin; p < S.child_end && clean; ++p)
+      if (b.pols[p].nflags & NF_NULL) clean = false;
+    clean_so_far = clean_so_far && clean;
+  }
+}
+
+int emit(const std::string& img, void** blob_out, size_t* blob_len) {
+  void* mem = malloc(img.size());
+  if (!mem) fail("out of memory");
+  memcpy(mem, img.data(), img.size());
+  *blob_out = mem;
+  *blob_len = img.size();
+  return 0;
+}
+
+// ------------------------------------------------------------------ incremental compile
+// One policy set compiled alone: its node records and pools with offsets from 0 (the
+// Builder's per-set state while it was compiled), keyed by the set's JSON text.  The
+// dictionary, regex rows and evaluation_cacheable table live in the builder and only grow,
+// so a fragment's interned ids stay valid across compiles (compiler.IncrementalCompiler).
+struct Fragment {
+  uint64_t h1 = 0, h2 = 0;
+  size_t len = 0;
+  std::vector<NodeRec> sets, pols, rules;
+  std::vector<RuleResAttr> rres;
+  std::vector<Pair> pairs;
+  std::vector<uint32_t> u32pool;
+  std::vector<uint8_t> spec_kind[3];
+  std::vector<std::vector<uint32_t>> spec_rows[3];
+};
+
+void swap_state(Builder& b, Fragment& f) {
+  std::swap(b.sets, f.sets);
+  std::swap(b.pols, f.pols);
+  std::swap(b.rules, f.rules);
+  std::swap(b.rres, f.rres);
+  std::swap(b.pairs, f.pairs);
+  std::swap(b.u32pool, f.u32pool);
+  for (int k = 0; k < 3; ++k) {
+    std::swap(b.spec_kind[k], f.spec_kind[k]);
+    std::swap(b.spec_rows[k], f.spec_rows[k]);
+  }
+}
+
+// a target's pool offsets (present targets only: an absent one keeps zeros)
+void shift_target(NodeRec& R, uint32_t pairs0, uint32_t rres0, uint32_t u320) {
+  if (!(R.nflags & NF_HAS_TARGET)) return;
+  R.subj_off += pairs0;
+  R.act_off += pairs0;
+  R.res_off += rres0;
+  R.acl_roles_off += u320;
+}
+
+// Append fragment f to the builder's tables, its offsets shifted to where it lands.
+void append(Builder& b, const Fragment& f) {
+  const uint32_t P0 = (uint32_t)b.pols.size(), R0 = (uint32_t)b.rules.size();
+  const uint32_t RR0 = (uint32_t)b.rres.size(), PA0 = (uint32_t)b.pairs.size(), U0 = (uint32_t)b.u32pool.size();
+  for (NodeRec S : f.sets) {
+    S.child_begin += P0;
+    S.child_end += P0;
+    shift_target(S, PA0, RR0, U0);
+    b.sets.push_back(S);
+  }
+  for (NodeRec P : f.pols) {
+    P.child_begin += R0;
+    P.child_end += R0;
+    P.fe += R0;
+    shift_target(P, PA0, RR0, U0);
+    b.pols.push_back(P);
+  }
+  for (NodeRec Q : f.rules) {
+    shift_target(Q, PA0, RR0, U0);
+    b.rules.push_back(Q);
+  }
+  b.rres.insert(b.rres.end(), f.rres.begin(), f.rres.end());
+  b.pairs.insert(b.pairs.end(), f.pairs.begin(), f.pairs.end());
+  b.u32pool.insert(b.u32pool.end(), f.u32pool.begin(), f.u32pool.end());
+  for (int k = 0; k < 3; ++k) {
+    b.spec_kind[k].insert(b.spec_kind[k].end(), f.spec_kind[k].begin(), f.spec_kind[k].end());
+    b.spec_rows[k].insert(b.spec_rows[k].end(), f.spec_rows[k].begin(), f.spec_rows[k].end());
+  }
+}
+
+// Two independent 64-bit hashes of a set's text in one pass (fragment identity: 128 bits and
+// the length).
+void text_hash(const char* p, size_t n, uint64_t* h1_out, uint64_t* h2_out) {
+  uint64_t h1 = 0x243F6A8885A308D3ull ^ (n * 0x9E3779B97F4A7C15ull), h2 = 0x13198A2E03707344ull ^ n;
+  size_t k = 0;
+  for (; k + 8 <= n; k += 8) {
+    uint64_t w;
+    memcpy(&w, p + k, 8);
+    h1 = (h1 ^ w) * 0xFF51AFD7ED558CCDull;
+    h1 ^= h1 >> 29;
+    h2 = (h2 + w) * 0xC4CEB9FE1A85EC53ull;
+    h2 ^= h2 >> 31;
+  }
+  uint64_t w = 0;
+  memcpy(&w, p + k, n - k);
+  h1 = (h1 ^ w) * 0xC4CEB9FE1A85EC53ull;
+  h2 = (h2 + w) * 0xFF51AFD7ED558CCDull;
+  *h1_out = h1 ^ (h1 >> 31);
+  *h2_out = h2 ^ (h2 >> 29);
+}
+
 thread_local std::string g_compile_err;
 
 }  // namespace
+
+struct acs_store_builder {
+  std::string urns_text, cas_text;  // the parsed config's bytes (the Builder points into them)
+  Arena ar;
+  Builder b;
+  std::vector<Fragment> frags;      // the last compile's sets, in Map order
+};
 
 extern "C" {
 
@@ -565,55 +720,12 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
     const JV* urns = p1.parse(urns_json, urns_json + urns_len);
     const JV* cas = p2.parse(cas_json, cas_json + cas_len);
     const JV* st = p3.parse(store_json, store_json + store_len);
-    if (urns->t != J_OBJ) fail("urns: expected a JSON object");
-    if (cas->t != J_ARR) fail("combining algorithms: expected a JSON array");
     if (st->t != J_ARR) fail("store: expected a JSON array of policy sets (Map values in order)");
     Builder b;
-    for (uint32_t k = 0; k < cas->n; ++k) {  // accessController.ts:51-62
-      const JV* m = get(&cas->a[k], "method");
-      uint8_t code;
-      if (m->t == J_STR && m->str() == "denyOverrides") code = CA_DENY_OVERRIDES;
-      else if (m->t == J_STR && m->str() == "permitOverrides") code = CA_PERMIT_OVERRIDES;
-      else if (m->t == J_STR && m->str() == "firstApplicable") code = CA_FIRST_APPLICABLE;
-      else fail("combining algorithm method");
-      const JV* u = get(&cas->a[k], "urn");
-      std::string key = u->t == J_UNDEF ? "m" : u->t == J_NULL ? "n" : u->t == J_STR ? "s" + std::string(u->str()) : "x";
-      bool found = false;
-      for (auto& kv : b.ca_map)
-        if (kv.first == key) {
-          kv.second = code;
-          found = true;
-        }
-      if (!found) b.ca_map.push_back({key, code});
-    }
-    for (uint32_t k = 0; k < urns->n; ++k) {  // URN ids first, in config order
-      const std::string name(urns->o[k].key());
-      const JV* v = &urns->o[k].v;
-      if (b.urn.count(name)) {
-        b.urn[name] = v;
-      } else {
-        b.urn.emplace(name, v);
-        b.urns.push_back({name, v});
-      }
-    }
-    for (auto& kv : b.urns) b.intern(b.urn[kv.first]);
+    configure(b, urns, cas);
     for (uint32_t k = 0; k < st->n; ++k) b.compile_set(&st->a[k]);
-    // compiler.mark_clean_below: every earlier set clean (NF_COND_FREE, valid CA, no null policy)
-    bool clean_so_far = true;
-    for (NodeRec& S : b.sets) {
-      if (clean_so_far) S.nflags |= NF_CLEAN_BELOW;
-      bool clean = (S.nflags & NF_COND_FREE) && S.ca != CA_INVALID;
-      for (uint32_t p = S.child_begin; p < S.child_end && clean; ++p)
-        if (b.pols[p].nflags & NF_NULL) clean = false;
-      clean_so_far = clean_so_far && clean;
-    }
-    const std::string img = build_image(b);
-    void* mem = malloc(img.size());
-    if (!mem) fail("out of memory");
-    memcpy(mem, img.data(), img.size());
-    *blob_out = mem;
-    *blob_len = img.size();
-    return 0;
+    mark_clean_below(b);
+    return emit(build_image(b), blob_out, blob_len);
   } catch (const CompileError& e) {
     g_compile_err = "acs_store_compile: " + e.why;
   } catch (const ParseError& e) {
@@ -624,5 +736,107 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
 }
 
 void acs_blob_free(void* blob) { free(blob); }
+
+acs_store_builder* acs_store_builder_create(const char* urns_json, size_t urns_len, const char* cas_json,
+                                            size_t cas_len) {
+  if (!urns_json || !cas_json) {
+    acs_internal_set_error("acs_store_builder_create: null argument");
+    return nullptr;
+  }
+  auto* sb = new acs_store_builder();
+  try {
+    sb->urns_text.assign(urns_json, urns_len);
+    sb->cas_text.assign(cas_json, cas_len);
+    Parser p1(sb->ar), p2(sb->ar);
+    const JV* urns = p1.parse(sb->urns_text.data(), sb->urns_text.data() + sb->urns_text.size());
+    const JV* cas = p2.parse(sb->cas_text.data(), sb->cas_text.data() + sb->cas_text.size());
+    configure(sb->b, urns, cas);
+    return sb;
+  } catch (const CompileError& e) {
+    g_compile_err = "acs_store_builder_create: " + e.why;
+  } catch (const ParseError& e) {
+    g_compile_err = std::string("acs_store_builder_create: ") + e.what;
+  }
+  acs_internal_set_error(g_compile_err.c_str());
+  delete sb;
+  return nullptr;
+}
+
+void acs_store_builder_free(acs_store_builder* sb) { delete sb; }
+
+int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, const size_t* lens, size_t n,
+                              void** blob_out, size_t* blob_len, size_t* recompiled) {
+  if (!sb || (n && (!sets || !lens)) || !blob_out || !blob_len) {
+    acs_internal_set_error("acs_store_builder_compile: null argument");
+    return -1;
+  }
+  *blob_out = nullptr;
+  *blob_len = 0;
+  size_t fresh = 0;
+  Builder& b = sb->b;
+  try {
+    // previous fragments by text hash: an unchanged set is reused as compiled
+    std::unordered_multimap<uint64_t, size_t> old;
+    for (size_t k = 0; k < sb->frags.size(); ++k) old.emplace(sb->frags[k].h1, k);
+    std::vector<bool> taken(sb->frags.size(), false);
+    std::vector<Fragment> next(n);
+    for (size_t k = 0; k < n; ++k) {
+      if (!sets[k]) {  // the caller's word: set k is the previous compile's set lens[k], unchanged
+        const size_t j = lens[k];
+        if (j >= sb->frags.size() || taken[j]) fail("unchanged-set index out of range or repeated");
+        next[k] = std::move(sb->frags[j]);
+        taken[j] = true;
+        continue;
+      }
+      uint64_t h1, h2;
+      text_hash(sets[k], lens[k], &h1, &h2);
+      bool reused = false;
+      auto range = old.equal_range(h1);
+      for (auto it = range.first; it != range.second && !reused; ++it) {
+        Fragment& f = sb->frags[it->second];
+        if (!taken[it->second] && f.h2 == h2 && f.len == lens[k]) {
+          next[k] = std::move(f);
+          taken[it->second] = true;
+          reused = true;
+        }
+      }
+      if (reused) continue;
+      Arena ar;
+      Parser p(ar);
+      const JV* ps = p.parse(sets[k], sets[k] + lens[k]);
+      Fragment& f = next[k];
+      swap_state(b, f);  // the builder's per-set state is empty between compiles
+      try {
+        b.compile_set(ps);
+      } catch (...) {
+        swap_state(b, f);
+        f = Fragment{};
+        throw;
+      }
+      swap_state(b, f);
+      f.h1 = h1;
+      f.h2 = h2;
+      f.len = lens[k];
+      ++fresh;
+    }
+    for (const Fragment& f : next) append(b, f);
+    mark_clean_below(b);
+    const std::string img = build_image(b);
+    Fragment empty;  // leave the builder's per-set state empty again
+    swap_state(b, empty);
+    sb->frags = std::move(next);
+    if (recompiled) *recompiled = fresh;
+    return emit(img, blob_out, blob_len);
+  } catch (const CompileError& e) {
+    g_compile_err = "acs_store_builder_compile: " + e.why;
+  } catch (const ParseError& e) {
+    g_compile_err = std::string("acs_store_builder_compile: ") + e.what;
+  }
+  Fragment empty;
+  swap_state(b, empty);
+  sb->frags.clear();  // (some fragments may have moved out: the next compile starts afresh)
+  acs_internal_set_error(g_compile_err.c_str());
+  return -1;
+}
 
 }  // extern "C"

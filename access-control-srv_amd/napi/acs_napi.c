@@ -8,6 +8,10 @@
  *
  * JS surface:
  *   compileStore(storeJson, urnsJson, casJson) -> Uint8Array   acs_store_compile
+ *   storeBuilderCreate(urnsJson, casJson) -> builder            acs_store_builder_create
+ *   storeBuilderCompile(builder, sets[]) -> {blob, recompiled}  acs_store_builder_compile
+ *     (sets[k]: set k's JSON text, or j = the previous compile's set j, unchanged)
+ *   storeBuilderFree(builder)                                   acs_store_builder_free
  *   compile(blob: Uint8Array, device?) -> tables                acs_compile
  *     (device = [d0, d1, ...]: one image per device, acs_compile_multi)
  *   devices(tables) -> number[]                                 acs_device_list
@@ -86,8 +90,8 @@ static napi_value throw_acs(napi_env env, const char* what) {
  * codecFree(codec), batchFree(batch) — and whatever is still registered when the environment
  * is torn down is released by its cleanup hook (objects with work in flight are left to the
  * process exit).  Each environment (main thread, worker_threads) has its own registry. */
-enum { H_TABLES = 1, H_CODEC = 2, H_BATCH = 3, H_PIPELINE = 4 };
-static const char* const KIND_KEY[5] = {"", "acsTables", "acsCodec", "acsBatch", "acsPipeline"};
+enum { H_TABLES = 1, H_CODEC = 2, H_BATCH = 3, H_PIPELINE = 4, H_BUILDER = 5 };
+static const char* const KIND_KEY[6] = {"", "acsTables", "acsCodec", "acsBatch", "acsPipeline", "acsStoreBuilder"};
 
 typedef struct env_state env_state;
 
@@ -125,6 +129,11 @@ typedef struct {
 } pipeline_h;
 
 typedef struct {
+  obj_base base;
+  acs_store_builder* b;
+} builder_h;
+
+typedef struct {
   int kind; /* 0: never used */
   uint32_t gen;
   obj_base* obj; /* NULL: freed (slot reusable) */
@@ -156,6 +165,10 @@ static void obj_release(obj_base* o) {
     if (h->codec) obj_unref(&h->codec->base);
     h->tables = NULL;
     h->codec = NULL;
+  } else if (o->kind == H_BUILDER) {
+    builder_h* h = (builder_h*)o;
+    if (h->b) acs_store_builder_free(h->b);
+    h->b = NULL;
   } else if (o->kind == H_BATCH) {
     batch_h* h = (batch_h*)o;
     if (h->b) acs_codec_batch_free(h->b); /* before its codec */
@@ -175,8 +188,8 @@ static void on_env_exit(void* arg) {
   env_state* st = (env_state*)arg;
   st->dead = 1;
   /* pipelines and batches first (they hold their codec / tables), then codecs and tables */
-  static const int order[4] = {H_PIPELINE, H_BATCH, H_CODEC, H_TABLES};
-  for (int k = 0; k < 4; ++k)
+  static const int order[5] = {H_PIPELINE, H_BATCH, H_CODEC, H_TABLES, H_BUILDER};
+  for (int k = 0; k < 5; ++k)
     for (uint32_t i = 0; i < st->n; ++i) {
       slot_t* s = &st->slots[i];
       if (!s->obj || s->obj->kind != order[k]) continue;
@@ -538,6 +551,118 @@ static napi_value js_compile_store(napi_env env, napi_callback_info info) {
   for (int k = 0; k < 3; ++k)
     if (own[k]) free(s[k]);
   return ret;
+}
+
+/* storeBuilderCreate(urnsJson, casJson) -> builder: acs_store_builder_create (incremental
+ * compile, one fragment per policy set). */
+static napi_value js_builder_create(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  char* s[2] = {NULL, NULL};
+  size_t n[2] = {0, 0};
+  int own[2] = {0, 0};
+  int ok = argc == 2;
+  for (int k = 0; k < 2 && ok; ++k) ok = get_text(env, argv[k], &s[k], &n[k], &own[k]) == 0;
+  napi_value ret = NULL;
+  if (!ok) {
+    napi_throw_type_error(env, NULL, "storeBuilderCreate(urnsJson, casJson)");
+  } else {
+    acs_store_builder* b = acs_store_builder_create(s[0], n[0], s[1], n[1]);
+    if (!b) {
+      throw_acs(env, "acs_store_builder_create");
+    } else {
+      builder_h* h = (builder_h*)calloc(1, sizeof *h);
+      if (!h) {
+        acs_store_builder_free(b);
+        napi_throw_error(env, NULL, "out of memory");
+      } else {
+        h->b = b;
+        ret = make_handle(env, &h->base, H_BUILDER);
+      }
+    }
+  }
+  for (int k = 0; k < 2; ++k)
+    if (own[k]) free(s[k]);
+  return ret;
+}
+
+/* storeBuilderCompile(builder, sets) -> {blob: Uint8Array, recompiled}: sets[k] is policy set
+ * k's JSON text (Map order), or a number j: the previous compile's set j, unchanged. */
+static napi_value js_builder_compile(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int freed = 0;
+  builder_h* h = argc == 2 ? (builder_h*)lookup(env, argv[0], H_BUILDER, &freed) : NULL;
+  bool is_arr = false;
+  if (!h || napi_is_array(env, argv[1], &is_arr) != napi_ok || !is_arr) {
+    napi_throw_type_error(env, NULL, freed ? "store builder already freed" : "storeBuilderCompile(builder, sets[])");
+    return NULL;
+  }
+  uint32_t n = 0;
+  CHECK(env, napi_get_array_length(env, argv[1], &n));
+  const char** texts = (const char**)calloc(n ? n : 1, sizeof *texts);
+  size_t* lens = (size_t*)calloc(n ? n : 1, sizeof *lens);
+  int* own = (int*)calloc(n ? n : 1, sizeof *own);
+  napi_value ret = NULL;
+  int ok = texts && lens && own;
+  for (uint32_t k = 0; k < n && ok; ++k) {
+    napi_value e;
+    napi_valuetype t;
+    ok = napi_get_element(env, argv[1], k, &e) == napi_ok && napi_typeof(env, e, &t) == napi_ok;
+    if (!ok) break;
+    if (t == napi_number) {
+      int64_t j = -1;
+      ok = napi_get_value_int64(env, e, &j) == napi_ok && j >= 0;
+      texts[k] = NULL;
+      lens[k] = (size_t)j;
+    } else {
+      char* p = NULL;
+      ok = get_text(env, e, &p, &lens[k], &own[k]) == 0;
+      texts[k] = p;
+    }
+  }
+  if (!ok) {
+    napi_throw_type_error(env, NULL, "storeBuilderCompile: sets[] holds JSON texts or previous indices");
+  } else {
+    void* blob = NULL;
+    size_t len = 0, rec = 0;
+    if (acs_store_builder_compile(h->b, texts, lens, n, &blob, &len, &rec) != 0) {
+      throw_acs(env, "acs_store_builder_compile");
+    } else {
+      void* d;
+      napi_value arr = new_u8(env, len, &d), obj, rv;
+      if (arr && napi_create_object(env, &obj) == napi_ok && napi_create_double(env, (double)rec, &rv) == napi_ok &&
+          napi_set_named_property(env, obj, "blob", arr) == napi_ok &&
+          napi_set_named_property(env, obj, "recompiled", rv) == napi_ok) {
+        memcpy(d, blob, len);
+        ret = obj;
+      }
+      acs_blob_free(blob);
+    }
+  }
+  for (uint32_t k = 0; k < n && own; ++k)
+    if (own[k]) free((void*)texts[k]);
+  free(texts);
+  free(lens);
+  free(own);
+  return ret;
+}
+
+/* storeBuilderFree(builder). */
+static napi_value js_builder_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  int freed = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  builder_h* h = argc > 0 ? (builder_h*)lookup(env, argv[0], H_BUILDER, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "storeBuilderFree(builder)");
+    return NULL;
+  }
+  handle_free(&h->base);
+  return NULL;
 }
 
 /* ------------------------------------------------------------------ tables */
@@ -1328,6 +1453,9 @@ static napi_value init(napi_env env, napi_value exports) {
   if (!get_state(env)) return NULL; /* this environment's handle registry + its cleanup hook */
   const napi_property_descriptor d[] = {
       {"compileStore", NULL, js_compile_store, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"storeBuilderCreate", NULL, js_builder_create, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"storeBuilderCompile", NULL, js_builder_compile, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"storeBuilderFree", NULL, js_builder_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},
       {"free", NULL, js_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecCreate", NULL, js_codec_create, NULL, NULL, NULL, napi_enumerable, NULL},

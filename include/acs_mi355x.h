@@ -243,6 +243,23 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
                       const char* cas_json, size_t cas_len, void** blob_out, size_t* blob_len);
 void acs_blob_free(void* blob);
 
+/* Incremental store compile for a host that mutates its policySets Map
+ * in place (accessController.ts:897-937 updatePolicySet .. removeRule, resourceManager.ts:274,
+ * 305): the builder keeps each policy set's compiled fragment keyed by the set's JSON text (the
+ * snapshot element acs_store_compile reads: JSON.stringify of the set with its combinables as
+ * arrays), so a compile recompiles only the sets whose text changed and re-concatenates the
+ * rest with shifted offsets.  Interned strings only accumulate (ids stay valid); the first
+ * compile of a builder is byte-identical to acs_store_compile of the same store.
+ * sets[k] / lens[k]: set k's JSON text in Map order — or sets[k] = NULL and lens[k] = j: set k
+ * is set j of the previous compile, unchanged (no text passed, nothing hashed); *recompiled:
+ * sets compiled afresh. */
+typedef struct acs_store_builder acs_store_builder;
+acs_store_builder* acs_store_builder_create(const char* urns_json, size_t urns_len, const char* cas_json,
+                                            size_t cas_len);
+int acs_store_builder_compile(acs_store_builder* b, const char* const* sets, const size_t* lens, size_t n,
+                              void** blob_out, size_t* blob_len, size_t* recompiled);
+void acs_store_builder_free(acs_store_builder* b);
+
 typedef struct acs_codec acs_codec;
 typedef struct acs_codec_batch acs_codec_batch;
 #define ACS_RQ_HOST 0x2u

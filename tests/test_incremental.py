@@ -156,6 +156,47 @@ def test_incremental_recompiles_only_touched_sets():
     assert got  # the updated rule was evaluated
 
 
+def _native_records(blob, reqs):
+    """isAllowed records of ``reqs`` against a native-compiled image (its own codec, CPU core)."""
+    import ctypes as C
+    from acs_mi355x.codec import NativeCodec
+    nb = NativeCodec(blob).encode(reqs)
+    out = np.zeros(nb.n, L.DECISION_DT)
+    assert host_core.lib().acs_host_is_allowed(blob, len(blob), C.byref(nb.struct), out.ctypes.data) == 0
+    return out.view(np.uint64)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_native_builder_matches_fresh_compile(seed):
+    """acs_store_builder (the Node drop-in's incremental compile): its first image is the
+    full compiler's byte for byte; after each mutation it recompiles at most the touched set
+    and decides every request exactly as a fresh full compile of the mutated Map."""
+    urns, doc, reqs = randgen.rand_case(seed)
+    try:
+        base = pstore.populate(doc)
+        first = compiler.native_store_blob(base, urns, DEFAULT_CAS)
+    except Exception:
+        pytest.skip("store outside the compiled subset")
+    b = compiler.NativeStoreBuilder(urns, DEFAULT_CAS)
+    assert b.compile(base) == first and b.recompiled == len(base)
+    donors = list(pstore.populate(randgen.rand_case(seed + 1000)[1]).values()) or list(base.values())
+    rng = random.Random(seed)
+    ctl = _ctl(urns)
+    ctl.policySets = base
+    for step in range(8):
+        op = _mutate(rng, ctl, donors)
+        try:
+            fresh = compiler.native_store_blob(ctl.policySets, urns, DEFAULT_CAS)
+        except compiler.Unsupported:
+            with pytest.raises(compiler.Unsupported):
+                b.compile(ctl.policySets)
+            return
+        blob = b.compile(ctl.policySets)
+        assert b.recompiled <= 1, (seed, step, op)
+        assert np.array_equal(_native_records(blob, reqs), _native_records(fresh, reqs)), (seed, step, op)
+    b.close()
+
+
 def test_fresh_compile_is_byte_stable():
     """compile_store (one IncrementalCompiler pass) gives the same blob twice."""
     m = pstore.populate(synth.c2_store())
@@ -194,8 +235,10 @@ def test_incremental_gpu(seed):
         try:
             got = ctl.isAllowed_batch(reqs)
             got_w = ctl.whatIsAllowed_batch(reqs)
-        except Exception:
-            return  # an unsupported store: covered by the CPU test's both-paths-agree check
+        except Exception as e:  # an unsupported store: a fresh compile refuses it the same way
+            with pytest.raises(type(e)):
+                compiler.compile_store(ctl.policySets, urns, DEFAULT_CAS)
+            return
         fresh = AccessController(opts)
         fresh.policySets = dict(ctl.policySets)
         assert [repr(x) for x in got] == [repr(x) for x in fresh.isAllowed_batch(reqs)], (seed, step, op)
