@@ -68,22 +68,26 @@ function without(o, drop) {
   return out;
 }
 
-// The policySets Map as the JSON text acs_store_compile reads: the Map's values in order,
-// each set's / policy's `combinables` the array of its Map's values (null entries kept).
-function snapshotStore(policySets) {
-  const sets = mapValues(policySets).map((ps) => {
-    if (!ps || typeof ps !== 'object') return null;
-    const s = without(ps, ['combinables', 'policies']);
-    s.combinables = mapValues(ps.combinables).map((p) => {
-      if (!p || typeof p !== 'object') return null;
-      const po = without(p, ['combinables']);
-      po.combinables = mapValues(p.combinables).map((r) => (r && typeof r === 'object' ? r : null));
-      return po;
-    });
-    return s;
+// One policy set as an element of the snapshot acs_store_compile reads: the set with its
+// `combinables` the array of its Map's values, each policy's likewise (null entries kept).
+function snapshotSet(ps) {
+  if (!ps || typeof ps !== 'object') return null;
+  const s = without(ps, ['combinables', 'policies']);
+  s.combinables = mapValues(ps.combinables).map((p) => {
+    if (!p || typeof p !== 'object') return null;
+    const po = without(p, ['combinables']);
+    po.combinables = mapValues(p.combinables).map((r) => (r && typeof r === 'object' ? r : null));
+    return po;
   });
-  return JSON.stringify(sets);
+  return s;
 }
+
+// The policySets Map as the JSON text acs_store_compile reads: the Map's values in order.
+function snapshotStore(policySets) {
+  return JSON.stringify(mapValues(policySets).map(snapshotSet));
+}
+
+const isNil = (v) => v === undefined || v === null; // lodash _.isNil
 
 // The node order of the compiled image (acs_mi355x/compiler.py _compile_set/_assemble):
 // sets in Map order, their policies flattened (null entries keep a slot), then rules.
@@ -130,6 +134,7 @@ class GpuAccessController {
     this.threads = o.threads || 4;
     this.chunk = o.chunk || 0; // pipeline chunk (requests); 0: the library's default
     this.pipelineBytes = o.pipelineBytes === undefined ? (1 << 20) : o.pipelineBytes; // null: never
+    this.compileOnly = !!o.compileOnly; // compile the image only (no device): this.blob
     this.pipeline = null;
     this.hostEvaluator = o.hostEvaluator || null;
     this.urns = urns instanceof Map ? Object.fromEntries(urns) : urns;
@@ -137,13 +142,48 @@ class GpuAccessController {
     this.stats = { requests: 0, host: 0, compiles: 0 };
     this.tables = null;
     this.codec = null;
+    // incremental compile (acs_store_builder): one compiled fragment per policy set; a refresh
+    // passes the sets it knows unchanged by their previous index, the others as JSON text
+    this.builder = addon.storeBuilderCreate(JSON.stringify(this.urns), JSON.stringify(this.cas));
+    this.setIndex = new Map(); // set key -> {obj, index} of the last compile
+    this.dirty = new Set();    // set keys the mutators touched since (null: unknown, re-serialise all)
+    this.stale = false;
+    this.lastRefresh = null;   // {ms, recompiled, sets}
     this.refresh(policySets);
   }
 
   // Recompile from the (mutated) policySets Map; the reference re-reads its Map on every
-  // request, so call this after each policy CRUD event (before the next batch).
-  refresh(policySets) {
-    const blob = addon.compileStore(snapshotStore(policySets), JSON.stringify(this.urns), JSON.stringify(this.cas));
+  // request, so call this after each policy CRUD event (before the next batch).  `changed`
+  // (optional): the ids of the policy sets the event touched; every other set still holding
+  // the object it held at the last refresh is passed to the builder as unchanged (neither
+  // re-serialised nor recompiled).  Without it every set is re-serialised, and the builder
+  // still recompiles only the sets whose JSON text changed.
+  refresh(policySets, changed) {
+    const t0 = Date.now();
+    const dirty = changed ? new Set(changed) : null;
+    const entries = policySets instanceof Map ? Array.from(policySets.entries())
+      : mapValues(policySets).map((ps, k) => [k, ps]);
+    const items = new Array(entries.length);
+    for (let k = 0; k < entries.length; ++k) {
+      const [key, ps] = entries[k];
+      const prev = this.setIndex.get(key);
+      items[k] = dirty && prev && prev.obj === ps && !dirty.has(key) ? prev.index : JSON.stringify(snapshotSet(ps));
+    }
+    const r = addon.storeBuilderCompile(this.builder, items);
+    const blob = r.blob;
+    const setIndex = new Map();
+    for (let k = 0; k < entries.length; ++k) setIndex.set(entries[k][0], { obj: entries[k][1], index: k });
+    if (this.compileOnly) { // tooling: the image without a device (no tables / codec / pipeline)
+      this.blob = blob;
+      this.index = nodeIndex(policySets);
+      this.stats.compiles += 1;
+      this.policySets = policySets;
+      this.setIndex = setIndex;
+      this.dirty = new Set();
+      this.stale = false;
+      this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
+      return;
+    }
     const tables = addon.compile(blob, this.device);
     const codec = addon.codecCreate(blob);
     const pipeline = this.pipelineBytes === null ? null : addon.pipelineCreate(tables, codec, this.threads, this.chunk);
@@ -159,6 +199,78 @@ class GpuAccessController {
     this.scopes = this.scopes || new Map();
     for (const [k, v] of this.scopes) addon.codecSetSubjectScopes(codec, k, v);
     this.stats.compiles += 1;
+    this.policySets = policySets;
+    this.setIndex = setIndex;
+    this.dirty = new Set();
+    this.stale = false;
+    this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
+  }
+
+  // The reference's in-memory store handlers (accessController.ts:897-937) on the Map this
+  // controller compiled (the host's AccessController.policySets, shared): each mutates the
+  // Map as the reference does and marks the touched set, and the next batch recompiles only
+  // that set.  A host that mutates the Map itself calls markChanged(setId) instead.
+  updatePolicySet(policySet) {
+    this.policySets.set(policySet.id, policySet);
+    this.markChanged(policySet.id);
+  }
+
+  removePolicySet(policySetID) {
+    this.policySets.delete(policySetID);
+    this.markChanged(null);
+  }
+
+  updatePolicy(policySetID, policy) {
+    const ps = this.policySets.get(policySetID);
+    if (!isNil(ps)) {
+      ps.combinables.set(policy.id, policy);
+      this.markChanged(policySetID);
+    }
+  }
+
+  removePolicy(policySetID, policyID) {
+    const ps = this.policySets.get(policySetID);
+    if (!isNil(ps)) {
+      ps.combinables.delete(policyID);
+      this.markChanged(policySetID);
+    }
+  }
+
+  updateRule(policySetID, policyID, rule) {
+    const ps = this.policySets.get(policySetID);
+    if (!isNil(ps)) {
+      const p = ps.combinables.get(policyID);
+      if (!isNil(p)) {
+        p.combinables.set(rule.id, rule);
+        this.markChanged(policySetID);
+      }
+    }
+  }
+
+  removeRule(policySetID, policyID, ruleID) {
+    const ps = this.policySets.get(policySetID);
+    if (!isNil(ps)) {
+      const p = ps.combinables.get(policyID);
+      if (!isNil(p)) {
+        p.combinables.delete(ruleID);
+        this.markChanged(policySetID);
+      }
+    }
+  }
+
+  clearPolicies() {
+    this.policySets.clear();
+    this.markChanged(null);
+  }
+
+  // setId: a policy set whose contents changed in place (null: only the Map's key set changed)
+  markChanged(setId) {
+    if (setId !== null && setId !== undefined) this.dirty.add(setId);
+    this.stale = true;
+  }
+
+  _sync() {
+    if (this.stale) this.refresh(this.policySets, Array.from(this.dirty));
   }
 
   // The per-subject HR-scope cache (createHRScope / evictHRScopes, accessController.ts:717-783):
@@ -176,6 +288,8 @@ class GpuAccessController {
 
   // Releases the GPU tables and the codec (handles are freed explicitly, napi/acs_napi.c).
   close() {
+    if (this.builder) addon.storeBuilderFree(this.builder);
+    this.builder = null;
     if (this.pipeline) addon.pipelineFree(this.pipeline);
     if (this.tables) addon.free(this.tables);
     if (this.codec) addon.codecFree(this.codec);
@@ -219,6 +333,7 @@ class GpuAccessController {
   // requests: an array of Request objects, or their JSON text.  Resolves to one entry per
   // request: a Response, or an Error (per request, as the reference's promises would reject).
   async isAllowedBatch(requests) {
+    this._sync();
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
     const ec = this.ec; // the codec's table: refresh() may swap this.ec while the batch is in flight
     const bytes = typeof text === 'string' ? text.length : text.byteLength;
@@ -342,6 +457,7 @@ class GpuAccessController {
   // Batch whatIsAllowed (encode + kernels on the calling thread; host-path requests then go
   // to the host evaluator).  Resolves to one entry per request: a ReverseQuery or an Error.
   async whatIsAllowedBatch(requests) {
+    this._sync();
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
     const batch = addon.encode(this.codec, text, this.threads);
     try {

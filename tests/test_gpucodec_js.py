@@ -253,3 +253,177 @@ def test_js_controller_synthetic_gpu(tmp_path):
         else:
             assert r == out[1]["isAllowed"][i], i
     assert np.isfinite(out[1]["stats"]["requests"])
+
+
+# ---------------------------------------------------------------- incremental store (f2)
+MUT_RUNNER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "js", "gpu_mutate_run.js")
+MUTATORS = ("updateRule", "updatePolicy", "removeRule", "updatePolicySet", "removePolicy", "removePolicySet",
+            "clearPolicies")
+
+
+def _mutation_script(seed):
+    """A randomised store, its requests and a step list through all seven of the reference's
+    store handlers (accessController.ts:897-937), with donor objects from another store."""
+    import random
+    urns, doc, reqs = randgen.rand_case(seed)
+    donor = randgen.rand_case(seed + 1000)[1]
+    rng = random.Random(seed)
+    sets = [ps for ps in doc["policy_sets"] if ps.get("policies")]
+    d_sets = [ps for ps in donor["policy_sets"] if ps.get("policies")] or sets
+    if not sets:
+        return None
+    a = rng.choice(sets)
+    p = rng.choice(a["policies"])
+    d_pols = [x for s in d_sets for x in s["policies"]]
+    d_rules = [r for x in d_pols for r in x.get("rules") or []]
+    steps = []
+    if d_rules:
+        steps.append({"op": "updateRule", "args": [a["id"], p["id"], dict(rng.choice(d_rules), id="Rnew")]})
+    steps.append({"op": "updatePolicy", "args": [a["id"], dict(rng.choice(d_pols), id=p["id"])]})
+    if p.get("rules"):
+        steps.append({"op": "removeRule", "args": [a["id"], p["id"], p["rules"][0]["id"]]})
+    steps.append({"op": "updatePolicySet", "args": [dict(rng.choice(d_sets), id="Snew")]})
+    steps.append({"op": "removePolicy", "args": [a["id"], a["policies"][-1]["id"]]})
+    steps.append({"op": "removePolicySet", "args": [sets[0]["id"]]})
+    steps.append({"op": "clearPolicies", "args": []})
+    steps.append({"op": "updatePolicySet", "args": [dict(rng.choice(d_sets), id="Safter")]})
+    return {"doc": doc, "urns": urns, "cas": DEFAULT_CAS, "requests": reqs, "steps": steps}
+
+
+def _replay(script):
+    """The same steps on the Python product's store (acs_mi355x.store shape, the controller's
+    handlers): the Map after each step (step 0 = the loaded store)."""
+    from acs_mi355x.controller import AccessController
+    import host_core
+    ctl = AccessController({"urns": script["urns"], "combiningAlgorithms": DEFAULT_CAS}, engine=host_core.Tables)
+    ctl.policySets = store.populate(script["doc"])
+    one_set = lambda ps: next(iter(store.populate({"policy_sets": [ps]}).values()))  # noqa: E731
+    one_pol = lambda py: one_set({"id": "_", "policies": [py]})["combinables"][py.get("id")]  # noqa: E731
+    maps = [copy_map(ctl.policySets)]
+    for st in script["steps"]:
+        a = st["args"]
+        op = st["op"]
+        if op == "updatePolicySet":
+            ctl.updatePolicySet(one_set(a[0]))
+        elif op == "updatePolicy":
+            ctl.updatePolicy(a[0], one_pol(a[1]))
+        elif op == "updateRule":
+            ctl.updateRule(a[0], a[1], store.make_rule(a[2]))
+        elif op == "clearPolicies":
+            ctl.clearPolicies()
+        else:
+            getattr(ctl, op)(*a)
+        maps.append(copy_map(ctl.policySets))
+    return maps
+
+
+def copy_map(m):
+    import copy
+    return copy.deepcopy(m)
+
+
+def _mut_run(tmp, script, mode, timeout=900):
+    _addon()
+    tmp.joinpath("script.json").write_text(json.dumps(script))
+    r = subprocess.run([NODE, MUT_RUNNER, str(tmp), mode], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.returncode, r.stderr[-4000:])
+    return json.loads(tmp.joinpath("out.json").read_text())
+
+
+def test_js_mutators_incremental_compile(tmp_path):
+    """GpuAccessController's store handlers: after each step the incrementally compiled image
+    (compileOnly) decides every request as a fresh full compile of the same Map, recompiling
+    at most the touched set; the first image is acs_store_compile's byte for byte."""
+    import ctypes as C
+    import host_core
+    from acs_mi355x import layout as L
+    covered, checked = set(), 0
+    for seed in range(0, 60, 3):
+        script = _mutation_script(seed)
+        if script is None:
+            continue
+        try:
+            maps = _replay(script)
+            fresh = [compiler.native_store_blob(m, script["urns"], DEFAULT_CAS) for m in maps]
+        except Unsupported:
+            continue
+        d = tmp_path / f"s{seed}"
+        d.mkdir()
+        out = _mut_run(d, script, "compile")
+        assert len(out) == len(maps)
+        for k, m in enumerate(maps):
+            blob = d.joinpath(f"blob_{k}.bin").read_bytes()
+            if k == 0:
+                assert blob == fresh[0], seed
+            else:
+                assert out[k]["refresh"]["recompiled"] <= 1, (seed, k, out[k])
+                covered.add(script["steps"][k - 1]["op"])
+            recs = []
+            for b in (blob, fresh[k]):
+                nb = NativeCodec(b).encode(script["requests"])
+                o = np.zeros(nb.n, L.DECISION_DT)
+                assert host_core.lib().acs_host_is_allowed(b, len(b), C.byref(nb.struct), o.ctypes.data) == 0
+                recs.append(o.view(np.uint64))
+            assert np.array_equal(recs[0], recs[1]), (seed, k)
+            checked += 1
+    assert covered == set(MUTATORS) and checked >= 60, (covered, checked)
+
+
+@pytest.mark.gpu
+def test_js_mutators_vs_oracle_gpu(tmp_path):
+    """The seven store handlers through GpuAccessController on the GPU: after every step the
+    Responses equal the oracle's on the mutated Map (the Python replay of the same steps)."""
+    _gpu()
+    from diff_utils import oracle_from_store
+    vs_oracle, steps = 0, set()
+    for seed in range(0, 40, 4):
+        script = _mutation_script(seed)
+        if script is None:
+            continue
+        try:
+            maps = _replay(script)
+            for m in maps:
+                compiler.compile_store(m, script["urns"], DEFAULT_CAS)
+        except Unsupported:
+            continue
+        d = tmp_path / f"s{seed}"
+        d.mkdir()
+        out = _mut_run(d, script, "decide")
+        for k, (m, got) in enumerate(zip(maps, out)):
+            if k:
+                steps.add(script["steps"][k - 1]["op"])
+            o = oracle_from_store(script["urns"], m)
+            for req, r in zip(script["requests"], got["isAllowed"]):
+                if r.get("$error") == "HostPathRequired":
+                    continue
+                try:
+                    want = oracle_outcome(o, req)
+                except OracleUnsupported:
+                    continue
+                if "$error" in r:
+                    assert want == ("ERR", r["$error"]), (seed, k, r, want)
+                else:
+                    ec = r.get("evaluation_cacheable", "undefined")
+                    assert want == ("OK", r["decision"], ec, r["operation_status"]["code"]), (seed, k, r, want)
+                vs_oracle += 1
+    assert steps == set(MUTATORS) and vs_oracle >= 300, (steps, vs_oracle)
+
+
+@pytest.mark.gpu
+def test_js_c5_update_latency_gpu(tmp_path):
+    """c5 (1M rules): one updateRule through GpuAccessController — the incremental refresh
+    (one set re-serialised and recompiled) against a full refresh; printed for the record."""
+    _gpu()
+    import copy
+    doc = synth.c5_store()
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 200, "c3", seed=3, classes=False)
+    ps = doc["policy_sets"][500]
+    rule = copy.deepcopy(ps["policies"][3]["rules"][7])
+    rule["effect"] = "DENY" if rule.get("effect") != "DENY" else "PERMIT"
+    script = {"doc": doc, "urns": FULL_URNS, "cas": DEFAULT_CAS, "requests": [sb.decode(i) for i in range(200)],
+              "steps": [{"op": "updateRule", "args": [ps["id"], ps["policies"][3]["id"], rule]}]}
+    out = _mut_run(tmp_path, script, "latency", timeout=1100)[0]
+    print("c5 update latency:", json.dumps(out))
+    assert out["incremental"]["stats"]["recompiled"] == 1 and out["decided"] == 200
+    assert out["incremental"]["ms"] < out["full_refresh"]["ms"]
