@@ -298,13 +298,13 @@ struct HrForest {
   bool is_array = false;
   std::vector<Scalar> roots;  // hierarchical_scopes[i].role
   std::vector<Scalar> keys;   // verifyACL effective-role keys, first-seen order
-  std::deque<std::string> ids;  // storage of the org ids `masks` is keyed by
-  std::unordered_map<std::string_view, uint64_t, FastHash> masks;  // org id -> root bits | key bits << 32
+  StrPool ids;                // storage of the org ids `masks` is keyed by
+  StrMap<uint64_t> masks;     // org id -> root bits | key bits << 32 (flat: one probe run per owner lookup)
   std::string text;           // inline forests: the exact JSON text they were built from
   size_t bytes() const { return text.size() + masks.size() * 64 + 256; }
   uint64_t mask(std::string_view id) const {
-    auto it = masks.find(id);
-    return it == masks.end() ? 0 : it->second;
+    const auto* e = masks.find(id);
+    return e ? e->v : 0;
   }
 };
 
@@ -369,12 +369,11 @@ void build_forest(HrForest& F, const JV* hrs) {
             F.keys.push_back(vals[vi]);
           }
           if (hid->t == J_STR) {
-            auto it = F.masks.find(hid->str());
-            if (it == F.masks.end()) {
-              F.ids.emplace_back(hid->s, hid->n);
-              it = F.masks.emplace(std::string_view(F.ids.back()), 0ull).first;
-            }
-            it->second |= (1ull << r) | (1ull << (32 + val_key[vi]));
+            const std::string_view sid = hid->str();
+            const uint64_t h = fast_hash(sid.data(), sid.size());
+            auto* e = const_cast<StrMap<uint64_t>::Slot*>(F.masks.find(h, sid));
+            if (!e) e = F.masks.insert(h, F.ids.put(sid), (uint32_t)sid.size(), 0ull);
+            e->v |= (1ull << r) | (1ull << (32 + val_key[vi]));
           }
         }
         const JV* ch = get(h, "children");
