@@ -42,7 +42,7 @@ def _hipcc(src, out, extra=(), host_srcs=()):
     for h in host_srcs:
         o = out + "." + os.path.basename(h) + ".o"
         subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread",
-                        "-I", CSRC, "-I", os.path.join(ROOT, "include"), "-c", h, "-o", o], check=True)
+                        "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, "-c", h, "-o", o], check=True)
         objs.append(o)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-Wno-unused-function", "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, src,

@@ -342,15 +342,19 @@ struct ReqCtx {
   // instead of being held as six pointers and six counts: K1's per-lane state stays small.
   uint32_t c0, c1;  // arena counts: [0] grants | rolese<<8 | slots<<16 | roots<<24, [1] tse | hrkeys<<8
   uint32_t ext;     // compact batch: 1 + 16-B unit offset of the extension record (0: none)
+  bool soa;         // the rows past the line are SoA rows (else the extension record); false as a
+                    // constant in the compact-batch kernels, so their SoA paths compile away
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
 #endif
 
   // ln: the request's packed line (acs_layout.h ReqLine), nullptr: the SoA rows
-  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr)
+  ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr,
+                bool soa_ok = true)
       : T(t), B(b), i(idx), h(hd) {
-    if (ln) {
+    soa = soa_ok && B.hdr != nullptr;
+    if (ln || !soa_ok) {
       ext = ln->ext;
       s0i = ln->s0.id; s0v = ln->s0.value; s1i = ln->s1.id; s1v = ln->s1.value;
       a0i = ln->a0.id; a0v = ln->a0.value;
@@ -390,7 +394,7 @@ struct ReqCtx {
   // Rows past the line: the SoA rows, or a compact batch's extension record.
   ACS_FN ExtGeom geom() const { return ext_geom(h.nres, h.nsubj, h.nact, h.nroles); }
   ACS_FN ReqRes res_row(uint32_t j) const {
-    if (B.hdr) return B.res[(size_t)j * B.n + i];
+    if (soa) return B.res[(size_t)j * B.n + i];
     const uint32_t* w = ex() + 4u * (j - (uint32_t)LINE_RES);
     ReqRes q;
     __builtin_memcpy(&q, w, sizeof q);
@@ -398,7 +402,7 @@ struct ReqCtx {
   }
   ACS_FN Pair subj(uint32_t j) const {
     if (j >= 2) {
-      if (B.hdr) return B.subj[(size_t)j * B.n + i];
+      if (soa) return B.subj[(size_t)j * B.n + i];
       const uint32_t* w = ex() + geom().subj + 2u * (j - 2u);
       return Pair{w[0], w[1]};
     }
@@ -409,7 +413,7 @@ struct ReqCtx {
   }
   ACS_FN Pair act(uint32_t j) const {
     if (j >= 1) {
-      if (B.hdr) return B.act[(size_t)j * B.n + i];
+      if (soa) return B.act[(size_t)j * B.n + i];
       const uint32_t* w = ex() + geom().act + 2u * (j - 1u);
       return Pair{w[0], w[1]};
     }
@@ -420,7 +424,7 @@ struct ReqCtx {
   }
   ACS_FN uint32_t role(uint32_t j) const {
     if (j < 2) return j == 0 ? role0 : role1;
-    return B.hdr ? B.roles[(size_t)j * B.n + i] : ex()[geom().roles + (j - 2u)];
+    return soa ? B.roles[(size_t)j * B.n + i] : ex()[geom().roles + (j - 2u)];
   }
   ACS_FN uint8_t rx(uint32_t col, uint32_t row) const { return B.rx[(size_t)col * B.rx_rows + row]; }
   ACS_FN bool flag(uint32_t f) const { return (h.flags & f) != 0; }
@@ -442,8 +446,8 @@ struct ReqLds : ReqCtx {
   uint32_t stride;
   uint32_t e0_val, e0_col;  // the request's only entity attribute (RQ_ENT_SHIFT field 1..6)
   ACS_FN ReqLds(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqRes* c, uint32_t st,
-                const ReqLine* ln = nullptr)
-      : ReqCtx(t, b, idx, hd, ln), col(c), stride(st) {
+                const ReqLine* ln = nullptr, bool soa_ok = true)
+      : ReqCtx(t, b, idx, hd, ln, soa_ok), col(c), stride(st) {
     const uint32_t e = (h.flags >> RQ_ENT_SHIFT) & 7u;
     e0_val = e0_col = 0;
     if (e >= 1 && e <= 6) {

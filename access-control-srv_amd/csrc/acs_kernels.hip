@@ -71,6 +71,9 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
 #define ACS_AB_PROLOGUE_ONLY 0
 #endif
+#ifndef ACS_AB_NO_CB           // compact batches run the kernels instantiated for SoA batches
+#define ACS_AB_NO_CB 0
+#endif
 #ifndef ACS_AB_WAVE_VERDICTS   // verdicts only in one-class waves (no per-lane class-row reads)
 #define ACS_AB_WAVE_VERDICTS 0
 #endif
@@ -520,14 +523,22 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 // 1.98 -> 1.87 ms in a same-call A/B (r02_q; c2 0.180 -> 0.190 ms), 4 slots alone 1.95 ms
 #define ACS_K1_WAVES_PER_EU 5
 #endif
-template <class FL>
+// CB: a compact batch (request lines + extension records, no SoA rows): the kernels are
+// instantiated for it separately so that its row accessors carry no SoA paths (fewer live
+// registers; acs_eval.h ReqCtx::soa).
+template <bool CB>
+__device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) {
+  return CB ? B.lines + i : (in && B.lines ? B.lines + i : nullptr);  // one gather for the first rows
+}
+
+template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
-  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;  // one gather for the first rows
+  const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
   if (in) h = ln ? ln->h : B.hdr[i];
   bool done = true;
@@ -547,11 +558,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
-    const ReqLds R(T, B, i, h, col, BLOCK, ln);
+    const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
     d = is_allowed_t(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln), F);
+    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -573,7 +584,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
-template <class FL>
+template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                                 BitsLayout BL, uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
@@ -583,7 +594,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const bool in = k < B.n;
   const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
-  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;  // one gather for the first rows
+  const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
   if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
@@ -599,7 +610,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
-    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln), F, BL, sink, log);
+    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
   }
   sink.finish();
   obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
@@ -615,7 +626,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
 // obl[c][j] / obl_n[c][j]: range c's log and total push count (> cap: re-run with that
 // cap); a request's log is the concatenation over c.  An index outside the batch writes
 // 0xFFFFFFFF and reads nothing.
-template <class FL>
+template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Batch B, const uint32_t* __restrict__ idx,
                                                                     uint32_t m, uint32_t chunks, uint32_t cap,
                                                                     uint32_t* __restrict__ obl,
@@ -630,7 +641,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
   const uint64_t k = (uint64_t)c * m + j;  // output slot [c][j]
   const uint32_t i = live ? idx[j] : 0u;
   const bool in = live && i < B.n;
-  const ReqLine* ln = in && B.lines ? B.lines + i : nullptr;
+  const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
   if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
@@ -649,7 +660,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
     for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = ln ? ln->res[q] : B.res[(size_t)q * B.n + i];
     const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks), s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
     NullSink none;
-    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln), F, BitsLayout{}, none, log, s0, s1);
+    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BitsLayout{}, none, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
   }
   obl_n[k] = total;
@@ -818,12 +829,21 @@ FilterForm filter_form(const Batch& B) {
   return B.cand_words <= LDS_FILTER_WORDS && B.cand_wv ? FilterForm::Lds : FilterForm::General;
 }
 
-#define ACS_LAUNCH_FILTERED(kernel, grid, lds, stream, form, ...)                                       \
+// one instantiation per filter form and batch form (compact: no SoA rows)
+#define ACS_LAUNCH_FILTERED(kernel, grid, lds, stream, form, compact, ...)                              \
   do {                                                                                                  \
-    switch (form) {                                                                                     \
-      case FilterForm::All: hipLaunchKernelGGL(kernel<FilterAll>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-      case FilterForm::Lds: hipLaunchKernelGGL(kernel<FilterLds>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-      default: hipLaunchKernelGGL(kernel<Filter>, grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+    if (compact) {                                                                                      \
+      switch (form) {                                                                                   \
+        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        default: hipLaunchKernelGGL((kernel<Filter, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+      }                                                                                                 \
+    } else {                                                                                            \
+      switch (form) {                                                                                   \
+        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        default: hipLaunchKernelGGL((kernel<Filter, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+      }                                                                                                 \
     }                                                                                                   \
   } while (0)
 
@@ -1314,7 +1334,8 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   dim3 grid((b->n + BLOCK - 1) / BLOCK);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, (Decision*)out);
+  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, perm,
+                      (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
@@ -1351,7 +1372,7 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), t->view, B, perm, BL, bits,
+  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, perm, BL, bits,
                       obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
@@ -1380,7 +1401,8 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const 
   Batch B = to_batch(b);
   const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
   ACS_LAUNCH_FILTERED(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), filter_lds_bytes(B),
-                      (hipStream_t)stream, filter_form(B), t->view, B, idx, (uint32_t)m, chunks, cap, obl, obl_n);
+                      (hipStream_t)stream, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, idx, (uint32_t)m, chunks, cap, obl,
+                      obl_n);
   HIP_OK(hipGetLastError());
   return 0;
 }

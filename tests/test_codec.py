@@ -302,3 +302,37 @@ def test_codec_class_rows_match_python_at_every_level(level, monkeypatch):
         assert _request_rows(pb) == _request_rows(nb)
         checked += 1
     assert checked >= 8
+
+
+def test_parallel_delimiter_matches_serial():
+    """The three-pass parallel delimiter of the request array (acs_codec.cpp split_items: quote
+    parity, per-chunk depth minima, top-level commas) gives the serial delimiter's items on a
+    > 4 MB array whose strings hold quotes, escapes, brackets and "},{" sequences, chunk
+    boundaries falling anywhere."""
+    import random
+    doc = synth.c2_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 400, "c2", seed=13)
+    base = [sb.decode(i) for i in range(sb.batch.n)]
+    rng = random.Random(5)
+    nasty = ['a"b', 'x\\\\"},{"y', '[[{', '}]', '\\\\', 'q\\\\\\\\"', '},{', ',,,', 'tab\\there', 'ü"ñ']
+    reqs, size = [], 0
+    while size < (5 << 20):
+        r = json.loads(json.dumps(rng.choice(base)))
+        r["target"]["subjects"].append({"id": "urn:x", "value": rng.choice(nasty) * rng.randint(1, 4)})
+        if rng.random() < 0.3:
+            r["note"] = {"deep": [[{"s": rng.choice(nasty)}]], "t": rng.choice(nasty)}
+        reqs.append(r)
+        size += len(json.dumps(r)) + 2
+    codec = NativeCodec(compiler.store_blob(cs))
+    # batch-local string ids depend on the encoding thread: compare what does not
+    shape = lambda b: np.stack([b.lines["h"][f].astype(np.int64) for f in ("flags", "nres", "nsubj", "nact", "nroles")])  # noqa: E731
+    for text in (json.dumps(reqs), json.dumps(reqs, indent=1), json.dumps(reqs, ensure_ascii=False)):
+        one = codec.encode(text, threads=1)
+        want = host_core.is_allowed(cs, one, compact=True).view(np.uint64)
+        for t in (3, 7):
+            many = codec.encode(text, threads=t)
+            assert many.n == one.n == len(reqs)
+            assert np.array_equal(shape(many), shape(one))
+            assert many.host_reasons == one.host_reasons
+            assert np.array_equal(host_core.is_allowed(cs, many, compact=True).view(np.uint64), want)
