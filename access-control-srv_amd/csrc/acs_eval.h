@@ -81,6 +81,13 @@ __device__ inline void scan_count(uint32_t bytes) {
 #define ACS_SCAN(bytes)
 #endif
 
+// Table record reads: 0 all-lane vector loads + readfirstlane (product), 1 one-lane vector
+// loads (c3 K1 1.891 ms vs 1.851, same-call A/B r03_g), 2 scalar loads (1.791 ms, but a scalar
+// load ignores EXEC: a block the compiler enters with no active lane reads an unchecked
+// address — the counting build faulted on c4 — so it stays an A/B form).
+#ifndef ACS_LOAD_MODE
+#define ACS_LOAD_MODE 0
+#endif
 // Table records are read as whole dwords through wave-uniform addresses and unpacked in
 // registers (vector loads, then SGPRs: see below).
 template <class X, int NW = sizeof(X) / 4>
@@ -91,12 +98,37 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
 #if defined(__HIP_DEVICE_COMPILE__)
+#if ACS_LOAD_MODE == 2
+  // Scalar loads: the address moves to SGPRs and the record is read through the constant
+  // address space (s_load_dwordxN into SGPRs): no vector-memory instruction, no VGPR.
+  typedef __attribute__((address_space(4))) const uint32_t const_u32;
+  const uint64_t a = reinterpret_cast<uint64_t>(w);
+  const uint64_t ua = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                      __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const const_u32* q = (const const_u32*)ua;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = q[k];
+#elif ACS_LOAD_MODE == 1
+  // One lane loads (the wave's first active lane: 1/64 of the address and return traffic of
+  // an all-lane load of the same record), then the record moves to SGPRs.
+  const uint64_t act = __ballot(1);
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = 0u;
+  if (lane == (uint32_t)__builtin_ctzll(act)) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) v[k] = w[k];
+  }
+#pragma unroll
+  for (int k = 0; k < NW; ++k) v[k] = __builtin_amdgcn_readfirstlane(v[k]);
+#else
   // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
   // the wave-uniform record moves to SGPRs: its fields feed scalar compares and branches and
   // free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself proves
   // the address uniform it emits s_load; nothing here forces a scalar load.
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = __builtin_amdgcn_readfirstlane(w[k]);
+#endif
 #else
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];

@@ -65,14 +65,23 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_BLOB_RULES      // rule records in the blob layout instead of 128-B lines
 #define ACS_AB_BLOB_RULES 0
 #endif
-#ifndef ACS_AB_NO_SCATTER      // timing only: K1 writes records in sort order (out[k])
+#ifndef ACS_AB_NO_SCATTER      // timing only: K1/K2 write records in sort order (out[k])
 #define ACS_AB_NO_SCATTER 0
 #endif
 #ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
 #define ACS_AB_PROLOGUE_ONLY 0
 #endif
+#ifndef ACS_AB_NO_BITS         // timing only: K2 stores no inclusion bitset
+#define ACS_AB_NO_BITS 0
+#endif
+#ifndef ACS_AB_NO_PAD          // whatIsAllowed waves may mix classes (no wave-aligned class runs)
+#define ACS_AB_NO_PAD 0
+#endif
 #ifndef ACS_AB_NO_CB           // compact batches run the kernels instantiated for SoA batches
 #define ACS_AB_NO_CB 0
+#endif
+#ifndef ACS_AB_K2_NOCB         // whatIsAllowed only: compact batches run the SoA instantiation
+#define ACS_AB_K2_NOCB 0
 #endif
 #ifndef ACS_AB_WAVE_VERDICTS   // verdicts only in one-class waves (no per-lane class-row reads)
 #define ACS_AB_WAVE_VERDICTS 0
@@ -329,7 +338,10 @@ __global__ __launch_bounds__(BLOCK) void class_columns_kernel(uint32_t* __restri
   tot[k] = run;
 }
 
-__global__ __launch_bounds__(CS_THREADS) void class_bases_kernel(uint32_t* __restrict__ tot, uint32_t K) {
+// pad: each key's run starts on a wave boundary (runs rounded up to 64 lanes; the holes stay
+// 0xFFFFFFFF), so no wave mixes keys (whatIsAllowed, where a wave walks the union of its
+// lanes' candidates).
+__global__ __launch_bounds__(CS_THREADS) void class_bases_kernel(uint32_t* __restrict__ tot, uint32_t K, uint32_t pad) {
   __shared__ uint32_t part[CS_THREADS];
   constexpr uint32_t PER_MAX = CS_BINS / CS_THREADS;  // 64: this thread's bins, loaded at once
   const uint32_t per = (K + CS_THREADS - 1) / CS_THREADS, k0 = threadIdx.x * per;
@@ -338,6 +350,7 @@ __global__ __launch_bounds__(CS_THREADS) void class_bases_kernel(uint32_t* __res
 #pragma unroll
   for (uint32_t j = 0; j < PER_MAX; ++j) {
     v[j] = j < per && k0 + j < K ? tot[k0 + j] : 0u;
+    if (pad) v[j] = (v[j] + 63u) & ~63u;
     s += v[j];
   }
   part[threadIdx.x] = s;
@@ -513,6 +526,13 @@ __device__ inline uint32_t request_pcol(const ReqHdr& h) {
   return (h.flags & RQ_NO_TARGET) ? PCOL_ALL : (h.flags >> RQ_PCOL_SHIFT);
 }
 
+#if defined(ACS_WAVE_TIMES)
+// Diagnostic build only: per-wave first-start / last-end wall clock of K2 and the class of the
+// wave's first lane (tools/wave_times.py).  Every lane folds its own times in (vector atomics).
+constexpr uint32_t WT_MAX = 1u << 16;
+__device__ unsigned long long acs_wt0[WT_MAX], acs_wt1[WT_MAX];
+__device__ unsigned int acs_wt_cls[WT_MAX], acs_wt_lanes[WT_MAX];
+#endif
 #if defined(ACS_PHASE_PROF)
 __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
@@ -533,11 +553,12 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
 
 template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
-    Tables T, Batch B, const uint32_t* __restrict__ perm, Decision* __restrict__ out) {
+    Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  const bool in = k < B.n;
-  const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
+  const bool in = pk < B.n;
+  const uint32_t i = in ? pk : 0u;
   const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
   if (in) h = ln ? ln->h : B.hdr[i];
@@ -567,7 +588,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   }
 #if !defined(ACS_PHASE_PROF)
 #if ACS_AB_NO_SCATTER
-  out[k] = d;  // A/B timing only: records in sort order (wrong order for the caller)
+  if (k < B.n) out[k] = d;  // A/B timing only: records in sort order (wrong order for the caller)
 #else
   out[i] = d;
 #endif
@@ -584,25 +605,54 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
+// K2 occupancy A/B (ACS_K2_WAVES_PER_EU=5/6/8: 96/80/64 VGPRs with spills) measured no gain
+// on c4 (6.92-6.95 ms vs 6.62, r03_g): K2 is not latency-bound per wave (SQ_WAIT_ANY ~90 % of
+// wave cycles at every occupancy tried), so the compiler's own 4 waves/SIMD stay.
+#if defined(ACS_K2_WAVES_PER_EU)
+#define ACS_K2_ATTR __attribute__((amdgpu_waves_per_eu(ACS_K2_WAVES_PER_EU)))
+#else
+#define ACS_K2_ATTR
+#endif
 template <class FL, bool CB>
-__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
-                                                                BitsLayout BL, uint32_t* __restrict__ bits,
+__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+                                                                uint32_t lanes, BitsLayout BL,
+                                                                uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
-  const bool in = k < B.n;
-  const uint32_t i = in ? (perm ? perm[k] : k) : 0u;
+  const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
+  const bool in = pk < B.n;
+  const uint32_t i = in ? pk : 0u;
   const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
   if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
+#if defined(ACS_WAVE_TIMES)
+  const uint32_t wt = k >> 6;
+  if (wt < WT_MAX) {
+    atomicMin(&acs_wt0[wt], (unsigned long long)wall_clock64());
+    if (in) {
+      atomicAdd(&acs_wt_lanes[wt], 1u);
+      atomicMin(&acs_wt_cls[wt], request_pcol(h));
+    }
+  }
+#endif
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                      wave_lds_row(B));
   if (!in) return;
-  ChunkSink sink(bits + (size_t)i * BL.words, BL);
-  OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
+#if ACS_AB_NO_SCATTER
+  const uint32_t o = k < B.n ? k : i;  // A/B timing only: rows in sort order (wrong order for the caller)
+#else
+  const uint32_t o = i;
+#endif
+#if ACS_AB_NO_BITS
+  NullSink sink;  // A/B timing only: no inclusion bitset stores
+#else
+  ChunkSink sink(bits + (size_t)o * BL.words, BL);
+#endif
+  OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
   Decision d{};
   if (host) {
     d.flags = OF_HOST_REQ;
@@ -613,8 +663,11 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
   }
   sink.finish();
-  obl_n[i] = (d.flags & OF_ERR) ? 0u : log.n;
-  out[i] = d;
+  obl_n[o] = (d.flags & OF_ERR) ? 0u : log.n;
+  out[o] = d;
+#if defined(ACS_WAVE_TIMES)
+  if (wt < WT_MAX) atomicMax(&acs_wt1[wt], (unsigned long long)wall_clock64());
+#endif
 }
 
 // Obligation-only pass for requests idx[0..m) — those whose K2 log
@@ -937,6 +990,31 @@ int acs_scan_read(unsigned long long* out) {
   HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(acs_scan_bytes), sizeof *out));
   HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_scan_bytes), &z, sizeof z));
   return 0;
+}
+#endif
+
+#if defined(ACS_WAVE_TIMES)
+// Diagnostic build only: copy out the per-wave K2 records of the last launch(es) (ticks of the
+// 100 MHz wall clock) and reset them; returns the capacity.
+int acs_wave_times_read(unsigned long long* t0, unsigned long long* t1, unsigned int* cls, unsigned int* lanes,
+                        int n) {
+  static std::vector<unsigned long long> a(WT_MAX), b(WT_MAX);
+  static std::vector<unsigned int> c(WT_MAX), l(WT_MAX);
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(a.data(), HIP_SYMBOL(acs_wt0), WT_MAX * 8));
+  HIP_OK(hipMemcpyFromSymbol(b.data(), HIP_SYMBOL(acs_wt1), WT_MAX * 8));
+  HIP_OK(hipMemcpyFromSymbol(c.data(), HIP_SYMBOL(acs_wt_cls), WT_MAX * 4));
+  HIP_OK(hipMemcpyFromSymbol(l.data(), HIP_SYMBOL(acs_wt_lanes), WT_MAX * 4));
+  for (int k = 0; k < n && k < (int)WT_MAX; ++k) {
+    t0[k] = a[k]; t1[k] = b[k]; cls[k] = c[k]; lanes[k] = l[k];
+  }
+  std::vector<unsigned long long> hi(WT_MAX, ~0ull), lo(WT_MAX, 0ull);
+  std::vector<unsigned int> hc(WT_MAX, ~0u), lz(WT_MAX, 0u);
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_wt0), hi.data(), WT_MAX * 8));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_wt1), lo.data(), WT_MAX * 8));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_wt_cls), hc.data(), WT_MAX * 4));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_wt_lanes), lz.data(), WT_MAX * 4));
+  return (int)WT_MAX;
 }
 #endif
 
@@ -1281,8 +1359,12 @@ static int radix_passes(uint32_t* base, size_t n, uint32_t end_bit, bool hist0, 
 }
 
 // Coherence sort: permutation of request indices ordered by (class, low field).
-static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream_t s, const uint32_t** perm) {
+// pad (counting path only): each class's run starts a wave; *lanes = the launch width (holes and
+// the tail past the padded runs hold 0xFFFFFFFF).  Without padding *lanes = n.
+static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream_t s, const uint32_t** perm,
+                          bool pad = false, size_t* lanes = nullptr) {
   *perm = nullptr;
+  if (lanes) *lanes = B.n;
   if (!t->sort || B.n < 2 * BLOCK) return 0;
   const size_t n = B.n;
   uint32_t lowbits, end_bit;
@@ -1297,11 +1379,17 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
       chunk = CS_MAX_CHUNK;
       nb = (uint32_t)((n + chunk - 1) / chunk);
     }
-    const size_t words = 2 * n + (size_t)nb * K + K;
+    pad = pad && lanes;
+    const size_t width = pad ? n + 63 * std::min<size_t>(n, K) : n;  // padded runs fit in it
+    const size_t words = n + width + (size_t)nb * K + K;
     if (W.sort.reserve(words * sizeof(uint32_t))) return -1;
     uint32_t* keys = (uint32_t*)W.sort.p;
     uint32_t* out = keys + n;
-    uint32_t* counts = out + n;
+    uint32_t* counts = out + width;
+    if (pad) {
+      HIP_OK(hipMemsetAsync(out, 0xFF, width * sizeof(uint32_t), s));
+      *lanes = width;
+    }
     uint32_t* tot = counts + (size_t)nb * K;
     hipLaunchKernelGGL(class_count_kernel, dim3(nb), dim3(CS_THREADS), 0, s, B, lowbits, end_bit - lowbits, chunk,
                        (uint32_t)K, keys, counts);
@@ -1309,7 +1397,7 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
     hipLaunchKernelGGL(class_columns_kernel, dim3((unsigned)((K + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, counts, nb,
                        (uint32_t)K, tot);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(class_bases_kernel, dim3(1), dim3(CS_THREADS), 0, s, tot, (uint32_t)K);
+    hipLaunchKernelGGL(class_bases_kernel, dim3(1), dim3(CS_THREADS), 0, s, tot, (uint32_t)K, (uint32_t)pad);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(class_scatter_kernel, dim3(nb), dim3(CS_THREADS), 0, s, (const uint32_t*)keys, (uint32_t)n,
                        chunk, (uint32_t)K, (const uint32_t*)counts, (const uint32_t*)tot, out);
@@ -1330,12 +1418,16 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
 static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  if (coherence_perm(t, W, B, s, &perm)) return -1;
-  dim3 grid((b->n + BLOCK - 1) / BLOCK);
+  // wave-aligned class runs when the classes are short (most waves would mix two or three
+  // classes and walk the union of their candidates): below 256 requests per class on average
+  const bool pad = !ACS_AB_NO_PAD && B.cand && (uint64_t)B.n < 256ull * B.cand_rows;
+  size_t lanes = b->n;
+  if (coherence_perm(t, W, B, s, &perm, pad, &lanes)) return -1;
+  dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, perm,
-                      (Decision*)out);
+                      (uint32_t)lanes, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));
@@ -1366,13 +1458,14 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
                                   uint32_t* obl_n, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
-  if (coherence_perm(t, W, B, s, &perm)) return -1;
-  dim3 grid((b->n + BLOCK - 1) / BLOCK);
+  size_t lanes = b->n;
+  if (coherence_perm(t, W, B, s, &perm, !ACS_AB_NO_PAD, &lanes)) return -1;
+  dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, perm, BL, bits,
+  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB && !ACS_AB_K2_NOCB, t->view, B, perm, (uint32_t)lanes, BL, bits,
                       obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {

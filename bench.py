@@ -91,9 +91,10 @@ def measured_scan_bytes(blob, db, local, what="is_allowed"):
     import ctypes as C
     from acs_mi355x import build as B, native
     from acs_mi355x.device import is_allowed_device, what_is_allowed_device
-    if not os.path.exists(B.SCAN_LIB):
-        raise SystemExit(f"bench.py: counting build missing: {B.SCAN_LIB} (run __graft_entry__.build())")
-    lib = native._declare(C.CDLL(B.SCAN_LIB))
+    scan_lib = os.environ.get("ACS_SCAN_LIB", B.SCAN_LIB)  # A/B: another counting build
+    if not os.path.exists(scan_lib):
+        raise SystemExit(f"bench.py: counting build missing: {scan_lib} (run __graft_entry__.build())")
+    lib = native._declare(C.CDLL(scan_lib))
     lib.acs_scan_read.argtypes = [C.POINTER(C.c_ulonglong)]
 
     class _T:  # the duck-typed tables handle device.py's launchers take
