@@ -65,6 +65,8 @@ struct Tables {
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
+  uint32_t rep_n;    // device image copies (ACS_TABLE_REPLICAS A/B; 1 in the product)
+  uint64_t rep_stride;  // bytes between copies
 };
 
 #if defined(ACS_SCAN_COUNT)

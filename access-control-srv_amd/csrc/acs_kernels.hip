@@ -71,6 +71,9 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
 #define ACS_AB_PROLOGUE_ONLY 0
 #endif
+#ifndef ACS_TABLE_REPLICAS     // A/B: copies of the device image, spread over L2 channels
+#define ACS_TABLE_REPLICAS 1
+#endif
 #ifndef ACS_AB_NO_BITS         // timing only: K2 stores no inclusion bitset
 #define ACS_AB_NO_BITS 0
 #endif
@@ -546,6 +549,21 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 // CB: a compact batch (request lines + extension records, no SoA rows): the kernels are
 // instantiated for it separately so that its row accessors carry no SoA paths (fewer live
 // registers; acs_eval.h ReqCtx::soa).
+// This block's copy of the tables (ACS_TABLE_REPLICAS): blocks are dealt to the 8 XCDs
+// round-robin, so blockIdx / 8 numbers a block within its XCD.
+__device__ inline Tables replica_view(Tables T) {
+#if ACS_TABLE_REPLICAS > 1
+  const uint64_t d = (uint64_t)((blockIdx.x >> 3) % T.rep_n) * T.rep_stride;
+  T.sets = (const NodeRec*)((const char*)T.sets + d);
+  T.pols = (const NodeRec*)((const char*)T.pols + d);
+  T.rules = (const NodeRec*)((const char*)T.rules + d);
+  T.rres = (const RuleResAttr*)((const char*)T.rres + d);
+  T.pairs = (const Pair*)((const char*)T.pairs + d);
+  T.u32pool = (const uint32_t*)((const char*)T.u32pool + d);
+#endif
+  return T;
+}
+
 template <bool CB>
 __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) {
   return CB ? B.lines + i : (in && B.lines ? B.lines + i : nullptr);  // one gather for the first rows
@@ -553,7 +571,8 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
 
 template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
-    Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
+    Tables T0, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
+  const Tables T = replica_view(T0);
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
@@ -614,12 +633,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #define ACS_K2_ATTR
 #endif
 template <class FL, bool CB>
-__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T0, Batch B, const uint32_t* __restrict__ perm,
                                                                 uint32_t lanes, BitsLayout BL,
                                                                 uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
+  const Tables T = replica_view(T0);
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
@@ -1157,9 +1177,17 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
-  const size_t alloc = up_bytes + 128;
-  if (hipSetDevice(device) != hipSuccess || hipMalloc(&t->dev, alloc) != hipSuccess ||
-      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) != hipSuccess ||
+  // ACS_TABLE_REPLICAS (A/B): R copies of the image at a stride that is an odd multiple of
+  // 256 B, so one record's copies sit in different L2 channels; blocks pick a copy by their
+  // index within their XCD (replica_view)
+  const uint32_t reps = ACS_TABLE_REPLICAS > 1 ? ACS_TABLE_REPLICAS : 1;
+  const size_t rep_stride = ((up_bytes + 255) & ~(size_t)255) | 256;
+  const size_t img_total = reps > 1 ? rep_stride * reps : up_bytes;
+  const size_t alloc = img_total + 128;
+  bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, alloc) == hipSuccess;
+  for (uint32_t c = 0; copied && c < reps; ++c)
+    copied = hipMemcpy((char*)t->dev + c * rep_stride, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess;
+  if (!copied ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
     fail("acs_compile: device allocation / upload failed");
@@ -1179,7 +1207,9 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
-  t->image_bytes = up_bytes;
+  t->view.rep_n = reps;
+  t->view.rep_stride = rep_stride;
+  t->image_bytes = img_total;
   return t;
 }
 
