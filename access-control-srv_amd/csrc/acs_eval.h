@@ -151,6 +151,36 @@ ACS_FN NodeRec rule_at(const Tables& T, uint32_t r) {
   return node_at(T, T.rules, r * T.rstride, T.n_rules * T.rstride);
 }
 
+#ifndef ACS_AB_RULE_PREFETCH  // A/B: K2 loads the next candidate rule's record ahead
+#define ACS_AB_RULE_PREFETCH 0
+#endif
+// A rule record still in VGPRs (loaded, not yet waited on) and its move to SGPRs.
+struct RawRec {
+  uint32_t v[sizeof(NodeRec) / 4];
+};
+ACS_FN RawRec raw_rule(const Tables& T, uint32_t r) {
+  ACS_SCAN(sizeof(NodeRec));
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(T.rules + (size_t)r * T.rstride);
+  RawRec o;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(NodeRec) / 4); ++k) o.v[k] = w[k];
+  return o;
+}
+ACS_FN NodeRec rec_of(const RawRec& x) {
+  uint32_t v[sizeof(NodeRec) / 4];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(NodeRec) / 4); ++k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    v[k] = __builtin_amdgcn_readfirstlane(x.v[k]);
+#else
+    v[k] = x.v[k];
+#endif
+  }
+  NodeRec out;
+  __builtin_memcpy(&out, v, sizeof out);
+  return out;
+}
+
 struct Batch {
   uint32_t n;
   const ReqHdr* hdr;      // [n]
@@ -1291,11 +1321,22 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
           any_rule = true;
         }
         uint32_t rest = wave_or(m & ~known);
+#if ACS_AB_RULE_PREFETCH
+        // the next candidate's record is in flight while this one is matched
+        RawRec nxt{};
+        if (rest) nxt = raw_rule(T, wave_uniform(base + (uint32_t)__builtin_ctz(rest)));
+#endif
         while (rest) {
           const uint32_t r = wave_uniform(base + (uint32_t)__builtin_ctz(rest));
           rest &= rest - 1u;
+#if ACS_AB_RULE_PREFETCH
+          const NodeRec Q = rec_of(nxt);
+          if (rest) nxt = raw_rule(T, wave_uniform(base + (uint32_t)__builtin_ctz(rest)));
+          if ((known >> (r & 31u)) & 1u) continue;  // included above
+#else
           if ((known >> (r & 31u)) & 1u) continue;  // included above
           const NodeRec Q = rule_at(T, r);
+#endif
           if (Q.nflags & NF_NULL) continue;
           tri mt = 1;
           if (Q.nflags & NF_HAS_TARGET) {
