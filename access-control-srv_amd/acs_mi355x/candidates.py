@@ -33,6 +33,18 @@ the *useful* sets, scans loop 2a over the candidate policies (they decide `exact
 `policyEffect`) and walks loop 2b over the useful policies only.  whatIsAllowed keeps the
 candidate sections (its obligations are pushed by any matching target).
 
+Composed rows (two required roles).  A request whose role associations name two roles some
+target requires has the key (entity, action, {a, b}); at 10M c3 requests with 1-2 roles there
+are ~0.7M such keys, too many rows.  The "composed" level keys rows by one role — (entity,
+action, a) and (entity, action, b) — and the kernel ORs the request's two rows
+(ReqLine.cls2).  checkSubjectMatches' role test is an OR over the request's roles, so the
+candidate rule and policy sections compose exactly; the derived sections are built
+role-relaxed so that their OR covers the joint key's: candidate sets ignore set targets' role
+tests (a set kept because a role-free candidate policy is in it), and a policy is useful
+through a candidate rule when its target passes with the role test ignored (``_useful_relaxed``).
+The target verdicts compose too: known true = OR, known false = AND (both rows know it).  For
+stores whose set / policy targets carry no role (c3, c5) the relaxed rows equal the exact ones.
+
 Layout: ``cand[class][W]`` u32 words, sections in this order: candidate sets (ws words),
 candidate policies (wp), useful sets (ws), useful policies (wp), candidate rules (wr);
 W = 2 ws + 2 wp + wr.  The class id sits in the request header's flags
@@ -392,21 +404,49 @@ def action_candidates(cs, pairs):
     return tuple(out)
 
 
+def _useful_relaxed(cs, s_free, p, p_free, r, thr_rows, pol_static, set_null):
+    """Useful sets / policies of composed-level rows (module docstring): a candidate policy is
+    useful when it may throw or is effect-only (its own role test applied), or when a candidate
+    rule sits under it and its target passes with the role test ignored; a role-free candidate
+    set is useful when one of its policies is (or it holds a null policy).  Each piece is an OR
+    over the roles of the row, so the OR of two rows covers the joint key's useful sections."""
+    C = s_free.shape[0]
+    if cs.n_pols and cs.n_rules:
+        cr = np.concatenate([np.zeros((C, 1), np.int64), np.cumsum(r, axis=1)], axis=1)
+        has_rule = (cr[:, cs.pols["child_end"].astype(np.int64)] - cr[:, cs.pols["child_begin"].astype(np.int64)]) > 0
+    else:
+        has_rule = np.zeros((C, cs.n_pols), bool)
+    up = (p & (pol_static[None, :] | thr_rows)) | (p_free & has_rule)
+    if cs.n_pols:
+        cu = np.concatenate([np.zeros((C, 1), np.int64), np.cumsum(up, axis=1)], axis=1)
+        any_up = (cu[:, cs.sets["child_end"].astype(np.int64)] - cu[:, cs.sets["child_begin"].astype(np.int64)]) > 0
+    else:
+        any_up = np.zeros((C, cs.n_sets), bool)
+    us = s_free & (any_up | set_null[None, :])
+    return us, up
+
+
+LEVELS = ("entity+roles+action", "composed", "entity+action", "entity")
+
+
 def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
-    """Class id per request (u32, PCOL_ALL = unfiltered) and the class rows [C, W] u32.
+    """Class id per request (u32, PCOL_ALL = unfiltered), the second class per request (u32,
+    1 + class id; 0 = none: composed rows), the class rows [C, W] u32 and the role factor.
 
     A class row is the AND of three node filters — entity column, role associations,
     action — and requests whose rows come out identical share a class (so the coherence
-    sort groups them).  When the keys would need too much memory (large stores) the key is
-    coarsened: (entity, action), then entity alone."""
+    sort groups them).  When the keys would need too much memory the key is coarsened:
+    per-role rows composed by the kernel (two required roles), then (entity, action) with a
+    role factor, then entity alone."""
     role_ids, req_rows = role_requirements(cs)
     nrr = len(role_ids)
     n = len(hdr)
     active = (pcol != L.PCOL_ALL) & ((hdr["flags"] & (L.RQ_HOST | L.RQ_NO_TARGET)) == 0)
     cls = np.full(n, L.PCOL_ALL, np.uint32)
+    cls2 = np.zeros(n, np.uint32)
     W = row_layout(cs)[4]
     if not active.any():
-        return cls, np.zeros((1, W), np.uint32), None, None
+        return cls, cls2, np.zeros((1, W), np.uint32), None, None
     if act is not None:
         ak, apairs = action_keys(hdr, act)
     else:
@@ -414,7 +454,8 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
     A = action_candidates(cs, apairs)
     rs = _role_sets(hdr, roles, role_ids)
     used = rs[:, ::-1]  # largest rows first; -1 padding last
-    width = max(int((used >= 0).sum(axis=1).max()) if n else 0, 1)
+    nused = (used >= 0).sum(axis=1) if n else np.zeros(0, np.int64)
+    width = max(int(nused.max()) if n else 0, 1)
     E_s, E_p, E_r = ent
     A_s, A_p, A_r = A
     b_s = cs.sets["child_begin"].astype(np.int64)
@@ -423,19 +464,36 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
     pol_static, set_null = useful_static(cs)
     if thr is None:
         thr = np.zeros((int(pcol[pcol != L.PCOL_ALL].max(initial=0)) + 1, cs.n_pols), bool)
-    levels = ("entity+roles+action", "entity+action", "entity")
-    for level in (levels if FORCE_LEVEL is None else (FORCE_LEVEL,)):
+    act_idx = np.flatnonzero(active)
+    for level in (LEVELS if FORCE_LEVEL is None else (FORCE_LEVEL,)):
+        if level == "composed" and nrr == 0:  # no target requires a role: the joint keys are role-free
+            level = "entity+roles+action"
+        composed = level == "composed"
+        role_filter = level in ("entity+roles+action", "composed")
+        action_filter = level != "entity"
         cols = [pcol.astype(np.int64)[:, None]]
-        if level != "entity":
+        if action_filter:
             cols.append(ak[:, None])
         if level == "entity+roles+action":
             cols.append(used[:, :width])
+        elif composed:
+            # primary key: the request's first required role (all of them past two); secondary:
+            # its second role, for the requests with exactly two
+            prim = np.full((n, width), -1, np.int64)
+            prim[:, 0] = used[:, 0]
+            big = nused > 2
+            prim[big] = used[big, :width]
+            cols.append(prim)
         key = np.concatenate(cols, axis=1)
-        ckey, inv = _unique_rows(key[active])
+        kact = key[active]
+        two = np.flatnonzero(active & (nused == 2))
+        if composed and len(two):
+            sec = key[two].copy()
+            sec[:, 2] = used[two, 1]
+            kact = np.concatenate([kact, sec])
+        ckey, inv = _unique_rows(kact)
         if len(ckey) * W * 4 > _KEY_ROW_BYTES and level != "entity":
             continue
-        role_filter = level == "entity+roles+action"
-        action_filter = level != "entity"
         out = np.zeros((len(ckey), W), np.uint32)
         chunk = max(8, min(_CHUNK, _CHUNK_NODE_BITS // max(1, cs.n_sets + cs.n_pols + cs.n_rules)))
         for c0 in range(0, len(ckey), chunk):
@@ -457,14 +515,23 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
 
             p = E_p[pc] & role_ok(req_rows[1]) & A_p[a]
             r = E_r[pc] & role_ok(req_rows[2]) & A_r[a]
-            s = E_s[pc] & role_ok(req_rows[0]) & A_s[a]
+            thr_rows = thr[np.minimum(pc, len(thr) - 1)]
+            if composed:  # role-relaxed derived sections (module docstring)
+                p_free = E_p[pc] & A_p[a]
+                s = E_s[pc] & A_s[a]
+            else:
+                s = E_s[pc] & role_ok(req_rows[0]) & A_s[a]
+            pc_ = p_free if composed else p
             if cs.n_pols:
-                cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
+                cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(pc_, axis=1)], axis=1)
                 pol_any = (cum[:, e_s] - cum[:, b_s]) > 0
             else:
                 pol_any = np.zeros((len(ck), cs.n_sets), bool)
             s &= pol_any & nonempty[None, :]
-            us, up = _useful(cs, s, p, r, thr[np.minimum(pc, len(thr) - 1)], pol_static, set_null)
+            if composed:
+                us, up = _useful_relaxed(cs, s, p, p_free, r, thr_rows, pol_static, set_null)
+            else:
+                us, up = _useful(cs, s, p, r, thr_rows, pol_static, set_null)
             verdicts = None
             if res is not None:
                 pxt, pxf, prt, prf = _verdicts(cs, 1, pc, a, A_p, role_ok(req_rows[1]), role_filter, action_filter,
@@ -488,11 +555,51 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
     rank = np.empty(len(cost), np.int64)
     rank[np.argsort(-cost, kind="stable")] = np.arange(len(cost))
     urows = np.ascontiguousarray(urows[np.argsort(rank)])
-    cls[active] = rank[rinv[inv]].astype(np.uint32)
+    kcls = rank[rinv[inv]]
+    cls[act_idx] = kcls[:len(act_idx)].astype(np.uint32)
+    if composed and len(two):
+        # the heavier class first (the coherence order groups by it), the same row once
+        c_a = cls[two].astype(np.int64)
+        c_b = kcls[len(act_idx):]
+        cls[two] = np.minimum(c_a, c_b).astype(np.uint32)
+        cls2[two] = np.where(c_a == c_b, 0, np.maximum(c_a, c_b) + 1).astype(np.uint32)
     if role_filter or nrr == 0:
-        return cls, urows, None, None
+        return cls, cls2, urows, None, None
     rkey, rbits = _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr.any(axis=0), pol_static, set_null)
-    return cls, urows, rkey, rbits
+    return cls, cls2, urows, rkey, rbits
+
+
+def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
+    """The encoder's coherence order (acs_req_batch.perm): request indices grouped so that a
+    wave shares its class row(s) — [bucket | second class] with bucket = 1 + class (0: an
+    unfiltered request), or role-major [role key | bucket] with a role factor — stable (index
+    order within a key).  pad (default: 32 to 256 requests per class on average, and no
+    role factor): each bucket's run starts on a 64-lane wave boundary, the holes 0xFFFFFFFF
+    (shorter classes would multiply the launch width).
+    acs_codec.cpp writes the same order.  Returns u32 [lanes]."""
+    n = len(cls)
+    c = cls.astype(np.int64)
+    bucket = np.where(c < cand_rows, c + 1, 0)
+    if role_key is not None:
+        rk = np.minimum(role_key.astype(np.int64), 0xFFFF)
+        key = (rk << 17) | bucket
+        pad = False
+    else:
+        key = (bucket << 17) | cls2.astype(np.int64)
+    perm = np.argsort(key, kind="stable").astype(np.uint32)
+    if pad is None:
+        pad = 32 * cand_rows <= n < 256 * cand_rows
+    if not pad or n == 0:
+        return perm
+    b = bucket[perm]
+    starts = np.flatnonzero(np.concatenate([[True], b[1:] != b[:-1]]))
+    sizes = np.diff(np.append(starts, n))
+    padded = (sizes + 63) & ~63
+    dst0 = np.concatenate([[0], np.cumsum(padded)[:-1]])
+    out = np.full(int(padded.sum()), 0xFFFFFFFF, np.uint32)
+    pos = np.repeat(dst0 - starts, sizes) + np.arange(n)
+    out[pos] = perm
+    return out
 
 
 def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr_any, pol_static, set_null):

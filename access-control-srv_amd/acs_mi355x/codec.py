@@ -100,6 +100,8 @@ class CodecBatch:
                           if s.role_key else None)
         self.lines = _view(s.lines, L.REQ_LINE_DT, n) if s.lines else np.zeros(0, L.REQ_LINE_DT)
         self.ext = _view(s.ext, np.uint32, int(s.ext_words)) if s.ext else np.zeros(0, np.uint32)
+        self.perm = _view(s.perm, np.uint32, int(s.perm_lanes)) if s.perm else None  # coherence order
+        self.cls2 = self.lines["cls2"]  # 1 + second class (composed class rows; 0: none)
         self.overlay = _Strings(self)
         self.host_reasons = {}
         for i in np.flatnonzero((self.lines["h"]["flags"] & np.uint32(L.RQ_HOST)) != 0):
@@ -138,13 +140,14 @@ class CodecBatch:
         """Bytes of the compact form (what the host-buffer path uploads)."""
         return sum(a.nbytes for a in (self.lines, self.ext, self.arena, self.rx)) + \
             (self.cand.nbytes if self.cand is not None else 0) + \
-            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
+            (self.perm.nbytes if self.perm is not None else 0)
 
     compact_nbytes = nbytes
 
     def close(self):
         if self.h:
-            for k in ("arena", "rx", "cand", "role_key", "role_bits", "lines", "ext"):
+            for k in ("arena", "rx", "cand", "role_key", "role_bits", "lines", "ext", "perm", "cls2"):
                 setattr(self, k, None)
             self._soa = None
             _lib().acs_codec_batch_free(self.h)

@@ -44,6 +44,9 @@ class DeviceBatch:
         if compact:
             ext = getattr(batch, "ext", None)
             self.t["ext"] = _to_dev(ext if ext is not None and ext.size else np.zeros(4, np.uint32), self.dev)
+        perm = getattr(batch, "perm", None)
+        if perm is not None and perm.size:  # the encoder's coherence order (no device sort)
+            self.t["perm"] = _to_dev(perm, self.dev)
         self.ptrs = {k: v.data_ptr() for k, v in self.t.items()}
         self.struct = batch_struct(batch, self.ptrs, compact=compact)
         self.nbytes = sum(v.numel() for v in self.t.values())

@@ -56,20 +56,24 @@ class RequestBatch:
     role_bits: np.ndarray | None = None  # [role rows, W] u32
     lines: np.ndarray | None = None      # [n] REQ_LINE_DT packed first rows (pack_lines)
     ext: np.ndarray | None = None        # u32 extension records of the rows past each line (pack_ext)
+    cls2: np.ndarray | None = None       # [n] u32 1 + second class (composed class rows; 0: none)
+    perm: np.ndarray | None = None       # u32 coherence order (candidates.coherence_order)
 
     def nbytes(self):
         return sum(a.nbytes for a in (self.hdr, self.res, self.subj, self.act, self.roles, self.arena, self.rx)) + \
             (self.cand.nbytes if self.cand is not None else 0) + \
             (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
             (self.lines.nbytes if self.lines is not None else 0) + \
-            (self.ext.nbytes if self.ext is not None else 0)
+            (self.ext.nbytes if self.ext is not None else 0) + \
+            (self.perm.nbytes if self.perm is not None else 0)
 
     def compact_nbytes(self):
         """Bytes of the compact form (acs_layout.h): lines + extension records + arena + regex
         matrix + class / role-factor rows — what the host-buffer path uploads."""
         return self.lines.nbytes + self.ext.nbytes + self.arena.nbytes + self.rx.nbytes + \
             (self.cand.nbytes if self.cand is not None else 0) + \
-            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0)
+            (self.role_key.nbytes + self.role_bits.nbytes if self.role_key is not None else 0) + \
+            (self.perm.nbytes if self.perm is not None else 0)
 
 
 def _attr_list(v, what):
@@ -482,6 +486,8 @@ def pack_lines(b: RequestBatch) -> np.ndarray:
     ln["a0"] = np.where(h["nact"] > 0, b.act[0], zp)
     ln["r0"] = np.where(h["nroles"] > 0, b.roles[0], 0)
     ln["r1"] = np.where(h["nroles"] > 1, b.roles[1], 0)
+    if b.cls2 is not None:
+        ln["cls2"] = b.cls2
     live = (h["flags"] & np.uint32(L.RQ_HOST | L.RQ_NO_TARGET)) == 0
     off = h["arena_off"].astype(np.int64)
     if b.arena.size:
@@ -534,7 +540,9 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     b.cand_wv = candidates.verdict_offset(cs)
     pcol = candidates.primary_columns(b.res["kind"], b.res["col"], b.hdr["nres"], ncols)
     roles = b.roles if role_filter else np.zeros((0, b.n), np.uint32)
-    cls, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr, res)
+    cls, b.cls2, b.cand, b.role_key, b.role_bits = candidates.classes(cs, b.hdr, roles, pcol, ent, b.act, thr, res)
     b.hdr["flags"] = (b.hdr["flags"] & np.uint32(0xFFFF)) | (cls.astype(np.uint32) << np.uint32(L.RQ_PCOL_SHIFT))
     b.lines = pack_lines(b)
     b.ext = pack_ext(b)
+    # the coherence order the kernels run in (the encoder knows every class: no device sort)
+    b.perm = candidates.coherence_order(cls, b.cls2, b.cand.shape[0], b.role_key)

@@ -53,7 +53,7 @@ DECISION_DT = np.dtype([("decision", u8), ("ec", u8), ("flags", u8), ("err", u8)
 # acs_layout.h ReqLine: a request's first rows packed into one 128-B line
 REQ_LINE_DT = np.dtype([("h", REQ_HDR_DT), ("res", REQ_RES_DT, (4,)), ("s0", PAIR_DT), ("s1", PAIR_DT),
                         ("a0", PAIR_DT), ("r0", u32), ("r1", u32), ("ar0", u32), ("ar1", u32), ("ext", u32),
-                        ("pad", u32)])
+                        ("cls2", u32)])
 assert REQ_LINE_DT.itemsize == 128
 
 

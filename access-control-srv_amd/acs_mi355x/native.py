@@ -25,7 +25,8 @@ class ReqBatchC(C.Structure):
                 ("cand_rows", C.c_uint32), ("cand_wsu", C.c_uint32), ("cand_wpu", C.c_uint32),
                 ("cand_wv", C.c_uint32),
                 ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
-                ("role_rows", C.c_uint32), ("lines", C.c_void_p), ("ext", C.c_void_p), ("ext_words", C.c_size_t)]
+                ("role_rows", C.c_uint32), ("lines", C.c_void_p), ("ext", C.c_void_p), ("ext_words", C.c_size_t),
+                ("perm", C.c_void_p), ("perm_lanes", C.c_size_t)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -119,6 +120,8 @@ def batch_struct(b, ptrs=None, compact=False) -> ReqBatchC:
             s.lines = b.lines.ctypes.data
         if compact and b.ext.size:
             s.ext = b.ext.ctypes.data
+        if getattr(b, "perm", None) is not None and b.perm.size:
+            s.perm = b.perm.ctypes.data
     else:
         for k in ("hdr", "res", "subj", "act", "roles"):
             if not compact:
@@ -128,6 +131,9 @@ def batch_struct(b, ptrs=None, compact=False) -> ReqBatchC:
         s.role_key, s.role_rows_bits = ptrs.get("role_key"), ptrs.get("role_bits")
         s.lines = ptrs.get("lines")
         s.ext = ptrs.get("ext") if compact else None
+        s.perm = ptrs.get("perm")
+    if s.perm:
+        s.perm_lanes = int(b.perm.size)
     if compact:
         s.ext_words = int(b.ext.size)
     s.arena_words = int(b.arena.size)

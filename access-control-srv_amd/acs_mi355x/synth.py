@@ -349,9 +349,10 @@ class SynthBatch:
         """JSON array text of requests ``idx`` (default: all), built from string templates —
         millions per second's worth, for the end-to-end (JSON -> decision) measurement.  Equal,
         request for request, to ``json.dumps(decode(i))`` except that at c3 the subject names
-        its HR forest by reference — ``"$hrs": hrs_key(i)`` in place of the inline
-        ``hierarchical_scopes`` tree (the per-subject forest cache of acs_codec; register
-        the forests with ``hrs_forests``)."""
+        its HR forests by reference — ``"$hrs": [keys]``, one registered forest per role
+        association, in place of the inline ``hierarchical_scopes`` trees (the per-subject
+        forest cache of acs_codec, which concatenates the listed forests' roots; register them
+        with ``hrs_forests``)."""
         d = self.draws
         idx = np.arange(self.batch.n) if idx is None else np.asarray(idx)
         u_ent, u_prop, u_rid = URN["entity"], URN["property"], URN["resourceID"]
@@ -385,7 +386,7 @@ class SynthBatch:
                        f'[{{"id":"{rsi}","value":"org{int(scope2[i])}"}}]}}]}}') if r2 >= 0 else ""
                 ctx = (f'"context":{{"subject":{{"id":"u{u}","role_associations":[{{"role":"r{r}","attributes":['
                        f'{{"id":"{rse}","value":"{ORG_ENTITY}","attributes":[{{"id":"{rsi}","value":"org{sc}"}}]}}]}}{ra2}],'
-                       f'"$hrs":"{self.hrs_key(i)}"}},"resources":[{{"id":"res{int(rid[i])}","meta":{{"owners":['
+                       f'"$hrs":{self.hrs_keys_json(i)}}},"resources":[{{"id":"res{int(rid[i])}","meta":{{"owners":['
                        f'{{"id":"{oe}","value":"{ORG_ENTITY}","attributes":[{{"id":"{oi}","value":"org{int(owner[i])}"}}]}}'
                        + (f'],"acls":[{{"id":"{ae}","value":"{ORG_ENTITY}","attributes":[{{"id":"{ai}",'
                           f'"value":"org{int(acl[i])}"}}]}}' if int(acl[i]) >= 0 else '') +
@@ -393,24 +394,29 @@ class SynthBatch:
             out.append(head + ctx)
         return ("[" + ",".join(out) + "]").encode()
 
-    def hrs_key(self, i):
-        """The subject forest a c3 request names: its scope org and role (and the second
-        association's, when it has one)."""
-        k = f"s{int(self.draws['scope'][i])}:r{int(self.draws['role'][i])}"
+    def hrs_keys(self, i):
+        """The subject forests a c3 request names, one per role association: (scope org, role),
+        and the second association's when it has one; their root arrays concatenate into the
+        subject's hierarchical_scopes."""
+        keys = [(int(self.draws["scope"][i]), int(self.draws["role"][i]))]
         r2 = int(self.draws["role2"][i]) if "role2" in self.draws else -1
-        return k if r2 < 0 else f"{k}:s{int(self.draws['scope2'][i])}:r{r2}"
+        if r2 >= 0:
+            keys.append((int(self.draws["scope2"][i]), r2))
+        return keys
+
+    def hrs_keys_json(self, i):
+        return "[" + ",".join(f'"s{sc}:r{r}"' for sc, r in self.hrs_keys(i)) + "]"
 
     def hrs_forests(self, idx=None):
-        """{hrs_key: hierarchical_scopes} of requests ``idx`` (the forests to register)."""
+        """{key: hierarchical_scopes} of the per-association forests requests ``idx`` name (the
+        forests to register: at most one per (scope org, role))."""
         out = {}
         idx = np.arange(self.batch.n) if idx is None else np.asarray(idx)
         for i in idx.tolist():
-            k = self.hrs_key(i)
-            if k not in out:
-                out[k] = [self.tree.subtree_json(int(self.draws["scope"][i]), role(int(self.draws["role"][i])))]
-                r2 = int(self.draws["role2"][i]) if "role2" in self.draws else -1
-                if r2 >= 0:
-                    out[k].append(self.tree.subtree_json(int(self.draws["scope2"][i]), role(r2)))
+            for sc, r in self.hrs_keys(i):
+                k = f"s{sc}:r{r}"
+                if k not in out:
+                    out[k] = [self.tree.subtree_json(sc, role(r))]
         return out
 
 

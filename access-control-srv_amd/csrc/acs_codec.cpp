@@ -22,6 +22,7 @@
 // id, the bit masks of the roots whose subtree (Euler interval of the DFS) holds it.  A
 // request then costs one hash lookup per owner instance instead of a tree walk.
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -302,10 +303,29 @@ struct HrForest {
   StrPool ids;                // storage of the org ids `masks` is keyed by
   StrMap<uint64_t> masks;     // org id -> root bits | key bits << 32 (flat: one probe run per owner lookup)
   std::string text;           // inline forests: the exact JSON text they were built from
+  // A composed forest ("$hrs": [k1, k2, ...]: the concatenation of registered root arrays) has
+  // no masks of its own: its parts', root bits shifted by the part's first root, key bits
+  // remapped into the merged first-seen key order.
+  struct Part {
+    std::shared_ptr<const HrForest> f;
+    uint32_t root_off = 0;
+    uint8_t key_map[MAX_HRKEYS] = {};
+  };
+  std::vector<Part> parts;
   size_t bytes() const { return text.size() + masks.size() * 64 + 256; }
   uint64_t mask(std::string_view id) const {
-    const auto* e = masks.find(id);
-    return e ? e->v : 0;
+    if (parts.empty()) {
+      const auto* e = masks.find(id);
+      return e ? e->v : 0;
+    }
+    uint64_t m = 0;
+    for (const Part& p : parts) {
+      const uint64_t x = p.f->mask(id);
+      if (!x) continue;
+      m |= (x & 0xFFFFFFFFull) << p.root_off;
+      for (uint32_t k = (uint32_t)(x >> 32); k; k &= k - 1) m |= 1ull << (32 + p.key_map[__builtin_ctz(k)]);
+    }
+    return m;
   }
 };
 
@@ -390,6 +410,40 @@ void build_forest(HrForest& F, const JV* hrs) {
   } catch (const Unsup& u) {
     F.why = u.why;
   }
+}
+
+// The forest of the concatenated root arrays of `parts` (build_forest over the concatenation:
+// roots in order, effective-role keys in first-seen order across the parts).
+std::shared_ptr<HrForest> compose_forests(const std::vector<std::shared_ptr<const HrForest>>& parts) {
+  auto F = std::make_shared<HrForest>();
+  F->is_array = true;
+  for (const auto& f : parts) {
+    if (f->why && !F->why) F->why = f->why;
+    if (!f->is_array && !F->why) F->why = "registered HR scopes are not an array";
+    if (F->why) continue;
+    HrForest::Part P;
+    P.f = f;
+    P.root_off = (uint32_t)F->roots.size();
+    if (F->roots.size() + f->roots.size() > (size_t)MAX_ROOTS) {
+      F->why = "too many HR scope roots";
+      continue;
+    }
+    F->roots.insert(F->roots.end(), f->roots.begin(), f->roots.end());
+    for (size_t k = 0; k < f->keys.size(); ++k) {
+      size_t at = 0;
+      while (at < F->keys.size() && !scalar_eq(F->keys[at], f->keys[k])) ++at;
+      if (at == F->keys.size()) {
+        if (F->keys.size() >= (size_t)MAX_HRKEYS) {
+          F->why = "too many HR effective roles";
+          break;
+        }
+        F->keys.push_back(f->keys[k]);
+      }
+      P.key_map[k] = (uint8_t)at;
+    }
+    F->parts.push_back(std::move(P));
+  }
+  return F;
 }
 
 }  // namespace
@@ -712,7 +766,7 @@ struct acs_codec_batch {
   acs_codec* codec = nullptr;
   std::shared_ptr<HostPool> pool;
   uint32_t n = 0;
-  HostBlock lines_b, ext_b, arena_b, cand_b;
+  HostBlock lines_b, ext_b, arena_b, cand_b, perm_b;
   ReqLine* lines = nullptr;   // [n]
   uint32_t* ext = nullptr;    // extension records (ReqLine.ext)
   size_t ext_words = 0;
@@ -724,6 +778,8 @@ struct acs_codec_batch {
   uint32_t cand_rows = 0, cand_words = 0, cand_wp = 0, cand_wr = 0, cand_wsu = 0, cand_wpu = 0, cand_wv = 0;
   std::vector<uint32_t> role_key, role_bits;
   uint32_t role_rows = 0;
+  uint32_t* perm = nullptr;  // coherence order (candidates.coherence_order), perm_lanes entries
+  size_t perm_lanes = 0;
   // SoA rows (acs_codec_batch_expand)
   bool expanded = false;
   std::vector<ReqHdr> hdr;
@@ -741,6 +797,7 @@ struct acs_codec_batch {
     pool->release(ext_b);
     pool->release(arena_b);
     pool->release(cand_b);
+    pool->release(perm_b);
   }
   // request rows of the compact form
   const ReqHdr& h(uint32_t i) const { return lines[i].h; }
@@ -912,6 +969,7 @@ class Encoder {
   }
   std::shared_ptr<const HrForest> inline_forest(const JV* raw);
   const HrForest* subject_forest(const JV* key);
+  const std::shared_ptr<const HrForest>& registered_forest(const JV* key);
   void encode_one(uint32_t i, const JV* req);
 
   acs_codec& C;
@@ -929,13 +987,13 @@ class Encoder {
   static constexpr size_t RECENT = 4096;
   std::unique_ptr<RecentString[]> recent_{new RecentString[RECENT]};
   // this thread's view of batch-wide state, keyed by views into the request text (valid for
-  // the batch): entity value -> regex-matrix column, "$hrs" subject key -> forest (the
-  // shared_ptrs in `held_` keep the forests alive), so the shared maps and their locks are
-  // touched once per distinct value per thread, not once per request
+  // the batch): entity value -> regex-matrix column, "$hrs" subject key (or key list) ->
+  // forest (the maps' shared_ptrs keep the forests alive), so the shared maps and their locks
+  // are touched once per distinct value per thread, not once per request
   std::unordered_map<std::string_view, uint32_t, FastHash> cols_;
   uint32_t col_undef_ = NONE32, col_null_ = NONE32;
-  std::unordered_map<std::string_view, const HrForest*, FastHash> forests_;
-  std::vector<std::shared_ptr<const HrForest>> held_;
+  std::unordered_map<std::string_view, std::shared_ptr<const HrForest>, FastHash> forests_;
+  std::unordered_map<std::string, std::shared_ptr<const HrForest>> composed_;  // "$hrs" key lists
   // per-request scratch (cleared, never freed)
   std::vector<const JV*> slot_objs_;
   std::vector<std::pair<uint32_t, uint8_t>> keys_a_, keys_b_;
@@ -973,25 +1031,44 @@ std::shared_ptr<const HrForest> Encoder::inline_forest(const JV* raw) {
   return F;
 }
 
+// A "$hrs" key: one registered forest (createHRScope's per-subject cache), or a list of them
+// whose root arrays concatenate into the subject's hierarchical_scopes (e.g. one cached forest
+// per role association), composed once per distinct list per thread and batch.
 const HrForest* Encoder::subject_forest(const JV* key) {
+  if (key->t != J_ARR) {
+    const HrForest* f = registered_forest(key).get();
+    ++hits;
+    return f;
+  }
+  std::string ck;
+  for (uint32_t k = 0; k < key->n; ++k) {
+    if (key->a[k].t != J_STR) unsup("$hrs subject key is not a string");
+    ck.append(key->a[k].s, key->a[k].n);
+    ck.push_back('\x1f');
+  }
+  ++hits;
+  auto it = composed_.find(ck);
+  if (it != composed_.end()) return it->second.get();
+  std::vector<std::shared_ptr<const HrForest>> parts;
+  for (uint32_t k = 0; k < key->n; ++k) parts.push_back(registered_forest(&key->a[k]));
+  std::shared_ptr<const HrForest> F = compose_forests(parts);
+  return composed_.emplace(std::move(ck), F).first->second.get();
+}
+
+const std::shared_ptr<const HrForest>& Encoder::registered_forest(const JV* key) {
   if (key->t != J_STR) unsup("$hrs subject key is not a string");
   auto mine = forests_.find(key->str());
-  if (mine != forests_.end()) {
-    if (!mine->second) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
-    ++hits;
-    return mine->second;
+  if (mine == forests_.end()) {
+    std::shared_ptr<const HrForest> f;
+    {
+      std::shared_lock<std::shared_mutex> lock(C.hr_mu);
+      auto it = C.hr_subject.find(std::string(key->str()));
+      if (it != C.hr_subject.end()) f = it->second;
+    }
+    mine = forests_.emplace(key->str(), std::move(f)).first;
   }
-  std::shared_ptr<const HrForest> f;
-  {
-    std::shared_lock<std::shared_mutex> lock(C.hr_mu);
-    auto it = C.hr_subject.find(std::string(key->str()));
-    if (it != C.hr_subject.end()) f = it->second;
-  }
-  forests_.emplace(key->str(), f.get());
-  if (!f) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
-  held_.push_back(f);
-  ++hits;
-  return f.get();
+  if (!mine->second) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+  return mine->second;
 }
 
 #if defined(ACS_CODEC_TIMING)  // profiling harness only: cycles in parse / encode_one
@@ -1666,6 +1743,42 @@ struct Classes {
     return r;
   }
 
+  // Composed-level row (candidates.py "composed", _useful_relaxed): candidate policies and rules
+  // with the roles' test, candidate sets and the useful sections role-relaxed so that the OR of
+  // two rows covers the joint key's.  [S | P | useful S | useful P | R] like assemble.
+  Row composed_row(uint32_t pc, uint32_t a, const int32_t* roles, int nroles, const Row* thr,
+                   const std::vector<std::shared_ptr<const Row>>& ent,
+                   const std::vector<std::shared_ptr<const Row>>& arow) const {
+    Row base(*ent[pc]);  // role-free: entity & action
+    const Row& A = *arow[a];
+    for (uint32_t w = 0; w < C.W; ++w) base[w] &= A[w] & valid[w];
+    Row r(base);
+    const Row f = role_filter_fn(roles, nroles);
+    for (uint32_t w = 0; w < C.W; ++w) r[w] &= f[w];
+    sets_need_policies(base);  // role-free sets holding a role-free candidate policy
+    Row out(C.W2, 0u);
+    std::copy(base.begin(), base.begin() + C.ws, out.begin());
+    std::copy(r.begin() + C.ws, r.begin() + C.ws + C.wp, out.begin() + C.ws);
+    std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
+    const uint32_t wsu = C.ws + C.wp, wpu = 2 * C.ws + C.wp, rr = C.ws + C.wp;
+    for (uint32_t q = 0; q < C.P; ++q) {
+      bool use = bit(r, C.ws, q) && (C.pol_static[q] || (thr && bit(*thr, 0, q)));
+      if (!use && bit(base, C.ws, q)) {
+        const NodeRec& N = C.nodes[C.S + q];
+        for (uint32_t k = N.child_begin; k < N.child_end && !use; ++k) use = bit(r, rr, k);
+      }
+      if (use) out[wpu + (q >> 5)] |= 1u << (q & 31);
+    }
+    for (uint32_t s = 0; s < C.S; ++s) {
+      if (!bit(base, 0, s)) continue;
+      bool use = C.set_null[s];
+      const NodeRec& N = C.nodes[s];
+      for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(out, wpu, q);
+      if (use) out[wsu + (s >> 5)] |= 1u << (s & 31);
+    }
+    return out;
+  }
+
   void run();
 };
 
@@ -1860,54 +1973,90 @@ void Classes::run() {
   };
   const size_t KEY_ROW_BYTES = size_t(512) << 20, ROLE_ROW_BYTES = size_t(256) << 20;
   const uint32_t MAX_CLASSES = PCOL_ALL;
-  // tests pin the key level (candidates.FORCE_LEVEL) through acs_internal_codec_force_level
+  // key levels (candidates.LEVELS): 0 entity+roles+action, 1 composed (per-role rows the kernel
+  // ORs, two required roles), 2 entity+action (+ role factor), 3 entity; tests pin one
+  // (candidates.FORCE_LEVEL) through acs_internal_codec_force_level
   const int force = C.force_level;
-  const int first_level = force >= 0 && force <= 2 ? force : 0;
-  const int last_level = force >= 0 && force <= 2 ? first_level + 1 : 3;
+  const int first_level = force >= 0 && force <= 3 ? force : 0;
+  const int last_level = force >= 0 && force <= 3 ? first_level + 1 : 4;
   const bool packable = C.role_ids.size() < 512;
-  for (int level = first_level; level < last_level; ++level) {
-    const bool role_filter = level == 0 && have_roles;
-    const bool action_filter = level < 2;
-    // distinct keys of the active requests, numbered in order of first appearance: 64-bit
-    // packed keys deduplicated per thread range, then merged in range order
+  // requests with exactly two required roles (the composed level's second keys)
+  std::vector<uint32_t> two;
+  for (uint32_t i = 0; i < n; ++i)
+    if (active[i] && nrs[i] == 2) two.push_back(i);
+  for (int lv = first_level; lv < last_level; ++lv) {
+    const int level = lv == 1 && !have_roles ? 0 : lv;  // no target requires a role: role-free keys
+    const bool composed = level == 1;
+    const bool role_filter = level <= 1 && have_roles;
+    const bool action_filter = level < 3;
+    // key items: item t < n is request t's (primary) key, item n + j the second key of two[j]
+    // (composed level); each names its request and its role rows
+    const size_t N = composed ? (size_t)n + two.size() : (size_t)n;
+    auto req_of = [&](size_t t) -> uint32_t { return t < n ? (uint32_t)t : two[t - n]; };
+    auto item_active = [&](size_t t) -> bool { return t >= n || active[t]; };
+    // role rows of item t: level 0 all (ascending); composed: the largest (all past two) for a
+    // primary, the second largest for a secondary
+    auto roles_of = [&](size_t t, int* m) -> const int32_t* {
+      const uint32_t i = req_of(t);
+      const int32_t* r = &rs[(size_t)i * RW];
+      const int k = nrs[i];
+      if (!role_filter) {
+        *m = 0;
+        return r;
+      }
+      if (!composed || k > 2) {
+        *m = k;
+        return r;
+      }
+      if (k == 0) {
+        *m = 0;
+        return r;
+      }
+      *m = 1;
+      return t < n ? r + (k - 1) : r + (k - 2);
+    };
     bool pack_ok = packable;
     if (role_filter)
       for (uint32_t i = 0; i < n && pack_ok; ++i) pack_ok = nrs[i] <= 4;
-    auto kv = [&](uint32_t i) -> uint64_t {  // pcol 16 | ak 6 | nrs 3 | 4 x 9-bit role rows
+    auto kv = [&](size_t t) -> uint64_t {  // pcol 16 | ak 6 | nrs 3 | 4 x 9-bit role rows
+      const uint32_t i = req_of(t);
       uint64_t k = (uint64_t)(pcol[i] & 0xFFFF) << 48 | (uint64_t)(action_filter ? ak[i] : 0) << 42;
-      if (role_filter) {
-        k |= (uint64_t)nrs[i] << 36;
-        for (int j = 0; j < nrs[i]; ++j) k |= (uint64_t)rs[(size_t)i * RW + j] << (9 * j);
-      }
+      int m;
+      const int32_t* r = roles_of(t, &m);
+      k |= (uint64_t)m << 36;
+      for (int j = 0; j < m; ++j) k |= (uint64_t)r[j] << (9 * j);
       return k;
     };
-    auto ks = [&](uint32_t i) -> std::string {
+    auto ks = [&](size_t t) -> std::string {
+      const uint32_t i = req_of(t);
       std::string kb((const char*)&pcol[i], 4);
       if (action_filter) kb.append((const char*)&ak[i], 4);
-      if (role_filter) kb.append((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      int m;
+      const int32_t* r = roles_of(t, &m);
+      kb.append((const char*)r, 4 * (size_t)m);
       return kb;
     };
-    std::vector<uint32_t> key_of(n, NONE32), key_first;
+    std::vector<uint32_t> key_of(N, NONE32), key_first;  // key_first: first item of each key
     {
       int T = threads < 1 ? 1 : threads;
-      if ((size_t)T > n / 4096 + 1) T = (int)(n / 4096 + 1);
+      if ((size_t)T > N / 4096 + 1) T = (int)(N / 4096 + 1);
       std::vector<std::vector<uint32_t>> firsts(T);
-      parallel_ranges(T, n, [&](int t, size_t lo, size_t hi) {
+      parallel_ranges(T, N, [&](int t, size_t lo, size_t hi) {
         if (pack_ok) {
           U64Map m(1024);
           bool ins;
-          for (uint32_t i = (uint32_t)lo; i < hi; ++i) {
-            if (!active[i]) continue;
-            key_of[i] = m.get_or_put(kv(i), (uint32_t)firsts[t].size(), &ins);
-            if (ins) firsts[t].push_back(i);
+          for (size_t x = lo; x < hi; ++x) {
+            if (!item_active(x)) continue;
+            key_of[x] = m.get_or_put(kv(x), (uint32_t)firsts[t].size(), &ins);
+            if (ins) firsts[t].push_back((uint32_t)x);
           }
         } else {
           std::unordered_map<std::string, uint32_t> m;
-          for (uint32_t i = (uint32_t)lo; i < hi; ++i) {
-            if (!active[i]) continue;
-            auto it = m.emplace(ks(i), (uint32_t)firsts[t].size());
-            if (it.second) firsts[t].push_back(i);
-            key_of[i] = it.first->second;
+          for (size_t x = lo; x < hi; ++x) {
+            if (!item_active(x)) continue;
+            auto it = m.emplace(ks(x), (uint32_t)firsts[t].size());
+            if (it.second) firsts[t].push_back((uint32_t)x);
+            key_of[x] = it.first->second;
           }
         }
       });
@@ -1918,33 +2067,33 @@ void Classes::run() {
       for (int t = 0; t < T; ++t) {
         remap[t].resize(firsts[t].size());
         for (size_t k = 0; k < firsts[t].size(); ++k) {
-          const uint32_t i = firsts[t][k];
+          const uint32_t x = firsts[t][k];
           uint32_t g;
           bool ins;
           if (pack_ok) {
-            g = gm.get_or_put(kv(i), (uint32_t)key_first.size(), &ins);
+            g = gm.get_or_put(kv(x), (uint32_t)key_first.size(), &ins);
           } else {
-            auto it = gs.emplace(ks(i), (uint32_t)key_first.size());
+            auto it = gs.emplace(ks(x), (uint32_t)key_first.size());
             g = it.first->second;
             ins = it.second;
           }
-          if (ins) key_first.push_back(i);
+          if (ins) key_first.push_back(x);
           remap[t][k] = g;
         }
       }
-      parallel_ranges(T, n, [&](int t, size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i)
-          if (key_of[i] != NONE32) key_of[i] = remap[t][key_of[i]];
+      parallel_ranges(T, N, [&](int t, size_t lo, size_t hi) {
+        for (size_t x = lo; x < hi; ++x)
+          if (key_of[x] != NONE32) key_of[x] = remap[t][key_of[x]];
       });
     }
     const size_t nk = key_first.size();
-    if (level < 2 && nk * W * 4 > KEY_ROW_BYTES) continue;
+    if (level < 3 && nk * W * 4 > KEY_ROW_BYTES) continue;
     // cache lookup by (level, entity value, action, roles); compute the misses in parallel
     std::vector<std::string> gkey(nk);
     std::vector<std::shared_ptr<const ClassEntry>> entry(nk);
     std::vector<uint32_t> miss;
     for (size_t k = 0; k < nk; ++k) {
-      const uint32_t i = key_first[k];
+      const uint32_t x = key_first[k], i = req_of(x);
       std::string g(1, (char)('0' + level));
       g += col_key(pcol[i]);
       g.push_back('\0');
@@ -1954,7 +2103,9 @@ void Classes::run() {
         else g.append((const char*)&pairs_k[a - 2], 8);
       }
       g.push_back('|');
-      if (role_filter) g.append((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      int m;
+      const int32_t* r = roles_of(x, &m);
+      g.append((const char*)r, 4 * (size_t)m);
       gkey[k] = std::move(g);
     }
     {
@@ -1974,11 +2125,14 @@ void Classes::run() {
         for (;;) {
           const size_t m = next.fetch_add(1);
           if (m >= miss.size()) return;
-          const uint32_t i = key_first[miss[m]];
+          const uint32_t x = key_first[miss[m]], i = req_of(x);
           const uint32_t a = action_filter ? ak[i] : 1u;
-          rows[m] = assemble(class_row(pcol[i], a, &rs[(size_t)i * RW], nrs[i], role_filter, ent, arow),
-                             pcol[i] < ncols ? thr[pcol[i]].get() : nullptr);
-          verdicts(rows[m], pcol[i], a, &rs[(size_t)i * RW], nrs[i], role_filter, action_filter, arow);
+          int nr;
+          const int32_t* r = roles_of(x, &nr);
+          const Row* tr = pcol[i] < ncols ? thr[pcol[i]].get() : nullptr;
+          rows[m] = composed ? composed_row(pcol[i], a, r, nr, tr, ent, arow)
+                             : assemble(class_row(pcol[i], a, r, nr, role_filter, ent, arow), tr);
+          verdicts(rows[m], pcol[i], a, r, nr, role_filter, action_filter, arow);
         }
       };
       std::vector<std::thread> pool;
@@ -2021,7 +2175,7 @@ void Classes::run() {
       if (it.second) uent.push_back(entry[k].get());
       cls_of_key[k] = it.first->second;
     }
-    if (uent.size() > MAX_CLASSES && level < 2) continue;
+    if (uent.size() > MAX_CLASSES && level < 3) continue;
     if (uent.size() > MAX_CLASSES) {
       acs_internal_set_error("acs_codec_encode: too many request classes");
       throw Unsup{"too many request classes"};
@@ -2040,6 +2194,15 @@ void Classes::run() {
     std::vector<uint32_t> cls(n, PCOL_ALL);
     for (uint32_t i = 0; i < n; ++i)
       if (active[i]) cls[i] = rank[cls_of_key[key_of[i]]];
+    if (composed) {
+      // the second class of each two-role request: the heavier class first (the coherence
+      // order groups by it), the same row once
+      for (size_t j = 0; j < two.size(); ++j) {
+        const uint32_t i = two[j], a = cls[i], b = rank[cls_of_key[key_of[n + j]]];
+        cls[i] = a < b ? a : b;
+        B.lines[i].cls2 = a == b ? 0u : (a < b ? b : a) + 1u;
+      }
+    }
     finish(cls);
     if (role_filter || !have_roles) return;
     // role factor (candidates._role_factor): one row per distinct role set of the active
@@ -2350,6 +2513,104 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// acs_req_batch.perm (candidates.coherence_order): request indices grouped by [bucket | second
+// class] (bucket = 1 + class; 0: an unfiltered request) or, with a role factor, role-major
+// [role key | bucket]; stable (index order within a key).  Runs of equal buckets start on
+// 64-lane wave boundaries (holes 0xFFFFFFFF) when the classes average 32 to 256 requests and
+// there is no role factor.  A parallel LSD radix sort of 32-bit keys, 8-bit digits, a
+// digit whose value every key shares skipped.
+void coherence_order(acs_codec_batch& B, int threads) {
+  const size_t n = B.n;
+  const bool rmaj = !B.role_key.empty();
+  std::vector<uint32_t> key(n), idx(n), key2(n), idx2(n);
+  int T = threads < 1 ? 1 : threads;
+  if ((size_t)T > n / 65536 + 1) T = (int)(n / 65536 + 1);
+  parallel_ranges(T, n, [&](int, size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const uint32_t c = B.lines[i].h.flags >> RQ_PCOL_SHIFT;
+      const uint32_t bucket = c < B.cand_rows ? c + 1u : 0u;
+      key[i] = rmaj ? (std::min<uint32_t>(B.role_key[i], 0xFFFFu) << 16 | bucket) : (bucket << 16 | B.lines[i].cls2);
+      idx[i] = (uint32_t)i;
+    }
+  });
+  std::vector<std::array<size_t, 256>> cnt(T);
+  for (int sh = 0; sh < 32; sh += 8) {
+    auto range = [&](int t, size_t& lo, size_t& hi) {
+      lo = n * t / T;
+      hi = n * (t + 1) / T;
+    };
+    std::vector<std::thread> pool;
+    auto hist = [&](int t) {
+      size_t lo, hi;
+      range(t, lo, hi);
+      cnt[t].fill(0);
+      for (size_t x = lo; x < hi; ++x) ++cnt[t][(key[x] >> sh) & 255u];
+    };
+    for (int t = 1; t < T; ++t) pool.emplace_back(hist, t);
+    hist(0);
+    for (auto& th : pool) th.join();
+    pool.clear();
+    size_t total = 0;
+    bool constant = false;
+    for (uint32_t d = 0; d < 256 && !constant; ++d) {
+      size_t c = 0;
+      for (int t = 0; t < T; ++t) c += cnt[t][d];
+      constant = c == n;
+    }
+    if (constant) continue;
+    for (uint32_t d = 0; d < 256; ++d)  // per (digit, thread) exclusive offsets
+      for (int t = 0; t < T; ++t) {
+        const size_t c = cnt[t][d];
+        cnt[t][d] = total;
+        total += c;
+      }
+    auto scatter = [&](int t) {
+      size_t lo, hi;
+      range(t, lo, hi);
+      std::array<size_t, 256>& o = cnt[t];
+      for (size_t x = lo; x < hi; ++x) {
+        const size_t at = o[(key[x] >> sh) & 255u]++;
+        key2[at] = key[x];
+        idx2[at] = idx[x];
+      }
+    };
+    for (int t = 1; t < T; ++t) pool.emplace_back(scatter, t);
+    scatter(0);
+    for (auto& th : pool) th.join();
+    key.swap(key2);
+    idx.swap(idx2);
+  }
+  const bool pad = !rmaj && n >= 32ull * B.cand_rows && n < 256ull * B.cand_rows;
+  size_t lanes = n;
+  if (pad) {
+    lanes = 0;
+    for (size_t x = 0; x < n;) {
+      size_t y = x + 1;
+      while (y < n && (key[y] >> 16) == (key[x] >> 16)) ++y;
+      lanes += (y - x + 63) & ~size_t(63);
+      x = y;
+    }
+  }
+  B.perm_b = B.pool->acquire(lanes * sizeof(uint32_t));
+  B.perm = (uint32_t*)B.perm_b.p;
+  B.perm_lanes = lanes;
+  if (!pad) {
+    memcpy(B.perm, idx.data(), n * sizeof(uint32_t));
+    return;
+  }
+  size_t at = 0;
+  for (size_t x = 0; x < n;) {
+    size_t y = x + 1;
+    while (y < n && (key[y] >> 16) == (key[x] >> 16)) ++y;
+    memcpy(B.perm + at, idx.data() + x, (y - x) * sizeof(uint32_t));
+    const size_t run = (y - x + 63) & ~size_t(63);
+    for (size_t k = y - x; k < run; ++k) B.perm[at + k] = 0xFFFFFFFFu;
+    at += run;
+    x = y;
+  }
+}
+
+
 using Items = std::vector<std::pair<const char*, const char*>>;
 
 acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const char*>* items, size_t count,
@@ -2502,6 +2763,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
   Classes cl(*c, *B, T);
   cl.col_keys = keys;  // padding column: ''
   cl.run();
+  coherence_order(*B, T);  // the kernels' order: the classes are known here (no device sort)
   const double t3 = now_s();
   B->seconds[0] = t1 - t0;
   B->seconds[1] = t2 - t1;
@@ -2625,7 +2887,7 @@ acs_codec_batch* acs_internal_encode_range(acs_codec* c, const acs_internal_item
 }
 
 // Test hook (not in include/acs_mi355x.h): pin the candidate-class key level of every later
-// encode (0 entity+roles+action, 1 entity+action, 2 entity; -1 automatic).
+// encode (0 entity+roles+action, 1 composed, 2 entity+action, 3 entity; -1 automatic).
 int acs_internal_codec_force_level(acs_codec* c, int level) {
   if (!c) return -1;
   c->force_level = level;
@@ -2696,6 +2958,8 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
     v.role_rows_bits = b->role_bits.data();
     v.role_rows = b->role_rows;
   }
+  v.perm = b->n ? b->perm : nullptr;
+  v.perm_lanes = b->n ? b->perm_lanes : 0;
   *out = v;
   return 0;
 }

@@ -65,8 +65,6 @@ struct Tables {
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
-  uint32_t rep_n;    // device image copies (ACS_TABLE_REPLICAS A/B; 1 in the product)
-  uint64_t rep_stride;  // bytes between copies
 };
 
 #if defined(ACS_SCAN_COUNT)
@@ -83,15 +81,14 @@ __device__ inline void scan_count(uint32_t bytes) {
 #define ACS_SCAN(bytes)
 #endif
 
-// Table record reads: 0 all-lane vector loads + readfirstlane (product), 1 one-lane vector
-// loads (c3 K1 1.891 ms vs 1.851, same-call A/B r03_g), 2 scalar loads (1.791 ms, but a scalar
-// load ignores EXEC: a block the compiler enters with no active lane reads an unchecked
-// address — the counting build faulted on c4 — so it stays an A/B form).
-#ifndef ACS_LOAD_MODE
-#define ACS_LOAD_MODE 0
-#endif
 // Table records are read as whole dwords through wave-uniform addresses and unpacked in
-// registers (vector loads, then SGPRs: see below).
+// registers.  Vector loads (exec-masked, so a block entered with no active lane loads
+// nothing), then the wave-uniform record moves to SGPRs: its fields feed scalar compares and
+// branches and free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself
+// proves the address uniform it emits s_load; nothing here forces a scalar load (a scalar
+// load ignores EXEC, so a block entered with no active lane would read an unchecked address:
+// the round-3 scalar-load A/B form faulted on c4 and was removed).  One-lane vector loads
+// measured slower (c3 K1 1.891 vs 1.851 ms, r03_g).
 template <class X, int NW = sizeof(X) / 4>
 ACS_FN X load_words(const Tables& T, const X* p) {
   static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
@@ -100,37 +97,8 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
 #if defined(__HIP_DEVICE_COMPILE__)
-#if ACS_LOAD_MODE == 2
-  // Scalar loads: the address moves to SGPRs and the record is read through the constant
-  // address space (s_load_dwordxN into SGPRs): no vector-memory instruction, no VGPR.
-  typedef __attribute__((address_space(4))) const uint32_t const_u32;
-  const uint64_t a = reinterpret_cast<uint64_t>(w);
-  const uint64_t ua = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                      __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const const_u32* q = (const const_u32*)ua;
-#pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = q[k];
-#elif ACS_LOAD_MODE == 1
-  // One lane loads (the wave's first active lane: 1/64 of the address and return traffic of
-  // an all-lane load of the same record), then the record moves to SGPRs.
-  const uint64_t act = __ballot(1);
-  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-#pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = 0u;
-  if (lane == (uint32_t)__builtin_ctzll(act)) {
-#pragma unroll
-    for (int k = 0; k < NW; ++k) v[k] = w[k];
-  }
-#pragma unroll
-  for (int k = 0; k < NW; ++k) v[k] = __builtin_amdgcn_readfirstlane(v[k]);
-#else
-  // Vector loads (exec-masked, so a block entered with no active lane loads nothing), then
-  // the wave-uniform record moves to SGPRs: its fields feed scalar compares and branches and
-  // free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself proves
-  // the address uniform it emits s_load; nothing here forces a scalar load.
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = __builtin_amdgcn_readfirstlane(w[k]);
-#endif
 #else
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];
@@ -149,36 +117,6 @@ ACS_FN NodeRec node_at(const Tables& T, const NodeRec* sec, uint32_t x, uint32_t
 // Rule r.  The device image stores each rule in a 128-B line (record + inline attributes).
 ACS_FN NodeRec rule_at(const Tables& T, uint32_t r) {
   return node_at(T, T.rules, r * T.rstride, T.n_rules * T.rstride);
-}
-
-#ifndef ACS_AB_RULE_PREFETCH  // A/B: K2 loads the next candidate rule's record ahead
-#define ACS_AB_RULE_PREFETCH 0
-#endif
-// A rule record still in VGPRs (loaded, not yet waited on) and its move to SGPRs.
-struct RawRec {
-  uint32_t v[sizeof(NodeRec) / 4];
-};
-ACS_FN RawRec raw_rule(const Tables& T, uint32_t r) {
-  ACS_SCAN(sizeof(NodeRec));
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(T.rules + (size_t)r * T.rstride);
-  RawRec o;
-#pragma unroll
-  for (int k = 0; k < (int)(sizeof(NodeRec) / 4); ++k) o.v[k] = w[k];
-  return o;
-}
-ACS_FN NodeRec rec_of(const RawRec& x) {
-  uint32_t v[sizeof(NodeRec) / 4];
-#pragma unroll
-  for (int k = 0; k < (int)(sizeof(NodeRec) / 4); ++k) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    v[k] = __builtin_amdgcn_readfirstlane(x.v[k]);
-#else
-    v[k] = x.v[k];
-#endif
-  }
-  NodeRec out;
-  __builtin_memcpy(&out, v, sizeof out);
-  return out;
 }
 
 struct Batch {
@@ -207,6 +145,28 @@ struct Batch {
   const uint32_t* ext;        // compact batches (hdr == nullptr): extension records (ReqLine.ext)
 };
 
+// The second class row of request i (ReqLine.cls2, composed class rows) or nullptr.  A cls2
+// outside the batch's rows leaves the request unfiltered (*bad), never narrower.
+ACS_FN const uint32_t* second_row(const Batch& B, uint32_t i, bool* bad) {
+  *bad = false;
+  if (!B.lines || !B.cand) return nullptr;
+  const uint32_t c2 = B.lines[i].cls2;
+  if (!c2) return nullptr;
+  if (c2 - 1u >= B.cand_rows) {
+    *bad = true;
+    return nullptr;
+  }
+  return B.cand + (size_t)(c2 - 1u) * B.cand_words;
+}
+
+// Target-verdict word of a lane with one or two class rows: a known-true section (exact /
+// RegExp true, rules retried true) is true when either row knows it (the composed request holds
+// both role sets); a known-false section (`conj`) only when both do.
+ACS_FN uint32_t compose_verdict(uint32_t a, const uint32_t* row2, uint32_t at, bool conj) {
+  if (!row2) return a;
+  return conj ? a & row2[at] : a | row2[at];
+}
+
 // OR of x over the wave's ACTIVE lanes, returned in an SGPR.  A lane drops out once its bits
 // are covered, so the loop runs once per lane that still adds bits (lanes sharing a row
 // share the value: a few rounds).  Host build: x itself (one request).
@@ -231,19 +191,23 @@ ACS_FN uint32_t wave_or(uint32_t x) {
 // the iteration needs (lanes that returned or skipped the enclosing policy read nothing).
 struct Filter {
   const uint32_t* row;     // this request's class row
-  const uint32_t* rrow;    // its role-factor row (== row when the batch has no role factor)
+  const uint32_t* row2;    // its second class row (composed rows; nullptr: none)
+  const uint32_t* rrow;    // its role-factor row (nullptr: the batch has no role factor)
   const uint32_t* lds;     // GPU: the wave's OR of its (class & role) rows, words [0, lds_n)
   uint32_t lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
   uint32_t wsu, wpu;       // isAllowed: useful sets / loop-2b policies (0 / wp without them)
   uint32_t wv;             // target-verdict sections (candidates.verdict_offset)
-  bool vok;                // the verdicts apply: the row is this request's own class row
+  bool vok;                // the verdicts apply: the rows are this request's own class rows
   bool all;                // no filtering
-  // bit i of the verdict section at word `sec` past wv (false when the verdicts do not apply)
-  ACS_FN bool verdict(uint32_t sec, uint32_t i) const {
-    return vok && ((row[wv + sec + (i >> 5)] >> (i & 31)) & 1u);
+  // word w of the verdict section at word `sec` past wv (0 when the verdicts do not apply);
+  // conj: a known-false section (AND over the request's rows)
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
+    return vok ? compose_verdict(row[wv + sec + w], row2, wv + sec + w, conj) : 0u;
   }
-  ACS_FN uint32_t vword(uint32_t sec, uint32_t w) const { return vok ? row[wv + sec + w] : 0u; }
+  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {
+    return (vword(sec, i >> 5, conj) >> (i & 31)) & 1u;
+  }
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -251,7 +215,10 @@ struct Filter {
     if (w < lds_n) return wave_uniform(((lds_u32*)lds)[w]);
 #endif
     ACS_SCAN(8);  // a word of the lanes' class and role rows (counted once per wave)
-    return wave_or(row[w] & rrow[w]);
+    uint32_t x = row[w];
+    if (row2) x |= row2[w];
+    if (rrow) x &= rrow[w];
+    return wave_or(x);
   }
 };
 
@@ -262,19 +229,21 @@ struct Filter {
 struct FilterAll {
   uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
-  ACS_FN bool verdict(uint32_t, uint32_t) const { return false; }  // no class rows
-  ACS_FN uint32_t vword(uint32_t, uint32_t) const { return 0u; }
+  ACS_FN bool verdict(uint32_t, uint32_t, bool = false) const { return false; }  // no class rows
+  ACS_FN uint32_t vword(uint32_t, uint32_t, bool = false) const { return 0u; }
 };
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
 // kernel before any lane diverges (all ones for a wave holding an unfiltered request).  The
-// target verdicts are class facts: a wave of one class reads them from its LDS row (`single`);
-// in a wave that mixes classes each lane reads its own class row (`own`, L2-resident; nullptr
-// for an unfiltered lane: no verdicts).
+// target verdicts are class facts: a wave of one class (no composed lane) reads them from its
+// LDS row (`single`); in a wave that mixes classes each lane reads its own class row (`own`,
+// L2-resident; nullptr for an unfiltered lane: no verdicts) and a composed lane also its second
+// row (`own2`).
 struct FilterLds {
   const uint32_t* lds;
   uint32_t wp, wr, wsu, wpu, wv;
   const uint32_t* own;
+  const uint32_t* own2;
   bool single;
   ACS_FN uint32_t word(uint32_t w) const {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -284,18 +253,15 @@ struct FilterLds {
     return lds[w];
 #endif
   }
-  // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane)
-  ACS_FN uint32_t vword(uint32_t sec, uint32_t w) const {
-#if defined(ACS_NO_VERDICT_CODE)  // A/B builds: the traversal without any verdict lookup
-    (void)sec;
-    (void)w;
-    return 0u;
-#else
+  // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane);
+  // conj: a known-false section
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
     if (single) return word(wv + sec + w);
-    return own ? own[wv + sec + w] : 0u;
-#endif
+    return own ? compose_verdict(own[wv + sec + w], own2, wv + sec + w, conj) : 0u;
   }
-  ACS_FN bool verdict(uint32_t sec, uint32_t i) const { return (vword(sec, i >> 5) >> (i & 31)) & 1u; }
+  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {
+    return (vword(sec, i >> 5, conj) >> (i & 31)) & 1u;
+  }
 };
 
 // Ascending iteration over the candidate indices in [b, e) of one bitset section.  Every
@@ -356,14 +322,12 @@ struct CandRangeRev {
 
 ACS_FN bool loose_eq(uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); }
 
-#ifndef ACS_POLICY_VERDICTS
-#define ACS_POLICY_VERDICTS 1  // K1 also skips policy target matching on known verdicts
-#endif
-
 // Target verdicts, F.verdict(sec, i) (candidates.verdict_offset): bit i of the section at
 // word `sec` past the verdict base — policies known exact-true (sec 0), exact-false (WP),
 // RegExp-true (2 WP), RegExp-false (3 WP), rules whose retried match is known true (4 WP);
-// WP = ceil(P / 32).  False wherever the class's verdicts do not apply.
+// WP = ceil(P / 32).  False wherever the class's verdicts do not apply.  The known-false
+// sections (WP, 3 WP) are read with conj = true: a composed request (two class rows) knows a
+// target false only when both of its rows do.
 
 // tri-state result: 1 true, 0 false, <0 -ErrKind (the reference throws)
 typedef int tri;
@@ -975,11 +939,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) return *ev = make_err(-(tri)ERR_TYPE, s + 1), SET_EVENT;
       if (P.nflags & NF_HAS_TARGET) {
-#if ACS_POLICY_VERDICTS
-        const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
-#else
-        const tri m = target_match(P, R, P.pe_at, false, false, nullptr);
-#endif
+        const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p, true) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
         if (m) {
           exact = true;
@@ -1008,12 +968,8 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     if (P.nflags & NF_HAS_TARGET) {
       PROF_T0(tp);
       // the class's verdict for this lane's mode
-#if ACS_POLICY_VERDICTS
       const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
-      const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
-#else
-      const bool kt = false, kf = false;
-#endif
+      const bool kf = exact ? F.verdict(WP, p, true) : F.verdict(3 * WP, p, true);
       const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
       if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
       if (!m) {
@@ -1167,14 +1123,24 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   F.wv = B.cand_wv;
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
-  F.row = F.rrow = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
+  F.row = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
+  F.row2 = F.rrow = nullptr;
   F.vok = !F.all && B.cand_wv != 0;  // the request's own class row
   return F;
 }
 
 ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h, uint32_t i) {
   Filter F = request_filter(B, h);
-  if (!F.all && B.role_key && B.role_key[i] < B.role_rows) F.rrow = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
+  if (F.all) return F;
+  bool bad = false;
+  F.row2 = second_row(B, i, &bad);
+  if (bad) {  // a second class outside the rows: unfiltered, no verdicts
+    F.all = true;
+    F.vok = false;
+    F.row2 = nullptr;
+    return F;
+  }
+  if (B.role_key && B.role_key[i] < B.role_rows) F.rrow = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
   return F;
 }
 
@@ -1276,7 +1242,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           // a verdict-known target has no property attribute, so it pushes no obligation
-          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p) ? 0 : target_match(P, R, P.pe_at, false, true, &obl);
+          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p, true) ? 0 : target_match(P, R, P.pe_at, false, true, &obl);
           if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
@@ -1299,7 +1265,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
         const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
-        const bool kf = exact ? F.verdict(WP, p) : F.verdict(3 * WP, p);
+        const bool kf = exact ? F.verdict(WP, p, true) : F.verdict(3 * WP, p, true);
         const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, true, &obl);
         if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
@@ -1321,22 +1287,11 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
           any_rule = true;
         }
         uint32_t rest = wave_or(m & ~known);
-#if ACS_AB_RULE_PREFETCH
-        // the next candidate's record is in flight while this one is matched
-        RawRec nxt{};
-        if (rest) nxt = raw_rule(T, wave_uniform(base + (uint32_t)__builtin_ctz(rest)));
-#endif
         while (rest) {
           const uint32_t r = wave_uniform(base + (uint32_t)__builtin_ctz(rest));
           rest &= rest - 1u;
-#if ACS_AB_RULE_PREFETCH
-          const NodeRec Q = rec_of(nxt);
-          if (rest) nxt = raw_rule(T, wave_uniform(base + (uint32_t)__builtin_ctz(rest)));
-          if ((known >> (r & 31u)) & 1u) continue;  // included above
-#else
           if ((known >> (r & 31u)) & 1u) continue;  // included above
           const NodeRec Q = rule_at(T, r);
-#endif
           if (Q.nflags & NF_NULL) continue;
           tri mt = 1;
           if (Q.nflags & NF_HAS_TARGET) {

@@ -10,6 +10,7 @@
 //                             (class, low) keys -> the permutation K1 / K2 run in.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -49,7 +50,9 @@ constexpr int BLOCK = 256;
 
 // A/B switches of experiment builds (acs_mi355x/build.build_variant, `bench.py --lib`), fixed
 // at compile time: the product library defines none of them, so no environment variable can
-// change how a service evaluates.
+// change how a service evaluates.  (Forms that measured no gain — table replicas over L2
+// channels, scalar / one-lane record loads, K2 occupancy and rule prefetch, SoA-instantiated
+// compact kernels, unscattered records — were removed after their A/Bs: DESIGN.md §3.)
 #ifndef ACS_AB_NO_CUT          // combining loops and the set walk always run to their end
 #define ACS_AB_NO_CUT 0
 #endif
@@ -59,41 +62,11 @@ constexpr int BLOCK = 256;
 #ifndef ACS_AB_NO_VERDICTS     // ignore the per-class target verdicts
 #define ACS_AB_NO_VERDICTS 0
 #endif
-#ifndef ACS_AB_NO_LINES        // read the SoA rows instead of the packed request lines
-#define ACS_AB_NO_LINES 0
-#endif
-#ifndef ACS_AB_BLOB_RULES      // rule records in the blob layout instead of 128-B lines
-#define ACS_AB_BLOB_RULES 0
-#endif
-#ifndef ACS_AB_NO_SCATTER      // timing only: K1/K2 write records in sort order (out[k])
-#define ACS_AB_NO_SCATTER 0
-#endif
-#ifndef ACS_AB_PROLOGUE_ONLY   // timing only: K1 stops after the filter build and line read
-#define ACS_AB_PROLOGUE_ONLY 0
-#endif
-#ifndef ACS_TABLE_REPLICAS     // A/B: copies of the device image, spread over L2 channels
-#define ACS_TABLE_REPLICAS 1
-#endif
-#ifndef ACS_AB_NO_BITS         // timing only: K2 stores no inclusion bitset
-#define ACS_AB_NO_BITS 0
-#endif
-#ifndef ACS_AB_NO_PAD          // whatIsAllowed waves may mix classes (no wave-aligned class runs)
+#ifndef ACS_AB_NO_PAD          // device sort: waves may mix classes (no wave-aligned class runs)
 #define ACS_AB_NO_PAD 0
 #endif
-#ifndef ACS_AB_NO_CB           // compact batches run the kernels instantiated for SoA batches
-#define ACS_AB_NO_CB 0
-#endif
-#ifndef ACS_AB_K2_NOCB         // whatIsAllowed only: compact batches run the SoA instantiation
-#define ACS_AB_K2_NOCB 0
-#endif
-#ifndef ACS_AB_WAVE_VERDICTS   // verdicts only in one-class waves (no per-lane class-row reads)
-#define ACS_AB_WAVE_VERDICTS 0
-#endif
-#ifndef ACS_AB_RADIX_ONLY      // the coherence sort always takes the radix passes
-#define ACS_AB_RADIX_ONLY 0
-#endif
-#ifndef ACS_AB_FILTER_GENERAL  // the general filter form for every batch
-#define ACS_AB_FILTER_GENERAL 0
+#ifndef ACS_AB_DEVICE_SORT     // ignore the encoder's coherence order (the device sorts, round-3 form)
+#define ACS_AB_DEVICE_SORT 0
 #endif
 
 // Sort key that makes a wave share its request class (one candidate row) and action — or,
@@ -409,13 +382,32 @@ constexpr uint32_t LDS_FILTER_WORDS = 1024;
 #ifndef ACS_SORT_ROLE_MAJOR_DEFAULT
 #define ACS_SORT_ROLE_MAJOR_DEFAULT 1  // c5 A/B: 269 ms class-major, 244 ms role-major (r02_h)
 #endif
+// OR the second class rows of the wave's composed lanes (ReqLine.cls2 = c2, 1 + class) into
+// its LDS row, words [0, LW); *any: the wave holds a composed lane.  False when one names a row
+// outside the batch (the wave then runs unfiltered).
+__device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, uint32_t* lds, uint32_t LW, bool* any) {
+  const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
+  uint64_t pending = __ballot(valid && c2 != 0u);
+  *any = pending != 0;
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const uint32_t k = __builtin_amdgcn_readlane(c2, leader);
+    if (k - 1u >= B.cand_rows) return false;
+    const uint32_t* row = B.cand + (size_t)(k - 1u) * W;
+    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w];
+    ACS_SCAN(LW * 4u);
+    pending &= ~__ballot(valid && c2 == k);
+  }
+  return true;
+}
+
 // Candidate filter of a wave, built with every lane present before any lane diverges.  A
-// request's row is its class row, AND-ed with its role-factor row when the batch has one.
-// The LDS part is the OR of the rows of all the wave's active requests over the first
-// lds_n words, however many (class, role key) pairs the wave spans; Filter::word ORs the
-// active lanes' own rows past it.  An unfiltered request (PCOL_ALL) disables filtering for
-// its wave.
-__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
+// request's row is its class row (OR its second class row: composed rows), AND-ed with its
+// role-factor row when the batch has one.  The LDS part is the OR of the rows of all the
+// wave's active requests over the first lds_n words, however many (class, role key) pairs the
+// wave spans; Filter::word ORs the active lanes' own rows past it.  An unfiltered request
+// (PCOL_ALL) disables filtering for its wave.
+__device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t c2, uint32_t* lds) {
   Filter F{};
   F.wp = B.cand_wp;
   F.wr = B.cand_wr;
@@ -432,7 +424,8 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   // this lane's own rows (any valid row for a lane that evaluates nothing)
   const bool own = valid && cls < B.cand_rows;
   F.row = B.cand ? B.cand + (size_t)(own ? cls : 0u) * W : nullptr;
-  F.rrow = own && rk < nroles ? B.role_bits + (size_t)rk * W : F.row;
+  F.row2 = own && c2 && c2 - 1u < B.cand_rows ? B.cand + (size_t)(c2 - 1u) * W : nullptr;
+  F.rrow = own && rk < nroles ? B.role_bits + (size_t)rk * W : nullptr;
   if (F.all) return F;
   for (uint32_t w = lane; w < LW; w += 64) lds[w] = 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
@@ -451,17 +444,21 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
     ACS_SCAN(LW * (rrow == row ? 4u : 8u));
     pending &= ~__ballot(valid && key == k);
   }
+  bool any2;
+  if (!F.all && !or_second_rows(B, valid, c2, lds, LW, &any2)) F.all = true;
   return F;
 }
 
 // The LDS form (FilterLds): the wave's OR row over its (class & role) rows in this wave's
 // W-word LDS region, all ones when the wave holds an unfiltered request.
-__device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, nullptr, false};
+__device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t c2,
+                                            uint32_t* lds) {
+  FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, nullptr, nullptr,
+              false};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
-  bool all = false;
+  bool all = false, any2 = false;
   uint32_t first_cls = PCOL_ALL, classes = 0;
   for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
   uint64_t pending = __ballot(valid);
@@ -482,13 +479,16 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     }
     pending &= ~__ballot(valid && key == k);
   }
+  if (!all && !or_second_rows(B, valid, c2, lds, W, &any2)) all = true;
   if (all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
   // the verdicts are the class's (role keys may differ: role rows keep the verdict sections
-  // whole): a wave of one class reads them from LDS, any other lane from its own class row
-  // (the LDS form is only chosen for batches that carry verdict sections)
-  F.single = !all && classes == 1 && !B.no_verdicts;
-  F.own = valid && cls < B.cand_rows && !B.no_verdicts && !ACS_AB_WAVE_VERDICTS ? B.cand + (size_t)cls * W : nullptr;
+  // whole): a wave of one class and no composed lane reads them from LDS, any other lane from
+  // its own class row(s) (the LDS form is only chosen for batches that carry verdict sections)
+  F.single = !all && classes == 1 && !any2 && !B.no_verdicts;
+  const bool c2ok = c2 == 0u || c2 - 1u < B.cand_rows;
+  F.own = valid && cls < B.cand_rows && c2ok && !B.no_verdicts ? B.cand + (size_t)cls * W : nullptr;
+  F.own2 = F.own && c2 ? B.cand + (size_t)(c2 - 1u) * W : nullptr;
   return F;
 }
 
@@ -499,17 +499,17 @@ __device__ inline FilterAll wave_filter_all(const Batch& B) {
 // One maker per filter form, selected by the kernel's template argument.
 template <class FL> struct FilterMaker;
 template <> struct FilterMaker<Filter> {
-  static __device__ Filter make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-    return wave_filter(B, valid, cls, rk, lds);
+  static __device__ Filter make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t c2, uint32_t* lds) {
+    return wave_filter(B, valid, cls, rk, c2, lds);
   }
 };
 template <> struct FilterMaker<FilterLds> {
-  static __device__ FilterLds make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t* lds) {
-    return wave_filter_lds(B, valid, cls, rk, lds);
+  static __device__ FilterLds make(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t c2, uint32_t* lds) {
+    return wave_filter_lds(B, valid, cls, rk, c2, lds);
   }
 };
 template <> struct FilterMaker<FilterAll> {
-  static __device__ FilterAll make(const Batch& B, bool, uint32_t, uint32_t, uint32_t*) {
+  static __device__ FilterAll make(const Batch& B, bool, uint32_t, uint32_t, uint32_t, uint32_t*) {
     return wave_filter_all(B);
   }
 };
@@ -548,31 +548,18 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 // CB: a compact batch (request lines + extension records, no SoA rows): the kernels are
 // instantiated for it separately so that its row accessors carry no SoA paths (fewer live
-// registers; acs_eval.h ReqCtx::soa).
-// This block's copy of the tables (ACS_TABLE_REPLICAS): blocks are dealt to the 8 XCDs
-// round-robin, so blockIdx / 8 numbers a block within its XCD.
-__device__ inline Tables replica_view(Tables T) {
-#if ACS_TABLE_REPLICAS > 1
-  const uint64_t d = (uint64_t)((blockIdx.x >> 3) % T.rep_n) * T.rep_stride;
-  T.sets = (const NodeRec*)((const char*)T.sets + d);
-  T.pols = (const NodeRec*)((const char*)T.pols + d);
-  T.rules = (const NodeRec*)((const char*)T.rules + d);
-  T.rres = (const RuleResAttr*)((const char*)T.rres + d);
-  T.pairs = (const Pair*)((const char*)T.pairs + d);
-  T.u32pool = (const uint32_t*)((const char*)T.u32pool + d);
-#endif
-  return T;
-}
-
+// registers; acs_eval.h ReqCtx::soa; A/B c3 K1 1.94 -> 1.85 ms, r03_g).
 template <bool CB>
 __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) {
   return CB ? B.lines + i : (in && B.lines ? B.lines + i : nullptr);  // one gather for the first rows
 }
 
+// 1 + the lane's second class (composed class rows; 0: none)
+__device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && ln ? ln->cls2 : 0u; }
+
 template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
-    Tables T0, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
-  const Tables T = replica_view(T0);
+    Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
@@ -585,14 +572,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
   Decision d{};
   if (in) d = early_decision(h, &done);
   const FL F = FilterMaker<FL>::make(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B));
+                                     lane_cls2(ln, in), wave_lds_row(B));
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
 #else
   if (!in) return;
 #endif
-  if (ACS_AB_PROLOGUE_ONLY) done = true;  // A/B timing only: filter build + line read, no walk
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
@@ -606,11 +592,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
-#if ACS_AB_NO_SCATTER
-  if (k < B.n) out[k] = d;  // A/B timing only: records in sort order (wrong order for the caller)
-#else
   out[i] = d;
-#endif
 #else
   if (in) out[i] = d;
   for (int k = 0; k < PH_N; ++k) {  // lane-cycles per phase, one atomic per wave
@@ -624,22 +606,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
-// K2 occupancy A/B (ACS_K2_WAVES_PER_EU=5/6/8: 96/80/64 VGPRs with spills) measured no gain
-// on c4 (6.92-6.95 ms vs 6.62, r03_g): K2 is not latency-bound per wave (SQ_WAIT_ANY ~90 % of
-// wave cycles at every occupancy tried), so the compiler's own 4 waves/SIMD stay.
-#if defined(ACS_K2_WAVES_PER_EU)
-#define ACS_K2_ATTR __attribute__((amdgpu_waves_per_eu(ACS_K2_WAVES_PER_EU)))
-#else
-#define ACS_K2_ATTR
-#endif
+// K2 occupancy A/B (5/6/8 waves per SIMD: 96/80/64 VGPRs with spills) measured no gain on c4
+// (6.92-6.95 ms vs 6.62, r03_g): the compiler's own 4 waves/SIMD stay.
 template <class FL, bool CB>
-__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T0, Batch B, const uint32_t* __restrict__ perm,
+__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                                 uint32_t lanes, BitsLayout BL,
                                                                 uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
-  const Tables T = replica_view(T0);
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
@@ -660,18 +635,10 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
   }
 #endif
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B));
+                                     lane_cls2(ln, in), wave_lds_row(B));
   if (!in) return;
-#if ACS_AB_NO_SCATTER
-  const uint32_t o = k < B.n ? k : i;  // A/B timing only: rows in sort order (wrong order for the caller)
-#else
   const uint32_t o = i;
-#endif
-#if ACS_AB_NO_BITS
-  NullSink sink;  // A/B timing only: no inclusion bitset stores
-#else
   ChunkSink sink(bits + (size_t)o * BL.words, BL);
-#endif
   OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
   Decision d{};
   if (host) {
@@ -719,7 +686,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
   if (in) h = ln ? ln->h : B.hdr[i];
   const bool host = (h.flags & RQ_HOST) != 0;
   const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     wave_lds_row(B));
+                                     lane_cls2(ln, in), wave_lds_row(B));
   if (!live) return;
   if (!in) {
     obl_n[k] = 0xFFFFFFFFu;
@@ -893,11 +860,9 @@ size_t filter_lds_bytes(const Batch& B) {
   return (size_t)(BLOCK / 64) * lds_wave_words(B) * 4;
 }
 
-// Which filter form a batch's kernels are instantiated with (ACS_AB_FILTER_GENERAL: the
-// general form everywhere, A/B builds of the specialisation).
+// Which filter form a batch's kernels are instantiated with.
 enum class FilterForm { All, Lds, General };
 FilterForm filter_form(const Batch& B) {
-  if (ACS_AB_FILTER_GENERAL) return FilterForm::General;
   if (!B.cand) return FilterForm::All;
   return B.cand_words <= LDS_FILTER_WORDS && B.cand_wv ? FilterForm::Lds : FilterForm::General;
 }
@@ -1115,8 +1080,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   // record, action and resource reads hit one cache line instead of three (large stores miss
   // L2 on each).  The rres and pair pools follow the lines, and one base (the first line)
   // addresses both: every node's res_off / act_off / subj_off is rebased, inline attributes
-  // point into their line.  ACS_AB_BLOB_RULES: the blob layout (A/B builds).
-  const bool rule_lines = !ACS_AB_BLOB_RULES;
+  // point into their line (pools too large for rebased u32 offsets keep the blob layout).
   const char* bsrc = (const char*)blob + src;
   std::vector<char> img;
   size_t doff[6];
@@ -1126,7 +1090,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   const size_t lines = (size_t)h.n_rules * 128;
   const size_t l0 = (align16(sz[0]) + align16(sz[1]) + 127) & ~size_t(127);
   const size_t p_rel = lines + align16(sz[3]);  // pair pool, bytes past the first line
-  if (rule_lines && h.n_rules && (p_rel / 8 + h.n_pairs) < 0xFFFFFFFFull && (lines / 16 + h.n_rres) < 0xFFFFFFFFull) {
+  if (h.n_rules && (p_rel / 8 + h.n_pairs) < 0xFFFFFFFFull && (lines / 16 + h.n_rres) < 0xFFFFFFFFull) {
     rstride = 2;
     doff[0] = 0;
     doff[1] = align16(sz[0]);
@@ -1177,16 +1141,9 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
-  // ACS_TABLE_REPLICAS (A/B): R copies of the image at a stride that is an odd multiple of
-  // 256 B, so one record's copies sit in different L2 channels; blocks pick a copy by their
-  // index within their XCD (replica_view)
-  const uint32_t reps = ACS_TABLE_REPLICAS > 1 ? ACS_TABLE_REPLICAS : 1;
-  const size_t rep_stride = ((up_bytes + 255) & ~(size_t)255) | 256;
-  const size_t img_total = reps > 1 ? rep_stride * reps : up_bytes;
-  const size_t alloc = img_total + 128;
-  bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, alloc) == hipSuccess;
-  for (uint32_t c = 0; copied && c < reps; ++c)
-    copied = hipMemcpy((char*)t->dev + c * rep_stride, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess;
+  const size_t img_total = up_bytes;
+  const bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess &&
+                      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess;
   if (!copied ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
@@ -1207,8 +1164,6 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
-  t->view.rep_n = reps;
-  t->view.rep_stride = rep_stride;
   t->image_bytes = img_total;
   return t;
 }
@@ -1311,7 +1266,7 @@ static Batch to_batch(const acs_req_batch* b) {
   B.role_bits = b->role_rows_bits;
   B.role_rows = b->role_key ? b->role_rows : 0u;
   // compact batches (no SoA rows) always read their lines; SoA batches may skip them (A/B)
-  B.lines = (ACS_AB_NO_LINES && b->hdr) ? nullptr : (const ReqLine*)b->lines;
+  B.lines = (const ReqLine*)b->lines;  // (composed class rows are read from the lines)
   B.ext = b->ext;
   return B;
 }
@@ -1401,7 +1356,7 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
   sort_bits(B, &lowbits, &end_bit);
   // key space: class-major keys are < (cand_rows + 1) << lowbits, role-major ones < 2^end_bit
   const uint64_t K = B.role_major ? (1ull << end_bit) : ((uint64_t)B.cand_rows + 1u) << lowbits;
-  if (K <= CS_BINS && !ACS_AB_RADIX_ONLY) {  // one counting pass (class_count_kernel)
+  if (K <= CS_BINS) {  // one counting pass (class_count_kernel)
     uint32_t nb = (uint32_t)((n + 1023) / 1024);
     if (nb > 256) nb = 256;  // one block per CU
     uint32_t chunk = (uint32_t)((n + nb - 1) / nb);
@@ -1445,18 +1400,38 @@ static int coherence_perm(acs_tables* t, Workspace& W, const Batch& B, hipStream
   return radix_passes(k0, n, end_bit, true, s, perm);
 }
 
+// The order the evaluation kernels run a batch in: the encoder's coherence order when the batch
+// carries one (it knows every request's class: no device sort on the step), else the device
+// coherence sort (pad: wave-aligned class runs of the counting sort), or input order with
+// ACS_OPT_SORT off.  *lanes = the launch width.
+static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, const Batch& B, hipStream_t s,
+                       const uint32_t** perm, bool pad, size_t* lanes) {
+  *perm = nullptr;
+  *lanes = b->n;
+  if (b->perm && !ACS_AB_DEVICE_SORT) {
+    if (b->perm_lanes < b->n || b->perm_lanes > 0xFFFFFFFFull) return fail("batch: perm_lanes outside [n, 2^32)");
+    if (!t->sort) return 0;
+    *perm = b->perm;
+    *lanes = b->perm_lanes;
+    return 0;
+  }
+  return coherence_perm(t, W, B, s, perm, pad, lanes);
+}
+
 static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
   // wave-aligned class runs when the classes are short (most waves would mix two or three
-  // classes and walk the union of their candidates): below 256 requests per class on average
-  const bool pad = !ACS_AB_NO_PAD && B.cand && (uint64_t)B.n < 256ull * B.cand_rows;
+  // classes and walk the union of their candidates): 32 to 256 requests per class on average
+  // (shorter classes would multiply the launch width)
+  const bool pad = !ACS_AB_NO_PAD && B.cand && (uint64_t)B.n >= 32ull * B.cand_rows &&
+                   (uint64_t)B.n < 256ull * B.cand_rows;
   size_t lanes = b->n;
-  if (coherence_perm(t, W, B, s, &perm, pad, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, perm,
+  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm,
                       (uint32_t)lanes, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
@@ -1489,13 +1464,13 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
   size_t lanes = b->n;
-  if (coherence_perm(t, W, B, s, &perm, !ACS_AB_NO_PAD, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB && !ACS_AB_K2_NOCB, t->view, B, perm, (uint32_t)lanes, BL, bits,
+  ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, BL, bits,
                       obl, obl_n, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
@@ -1524,7 +1499,7 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const 
   Batch B = to_batch(b);
   const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
   ACS_LAUNCH_FILTERED(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), filter_lds_bytes(B),
-                      (hipStream_t)stream, filter_form(B), B.hdr == nullptr && !ACS_AB_NO_CB, t->view, B, idx, (uint32_t)m, chunks, cap, obl,
+                      (hipStream_t)stream, filter_form(B), B.hdr == nullptr, t->view, B, idx, (uint32_t)m, chunks, cap, obl,
                       obl_n);
   HIP_OK(hipGetLastError());
   return 0;
@@ -1669,6 +1644,7 @@ int upload_batch(Workspace& W, const acs_req_batch* b, acs_req_batch* dev, hipSt
     I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
           (const void**)&I.d.role_rows_bits);
   }
+  if (b->perm) I.add(b->perm, b->perm_lanes * sizeof(uint32_t), (const void**)&I.d.perm);
   if (W.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
   char* base = (char*)W.img.p;
   size_t off = 0;
@@ -1685,8 +1661,10 @@ int upload_batch(Workspace& W, const acs_req_batch* b, acs_req_batch* dev, hipSt
 // arena words only (the shard's slices, uploaded so that the batch's absolute offsets still
 // index them: the device pointers are based one slice-start below the copy), plus the whole
 // regex matrix and class rows.  arena_end: per request, one past its last arena word.
+// sperm: the shard's coherence order (shard-relative indices, the batch's order restricted to
+// the shard) or empty.
 int upload_shard(Workspace& W, const acs_req_batch* b, size_t lo, size_t hi, const uint32_t* arena_end,
-                 acs_req_batch* dev, hipStream_t s) {
+                 const std::vector<uint32_t>& sperm, acs_req_batch* dev, hipStream_t s) {
   size_t plan[4];
   acs_internal_shard_plan(b, lo, hi, arena_end, plan);
   const size_t a0 = plan[0], a1 = plan[1], e0 = plan[2], e1 = plan[3];
@@ -1705,6 +1683,12 @@ int upload_shard(Workspace& W, const acs_req_batch* b, size_t lo, size_t hi, con
     I.add(b->role_key + lo, m * sizeof(uint32_t), (const void**)&I.d.role_key);
     I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
           (const void**)&I.d.role_rows_bits);
+  }
+  I.d.perm = nullptr;
+  I.d.perm_lanes = 0;
+  if (!sperm.empty()) {
+    I.add(sperm.data(), sperm.size() * sizeof(uint32_t), (const void**)&I.d.perm);
+    I.d.perm_lanes = sperm.size();
   }
   if (W.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
   char* base = (char*)W.img.p;
@@ -1749,21 +1733,53 @@ static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision*
   dev.insert(dev.end(), t->peers.begin(), t->peers.end());
   size_t D = dev.size();
   if (b->n / D < MULTI_MIN_PER_DEVICE) D = b->n / MULTI_MIN_PER_DEVICE;
+  const size_t n = b->n;
+  auto lo_of = [&](size_t k) { return n * k / D; };
+  // each shard's coherence order: the batch's order restricted to the shard (holes dropped)
+  std::vector<std::vector<uint32_t>> sperm(D);
+  if (b->perm) {
+    for (size_t k = 0; k < D; ++k) sperm[k].reserve(lo_of(k + 1) - lo_of(k));
+    for (size_t x = 0; x < b->perm_lanes; ++x) {
+      const uint32_t i = b->perm[x];
+      if (i >= n) continue;
+      size_t k = std::min(D - 1, (size_t)i * D / n);
+      while (k > 0 && i < lo_of(k)) --k;
+      while (k + 1 < D && i >= lo_of(k + 1)) ++k;
+      sperm[k].push_back((uint32_t)(i - lo_of(k)));
+    }
+  }
   std::vector<std::unique_lock<std::mutex>> locks;
   for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
+  size_t launched = 0;  // devices with work queued into `out`
+  // on a failure, wait for every shard already queued (its kernel and its copy into the
+  // caller's `out`) before returning: the caller may free `out` and the next call reuse the
+  // workspaces
+  auto drain = [&] {
+    const std::string err = g_err;
+    for (size_t k = 0; k < launched; ++k) {
+      (void)hipSetDevice(dev[k]->device);
+      (void)hipStreamSynchronize(dev[k]->stream);
+    }
+    (void)hipSetDevice(t->device);
+    g_err = err;
+    return -1;
+  };
   for (size_t k = 0; k < D; ++k) {
     acs_tables* T = dev[k];
-    const size_t lo = b->n * k / D, hi = b->n * (k + 1) / D;
-    HIP_OK(hipSetDevice(T->device));
+    const size_t lo = lo_of(k), hi = lo_of(k + 1);
+    if (hipSetDevice(T->device) != hipSuccess) return fail("acs_is_allowed: hipSetDevice failed"), drain();
+    launched = k + 1;  // the copies below are queued on T's stream from here on
     acs_req_batch d;
-    if (upload_shard(T->hws, b, lo, hi, arena_end, &d, T->stream)) return -1;
-    if (T->hws.out.reserve((hi - lo) * sizeof(Decision))) return -1;
-    if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return -1;
-    HIP_OK(hipMemcpyAsync(out + lo, T->hws.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, T->stream));
+    if (upload_shard(T->hws, b, lo, hi, arena_end, sperm[k], &d, T->stream)) return drain();
+    if (T->hws.out.reserve((hi - lo) * sizeof(Decision))) return drain();
+    if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return drain();
+    if (hipMemcpyAsync(out + lo, T->hws.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, T->stream) !=
+        hipSuccess)
+      return fail("acs_is_allowed: result copy failed"), drain();
   }
   for (size_t k = 0; k < D; ++k) {
-    HIP_OK(hipSetDevice(dev[k]->device));
-    HIP_OK(hipStreamSynchronize(dev[k]->stream));
+    if (hipSetDevice(dev[k]->device) != hipSuccess || hipStreamSynchronize(dev[k]->stream) != hipSuccess)
+      return fail("acs_is_allowed: device synchronisation failed"), drain();
   }
   HIP_OK(hipSetDevice(t->device));
   return 0;
@@ -1918,6 +1934,26 @@ int pipeline_retire(acs_pipeline* p, acs_pipeline::Slot& S, acs_decision* out, a
   return 0;
 }
 
+// Drop every slot's chunk without copying it anywhere: wait for its device work (its download
+// writes the slot's own staging buffer, never the caller's), free its batch.  Run after a
+// failed run — whose slots may still hold chunks in flight — and at the start of each run, so
+// no later retire copies a stale chunk into a new caller's output.  Keeps the error message.
+void pipeline_reset(acs_pipeline* p) {
+  const std::string err = g_err;
+  for (auto& S : p->slot) {
+    if (S.busy) {
+      (void)hipSetDevice(S.T->device);
+      (void)hipEventSynchronize(S.done);
+    }
+    if (S.batch) acs_codec_batch_free(S.batch);
+    S.batch = nullptr;
+    S.busy = false;
+    S.lo = S.n = 0;
+  }
+  (void)hipSetDevice(p->t->device);
+  g_err = err;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1971,6 +2007,7 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
                             size_t* n_out, acs_pipeline_stats* st) {
   if (!p || (!json && len) || !n_out) return fail("acs_pipeline_is_allowed: null argument");
   std::lock_guard<std::mutex> lock(p->mu);
+  pipeline_reset(p);  // nothing of an earlier (failed) run may retire into this one's `out`
   if (st) *st = acs_pipeline_stats{};
   p->reasons.clear();
   const double t0 = steady_s();
@@ -1984,56 +2021,68 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     ~Free() { acs_internal_items_free(it); }
   } free_items{items};
   if (n > out_cap || (n && !out)) return fail("acs_pipeline_is_allowed: output holds fewer records than the requests");
+  // any failure once a chunk is in flight: drain every slot (pipeline_reset) before returning
+  auto bail = [&] {
+    pipeline_reset(p);
+    return -1;
+  };
+#define PIPE_HIP(expr)                                                              \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) return fail(std::string(#expr ": ") + hipGetErrorString(e_)), bail(); \
+  } while (0)
   const size_t D = p->slot.size() / 2;
   size_t k = 0;
   for (size_t lo = 0; lo < n; lo += p->chunk, ++k) {
     const size_t hi = lo + p->chunk < n ? lo + p->chunk : n;
     const double e0 = steady_s();
     acs_codec_batch* b = acs_internal_encode_range(p->c, items, lo, hi, p->threads);
-    if (!b) return -1;
+    if (!b) return bail();
     if (st) st->encode_s += steady_s() - e0;
     acs_pipeline::Slot& S = p->slot[2 * (k % D) + (k / D) % 2];
     if (pipeline_retire(p, S, out, st)) {  // this slot's previous chunk
       acs_codec_batch_free(b);
-      return -1;
+      return bail();
     }
-    S.batch = b;
+    S.batch = b;  // owned by the slot from here on (pipeline_reset frees it on a failure)
     S.lo = lo;
     S.n = hi - lo;
     acs_tables* T = S.T;
     acs_req_batch view;
     const double c0 = steady_s();
-    if (acs_codec_batch_view(b, &view) || check_batch(T, &view)) return -1;
+    if (acs_codec_batch_view(b, &view) || check_batch(T, &view)) return bail();
     if (st) st->check_s += steady_s() - c0;
-    HIP_OK(hipSetDevice(T->device));
+    PIPE_HIP(hipSetDevice(T->device));
     if (S.stage_n < S.n) {
-      if (S.stage) HIP_OK(hipHostFree(S.stage));
+      if (S.stage) PIPE_HIP(hipHostFree(S.stage));
       S.stage = nullptr;
       S.stage_n = 0;
-      HIP_OK(hipHostMalloc((void**)&S.stage, S.n * sizeof(acs_decision), hipHostMallocPortable));
+      PIPE_HIP(hipHostMalloc((void**)&S.stage, S.n * sizeof(acs_decision), hipHostMallocPortable));
       S.stage_n = S.n;
     }
     {
       std::lock_guard<std::mutex> tl(T->mu);  // the device handle's launch bookkeeping
       acs_req_batch d;
-      HIP_OK(hipEventRecord(S.ev0, S.stream));
-      if (upload_batch(S.ws, &view, &d, S.stream)) return -1;
-      if (S.ws.out.reserve(S.n * sizeof(Decision))) return -1;
-      if (is_allowed_launch(T, S.ws, &d, (acs_decision*)S.ws.out.p, S.stream)) return -1;
-      HIP_OK(hipMemcpyAsync(S.stage, S.ws.out.p, S.n * sizeof(Decision), hipMemcpyDeviceToHost, S.stream));
-      HIP_OK(hipEventRecord(S.ev1, S.stream));
-      HIP_OK(hipEventRecord(S.done, S.stream));
+      S.busy = true;  // work may be queued from here on: a failure waits for it
+      PIPE_HIP(hipEventRecord(S.ev0, S.stream));
+      if (upload_batch(S.ws, &view, &d, S.stream)) return bail();
+      if (S.ws.out.reserve(S.n * sizeof(Decision))) return bail();
+      if (is_allowed_launch(T, S.ws, &d, (acs_decision*)S.ws.out.p, S.stream)) return bail();
+      PIPE_HIP(hipMemcpyAsync(S.stage, S.ws.out.p, S.n * sizeof(Decision), hipMemcpyDeviceToHost, S.stream));
+      PIPE_HIP(hipEventRecord(S.ev1, S.stream));
+      PIPE_HIP(hipEventRecord(S.done, S.stream));
     }
-    S.busy = true;
     if (st) {
       st->chunks += 1;
       st->upload_bytes += (double)(S.n * sizeof(ReqLine) + view.ext_words * 4 + view.arena_words * 4 +
                                    (size_t)view.rx_cols * view.rx_rows +
-                                   (size_t)view.cand_rows * view.cand_words * 4);
+                                   (size_t)view.cand_rows * view.cand_words * 4 +
+                                   (view.perm ? view.perm_lanes * 4 : 0));
     }
   }
   for (auto& S : p->slot)
-    if (pipeline_retire(p, S, out, st)) return -1;
+    if (pipeline_retire(p, S, out, st)) return bail();
+#undef PIPE_HIP
   HIP_OK(hipSetDevice(p->t->device));
   if (st) {
     st->requests = n;

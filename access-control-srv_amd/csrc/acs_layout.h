@@ -193,8 +193,13 @@ struct ReqLine {             // 128 B
   uint32_t r0, r1;
   uint32_t ar0, ar1;
   uint32_t ext;              // 1 + 16-B unit offset of the extension record (0: none)
-  uint32_t pad;
+  uint32_t cls2;             // composed class rows: 1 + the request's second class (0: none), see below
 };
+// Composed class rows (candidates.py "composed" level): a request whose role associations name
+// two roles some target requires carries the classes of (entity, action, role a) and (entity,
+// action, role b); its filter is the OR of the two rows and its target verdicts are the OR of
+// their known-true sections and the AND of their known-false sections.  Both rows are built with
+// the role-relaxed useful sections that make the OR exact-or-wider (candidates.py).
 
 // Extension record geometry (u32 words) of a request with the given counts.
 struct ExtGeom {

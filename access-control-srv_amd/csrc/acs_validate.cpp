@@ -110,6 +110,21 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
       return bad("batch: candidate row layout", b->cand_words);
     if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
   }
+  // the encoder's coherence order: every request exactly once, holes 0xFFFFFFFF (the kernels
+  // skip an index >= n; a request missing from it would leave its record unwritten)
+  if (b->perm) {
+    if (b->perm_lanes < n || b->perm_lanes > 0xFFFFFFFFull) return bad("batch: perm_lanes", b->perm_lanes);
+    std::vector<uint8_t> seen(n, 0);
+    size_t got = 0;
+    for (size_t x = 0; x < b->perm_lanes; ++x) {
+      const uint32_t i = b->perm[x];
+      if (i == 0xFFFFFFFFu) continue;
+      if (i >= n || seen[i]) return bad("batch: perm (an index outside the batch, or twice)", x);
+      seen[i] = 1;
+      ++got;
+    }
+    if (got != n) return bad("batch: perm misses requests", got);
+  }
   // RES_RX_SAFE on an attribute lets K1 stop early (the clean-below set walk, the final-fold
   // cuts): it claims that no cell of the value's regex-matrix column throws or needs the host.
   // Checked per column once (RX_THROW_TYPE | RX_THROW_SYNTAX | RX_HOST = 4 | 8 | 16).
@@ -162,6 +177,7 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
         want.ar1 = ar[1];
       }
       want.ext = lines[i].ext;  // (an SoA batch reads its rows, not extension records)
+      want.cls2 = lines[i].cls2;  // (a class fact, not a row: checked below)
       if (std::memcmp(&want, &lines[i], sizeof want) != 0) return bad("batch: request line differs from its rows", i);
     }
     auto res_at = [&](uint32_t j) -> ReqRes {
@@ -198,6 +214,11 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
       if ((size_t)tse[3 * e + 2] + 2 * (size_t)ni > used) used = (size_t)tse[3 * e + 2] + 2 * (size_t)ni;
     }
     if (arena_end) arena_end[i] = (uint32_t)(o + used);
+    // composed class rows: a second class needs a valid first one, and no role factor
+    if (lines && lines[i].cls2) {
+      const uint32_t c1 = hd.flags >> RQ_PCOL_SHIFT, c2 = lines[i].cls2 - 1u;
+      if (!b->cand || b->role_key || c1 >= b->cand_rows || c2 >= b->cand_rows) return bad("batch: second class row", i);
+    }
     const uint32_t ent = (hd.flags >> RQ_ENT_SHIFT) & 7u;
     const uint32_t e0 = ent >= 1 && ent <= 6 ? ent - 1 : (uint32_t)QMAX;  // the lone entity attr's slot
     if (compact && e0 < QMAX && e0 >= hd.nres) return bad("batch: entity slot", i);

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Benchmark: isAllowed decisions/sec of the MI355X evaluator (BASELINE.json metric).
 
-A step = the coherence sort + one K1 launch evaluating one full batch of synthetic
-requests that is already resident in HBM.  Default workload: c3 = 10M requests x 10k
-rules, mixed combining algorithms + HR role scoping, the north star's
+A step = one K1 launch evaluating one full batch of synthetic requests that is already
+resident in HBM, in the coherence order the encoder wrote with the batch (the encoder assigns
+every request's class, so it also groups them: no device sort on the step).  Default
+workload: c3 = 10M requests x 10k rules, mixed combining algorithms + HR role scoping, each
+request with 1-2 role associations (half of them two: SURVEY.md §8(d)), the north star's
 10k-rule configuration.  Multi-GPU: one process per GPU; `--gpus N` without a
 torch.distributed environment launches the N ranks itself (torch.distributed.run on
 127.0.0.1, before anything touches the GPU).  Each rank evaluates its own batch against
@@ -28,12 +30,13 @@ import torch  # noqa: E402
 
 WORKLOADS = {
     "c2": ("c2: isAllowed, 1M requests/GPU vs 100 policy sets / 200 policies / 1k rules, flat roles", 1_000_000),
-    "c3": ("c3: isAllowed, 10M requests/GPU vs 10k rules, mixed CAs + HR role scoping (depth-8 org tree)", 10_000_000),
+    "c3": ("c3: isAllowed, 10M requests/GPU vs 10k rules, mixed CAs + HR role scoping (depth-8 org tree), 1-2 "
+           "org-scoped role associations per request (half with two, SURVEY §8(d))", 10_000_000),
+    "c3r1": ("c3r1: the c3 workload with one role association per request (the round-1..3 headline form)",
+             10_000_000),
     "c3adv": ("c3adv: c3-adverse, 1M requests/GPU vs the c3 store with 0.5 % condition rules in the first 20 sets, a "
               "null policy behind a rare set target and ACLs on 10 % of the context resources (no early stop below "
               "the top sets); requests encoded from JSON by the native codec", 1_000_000),
-    "c3r2": ("c3r2: the c3 workload with a second org-scoped role association (and HR subtree) on half of the "
-             "subjects (SURVEY §8(d): 1-2 role associations)", 10_000_000),
     "c4": ("c4: whatIsAllowed, 1M reverse queries/GPU vs 10k rules (c3 store, 30% of rules with properties), "
            "inclusion bitsets over sets|policies|rules + maskedProperty logs", 1_000_000),
     "c5": ("c5: isAllowed, 1M-request batches/GPU vs 1M rules (1,000 sets x 10 policies x 100 rules, c3 rule mix "
@@ -43,7 +46,7 @@ WORKLOADS = {
 
 def make_store(kind):
     from acs_mi355x import synth
-    return {"c2": synth.c2_store, "c3": synth.c3_store, "c3r2": synth.c3_store, "c3adv": synth.c3_adverse_store,
+    return {"c2": synth.c2_store, "c3": synth.c3_store, "c3r1": synth.c3_store, "c3adv": synth.c3_adverse_store,
             "c4": synth.c3_store,
             "c5": synth.c5_store}[kind]()
 
@@ -51,8 +54,8 @@ def make_store(kind):
 def request_kind(kind):
     return "c2" if kind == "c2" else "c3"  # c4 / c5 draw c3-shaped requests (HR context)
 # c3-shaped requests: share of subjects with a second org-scoped role association (§8(d): 1-2);
-# set per config in main() (c3r2: 0.5, the others 0) unless --second-role is given
-SECOND_ROLE = 0.0
+# set per config in main() (0.5; c3r1: 0) unless --second-role is given
+SECOND_ROLE = 0.5
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s
 _T0 = time.time()
 
@@ -219,7 +222,7 @@ def oracle_parity(kind, doc, sb, gpu_dec, cs, fraction, seconds):
     n = sb.batch.n
     want_n = max(1, int(round(fraction * n)))
     idx = np.random.default_rng(1234).permutation(n)[:want_n]
-    chunk = {"c2": 50_000, "c3": 10_000, "c3r2": 10_000, "c3adv": 10_000}.get(kind, 256)
+    chunk = {"c2": 50_000, "c3": 10_000, "c3r1": 10_000, "c3adv": 10_000}.get(kind, 256)
     done = busy = mism = unsup = host = host_both = 0
     wall0 = time.perf_counter()
     while done < len(idx) and busy < seconds and time.perf_counter() - wall0 < 2 * seconds + 30:
@@ -528,7 +531,7 @@ def main():
                          f"{args.gpus}, or run without a torch.distributed environment)")
     if args.selftest:
         return selftest(world, rank)
-    globals()["SECOND_ROLE"] = args.second_role if args.second_role is not None else (0.5 if args.config == "c3r2" else 0.0)
+    globals()["SECOND_ROLE"] = args.second_role if args.second_role is not None else (0.0 if args.config == "c3r1" else 0.5)
     dist = world > 1
     global REHEARSAL
     # ACS_BENCH_REHEARSAL=1: several ranks on ONE GPU over gloo (collectives through host
@@ -690,9 +693,7 @@ def main():
             line["pcie_inclusive"] = pcie
         if shard_check:
             line["rule_shard"] = shard_check
-        if kind == "c3r2":  # each request's (scope, role) x (scope2, role2) forest is its own: no codec forest cache
-            line["end_to_end"] = "not run for c3r2 (see the c3 line)"
-        elif world == 1 and args.e2e_requests and not args.rule_shard:
+        if world == 1 and args.e2e_requests and not args.rule_shard:
             log("end to end: JSON -> native codec -> GPU -> decisions")
             line["end_to_end"] = end_to_end(kind, cs, sb, tables, dec, args.e2e_requests,
                                             max(1, min(16, os.cpu_count() or 1)))
@@ -700,7 +701,7 @@ def main():
             line["rehearsal"] = "gloo, all ranks on one GPU: code-path check, not a measurement"
         if world == 1 and not args.no_cpu_baseline:
             log("oracle parity + CPU baseline (C++ oracle)")
-            frac = args.parity_fraction if kind in ("c2", "c3", "c3r2", "c3adv") else 1000 / n  # c5: 1M rules, 1000 requests
+            frac = args.parity_fraction if kind in ("c2", "c3", "c3r1", "c3adv") else 1000 / n  # c5: 1M rules, 1000 requests
             cb, par = oracle_parity(kind, doc, sb, dec, cs, frac, args.cpu_seconds)
             line["cpu_baseline"] = cb
             line["parity"] = par

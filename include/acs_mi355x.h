@@ -83,6 +83,15 @@ typedef struct {
    * u32 words.  May be NULL when no request needs one. */
   const uint32_t* ext;
   size_t ext_words;
+  /* Optional coherence order, written by the encoder that assigned the classes (it knows every
+   * request's class, so the device does not sort): perm_lanes entries (>= n), each a request
+   * index or 0xFFFFFFFF for a hole that pads a class's run to a 64-lane wave boundary; every
+   * request appears exactly once.  Lane k of the evaluation kernels takes request perm[k];
+   * records are still written in request order.  NULL = the device entry points sort the batch
+   * themselves (ACS_OPT_SORT).  A request line's `cls2` (1 + a second class, csrc/acs_layout.h)
+   * composes its filter from two class rows. */
+  const uint32_t* perm;
+  size_t perm_lanes;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */
@@ -189,10 +198,11 @@ int acs_shard_keys_device(acs_tables* t, const acs_decision* dev_dec, size_t n, 
                           uint64_t* dev_keys, void* stream);
 int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* dev_out, void* stream);
 
-/* Options.  ACS_OPT_SORT (default 1): before evaluating, the device entry points
- * order the batch by request class (entity, roles, action; + role key with a role factor)
- * with an LSD radix sort so that every wave shares its table-driven branches; results are
- * written in input order. */
+/* Options.  ACS_OPT_SORT (default 1): evaluate in coherence order — the batch's own `perm`
+ * (the encoder's class order) when it carries one, else the device entry points order the
+ * batch by request class (entity, roles, action; + role key with a role factor) with a
+ * counting / LSD radix sort — so that every wave shares its table-driven branches; results
+ * are written in input order.  0: input order. */
 #define ACS_OPT_SORT 1
 /* ACS_OPT_TIMING: record HIP events on the launch stream around every eval kernel (K1 of
  * acs_is_allowed_device, K2 of acs_what_is_allowed_device); acs_kernel_times returns the durations (ms) of the last n

@@ -261,24 +261,29 @@ def test_native_compiler_fixtures_and_configs_byte_identical():
 
 
 def _request_rows(b):
-    """Per request: (class row bytes or None, role-factor row bytes or None)."""
+    """Per request: (class row bytes or None, its second class row (composed rows) or None,
+    role-factor row bytes or None) — the rows as a set: which of two rows is first is the
+    batch's class order."""
     cls = (b.hdr["flags"] >> np.uint32(16)).astype(np.int64)
+    cls2 = b.lines["cls2"].astype(np.int64)
     out = []
     for i in range(b.n):
         c = b.cand[cls[i]].tobytes() if b.cand is not None and cls[i] < b.cand.shape[0] else None
+        c2 = b.cand[cls2[i] - 1].tobytes() if cls2[i] else None
         r = None
         if b.role_key is not None and b.role_key[i] < b.role_bits.shape[0]:
             r = b.role_bits[b.role_key[i]].tobytes()
-        out.append((c, r))
+        out.append((frozenset(x for x in (c, c2) if x is not None), r))
     return out
 
 
-@pytest.mark.parametrize("level", [0, 1, 2])
+@pytest.mark.parametrize("level", [0, 1, 2, 3])
 def test_codec_class_rows_match_python_at_every_level(level, monkeypatch):
     """The codec's class rows (with the useful sections) and role-factor rows equal the Python
-    candidates' for every request, at each key level (level 1 and 2 carry a role factor)."""
+    candidates' for every request, at each key level (level 1 composes per-role rows, levels 2
+    and 3 carry a role factor)."""
     from acs_mi355x import candidates
-    names = ["entity+roles+action", "entity+action", "entity"]
+    names = list(candidates.LEVELS)
     cases = [(FULL_URNS, store.populate(synth.c3_store(n_sets=40)), None)]
     for s in range(0, 60, 6):
         urns, doc, reqs = randgen.rand_case(s)
@@ -290,7 +295,7 @@ def test_codec_class_rows_match_python_at_every_level(level, monkeypatch):
         except Exception:
             continue
         if reqs is None:
-            sb = synth.requests(cs, 3000, "c3", seed=11, tree=synth.OrgTree(fanout=3, depth=5))
+            sb = synth.requests(cs, 3000, "c3", seed=11, tree=synth.OrgTree(fanout=3, depth=5), second_role=0.5)
             reqs = [sb.decode(i) for i in range(sb.batch.n)]
         monkeypatch.setattr(candidates, "FORCE_LEVEL", names[level])
         pb = encoder.Encoder(cs).encode(reqs)
@@ -336,3 +341,26 @@ def test_parallel_delimiter_matches_serial():
             assert np.array_equal(shape(many), shape(one))
             assert many.host_reasons == one.host_reasons
             assert np.array_equal(host_core.is_allowed(cs, many, compact=True).view(np.uint64), want)
+
+
+def test_codec_hrs_key_lists_compose_registered_forests():
+    """"$hrs": [k1, k2] names one registered forest per role association; the codec decides
+    such requests exactly as with the concatenated hierarchical_scopes inline (and as the
+    synthetic packer), for one- and two-association subjects."""
+    doc = synth.c3_store(n_sets=40)
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 3000, "c3", seed=9, tree=synth.OrgTree(fanout=3, depth=5), second_role=0.5)
+    codec = NativeCodec(compiler.store_blob(cs))
+    forests = sb.hrs_forests()
+    assert len(forests) < sb.batch.n  # one per (scope, role), shared
+    for k, v in forests.items():
+        codec.set_subject_scopes(k, v)
+    by_ref = codec.encode(sb.json_text(), threads=3)
+    assert not by_ref.host_reasons
+    inline = codec.encode([sb.decode(i) for i in range(sb.batch.n)], threads=3)
+    want = host_core.is_allowed(cs, inline, compact=True).view(np.uint64)
+    assert np.array_equal(host_core.is_allowed(cs, by_ref, compact=True).view(np.uint64), want)
+    assert np.array_equal(host_core.is_allowed(cs, sb.batch).view(np.uint64), want)
+    # a list naming an unregistered forest goes to the host
+    bad = codec.encode(sb.json_text([0]).replace(b'"$hrs":[', b'"$hrs":["nope",'))
+    assert bad.hdr["flags"][0] & L.RQ_HOST

@@ -150,6 +150,50 @@ def test_synthetic_config_gpu(kind, n, sample):
     t.close()
 
 
+@pytest.mark.parametrize("level", [None, "composed"])
+def test_c3_two_role_associations_gpu(level, monkeypatch):
+    """c3 as SURVEY §8(d) specifies it: 1-2 org-scoped role associations per request (half with
+    two, each with its own HR subtree root).  With composed class rows (two per-role rows the
+    kernel ORs, ReqLine.cls2) as with joint rows, the WHOLE batch equals the C++ oracle
+    (hierarchicalScope.ts:155-245 over several grants, accessController.ts:793-823), through the
+    host-buffer and the device-resident entry points, with the encoder's coherence order and
+    with the device sort; whatIsAllowed rows and obligation logs equal the CPU build's."""
+    from acs_mi355x import candidates
+    if level:
+        monkeypatch.setattr(candidates, "FORCE_LEVEL", level)
+    doc = synth.c3_store()
+    cs = compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS)
+    n = 60_000
+    sb = synth.requests(cs, n, "c3", second_role=0.5)
+    two = sb.batch.hdr["nroles"] == 2
+    assert 0.4 < two.mean() < 0.6
+    if level:
+        assert (sb.batch.lines["cls2"] != 0).mean() > 0.3
+    t = gpu_tables(cs)
+    dec = t.is_allowed(sb.batch)
+    ref = host_core.is_allowed(cs, sb.batch)
+    assert np.array_equal(dec.view(np.uint64), ref.view(np.uint64))
+    db = DeviceBatch(sb.batch, 0, compact=True)
+    dev = decisions_from_tensor(is_allowed_device(t, db))
+    assert np.array_equal(dev.view(np.uint64), ref.view(np.uint64))
+    perm, sb.batch.perm = sb.batch.perm, None  # the device's own coherence sort
+    dev2 = decisions_from_tensor(is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True)))
+    sb.batch.perm = perm
+    assert np.array_equal(dev2.view(np.uint64), ref.view(np.uint64))
+    assert coracle_check(doc, cs, sb, dec, np.arange(n)) == n
+    codes = np.bincount(dec["decision"][two], minlength=7)
+    assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
+    m = 6000  # whatIsAllowed on a slice of the same requests
+    sub = synth.requests(cs, m, "c3", second_role=0.5)
+    bits, obl, obl_n, out = t.what_is_allowed(sub.batch)
+    rbits, robl, robl_n, rout = host_core.what_is_allowed(cs, sub.batch)
+    assert np.array_equal(bits, rbits) and np.array_equal(obl_n, robl_n)
+    assert np.array_equal(out.view(np.uint64), rout.view(np.uint64))
+    for i in range(m):
+        assert np.array_equal(obl[i, :min(obl_n[i], L.OBL_MAX)], robl[i, :min(robl_n[i], L.OBL_MAX)]), i
+    t.close()
+
+
 def test_large_store_class_list_gpu():
     """Rows longer than the LDS union (W > 1024 words): waves of up to 4 classes use row
     pointers, mixed waves the LDS class list — both bit-identical to the CPU build."""
