@@ -405,9 +405,9 @@ def _compile_set(b: _Builder, ps) -> _Fragment:
 
 
 def mark_clean_below(sets, pols):
-    """NF_CLEAN_BELOW on every set all of whose predecessors are clean: NF_COND_FREE (no
-    condition rule, no invalid policy combining algorithm), a valid set combining algorithm
-    and no null policy (loop 2a's TypeError).  Depends on the Map order, so it is set on the
+    """NF_CLEAN_BELOW on every set all of whose predecessors are clean, NF_CLEAN on every clean
+    set: NF_COND_FREE (no condition rule, no invalid policy combining algorithm), a valid set
+    combining algorithm and no null policy (loop 2a's TypeError).  Depends on the Map order, so it is set on the
     assembled tables (acs_compiler.cpp does the same after its last set)."""
     if not len(sets):
         return
@@ -417,6 +417,7 @@ def mark_clean_below(sets, pols):
     clean = ((sets["nflags"] & L.NF_COND_FREE) != 0) & (sets["ca"] != L.CA_INVALID) & ~has_null
     below = np.concatenate([[True], np.logical_and.accumulate(clean)[:-1]])
     sets["nflags"] |= np.where(below, np.uint8(L.NF_CLEAN_BELOW), np.uint8(0))
+    sets["nflags"] |= np.where(clean, np.uint8(L.NF_CLEAN), np.uint8(0))
 
 
 def _assemble(b: _Builder, frags: list) -> CompiledStore:

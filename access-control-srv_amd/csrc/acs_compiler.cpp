@@ -20,6 +20,7 @@
 #include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -583,7 +584,7 @@ void configure(Builder& b, const JV* urns, const JV* cas) {
 }
 
 // compiler.mark_clean_below: NF_CLEAN_BELOW on a set when every earlier set is clean
-// (NF_COND_FREE, valid combining algorithm, no null policy)
+// (NF_COND_FREE, valid combining algorithm, no null policy), NF_CLEAN on a clean set
 void mark_clean_below(Builder& b) {
   bool clean_so_far = true;
   for (NodeRec& S : b.sets) {
@@ -591,6 +592,7 @@ void mark_clean_below(Builder& b) {
     bool clean = (S.nflags & NF_COND_FREE) && S.ca != CA_INVALID;
     for (uint32_t p = S.child_begin; p < S.child_end && clean; ++p)
       if (b.pols[p].nflags & NF_NULL) clean = false;
+    if (clean) S.nflags |= NF_CLEAN;
     clean_so_far = clean_so_far && clean;
   }
 }
@@ -774,17 +776,19 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
   *blob_len = 0;
   size_t fresh = 0;
   Builder& b = sb->b;
+  std::vector<Fragment> next(n);
+  std::vector<size_t> from(n, SIZE_MAX);  // next[k] moved out of the previous compile's frags[from[k]]
   try {
     // previous fragments by text hash: an unchanged set is reused as compiled
     std::unordered_multimap<uint64_t, size_t> old;
     for (size_t k = 0; k < sb->frags.size(); ++k) old.emplace(sb->frags[k].h1, k);
     std::vector<bool> taken(sb->frags.size(), false);
-    std::vector<Fragment> next(n);
     for (size_t k = 0; k < n; ++k) {
       if (!sets[k]) {  // the caller's word: set k is the previous compile's set lens[k], unchanged
         const size_t j = lens[k];
         if (j >= sb->frags.size() || taken[j]) fail("unchanged-set index out of range or repeated");
         next[k] = std::move(sb->frags[j]);
+        from[k] = j;
         taken[j] = true;
         continue;
       }
@@ -796,6 +800,7 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
         Fragment& f = sb->frags[it->second];
         if (!taken[it->second] && f.h2 == h2 && f.len == lens[k]) {
           next[k] = std::move(f);
+          from[k] = it->second;
           taken[it->second] = true;
           reused = true;
         }
@@ -831,10 +836,15 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
     g_compile_err = "acs_store_builder_compile: " + e.why;
   } catch (const ParseError& e) {
     g_compile_err = std::string("acs_store_builder_compile: ") + e.what;
+  } catch (const std::exception& e) {
+    g_compile_err = std::string("acs_store_builder_compile: ") + e.what();
   }
   Fragment empty;
   swap_state(b, empty);
-  sb->frags.clear();  // (some fragments may have moved out: the next compile starts afresh)
+  // a failed compile leaves the builder as the last successful one left it: the fragments it
+  // moved out go back (the dictionary only grew), so a caller's unchanged-set indices stay valid
+  for (size_t k = 0; k < n; ++k)
+    if (from[k] != SIZE_MAX) sb->frags[from[k]] = std::move(next[k]);
   acs_internal_set_error(g_compile_err.c_str());
   return -1;
 }

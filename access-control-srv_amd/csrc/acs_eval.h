@@ -1068,6 +1068,9 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   uint32_t s;
   while (sets.next(s)) {
     const NodeRec S = node_at(T, T.sets, s, T.n_sets);
+    // below the deciding set (or an event) only an event can change the record, and a clean
+    // set cannot raise one for a safe request: skip it (the unclean ones below are walked)
+    if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN)) continue;
     uint8_t e2 = EFF_UNDEF, c2 = EC_UNDEF;
     Decision d2{};
     const int o = eval_set(R, F, s, S, safe, &e2, &c2, &d2);

@@ -96,6 +96,7 @@ enum NodeFlags : uint8_t {
                                // combining algorithm, no null policy — so nothing there can
                                // throw or reach a condition for a safe request (K1 walks the
                                // sets last to first and stops at the deciding one)
+  NF_CLEAN = 1u << 7,          // set: itself clean (K1 skips it below the deciding set)
 };
 
 struct NodeRec {

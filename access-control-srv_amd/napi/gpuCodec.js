@@ -112,6 +112,54 @@ function parseRequests(requests) {
   return JSON.parse(typeof requests === 'string' ? requests : Buffer.from(requests).toString('utf8'));
 }
 
+// lodash _.isEmpty for the values a protobuf Any's `value` can hold (Buffer / typed array /
+// string: length; plain object: own keys; anything else: empty)
+function isEmptyValue(v) {
+  if (v === undefined || v === null) return true;
+  if (typeof v === 'string' || Array.isArray(v) || ArrayBuffer.isView(v)) return v.length === 0;
+  if (typeof v === 'object') return Object.keys(v).length === 0;
+  return true;
+}
+
+// unmarshallProtobufAny (src/accessControlService.ts:116-127) as JSON text: null for a nil
+// message or an empty value, else the value's text (the reference JSON.parses it)
+function unmarshalText(x) {
+  if (!x || isEmptyValue(x.value)) return 'null';
+  return x.value.toString();
+}
+
+// The JSON text of the request AccessControlService.isAllowed / whatIsAllowed builds from a
+// gRPC request (accessControlService.ts:62-65, 83-86: {target, context: unmarshallContext(
+// context) or {}}), without parsing the context: its members are protobuf Any messages whose
+// `value` already holds JSON text, which is spliced in as is.  The :106 quirk is kept: every
+// array member becomes _.map(context.resources, unmarshallProtobufAny), of the resources as
+// they are at that point (an array member after `resources` maps the already-unmarshalled
+// resources: those are parsed back for it).  The spliced text must be JSON the reference's
+// JSON.parse accepts: GpuAccessController.isAllowedGrpc re-runs a batch whose text does not
+// parse request by request.
+function grpcRequestJson(request) {
+  const ctx = request.context;
+  let body = '{}';
+  if (ctx) {
+    const done = new Map(); // member -> JSON text of its unmarshalled value
+    for (const prop in ctx) {
+      const x = ctx[prop];
+      if (Array.isArray(x)) {
+        const R = done.has('resources') ? JSON.parse(done.get('resources')) : ctx.resources;
+        const list = Array.isArray(R) ? R : (R && typeof R === 'object' ? Object.values(R) : []);
+        done.set(prop, '[' + list.map(unmarshalText).join(',') + ']');
+      } else {
+        done.set(prop, unmarshalText(x));
+      }
+    }
+    const parts = [];
+    for (const [k, v] of done) parts.push(JSON.stringify(k) + ':' + v);
+    body = '{' + parts.join(',') + '}';
+  }
+  const target = request.target === undefined ? '' : '"target":' + JSON.stringify(request.target) + ',';
+  return '{' + target + '"context":' + body + '}';
+}
+
 const clone = (v) => (v === undefined || v === null || typeof v !== 'object' ? v : JSON.parse(JSON.stringify(v)));
 
 function pick(obj, keys, into) {
@@ -135,8 +183,20 @@ class GpuAccessController {
     this.chunk = o.chunk || 0; // pipeline chunk (requests); 0: the library's default
     this.pipelineBytes = o.pipelineBytes === undefined ? (1 << 20) : o.pipelineBytes; // null: never
     this.compileOnly = !!o.compileOnly; // compile the image only (no device): this.blob
+    // the host edits rule / policy objects in place on the shared Map without the store
+    // handlers or markChanged: every refresh re-serialises every set (the builder still
+    // recompiles only the sets whose JSON text changed)
+    this.mapEditsInPlace = !!o.mapEditsInPlace;
     this.pipeline = null;
     this.hostEvaluator = o.hostEvaluator || null;
+    // micro-batching (SURVEY §8(f) rank 1): single isAllowed / whatIsAllowed calls — one per gRPC
+    // request (accessControlService.ts:62-101) — are gathered over one event-loop turn
+    // (batchWindowMs 0: setImmediate) or a window of batchWindowMs, at most batchMax at a time,
+    // and decided as one batch; each promise resolves to its own Response / ReverseQuery
+    this.batchMax = o.batchMax || 65536;
+    this.batchWindowMs = o.batchWindowMs || 0;
+    this._queues = { isAllowed: [], whatIsAllowed: [] };
+    this._armed = { isAllowed: false, whatIsAllowed: false };
     this.urns = urns instanceof Map ? Object.fromEntries(urns) : urns;
     this.cas = combiningAlgorithms;
     this.stats = { requests: 0, host: 0, compiles: 0 };
@@ -158,9 +218,15 @@ class GpuAccessController {
   // the object it held at the last refresh is passed to the builder as unchanged (neither
   // re-serialised nor recompiled).  Without it every set is re-serialised, and the builder
   // still recompiles only the sets whose JSON text changed.
+  //
+  // A refresh that throws (a set that does not compile, a device failure) leaves the
+  // controller stale: the next batch retries it, and succeeds once the store is fixed.  The
+  // builder keeps the fragments of its last successful compile when a compile fails, and
+  // setIndex always describes the builder's fragments, so the unchanged-set indices passed
+  // to it stay valid either way.
   refresh(policySets, changed) {
     const t0 = Date.now();
-    const dirty = changed ? new Set(changed) : null;
+    const dirty = changed && !this.mapEditsInPlace ? new Set(changed) : null;
     const entries = policySets instanceof Map ? Array.from(policySets.entries())
       : mapValues(policySets).map((ps, k) => [k, ps]);
     const items = new Array(entries.length);
@@ -169,16 +235,18 @@ class GpuAccessController {
       const prev = this.setIndex.get(key);
       items[k] = dirty && prev && prev.obj === ps && !dirty.has(key) ? prev.index : JSON.stringify(snapshotSet(ps));
     }
-    const r = addon.storeBuilderCompile(this.builder, items);
+    this.stale = true;
+    const r = addon.storeBuilderCompile(this.builder, items); // throws: the builder is unchanged
     const blob = r.blob;
+    // the builder now holds this compile's fragments, in this Map order
     const setIndex = new Map();
     for (let k = 0; k < entries.length; ++k) setIndex.set(entries[k][0], { obj: entries[k][1], index: k });
+    this.setIndex = setIndex;
     if (this.compileOnly) { // tooling: the image without a device (no tables / codec / pipeline)
       this.blob = blob;
       this.index = nodeIndex(policySets);
       this.stats.compiles += 1;
       this.policySets = policySets;
-      this.setIndex = setIndex;
       this.dirty = new Set();
       this.stale = false;
       this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
@@ -200,7 +268,6 @@ class GpuAccessController {
     for (const [k, v] of this.scopes) addon.codecSetSubjectScopes(codec, k, v);
     this.stats.compiles += 1;
     this.policySets = policySets;
-    this.setIndex = setIndex;
     this.dirty = new Set();
     this.stale = false;
     this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
@@ -333,8 +400,17 @@ class GpuAccessController {
   // requests: an array of Request objects, or their JSON text.  Resolves to one entry per
   // request: a Response, or an Error (per request, as the reference's promises would reject).
   async isAllowedBatch(requests) {
-    this._sync();
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
+    let parsed = null;
+    return this._isAllowedText(text, (i) => {
+      if (parsed === null) parsed = parseRequests(requests);
+      return parsed[i];
+    });
+  }
+
+  // The JSON array `text` of requests; request(i): request i as an object (host-path requests).
+  async _isAllowedText(text, request) {
+    this._sync();
     const ec = this.ec; // the codec's table: refresh() may swap this.ec while the batch is in flight
     const bytes = typeof text === 'string' ? text.length : text.byteLength;
     const r = this.pipeline && bytes >= this.pipelineBytes
@@ -344,12 +420,10 @@ class GpuAccessController {
     this.stats.requests += n;
     const out = new Array(n);
     const pending = [];
-    let parsed = null;
     for (let i = 0; i < n; ++i) {
       const v = this._response(r.records, i, r.host[i], ec);
       if (v instanceof HostPathRequired) {
-        if (parsed === null) parsed = parseRequests(requests);
-        pending.push(this._host('isAllowed', parsed[i], v).then((x) => { out[i] = x; }));
+        pending.push(this._host('isAllowed', request(i), v).then((x) => { out[i] = x; }));
       } else {
         out[i] = v;
       }
@@ -358,10 +432,76 @@ class GpuAccessController {
     return out;
   }
 
-  async isAllowed(request) {
-    const r = (await this.isAllowedBatch([request]))[0];
-    if (r instanceof Error) throw r;
-    return r;
+  // AccessController.isAllowed (accessController.ts:88-324) for one request, micro-batched with
+  // the concurrent calls (batchWindowMs / batchMax): resolves to its Response or rejects with
+  // the error the reference's promise would.
+  isAllowed(request) {
+    return this._enqueue('isAllowed', request, null);
+  }
+
+  // AccessControlService.isAllowed (accessControlService.ts:62-81) for a gRPC request whose
+  // context members are protobuf Any messages: their JSON text goes to the codec as is
+  // (grpcRequestJson), micro-batched like isAllowed().
+  isAllowedGrpc(grpcRequest) {
+    return this._enqueue('isAllowed', null, grpcRequestJson(grpcRequest));
+  }
+
+  whatIsAllowedGrpc(grpcRequest) {
+    return this._enqueue('whatIsAllowed', null, grpcRequestJson(grpcRequest));
+  }
+
+  _enqueue(op, request, text) {
+    return new Promise((resolve, reject) => {
+      const q = this._queues[op];
+      q.push({ request, text, resolve, reject });
+      if (q.length >= this.batchMax) {
+        this._flush(op);
+      } else if (!this._armed[op]) {
+        this._armed[op] = true;
+        const go = () => {
+          this._armed[op] = false;
+          this._flush(op);
+        };
+        if (this.batchWindowMs > 0) setTimeout(go, this.batchWindowMs);
+        else setImmediate(go);
+      }
+    });
+  }
+
+  // Decide the queued calls of `op` as one batch.  A batch whose text the codec rejects (a
+  // gRPC context value that is not JSON) is re-run without the requests whose text does not
+  // parse; those reject with the SyntaxError the reference's JSON.parse throws.
+  _flush(op) {
+    const items = this._queues[op];
+    if (!items.length) return;
+    this._queues[op] = [];
+    const texts = items.map((x) => (x.text !== null ? x.text : JSON.stringify(x.request)));
+    const request = (i) => (items[i].request !== null ? items[i].request : JSON.parse(items[i].text));
+    const text = '[' + texts.join(',') + ']';
+    const run = op === 'isAllowed' ? this._isAllowedText(text, request)
+      : this.whatIsAllowedBatch(text, request);
+    run.then((out) => {
+      for (let i = 0; i < items.length; ++i) {
+        if (out[i] instanceof Error) items[i].reject(out[i]);
+        else items[i].resolve(out[i]);
+      }
+    }, (err) => {
+      const ok = [];
+      for (const it of items) {
+        try {
+          if (it.text !== null) JSON.parse(it.text);
+          ok.push(it);
+        } catch (e) {
+          it.reject(e);
+        }
+      }
+      if (ok.length === items.length) { // not a text problem: the batch failed as a whole
+        for (const it of items) it.reject(err);
+        return;
+      }
+      this._queues[op] = ok.concat(this._queues[op]);
+      this._flush(op);
+    });
   }
 
   // maskedProperty push log -> obligations (find by entity value, else append;
@@ -456,18 +596,25 @@ class GpuAccessController {
 
   // Batch whatIsAllowed (encode + kernels on the calling thread; host-path requests then go
   // to the host evaluator).  Resolves to one entry per request: a ReverseQuery or an Error.
-  async whatIsAllowedBatch(requests) {
+  // request(i) (optional): request i as an object, for the host path (default: parsed from
+  // `requests`).
+  async whatIsAllowedBatch(requests, request) {
     this._sync();
     const text = typeof requests === 'string' || requests instanceof Uint8Array ? requests : JSON.stringify(requests);
+    let parsed = null;
+    const req = request || ((i) => {
+      if (parsed === null) parsed = parseRequests(requests);
+      return parsed[i];
+    });
     const batch = addon.encode(this.codec, text, this.threads);
     try {
-      return await this._whatIsAllowedEncoded(batch, requests);
+      return await this._whatIsAllowedEncoded(batch, req);
     } finally {
       addon.batchFree(batch);
     }
   }
 
-  async _whatIsAllowedEncoded(batch, requests) {
+  async _whatIsAllowedEncoded(batch, request) {
     const info = addon.batchInfo(batch);
     const w = addon.whatIsAllowed(this.tables, batch);
     const words = addon.wordsPerRequest(this.tables);
@@ -482,7 +629,6 @@ class GpuAccessController {
     const long = flagged.length ? this._resolveOverflow(batch, flagged) : new Map();
     const out = new Array(info.n);
     const pending = [];
-    let parsed = null;
     for (let i = 0; i < info.n; ++i) {
       const flags = w.out[i * REC_BYTES + 2] & (long.has(i) ? ~OF_OBL_OVERFLOW : 0xff);
       let err = null;
@@ -493,9 +639,8 @@ class GpuAccessController {
           : new GpuEvaluationError(ERR_KINDS[e] || 'Error');
       } else if (flags & OF_OBL_OVERFLOW) err = new HostPathRequired('maskedProperty log overflow');
       if (err instanceof HostPathRequired) {
-        if (parsed === null) parsed = parseRequests(requests);
         const at = i;
-        pending.push(this._host('whatIsAllowed', parsed[i], err).then((x) => { out[at] = x; }));
+        pending.push(this._host('whatIsAllowed', request(i), err).then((x) => { out[at] = x; }));
         continue;
       }
       if (err) {
@@ -515,11 +660,12 @@ class GpuAccessController {
     return out;
   }
 
-  async whatIsAllowed(request) {
-    const r = (await this.whatIsAllowedBatch([request]))[0];
-    if (r instanceof Error) throw r;
-    return r;
+  // AccessController.whatIsAllowed (accessController.ts:326-427) for one request,
+  // micro-batched like isAllowed().
+  whatIsAllowed(request) {
+    return this._enqueue('whatIsAllowed', request, null);
   }
 }
 
-module.exports = { GpuAccessController, HostPathRequired, GpuEvaluationError, snapshotStore, nodeIndex, addon };
+module.exports = { GpuAccessController, HostPathRequired, GpuEvaluationError, snapshotStore, nodeIndex,
+                   grpcRequestJson, addon };

@@ -70,6 +70,37 @@ const enc = (x) => (x instanceof Error ? { $error: x.name, reason: x.reason } : 
     const ia = await ctl.isAllowedBatch(c.isAllowed);
     const wa = await ctl.whatIsAllowedBatch(c.whatIsAllowed);
     const res = { isAllowed: ia.map(enc), whatIsAllowed: wa.map(enc), stats: ctl.stats };
+    {  // single calls, micro-batched (one event-loop turn), and the same requests as gRPC
+       // messages (context members as protobuf Any with JSON values): the same answers
+      const settle = (p) => p.then((x) => x, (e) => e);
+      const ia1 = await Promise.all(c.isAllowed.map((r) => settle(ctl.isAllowed(r))));
+      const wa1 = await Promise.all(c.whatIsAllowed.map((r) => settle(ctl.whatIsAllowed(r))));
+      // a request as the gRPC message it came from: context members as protobuf Any (resources a
+      // repeated Any); requests without an object context (the service would pass {}, not what
+      // the controller got) go as they are
+      const grpcable = (r) => r && typeof r === 'object' && r.context && typeof r.context === 'object' &&
+        !Array.isArray(r.context);
+      const grpc = (r) => {
+        const ctx = r.context;
+        const out = { target: r.target };
+        if (ctx) {
+          out.context = {};
+          const anyOf = (x) => ({ type_url: 't', value: Buffer.from(JSON.stringify(x)) });
+          for (const k of Object.keys(ctx)) {
+            const v = ctx[k];
+            if (v === undefined) continue;
+            out.context[k] = k === 'resources' && Array.isArray(v) ? v.map((x) => (x === undefined ? null : anyOf(x)))
+              : anyOf(v);
+          }
+        }
+        return out;
+      };
+      const ia2 = await Promise.all(c.isAllowed.map((r) => settle(grpcable(r) ? ctl.isAllowedGrpc(grpc(r))
+        : ctl.isAllowed(r))));
+      res.microSame = JSON.stringify(ia1.map(enc)) === JSON.stringify(res.isAllowed) &&
+        JSON.stringify(wa1.map(enc)) === JSON.stringify(res.whatIsAllowed);
+      res.grpcSame = JSON.stringify(ia2.map(enc)) === JSON.stringify(res.isAllowed);
+    }
     {  // the same requests through the decision pipeline (3-request chunks) on a handle
        // replicated twice on device 0: the same answers
       const opts2 = Object.assign({}, opts, { pipelineBytes: 0, chunk: 3, device: [0, 0] });

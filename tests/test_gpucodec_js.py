@@ -54,6 +54,7 @@ def _run(tmp, cases, mode, timeout=600):
     if mode == "decide":  # every case also ran through the pipeline on a two-replica handle
         for k, res in enumerate(out):
             assert "compileError" in res or (res["pipelineSame"] and res["devices"] == [0, 0]), k
+            assert "compileError" in res or (res["microSame"] and res["grpcSame"]), k
     return out
 
 
