@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Where K1's time goes: per-phase lane-cycles from the -DACS_PHASE_PROF build.
 
-usage: python tools/phase_prof.py [c2|c3|c5] [requests]
+usage: python tools/phase_prof.py [c2|c3|c5] [requests] [second_role]
 Prints, per phase, the share of lane-cycles inside is_allowed_t (set targets, the
 exact-policy scan, multi-entity check, policy targets, rule targets, HR, ACL; the
 rest is iteration / bookkeeping) and the kernel time of the profiling build.
@@ -27,15 +27,16 @@ PHASES = ["total", "set_target", "pol_exact_scan", "multi_entity", "pol_target",
 def main():
     kind = sys.argv[1] if len(sys.argv) > 1 else "c2"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+    second = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
     lib_path = build.build_prof()
     lib = native.load(lib_path)
     lib.acs_phase_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     mk = {"c2": synth.c2_store, "c3": synth.c3_store, "c5": synth.c5_store}[kind]
     cs = compiler.compile_store(store.populate(mk()), FULL_URNS, DEFAULT_CAS)
-    sb = synth.requests(cs, n, "c2" if kind == "c2" else "c3")
+    sb = synth.requests(cs, n, "c2" if kind == "c2" else "c3", second_role=second)
     t = native.Tables(compiler.store_blob(cs), 0)
     t.set_timing(True)
-    db = DeviceBatch(sb.batch, 0)
+    db = DeviceBatch(sb.batch, 0, compact=True)
     out = torch.empty((n, 8), dtype=torch.uint8, device="cuda")
     is_allowed_device(t, db, out)
     torch.cuda.synchronize()
@@ -48,7 +49,7 @@ def main():
     lib.acs_phase_read(acc, 16)
     v = np.array(acc[:len(PHASES)], np.float64)
     tot = v[0]
-    res = {"config": kind, "requests": n, "kernel_ms": float(np.mean(t.kernel_times(steps))),
+    res = {"config": kind, "requests": n, "second_role": second, "kernel_ms": float(np.mean(t.kernel_times(steps))),
            "lane_cycles_per_request": tot / (n * steps),
            "share": {p: float(v[k] / tot) for k, p in enumerate(PHASES) if k}}
     res["share"]["iteration_other"] = 1.0 - sum(res["share"].values())
