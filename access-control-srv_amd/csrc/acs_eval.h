@@ -65,6 +65,26 @@ struct Tables {
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
+  uint32_t se0;      // the most common roleScopingEntity of the targets (hr_owner_bits' memo key)
+};
+
+// The roleScopingEntity most targets carry (hr_owner_bits memoises checkHierarchicalScope's
+// owner tests for it): a Boyer-Moore majority vote over the nodes' non-empty `se` (the majority
+// when there is one, some frequent value otherwise: any value is correct, the memo just hits
+// less).  Feed every node with add(), read .value.
+struct ScopingEntityVote {
+  uint32_t value = ID_UNDEF, count = 0;
+  ACS_FN void add(uint32_t se) {
+    if (se <= ID_EMPTY) return;
+    if (count == 0) {
+      value = se;
+      count = 1;
+    } else if (se == value) {
+      ++count;
+    } else {
+      --count;
+    }
+  }
 };
 
 #if defined(ACS_SCAN_COUNT)
@@ -370,6 +390,7 @@ struct ReqCtx {
   // instead of being held as six pointers and six counts: K1's per-lane state stays small.
   uint32_t c0, c1;  // arena counts: [0] grants | rolese<<8 | slots<<16 | roots<<24, [1] tse | hrkeys<<8
   uint32_t ext;     // compact batch: 1 + 16-B unit offset of the extension record (0: none)
+  mutable uint32_t hrm;  // hr_owner_bits memo: [7:0] its context slot (0xFF: none yet), 3 bits per role
   bool soa;         // the rows past the line are SoA rows (else the extension record); false as a
                     // constant in the compact-batch kernels, so their SoA paths compile away
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
@@ -380,7 +401,7 @@ struct ReqCtx {
   // ln: the request's packed line (acs_layout.h ReqLine), nullptr: the SoA rows
   ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr,
                 bool soa_ok = true)
-      : T(t), B(b), i(idx), h(hd) {
+      : T(t), B(b), i(idx), h(hd), hrm(0xFFu) {
     soa = soa_ok && B.hdr != nullptr;
     if (ln || !soa_ok) {
       ext = ln->ext;
@@ -743,9 +764,35 @@ ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) 
   return false;
 }
 
+#ifndef ACS_AB_TIMING_NO_HR  // timing-only A/B builds: checkHierarchicalScope always true (wrong records)
+#define ACS_AB_TIMING_NO_HR 0
+#endif
+// The owner tests of checkHierarchicalScope for one context slot: bit 0 the direct owner <->
+// grant match (hierarchicalScope.ts:165-191), bit 1 the HR-tree match (:199-245, only when not
+// direct).  Both read the request's arena (grants, role-scoping pairs, roots, the slot's owner
+// records) and are pure in (slot, role, se), so a lane memoises them (ReqCtx::hrm) for its first
+// slot, the tables' common scoping entity T.se0 and the values of its first two role
+// associations: every candidate rule after the first of a role reuses the outcome instead of
+// re-reading the arena.
+ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
+  const uint32_t ms = R.hrm & 0xFFu;
+  uint32_t k = 2;
+  if (se == R.T.se0 && (ms == 0xFFu || ms == slot)) k = role == R.role0 ? 0u : (role == R.role1 ? 1u : 2u);
+  if (k < 2) {
+    const uint32_t sh = 8 + 3 * k;
+    if ((R.hrm >> sh) & 1u) return (R.hrm >> (sh + 1)) & 3u;
+    const uint32_t d = hr_direct(R, slot, role, se) ? 1u : 0u;
+    const uint32_t b = d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
+    R.hrm = (R.hrm & ~(0xFFu | (7u << sh))) | slot | ((1u | (b << 1)) << sh);
+    return b;
+  }
+  const uint32_t d = hr_direct(R, slot, role, se) ? 1u : 0u;
+  return d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
+}
+
 template <class RQ>
 ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
-  if (t.tflags & TF_HR_TRIVIAL) return 1;
+  if (ACS_AB_TIMING_NO_HR || (t.tflags & TF_HR_TRIVIAL)) return 1;
   if (R.flag(RQ_CTX_EMPTY)) return 0;
   bool all_direct = true, all_ok = true;
   const RuleResAttr* ra = R.T.rres + t.res_off;
@@ -770,9 +817,9 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
           const uint32_t slot = q.slot_a;
           if (slot == NONE8) return 0;
           if (slot_rec(R, slot)[0]) return 0;  // owners missing
-          const bool d = hr_direct(R, slot, t.role, t.se);
-          all_direct = all_direct && d;
-          all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
+          const uint32_t b = hr_owner_bits(R, slot, t.role, t.se);
+          all_direct = all_direct && (b & 1u);
+          all_ok = all_ok && b != 0u;
         }
       }
     } else if (r.kind & K_OP) {
@@ -782,9 +829,9 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
         const uint32_t slot = q.slot_b;
         if (slot == NONE8) return 0;
         if (slot_rec(R, slot)[0]) return 0;
-        const bool d = hr_direct(R, slot, t.role, t.se);
-        all_direct = all_direct && d;
-        all_ok = all_ok && (d || hr_tree(R, slot, t.role, t.se));
+        const uint32_t b = hr_owner_bits(R, slot, t.role, t.se);
+        all_direct = all_direct && (b & 1u);
+        all_ok = all_ok && b != 0u;
       }
     }
   }
