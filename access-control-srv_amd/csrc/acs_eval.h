@@ -961,11 +961,20 @@ ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
 // One policy set of isAllowed (the body of accessController.ts:125-295's set loop): no
 // effect, an effect (sf's eff / ec), or an event that ends the request there (an error the
 // reference throws, or a reached rule condition: the record in *ev).
+//
+// events_only: the set lies below the deciding set (or an event) and the request is safe, so
+// only an event it raises can still change the record (is_allowed_body).  For a safe request
+// only three things raise one: a null policy in loop 2a, a reached rule condition and an
+// invalid combining algorithm with a push.  So loop 2b skips the policies that have neither a
+// condition rule nor an invalid algorithm (NF_COND_FREE, valid ca), and in a policy with a
+// valid algorithm visits only its condition rules (a rule without one cannot raise an event,
+// and reaching a condition does not depend on the rules before it).  Sets with an invalid
+// algorithm are never evaluated this way (their event depends on any push).
 enum SetOutcome { SET_NONE = 0, SET_EFFECT = 1, SET_EVENT = 2 };
 
 template <class RQ, class FL>
-ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool safe, uint8_t* eff, uint8_t* ec,
-                    Decision* ev) {
+ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool safe, bool events_only,
+                    uint8_t* eff, uint8_t* ec, Decision* ev) {
   const Tables& T = R.T;
   const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
   if (S.nflags & NF_HAS_TARGET) {
@@ -1011,6 +1020,8 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   while (pols.next(p)) {
     const NodeRec P = node_at(T, T.pols, p, T.n_pols);
     if (P.nflags & NF_NULL) continue;
+    if (events_only && (P.nflags & NF_COND_FREE) && P.ca != CA_INVALID) continue;  // raises no event
+    const bool cond_rules_only = events_only && P.ca != CA_INVALID;
     bool psm = true;
     if (P.nflags & NF_HAS_TARGET) {
       PROF_T0(tp);
@@ -1042,6 +1053,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     while (rules.next(r)) {
       const NodeRec Q = rule_at(T, r);
       if (Q.nflags & NF_NULL) continue;
+      if (cond_rules_only && !(Q.nflags & NF_HAS_CONDITION)) continue;
       tri m = 1;
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
@@ -1120,7 +1132,8 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN)) continue;
     uint8_t e2 = EFF_UNDEF, c2 = EC_UNDEF;
     Decision d2{};
-    const int o = eval_set(R, F, s, S, safe, &e2, &c2, &d2);
+    const bool events_only = (have_ev || last_set) && safe && S.ca != CA_INVALID;
+    const int o = eval_set(R, F, s, S, safe, events_only, &e2, &c2, &d2);
     if (o == SET_EVENT) {
       ev = d2;  // lower than any event found so far
       have_ev = true;
