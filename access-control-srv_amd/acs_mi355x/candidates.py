@@ -580,9 +580,9 @@ def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
     n = len(cls)
     c = cls.astype(np.int64)
     bucket = np.where(c < cand_rows, c + 1, 0)
-    if role_key is not None:
-        rk = np.minimum(role_key.astype(np.int64), 0xFFFF)
-        key = (rk << 17) | bucket
+    if role_key is not None:  # role-major: [role row | second role row | bucket]
+        rk = role_key.astype(np.int64)
+        key = (((rk & 0xFFFF) << 16 | rk >> 16) << 17) | bucket
         pad = False
     else:
         key = (bucket << 17) | cls2.astype(np.int64)
@@ -603,21 +603,48 @@ def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
 
 
 def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr_any, pol_static, set_null):
-    """Role factor for class rows keyed without roles (large stores): one row per distinct
-    role-association set of the batch — the nodes a request holding those roles can reach
-    through checkSubjectMatches (accessController.ts:797-806), and the sets / policies
-    useful through those nodes — and each request's row index (0xFFFF: no role filtering).
-    The kernel ANDs it with the class row; both are supersets of the joint filter, so their
-    AND is too."""
+    """Role factor for class rows keyed without roles (large stores): the nodes a request's
+    role associations let through checkSubjectMatches (accessController.ts:797-806) and the
+    sets / policies useful through them, AND-ed by the kernel with the class row; both are
+    supersets of the joint filter, so their AND is too.
+
+    One row per required role (and one for "no required role"), built role-relaxed like the
+    composed class rows (module docstring): a request with two required roles ORs its two rows,
+    one with more gets a row of its whole role set.  role_key[i] = row | (1 + second row) << 16
+    (the high half 0: one row; 0xFFFF low: no role filtering).  Returns (role_key, rows) or
+    (None, None) when the rows would not fit."""
     W = row_layout(cs)[4]
     n = len(rs)
-    rkey = np.full(n, 0xFFFF, np.uint32)
-    keys, inv = _unique_rows(rs[active])
+    nused = (rs >= 0).sum(axis=1)
+    desc = rs[:, ::-1]  # largest role rows first, -1 padding last
+    width = max(int(nused.max()) if n else 0, 1)
+    # keys: one role row (or none) per request, the whole set past two roles; second keys
+    prim = np.full((n, width), -1, np.int64)
+    prim[:, 0] = desc[:, 0]
+    big = nused > 2
+    prim[big] = desc[big, :width]
+    act_idx = np.flatnonzero(active)
+    two = np.flatnonzero(active & (nused == 2))
+    sec = np.full((len(two), width), -1, np.int64)
+    if len(two):
+        sec[:, 0] = desc[two, 1]
+    keys, inv = _unique_rows(np.concatenate([prim[act_idx], sec]))
     if len(keys) == 0 or len(keys) * W * 4 > _ROLE_ROW_BYTES or len(keys) >= 0xFFFF:
         return None, None
-    rkey[active] = inv.astype(np.uint32)
+    kid = inv.astype(np.int64)
+    rkey = np.full(n, 0xFFFF, np.uint32)
+    rkey[act_idx] = kid[:len(act_idx)].astype(np.uint32)
+    if len(two):
+        a_, b_ = rkey[two].astype(np.int64), kid[len(act_idx):]
+        lo, hi = np.minimum(a_, b_), np.maximum(a_, b_)
+        rkey[two] = (lo | np.where(lo == hi, 0, hi + 1) << 16).astype(np.uint32)
     out = np.zeros((len(keys), W), np.uint32)
     chunk = max(8, min(_CHUNK, _CHUNK_NODE_BITS // max(1, cs.n_sets + cs.n_pols + cs.n_rules)))
+    p_free = np.ones((1, cs.n_pols), bool)
+    if cs.n_pols:
+        s_free = nonempty[None, :]  # every set with policies (its policies role-free)
+    else:
+        s_free = np.zeros((1, cs.n_sets), bool)
     for c0 in range(0, len(keys), chunk):
         ck = keys[c0:c0 + chunk]
         M = np.zeros((len(ck), nrr + 1), bool)
@@ -630,18 +657,17 @@ def _role_factor(cs, rs, active, req_rows, nrr, b_s, e_s, nonempty, thr_any, pol
         def role_ok(rr):
             return M[:, np.where(rr >= 0, rr, nrr)]
 
-        s, p, r = role_ok(req_rows[0]), role_ok(req_rows[1]), role_ok(req_rows[2])
-        if cs.n_pols:
-            cum = np.concatenate([np.zeros((len(ck), 1), np.int64), np.cumsum(p, axis=1)], axis=1)
-            s = s & ((cum[:, e_s] - cum[:, b_s]) > 0) & nonempty[None, :]
-        # useful sections from the role side alone (rules the roles reach; a policy that may
-        # throw for any column of the batch stays): AND-ed with the class row's useful
-        # sections (entity + action side) the kernel keeps a superset of the joint ones
-        us, up = _useful(cs, s, p, r, thr_any[None, :], pol_static, set_null)
+        p, r = role_ok(req_rows[1]), role_ok(req_rows[2])
+        s_ = np.broadcast_to(s_free, (len(ck), cs.n_sets))
+        # role-relaxed useful sections: a policy that may throw for some column of the batch, or
+        # is useful wherever it is a candidate, stays; one with a rule the roles reach is useful
+        # whatever its own role test (composable: OR over the request's role rows)
+        us, up = _useful_relaxed(cs, s_, p, np.broadcast_to(p_free, p.shape), r, thr_any[None, :], pol_static,
+                                 set_null)
         # the verdict sections are the class row's: the role side keeps them (all nodes)
         ap = np.ones((len(ck), cs.n_pols), bool)
         ar = np.ones((len(ck), cs.n_rules), bool)
-        out[c0:c0 + len(ck)] = _assemble(s, p, us, up, r, cs, (ap, ap, ap, ap, ar))
+        out[c0:c0 + len(ck)] = _assemble(s_, p, us, up, r, cs, (ap, ap, ap, ap, ar))
     return rkey, out
 
 

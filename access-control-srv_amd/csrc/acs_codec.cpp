@@ -2205,23 +2205,51 @@ void Classes::run() {
     }
     finish(cls);
     if (role_filter || !have_roles) return;
-    // role factor (candidates._role_factor): one row per distinct role set of the active
-    // requests, cached by (role set, the batch's may-throw policies)
+    // role factor (candidates._role_factor): role-relaxed rows like the composed level's, one per
+    // required role (and one for "no required role"; a request with more than two roles: one
+    // of its whole role set), cached by (roles, the batch's may-throw policies).  role_key:
+    // row | (1 + second row) << 16 for a request with two required roles
     std::unordered_map<std::string, uint32_t> sidx;
-    std::vector<uint32_t> set_first;
+    std::vector<std::pair<uint32_t, int>> key_roles;  // (request, 0 all / 1 largest / 2 second)
     std::vector<uint32_t> rkey(n, 0xFFFFu);
     std::string kb;
-    for (uint32_t i = 0; i < n; ++i) {
-      if (!active[i]) continue;
-      kb.assign((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+    auto role_span = [&](uint32_t i, int which, int* m) -> const int32_t* {
+      const int32_t* r = &rs[(size_t)i * RW];
+      const int k = nrs[i];
+      if (which == 0 || k > 2) {
+        *m = k;
+        return r;
+      }
+      if (k == 0) {
+        *m = 0;
+        return r;
+      }
+      *m = 1;
+      return which == 1 ? r + (k - 1) : r + (k - 2);
+    };
+    auto key_id = [&](uint32_t i, int which) -> uint32_t {
+      int m;
+      const int32_t* r = role_span(i, which, &m);
+      kb.assign((const char*)r, 4 * (size_t)m);
       auto it = sidx.find(kb);
       if (it == sidx.end()) {
-        it = sidx.emplace(kb, (uint32_t)set_first.size()).first;
-        set_first.push_back(i);
+        it = sidx.emplace(kb, (uint32_t)key_roles.size()).first;
+        key_roles.emplace_back(i, which);
       }
-      rkey[i] = it->second;
+      return it->second;
+    };
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!active[i]) continue;
+      const uint32_t a = key_id(i, nrs[i] > 2 ? 0 : 1);
+      rkey[i] = a;
+      if (nrs[i] == 2) {
+        const uint32_t b = key_id(i, 2);
+        const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+        rkey[i] = lo | (lo == hi ? 0u : (hi + 1u) << 16);
+      }
     }
-    if (set_first.empty() || set_first.size() * W * 4 > ROLE_ROW_BYTES || set_first.size() >= 0xFFFF) return;
+    const size_t nkr = key_roles.size();
+    if (nkr == 0 || nkr * W * 4 > ROLE_ROW_BYTES || nkr >= 0xFFFF) return;
     // the role side's useful sections keep every policy that may throw for some column
     Row thr_any(C.wp ? C.wp : 1, 0u);
     for (uint32_t c = 0; c < ncols; ++c) {
@@ -2231,15 +2259,16 @@ void Classes::run() {
         for (uint32_t w = 0; w < thr_any.size(); ++w) thr_any[w] |= (*tr)[w];
     }
     const std::string thr_key((const char*)thr_any.data(), thr_any.size() * 4);
-    B.role_bits.assign(set_first.size() * W, 0u);
-    std::vector<std::shared_ptr<const std::vector<uint32_t>>> rrow(set_first.size());
+    B.role_bits.assign(nkr * W, 0u);
+    std::vector<std::shared_ptr<const std::vector<uint32_t>>> rrow(nkr);
     std::vector<uint32_t> rmiss;
-    std::vector<std::string> rkeys(set_first.size());
+    std::vector<std::string> rkeys(nkr);
     {
       std::shared_lock<std::shared_mutex> lock(C.classes.mu);
-      for (size_t k = 0; k < set_first.size(); ++k) {
-        const uint32_t i = set_first[k];
-        rkeys[k].assign((const char*)&rs[(size_t)i * RW], 4 * nrs[i]);
+      for (size_t k = 0; k < nkr; ++k) {
+        int m;
+        const int32_t* r = role_span(key_roles[k].first, key_roles[k].second, &m);
+        rkeys[k].assign((const char*)r, 4 * (size_t)m);
         rkeys[k] += '|';
         rkeys[k] += thr_key;
         auto it = C.classes.role_rows.find(rkeys[k]);
@@ -2248,12 +2277,33 @@ void Classes::run() {
       }
     }
     B.classes_new += (uint32_t)rmiss.size();
+    const uint32_t wsu = C.ws + C.wp, wpu = 2 * C.ws + C.wp, rr = C.ws + C.wp;
     for (uint32_t k : rmiss) {
-      const uint32_t i = set_first[k];
-      Row r = role_filter_fn(&rs[(size_t)i * RW], nrs[i]);
+      int m;
+      const int32_t* roles = role_span(key_roles[k].first, key_roles[k].second, &m);
+      Row r = role_filter_fn(roles, m);
       for (uint32_t w = 0; w < C.W; ++w) r[w] &= valid[w];
-      sets_need_policies(r);
-      Row o = assemble(r, &thr_any);
+      Row o(C.W2, 0u);
+      // candidate sets: every set with policies (role-free, _role_factor's s_free)
+      for (uint32_t s = 0; s < C.S; ++s)
+        if (C.nodes[s].child_end > C.nodes[s].child_begin) o[s >> 5] |= 1u << (s & 31);
+      std::copy(r.begin() + C.ws, r.begin() + C.ws + C.wp, o.begin() + C.ws);
+      std::copy(r.begin() + C.ws + C.wp, r.end(), o.begin() + 2 * C.ws + 2 * C.wp);
+      // role-relaxed useful sections (_useful_relaxed with every policy role-free)
+      for (uint32_t q = 0; q < C.P; ++q) {
+        bool use = bit(r, C.ws, q) && (C.pol_static[q] || bit(thr_any, 0, q));
+        const NodeRec& N = C.nodes[C.S + q];
+        for (uint32_t x = N.child_begin; x < N.child_end && !use; ++x) use = bit(r, rr, x);
+        if (use) o[wpu + (q >> 5)] |= 1u << (q & 31);
+      }
+      for (uint32_t s = 0; s < C.S; ++s) {
+        if (!bit(o, 0, s)) continue;
+        bool use = C.set_null[s];
+        const NodeRec& N = C.nodes[s];
+        for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(o, wpu, q);
+        if (use) o[wsu + (s >> 5)] |= 1u << (s & 31);
+      }
+      // the verdict sections are the class row's: the role side keeps them (all nodes)
       for (uint32_t q = 0; q < C.P; ++q)
         for (int s = 0; s < 4; ++s) o[C.WV + s * C.wp + (q >> 5)] |= 1u << (q & 31);
       for (uint32_t x = 0; x < C.R; ++x) o[C.WV + 4 * C.wp + (x >> 5)] |= 1u << (x & 31);
@@ -2266,10 +2316,10 @@ void Classes::run() {
         C.classes.bytes += (size_t)W * 4 + rkeys[k].size() + 64;
       }
     }
-    for (size_t k = 0; k < set_first.size(); ++k)
+    for (size_t k = 0; k < nkr; ++k)
       std::copy(rrow[k]->begin(), rrow[k]->end(), B.role_bits.begin() + k * W);
     B.role_key = std::move(rkey);
-    B.role_rows = (uint32_t)set_first.size();
+    B.role_rows = (uint32_t)nkr;
     return;
   }
 }
@@ -2517,24 +2567,30 @@ double now_s() {
 // class] (bucket = 1 + class; 0: an unfiltered request) or, with a role factor, role-major
 // [role key | bucket]; stable (index order within a key).  Runs of equal buckets start on
 // 64-lane wave boundaries (holes 0xFFFFFFFF) when the classes average 32 to 256 requests and
-// there is no role factor.  A parallel LSD radix sort of 32-bit keys, 8-bit digits, a
-// digit whose value every key shares skipped.
+// there is no role factor.  A parallel LSD radix sort of 32-bit (role-major: 48-bit) keys,
+// 8-bit digits, a digit whose value every key shares skipped.
 void coherence_order(acs_codec_batch& B, int threads) {
   const size_t n = B.n;
   const bool rmaj = !B.role_key.empty();
-  std::vector<uint32_t> key(n), idx(n), key2(n), idx2(n);
+  std::vector<uint64_t> key(n), key2(n);
+  std::vector<uint32_t> idx(n), idx2(n);
   int T = threads < 1 ? 1 : threads;
   if ((size_t)T > n / 65536 + 1) T = (int)(n / 65536 + 1);
   parallel_ranges(T, n, [&](int, size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       const uint32_t c = B.lines[i].h.flags >> RQ_PCOL_SHIFT;
       const uint32_t bucket = c < B.cand_rows ? c + 1u : 0u;
-      key[i] = rmaj ? (std::min<uint32_t>(B.role_key[i], 0xFFFFu) << 16 | bucket) : (bucket << 16 | B.lines[i].cls2);
+      if (rmaj) {  // [role row | 1 + second role row | bucket]
+        const uint64_t rk = B.role_key[i];
+        key[i] = (rk & 0xFFFFu) << 32 | (rk >> 16) << 16 | bucket;
+      } else {
+        key[i] = bucket << 16 | B.lines[i].cls2;
+      }
       idx[i] = (uint32_t)i;
     }
   });
   std::vector<std::array<size_t, 256>> cnt(T);
-  for (int sh = 0; sh < 32; sh += 8) {
+  for (int sh = 0; sh < (rmaj ? 48 : 32); sh += 8) {
     auto range = [&](int t, size_t& lo, size_t& hi) {
       lo = n * t / T;
       hi = n * (t + 1) / T;

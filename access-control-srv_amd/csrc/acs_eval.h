@@ -179,6 +179,23 @@ ACS_FN const uint32_t* second_row(const Batch& B, uint32_t i, bool* bad) {
   return B.cand + (size_t)(c2 - 1u) * B.cand_words;
 }
 
+// The role-factor rows of a request's role key (role_key: row | (1 + second row) << 16; a
+// request with two required roles ORs its two rows).  Both nullptr: no role filtering (no
+// factor, or a key outside the rows — never narrower).
+ACS_FN void role_rows_of(const Batch& B, uint32_t rk, const uint32_t** r1, const uint32_t** r2) {
+  *r1 = *r2 = nullptr;
+  if (!B.role_key) return;
+  const uint32_t a = rk & 0xFFFFu, b = rk >> 16;
+  if (a >= B.role_rows || (b && b - 1u >= B.role_rows)) return;
+  *r1 = B.role_bits + (size_t)a * B.cand_words;
+  if (b) *r2 = B.role_bits + (size_t)(b - 1u) * B.cand_words;
+}
+
+// word w of the OR of a request's role rows (all ones: no role filtering)
+ACS_FN uint32_t role_word(const uint32_t* r1, const uint32_t* r2, uint32_t w) {
+  return r1 ? (r2 ? r1[w] | r2[w] : r1[w]) : ~0u;
+}
+
 // Target-verdict word of a lane with one or two class rows: a known-true section (exact /
 // RegExp true, rules retried true) is true when either row knows it (the composed request holds
 // both role sets); a known-false section (`conj`) only when both do.
@@ -212,7 +229,8 @@ ACS_FN uint32_t wave_or(uint32_t x) {
 struct Filter {
   const uint32_t* row;     // this request's class row
   const uint32_t* row2;    // its second class row (composed rows; nullptr: none)
-  const uint32_t* rrow;    // its role-factor row (nullptr: the batch has no role factor)
+  const uint32_t* rrow;    // its role-factor row (nullptr: no role filtering)
+  const uint32_t* rrow2;   // its second role-factor row (two required roles; nullptr: none)
   const uint32_t* lds;     // GPU: the wave's OR of its (class & role) rows, words [0, lds_n)
   uint32_t lds_n;
   uint32_t wp, wr;         // word offsets of the policy / rule sections
@@ -237,7 +255,7 @@ struct Filter {
     ACS_SCAN(8);  // a word of the lanes' class and role rows (counted once per wave)
     uint32_t x = row[w];
     if (row2) x |= row2[w];
-    if (rrow) x &= rrow[w];
+    if (rrow) x &= role_word(rrow, rrow2, w);
     return wave_or(x);
   }
 };
@@ -1187,7 +1205,7 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h) {
   const uint32_t pc = h.flags >> RQ_PCOL_SHIFT;
   F.all = B.cand == nullptr || pc == PCOL_ALL || pc >= B.cand_rows || (h.flags & RQ_NO_TARGET);
   F.row = F.all ? nullptr : B.cand + (size_t)pc * B.cand_words;
-  F.row2 = F.rrow = nullptr;
+  F.row2 = F.rrow = F.rrow2 = nullptr;
   F.vok = !F.all && B.cand_wv != 0;  // the request's own class row
   return F;
 }
@@ -1203,7 +1221,7 @@ ACS_FN Filter request_filter(const Batch& B, const ReqHdr& h, uint32_t i) {
     F.row2 = nullptr;
     return F;
   }
-  if (B.role_key && B.role_key[i] < B.role_rows) F.rrow = B.role_bits + (size_t)B.role_key[i] * B.cand_words;
+  if (B.role_key) role_rows_of(B, B.role_key[i], &F.rrow, &F.rrow2);
   return F;
 }
 

@@ -87,7 +87,7 @@ __device__ inline uint32_t sort_key(const Batch& B, uint32_t k, uint32_t lowbits
   // the action is read only when it is the low field (a 4-B read of a 128-B line still
   // moves a sector: with lowbits == 0 the key kernel reads the header alone)
   uint32_t low = 0, bucket = cls + 1;
-  if (B.role_key) low = B.role_key[k];
+  if (B.role_key) low = B.role_key[k] & 0xFFFFu;  // the first role row
   else if (lowbits && h.nact) low = ln ? ln->a0.value : B.act[k].value;
   if (cls >= B.cand_rows) {
     bucket = 0;
@@ -401,6 +401,8 @@ __device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, u
   return true;
 }
 
+constexpr uint32_t NO_ROLE_KEY = 0xFFFFFFFFu;  // a lane without role filtering (wave_filter keys)
+
 // Candidate filter of a wave, built with every lane present before any lane diverges.  A
 // request's row is its class row (OR its second class row: composed rows), AND-ed with its
 // role-factor row when the batch has one.  The LDS part is the OR of the rows of all the
@@ -418,31 +420,34 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
   F.all = B.cand == nullptr;
   F.lds = lds;
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
-  const uint32_t nroles = B.role_key ? B.role_rows : 0u;
   const uint32_t LW = W <= LDS_FILTER_WORDS ? W : B.lds_pref;
   F.lds_n = LW;
   // this lane's own rows (any valid row for a lane that evaluates nothing)
   const bool own = valid && cls < B.cand_rows;
   F.row = B.cand ? B.cand + (size_t)(own ? cls : 0u) * W : nullptr;
   F.row2 = own && c2 && c2 - 1u < B.cand_rows ? B.cand + (size_t)(c2 - 1u) * W : nullptr;
-  F.rrow = own && rk < nroles ? B.role_bits + (size_t)rk * W : nullptr;
+  const uint32_t *r1, *r2;
+  role_rows_of(B, rk, &r1, &r2);
+  F.rrow = own ? r1 : nullptr;
+  F.rrow2 = own ? r2 : nullptr;
   if (F.all) return F;
   for (uint32_t w = lane; w < LW; w += 64) lds[w] = 0u;
-  const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
+  const uint32_t rkey = r1 ? rk : NO_ROLE_KEY;
   uint64_t pending = __ballot(valid);
   if (!pending) F.all = true;  // no active lane: nothing is evaluated anyway
-  while (pending) {
+  while (pending) {  // once per distinct (class, role key) of the wave
     const int leader = __builtin_ctzll(pending);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader), c = k >> 16, r = k & 0xFFFFu;
+    const uint32_t c = __builtin_amdgcn_readlane(cls, leader), r = __builtin_amdgcn_readlane(rkey, leader);
     if (c == PCOL_ALL || c >= B.cand_rows) {
       F.all = true;
       break;
     }
     const uint32_t* row = B.cand + (size_t)c * W;
-    const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : row;
-    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & rrow[w];
-    ACS_SCAN(LW * (rrow == row ? 4u : 8u));
-    pending &= ~__ballot(valid && key == k);
+    const uint32_t *q1 = nullptr, *q2 = nullptr;
+    if (r != NO_ROLE_KEY) role_rows_of(B, r, &q1, &q2);
+    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & role_word(q1, q2, w);
+    ACS_SCAN(LW * (q1 ? (q2 ? 12u : 8u) : 4u));
+    pending &= ~__ballot(valid && cls == c && rkey == r);
   }
   bool any2;
   if (!F.all && !or_second_rows(B, valid, c2, lds, LW, &any2)) F.all = true;
@@ -456,28 +461,30 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
   FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, nullptr, nullptr,
               false};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
-  const uint32_t nroles = B.role_key ? B.role_rows : 0u;
-  const uint32_t key = cls << 16 | (rk < nroles ? rk : 0xFFFFu);
+  const uint32_t *r1, *r2;
+  role_rows_of(B, rk, &r1, &r2);
+  const uint32_t rkey = r1 ? rk : NO_ROLE_KEY;
   bool all = false, any2 = false;
   uint32_t first_cls = PCOL_ALL, classes = 0;
   for (uint32_t w = lane; w < W; w += 64) lds[w] = 0u;
   uint64_t pending = __ballot(valid);
-  while (pending) {
+  while (pending) {  // once per distinct (class, role key) of the wave
     const int leader = __builtin_ctzll(pending);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader), c = k >> 16, r = k & 0xFFFFu;
+    const uint32_t c = __builtin_amdgcn_readlane(cls, leader), r = __builtin_amdgcn_readlane(rkey, leader);
     if (c == PCOL_ALL || c >= B.cand_rows) {
       all = true;
       break;
     }
     const uint32_t* row = B.cand + (size_t)c * W;
-    const uint32_t* rrow = r < nroles ? B.role_bits + (size_t)r * W : nullptr;
-    for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & (rrow ? rrow[w] : ~0u);
-    ACS_SCAN(W * (rrow ? 8u : 4u));
+    const uint32_t *q1 = nullptr, *q2 = nullptr;
+    if (r != NO_ROLE_KEY) role_rows_of(B, r, &q1, &q2);
+    for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & role_word(q1, q2, w);
+    ACS_SCAN(W * (q1 ? (q2 ? 12u : 8u) : 4u));
     if (c != first_cls) {
       first_cls = c;
       ++classes;
     }
-    pending &= ~__ballot(valid && key == k);
+    pending &= ~__ballot(valid && cls == c && rkey == r);
   }
   if (!all && !or_second_rows(B, valid, c2, lds, W, &any2)) all = true;
   if (all)

@@ -109,6 +109,8 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
         (b->cand_wv && (uint64_t)b->cand_wv + 4ull * words32(n_pols) + words32(n_rules) > b->cand_words))
       return bad("batch: candidate row layout", b->cand_words);
     if (b->role_key && !b->role_rows_bits && b->role_rows) return bad("batch: role factor rows", 0);
+    // role keys pack two row indices in 16 bits each, 0xFFFF meaning "no role filtering"
+    if (b->role_key && b->role_rows >= 0xFFFFu) return bad("batch: role factor rows", b->role_rows);
   }
   // the encoder's coherence order: every request exactly once, holes 0xFFFFFFFF (the kernels
   // skip an index >= n; a request missing from it would leave its record unwritten)

@@ -67,9 +67,11 @@ typedef struct {
   uint32_t cand_rows;
   uint32_t cand_wsu, cand_wpu, cand_wv;
   /* Optional role factor (large stores, where class rows keyed by roles would not fit):
-   * [role_rows][cand_words] bitsets of the nodes a request with that role-association set
-   * can reach (checkSubjectMatches, accessController.ts:793-823), AND-ed with the class
-   * row; role_key[n] picks the row per request (>= role_rows: unfiltered).  NULL = none. */
+   * [role_rows][cand_words] bitsets of the nodes a request holding a required role (or a
+   * whole role set past two) can reach (checkSubjectMatches, accessController.ts:793-823),
+   * with role-relaxed useful sections so that rows OR; AND-ed with the class row.
+   * role_key[n] = row | (1 + second row) << 16 (high half 0: one row; a row index >=
+   * role_rows: unfiltered); the kernel ORs the two rows.  role_rows < 0xFFFF.  NULL = none. */
   const uint32_t* role_key;
   const uint32_t* role_rows_bits;
   uint32_t role_rows;

@@ -261,9 +261,9 @@ def test_native_compiler_fixtures_and_configs_byte_identical():
 
 
 def _request_rows(b):
-    """Per request: (class row bytes or None, its second class row (composed rows) or None,
-    role-factor row bytes or None) — the rows as a set: which of two rows is first is the
-    batch's class order."""
+    """Per request: (its class rows — the class row and its second class row (composed rows) —
+    and its role-factor rows (None: no role filtering)), each as a set: which of two rows is
+    first is the batch's row order."""
     cls = (b.hdr["flags"] >> np.uint32(16)).astype(np.int64)
     cls2 = b.lines["cls2"].astype(np.int64)
     out = []
@@ -271,8 +271,11 @@ def _request_rows(b):
         c = b.cand[cls[i]].tobytes() if b.cand is not None and cls[i] < b.cand.shape[0] else None
         c2 = b.cand[cls2[i] - 1].tobytes() if cls2[i] else None
         r = None
-        if b.role_key is not None and b.role_key[i] < b.role_bits.shape[0]:
-            r = b.role_bits[b.role_key[i]].tobytes()
+        if b.role_key is not None:  # row | (1 + second row) << 16
+            k = int(b.role_key[i])
+            r1, r2 = k & 0xFFFF, (k >> 16) - 1
+            if r1 < b.role_bits.shape[0] and r2 < b.role_bits.shape[0]:
+                r = frozenset(b.role_bits[x].tobytes() for x in (r1, r2) if x >= 0)
         out.append((frozenset(x for x in (c, c2) if x is not None), r))
     return out
 
