@@ -560,6 +560,13 @@ struct acs_codec {
   std::vector<uint32_t> norole_bits;          // [W]
   std::vector<std::vector<uint32_t>> role_node_list;  // per role row: node indices
   std::vector<uint8_t> node_need_act;
+  // per-node target facts as [W] bitsets (the word-parallel verdict sections): a target, an
+  // empty subjects list, a role-requiring subjects list, a target listing actions
+  std::vector<uint32_t> tgt_bits, subj_empty_bits, subj_role_bits, need_act_bits;
+  std::vector<uint32_t> need_act_nodes;  // nodes whose target lists actions
+  // resource verdict statics per section (policy / rule local bits): an empty resources list,
+  // an entity-only list (not empty)
+  std::vector<uint32_t> res_empty_p, res_empty_r, ent_only_p, ent_only_r;
   // useful sections (candidates.useful_static): policies useful wherever they are candidates,
   // sets holding a null policy; output row layout [S | P | useful S | useful P | R]
   std::vector<uint8_t> pol_static, set_null;
@@ -735,6 +742,32 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
   }
   std::sort(c->role_ids.begin(), c->role_ids.end());
   c->role_ids.erase(std::unique(c->role_ids.begin(), c->role_ids.end()), c->role_ids.end());
+  c->tgt_bits.assign(c->W, 0);
+  c->subj_empty_bits.assign(c->W, 0);
+  c->subj_role_bits.assign(c->W, 0);
+  c->need_act_bits.assign(c->W, 0);
+  for (uint32_t g = 0; g < nn; ++g) {
+    const NodeRec& N = c->nodes[g];
+    if (!(N.nflags & NF_HAS_TARGET)) continue;
+    const uint32_t w = c->node_word(g), b = c->node_bit(g);
+    c->tgt_bits[w] |= b;
+    if (N.tflags & TF_SUBJ_EMPTY) c->subj_empty_bits[w] |= b;
+    else if (N.tflags & TF_SUBJ_ROLE) c->subj_role_bits[w] |= b;
+    if (c->node_need_act[g]) c->need_act_bits[w] |= b;
+  }
+  for (uint32_t g = 0; g < nn; ++g)
+    if (c->node_need_act[g]) c->need_act_nodes.push_back(g);
+  c->res_empty_p.assign(c->wp ? c->wp : 1, 0);
+  c->ent_only_p.assign(c->wp ? c->wp : 1, 0);
+  c->res_empty_r.assign(c->wr ? c->wr : 1, 0);
+  c->ent_only_r.assign(c->wr ? c->wr : 1, 0);
+  for (uint32_t g = c->S; g < nn; ++g) {
+    const bool pol = g < c->S + c->P;
+    const uint32_t l = pol ? g - c->S : g - c->S - c->P;
+    const uint16_t tf = (uint16_t)c->nodes[g].tflags;
+    if (tf & TF_RES_EMPTY) (pol ? c->res_empty_p : c->res_empty_r)[l >> 5] |= 1u << (l & 31);
+    else if (tf & TF_RES_ENT_ONLY) (pol ? c->ent_only_p : c->ent_only_r)[l >> 5] |= 1u << (l & 31);
+  }
   c->norole_bits.assign(c->W, 0);
   c->role_node_list.assign(c->role_ids.size(), {});
   for (uint32_t g = 0; g < nn; ++g) {
@@ -1535,17 +1568,14 @@ struct Classes {
       auto it = C.act_rows.find(key);
       if (it != C.act_rows.end()) return it->second;
     }
-    auto row = std::make_shared<Row>(C.W, 0u);
+    auto row = std::make_shared<Row>(no_action_row());  // nodes listing no action, then:
     auto leq = [](uint32_t a, uint32_t b) { return a == b || (a <= ID_NULL && b <= ID_NULL); };
-    const uint32_t nn = C.S + C.P + C.R;
-    for (uint32_t g = 0; g < nn; ++g) {
+    for (uint32_t g : C.need_act_nodes) {
+      const NodeRec& N = C.nodes[g];
       bool ok = true;
-      if (C.node_need_act[g]) {
-        const NodeRec& N = C.nodes[g];
-        for (uint32_t k = 0; k < N.act_n && ok; ++k) {
-          const Pair& pr = C.pairs[N.act_off + k];
-          ok = leq(pr.id, id) && leq(pr.value, value);
-        }
+      for (uint32_t k = 0; k < N.act_n && ok; ++k) {
+        const Pair& pr = C.pairs[N.act_off + k];
+        ok = leq(pr.id, id) && leq(pr.value, value);
       }
       if (ok) set_node(*row, g);
     }
@@ -1559,9 +1589,7 @@ struct Classes {
 
   Row no_action_row() const {  // row 0: a request without action attributes
     Row r(C.W, 0u);
-    const uint32_t nn = C.S + C.P + C.R;
-    for (uint32_t g = 0; g < nn; ++g)
-      if (!C.node_need_act[g]) r[C.node_word(g)] |= C.node_bit(g);
+    for (uint32_t w = 0; w < C.W; ++w) r[w] = valid[w] & ~C.need_act_bits[w];
     return r;
   }
 
@@ -1574,15 +1602,32 @@ struct Classes {
 
   // set section: keep a set only if one of its policies is kept and it has policies
   void sets_need_policies(Row& r) const {
-    for (uint32_t s = 0; s < C.S; ++s) {
+    each_bit(r, 0, C.S, [&](uint32_t s) {
       const NodeRec& N = C.nodes[s];
-      bool any = false;
-      for (uint32_t p = N.child_begin; p < N.child_end && !any; ++p) any = (r[C.ws + (p >> 5)] >> (p & 31)) & 1u;
-      if (!any) r[s >> 5] &= ~(1u << (s & 31));
-    }
+      if (!range_any(r, C.ws, N.child_begin, N.child_end)) r[s >> 5] &= ~(1u << (s & 31));
+    });
   }
 
   static bool bit(const Row& r, uint32_t off, uint32_t i) { return (r[off + (i >> 5)] >> (i & 31)) & 1u; }
+
+  // any bit of [b, e) set in the section at word `off`
+  static bool range_any(const Row& r, uint32_t off, uint32_t b, uint32_t e) {
+    if (b >= e) return false;
+    const uint32_t wb = b >> 5, we = (e - 1) >> 5;
+    const uint32_t mb = ~0u << (b & 31), me = ~0u >> (31 - ((e - 1) & 31));
+    if (wb == we) return (r[off + wb] & mb & me) != 0;
+    if (r[off + wb] & mb) return true;
+    for (uint32_t w = wb + 1; w < we; ++w)
+      if (r[off + w]) return true;
+    return (r[off + we] & me) != 0;
+  }
+
+  // f(i) for each set bit i of the n-bit section at word `off` (ascending)
+  template <class F>
+  static void each_bit(const Row& r, uint32_t off, uint32_t n, F f) {
+    for (uint32_t w = 0; w < (n + 31) / 32; ++w)
+      for (uint32_t x = r[off + w]; x; x &= x - 1) f(w * 32 + (uint32_t)__builtin_ctz(x));
+  }
 
   // [S | P | R] row -> [S | P | useful S | useful P | R] (candidates._useful / _assemble);
   // thr: the column's throwing policies (P bits), or nullptr
@@ -1593,98 +1638,97 @@ struct Classes {
   };
   std::vector<std::unique_ptr<ResV>> resv;  // per column + the no-entity column
 
-  void build_resv(uint32_t ncols) {
-    resv.clear();
-    resv.resize(ncols + 1);
-    for (uint32_t c = 0; c <= ncols; ++c) {
-      auto v = std::make_unique<ResV>();
-      for (int k = 0; k < 4; ++k) {
-        v->p[k].assign(C.wp ? C.wp : 1, 0u);
-        v->r[k].assign(C.wr ? C.wr : 1, 0u);
-      }
-      const bool none = c == ncols, real = none || !col_keys[c].empty();
+  // resv[c] for column c (c == ncols: the no-entity column); resv sized ncols + 1 beforehand
+  void build_resv_column(uint32_t c, uint32_t ncols) {
+    auto v = std::make_unique<ResV>();
+    const bool none = c == ncols, real = none || !col_keys[c].empty();
+    // an empty resources list: exact and RegExp match known true
+    v->p[0] = v->p[2] = C.res_empty_p;
+    v->r[0] = v->r[2] = C.res_empty_r;
+    // an entity-only list (real columns): known false unless it lists the value's exact row or
+    // a RegExp row whose cell the value touched — those nodes are redone below
+    if (real) {
+      v->p[1] = v->p[3] = C.ent_only_p;
+      v->r[1] = v->r[3] = C.ent_only_r;
+    } else {
+      v->p[1].assign(C.res_empty_p.size(), 0u);
+      v->p[3] = v->p[1];
+      v->r[1].assign(C.res_empty_r.size(), 0u);
+      v->r[3] = v->r[1];
+    }
+    if (!none && real) {
+      const std::string& key = col_keys[c];
       uint32_t exact_row = NONE32;
-      const uint8_t* cells = nullptr;
-      if (!none && real) {
-        const std::string& key = col_keys[c];
-        uint32_t id = key[0] == 'm' ? ID_UNDEF : key[0] == 'n' ? ID_NULL : C.lookup(std::string_view(key).substr(1));
-        if (id != NONE32) {
-          auto it = C.row_of_id.find(id);
-          if (it != C.row_of_id.end()) exact_row = it->second;
-        }
-        cells = B.rx.data() + (size_t)c * B.rx_rows;
+      uint32_t id = key[0] == 'm' ? ID_UNDEF : key[0] == 'n' ? ID_NULL : C.lookup(std::string_view(key).substr(1));
+      if (id != NONE32) {
+        auto it = C.row_of_id.find(id);
+        if (it != C.row_of_id.end()) exact_row = it->second;
       }
-      const uint32_t nn = C.S + C.P + C.R;
-      for (uint32_t g = C.S; g < nn; ++g) {
-        const bool pol = g < C.S + C.P;
-        const uint32_t l = pol ? g - C.S : g - C.S - C.P;
-        Row* out = pol ? v->p : v->r;
-        const uint16_t tf = (uint16_t)C.nodes[g].tflags;
-        auto set = [&](int k) { out[k][l >> 5] |= 1u << (l & 31); };
-        if (tf & TF_RES_EMPTY) {
-          set(0);
-          set(2);
-          continue;
-        }
-        if (!(tf & TF_RES_ENT_ONLY) || !real) continue;
-        if (none) {
-          set(1);
-          set(3);
-          continue;
-        }
-        bool xt = false, em = false, thrown = false;
-        if (C.spec_kind[g] != 1)
-          for (uint32_t k = C.spec_ptr[g]; k < C.spec_ptr[g + 1]; ++k) {
-            const uint32_t row = C.spec_idx[k];
+      const uint8_t* cells = B.rx.data() + (size_t)c * B.rx_rows;
+      const uint32_t nrx = (uint32_t)C.rx_pat.size();
+      for (uint32_t rrow = 0; rrow < nrx; ++rrow) {
+        if (!cells[rrow] && rrow != exact_row) continue;
+        for (uint32_t k = C.row_ptr[rrow]; k < C.row_ptr[rrow + 1]; ++k) {
+          const uint32_t g = C.row_nodes[k];
+          if (g < C.S) continue;
+          const uint16_t tf = (uint16_t)C.nodes[g].tflags;
+          if ((tf & TF_RES_EMPTY) || !(tf & TF_RES_ENT_ONLY)) continue;
+          const bool pol = g < C.S + C.P;
+          const uint32_t l = pol ? g - C.S : g - C.S - C.P;
+          Row* out = pol ? v->p : v->r;
+          bool xt = false, em = false, thrown = false;
+          for (uint32_t q = C.spec_ptr[g]; q < C.spec_ptr[g + 1]; ++q) {
+            const uint32_t row = C.spec_idx[q];
             if (row == exact_row) xt = true;
-            const uint8_t cell = row < C.rx_pat.size() ? cells[row] : 0;
+            const uint8_t cell = row < nrx ? cells[row] : 0;
             if (cell & (C_RX_THROW_TYPE | C_RX_THROW_SYNTAX | C_RX_HOST)) thrown = true;
             if (cell & C_RX_HIT) em = true;
             else if (cell & C_RX_RESET) em = false;
           }
-        set(xt ? 0 : 1);
-        if (!thrown) set(em ? 2 : 3);
+          const uint32_t b = 1u << (l & 31), w = l >> 5;
+          for (int s = 0; s < 4; ++s) out[s][w] &= ~b;
+          out[xt ? 0 : 1][w] |= b;
+          if (!thrown) out[em ? 2 : 3][w] |= b;
+        }
       }
-      resv[c] = std::move(v);
     }
+    resv[c] = std::move(v);
   }
 
   // the verdict sections of one class (candidates._verdicts): pc column, a action key,
-  // roles / nroles the class's sorted role rows
+  // roles / nroles the class's sorted role rows.  Word-parallel over the policy and rule
+  // sections: per node, subjects known true (empty list, or a required role the class holds) /
+  // false (a required role it lacks), actions known true (none listed, or the class's single
+  // pair matches) / false, and the column's resource verdicts
   void verdicts(Row& out, uint32_t pc, uint32_t a, const int32_t* roles, int nroles, bool role_filter,
                 bool action_filter, const std::vector<std::shared_ptr<const Row>>& arow) const {
     const ResV& rv = *resv[pc];
     const Row& A = *arow[action_filter ? a : 1u];
     const bool fixed = action_filter && a != 1;
-    const uint32_t nn = C.S + C.P + C.R;
-    for (uint32_t g = C.S; g < nn; ++g) {
-      const NodeRec& N = C.nodes[g];
-      if (!(N.nflags & NF_HAS_TARGET)) continue;
-      const bool pol = g < C.S + C.P;
-      const uint32_t l = pol ? g - C.S : g - C.S - C.P;
+    Row in;  // nodes whose required role the class holds (| role-free nodes, masked off below)
+    if (role_filter) in = role_filter_fn(roles, nroles);
+    for (int sec = 0; sec < 2; ++sec) {
+      const bool pol = sec == 0;
+      const uint32_t base = pol ? C.ws : C.ws + C.wp, nw = pol ? C.wp : C.wr;
       const Row* res = pol ? rv.p : rv.r;
-      auto rb = [&](int k) { return (res[k][l >> 5] >> (l & 31)) & 1u; };
-      const bool sub_empty = N.tflags & TF_SUBJ_EMPTY;
-      const bool sub_role = (N.tflags & TF_SUBJ_ROLE) && !sub_empty;
-      bool in = false;
-      if (sub_role && role_filter && C.node_role[g] >= 0)
-        for (int k = 0; k < nroles && !in; ++k) in = roles[k] == C.node_role[g];
-      const bool subj_t = sub_empty || (sub_role && role_filter && in);
-      const bool subj_f = sub_role && role_filter && !in;
-      const bool need = C.node_need_act[g];
-      const bool abit = (A[C.node_word(g)] & C.node_bit(g)) != 0;
-      const bool act_t = !need || (fixed && abit);
-      const bool act_f = need && fixed && !abit;
-      const bool both_t = subj_t && act_t, any_f = subj_f || act_f;
-      const bool xt = both_t && rb(0), xf = any_f || rb(1), rt = both_t && rb(2), rf = any_f || rb(3);
-      auto put = [&](uint32_t sec) { out[C.WV + sec + (l >> 5)] |= 1u << (l & 31); };
-      if (pol) {
-        if (xt) put(0);
-        if (xf) put(C.wp);
-        if (rt) put(2 * C.wp);
-        if (rf) put(3 * C.wp);
-      } else if (xt || (xf && rt)) {
-        put(4 * C.wp);
+      for (uint32_t j = 0; j < nw; ++j) {
+        const uint32_t w = base + j, tg = C.tgt_bits[w];
+        if (!tg) continue;
+        const uint32_t sr = C.subj_role_bits[w], inw = role_filter ? in[w] & sr : 0u;
+        const uint32_t subj_t = C.subj_empty_bits[w] | inw, subj_f = role_filter ? sr & ~inw : 0u;
+        const uint32_t need = C.need_act_bits[w];
+        const uint32_t act_t = ~need | (fixed ? A[w] : 0u), act_f = fixed ? need & ~A[w] : 0u;
+        const uint32_t both_t = subj_t & act_t, any_f = subj_f | act_f;
+        const uint32_t xt = both_t & res[0][j], xf = any_f | res[1][j], rt = both_t & res[2][j],
+                       rf = any_f | res[3][j];
+        if (pol) {
+          out[C.WV + j] |= xt & tg;
+          out[C.WV + C.wp + j] |= xf & tg;
+          out[C.WV + 2 * C.wp + j] |= rt & tg;
+          out[C.WV + 3 * C.wp + j] |= rf & tg;
+        } else {
+          out[C.WV + 4 * C.wp + j] |= (xt | (xf & rt)) & tg;
+        }
       }
     }
   }
@@ -1712,20 +1756,15 @@ struct Classes {
     std::copy(r.begin(), r.begin() + C.ws + C.wp, out.begin());
     std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
     const uint32_t wsu = C.ws + C.wp, wpu = 2 * C.ws + C.wp, rr = C.ws + C.wp;
-    for (uint32_t q = 0; q < C.P; ++q) {
-      if (!bit(r, C.ws, q)) continue;
-      bool use = C.pol_static[q] || (thr && bit(*thr, 0, q));
+    each_bit(r, C.ws, C.P, [&](uint32_t q) {
       const NodeRec& N = C.nodes[C.S + q];
-      for (uint32_t k = N.child_begin; k < N.child_end && !use; ++k) use = bit(r, rr, k);
-      if (use) out[wpu + (q >> 5)] |= 1u << (q & 31);
-    }
-    for (uint32_t s = 0; s < C.S; ++s) {
-      if (!bit(r, 0, s)) continue;
-      bool use = C.set_null[s];
+      if (C.pol_static[q] || (thr && bit(*thr, 0, q)) || range_any(r, rr, N.child_begin, N.child_end))
+        out[wpu + (q >> 5)] |= 1u << (q & 31);
+    });
+    each_bit(r, 0, C.S, [&](uint32_t s) {
       const NodeRec& N = C.nodes[s];
-      for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(out, wpu, q);
-      if (use) out[wsu + (s >> 5)] |= 1u << (s & 31);
-    }
+      if (C.set_null[s] || range_any(out, wpu, N.child_begin, N.child_end)) out[wsu + (s >> 5)] |= 1u << (s & 31);
+    });
     return out;
   }
 
@@ -1761,21 +1800,16 @@ struct Classes {
     std::copy(r.begin() + C.ws, r.begin() + C.ws + C.wp, out.begin() + C.ws);
     std::copy(r.begin() + C.ws + C.wp, r.end(), out.begin() + 2 * C.ws + 2 * C.wp);
     const uint32_t wsu = C.ws + C.wp, wpu = 2 * C.ws + C.wp, rr = C.ws + C.wp;
-    for (uint32_t q = 0; q < C.P; ++q) {
-      bool use = bit(r, C.ws, q) && (C.pol_static[q] || (thr && bit(*thr, 0, q)));
-      if (!use && bit(base, C.ws, q)) {
-        const NodeRec& N = C.nodes[C.S + q];
-        for (uint32_t k = N.child_begin; k < N.child_end && !use; ++k) use = bit(r, rr, k);
-      }
+    each_bit(base, C.ws, C.P, [&](uint32_t q) {  // r's policies are base's with the roles' test
+      const NodeRec& N = C.nodes[C.S + q];
+      const bool use = (bit(r, C.ws, q) && (C.pol_static[q] || (thr && bit(*thr, 0, q)))) ||
+                       range_any(r, rr, N.child_begin, N.child_end);
       if (use) out[wpu + (q >> 5)] |= 1u << (q & 31);
-    }
-    for (uint32_t s = 0; s < C.S; ++s) {
-      if (!bit(base, 0, s)) continue;
-      bool use = C.set_null[s];
+    });
+    each_bit(base, 0, C.S, [&](uint32_t s) {
       const NodeRec& N = C.nodes[s];
-      for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(out, wpu, q);
-      if (use) out[wsu + (s >> 5)] |= 1u << (s & 31);
-    }
+      if (C.set_null[s] || range_any(out, wpu, N.child_begin, N.child_end)) out[wsu + (s >> 5)] |= 1u << (s & 31);
+    });
     return out;
   }
 
@@ -1946,25 +1980,43 @@ void Classes::run() {
     if (prepared) return;
     prepared = true;
     ent.assign(ncols + 1, nullptr);
-    for (uint32_t c = 0; c < ncols; ++c) {
-      if (col_keys[c].empty()) {
-        ent[c] = std::make_shared<Row>(C.always_bits);
-        continue;
-      }
-      std::vector<uint8_t> cells(B.rx.begin() + (size_t)c * B.rx_rows,
-                                 B.rx.begin() + (size_t)c * B.rx_rows + C.rx_pat.size());
-      ent[c] = entity_row(col_keys[c], cells);
-    }
-    ent[ncols] = std::make_shared<Row>(C.always_bits);
-    build_resv(ncols);
+    resv.clear();
+    resv.resize(ncols + 1);
     thr.clear();
     thr.resize(ncols + 1);
-    for (uint32_t c = 0; c < ncols; ++c) thr[c] = throw_row(c);
     arow.assign(2 + pairs_k.size(), nullptr);
-    arow[0] = std::make_shared<Row>(no_action_row());
-    arow[1] = std::make_shared<Row>(valid);
-    for (size_t k = 0; k < pairs_k.size(); ++k)
-      arow[2 + k] = action_row((uint32_t)(pairs_k[k] >> 32), (uint32_t)pairs_k[k]);
+    // per column (entity row, resource verdicts, throwing policies) and per action key, over
+    // the threads: each item writes only its own slot (entity / action rows: the codec's
+    // caches, under their lock)
+    const size_t ncol_items = (size_t)ncols + 1, items = ncol_items + arow.size();
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+      for (;;) {
+        const size_t x = next.fetch_add(1);
+        if (x >= items) return;
+        if (x >= ncol_items) {
+          const size_t k = x - ncol_items;
+          if (k == 0) arow[0] = std::make_shared<Row>(no_action_row());
+          else if (k == 1) arow[1] = std::make_shared<Row>(valid);
+          else arow[k] = action_row((uint32_t)(pairs_k[k - 2] >> 32), (uint32_t)pairs_k[k - 2]);
+          continue;
+        }
+        const uint32_t c = (uint32_t)x;
+        build_resv_column(c, ncols);
+        if (c == ncols || col_keys[c].empty()) {
+          ent[c] = std::make_shared<Row>(C.always_bits);
+          continue;
+        }
+        std::vector<uint8_t> cells(B.rx.begin() + (size_t)c * B.rx_rows,
+                                   B.rx.begin() + (size_t)c * B.rx_rows + C.rx_pat.size());
+        ent[c] = entity_row(col_keys[c], cells);
+        thr[c] = throw_row(c);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads && (size_t)t < items; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
   };
   // the column part of a cache key: the entity value (a padding column: never a key)
   auto col_key = [&](uint32_t c) -> std::string {
@@ -2290,19 +2342,16 @@ void Classes::run() {
       std::copy(r.begin() + C.ws, r.begin() + C.ws + C.wp, o.begin() + C.ws);
       std::copy(r.begin() + C.ws + C.wp, r.end(), o.begin() + 2 * C.ws + 2 * C.wp);
       // role-relaxed useful sections (_useful_relaxed with every policy role-free)
-      for (uint32_t q = 0; q < C.P; ++q) {
-        bool use = bit(r, C.ws, q) && (C.pol_static[q] || bit(thr_any, 0, q));
+      for (uint32_t q = 0; q < C.P; ++q) {  // every policy role-free
         const NodeRec& N = C.nodes[C.S + q];
-        for (uint32_t x = N.child_begin; x < N.child_end && !use; ++x) use = bit(r, rr, x);
+        const bool use = (bit(r, C.ws, q) && (C.pol_static[q] || bit(thr_any, 0, q))) ||
+                         range_any(r, rr, N.child_begin, N.child_end);
         if (use) o[wpu + (q >> 5)] |= 1u << (q & 31);
       }
-      for (uint32_t s = 0; s < C.S; ++s) {
-        if (!bit(o, 0, s)) continue;
-        bool use = C.set_null[s];
+      each_bit(o, 0, C.S, [&](uint32_t s) {
         const NodeRec& N = C.nodes[s];
-        for (uint32_t q = N.child_begin; q < N.child_end && !use; ++q) use = bit(o, wpu, q);
-        if (use) o[wsu + (s >> 5)] |= 1u << (s & 31);
-      }
+        if (C.set_null[s] || range_any(o, wpu, N.child_begin, N.child_end)) o[wsu + (s >> 5)] |= 1u << (s & 31);
+      });
       // the verdict sections are the class row's: the role side keeps them (all nodes)
       for (uint32_t q = 0; q < C.P; ++q)
         for (int s = 0; s < 4; ++s) o[C.WV + s * C.wp + (q >> 5)] |= 1u << (q & 31);

@@ -19,10 +19,12 @@
 // array of its rules — JSON.stringify of Array.from(map.values()) at each level.
 #include <charconv>
 #include <cmath>
-#include <cstdio>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <string_view>
 #include <unordered_map>
 #include <vector>
@@ -83,8 +85,10 @@ struct Builder {
   std::vector<Ec> ec{{0, 0, "", false}, {1, 0, "", false}, {2, 0, "", false}, {3, 0, "", true}};
   // node tables + candidate specs (kind 0 never, 1 always, 2 rows)
   std::vector<NodeRec> sets, pols, rules;
+  // flat per section (sets, policies, rules): kind per node, the node's end in spec_idx, and
+  // the regex rows of kind-2 nodes
   std::vector<uint8_t> spec_kind[3];
-  std::vector<std::vector<uint32_t>> spec_rows[3];
+  std::vector<uint32_t> spec_end[3], spec_idx[3];
 
   uint32_t intern(const JV* v) {
     if (v->t == J_UNDEF) return ID_UNDEF;
@@ -310,13 +314,11 @@ struct Builder {
   }
 
   void push_spec(int sec, bool has_target, const Target& T, bool null_rule) {
-    if (has_target) {  // rows listed but none (no entity attribute): never a candidate
-      spec_kind[sec].push_back((uint8_t)(T.spec_kind == 2 && T.rows.empty() ? 0 : T.spec_kind));
-      spec_rows[sec].push_back(T.spec_kind == 2 ? T.rows : std::vector<uint32_t>{});
-    } else {
-      spec_kind[sec].push_back(null_rule ? 0 : 1);
-      spec_rows[sec].push_back({});
-    }
+    // a target listing entity rows but none (no entity attribute): never a candidate
+    const uint8_t k = has_target ? (uint8_t)(T.spec_kind == 2 && T.rows.empty() ? 0 : T.spec_kind) : (null_rule ? 0 : 1);
+    spec_kind[sec].push_back(k);
+    if (k == 2) spec_idx[sec].insert(spec_idx[sec].end(), T.rows.begin(), T.rows.end());
+    spec_end[sec].push_back((uint32_t)spec_idx[sec].size());
   }
 
   // compiler._compile_set + _assemble (global offsets from the start)
@@ -480,74 +482,6 @@ void json_write(std::string& o, const JV* v) {
   }
 }
 
-template <class T>
-void put(std::string& out, const T* p, size_t n, size_t align) {
-  out.append((const char*)p, n * sizeof(T));
-  out.append((align - (n * sizeof(T)) % align) % align, '\0');
-}
-
-std::string build_image(Builder& b) {
-  // codec section (compiler.codec_section)
-  std::string sec;
-  const uint32_t n_str = (uint32_t)b.strings.size();
-  std::vector<uint32_t> urn_ids(N_CODEC_URNS);
-  for (int k = 0; k < N_CODEC_URNS; ++k) {
-    const JV* v = b.U(kCodecUrns[k]);
-    urn_ids[k] = v->t == J_STR ? b.intern(v) : ID_UNDEF;
-  }
-  std::vector<uint8_t> kind;
-  std::vector<uint32_t> ptr{0}, idx;
-  for (int s = 0; s < 3; ++s)
-    for (size_t k = 0; k < b.spec_kind[s].size(); ++k) {
-      kind.push_back(b.spec_kind[s][k]);
-      if (b.spec_kind[s][k] == 2) idx.insert(idx.end(), b.spec_rows[s][k].begin(), b.spec_rows[s][k].end());
-      ptr.push_back((uint32_t)idx.size());
-    }
-  std::vector<uint32_t> offs{0};
-  std::string sbytes;
-  for (uint32_t i = 0; i < n_str; ++i) {
-    if (i > ID_EMPTY) sbytes += b.strings[i];
-    offs.push_back((uint32_t)sbytes.size());
-  }
-  const uint32_t hd[8] = {0x43534341u, 2u, n_str, (uint32_t)N_CODEC_URNS, (uint32_t)b.rx_rows.size(),
-                          (uint32_t)kind.size(), (uint32_t)idx.size(), (uint32_t)sbytes.size()};
-  put(sec, hd, 8, 4);
-  put(sec, urn_ids.data(), urn_ids.size(), 4);
-  put(sec, b.rx_rows.data(), b.rx_rows.size(), 4);
-  put(sec, kind.data(), kind.size(), 4);
-  put(sec, ptr.data(), ptr.size(), 4);
-  put(sec, idx.data(), idx.size(), 4);
-  put(sec, offs.data(), offs.size(), 4);
-  put(sec, sbytes.data(), sbytes.size(), 4);
-  std::string ecj = "[";
-  for (size_t k = 4; k < b.ec.size(); ++k) {
-    if (k > 4) ecj += ',';
-    ecj += b.ec[k].json;
-  }
-  ecj += ']';
-  const uint32_t ecn = (uint32_t)ecj.size();
-  put(sec, &ecn, 1, 4);
-  put(sec, ecj.data(), ecj.size(), 4);
-  // node tables + pools (compiler.store_blob)
-  std::string body;
-  put(body, b.sets.data(), b.sets.size(), 16);
-  put(body, b.pols.data(), b.pols.size(), 16);
-  put(body, b.rules.data(), b.rules.size(), 16);
-  put(body, b.rres.data(), b.rres.size(), 16);
-  put(body, b.pairs.data(), b.pairs.size(), 16);
-  put(body, b.u32pool.data(), b.u32pool.size(), 16);
-  const JV* user = b.U("user");
-  const uint32_t id_user = user->t == J_UNDEF ? ID_UNDEF : b.intern(user);
-  const uint32_t hdr[16] = {ACS_BLOB_MAGIC, ACS_ABI_VERSION, (uint32_t)b.sets.size(), (uint32_t)b.pols.size(),
-                            (uint32_t)b.rules.size(), (uint32_t)b.rres.size(), (uint32_t)b.pairs.size(),
-                            (uint32_t)b.u32pool.size(), id_user, (uint32_t)(64 + body.size()), (uint32_t)sec.size(),
-                            0, 0, 0, 0, 0};
-  std::string out((const char*)hdr, sizeof hdr);
-  out += body;
-  out += sec;
-  return out;
-}
-
 // Combining algorithms (accessController.ts:51-62) and the URN config, URN ids interned first
 // in config order (compiler.compile_store).
 void configure(Builder& b, const JV* urns, const JV* cas) {
@@ -585,25 +519,17 @@ void configure(Builder& b, const JV* urns, const JV* cas) {
 
 // compiler.mark_clean_below: NF_CLEAN_BELOW on a set when every earlier set is clean
 // (NF_COND_FREE, valid combining algorithm, no null policy), NF_CLEAN on a clean set
-void mark_clean_below(Builder& b) {
+void mark_clean_below(NodeRec* sets, size_t n_sets, const NodeRec* pols) {
   bool clean_so_far = true;
-  for (NodeRec& S : b.sets) {
+  for (size_t k = 0; k < n_sets; ++k) {
+    NodeRec& S = sets[k];
     if (clean_so_far) S.nflags |= NF_CLEAN_BELOW;
     bool clean = (S.nflags & NF_COND_FREE) && S.ca != CA_INVALID;
     for (uint32_t p = S.child_begin; p < S.child_end && clean; ++p)
-      if (b.pols[p].nflags & NF_NULL) clean = false;
+      if (pols[p].nflags & NF_NULL) clean = false;
     if (clean) S.nflags |= NF_CLEAN;
     clean_so_far = clean_so_far && clean;
   }
-}
-
-int emit(const std::string& img, void** blob_out, size_t* blob_len) {
-  void* mem = malloc(img.size());
-  if (!mem) fail("out of memory");
-  memcpy(mem, img.data(), img.size());
-  *blob_out = mem;
-  *blob_len = img.size();
-  return 0;
 }
 
 // ------------------------------------------------------------------ incremental compile
@@ -611,6 +537,7 @@ int emit(const std::string& img, void** blob_out, size_t* blob_len) {
 // Builder's per-set state while it was compiled), keyed by the set's JSON text.  The
 // dictionary, regex rows and evaluation_cacheable table live in the builder and only grow,
 // so a fragment's interned ids stay valid across compiles (compiler.IncrementalCompiler).
+// A full compile is one fragment holding every set.
 struct Fragment {
   uint64_t h1 = 0, h2 = 0;
   size_t len = 0;
@@ -619,7 +546,7 @@ struct Fragment {
   std::vector<Pair> pairs;
   std::vector<uint32_t> u32pool;
   std::vector<uint8_t> spec_kind[3];
-  std::vector<std::vector<uint32_t>> spec_rows[3];
+  std::vector<uint32_t> spec_end[3], spec_idx[3];
 };
 
 void swap_state(Builder& b, Fragment& f) {
@@ -631,7 +558,8 @@ void swap_state(Builder& b, Fragment& f) {
   std::swap(b.u32pool, f.u32pool);
   for (int k = 0; k < 3; ++k) {
     std::swap(b.spec_kind[k], f.spec_kind[k]);
-    std::swap(b.spec_rows[k], f.spec_rows[k]);
+    std::swap(b.spec_end[k], f.spec_end[k]);
+    std::swap(b.spec_idx[k], f.spec_idx[k]);
   }
 }
 
@@ -644,34 +572,157 @@ void shift_target(NodeRec& R, uint32_t pairs0, uint32_t rres0, uint32_t u320) {
   R.acl_roles_off += u320;
 }
 
-// Append fragment f to the builder's tables, its offsets shifted to where it lands.
-void append(Builder& b, const Fragment& f) {
-  const uint32_t P0 = (uint32_t)b.pols.size(), R0 = (uint32_t)b.rules.size();
-  const uint32_t RR0 = (uint32_t)b.rres.size(), PA0 = (uint32_t)b.pairs.size(), U0 = (uint32_t)b.u32pool.size();
-  for (NodeRec S : f.sets) {
-    S.child_begin += P0;
-    S.child_end += P0;
-    shift_target(S, PA0, RR0, U0);
-    b.sets.push_back(S);
+size_t a16(size_t x) { return (x + 15) & ~size_t(15); }
+size_t a4(size_t x) { return (x + 3) & ~size_t(3); }
+
+// The store image (compiler.store_blob + compiler.codec_section) of the fragments in order,
+// written straight into one zeroed allocation: per fragment, its node records with their
+// offsets shifted to where they land, its pools and candidate specs (fragments in parallel,
+// each at its prefix-sum offsets), then the builder's dictionary / regex rows /
+// evaluation_cacheable table.  The caller owns the buffer (acs_blob_free).
+void* write_image(Builder& b, const std::vector<const Fragment*>& F, size_t* len_out) {
+  const size_t nf = F.size();
+  // per-fragment starts (prefix sums), the last entry the total
+  struct Off {
+    size_t s, p, r, rres, pairs, u32, k[3], i[3];
+  };
+  std::vector<Off> o(nf + 1);
+  o[0] = Off{};
+  for (size_t f = 0; f < nf; ++f) {
+    const Fragment& x = *F[f];
+    Off& n = o[f + 1];
+    n = o[f];
+    n.s += x.sets.size();
+    n.p += x.pols.size();
+    n.r += x.rules.size();
+    n.rres += x.rres.size();
+    n.pairs += x.pairs.size();
+    n.u32 += x.u32pool.size();
+    for (int q = 0; q < 3; ++q) {
+      n.k[q] += x.spec_kind[q].size();
+      n.i[q] += x.spec_idx[q].size();
+    }
   }
-  for (NodeRec P : f.pols) {
-    P.child_begin += R0;
-    P.child_end += R0;
-    P.fe += R0;
-    shift_target(P, PA0, RR0, U0);
-    b.pols.push_back(P);
+  const Off& T = o[nf];
+  if (T.s > UINT32_MAX || T.p > UINT32_MAX || T.r > UINT32_MAX || T.rres > UINT32_MAX || T.pairs > UINT32_MAX ||
+      T.u32 > UINT32_MAX)
+    fail("store too large");
+  // body layout: 64-B header, then 16-B aligned tables and pools
+  const size_t o_sets = 64, o_pols = o_sets + a16(T.s * sizeof(NodeRec)), o_rules = o_pols + a16(T.p * sizeof(NodeRec));
+  const size_t o_rres = o_rules + a16(T.r * sizeof(NodeRec)), o_pairs = o_rres + a16(T.rres * sizeof(RuleResAttr));
+  const size_t o_u32 = o_pairs + a16(T.pairs * sizeof(Pair)), o_sec = o_u32 + a16(T.u32 * 4);
+  // codec section: header, urn ids, regex rows, kinds, spec ptr / idx, string offsets + bytes, ec
+  std::vector<uint32_t> urn_ids(N_CODEC_URNS);
+  for (int k = 0; k < N_CODEC_URNS; ++k) {
+    const JV* v = b.U(kCodecUrns[k]);
+    urn_ids[k] = v->t == J_STR ? b.intern(v) : ID_UNDEF;
   }
-  for (NodeRec Q : f.rules) {
-    shift_target(Q, PA0, RR0, U0);
-    b.rules.push_back(Q);
+  const JV* user = b.U("user");
+  const uint32_t id_user = user->t == J_UNDEF ? ID_UNDEF : b.intern(user);
+  const uint32_t n_str2 = (uint32_t)b.strings.size();  // (configure interned every URN value)
+  std::vector<uint32_t> offs{0};
+  offs.reserve(n_str2 + 1);
+  size_t sb = 0;
+  for (uint32_t i = 0; i < n_str2; ++i) {
+    if (i > ID_EMPTY) sb += b.strings[i].size();
+    offs.push_back((uint32_t)sb);
   }
-  b.rres.insert(b.rres.end(), f.rres.begin(), f.rres.end());
-  b.pairs.insert(b.pairs.end(), f.pairs.begin(), f.pairs.end());
-  b.u32pool.insert(b.u32pool.end(), f.u32pool.begin(), f.u32pool.end());
-  for (int k = 0; k < 3; ++k) {
-    b.spec_kind[k].insert(b.spec_kind[k].end(), f.spec_kind[k].begin(), f.spec_kind[k].end());
-    b.spec_rows[k].insert(b.spec_rows[k].end(), f.spec_rows[k].begin(), f.spec_rows[k].end());
+  std::string ecj = "[";
+  for (size_t k = 4; k < b.ec.size(); ++k) {
+    if (k > 4) ecj += ',';
+    ecj += b.ec[k].json;
   }
+  ecj += ']';
+  const size_t K = T.k[0] + T.k[1] + T.k[2], I = T.i[0] + T.i[1] + T.i[2];
+  const size_t c_urn = o_sec + 32, c_rx = c_urn + 4 * (size_t)N_CODEC_URNS, c_kind = c_rx + 4 * b.rx_rows.size();
+  const size_t c_ptr = c_kind + a4(K), c_idx = c_ptr + 4 * (K + 1), c_offs = c_idx + 4 * I;
+  const size_t c_sb = c_offs + 4 * (size_t)(n_str2 + 1), c_ecn = c_sb + a4(sb), c_ec = c_ecn + 4;
+  const size_t total = c_ec + a4(ecj.size());
+  if (K > UINT32_MAX || I > UINT32_MAX || sb > UINT32_MAX || total - o_sec > UINT32_MAX || o_sec > UINT32_MAX)
+    fail("store too large");
+  uint8_t* out = (uint8_t*)calloc(total, 1);  // zeroed: the padding
+  if (!out) fail("out of memory");
+  const uint32_t hdr[16] = {ACS_BLOB_MAGIC, ACS_ABI_VERSION, (uint32_t)T.s, (uint32_t)T.p, (uint32_t)T.r,
+                            (uint32_t)T.rres, (uint32_t)T.pairs, (uint32_t)T.u32, id_user, (uint32_t)o_sec,
+                            (uint32_t)(total - o_sec), 0, 0, 0, 0, 0};
+  memcpy(out, hdr, sizeof hdr);
+  const size_t kb[3] = {0, T.k[0], T.k[0] + T.k[1]}, ib[3] = {0, T.i[0], T.i[0] + T.i[1]};
+  uint32_t* ptr = (uint32_t*)(out + c_ptr);  // ptr[0] = 0 (zeroed)
+  auto write = [&](size_t f0, size_t f1) {
+    for (size_t f = f0; f < f1; ++f) {
+      const Fragment& x = *F[f];
+      const Off& at = o[f];
+      const uint32_t P0 = (uint32_t)at.p, R0 = (uint32_t)at.r, RR0 = (uint32_t)at.rres, PA0 = (uint32_t)at.pairs,
+                     U0 = (uint32_t)at.u32;
+      NodeRec* S = (NodeRec*)(out + o_sets) + at.s;
+      for (size_t k = 0; k < x.sets.size(); ++k) {
+        NodeRec n = x.sets[k];
+        n.child_begin += P0;
+        n.child_end += P0;
+        shift_target(n, PA0, RR0, U0);
+        S[k] = n;
+      }
+      NodeRec* Pp = (NodeRec*)(out + o_pols) + at.p;
+      for (size_t k = 0; k < x.pols.size(); ++k) {
+        NodeRec n = x.pols[k];
+        n.child_begin += R0;
+        n.child_end += R0;
+        n.fe += R0;
+        shift_target(n, PA0, RR0, U0);
+        Pp[k] = n;
+      }
+      NodeRec* Rr = (NodeRec*)(out + o_rules) + at.r;
+      for (size_t k = 0; k < x.rules.size(); ++k) {
+        NodeRec n = x.rules[k];
+        shift_target(n, PA0, RR0, U0);
+        Rr[k] = n;
+      }
+      if (!x.rres.empty()) memcpy(out + o_rres + at.rres * sizeof(RuleResAttr), x.rres.data(), x.rres.size() * sizeof(RuleResAttr));
+      if (!x.pairs.empty()) memcpy(out + o_pairs + at.pairs * sizeof(Pair), x.pairs.data(), x.pairs.size() * sizeof(Pair));
+      if (!x.u32pool.empty()) memcpy(out + o_u32 + at.u32 * 4, x.u32pool.data(), x.u32pool.size() * 4);
+      for (int q = 0; q < 3; ++q) {
+        const size_t k0 = kb[q] + at.k[q], i0 = ib[q] + at.i[q];
+        if (!x.spec_kind[q].empty()) memcpy(out + c_kind + k0, x.spec_kind[q].data(), x.spec_kind[q].size());
+        for (size_t k = 0; k < x.spec_end[q].size(); ++k) ptr[k0 + k + 1] = (uint32_t)(i0 + x.spec_end[q][k]);
+        if (!x.spec_idx[q].empty()) memcpy(out + c_idx + 4 * i0, x.spec_idx[q].data(), x.spec_idx[q].size() * 4);
+      }
+    }
+  };
+  // fragments split by node count over the threads
+  const size_t nodes = T.s + T.p + T.r;
+  int nt = (int)std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if ((size_t)nt > nodes / 65536 + 1) nt = (int)(nodes / 65536 + 1);
+  if ((size_t)nt > nf) nt = (int)(nf ? nf : 1);
+  std::vector<size_t> cut(nt + 1, nf);
+  cut[0] = 0;
+  for (int t = 1; t < nt; ++t) {
+    const size_t want = nodes * t / nt;
+    size_t f = cut[t - 1];
+    while (f < nf && o[f].s + o[f].p + o[f].r < want) ++f;
+    cut[t] = f;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(write, cut[t], cut[t + 1]);
+  write(cut[0], cut[1]);
+  for (auto& th : pool) th.join();
+  mark_clean_below((NodeRec*)(out + o_sets), T.s, (const NodeRec*)(out + o_pols));
+  // codec section (compiler.codec_section)
+  const uint32_t hd[8] = {0x43534341u, 2u, n_str2, (uint32_t)N_CODEC_URNS, (uint32_t)b.rx_rows.size(),
+                          (uint32_t)K, (uint32_t)I, (uint32_t)sb};
+  memcpy(out + o_sec, hd, sizeof hd);
+  memcpy(out + c_urn, urn_ids.data(), 4 * urn_ids.size());
+  if (!b.rx_rows.empty()) memcpy(out + c_rx, b.rx_rows.data(), 4 * b.rx_rows.size());
+  memcpy(out + c_offs, offs.data(), 4 * offs.size());
+  uint8_t* w = out + c_sb;
+  for (uint32_t i = ID_EMPTY + 1; i < n_str2; ++i) {
+    memcpy(w, b.strings[i].data(), b.strings[i].size());
+    w += b.strings[i].size();
+  }
+  const uint32_t ecn = (uint32_t)ecj.size();
+  memcpy(out + c_ecn, &ecn, 4);
+  memcpy(out + c_ec, ecj.data(), ecj.size());
+  *len_out = total;
+  return out;
 }
 
 // Two independent 64-bit hashes of a set's text in one pass (fragment identity: 128 bits and
@@ -726,8 +777,10 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
     Builder b;
     configure(b, urns, cas);
     for (uint32_t k = 0; k < st->n; ++k) b.compile_set(&st->a[k]);
-    mark_clean_below(b);
-    return emit(build_image(b), blob_out, blob_len);
+    Fragment all;  // every set: one fragment
+    swap_state(b, all);
+    *blob_out = write_image(b, {&all}, blob_len);
+    return 0;
   } catch (const CompileError& e) {
     g_compile_err = "acs_store_compile: " + e.why;
   } catch (const ParseError& e) {
@@ -824,14 +877,13 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
       f.len = lens[k];
       ++fresh;
     }
-    for (const Fragment& f : next) append(b, f);
-    mark_clean_below(b);
-    const std::string img = build_image(b);
-    Fragment empty;  // leave the builder's per-set state empty again
-    swap_state(b, empty);
+    std::vector<const Fragment*> parts(n);
+    for (size_t k = 0; k < n; ++k) parts[k] = &next[k];
+    void* img = write_image(b, parts, blob_len);
     sb->frags = std::move(next);
     if (recompiled) *recompiled = fresh;
-    return emit(img, blob_out, blob_len);
+    *blob_out = img;
+    return 0;
   } catch (const CompileError& e) {
     g_compile_err = "acs_store_builder_compile: " + e.why;
   } catch (const ParseError& e) {

@@ -244,7 +244,7 @@ class GpuAccessController {
     this.setIndex = setIndex;
     if (this.compileOnly) { // tooling: the image without a device (no tables / codec / pipeline)
       this.blob = blob;
-      this.index = nodeIndex(policySets);
+      this._index = null; // built on the first whatIsAllowed (a refresh stays O(changed sets))
       this.stats.compiles += 1;
       this.policySets = policySets;
       this.dirty = new Set();
@@ -263,7 +263,7 @@ class GpuAccessController {
     this.codec = codec;
     this.pipeline = pipeline;
     this.ec = ecDecoder(codec);
-    this.index = nodeIndex(policySets);
+    this._index = null; // built on the first whatIsAllowed (a refresh stays O(changed sets))
     this.scopes = this.scopes || new Map();
     for (const [k, v] of this.scopes) addon.codecSetSubjectScopes(codec, k, v);
     this.stats.compiles += 1;
@@ -271,6 +271,13 @@ class GpuAccessController {
     this.dirty = new Set();
     this.stale = false;
     this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
+  }
+
+  // node index of the compiled Map (whatIsAllowed's ReverseQuery assembly), built lazily: it
+  // walks every rule, and isAllowed-only hosts never need it
+  get index() {
+    if (!this._index) this._index = nodeIndex(this.policySets);
+    return this._index;
   }
 
   // The reference's in-memory store handlers (accessController.ts:897-937) on the Map this
