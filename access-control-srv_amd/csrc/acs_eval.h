@@ -792,10 +792,14 @@ ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) 
 // slot, the tables' common scoping entity T.se0 and the values of its first two role
 // associations: every candidate rule after the first of a role reuses the outcome instead of
 // re-reading the arena.
+#ifndef ACS_AB_NO_HR_MEMO  // A/B builds: no memo (same records)
+#define ACS_AB_NO_HR_MEMO 0
+#endif
 ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   const uint32_t ms = R.hrm & 0xFFu;
   uint32_t k = 2;
-  if (se == R.T.se0 && (ms == 0xFFu || ms == slot)) k = role == R.role0 ? 0u : (role == R.role1 ? 1u : 2u);
+  if (!ACS_AB_NO_HR_MEMO && se == R.T.se0 && (ms == 0xFFu || ms == slot))
+    k = role == R.role0 ? 0u : (role == R.role1 ? 1u : 2u);
   if (k < 2) {
     const uint32_t sh = 8 + 3 * k;
     if ((R.hrm >> sh) & 1u) return (R.hrm >> (sh + 1)) & 3u;

@@ -38,6 +38,7 @@ function apply(ctl, st) {
 (async () => {
   const out = [];
   const maps = load(sc.doc);
+  sc.doc = null; // the Maps hold the store (c5: 1M rules in the default V8 heap)
   if (mode === 'latency') {
     const t0 = Date.now();
     const ctl = new g.GpuAccessController(maps, sc.urns, sc.cas, { threads: 8 });
