@@ -66,7 +66,39 @@ struct Tables {
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
   uint32_t se0;      // the most common roleScopingEntity of the targets (hr_owner_bits' memo key)
+  const uint32_t* ev_index;  // event index (build_event_index; nullptr: K1 never skips a set for it)
 };
+
+// K1's event index (is_allowed_body's events-only skip): per set its rules' range [r0, r1) and,
+// in bit 31 of the r1 word, whether it holds a null policy or a policy with an invalid combining
+// algorithm (events that need no rule); then one bit per rule carrying a condition.
+// event_index_words(n_sets, n_rules) u32 words, built on the host from the blob's records.
+inline size_t event_index_words(uint32_t n_sets, uint32_t n_rules) {
+  return 2 * (size_t)n_sets + ((size_t)n_rules + 31) / 32;
+}
+inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols,
+                              const NodeRec* rules, uint32_t n_rules, uint32_t* out) {
+  for (uint32_t s = 0; s < n_sets; ++s) {
+    const NodeRec& S = sets[s];
+    uint32_t r0 = 0xFFFFFFFFu, r1 = 0;
+    bool bare = false;  // an event source without any rule
+    for (uint32_t p = S.child_begin; p < S.child_end && p < n_pols; ++p) {
+      const NodeRec& P = pols[p];
+      if ((P.nflags & NF_NULL) || P.ca == CA_INVALID) bare = true;
+      if (P.child_end > P.child_begin) {
+        r0 = P.child_begin < r0 ? P.child_begin : r0;
+        r1 = P.child_end > r1 ? P.child_end : r1;
+      }
+    }
+    if (r0 >= r1) r0 = r1 = 0;
+    out[2 * s] = r0;
+    out[2 * s + 1] = (r1 & 0x7FFFFFFFu) | (bare ? 0x80000000u : 0u);
+  }
+  uint32_t* cb = out + 2 * (size_t)n_sets;
+  for (uint32_t w = 0; w < (n_rules + 31) / 32; ++w) cb[w] = 0;
+  for (uint32_t r = 0; r < n_rules; ++r)
+    if (rules[r].nflags & NF_HAS_CONDITION) cb[r >> 5] |= 1u << (r & 31);
+}
 
 // The roleScopingEntity most targets carry (hr_owner_bits memoises checkHierarchicalScope's
 // owner tests for it): a Boyer-Moore majority vote over the nodes' non-empty `se` (the majority
@@ -1120,6 +1152,30 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   return SET_EFFECT;
 }
 
+// Whether set s can raise an event for a safe request of this filter (is_allowed_body below the
+// deciding set): it holds a null policy or an invalid combining algorithm, or one of its rules
+// that carries a condition is a candidate of some active lane (a rule no lane can match cannot be
+// reached, and a safe request throws nowhere else).
+template <class FL>
+ACS_FN bool set_may_raise(const Tables& T, const FL& F, uint32_t s) {
+  if (!T.ev_index) return true;
+  const uint32_t r0 = T.ev_index[2 * s], w1 = T.ev_index[2 * s + 1];
+  if (w1 >> 31) return true;
+  const uint32_t r1 = w1 & 0x7FFFFFFFu;
+  if (r0 >= r1) return false;
+  const uint32_t* cb = T.ev_index + 2 * (size_t)T.n_sets;
+  const uint32_t w0 = r0 >> 5, wl = (r1 - 1) >> 5;
+  for (uint32_t w = w0; w <= wl; ++w) {
+    uint32_t m = ~0u;
+    if (w == w0) m &= ~0u << (r0 & 31);
+    if (w == wl) m &= ~0u >> (31 - ((r1 - 1) & 31));
+    const uint32_t c = cb[w] & m;
+    ACS_SCAN(4);
+    if (c && (F.word(F.wr + w) & c)) return true;
+  }
+  return false;
+}
+
 // isAllowed over the sets LAST TO FIRST.  Forward, the reference lets the last set with an
 // effect decide (`effect` is overwritten per set, :293-295) unless an earlier set ends the
 // request (the first error / reached condition).  So walking backwards, the first effect
@@ -1155,6 +1211,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     uint8_t e2 = EFF_UNDEF, c2 = EC_UNDEF;
     Decision d2{};
     const bool events_only = (have_ev || last_set) && safe && S.ca != CA_INVALID;
+    if (events_only && !set_may_raise(T, F, s)) continue;
     const int o = eval_set(R, F, s, S, safe, events_only, &e2, &c2, &d2);
     if (o == SET_EVENT) {
       ev = d2;  // lower than any event found so far

@@ -1145,12 +1145,19 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   } else {
     for (int k = 0; k < 6; ++k) doff[k] = off[k];
   }
+  // the event index (acs_eval.h build_event_index) after the image, from the blob's records
+  std::vector<uint32_t> evx(event_index_words(h.n_sets, h.n_rules));
+  build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
+                    (const NodeRec*)(bsrc + off[2]), h.n_rules, evx.data());
+  const size_t ev_off = align16(up_bytes);
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
-  const size_t img_total = up_bytes;
+  const size_t img_total = ev_off + evx.size() * sizeof(uint32_t);
   const bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess &&
-                      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess;
+                      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess &&
+                      (evx.empty() || hipMemcpy((char*)t->dev + ev_off, evx.data(), evx.size() * sizeof(uint32_t),
+                                                hipMemcpyHostToDevice) == hipSuccess);
   if (!copied ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
@@ -1171,6 +1178,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
+  t->view.ev_index = (const uint32_t*)(base + ev_off);
   {
     ScopingEntityVote v;  // (the blob's records: 16-B aligned sections, whole 64-B records)
     const uint32_t cnt[3] = {h.n_sets, h.n_pols, h.n_rules};
@@ -1235,6 +1243,7 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
     r->view.rres = (const RuleResAttr*)rebase(t->view.rres);
     r->view.pairs = (const Pair*)rebase(t->view.pairs);
     r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
+    r->view.ev_index = (const uint32_t*)rebase(t->view.ev_index);
     r->sort = t->sort;
     t->peers.push_back(r);
   }

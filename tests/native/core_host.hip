@@ -5,6 +5,7 @@
 // product library (libacs_mi355x.so has no CPU path).
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../include/acs_mi355x.h"
 #include "../../access-control-srv_amd/csrc/acs_eval.h"
@@ -42,6 +43,11 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   for (uint32_t k = 0; k < h.n_pols; ++k) v.add(T->pols[k].se);
   for (uint32_t k = 0; k < h.n_rules; ++k) v.add(T->rules[k].se);
   T->se0 = v.value;
+  // the event index (one per thread: the host entry points are called one batch at a time)
+  static thread_local std::vector<uint32_t> evx;
+  evx.assign(event_index_words(h.n_sets, h.n_rules), 0u);
+  build_event_index(T->sets, h.n_sets, T->pols, h.n_pols, T->rules, h.n_rules, evx.data());
+  T->ev_index = getenv("ACS_HOST_NO_EV_INDEX") ? nullptr : evx.data();
   return true;
 }
 

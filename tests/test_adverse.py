@@ -70,6 +70,29 @@ def test_adverse_host_core_vs_oracle(adverse):
     assert np.array_equal(host_core.is_allowed(cs, nb).view(np.uint64), dec.view(np.uint64))
 
 
+def test_adverse_event_index_changes_no_record(adverse, monkeypatch):
+    """The event index (acs_eval.h set_may_raise: below the deciding set, skip a set none of whose
+    condition rules is a candidate and that holds no null policy / invalid algorithm) gives the
+    records of the walk without it, over every filter form (class rows, role factor, none)."""
+    from acs_mi355x import candidates
+    _, cs, sb = adverse
+    reqs = [sb.decode(i) for i in range(sb.batch.n)]
+    for level in (None, "entity+action", "entity"):
+        monkeypatch.setattr(candidates, "FORCE_LEVEL", level)
+        b = encoder.Encoder(cs).encode(reqs)
+        with_ix = host_core.is_allowed(cs, b).view(np.uint64)
+        monkeypatch.setenv("ACS_HOST_NO_EV_INDEX", "1")
+        without = host_core.is_allowed(cs, b).view(np.uint64)
+        monkeypatch.delenv("ACS_HOST_NO_EV_INDEX")
+        assert np.array_equal(with_ix, without), level
+    b.cand = None
+    b.role_key = b.role_bits = None
+    b.lines["cls2"] = 0
+    with_ix = host_core.is_allowed(cs, b).view(np.uint64)
+    monkeypatch.setenv("ACS_HOST_NO_EV_INDEX", "1")
+    assert np.array_equal(with_ix, host_core.is_allowed(cs, b).view(np.uint64))
+
+
 @pytest.mark.gpu
 def test_adverse_gpu(adverse):
     torch = pytest.importorskip("torch")
