@@ -594,6 +594,35 @@ class NativeStoreBuilder:
         finally:
             self.lib.acs_blob_free(out)
 
+    def stage(self, text: bytes) -> int:
+        """acs_store_builder_stage: one set's text taken ahead of the next compile; returns the
+        handle to pass in compile_items."""
+        C = self.C
+        self.lib.acs_store_builder_stage.restype = C.c_longlong
+        self.lib.acs_store_builder_stage.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        h = self.lib.acs_store_builder_stage(self.h, text, len(text))
+        if h < 0:
+            raise Unsupported(self._err(self.lib))
+        return h
+
+    def compile_items(self, items) -> bytes:
+        """items[k]: set k's text (bytes), ("prev", j) = the previous compile's set j, or
+        ("staged", h) = a stage() handle."""
+        C = self.C
+        n = len(items)
+        staged = 1 << (8 * C.sizeof(C.c_size_t) - 1)
+        arr = (C.c_char_p * n)(*[x if isinstance(x, bytes) else None for x in items])
+        lens = (C.c_size_t * n)(*[len(x) if isinstance(x, bytes) else (x[1] if x[0] == "prev" else staged | x[1])
+                                  for x in items])
+        out, nb, rec = C.c_void_p(), C.c_size_t(), C.c_size_t()
+        if self.lib.acs_store_builder_compile(self.h, arr, lens, n, C.byref(out), C.byref(nb), C.byref(rec)) != 0:
+            raise Unsupported(self._err(self.lib))
+        self.recompiled = rec.value
+        try:
+            return C.string_at(out.value, nb.value)
+        finally:
+            self.lib.acs_blob_free(out)
+
     def compile(self, policy_sets: dict) -> bytes:
         return self.compile_texts(set_texts(policy_sets))
 

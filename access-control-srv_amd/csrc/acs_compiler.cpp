@@ -755,7 +755,40 @@ struct acs_store_builder {
   Arena ar;
   Builder b;
   std::vector<Fragment> frags;      // the last compile's sets, in Map order
+  // sets staged for the next compile (acs_store_builder_stage): compiled, or the previous
+  // compile's fragment reuse_of with the same text (reserved so two stagings never share one)
+  struct Staged {
+    Fragment f;
+    size_t reuse_of = SIZE_MAX;
+  };
+  std::vector<Staged> staged;
+  std::vector<bool> reserved;       // frags reserved by a staging
+  std::unordered_multimap<uint64_t, size_t> by_hash;  // frags by text hash (h1)
 };
+
+namespace {
+
+// Compile one set's text into a fragment (the builder's per-set state is empty between
+// compiles; the dictionary and regex rows grow).
+void compile_fragment(Builder& b, const char* text, size_t len, uint64_t h1, uint64_t h2, Fragment& f) {
+  Arena ar;
+  Parser p(ar);
+  const JV* ps = p.parse(text, text + len);
+  swap_state(b, f);
+  try {
+    b.compile_set(ps);
+  } catch (...) {
+    swap_state(b, f);
+    f = Fragment{};
+    throw;
+  }
+  swap_state(b, f);
+  f.h1 = h1;
+  f.h2 = h2;
+  f.len = len;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -819,6 +852,39 @@ acs_store_builder* acs_store_builder_create(const char* urns_json, size_t urns_l
 
 void acs_store_builder_free(acs_store_builder* sb) { delete sb; }
 
+long long acs_store_builder_stage(acs_store_builder* sb, const char* set_json, size_t len) {
+  if (!sb || !set_json) {
+    acs_internal_set_error("acs_store_builder_stage: null argument");
+    return -1;
+  }
+  try {
+    uint64_t h1, h2;
+    text_hash(set_json, len, &h1, &h2);
+    acs_store_builder::Staged st;
+    if (sb->reserved.size() != sb->frags.size()) sb->reserved.assign(sb->frags.size(), false);
+    auto range = sb->by_hash.equal_range(h1);
+    for (auto it = range.first; it != range.second; ++it) {
+      const Fragment& f = sb->frags[it->second];
+      if (!sb->reserved[it->second] && f.h2 == h2 && f.len == len) {
+        st.reuse_of = it->second;
+        sb->reserved[it->second] = true;
+        break;
+      }
+    }
+    if (st.reuse_of == SIZE_MAX) compile_fragment(sb->b, set_json, len, h1, h2, st.f);
+    sb->staged.push_back(std::move(st));
+    return (long long)sb->staged.size() - 1;
+  } catch (const CompileError& e) {
+    g_compile_err = "acs_store_builder_stage: " + e.why;
+  } catch (const ParseError& e) {
+    g_compile_err = std::string("acs_store_builder_stage: ") + e.what;
+  } catch (const std::exception& e) {
+    g_compile_err = std::string("acs_store_builder_stage: ") + e.what();
+  }
+  acs_internal_set_error(g_compile_err.c_str());
+  return -1;
+}
+
 int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, const size_t* lens, size_t n,
                               void** blob_out, size_t* blob_len, size_t* recompiled) {
   if (!sb || (n && (!sets || !lens)) || !blob_out || !blob_len) {
@@ -836,13 +902,40 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
     std::unordered_multimap<uint64_t, size_t> old;
     for (size_t k = 0; k < sb->frags.size(); ++k) old.emplace(sb->frags[k].h1, k);
     std::vector<bool> taken(sb->frags.size(), false);
+    std::vector<size_t> taken_by(sb->frags.size(), SIZE_MAX);  // the slot that holds frags[j] now
+    std::vector<bool> staged_used(sb->staged.size(), false);
+    // pass 1: the caller's unchanged sets (set k is the previous compile's set lens[k])
     for (size_t k = 0; k < n; ++k) {
-      if (!sets[k]) {  // the caller's word: set k is the previous compile's set lens[k], unchanged
-        const size_t j = lens[k];
-        if (j >= sb->frags.size() || taken[j]) fail("unchanged-set index out of range or repeated");
+      if (sets[k] || (lens[k] & ACS_BUILDER_STAGED)) continue;
+      const size_t j = lens[k];
+      if (j >= sb->frags.size() || taken[j]) fail("unchanged-set index out of range or repeated");
+      next[k] = std::move(sb->frags[j]);
+      from[k] = j;
+      taken[j] = true;
+      taken_by[j] = k;
+    }
+    // pass 2: staged sets and texts
+    for (size_t k = 0; k < n; ++k) {
+      if (!sets[k] && !(lens[k] & ACS_BUILDER_STAGED)) continue;
+      if (!sets[k]) {  // a staged set
+        const size_t h = lens[k] & ~ACS_BUILDER_STAGED;
+        if (h >= sb->staged.size() || staged_used[h]) fail("staged-set handle out of range or repeated");
+        staged_used[h] = true;
+        acs_store_builder::Staged& st = sb->staged[h];
+        if (st.reuse_of == SIZE_MAX) {
+          next[k] = std::move(st.f);
+          ++fresh;
+          continue;
+        }
+        const size_t j = st.reuse_of;
+        if (taken[j]) {  // the same text is also an unchanged set: a copy of its fragment
+          next[k] = next[taken_by[j]];
+          continue;
+        }
         next[k] = std::move(sb->frags[j]);
         from[k] = j;
         taken[j] = true;
+        taken_by[j] = k;
         continue;
       }
       uint64_t h1, h2;
@@ -855,32 +948,22 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
           next[k] = std::move(f);
           from[k] = it->second;
           taken[it->second] = true;
+          taken_by[it->second] = k;
           reused = true;
         }
       }
       if (reused) continue;
-      Arena ar;
-      Parser p(ar);
-      const JV* ps = p.parse(sets[k], sets[k] + lens[k]);
-      Fragment& f = next[k];
-      swap_state(b, f);  // the builder's per-set state is empty between compiles
-      try {
-        b.compile_set(ps);
-      } catch (...) {
-        swap_state(b, f);
-        f = Fragment{};
-        throw;
-      }
-      swap_state(b, f);
-      f.h1 = h1;
-      f.h2 = h2;
-      f.len = lens[k];
+      compile_fragment(b, sets[k], lens[k], h1, h2, next[k]);
       ++fresh;
     }
     std::vector<const Fragment*> parts(n);
     for (size_t k = 0; k < n; ++k) parts[k] = &next[k];
     void* img = write_image(b, parts, blob_len);
     sb->frags = std::move(next);
+    sb->staged.clear();
+    sb->reserved.assign(sb->frags.size(), false);
+    sb->by_hash.clear();
+    for (size_t k = 0; k < sb->frags.size(); ++k) sb->by_hash.emplace(sb->frags[k].h1, k);
     if (recompiled) *recompiled = fresh;
     *blob_out = img;
     return 0;
@@ -897,6 +980,8 @@ int acs_store_builder_compile(acs_store_builder* sb, const char* const* sets, co
   // moved out go back (the dictionary only grew), so a caller's unchanged-set indices stay valid
   for (size_t k = 0; k < n; ++k)
     if (from[k] != SIZE_MAX) sb->frags[from[k]] = std::move(next[k]);
+  sb->staged.clear();  // consumed either way (the caller stages again)
+  sb->reserved.assign(sb->frags.size(), false);
   acs_internal_set_error(g_compile_err.c_str());
   return -1;
 }

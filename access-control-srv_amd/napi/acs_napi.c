@@ -9,8 +9,10 @@
  * JS surface:
  *   compileStore(storeJson, urnsJson, casJson) -> Uint8Array   acs_store_compile
  *   storeBuilderCreate(urnsJson, casJson) -> builder            acs_store_builder_create
+ *   storeBuilderStage(builder, setJson) -> -(1 + h)             acs_store_builder_stage
  *   storeBuilderCompile(builder, sets[]) -> {blob, recompiled}  acs_store_builder_compile
- *     (sets[k]: set k's JSON text, or j = the previous compile's set j, unchanged)
+ *     (sets[k]: set k's JSON text, j >= 0 = the previous compile's set j, unchanged, or a
+ *     storeBuilderStage result)
  *   storeBuilderFree(builder)                                   acs_store_builder_free
  *   compile(blob: Uint8Array, device?) -> tables                acs_compile
  *     (device = [d0, d1, ...]: one image per device, acs_compile_multi)
@@ -612,11 +614,11 @@ static napi_value js_builder_compile(napi_env env, napi_callback_info info) {
     napi_valuetype t;
     ok = napi_get_element(env, argv[1], k, &e) == napi_ok && napi_typeof(env, e, &t) == napi_ok;
     if (!ok) break;
-    if (t == napi_number) {
-      int64_t j = -1;
-      ok = napi_get_value_int64(env, e, &j) == napi_ok && j >= 0;
+    if (t == napi_number) {  /* j >= 0: previous set j; j < 0: staged handle -(j + 1) */
+      int64_t j = 0;
+      ok = napi_get_value_int64(env, e, &j) == napi_ok;
       texts[k] = NULL;
-      lens[k] = (size_t)j;
+      lens[k] = j >= 0 ? (size_t)j : (ACS_BUILDER_STAGED | (size_t)(-(j + 1)));
     } else {
       char* p = NULL;
       ok = get_text(env, e, &p, &lens[k], &own[k]) == 0;
@@ -647,6 +649,36 @@ static napi_value js_builder_compile(napi_env env, napi_callback_info info) {
   free(texts);
   free(lens);
   free(own);
+  return ret;
+}
+
+/* storeBuilderStage(builder, setJson) -> -(1 + handle): one set's text staged for the next
+ * storeBuilderCompile (acs_store_builder_stage); pass the returned number in its sets[]. */
+static napi_value js_builder_stage(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  int freed = 0;
+  builder_h* h = argc == 2 ? (builder_h*)lookup(env, argv[0], H_BUILDER, &freed) : NULL;
+  if (!h) {
+    napi_throw_type_error(env, NULL, freed ? "store builder already freed" : "storeBuilderStage(builder, setJson)");
+    return NULL;
+  }
+  char* p = NULL;
+  size_t len = 0;
+  int own = 0;
+  if (get_text(env, argv[1], &p, &len, &own) != 0) {
+    napi_throw_type_error(env, NULL, "storeBuilderStage: setJson must be a string or bytes");
+    return NULL;
+  }
+  const long long id = acs_store_builder_stage(h->b, p, len);
+  if (own) free(p);
+  if (id < 0) {
+    throw_acs(env, "acs_store_builder_stage");
+    return NULL;
+  }
+  napi_value ret;
+  CHECK(env, napi_create_double(env, -(double)(id + 1), &ret));
   return ret;
 }
 
@@ -1454,6 +1486,7 @@ static napi_value init(napi_env env, napi_value exports) {
   const napi_property_descriptor d[] = {
       {"compileStore", NULL, js_compile_store, NULL, NULL, NULL, napi_enumerable, NULL},
       {"storeBuilderCreate", NULL, js_builder_create, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"storeBuilderStage", NULL, js_builder_stage, NULL, NULL, NULL, napi_enumerable, NULL},
       {"storeBuilderCompile", NULL, js_builder_compile, NULL, NULL, NULL, napi_enumerable, NULL},
       {"storeBuilderFree", NULL, js_builder_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -230,12 +230,15 @@ class GpuAccessController {
     const entries = policySets instanceof Map ? Array.from(policySets.entries())
       : mapValues(policySets).map((ps, k) => [k, ps]);
     const items = new Array(entries.length);
+    this.stale = true;
     for (let k = 0; k < entries.length; ++k) {
       const [key, ps] = entries[k];
       const prev = this.setIndex.get(key);
-      items[k] = dirty && prev && prev.obj === ps && !dirty.has(key) ? prev.index : JSON.stringify(snapshotSet(ps));
+      // a changed set's text is staged at once (compiled, or matched to its unchanged fragment),
+      // so no more than one set's JSON text is held at a time (c5: 1M rules in V8's default heap)
+      items[k] = dirty && prev && prev.obj === ps && !dirty.has(key) ? prev.index
+        : addon.storeBuilderStage(this.builder, JSON.stringify(snapshotSet(ps)));
     }
-    this.stale = true;
     const r = addon.storeBuilderCompile(this.builder, items); // throws: the builder is unchanged
     const blob = r.blob;
     // the builder now holds this compile's fragments, in this Map order

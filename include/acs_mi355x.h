@@ -263,11 +263,19 @@ void acs_blob_free(void* blob);
  * rest with shifted offsets.  Interned strings only accumulate (ids stay valid); the first
  * compile of a builder is byte-identical to acs_store_compile of the same store.
  * sets[k] / lens[k]: set k's JSON text in Map order — or sets[k] = NULL and lens[k] = j: set k
- * is set j of the previous compile, unchanged (no text passed, nothing hashed); *recompiled:
- * sets compiled afresh. */
+ * is set j of the previous compile, unchanged (no text passed, nothing hashed) — or sets[k] =
+ * NULL and lens[k] = ACS_BUILDER_STAGED | h: the set staged as handle h; *recompiled: sets
+ * compiled afresh.
+ * acs_store_builder_stage: one set's JSON text taken ahead of the next compile (compiled now,
+ * or matched to an unchanged fragment of the previous compile by its text), so a host can
+ * serialise a large store one set at a time instead of holding every set's text at once.
+ * Returns the handle (>= 0) or -1 (the set does not compile; the error names it).  A compile
+ * consumes every staged set, used or not. */
 typedef struct acs_store_builder acs_store_builder;
+#define ACS_BUILDER_STAGED ((size_t)1 << (8 * sizeof(size_t) - 1))
 acs_store_builder* acs_store_builder_create(const char* urns_json, size_t urns_len, const char* cas_json,
                                             size_t cas_len);
+long long acs_store_builder_stage(acs_store_builder* b, const char* set_json, size_t len);
 int acs_store_builder_compile(acs_store_builder* b, const char* const* sets, const size_t* lens, size_t n,
                               void** blob_out, size_t* blob_len, size_t* recompiled);
 void acs_store_builder_free(acs_store_builder* b);

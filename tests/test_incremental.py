@@ -197,6 +197,47 @@ def test_native_builder_matches_fresh_compile(seed):
     b.close()
 
 
+@pytest.mark.parametrize("seed", range(0, 40, 2))
+def test_native_builder_staged_sets(seed):
+    """acs_store_builder_stage (the Node drop-in stages one set's text at a time): staging every
+    set gives the text compile's image byte for byte; restaging an unchanged set reuses its
+    fragment (nothing recompiled); a mutated set staged beside previous-set indices decides like
+    a fresh compile; a staging that does not compile leaves the builder as it was."""
+    urns, doc, reqs = randgen.rand_case(seed)
+    try:
+        base = pstore.populate(doc)
+        first = compiler.native_store_blob(base, urns, DEFAULT_CAS)
+    except Exception:
+        pytest.skip("store outside the compiled subset")
+    texts = compiler.set_texts(base)
+    b = compiler.NativeStoreBuilder(urns, DEFAULT_CAS)
+    assert b.compile_items([("staged", b.stage(t)) for t in texts]) == first and b.recompiled == len(texts)
+    assert b.compile_items([("staged", b.stage(t)) for t in texts]) == first and b.recompiled == 0
+    rng = random.Random(seed)
+    donors = list(pstore.populate(randgen.rand_case(seed + 1000)[1]).values()) or list(base.values())
+    ctl = _ctl(urns)
+    ctl.policySets = base
+    for step in range(4):
+        _mutate(rng, ctl, donors)
+        try:
+            fresh = compiler.native_store_blob(ctl.policySets, urns, DEFAULT_CAS)
+        except compiler.Unsupported:
+            return
+        new_texts = compiler.set_texts(ctl.policySets)
+        old = {t: k for k, t in enumerate(texts)}
+        items = []
+        for t in new_texts:  # unchanged texts by index (once each), the rest staged
+            j = old.pop(t, None)
+            items.append(("prev", j) if j is not None else ("staged", b.stage(t)))
+        blob = b.compile_items(items)
+        assert np.array_equal(_native_records(blob, reqs), _native_records(fresh, reqs)), (seed, step)
+        texts = new_texts
+    with pytest.raises(compiler.Unsupported):
+        b.stage(b'{"combinables": 7}')
+    assert b.compile_items([("prev", k) for k in range(len(texts))]) == blob and b.recompiled == 0
+    b.close()
+
+
 def test_fresh_compile_is_byte_stable():
     """compile_store (one IncrementalCompiler pass) gives the same blob twice."""
     m = pstore.populate(synth.c2_store())
