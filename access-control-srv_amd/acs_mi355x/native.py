@@ -34,7 +34,7 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_layout_sizes", "acs_device_count", "acs_set_option", "acs_kernel_times",
            "acs_shard_keys_device", "acs_shard_decode_device", "acs_what_is_allowed_obl",
            "acs_what_is_allowed_obl_device", "acs_store_compile", "acs_blob_free", "acs_store_builder_create",
-           "acs_store_builder_compile", "acs_store_builder_free", "acs_codec_create",
+           "acs_store_builder_stage", "acs_store_builder_compile", "acs_store_builder_free", "acs_codec_create",
            "acs_codec_free", "acs_codec_set_subject_scopes", "acs_codec_evict_subject", "acs_codec_encode",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",

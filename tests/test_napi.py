@@ -35,7 +35,7 @@ def test_addon_loads_with_surface():
                                    "codecSetSubjectScopes",
                                    "codecEvictSubject", "codecEcValues", "encode", "batchInfo", "batchString",
                                    "decideAsync", "pipelineCreate", "pipelineFree", "pipelineDecideAsync",
-                                   "storeBuilderCreate", "storeBuilderCompile", "storeBuilderFree",
+                                   "storeBuilderCreate", "storeBuilderStage", "storeBuilderCompile", "storeBuilderFree",
                                    "devices", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
                                    "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
     assert info["sizes"] == [64, 16, 16, 16, 8]
