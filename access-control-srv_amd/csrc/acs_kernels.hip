@@ -1755,7 +1755,14 @@ static bool split_across_devices(const acs_tables* t, const acs_req_batch* b) {
   return !t->peers.empty() && !b->hdr && b->lines && b->n >= 2 * MULTI_MIN_PER_DEVICE;
 }
 
-static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out, const uint32_t* arena_end) {
+// Run `shard(T, d, lo, hi)` for each device's contiguous shard [lo, hi) of a compact batch: d is
+// the shard uploaded to T (its slices, its coherence order), shard queues T's kernels and its
+// copies into the caller's buffers on T->stream (returning nonzero on failure); then every
+// device is synchronised.  On a failure every shard already queued is drained first (the caller
+// may free its buffers, and the next call reuses the workspaces).
+extern "C++" {
+template <class F>
+static int multi_run(acs_tables* t, const acs_req_batch* b, const uint32_t* arena_end, const char* what, F shard) {
   std::vector<acs_tables*> dev{t};
   dev.insert(dev.end(), t->peers.begin(), t->peers.end());
   size_t D = dev.size();
@@ -1777,10 +1784,7 @@ static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision*
   }
   std::vector<std::unique_lock<std::mutex>> locks;
   for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
-  size_t launched = 0;  // devices with work queued into `out`
-  // on a failure, wait for every shard already queued (its kernel and its copy into the
-  // caller's `out`) before returning: the caller may free `out` and the next call reuse the
-  // workspaces
+  size_t launched = 0;  // devices with work queued into the caller's buffers
   auto drain = [&] {
     const std::string err = g_err;
     for (size_t k = 0; k < launched; ++k) {
@@ -1791,25 +1795,61 @@ static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision*
     g_err = err;
     return -1;
   };
+  const std::string sync_msg = std::string(what) + ": device synchronisation failed";
   for (size_t k = 0; k < D; ++k) {
     acs_tables* T = dev[k];
     const size_t lo = lo_of(k), hi = lo_of(k + 1);
-    if (hipSetDevice(T->device) != hipSuccess) return fail("acs_is_allowed: hipSetDevice failed"), drain();
+    if (hipSetDevice(T->device) != hipSuccess) return fail(sync_msg.c_str()), drain();
     launched = k + 1;  // the copies below are queued on T's stream from here on
     acs_req_batch d;
     if (upload_shard(T->hws, b, lo, hi, arena_end, sperm[k], &d, T->stream)) return drain();
-    if (T->hws.out.reserve((hi - lo) * sizeof(Decision))) return drain();
-    if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return drain();
-    if (hipMemcpyAsync(out + lo, T->hws.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, T->stream) !=
-        hipSuccess)
-      return fail("acs_is_allowed: result copy failed"), drain();
+    if (shard(T, &d, lo, hi)) return drain();
   }
   for (size_t k = 0; k < D; ++k) {
     if (hipSetDevice(dev[k]->device) != hipSuccess || hipStreamSynchronize(dev[k]->stream) != hipSuccess)
-      return fail("acs_is_allowed: device synchronisation failed"), drain();
+      return fail(sync_msg.c_str()), drain();
   }
   HIP_OK(hipSetDevice(t->device));
   return 0;
+}
+}  // extern "C++"
+
+static int multi_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out, const uint32_t* arena_end) {
+  return multi_run(t, b, arena_end, "acs_is_allowed", [&](acs_tables* T, const acs_req_batch* d, size_t lo, size_t hi) {
+    if (T->hws.out.reserve((hi - lo) * sizeof(Decision))) return -1;
+    if (is_allowed_launch(T, T->hws, d, (acs_decision*)T->hws.out.p, T->stream)) return -1;
+    if (hipMemcpyAsync(out + lo, T->hws.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, T->stream) !=
+        hipSuccess)
+      return fail("acs_is_allowed: result copy failed");
+    return 0;
+  });
+}
+
+// whatIsAllowed over the replicas: each device decides its shard and writes its rows of the
+// caller's bitset / logs / records (the same bytes as one device: K2 is per request).
+static int multi_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
+                                 uint32_t* obl_n, acs_decision* out, const uint32_t* arena_end) {
+  const size_t words = acs_wia_words_per_request(t);
+  return multi_run(t, b, arena_end, "acs_what_is_allowed",
+                   [&](acs_tables* T, const acs_req_batch* d, size_t lo, size_t hi) {
+    const size_t m = hi - lo;
+    OutLayout O;
+    const size_t o_bits = O.put(m * words * sizeof(uint32_t)), o_obl = O.put(m * 2 * OBL_MAX * sizeof(uint32_t));
+    const size_t o_n = O.put(m * sizeof(uint32_t)), o_out = O.put(m * sizeof(Decision));
+    if (T->hws.out.reserve(O.total)) return -1;
+    char* ob = (char*)T->hws.out.p;
+    if (what_is_allowed_launch(T, T->hws, d, (uint32_t*)(ob + o_bits), (uint32_t*)(ob + o_obl),
+                               (uint32_t*)(ob + o_n), (acs_decision*)(ob + o_out), T->stream))
+      return -1;
+    if (hipMemcpyAsync(bits + lo * words, ob + o_bits, m * words * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       T->stream) != hipSuccess ||
+        hipMemcpyAsync(obl + lo * 2 * OBL_MAX, ob + o_obl, m * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       T->stream) != hipSuccess ||
+        hipMemcpyAsync(obl_n + lo, ob + o_n, m * sizeof(uint32_t), hipMemcpyDeviceToHost, T->stream) != hipSuccess ||
+        hipMemcpyAsync(out + lo, ob + o_out, m * sizeof(Decision), hipMemcpyDeviceToHost, T->stream) != hipSuccess)
+      return fail("acs_what_is_allowed: result copy failed");
+    return 0;
+  });
 }
 
 int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
@@ -1842,6 +1882,13 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
                         acs_decision* out) {
   if (!t || !b || (b->n && (!bits || !obl || !obl_n || !out))) return fail("acs_what_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (split_across_devices(t, b)) {
+    std::vector<uint32_t> arena_end(b->n);
+    if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
+                                  arena_end.data()))
+      return -1;
+    return multi_what_is_allowed(t, b, bits, obl, obl_n, out, arena_end.data());
+  }
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));

@@ -121,10 +121,12 @@ void acs_free(acs_tables* t);
 /* Multi-GPU (requests are independent, accessController.ts:125-297 keeps no
  * cross-request state): one image replicated to every device in `devices` (C0: uploaded to
  * devices[0], copied to the others over xGMI).  The host-buffer entry points (acs_is_allowed,
- * acs_pipeline_*) then split a compact batch into contiguous shards, one per device, each on
- * its own stream with only its shard's request lines / extension records / arena words
- * uploaded, and gather the records in request order; the *_device entry points use
- * devices[0].  acs_device_list: the handle's devices (returns their count). */
+ * acs_what_is_allowed, acs_pipeline_*) then split a compact batch of >= 8192 requests into
+ * contiguous shards, one per device, each on its own stream with only its shard's request
+ * lines / extension records / arena words uploaded, and gather the records (whatIsAllowed: the
+ * bitset rows and logs too) in request order; the *_device entry points and
+ * acs_what_is_allowed_obl use devices[0].  acs_last_kernel_ms is not set by a split call.
+ * acs_device_list: the handle's devices (returns their count). */
 acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 int acs_device_list(const acs_tables* t, int* devices, int n);
 

@@ -6,8 +6,8 @@ request order.
 
 CPU: the same split (plan + slice copies + rebased pointers) run through the CPU build of
 the evaluator core shard by shard equals the whole batch.  GPU: a handle replicated on
-device 0 twice (two images, two streams) equals a single handle, through acs_is_allowed
-and the pipeline."""
+device 0 twice (two images, two streams) equals a single handle, through acs_is_allowed,
+acs_what_is_allowed and the pipeline."""
 import ctypes as C
 
 import numpy as np
@@ -34,9 +34,10 @@ def _plan_lib():
     return lib
 
 
-def split_is_allowed_host(cs, batch, cuts):
-    """acs_is_allowed's multi-device split restated over the host core: shards [cuts[k],
-    cuts[k+1]) each evaluated from copies of only its slices."""
+def split_is_allowed_host(cs, batch, cuts, what=False):
+    """acs_is_allowed's (what: acs_what_is_allowed's) multi-device split restated over the host
+    core: shards [cuts[k], cuts[k+1]) each evaluated from copies of only its slices; what
+    returns (bits, obl, obl_n, out) gathered in request order."""
     lib = _plan_lib()
     s = native.host_struct(batch, True)
     n = int(s.n)
@@ -48,6 +49,12 @@ def split_is_allowed_host(cs, batch, cuts):
            else np.zeros(0, np.uint32))
     out = np.zeros(n, host_core.L.DECISION_DT)
     blob = compiler.store_blob(cs)
+    if what:
+        from acs_mi355x.results import bits_layout
+        words = max(bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)[2], 1)
+        bits = np.zeros((n, words), np.uint32)
+        obl = np.zeros((n, host_core.L.OBL_MAX, 2), np.uint32)
+        obl_n = np.zeros(n, np.uint32)
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         if hi == lo:
             continue
@@ -67,13 +74,29 @@ def split_is_allowed_host(cs, batch, cuts):
             rk = np.array(np.ctypeslib.as_array((C.c_uint32 * n).from_address(s.role_key))[lo:hi])
             d.role_key = rk.ctypes.data
         sub = np.zeros(hi - lo, host_core.L.DECISION_DT)
-        assert host_core.lib().acs_host_is_allowed(blob, len(blob), C.byref(d), sub.ctypes.data) == 0
+        if what:
+            sb_, so, sn = np.zeros((hi - lo, words), np.uint32), np.zeros((hi - lo, host_core.L.OBL_MAX, 2), np.uint32), \
+                np.zeros(hi - lo, np.uint32)
+            assert host_core.lib().acs_host_what_is_allowed(blob, len(blob), C.byref(d), sb_.ctypes.data, so.ctypes.data,
+                                                            sn.ctypes.data, sub.ctypes.data) == 0
+            bits[lo:hi], obl[lo:hi], obl_n[lo:hi] = sb_, so, sn
+        else:
+            assert host_core.lib().acs_host_is_allowed(blob, len(blob), C.byref(d), sub.ctypes.data) == 0
         out[lo:hi] = sub
         # the plan covers every request's arena words
         for i in range(lo, hi):
             off = int(batch.lines["h"]["arena_off"][i])
             assert arena_end[i] == off or (a0 <= off and arena_end[i] <= a1)
-    return out
+    return (bits, obl, obl_n, out) if what else out
+
+
+def _same_wia(a, b):
+    bits, obl, obl_n, out = a
+    bits2, obl2, obl_n2, out2 = b
+    assert np.array_equal(bits, bits2) and np.array_equal(obl_n, obl_n2) and np.array_equal(_u64(out), _u64(out2))
+    for i in range(len(obl_n)):
+        k = min(int(obl_n[i]), obl.shape[1])
+        assert np.array_equal(obl[i, :k], obl2[i, :k]), i
 
 
 def _cuts(n, parts, rng):
@@ -118,9 +141,11 @@ def test_split_gather_codec_batch_host(kind):
             codec.set_subject_scopes(k, v)
     b = codec.encode(sb.json_text(idx), threads=4)
     whole = host_core.is_allowed(cs, b, compact=True)
+    wia = host_core.what_is_allowed(cs, b, compact=True)
     for parts in (2, 5):
         cuts = [n * k // parts for k in range(parts + 1)]
         assert np.array_equal(_u64(split_is_allowed_host(cs, b, cuts)), _u64(whole)), parts
+        _same_wia(split_is_allowed_host(cs, b, cuts, what=True), wia)  # acs_what_is_allowed's split
     b.close()
     codec.close()
 
@@ -149,6 +174,7 @@ def test_two_replicas_on_one_device_gpu():
     b = codec.encode(text, threads=4)
     want = one.is_allowed(b)
     assert np.array_equal(_u64(two.is_allowed(b)), _u64(want))
+    _same_wia(two.what_is_allowed(b), one.what_is_allowed(b))  # whatIsAllowed split over the replicas
     assert np.array_equal(_u64(two.is_allowed(sb.batch, compact=True)), _u64(want))
     p = Pipeline(two, codec, threads=4, chunk=3000)
     got, st = p.is_allowed(text, n)
