@@ -65,7 +65,6 @@ struct Tables {
   uint32_t n_sets, n_pols, n_rules;
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
-  uint32_t se0;      // the most common roleScopingEntity of the targets (hr_owner_bits' memo key)
   const uint32_t* ev_index;  // event index (build_event_index; nullptr: K1 never skips a set for it)
 };
 
@@ -99,25 +98,6 @@ inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRe
   for (uint32_t r = 0; r < n_rules; ++r)
     if (rules[r].nflags & NF_HAS_CONDITION) cb[r >> 5] |= 1u << (r & 31);
 }
-
-// The roleScopingEntity most targets carry (hr_owner_bits memoises checkHierarchicalScope's
-// owner tests for it): a Boyer-Moore majority vote over the nodes' non-empty `se` (the majority
-// when there is one, some frequent value otherwise: any value is correct, the memo just hits
-// less).  Feed every node with add(), read .value.
-struct ScopingEntityVote {
-  uint32_t value = ID_UNDEF, count = 0;
-  ACS_FN void add(uint32_t se) {
-    if (se <= ID_EMPTY) return;
-    if (count == 0) {
-      value = se;
-      count = 1;
-    } else if (se == value) {
-      ++count;
-    } else {
-      --count;
-    }
-  }
-};
 
 #if defined(ACS_SCAN_COUNT)
 // Counting build (bench.py's B_scan): bytes of every table read a wave issues, once per wave.
@@ -440,7 +420,6 @@ struct ReqCtx {
   // instead of being held as six pointers and six counts: K1's per-lane state stays small.
   uint32_t c0, c1;  // arena counts: [0] grants | rolese<<8 | slots<<16 | roots<<24, [1] tse | hrkeys<<8
   uint32_t ext;     // compact batch: 1 + 16-B unit offset of the extension record (0: none)
-  mutable uint32_t hrm;  // hr_owner_bits memo: [7:0] its context slot (0xFF: none yet), 3 bits per role
   bool soa;         // the rows past the line are SoA rows (else the extension record); false as a
                     // constant in the compact-batch kernels, so their SoA paths compile away
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
@@ -451,7 +430,7 @@ struct ReqCtx {
   // ln: the request's packed line (acs_layout.h ReqLine), nullptr: the SoA rows
   ACS_FN ReqCtx(const Tables& t, const Batch& b, uint32_t idx, const ReqHdr& hd, const ReqLine* ln = nullptr,
                 bool soa_ok = true)
-      : T(t), B(b), i(idx), h(hd), hrm(0xFFu) {
+      : T(t), B(b), i(idx), h(hd) {
     soa = soa_ok && B.hdr != nullptr;
     if (ln || !soa_ok) {
       ext = ln->ext;
@@ -819,27 +798,8 @@ ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) 
 #endif
 // The owner tests of checkHierarchicalScope for one context slot: bit 0 the direct owner <->
 // grant match (hierarchicalScope.ts:165-191), bit 1 the HR-tree match (:199-245, only when not
-// direct).  Both read the request's arena (grants, role-scoping pairs, roots, the slot's owner
-// records) and are pure in (slot, role, se), so a lane memoises them (ReqCtx::hrm) for its first
-// slot, the tables' common scoping entity T.se0 and the values of its first two role
-// associations: every candidate rule after the first of a role reuses the outcome instead of
-// re-reading the arena.
-#ifndef ACS_AB_NO_HR_MEMO  // A/B builds: no memo (same records)
-#define ACS_AB_NO_HR_MEMO 0
-#endif
+// direct).
 ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
-  const uint32_t ms = R.hrm & 0xFFu;
-  uint32_t k = 2;
-  if (!ACS_AB_NO_HR_MEMO && se == R.T.se0 && (ms == 0xFFu || ms == slot))
-    k = role == R.role0 ? 0u : (role == R.role1 ? 1u : 2u);
-  if (k < 2) {
-    const uint32_t sh = 8 + 3 * k;
-    if ((R.hrm >> sh) & 1u) return (R.hrm >> (sh + 1)) & 3u;
-    const uint32_t d = hr_direct(R, slot, role, se) ? 1u : 0u;
-    const uint32_t b = d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
-    R.hrm = (R.hrm & ~(0xFFu | (7u << sh))) | slot | ((1u | (b << 1)) << sh);
-    return b;
-  }
   const uint32_t d = hr_direct(R, slot, role, se) ? 1u : 0u;
   return d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
 }

@@ -1179,17 +1179,6 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
   t->view.ev_index = (const uint32_t*)(base + ev_off);
-  {
-    ScopingEntityVote v;  // (the blob's records: 16-B aligned sections, whole 64-B records)
-    const uint32_t cnt[3] = {h.n_sets, h.n_pols, h.n_rules};
-    for (int k = 0; k < 3; ++k)
-      for (uint32_t i = 0; i < cnt[k]; ++i) {
-        NodeRec N;
-        std::memcpy(&N, bsrc + off[k] + (size_t)i * sizeof(NodeRec), sizeof N);
-        v.add(N.se);
-      }
-    t->view.se0 = v.value;
-  }
   t->image_bytes = img_total;
   return t;
 }

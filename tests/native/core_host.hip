@@ -38,11 +38,6 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   T->n_rules = h.n_rules;
   T->id_user = h.id_user;
   T->rstride = 1;  // blob layout: 64-B rule records, separate pools
-  ScopingEntityVote v;
-  for (uint32_t k = 0; k < h.n_sets; ++k) v.add(T->sets[k].se);
-  for (uint32_t k = 0; k < h.n_pols; ++k) v.add(T->pols[k].se);
-  for (uint32_t k = 0; k < h.n_rules; ++k) v.add(T->rules[k].se);
-  T->se0 = v.value;
   // the event index (one per thread: the host entry points are called one batch at a time)
   static thread_local std::vector<uint32_t> evx;
   evx.assign(event_index_words(h.n_sets, h.n_rules), 0u);
