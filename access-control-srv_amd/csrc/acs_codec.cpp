@@ -303,29 +303,10 @@ struct HrForest {
   StrPool ids;                // storage of the org ids `masks` is keyed by
   StrMap<uint64_t> masks;     // org id -> root bits | key bits << 32 (flat: one probe run per owner lookup)
   std::string text;           // inline forests: the exact JSON text they were built from
-  // A composed forest ("$hrs": [k1, k2, ...]: the concatenation of registered root arrays) has
-  // no masks of its own: its parts', root bits shifted by the part's first root, key bits
-  // remapped into the merged first-seen key order.
-  struct Part {
-    std::shared_ptr<const HrForest> f;
-    uint32_t root_off = 0;
-    uint8_t key_map[MAX_HRKEYS] = {};
-  };
-  std::vector<Part> parts;
   size_t bytes() const { return text.size() + masks.size() * 64 + 256; }
   uint64_t mask(std::string_view id) const {
-    if (parts.empty()) {
-      const auto* e = masks.find(id);
-      return e ? e->v : 0;
-    }
-    uint64_t m = 0;
-    for (const Part& p : parts) {
-      const uint64_t x = p.f->mask(id);
-      if (!x) continue;
-      m |= (x & 0xFFFFFFFFull) << p.root_off;
-      for (uint32_t k = (uint32_t)(x >> 32); k; k &= k - 1) m |= 1ull << (32 + p.key_map[__builtin_ctz(k)]);
-    }
-    return m;
+    const auto* e = masks.find(id);
+    return e ? e->v : 0;
   }
 };
 
@@ -410,40 +391,6 @@ void build_forest(HrForest& F, const JV* hrs) {
   } catch (const Unsup& u) {
     F.why = u.why;
   }
-}
-
-// The forest of the concatenated root arrays of `parts` (build_forest over the concatenation:
-// roots in order, effective-role keys in first-seen order across the parts).
-std::shared_ptr<HrForest> compose_forests(const std::vector<std::shared_ptr<const HrForest>>& parts) {
-  auto F = std::make_shared<HrForest>();
-  F->is_array = true;
-  for (const auto& f : parts) {
-    if (f->why && !F->why) F->why = f->why;
-    if (!f->is_array && !F->why) F->why = "registered HR scopes are not an array";
-    if (F->why) continue;
-    HrForest::Part P;
-    P.f = f;
-    P.root_off = (uint32_t)F->roots.size();
-    if (F->roots.size() + f->roots.size() > (size_t)MAX_ROOTS) {
-      F->why = "too many HR scope roots";
-      continue;
-    }
-    F->roots.insert(F->roots.end(), f->roots.begin(), f->roots.end());
-    for (size_t k = 0; k < f->keys.size(); ++k) {
-      size_t at = 0;
-      while (at < F->keys.size() && !scalar_eq(F->keys[at], f->keys[k])) ++at;
-      if (at == F->keys.size()) {
-        if (F->keys.size() >= (size_t)MAX_HRKEYS) {
-          F->why = "too many HR effective roles";
-          break;
-        }
-        F->keys.push_back(f->keys[k]);
-      }
-      P.key_map[k] = (uint8_t)at;
-    }
-    F->parts.push_back(std::move(P));
-  }
-  return F;
 }
 
 }  // namespace
@@ -1000,9 +947,37 @@ class Encoder {
     else cols_.emplace(v->str(), c);
     return c;
   }
+  // A registered forest as this thread sees it: the forest and its roots / effective-role
+  // keys interned once per thread and batch
+  struct Registered {
+    std::shared_ptr<const HrForest> f;
+    std::vector<uint32_t> root_ids, key_ids;
+  };
+  // The subject's HR forest for one request: one forest (inline or registered), or the parts of
+  // a "$hrs" key list composed in place — roots concatenated, keys merged in first-seen order,
+  // owner masks read from the parts and remapped — without building a forest per request
+  struct SubjectForest {
+    const HrForest* one = nullptr;
+    const Registered* part[MAX_ROOTS];
+    uint32_t n = 0;
+    uint32_t root_off[MAX_ROOTS];
+    uint8_t key_map[MAX_ROOTS][MAX_HRKEYS];
+    bool is_array = false;
+    uint64_t mask(std::string_view id) const {
+      if (one) return one->mask(id);
+      uint64_t m = 0;
+      for (uint32_t p = 0; p < n; ++p) {
+        const uint64_t x = part[p]->f->mask(id);
+        if (!x) continue;
+        m |= (x & 0xFFFFFFFFull) << root_off[p];
+        for (uint32_t k = (uint32_t)(x >> 32); k; k &= k - 1) m |= 1ull << (32 + key_map[p][__builtin_ctz(k)]);
+      }
+      return m;
+    }
+  };
   std::shared_ptr<const HrForest> inline_forest(const JV* raw);
-  const HrForest* subject_forest(const JV* key);
-  const std::shared_ptr<const HrForest>& registered_forest(const JV* key);
+  void subject_forest(const JV* key, SubjectForest& out, std::vector<uint32_t>& roots, std::vector<uint32_t>& keys);
+  const Registered& registered_forest(const JV* key);
   void encode_one(uint32_t i, const JV* req);
 
   acs_codec& C;
@@ -1025,8 +1000,7 @@ class Encoder {
   // are touched once per distinct value per thread, not once per request
   std::unordered_map<std::string_view, uint32_t, FastHash> cols_;
   uint32_t col_undef_ = NONE32, col_null_ = NONE32;
-  std::unordered_map<std::string_view, std::shared_ptr<const HrForest>, FastHash> forests_;
-  std::unordered_map<std::string, std::shared_ptr<const HrForest>> composed_;  // "$hrs" key lists
+  std::unordered_map<std::string_view, Registered, FastHash> forests_;
   // per-request scratch (cleared, never freed)
   std::vector<const JV*> slot_objs_;
   std::vector<std::pair<uint32_t, uint8_t>> keys_a_, keys_b_;
@@ -1066,29 +1040,46 @@ std::shared_ptr<const HrForest> Encoder::inline_forest(const JV* raw) {
 
 // A "$hrs" key: one registered forest (createHRScope's per-subject cache), or a list of them
 // whose root arrays concatenate into the subject's hierarchical_scopes (e.g. one cached forest
-// per role association), composed once per distinct list per thread and batch.
-const HrForest* Encoder::subject_forest(const JV* key) {
-  if (key->t != J_ARR) {
-    const HrForest* f = registered_forest(key).get();
-    ++hits;
-    return f;
-  }
-  std::string ck;
-  for (uint32_t k = 0; k < key->n; ++k) {
-    if (key->a[k].t != J_STR) unsup("$hrs subject key is not a string");
-    ck.append(key->a[k].s, key->a[k].n);
-    ck.push_back('\x1f');
-  }
+// per role association: compose_forests' semantics, composed in place per request).  Fills the
+// request's roots and effective-role keys (interned); unsupported forests send it to the host.
+void Encoder::subject_forest(const JV* key, SubjectForest& out, std::vector<uint32_t>& roots,
+                             std::vector<uint32_t>& keys) {
   ++hits;
-  auto it = composed_.find(ck);
-  if (it != composed_.end()) return it->second.get();
-  std::vector<std::shared_ptr<const HrForest>> parts;
-  for (uint32_t k = 0; k < key->n; ++k) parts.push_back(registered_forest(&key->a[k]));
-  std::shared_ptr<const HrForest> F = compose_forests(parts);
-  return composed_.emplace(std::move(ck), F).first->second.get();
+  if (key->t != J_ARR) {
+    const Registered& r = registered_forest(key);
+    if (r.f->why) unsup(r.f->why);
+    out.one = r.f.get();
+    out.is_array = r.f->is_array;
+    if (out.is_array) {
+      roots.insert(roots.end(), r.root_ids.begin(), r.root_ids.end());
+      keys.insert(keys.end(), r.key_ids.begin(), r.key_ids.end());
+    }
+    return;
+  }
+  if (key->n > (uint32_t)MAX_ROOTS) unsup("too many HR scope roots");
+  out.is_array = true;
+  for (uint32_t k = 0; k < key->n; ++k) {
+    const Registered& r = registered_forest(&key->a[k]);
+    if (r.f->why) unsup(r.f->why);
+    if (!r.f->is_array) unsup("registered HR scopes are not an array");
+    if (roots.size() + r.root_ids.size() > (size_t)MAX_ROOTS) unsup("too many HR scope roots");
+    const uint32_t p = out.n++;
+    out.part[p] = &r;
+    out.root_off[p] = (uint32_t)roots.size();
+    roots.insert(roots.end(), r.root_ids.begin(), r.root_ids.end());
+    for (size_t q = 0; q < r.key_ids.size(); ++q) {
+      size_t at = 0;
+      while (at < keys.size() && keys[at] != r.key_ids[q]) ++at;
+      if (at == keys.size()) {
+        if (keys.size() >= (size_t)MAX_HRKEYS) unsup("too many HR effective roles");
+        keys.push_back(r.key_ids[q]);
+      }
+      out.key_map[p][q] = (uint8_t)at;
+    }
+  }
 }
 
-const std::shared_ptr<const HrForest>& Encoder::registered_forest(const JV* key) {
+const Encoder::Registered& Encoder::registered_forest(const JV* key) {
   if (key->t != J_STR) unsup("$hrs subject key is not a string");
   auto mine = forests_.find(key->str());
   if (mine == forests_.end()) {
@@ -1098,9 +1089,15 @@ const std::shared_ptr<const HrForest>& Encoder::registered_forest(const JV* key)
       auto it = C.hr_subject.find(std::string(key->str()));
       if (it != C.hr_subject.end()) f = it->second;
     }
-    mine = forests_.emplace(key->str(), std::move(f)).first;
+    if (!f) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
+    Registered r;
+    if (!f->why && f->is_array) {
+      for (const Scalar& x : f->roots) r.root_ids.push_back(intern(x));
+      for (const Scalar& x : f->keys) r.key_ids.push_back(intern(x));
+    }
+    r.f = std::move(f);
+    mine = forests_.emplace(key->str(), std::move(r)).first;
   }
-  if (!mine->second) unsup("subject HR scopes not in the codec cache (acs_codec_set_subject_scopes)");
   return mine->second;
 }
 
@@ -1167,26 +1164,39 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   const JV* ras = truthy(ras_v) ? dict_list(ras_v, n_ras) : nullptr;
   if (n_ras > (uint32_t)RMAX) unsup("too many role associations");
   const JV* hrs = get(subj, "hierarchical_scopes");
-  const HrForest* forest = nullptr;
+  // the subject's forest: its roots and effective-role keys (interned) and owner masks
+  SubjectForest forest;
+  bool have_forest = false;
+  std::vector<uint32_t>& roots = roots_;
+  std::vector<uint32_t>& hr_keys = hr_keys_;
+  roots.clear();
+  hr_keys.clear();
   std::shared_ptr<const HrForest> inl;  // an inline forest (the codec's cache may drop it)
   if (hrs->t == J_RAW) {
     if (hrs->raw == J_ARR) {
       inl = inline_forest(hrs);
-      forest = inl.get();
+      if (inl->why) unsup(inl->why);
+      forest.one = inl.get();
+      forest.is_array = inl->is_array;
+      have_forest = true;
+      if (inl->is_array) {
+        for (const Scalar& r : inl->roots) roots.push_back(intern(r));
+        for (const Scalar& k : inl->keys) hr_keys.push_back(intern(k));
+      }
     }
     else if (hrs->raw != J_NULL) unsup("hierarchical_scopes is not an array");
   } else if (hrs->t == J_UNDEF) {
     const JV* key = get(subj, "$hrs");  // the subject's registered forest (createHRScope's cache)
-    if (key->t != J_UNDEF) forest = subject_forest(key);
+    if (key->t != J_UNDEF) {
+      subject_forest(key, forest, roots, hr_keys);
+      have_forest = true;
+    }
   } else if (hrs->t == J_ARR || hrs->t == J_OBJ) {
     unsup("hierarchical_scopes outside the codec's forest cache");  // (only reached without raw_key)
   } else if (!nullish(hrs)) {
     unsup("hierarchical_scopes is not an array");
   }
-  if (forest) {
-    if (forest->why) unsup(forest->why);
-    if (forest->is_array) flags |= RQ_HRS_ITERABLE;
-  }
+  if (have_forest && forest.is_array) flags |= RQ_HRS_ITERABLE;
 
   // ---- resources: kinds, ids, regex columns, suffixes, indexOf masks
   uint8_t kinds[QMAX] = {};
@@ -1335,18 +1345,10 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
   }
   if (grants.size() / 3 > 255 || rolese.size() / 2 > 255) unsup("too many role scoping grants");
 
-  // ---- hierarchical_scopes: roots and effective-role keys from the cached forest
-  std::vector<uint32_t>& roots = roots_;
-  std::vector<uint32_t>& hr_keys = hr_keys_;
-  roots.clear();
-  hr_keys.clear();
-  if (forest && forest->is_array) {
-    for (const Scalar& r : forest->roots) roots.push_back(intern(r));
-    for (const Scalar& k : forest->keys) hr_keys.push_back(intern(k));
-  }
+  // ---- hierarchical_scopes: owner masks from the subject's forest (roots / keys above)
   auto masks_of = [&](const JV* v) -> uint64_t {
-    if (!forest || v->t != J_STR) return 0;
-    return forest->mask(v->str());
+    if (!have_forest || v->t != J_STR) return 0;
+    return forest.mask(v->str());
   };
 
   // ---- verifyACL request loop (verifyACL.ts:37-88)
