@@ -109,6 +109,10 @@ __device__ inline void scan_count(uint32_t bytes) {
   if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&acs_scan_bytes, (unsigned long long)bytes);
 }
 #define ACS_SCAN(bytes) scan_count(bytes)
+#elif defined(ACS_HOST_WORK) && !defined(__HIP_DEVICE_COMPILE__)
+// Work-counting host build (tools/lane_work.py, test infrastructure): table bytes one request reads
+extern thread_local unsigned long long acs_host_work;
+#define ACS_SCAN(bytes) (acs_host_work += (bytes))
 #else
 #define ACS_SCAN(bytes)
 #endif

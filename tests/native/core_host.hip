@@ -155,3 +155,39 @@ extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const ac
     }
   return 0;
 }
+
+#if defined(ACS_HOST_WORK)
+namespace acs {
+thread_local unsigned long long acs_host_work = 0;
+}
+// Per request: its record and the table bytes its evaluation read (tools/lane_work.py).
+extern "C" int acs_host_is_allowed_work(const void* blob, size_t n, const acs_req_batch* b, acs_decision* out,
+                                        unsigned long long* work) {
+  Tables T;
+  if (!host_tables(blob, n, &T)) return -1;
+  Batch B = host_batch(b);
+  for (uint32_t i = 0; i < B.n; ++i) {
+    acs_host_work = 0;
+    Decision d = is_allowed(T, B, i);
+    std::memcpy(&out[i], &d, sizeof d);
+    work[i] = acs_host_work;
+  }
+  return 0;
+}
+
+extern "C" int acs_host_what_is_allowed_work(const void* blob, size_t n, const acs_req_batch* b, unsigned long long* work) {
+  Tables T;
+  if (!host_tables(blob, n, &T)) return -1;
+  Batch B = host_batch(b);
+  const uint32_t words = bits_layout(T.n_sets, T.n_pols, T.n_rules).words;
+  std::vector<uint32_t> row(words), obl(2 * OBL_MAX);
+  for (uint32_t i = 0; i < B.n; ++i) {
+    acs_host_work = 0;
+    uint32_t on = 0;
+    for (uint32_t& w : row) w = 0;
+    what_is_allowed(T, B, i, row.data(), obl.data(), &on);
+    work[i] = acs_host_work;
+  }
+  return 0;
+}
+#endif

@@ -82,8 +82,9 @@ def run_batch(cs, b, n):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     if len(sys.argv) > 2 and sys.argv[2] == "orders":
-        for r in run("c3adv", 0.1, n, 0.5, perms=True):
-            print(json.dumps(r), flush=True)
+        for kind, acl in (("c3adv", 0.1), ("c3", 0.0)):
+            for r in run(kind, acl, n, 0.5, perms=True):
+                print(json.dumps(dict(r, store=kind, acl=acl)), flush=True)
         return
     for kind, acl, second in (("c3", 0.0, 0.5), ("c3", 0.1, 0.5), ("c3adv", 0.0, 0.5), ("c3adv", 0.1, 0.5),
                               ("c3adv", 0.1, 0.0)):
