@@ -569,33 +569,29 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
     return cls, cls2, urows, rkey, rbits
 
 
-def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None, acl_eval=None):
+def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
     """The encoder's coherence order (acs_req_batch.perm): request indices grouped so that a
     wave shares its class row(s) — [bucket | second class] with bucket = 1 + class (0: an
     unfiltered request), or role-major [role key | bucket] with a role factor — stable (index
-    order within a key).  acl_eval (bool [n]): requests whose rules run verifyACL's per-rule
-    loop (a context resource with ACLs, ACL_CONTINUE) go after all others: they walk several
-    times longer (c3adv: 3.6x the table bytes), and a wave runs as long as its longest lane.
-    pad (default: 32 to 256 requests per class on average, and no role factor): each
-    (acl_eval, bucket) run starts on a 64-lane wave boundary, the holes 0xFFFFFFFF (shorter
-    classes would multiply the launch width).
+    order within a key).  pad (default: 32 to 256 requests per class on average, and no
+    role factor): each bucket's run starts on a 64-lane wave boundary, the holes 0xFFFFFFFF
+    (shorter classes would multiply the launch width).
     acs_codec.cpp writes the same order.  Returns u32 [lanes]."""
     n = len(cls)
     c = cls.astype(np.int64)
     bucket = np.where(c < cand_rows, c + 1, 0)
-    heavy = np.zeros(n, np.int64) if acl_eval is None else acl_eval.astype(np.int64)
-    if role_key is not None:  # role-major: [acl_eval | role row | second role row | bucket]
+    if role_key is not None:  # role-major: [role row | second role row | bucket]
         rk = role_key.astype(np.int64)
-        key = (heavy << 50) | ((((rk & 0xFFFF) << 16 | rk >> 16) << 17) | bucket)
+        key = (((rk & 0xFFFF) << 16 | rk >> 16) << 17) | bucket
         pad = False
     else:
-        key = (heavy << 50) | (bucket << 17) | cls2.astype(np.int64)
+        key = (bucket << 17) | cls2.astype(np.int64)
     perm = np.argsort(key, kind="stable").astype(np.uint32)
     if pad is None:
         pad = 32 * cand_rows <= n < 256 * cand_rows
     if not pad or n == 0:
         return perm
-    b = (heavy << 20 | bucket)[perm]
+    b = bucket[perm]
     starts = np.flatnonzero(np.concatenate([[True], b[1:] != b[:-1]]))
     sizes = np.diff(np.append(starts, n))
     padded = (sizes + 63) & ~63

@@ -545,5 +545,4 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     b.lines = pack_lines(b)
     b.ext = pack_ext(b)
     # the coherence order the kernels run in (the encoder knows every class: no device sort)
-    acl_eval = ((b.hdr["flags"] >> np.uint32(L.RQ_ACL_SHIFT)) & np.uint32(3)) == L.ACL_CONTINUE
-    b.perm = candidates.coherence_order(cls, b.cls2, b.cand.shape[0], b.role_key, acl_eval=acl_eval)
+    b.perm = candidates.coherence_order(cls, b.cls2, b.cand.shape[0], b.role_key)

@@ -2614,12 +2614,11 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// acs_req_batch.perm (candidates.coherence_order): request indices grouped by [acl | bucket |
-// second class] (acl: the request runs verifyACL's per-rule loop; bucket = 1 + class, 0: an
-// unfiltered request) or, with a role factor, role-major [acl | role key | bucket]; stable
-// (index order within a key).  Runs of equal buckets start on
+// acs_req_batch.perm (candidates.coherence_order): request indices grouped by [bucket | second
+// class] (bucket = 1 + class; 0: an unfiltered request) or, with a role factor, role-major
+// [role key | bucket]; stable (index order within a key).  Runs of equal buckets start on
 // 64-lane wave boundaries (holes 0xFFFFFFFF) when the classes average 32 to 256 requests and
-// there is no role factor.  A parallel LSD radix sort of 33-bit (role-major: 49-bit) keys,
+// there is no role factor.  A parallel LSD radix sort of 32-bit (role-major: 48-bit) keys,
 // 8-bit digits, a digit whose value every key shares skipped.
 void coherence_order(acs_codec_batch& B, int threads) {
   const size_t n = B.n;
@@ -2632,19 +2631,17 @@ void coherence_order(acs_codec_batch& B, int threads) {
     for (size_t i = lo; i < hi; ++i) {
       const uint32_t c = B.lines[i].h.flags >> RQ_PCOL_SHIFT;
       const uint32_t bucket = c < B.cand_rows ? c + 1u : 0u;
-      // requests running verifyACL's per-rule loop (ACL_CONTINUE) after all others
-      const uint64_t heavy = ((B.lines[i].h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_CONTINUE ? 1u : 0u;
-      if (rmaj) {  // [acl | role row | 1 + second role row | bucket]
+      if (rmaj) {  // [role row | 1 + second role row | bucket]
         const uint64_t rk = B.role_key[i];
-        key[i] = heavy << 48 | (rk & 0xFFFFu) << 32 | (rk >> 16) << 16 | bucket;
-      } else {  // [acl | bucket | second class]
-        key[i] = heavy << 32 | (uint64_t)bucket << 16 | B.lines[i].cls2;
+        key[i] = (rk & 0xFFFFu) << 32 | (rk >> 16) << 16 | bucket;
+      } else {
+        key[i] = bucket << 16 | B.lines[i].cls2;
       }
       idx[i] = (uint32_t)i;
     }
   });
   std::vector<std::array<size_t, 256>> cnt(T);
-  for (int sh = 0; sh < (rmaj ? 56 : 40); sh += 8) {
+  for (int sh = 0; sh < (rmaj ? 48 : 32); sh += 8) {
     auto range = [&](int t, size_t& lo, size_t& hi) {
       lo = n * t / T;
       hi = n * (t + 1) / T;

@@ -93,28 +93,6 @@ def test_adverse_event_index_changes_no_record(adverse, monkeypatch):
     assert np.array_equal(with_ix, host_core.is_allowed(cs, b).view(np.uint64))
 
 
-def test_acl_requests_ordered_last(adverse):
-    """Requests that run verifyACL's per-rule loop (a context resource with ACLs) come after all
-    others in both encoders' coherence order (each class run of the rest first), every request
-    exactly once."""
-    _, cs, sb = adverse
-    reqs = [sb.decode(i) for i in range(sb.batch.n)]
-    pb = encoder.Encoder(cs).encode(reqs)
-    codec = NativeCodec(compiler.store_blob(cs))
-    for k, v in sb.hrs_forests().items():
-        codec.set_subject_scopes(k, v)
-    nb = codec.encode(sb.json_text(), threads=3)
-    for b in (pb, nb):
-        flags = b.lines["h"]["flags"].astype(np.int64)
-        acl = ((flags >> L.RQ_ACL_SHIFT) & 3) == L.ACL_CONTINUE
-        assert 0.05 < acl.mean() < 0.2
-        perm = np.array(b.perm)
-        real = perm[perm != 0xFFFFFFFF].astype(np.int64)
-        assert sorted(real.tolist()) == list(range(b.n))
-        first_acl = np.flatnonzero(acl[real])[0]
-        assert acl[real][first_acl:].all() and not acl[real][:first_acl].any()
-
-
 @pytest.mark.gpu
 def test_adverse_gpu(adverse):
     torch = pytest.importorskip("torch")

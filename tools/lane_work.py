@@ -3,6 +3,9 @@
 evaluator core counting, per request, the table bytes its evaluation reads
 (-DACS_HOST_WORK), then per 64-lane wave of an order: sum(work) / (64 x max(work)) — the share of
 a wave's lane-time that does work when every lane runs as long as the wave's longest.
+This ignores the union of the wave's candidate rows: grouping c3adv's ACL requests after the
+rest raised this figure 0.22 -> 0.70 but made K1 slower on the GPU (3.3 -> 4.7 ms, the ACL waves
+mixing many classes; profiles/r04_h), so it ranks orders only among class-coherent ones.
 usage: python tools/lane_work.py <c3|c3adv|c4> [requests] [second_role]"""
 import ctypes as C
 import json
