@@ -38,7 +38,7 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_codec_free", "acs_codec_set_subject_scopes", "acs_codec_evict_subject", "acs_codec_encode",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",
-           "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_device_list",
+           "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_compile_sharded", "acs_device_list",
            "acs_pipeline_host_reason", "acs_overflow_index_device", "acs_overflow_repass_device"]
 
 
@@ -53,6 +53,8 @@ def _declare(lib):
     lib.acs_compile.argtypes = [vp, C.c_size_t, C.c_int]
     lib.acs_compile_multi.restype = vp
     lib.acs_compile_multi.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    lib.acs_compile_sharded.restype = vp
+    lib.acs_compile_sharded.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
     lib.acs_device_list.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
     lib.acs_free.argtypes = [vp]
     lib.acs_free.restype = None
@@ -200,12 +202,15 @@ class Tables:
     compact host batches and the pipeline split across them; the *_device entry points and
     ``device`` name d0."""
 
-    def __init__(self, blob: bytes, device: int = 0, lib=None, devices=None):
+    def __init__(self, blob: bytes, device: int = 0, lib=None, devices=None, sharded: bool = False):
+        """sharded: devices=[...] each hold a run of the store's policy sets (acs_compile_sharded,
+        rule sharding in one process: is_allowed only) instead of a replica."""
         self.lib = lib or load()
         self._blob = blob
         if devices:
             arr = (C.c_int * len(devices))(*devices)
-            self.h = self.lib.acs_compile_multi(blob, len(blob), arr, len(devices))
+            compile_fn = self.lib.acs_compile_sharded if sharded else self.lib.acs_compile_multi
+            self.h = compile_fn(blob, len(blob), arr, len(devices))
             device = int(devices[0])
         else:
             self.h = self.lib.acs_compile(blob, len(blob), device)

@@ -1489,6 +1489,61 @@ ACS_FN uint64_t shard_key(const Tables& T, const Decision& d, const ShardBase& b
   return (uint64_t)last << 33 | payload;
 }
 
+// A rule-sharded handle's class rows (acs_compile_sharded): the batch's rows in the global
+// layout [S | P | useful S | useful P | R | verdicts: 4 x P, R] cut to one shard's nodes —
+// each section's bits [bit0, bit0 + nbits) moved to bit 0 of the shard's section.
+struct RowSlice {
+  uint32_t n;                                // sections present
+  uint32_t src[10], dst[10], bit0[10], nbits[10];
+  uint32_t words;                            // the shard's row length
+  uint32_t wp, wr, wsu, wpu, wv;             // its section offsets (acs_req_batch.cand_*)
+};
+
+// Build the slice of a global layout (offsets as in acs_req_batch; 0: section absent) for a
+// shard holding sets / policies / rules [b.*_base, + n_*).
+inline RowSlice make_row_slice(uint32_t g_pols, uint32_t cand_wp, uint32_t cand_wr, uint32_t cand_wsu,
+                               uint32_t cand_wpu, uint32_t cand_wv, const ShardBase& b, uint32_t ns,
+                               uint32_t np, uint32_t nr) {
+  RowSlice L{};
+  const uint32_t ws = (ns + 31) / 32, wp = (np + 31) / 32, wr = (nr + 31) / 32, gwp = (g_pols + 31) / 32;
+  uint32_t at = 0;
+  auto add = [&](uint32_t src, uint32_t bit0, uint32_t nbits, uint32_t w) {
+    L.src[L.n] = src;
+    L.dst[L.n] = at;
+    L.bit0[L.n] = bit0;
+    L.nbits[L.n] = nbits;
+    ++L.n;
+    const uint32_t d = at;
+    at += w;
+    return d;
+  };
+  add(0, b.set_base, ns, ws);
+  L.wp = add(cand_wp, b.pol_base, np, wp);
+  if (cand_wsu) L.wsu = add(cand_wsu, b.set_base, ns, ws);
+  if (cand_wpu) L.wpu = add(cand_wpu, b.pol_base, np, wp);
+  L.wr = add(cand_wr, b.rule_base, nr, wr);
+  if (cand_wv) {
+    L.wv = at;
+    for (uint32_t k = 0; k < 4; ++k) add(cand_wv + k * gwp, b.pol_base, np, wp);
+    add(cand_wv + 4 * gwp, b.rule_base, nr, wr);
+  }
+  L.words = at;
+  return L;
+}
+
+// Word w of the shard's row cut from global row `row` (src_words long).
+ACS_FN uint32_t slice_word(const uint32_t* row, uint32_t src_words, const RowSlice& L, uint32_t w) {
+  uint32_t k = 0;
+  while (k + 1 < L.n && L.dst[k + 1] <= w) ++k;
+  const uint32_t j = w - L.dst[k];
+  if (32 * j >= L.nbits[k]) return 0u;
+  const uint32_t bit = L.bit0[k] + 32 * j, sw = L.src[k] + (bit >> 5), sh = bit & 31u;
+  uint32_t x = sw < src_words ? row[sw] >> sh : 0u;
+  if (sh && sw + 1 < src_words) x |= row[sw + 1] << (32u - sh);
+  const uint32_t left = L.nbits[k] - 32 * j;
+  return left >= 32 ? x : x & ((1u << left) - 1u);
+}
+
 // Reduced key -> the decision record an unsharded evaluation writes (global indices).
 ACS_FN Decision shard_decode(uint64_t key) {
   Decision d{};

@@ -725,6 +725,23 @@ __global__ __launch_bounds__(BLOCK) void shard_decode_kernel(const uint64_t* __r
   if (i < n) out[i] = shard_decode(keys[i]);
 }
 
+// Rule-sharded handles: the batch's class rows cut to this shard's nodes (acs_eval.h
+// RowSlice), one thread per output word.
+__global__ __launch_bounds__(BLOCK) void slice_rows_kernel(const uint32_t* __restrict__ src, uint32_t src_words,
+                                                           uint32_t rows, RowSlice L, uint32_t* __restrict__ dst) {
+  const size_t k = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (k >= (size_t)rows * L.words) return;
+  const uint32_t r = (uint32_t)(k / L.words), w = (uint32_t)(k % L.words);
+  dst[k] = slice_word(src + (size_t)r * src_words, src_words, L, w);
+}
+
+// keys[i] = max(keys[i], other[i]): the MAX reduction of the shards' decision keys.
+__global__ __launch_bounds__(BLOCK) void max_keys_kernel(uint64_t* __restrict__ keys, const uint64_t* __restrict__ other,
+                                                         uint32_t n) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i < n && other[i] > keys[i]) keys[i] = other[i];
+}
+
 // ---------------------------------------------------------------- stable selection
 // The overflowed-log bookkeeping of the device path: the indices i < n a predicate selects,
 // in index order (count per 2048-item tile -> one-block exclusive scan -> per-tile write,
@@ -919,10 +936,13 @@ struct DevBuf {
 // permutation, the uploaded request image and the outputs.
 struct Workspace {
   DevBuf sort, img, out;
+  DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
   void release() {
     sort.release();
     img.release();
     out.release();
+    slice.release();
+    keys.release();
   }
 };
 }  // namespace
@@ -952,7 +972,19 @@ struct acs_tables {
   // entry points split a compact batch across this handle and its replicas
   std::vector<acs_tables*> peers;
   size_t image_bytes = 0;
+  // acs_compile_sharded: this image holds policy sets [base.set_base, + view.n_sets) of a store
+  // of g_* sets / policies / rules; the peers hold the following runs (rule sharding, C1)
+  int sharded = 0;
+  ShardBase base{};
+  uint32_t g_sets = 0, g_pols = 0, g_rules = 0;
 };
+
+// The entry points a rule-sharded handle does not serve (records need the cross-shard reduction)
+static int refuse_sharded(const acs_tables* t, const char* fn) {
+  if (!t || !t->sharded) return 0;
+  g_err = std::string(fn) + ": a rule-sharded handle (acs_compile_sharded) serves acs_is_allowed only";
+  return -1;
+}
 
 // csrc/acs_validate.cpp
 extern "C" int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_min);
@@ -1240,6 +1272,176 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
   return t;
 }
 
+// ---------------------------------------------------------------- rule-sharded handles (C1)
+// The sub-image of policy sets [s0, s1) of a validated blob: those sets' node records, their
+// policies' and rules' child ranges rebased to the slice and NF_CLEAN_BELOW recomputed from the
+// slice's first set (the other shards find the events below it), the pools whole (pool offsets
+// unchanged), no codec section.  *b: the slice's first global set / policy / rule.
+static std::vector<char> slice_blob(const void* blob, uint32_t s0, uint32_t s1, ShardBase* b) {
+  acs_blob_header h;
+  std::memcpy(&h, blob, sizeof h);
+  const char* p = (const char*)blob + align16(sizeof h);
+  const NodeRec* sets = (const NodeRec*)p;
+  p += align16((size_t)h.n_sets * sizeof(NodeRec));
+  const NodeRec* pols = (const NodeRec*)p;
+  p += align16((size_t)h.n_pols * sizeof(NodeRec));
+  const NodeRec* rules = (const NodeRec*)p;
+  p += align16((size_t)h.n_rules * sizeof(NodeRec));
+  const size_t pool_bytes = align16((size_t)h.n_rres * sizeof(RuleResAttr)) + align16((size_t)h.n_pairs * sizeof(Pair)) +
+                            align16((size_t)h.n_u32pool * sizeof(uint32_t));
+  const uint32_t p0 = s0 < s1 ? sets[s0].child_begin : 0u, p1 = s0 < s1 ? sets[s1 - 1].child_end : 0u;
+  const uint32_t r0 = p0 < p1 ? pols[p0].child_begin : 0u, r1 = p0 < p1 ? pols[p1 - 1].child_end : r0;
+  *b = ShardBase{s0, p0, r0};
+  acs_blob_header o = h;
+  o.n_sets = s1 - s0;
+  o.n_pols = p1 - p0;
+  o.n_rules = r1 - r0;
+  for (uint32_t& x : o.reserved) x = 0;
+  const size_t total = align16(sizeof o) + align16((size_t)o.n_sets * sizeof(NodeRec)) +
+                       align16((size_t)o.n_pols * sizeof(NodeRec)) + align16((size_t)o.n_rules * sizeof(NodeRec)) +
+                       pool_bytes;
+  std::vector<char> out(total, 0);
+  char* q = out.data();
+  std::memcpy(q, &o, sizeof o);
+  q += align16(sizeof o);
+  NodeRec* S = (NodeRec*)q;
+  bool clean_so_far = true;
+  for (uint32_t k = 0; k < o.n_sets; ++k) {
+    NodeRec n = sets[s0 + k];
+    n.child_begin -= p0;
+    n.child_end -= p0;
+    n.nflags &= (uint8_t)~NF_CLEAN_BELOW;
+    if (clean_so_far) n.nflags |= NF_CLEAN_BELOW;
+    clean_so_far = clean_so_far && (n.nflags & NF_CLEAN);
+    S[k] = n;
+  }
+  q += align16((size_t)o.n_sets * sizeof(NodeRec));
+  NodeRec* P = (NodeRec*)q;
+  for (uint32_t k = 0; k < o.n_pols; ++k) {
+    NodeRec n = pols[p0 + k];
+    n.child_begin -= r0;
+    n.child_end -= r0;
+    n.fe -= r0;
+    P[k] = n;
+  }
+  q += align16((size_t)o.n_pols * sizeof(NodeRec));
+  if (o.n_rules) std::memcpy(q, rules + r0, (size_t)o.n_rules * sizeof(NodeRec));
+  q += align16((size_t)o.n_rules * sizeof(NodeRec));
+  std::memcpy(q, p, pool_bytes);
+  return out;
+}
+
+// Contiguous set runs [cut[k], cut[k + 1]), balanced by sets + policies + rules
+// (acs_mi355x/shard.partition).
+static std::vector<uint32_t> shard_cuts(const void* blob, int parts) {
+  acs_blob_header h;
+  std::memcpy(&h, blob, sizeof h);
+  const NodeRec* sets = (const NodeRec*)((const char*)blob + align16(sizeof h));
+  const NodeRec* pols = (const NodeRec*)((const char*)sets + align16((size_t)h.n_sets * sizeof(NodeRec)));
+  std::vector<double> cum(h.n_sets + 1, 0.0);
+  for (uint32_t s = 0; s < h.n_sets; ++s) {
+    double w = 1.0 + (sets[s].child_end - sets[s].child_begin);
+    for (uint32_t q = sets[s].child_begin; q < sets[s].child_end && q < h.n_pols; ++q)
+      w += pols[q].child_end - pols[q].child_begin;
+    cum[s + 1] = cum[s] + w;
+  }
+  std::vector<uint32_t> cut{0};
+  for (int r = 1; r < parts; ++r) {
+    const double want = cum[h.n_sets] * r / parts;
+    uint32_t c = (uint32_t)(std::lower_bound(cum.begin(), cum.end(), want) - cum.begin());
+    cut.push_back(std::min(std::max(c, cut.back()), h.n_sets));
+  }
+  cut.push_back(h.n_sets);
+  return cut;
+}
+
+// Test hook (tests/test_rule_shard_lib.py): shard k of `parts` as acs_compile_sharded cuts it.
+int acs_internal_shard_blob(const void* blob, size_t n_bytes, int parts, int k, void** out, size_t* out_len,
+                            acs_shard* base) {
+  if (!blob || n_bytes < sizeof(acs_blob_header) || parts < 1 || k < 0 || k >= parts || !out || !out_len || !base)
+    return fail("acs_internal_shard_blob: bad argument");
+  uint32_t rows = 0;
+  if (acs_internal_check_blob(blob, n_bytes, &rows)) return -1;
+  const std::vector<uint32_t> cut = shard_cuts(blob, parts);
+  ShardBase b{};
+  std::vector<char> img = slice_blob(blob, cut[k], cut[k + 1], &b);
+  void* mem = malloc(img.size());
+  if (!mem) return fail("acs_internal_shard_blob: out of memory");
+  std::memcpy(mem, img.data(), img.size());
+  *out = mem;
+  *out_len = img.size();
+  base->set_base = b.set_base;
+  base->pol_base = b.pol_base;
+  base->rule_base = b.rule_base;
+  return 0;
+}
+
+// Test hook: a batch's class rows (and role rows) cut to a shard's nodes on the host, with
+// the slice_rows_kernel's code (acs_eval.h RowSlice / slice_word).  layout[6] <- the shard's
+// row words, cand_wp, cand_wr, cand_wsu, cand_wpu, cand_wv; dst_rows NULL: layout only.
+int acs_internal_slice_rows(const acs_req_batch* b, uint32_t g_pols, const acs_shard* base, uint32_t ns,
+                            uint32_t np, uint32_t nr, uint32_t* dst_rows, uint32_t* dst_role_rows, uint32_t* layout) {
+  if (!b || !base || !layout || !b->cand) return fail("acs_internal_slice_rows: bad argument");
+  const ShardBase sb{base->set_base, base->pol_base, base->rule_base};
+  const RowSlice L = make_row_slice(g_pols, b->cand_wp, b->cand_wr, b->cand_wsu, b->cand_wpu, b->cand_wv, sb, ns, np, nr);
+  const uint32_t lay[6] = {L.words, L.wp, L.wr, L.wsu, L.wpu, L.wv};
+  std::memcpy(layout, lay, sizeof lay);
+  if (!dst_rows) return 0;
+  for (uint32_t r = 0; r < b->cand_rows; ++r)
+    for (uint32_t w = 0; w < L.words; ++w)
+      dst_rows[(size_t)r * L.words + w] = slice_word(b->cand + (size_t)r * b->cand_words, b->cand_words, L, w);
+  if (b->role_key && dst_role_rows)
+    for (uint32_t r = 0; r < b->role_rows; ++r)
+      for (uint32_t w = 0; w < L.words; ++w)
+        dst_role_rows[(size_t)r * L.words + w] =
+            slice_word(b->role_rows_bits + (size_t)r * b->cand_words, b->cand_words, L, w);
+  return 0;
+}
+
+acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices) {
+  if (!blob || n_bytes < sizeof(acs_blob_header) || !devices || n_devices < 1) {
+    fail("acs_compile_sharded: bad argument");
+    return nullptr;
+  }
+  acs_blob_header h;
+  std::memcpy(&h, blob, sizeof h);
+  if (h.magic != ACS_BLOB_MAGIC || h.version != ACS_ABI_VERSION) {
+    fail("acs_compile_sharded: bad blob magic/version");
+    return nullptr;
+  }
+  const size_t need = align16(sizeof h) + align16((size_t)h.n_sets * sizeof(NodeRec)) +
+                      align16((size_t)h.n_pols * sizeof(NodeRec)) + align16((size_t)h.n_rules * sizeof(NodeRec)) +
+                      align16((size_t)h.n_rres * sizeof(RuleResAttr)) + align16((size_t)h.n_pairs * sizeof(Pair)) +
+                      align16((size_t)h.n_u32pool * sizeof(uint32_t));
+  uint32_t rows = 0;
+  if (need > n_bytes) {
+    fail("acs_compile_sharded: blob shorter than its header declares");
+    return nullptr;
+  }
+  if (acs_internal_check_blob(blob, n_bytes, &rows)) return nullptr;
+  const std::vector<uint32_t> cut = shard_cuts(blob, n_devices);
+  acs_tables* t = nullptr;
+  for (int k = 0; k < n_devices; ++k) {
+    ShardBase b{};
+    const std::vector<char> img = slice_blob(blob, cut[k], cut[k + 1], &b);
+    acs_tables* s = acs_compile(img.data(), img.size(), devices[k]);
+    if (!s) {
+      acs_free(t);
+      return nullptr;
+    }
+    s->sharded = 1;
+    s->base = b;
+    s->g_sets = h.n_sets;
+    s->g_pols = h.n_pols;
+    s->g_rules = h.n_rules;
+    s->rx_rows_min = rows;
+    if (!t) t = s;
+    else t->peers.push_back(s);
+  }
+  (void)hipSetDevice(t->device);
+  return t;
+}
+
 int acs_device_list(const acs_tables* t, int* devices, int n) {
   if (!t) return fail("acs_device_list: null tables");
   const int m = 1 + (int)t->peers.size();
@@ -1458,6 +1660,7 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
 }
 
 int acs_is_allowed_device(acs_tables* t, const acs_req_batch* b, acs_decision* out, void* stream) {
+  if (refuse_sharded(t, "acs_is_allowed_device")) return -1;
   if (!t || !b) return fail("acs_is_allowed_device: null argument");
   if (b->n == 0) return 0;
   return is_allowed_launch(t, t->dws, b, out, (hipStream_t)stream);
@@ -1498,6 +1701,7 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
 
 int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
                                uint32_t* obl_n, acs_decision* out, void* stream) {
+  if (refuse_sharded(t, "acs_what_is_allowed_device")) return -1;
   if (!t || !b) return fail("acs_what_is_allowed_device: null argument");
   if (b->n == 0) return 0;
   return what_is_allowed_launch(t, t->dws, b, bits, obl, obl_n, out, (hipStream_t)stream);
@@ -1507,6 +1711,7 @@ constexpr uint32_t OBL_CAP_LIMIT = 1u << 20;
 
 int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m,
                                    uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n, void* stream) {
+  if (refuse_sharded(t, "acs_what_is_allowed_obl_device")) return -1;
   if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl_device: null argument");
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl_device: cap must be in [1, 2^20]");
   if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl_device: chunks must be in [1, 64]");
@@ -1841,9 +2046,93 @@ static int multi_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t
   });
 }
 
+// A rule-sharded handle (acs_compile_sharded): every device evaluates the whole batch against
+// its run of policy sets — the batch uploaded to each, its class rows cut to the device's nodes
+// (slice_rows_kernel), K1, then the records turned into 64-bit keys (shard_key) — and the
+// primary MAX-reduces the keys (peer copies over xGMI, max_keys_kernel) and decodes them into
+// the records an unsharded evaluation writes.
+static int sharded_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
+  if (acs_internal_check_batch(b, t->g_sets, t->g_pols, t->g_rules, t->rx_rows_min)) return -1;
+  if (b->n > 0xFFFFFFFFull) return fail("acs_is_allowed: batch too large");
+  std::vector<acs_tables*> dev{t};
+  dev.insert(dev.end(), t->peers.begin(), t->peers.end());
+  const size_t D = dev.size(), n = b->n;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
+  size_t launched = 0;
+  auto drain = [&] {
+    const std::string err = g_err;
+    for (size_t k = 0; k < launched; ++k) {
+      (void)hipSetDevice(dev[k]->device);
+      (void)hipStreamSynchronize(dev[k]->stream);
+    }
+    (void)hipSetDevice(t->device);
+    g_err = err;
+    return -1;
+  };
+  const dim3 grid_n((unsigned)((n + BLOCK - 1) / BLOCK));
+  for (size_t k = 0; k < D; ++k) {
+    acs_tables* T = dev[k];
+    if (hipSetDevice(T->device) != hipSuccess) return fail("acs_is_allowed: hipSetDevice failed"), drain();
+    launched = k + 1;
+    acs_req_batch d;
+    if (upload_batch(T->hws, b, &d, T->stream)) return drain();
+    if (b->cand) {
+      const RowSlice L = make_row_slice(t->g_pols, b->cand_wp, b->cand_wr, b->cand_wsu, b->cand_wpu, b->cand_wv,
+                                        T->base, T->view.n_sets, T->view.n_pols, T->view.n_rules);
+      const size_t rows_w = (size_t)b->cand_rows * L.words, role_w = b->role_key ? (size_t)b->role_rows * L.words : 0;
+      if (T->hws.slice.reserve((rows_w + role_w + 1) * sizeof(uint32_t))) return drain();
+      uint32_t* dst = (uint32_t*)T->hws.slice.p;
+      if (rows_w)
+        hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((rows_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                           T->stream, d.cand, b->cand_words, b->cand_rows, L, dst);
+      if (role_w)
+        hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((role_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                           T->stream, d.role_rows_bits, b->cand_words, b->role_rows, L, dst + rows_w);
+      if (hipGetLastError() != hipSuccess) return fail("acs_is_allowed: row slice launch failed"), drain();
+      d.cand = dst;
+      d.cand_words = L.words;
+      d.cand_wp = L.wp;
+      d.cand_wr = L.wr;
+      d.cand_wsu = L.wsu;
+      d.cand_wpu = L.wpu;
+      d.cand_wv = L.wv;
+      d.role_rows_bits = role_w ? dst + rows_w : nullptr;
+    }
+    if (T->hws.out.reserve(n * sizeof(Decision)) || T->hws.keys.reserve(n * sizeof(uint64_t) * (k == 0 ? 2 : 1)))
+      return drain();
+    if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return drain();
+    hipLaunchKernelGGL(shard_key_kernel, grid_n, dim3(BLOCK), 0, T->stream, T->view, (const Decision*)T->hws.out.p,
+                       (uint32_t)n, T->base, (uint64_t*)T->hws.keys.p);
+    if (hipGetLastError() != hipSuccess || (k > 0 && hipEventRecord(T->ev1, T->stream) != hipSuccess))
+      return fail("acs_is_allowed: shard key launch failed"), drain();
+  }
+  if (hipSetDevice(t->device) != hipSuccess) return fail("acs_is_allowed: hipSetDevice failed"), drain();
+  uint64_t* keys = (uint64_t*)t->hws.keys.p;
+  for (size_t k = 1; k < D; ++k) {
+    if (hipStreamWaitEvent(t->stream, dev[k]->ev1, 0) != hipSuccess ||
+        hipMemcpyPeerAsync(keys + n, t->device, dev[k]->hws.keys.p, dev[k]->device, n * sizeof(uint64_t),
+                           t->stream) != hipSuccess)
+      return fail("acs_is_allowed: key gather failed"), drain();
+    hipLaunchKernelGGL(max_keys_kernel, grid_n, dim3(BLOCK), 0, t->stream, keys, (const uint64_t*)(keys + n),
+                       (uint32_t)n);
+  }
+  hipLaunchKernelGGL(shard_decode_kernel, grid_n, dim3(BLOCK), 0, t->stream, (const uint64_t*)keys, (uint32_t)n,
+                     (Decision*)t->hws.out.p);
+  if (hipGetLastError() != hipSuccess ||
+      hipMemcpyAsync(out, t->hws.out.p, n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream) != hipSuccess)
+    return fail("acs_is_allowed: decode / result copy failed"), drain();
+  for (size_t k = 0; k < D; ++k)
+    if (hipSetDevice(dev[k]->device) != hipSuccess || hipStreamSynchronize(dev[k]->stream) != hipSuccess)
+      return fail("acs_is_allowed: device synchronisation failed"), drain();
+  HIP_OK(hipSetDevice(t->device));
+  return 0;
+}
+
 int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
   if (!t || !b || (b && b->n && !out)) return fail("acs_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (t->sharded) return sharded_is_allowed(t, b, out);
   if (split_across_devices(t, b)) {
     std::vector<uint32_t> arena_end(b->n);
     if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
@@ -1869,6 +2158,7 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
 
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl, uint32_t* obl_n,
                         acs_decision* out) {
+  if (refuse_sharded(t, "acs_what_is_allowed")) return -1;
   if (!t || !b || (b->n && (!bits || !obl || !obl_n || !out))) return fail("acs_what_is_allowed: null argument");
   if (b->n == 0) return 0;
   if (split_across_devices(t, b)) {
@@ -1905,6 +2195,7 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
 
 int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t chunks,
                             uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
+  if (refuse_sharded(t, "acs_what_is_allowed_obl")) return -1;
   if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl: null argument");
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl: cap must be in [1, 2^20]");
   if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl: chunks must be in [1, 64]");
@@ -2026,6 +2317,7 @@ acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint
     fail("acs_pipeline_create: null argument");
     return nullptr;
   }
+  if (refuse_sharded(t, "acs_pipeline_create")) return nullptr;
   auto p = new acs_pipeline();
   p->t = t;
   p->c = c;

@@ -130,6 +130,15 @@ void acs_free(acs_tables* t);
 acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 int acs_device_list(const acs_tables* t, int* devices, int n);
 
+/* Rule-sharded handle (SURVEY §8(e) configs[4] variant ii, in one process): the store's policy
+ * sets cut into n_devices contiguous runs balanced by node count (acs_mi355x/shard.partition),
+ * run k compiled alone onto devices[k].  acs_is_allowed then evaluates every request on every
+ * device — the batch uploaded to each, its class rows cut to the device's nodes on the device —
+ * turns each device's records into acs_shard_keys_device keys, MAX-reduces them on devices[0]
+ * (peer copies over xGMI) and decodes them: the records of an unsharded evaluation.  The other
+ * evaluation entry points refuse a sharded handle. */
+acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices);
+
 /* Replaces: AccessController.isAllowed (accessController.ts:88-324), for a batch.
  * Host buffers in and out; synchronous (H2D, kernel, D2H on an internal stream).  Safe to
  * call from several host threads on one handle (calls are serialised per handle). */
