@@ -553,20 +553,6 @@ __device__ unsigned long long acs_phase_acc[PH_N];
 // 1.98 -> 1.87 ms in a same-call A/B (r02_q; c2 0.180 -> 0.190 ms), 4 slots alone 1.95 ms
 #define ACS_K1_WAVES_PER_EU 5
 #endif
-// XCD-aware tiles: the hardware dispatches workgroups round-robin over the 8 XCDs (block b on
-// XCD b % 8), each XCD with its own L2.  Consecutive tiles of the coherence order share class
-// rows, so block b takes tile x * per + min(x, rem) + b / 8 (x = b % 8): every XCD walks one
-// contiguous run of tiles and a class's rows are fetched into one L2, not eight.
-#ifndef ACS_AB_NO_XCD  // A/B builds: tile = blockIdx.x
-#define ACS_AB_NO_XCD 0
-#endif
-constexpr uint32_t N_XCD = 8;
-__device__ inline uint32_t xcd_tile(uint32_t b, uint32_t nb) {
-  if (ACS_AB_NO_XCD) return b;
-  const uint32_t x = b % N_XCD, q = b / N_XCD, per = nb / N_XCD, rem = nb % N_XCD;
-  return x * per + (x < rem ? x : rem) + q;
-}
-
 // CB: a compact batch (request lines + extension records, no SoA rows): the kernels are
 // instantiated for it separately so that its row accessors carry no SoA paths (fewer live
 // registers; acs_eval.h ReqCtx::soa; A/B c3 K1 1.94 -> 1.85 ms, r03_g).
@@ -582,7 +568,7 @@ template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
@@ -637,7 +623,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
