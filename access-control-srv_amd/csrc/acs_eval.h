@@ -1289,22 +1289,6 @@ struct RowSink {   // host build: OR into a zeroed row
 // traversal moves past it; the chunks it skipped are stored as zeros.  Every word of the
 // row is written exactly once (no zeroing pass, no read-modify-write, no scratch), 16 B per
 // store, and a lane writes its row front to back, so L2 merges the pieces into whole lines.
-#ifndef ACS_AB_NO_NT  // A/B builds: plain stores
-#define ACS_AB_NO_NT 0
-#endif
-// Output rows are written once and never read back by the kernel: non-temporal stores, so the
-// 1.4 KB per request of c4 rows stream through L2 without evicting the tables the walk re-reads.
-ACS_FN void store_stream(uint4* p, const uint4& v) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (!ACS_AB_NO_NT) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const v4u x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
-    return;
-  }
-#endif
-  *p = v;
-}
 struct ChunkSink {
   uint4* row;
   uint32_t cur[3], lim[3];
@@ -1316,8 +1300,8 @@ struct ChunkSink {
     for (int k = 0; k < 3; ++k) buf[k] = make_uint4(0u, 0u, 0u, 0u);
   }
   template <int S> ACS_FN void flush(uint32_t upto) {
-    store_stream(row + cur[S], buf[S]);
-    for (uint32_t c = cur[S] + 1; c < upto; ++c) store_stream(row + c, make_uint4(0u, 0u, 0u, 0u));
+    row[cur[S]] = buf[S];
+    for (uint32_t c = cur[S] + 1; c < upto; ++c) row[c] = make_uint4(0u, 0u, 0u, 0u);
     cur[S] = upto;
     buf[S] = make_uint4(0u, 0u, 0u, 0u);
   }
