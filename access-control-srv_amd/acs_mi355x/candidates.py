@@ -492,7 +492,11 @@ def classes(cs, hdr, roles, pcol, ent, act=None, thr=None, res=None):
             sec[:, 2] = used[two, 1]
             kact = np.concatenate([kact, sec])
         ckey, inv = _unique_rows(kact)
-        if len(ckey) * W * 4 > _KEY_ROW_BYTES and level != "entity":
+        if level != "entity" and (len(ckey) * W * 4 > _KEY_ROW_BYTES or
+                                  (level == LEVELS[0] and FORCE_LEVEL is None and 4 * len(ckey) > len(pcol))):
+            # over the row budget; or joint keys covering fewer than 4 requests each (waves could
+            # not share them, and the rows would outweigh the requests: a pipeline chunk of c3
+            # shipped 1.2 KB of joint rows per request, the composed level's rows 0.1 KB)
             continue
         out = np.zeros((len(ckey), W), np.uint32)
         chunk = max(8, min(_CHUNK, _CHUNK_NODE_BITS // max(1, cs.n_sets + cs.n_pols + cs.n_rules)))

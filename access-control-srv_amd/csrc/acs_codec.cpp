@@ -2141,7 +2141,9 @@ void Classes::run() {
       });
     }
     const size_t nk = key_first.size();
-    if (level < 3 && nk * W * 4 > KEY_ROW_BYTES) continue;
+    // over the row budget; or joint keys covering fewer than 4 requests each (candidates.classes:
+    // waves could not share them, and the rows would outweigh the requests)
+    if (level < 3 && (nk * W * 4 > KEY_ROW_BYTES || (level == 0 && force < 0 && 4 * nk > (size_t)n))) continue;
     // cache lookup by (level, entity value, action, roles); compute the misses in parallel
     std::vector<std::string> gkey(nk);
     std::vector<std::shared_ptr<const ClassEntry>> entry(nk);
