@@ -586,11 +586,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
 #else
   if (!in) return;
 #endif
-#if defined(ACS_AB_PROLOGUE_ONLY)  // timing-only A/B builds: the filter build and line read alone
-  out[i] = d;
-  if (F.word(0) == 0x12345678u) out[i].aux = 1u;  // keep the filter live
-  return;
-#endif
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
