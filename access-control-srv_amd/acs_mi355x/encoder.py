@@ -97,6 +97,30 @@ def _dict_list(v, what):
     return v
 
 
+def _acl_none(flags, tse, grants, rolese, sid, id_user, I):
+    """ACL_NONE (csrc/acs_layout.h): the request's ACLs make verifyACL (verifyACL.ts:89-251) false
+    for every rule, whatever the rule's scoped roles, and it throws nowhere — no role
+    associations; an action other than create / read / modify / delete; a create with an ACL
+    entity that no role association scopes; a read / modify / delete where no ACL instance is the
+    subject (for the user entity) or a grant's instance of the same entity."""
+    if flags & L.RQ_SUBJ_MISSING or not (flags & L.RQ_RA_EMPTY or flags & L.RQ_HRS_ITERABLE):
+        return False
+    if flags & L.RQ_RA_EMPTY or not flags & (L.RQ_ACT_CREATE | L.RQ_ACT_RMD):
+        return True
+    if not tse:
+        return False
+    if flags & L.RQ_ACT_CREATE:
+        scoped = {se for _, se in rolese}
+        return any(se != id_user and se not in scoped for se in tse)
+    for se, insts in tse.items():
+        ids = {I(v) for v in insts}
+        if se == id_user and sid in ids:
+            return False
+        if any(g[1] == se and g[2] in ids for g in grants):
+            return False
+    return True
+
+
 class Encoder:
     """Encodes request batches against one compiled store (reusable across batches)."""
 
@@ -404,8 +428,10 @@ class Encoder:
         words[0] = len(grants) | (len(rolese) << 8) | (len(slot_objs) << 16) | (len(roots) << 24)
         words[1] = len(tse_items) | (len(hr_keys) << 8)
 
-        hdr = (flags, len(resources), len(subjects), len(actions), len(roles), 0,
-               I(check_scalar(get(subj, "id"))))
+        sid = I(check_scalar(get(subj, "id")))
+        if acl_state == L.ACL_CONTINUE and _acl_none(flags, tse, grants, rolese, sid, self.cs.id_user, I):
+            flags = (flags & ~(3 << L.RQ_ACL_SHIFT)) | (L.ACL_NONE << L.RQ_ACL_SHIFT)
+        hdr = (flags, len(resources), len(subjects), len(actions), len(roles), 0, sid)
         subj_pairs = [(I(a.get("id", MISSING)), I(a.get("value", MISSING))) for a in subjects]
         act_pairs = [(I(a.get("id", MISSING)), I(a.get("value", MISSING))) for a in actions]
         return hdr, packed_res, subj_pairs, act_pairs, roles, words

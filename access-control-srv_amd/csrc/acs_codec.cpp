@@ -1469,6 +1469,36 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
 
   const JV* sid = get(subj, "id");
   check_scalar(sid);
+  // ACL_NONE (acs_layout.h): verifyACL false for every rule, rule-independently and without an
+  // error (encoder._acl_none)
+  if (acl_state == ACL_CONTINUE && !(flags & RQ_SUBJ_MISSING) && ((flags & RQ_RA_EMPTY) || (flags & RQ_HRS_ITERABLE))) {
+    bool none;
+    if ((flags & RQ_RA_EMPTY) || !(flags & (RQ_ACT_CREATE | RQ_ACT_RMD))) {
+      none = true;
+    } else if (tse.empty()) {
+      none = false;
+    } else if (flags & RQ_ACT_CREATE) {
+      none = false;
+      for (const auto& e : tse) {
+        if (e.first == C.urn[U_USER]) continue;
+        bool scoped = false;
+        for (size_t k = 0; k + 1 < rolese.size() && !scoped; k += 2) scoped = rolese[k + 1] == e.first;
+        if (!scoped) none = true;
+      }
+    } else {  // read / modify / delete
+      none = true;
+      const uint32_t sid_id = intern(sid);
+      for (const auto& e : tse) {
+        for (const JV* v : e.second) {
+          const uint32_t x = intern(v);
+          if (e.first == C.urn[U_USER] && x == sid_id) none = false;
+          for (size_t g = 0; g + 2 < grants.size() && none; g += 3)
+            if (grants[g + 1] == e.first && grants[g + 2] == x) none = false;
+        }
+      }
+    }
+    if (none) flags = (flags & ~(3u << RQ_ACL_SHIFT)) | ACL_NONE << RQ_ACL_SHIFT;
+  }
   ReqHdr h{};
   h.flags = flags;
   h.nres = (uint8_t)nr;

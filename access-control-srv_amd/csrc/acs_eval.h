@@ -70,10 +70,13 @@ struct Tables {
 
 // K1's event index (is_allowed_body's events-only skip): per set its rules' range [r0, r1) and,
 // in bit 31 of the r1 word, whether it holds a null policy or a policy with an invalid combining
-// algorithm (events that need no rule); then one bit per rule carrying a condition.
-// event_index_words(n_sets, n_rules) u32 words, built on the host from the blob's records.
-inline size_t event_index_words(uint32_t n_sets, uint32_t n_rules) {
-  return 2 * (size_t)n_sets + ((size_t)n_rules + 31) / 32;
+// algorithm (events that need no rule), in bit 30 whether every policy of it has rules and is
+// ACL-gated (below); then one bit per rule carrying a condition; then one bit
+// per policy whose every non-null rule has a target and does not skip ACLs (ACL-gated: for an
+// ACL_NONE request none of its rules can push).
+// event_index_words(n_sets, n_pols, n_rules) u32 words, built on the host from the blob's records.
+inline size_t event_index_words(uint32_t n_sets, uint32_t n_pols, uint32_t n_rules) {
+  return 2 * (size_t)n_sets + ((size_t)n_rules + 31) / 32 + ((size_t)n_pols + 31) / 32;
 }
 inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols,
                               const NodeRec* rules, uint32_t n_rules, uint32_t* out) {
@@ -91,12 +94,41 @@ inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRe
     }
     if (r0 >= r1) r0 = r1 = 0;
     out[2 * s] = r0;
-    out[2 * s + 1] = (r1 & 0x7FFFFFFFu) | (bare ? 0x80000000u : 0u);
+    out[2 * s + 1] = (r1 & 0x3FFFFFFFu) | (bare ? 0x80000000u : 0u);
   }
   uint32_t* cb = out + 2 * (size_t)n_sets;
   for (uint32_t w = 0; w < (n_rules + 31) / 32; ++w) cb[w] = 0;
   for (uint32_t r = 0; r < n_rules; ++r)
     if (rules[r].nflags & NF_HAS_CONDITION) cb[r >> 5] |= 1u << (r & 31);
+  uint32_t* gb = cb + (n_rules + 31) / 32;
+  for (uint32_t w = 0; w < (n_pols + 31) / 32; ++w) gb[w] = 0;
+  for (uint32_t p = 0; p < n_pols; ++p) {
+    bool gated = true;
+    for (uint32_t r = pols[p].child_begin; r < pols[p].child_end && r < n_rules && gated; ++r) {
+      const NodeRec& Q = rules[r];
+      if (Q.nflags & NF_NULL) continue;
+      gated = (Q.nflags & NF_HAS_TARGET) && !(Q.tflags & TF_ACL_SKIP);
+    }
+    if (gated) gb[p >> 5] |= 1u << (p & 31);
+  }
+  for (uint32_t s = 0; s < n_sets; ++s) {  // bit 30: every policy has rules and is ACL-gated
+    bool inert = true;
+    for (uint32_t p = sets[s].child_begin; p < sets[s].child_end && p < n_pols && inert; ++p)
+      inert = !(pols[p].nflags & NF_NULL) && pols[p].map_size != 0 && ((gb[p >> 5] >> (p & 31)) & 1u);
+    if (inert) out[2 * s + 1] |= 0x40000000u;
+  }
+}
+
+// Set s cannot push for an ACL_NONE request: every policy of it has rules and is ACL-gated.
+ACS_FN bool set_acl_inert(const Tables& T, uint32_t s) {
+  return T.ev_index && ((T.ev_index[2 * s + 1] >> 30) & 1u);
+}
+
+// Policy p's rules can all be vetoed by verifyACL (event index, above).
+ACS_FN bool acl_gated(const Tables& T, uint32_t p) {
+  if (!T.ev_index) return false;
+  const uint32_t* gb = T.ev_index + 2 * (size_t)T.n_sets + (T.n_rules + 31) / 32;
+  return (gb[p >> 5] >> (p & 31)) & 1u;
 }
 
 #if defined(ACS_SCAN_COUNT)
@@ -871,7 +903,7 @@ ACS_FN tri verify_acl(const NodeRec& t, const ReqCtx& R) {
   if (t.tflags & TF_ACL_SKIP) return 1;
   const uint32_t st = (R.h.flags >> RQ_ACL_SHIFT) & 3u;
   if (st == ACL_RET_TRUE) return 1;
-  if (st == ACL_RET_FALSE) return 0;
+  if (st == ACL_RET_FALSE || st == ACL_NONE) return 0;
   if (R.flag(RQ_SUBJ_MISSING)) return -(tri)ERR_TYPE;
   if (R.flag(RQ_RA_EMPTY)) return 0;
   if (!R.flag(RQ_HRS_ITERABLE)) return -(tri)ERR_TYPE;  // getRoleOrgMapping(undefined)
@@ -1039,7 +1071,13 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     const NodeRec P = node_at(T, T.pols, p, T.n_pols);
     if (P.nflags & NF_NULL) continue;
     if (events_only && (P.nflags & NF_COND_FREE) && P.ca != CA_INVALID) continue;  // raises no event
-    const bool cond_rules_only = events_only && P.ca != CA_INVALID;
+    // a safe request whose ACLs veto every rule's push (ACL_NONE): only rules that skip ACLs,
+    // have no target (no verifyACL) or carry a condition (an event) can matter; in an ACL-gated
+    // policy with rules only its condition rules, and with none the policy does nothing
+    const bool acl_none = safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+    const bool gated = acl_none && P.map_size != 0 && acl_gated(T, p);
+    if (gated && (P.nflags & NF_COND_FREE)) continue;
+    const bool cond_rules_only = (events_only && P.ca != CA_INVALID) || gated;
     bool psm = true;
     if (P.nflags & NF_HAS_TARGET) {
       PROF_T0(tp);
@@ -1072,6 +1110,8 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       const NodeRec Q = rule_at(T, r);
       if (Q.nflags & NF_NULL) continue;
       if (cond_rules_only && !(Q.nflags & NF_HAS_CONDITION)) continue;
+      if (acl_none && (Q.nflags & NF_HAS_TARGET) && !(Q.nflags & NF_HAS_CONDITION) && !(Q.tflags & TF_ACL_SKIP))
+        continue;
       tri m = 1;
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
@@ -1125,7 +1165,7 @@ ACS_FN bool set_may_raise(const Tables& T, const FL& F, uint32_t s) {
   if (!T.ev_index) return true;
   const uint32_t r0 = T.ev_index[2 * s], w1 = T.ev_index[2 * s + 1];
   if (w1 >> 31) return true;
-  const uint32_t r1 = w1 & 0x7FFFFFFFu;
+  const uint32_t r1 = w1 & 0x3FFFFFFFu;
   if (r0 >= r1) return false;
   const uint32_t* cb = T.ev_index + 2 * (size_t)T.n_sets;
   const uint32_t w0 = r0 >> 5, wl = (r1 - 1) >> 5;
@@ -1161,6 +1201,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     const ReqRes q = R.res(j);
     if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
   }
+  const bool acl_none = safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;  // 1 + the last set with an effect (0: none yet)
   Decision ev{};
@@ -1176,6 +1217,8 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     Decision d2{};
     const bool events_only = (have_ev || last_set) && safe && S.ca != CA_INVALID;
     if (events_only && !set_may_raise(T, F, s)) continue;
+    // an ACL_NONE request gets no push from an ACL-inert set: only its events matter
+    if (acl_none && set_acl_inert(T, s) && !set_may_raise(T, F, s)) continue;
     const int o = eval_set(R, F, s, S, safe, events_only, &e2, &c2, &d2);
     if (o == SET_EVENT) {
       ev = d2;  // lower than any event found so far

@@ -1178,7 +1178,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     for (int k = 0; k < 6; ++k) doff[k] = off[k];
   }
   // the event index (acs_eval.h build_event_index) after the image, from the blob's records
-  std::vector<uint32_t> evx(event_index_words(h.n_sets, h.n_rules));
+  std::vector<uint32_t> evx(event_index_words(h.n_sets, h.n_pols, h.n_rules));
   build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
                     (const NodeRec*)(bsrc + off[2]), h.n_rules, evx.data());
   const size_t ev_off = align16(up_bytes);

@@ -153,7 +153,11 @@ enum ReqFlags : uint32_t {
   RQ_PCOL_SHIFT = 16,        // 16 bits: candidate column of the request's entity attrs
 };
 constexpr uint32_t PCOL_ALL = 0xFFFF;  // several distinct entity columns / unfiltered request
-enum AclState : uint32_t { ACL_CONTINUE = 0, ACL_RET_TRUE = 1, ACL_RET_FALSE = 2 };
+// ACL_NONE: the loop continues (the resource has ACLs) but verifyACL is false for every rule —
+// rule-independently (verifyACL.ts:89-251: no owner / grant instance matches an ACL instance, a
+// `create` with an ACL entity no role association scopes, another action, no role associations)
+// and without an error, so the kernel need not evaluate rules whose push it would veto.
+enum AclState : uint32_t { ACL_CONTINUE = 0, ACL_RET_TRUE = 1, ACL_RET_FALSE = 2, ACL_NONE = 3 };
 
 struct ReqHdr {              // 16 B
   uint32_t flags;

@@ -40,7 +40,7 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   T->rstride = 1;  // blob layout: 64-B rule records, separate pools
   // the event index (one per thread: the host entry points are called one batch at a time)
   static thread_local std::vector<uint32_t> evx;
-  evx.assign(event_index_words(h.n_sets, h.n_rules), 0u);
+  evx.assign(event_index_words(h.n_sets, h.n_pols, h.n_rules), 0u);
   build_event_index(T->sets, h.n_sets, T->pols, h.n_pols, T->rules, h.n_rules, evx.data());
   T->ev_index = getenv("ACS_HOST_NO_EV_INDEX") ? nullptr : evx.data();
   return true;

@@ -93,6 +93,28 @@ def test_adverse_event_index_changes_no_record(adverse, monkeypatch):
     assert np.array_equal(with_ix, host_core.is_allowed(cs, b).view(np.uint64))
 
 
+def test_acl_none_changes_no_record(adverse):
+    """ACL_NONE (the encoders' rule-independent verifyACL veto, acs_layout.h): both encoders mark
+    the same requests, some of them, and turning the state back to ACL_CONTINUE (verifyACL per
+    rule, every rule evaluated) gives the same records."""
+    _, cs, sb = adverse
+    reqs = [sb.decode(i) for i in range(sb.batch.n)]
+    pb = encoder.Encoder(cs).encode(reqs)
+    codec = NativeCodec(compiler.store_blob(cs))
+    for k, v in sb.hrs_forests().items():
+        codec.set_subject_scopes(k, v)
+    nb = codec.encode(sb.json_text(), threads=3)
+    st_p = (pb.hdr["flags"] >> L.RQ_ACL_SHIFT) & 3
+    st_n = (nb.lines["h"]["flags"] >> L.RQ_ACL_SHIFT) & 3
+    assert np.array_equal(st_p, st_n)
+    none = st_p == L.ACL_NONE
+    assert none.sum() > 50, int(none.sum())
+    want = host_core.is_allowed(cs, pb).view(np.uint64).copy()
+    pb.hdr["flags"] = np.where(none, pb.hdr["flags"] & ~np.uint32(3 << L.RQ_ACL_SHIFT), pb.hdr["flags"])
+    pb.lines["h"]["flags"] = pb.hdr["flags"]
+    assert np.array_equal(host_core.is_allowed(cs, pb).view(np.uint64), want)
+
+
 @pytest.mark.gpu
 def test_adverse_gpu(adverse):
     torch = pytest.importorskip("torch")
