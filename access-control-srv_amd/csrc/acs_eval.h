@@ -124,6 +124,9 @@ ACS_FN bool set_acl_inert(const Tables& T, uint32_t s) {
   return T.ev_index && ((T.ev_index[2 * s + 1] >> 30) & 1u);
 }
 
+#ifndef ACS_AB_NO_ACL_NONE  // A/B builds: K1 ignores ACL_NONE (verifyACL still returns 0 for it)
+#define ACS_AB_NO_ACL_NONE 0
+#endif
 // Policy p's rules can all be vetoed by verifyACL (event index, above).
 ACS_FN bool acl_gated(const Tables& T, uint32_t p) {
   if (!T.ev_index) return false;
@@ -1074,7 +1077,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     // a safe request whose ACLs veto every rule's push (ACL_NONE): only rules that skip ACLs,
     // have no target (no verifyACL) or carry a condition (an event) can matter; in an ACL-gated
     // policy with rules only its condition rules, and with none the policy does nothing
-    const bool acl_none = safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+    const bool acl_none = !ACS_AB_NO_ACL_NONE && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
     const bool gated = acl_none && P.map_size != 0 && acl_gated(T, p);
     if (gated && (P.nflags & NF_COND_FREE)) continue;
     const bool cond_rules_only = (events_only && P.ca != CA_INVALID) || gated;
@@ -1201,7 +1204,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     const ReqRes q = R.res(j);
     if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
   }
-  const bool acl_none = safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+  const bool acl_none = !ACS_AB_NO_ACL_NONE && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;  // 1 + the last set with an effect (0: none yet)
   Decision ev{};
