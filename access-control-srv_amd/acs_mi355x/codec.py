@@ -101,6 +101,7 @@ class CodecBatch:
         self.lines = _view(s.lines, L.REQ_LINE_DT, n) if s.lines else np.zeros(0, L.REQ_LINE_DT)
         self.ext = _view(s.ext, np.uint32, int(s.ext_words)) if s.ext else np.zeros(0, np.uint32)
         self.perm = _view(s.perm, np.uint32, int(s.perm_lanes)) if s.perm else None  # coherence order
+        self.hints = int(s.hints)  # ACS_HINT_* (acs_req_batch.hints)
         self.cls2 = self.lines["cls2"]  # 1 + second class (composed class rows; 0: none)
         self.overlay = _Strings(self)
         self.host_reasons = {}

@@ -55,6 +55,7 @@ class RequestBatch:
     role_key: np.ndarray | None = None   # [n] u32 role-factor row per request (large stores)
     role_bits: np.ndarray | None = None  # [role rows, W] u32
     lines: np.ndarray | None = None      # [n] REQ_LINE_DT packed first rows (pack_lines)
+    hints: int = 0                       # ACS_HINT_* (acs_req_batch.hints)
     ext: np.ndarray | None = None        # u32 extension records of the rows past each line (pack_ext)
     cls2: np.ndarray | None = None       # [n] u32 1 + second class (composed class rows; 0: none)
     perm: np.ndarray | None = None       # u32 coherence order (candidates.coherence_order)
@@ -572,3 +573,5 @@ def attach_candidates(cs, b: RequestBatch, col_values, role_filter: bool = True)
     b.ext = pack_ext(b)
     # the coherence order the kernels run in (the encoder knows every class: no device sort)
     b.perm = candidates.coherence_order(cls, b.cls2, b.cand.shape[0], b.role_key)
+    acl_none = ((b.hdr["flags"] >> np.uint32(L.RQ_ACL_SHIFT)) & np.uint32(3)) == L.ACL_NONE
+    b.hints = L.HINT_ACL_NONE if acl_none.any() else 0

@@ -26,7 +26,7 @@ class ReqBatchC(C.Structure):
                 ("cand_wv", C.c_uint32),
                 ("role_key", C.c_void_p), ("role_rows_bits", C.c_void_p),
                 ("role_rows", C.c_uint32), ("lines", C.c_void_p), ("ext", C.c_void_p), ("ext_words", C.c_size_t),
-                ("perm", C.c_void_p), ("perm_lanes", C.c_size_t)]
+                ("perm", C.c_void_p), ("perm_lanes", C.c_size_t), ("hints", C.c_uint32)]
 
 
 EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device", "acs_wia_words_per_request",
@@ -136,6 +136,7 @@ def batch_struct(b, ptrs=None, compact=False) -> ReqBatchC:
         s.perm = ptrs.get("perm")
     if s.perm:
         s.perm_lanes = int(b.perm.size)
+    s.hints = int(getattr(b, "hints", 0) or 0)
     if compact:
         s.ext_words = int(b.ext.size)
     s.arena_words = int(b.arena.size)

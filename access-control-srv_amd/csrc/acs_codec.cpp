@@ -760,6 +760,7 @@ struct acs_codec_batch {
   uint32_t role_rows = 0;
   uint32_t* perm = nullptr;  // coherence order (candidates.coherence_order), perm_lanes entries
   size_t perm_lanes = 0;
+  uint32_t hints = 0;  // acs_req_batch.hints
   // SoA rows (acs_codec_batch_expand)
   bool expanded = false;
   std::vector<ReqHdr> hdr;
@@ -839,6 +840,7 @@ class Encoder {
   std::vector<uint32_t> arena;  // this thread's context arena words
   std::vector<uint32_t> ext;    // this thread's extension records
   uint64_t hits = 0, misses = 0;
+  uint32_t hints = 0;  // ACS_HINT_* of the requests this encoder wrote
 
  private:
   // String -> id: the store dictionary, else this thread's batch-local strings.  A
@@ -1497,7 +1499,10 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
         }
       }
     }
-    if (none) flags = (flags & ~(3u << RQ_ACL_SHIFT)) | ACL_NONE << RQ_ACL_SHIFT;
+    if (none) {
+      flags = (flags & ~(3u << RQ_ACL_SHIFT)) | ACL_NONE << RQ_ACL_SHIFT;
+      hints |= HINT_ACL_NONE;
+    }
   }
   ReqHdr h{};
   h.flags = flags;
@@ -2782,6 +2787,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
   std::vector<std::vector<uint32_t>> arenas(T), exts(T);
   std::vector<std::string> errs(T);
   std::atomic<uint64_t> hits{0}, misses{0};
+  std::atomic<uint32_t> hints{0};
   auto range = [&](int t, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)((uint64_t)n * t / T);
     hi = (uint32_t)((uint64_t)n * (t + 1) / T);
@@ -2796,6 +2802,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
       exts[t] = std::move(enc.ext);
       hits += enc.hits;
       misses += enc.misses;
+      hints |= enc.hints;
     } catch (const ParseError& e) {
       errs[t] = std::string("requests: ") + e.what;
     } catch (const std::exception& e) {
@@ -2812,6 +2819,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
     if (!e.empty()) throw std::runtime_error(e);
   B->hr_hits = hits;
   B->hr_misses = misses;
+  B->hints = hints;
   const double t1 = now_s();
   // regex-matrix columns in first-use order (request, attribute), as encoder.py numbers them
   std::vector<uint32_t> order(sh.cols.size()), remap(sh.cols.size());
@@ -3099,6 +3107,7 @@ int acs_codec_batch_view(const acs_codec_batch* b, acs_req_batch* out) {
   }
   v.perm = b->n ? b->perm : nullptr;
   v.perm_lanes = b->n ? b->perm_lanes : 0;
+  v.hints = b->hints;
   *out = v;
   return 0;
 }

@@ -124,9 +124,6 @@ ACS_FN bool set_acl_inert(const Tables& T, uint32_t s) {
   return T.ev_index && ((T.ev_index[2 * s + 1] >> 30) & 1u);
 }
 
-#ifndef ACS_AB_NO_ACL_NONE  // A/B builds: K1 ignores ACL_NONE (verifyACL still returns 0 for it)
-#define ACS_AB_NO_ACL_NONE 0
-#endif
 // Policy p's rules can all be vetoed by verifyACL (event index, above).
 ACS_FN bool acl_gated(const Tables& T, uint32_t p) {
   if (!T.ev_index) return false;
@@ -1000,13 +997,15 @@ ACS_FN Decision make_err(tri e, uint32_t at = 0) {
   return d;
 }
 
-template <class RQ, class FL>
+// AN: compile the ACL_NONE skips (acs_req_batch.hints); without them an ACL_NONE request is
+// still decided exactly (verify_acl vetoes its pushes), the skips only cost registers.
+template <bool AN = true, class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F);
 
-template <class RQ, class FL>
+template <bool AN = true, class RQ, class FL>
 ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
   PROF_T0(t_total);
-  const Decision d = is_allowed_body(R, F);
+  const Decision d = is_allowed_body<AN>(R, F);
   PROF_ADD(PH_TOTAL, t_total);
   return d;
 }
@@ -1025,7 +1024,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
 // algorithm are never evaluated this way (their event depends on any push).
 enum SetOutcome { SET_NONE = 0, SET_EFFECT = 1, SET_EVENT = 2 };
 
-template <class RQ, class FL>
+template <bool AN, class RQ, class FL>
 ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool safe, bool events_only,
                     uint8_t* eff, uint8_t* ec, Decision* ev) {
   const Tables& T = R.T;
@@ -1077,7 +1076,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     // a safe request whose ACLs veto every rule's push (ACL_NONE): only rules that skip ACLs,
     // have no target (no verifyACL) or carry a condition (an event) can matter; in an ACL-gated
     // policy with rules only its condition rules, and with none the policy does nothing
-    const bool acl_none = !ACS_AB_NO_ACL_NONE && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+    const bool acl_none = AN && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
     const bool gated = acl_none && P.map_size != 0 && acl_gated(T, p);
     if (gated && (P.nflags & NF_COND_FREE)) continue;
     const bool cond_rules_only = (events_only && P.ca != CA_INVALID) || gated;
@@ -1190,7 +1189,7 @@ ACS_FN bool set_may_raise(const Tables& T, const FL& F, uint32_t s) {
 // over everything.  Once something was found and every set below is clean (NF_CLEAN_BELOW)
 // and the request safe (nothing of it can throw there: see `safe`), no set below can change
 // the record and the lane stops; otherwise it walks on to set 0.
-template <class RQ, class FL>
+template <bool AN, class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   const Tables& T = R.T;
   // Cutting a combining loop short: once a fold's result is final (Fold::final), the rest of
@@ -1204,7 +1203,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     const ReqRes q = R.res(j);
     if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
   }
-  const bool acl_none = !ACS_AB_NO_ACL_NONE && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+  const bool acl_none = AN && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;  // 1 + the last set with an effect (0: none yet)
   Decision ev{};
@@ -1222,7 +1221,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     if (events_only && !set_may_raise(T, F, s)) continue;
     // an ACL_NONE request gets no push from an ACL-inert set: only its events matter
     if (acl_none && set_acl_inert(T, s) && !set_may_raise(T, F, s)) continue;
-    const int o = eval_set(R, F, s, S, safe, events_only, &e2, &c2, &d2);
+    const int o = eval_set<AN>(R, F, s, S, safe, events_only, &e2, &c2, &d2);
     if (o == SET_EVENT) {
       ev = d2;  // lower than any event found so far
       have_ev = true;

@@ -564,7 +564,9 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
 // 1 + the lane's second class (composed class rows; 0: none)
 __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && ln ? ln->cls2 : 0u; }
 
-template <class FL, bool CB>
+// AN: the batch holds ACL_NONE requests (acs_req_batch.hints): instantiate the skips for them
+// (acs_eval.h is_allowed_t; they cost c3's plain batches registers: K1 3.12 -> 3.44 ms, r04_n).
+template <class FL, bool CB, bool AN>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
@@ -592,10 +594,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WA
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
     const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
-    d = is_allowed_t(R, F);
+    d = is_allowed_t<AN>(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
+    d = is_allowed_t<AN>(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -891,20 +893,25 @@ FilterForm filter_form(const Batch& B) {
   return B.cand_words <= LDS_FILTER_WORDS && B.cand_wv ? FilterForm::Lds : FilterForm::General;
 }
 
-// one instantiation per filter form and batch form (compact: no SoA rows)
-#define ACS_LAUNCH_FILTERED(kernel, grid, lds, stream, form, compact, ...)                              \
+// one instantiation per filter form and batch form (compact: no SoA rows); X: further template
+// arguments (ACS_TARGS_NONE, or K1's ACS_TARGS_ACL_NONE / ACS_TARGS_ACL_PLAIN)
+#define ACS_TARGS_NONE
+#define ACS_TARGS_ACL_NONE , true
+#define ACS_TARGS_ACL_PLAIN , false
+#define ACS_LAUNCH_FILTERED(kernel, ...) ACS_LAUNCH_FILTERED_X(kernel, ACS_TARGS_NONE, __VA_ARGS__)
+#define ACS_LAUNCH_FILTERED_X(kernel, X, grid, lds, stream, form, compact, ...)                           \
   do {                                                                                                  \
     if (compact) {                                                                                      \
       switch (form) {                                                                                   \
-        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-        default: hipLaunchKernelGGL((kernel<Filter, true>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, true X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, true X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        default: hipLaunchKernelGGL((kernel<Filter, true X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
       }                                                                                                 \
     } else {                                                                                            \
       switch (form) {                                                                                   \
-        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
-        default: hipLaunchKernelGGL((kernel<Filter, false>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
+        case FilterForm::All: hipLaunchKernelGGL((kernel<FilterAll, false X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        case FilterForm::Lds: hipLaunchKernelGGL((kernel<FilterLds, false X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break; \
+        default: hipLaunchKernelGGL((kernel<Filter, false X>), grid, dim3(BLOCK), lds, stream, __VA_ARGS__); break;                \
       }                                                                                                 \
     }                                                                                                   \
   } while (0)
@@ -1649,8 +1656,12 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-  ACS_LAUNCH_FILTERED(is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm,
-                      (uint32_t)lanes, (Decision*)out);
+  if (b->hints & ACS_HINT_ACL_NONE)
+    ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
+                          B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
+  else
+    ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN, grid, filter_lds_bytes(B), s, filter_form(B),
+                          B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));

@@ -158,6 +158,7 @@ constexpr uint32_t PCOL_ALL = 0xFFFF;  // several distinct entity columns / unfi
 // `create` with an ACL entity no role association scopes, another action, no role associations)
 // and without an error, so the kernel need not evaluate rules whose push it would veto.
 enum AclState : uint32_t { ACL_CONTINUE = 0, ACL_RET_TRUE = 1, ACL_RET_FALSE = 2, ACL_NONE = 3 };
+constexpr uint32_t HINT_ACL_NONE = 1u;  // acs_req_batch.hints: some request is ACL_NONE
 
 struct ReqHdr {              // 16 B
   uint32_t flags;

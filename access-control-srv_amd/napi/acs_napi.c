@@ -424,7 +424,8 @@ static int read_batch(napi_env env, napi_value v, acs_req_batch* b) {
       prop_u32(env, v, "candWords", &b->cand_words) || prop_u32(env, v, "candWp", &b->cand_wp) ||
       prop_u32(env, v, "candWr", &b->cand_wr) || prop_u32(env, v, "candRows", &b->cand_rows) ||
       prop_u32(env, v, "roleRows", &b->role_rows) || prop_u32(env, v, "candWsu", &b->cand_wsu) ||
-      prop_u32(env, v, "candWpu", &b->cand_wpu) || prop_u32(env, v, "candWv", &b->cand_wv))
+      prop_u32(env, v, "candWpu", &b->cand_wpu) || prop_u32(env, v, "candWv", &b->cand_wv) ||
+      prop_u32(env, v, "hints", &b->hints))
     return -1;
   /* compact batch (csrc/acs_layout.h): lines + ext, no SoA rows */
   if (field(env, v, "lines", n * LINE_B, 0, &b->lines, NULL, &bad)) goto fail;

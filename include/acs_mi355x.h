@@ -94,6 +94,11 @@ typedef struct {
    * composes its filter from two class rows. */
   const uint32_t* perm;
   size_t perm_lanes;
+  /* Hints (optional, 0: none): ACS_HINT_ACL_NONE — some request carries the ACL_NONE verifyACL
+   * state (csrc/acs_layout.h), so K1 is launched with the code that skips the rules its ACLs
+   * veto.  Without the hint such requests are still decided exactly (verifyACL returns false
+   * for them), only without the skip; both encoders set it. */
+  uint32_t hints;
 } acs_req_batch;
 
 /* 8-byte decision record (csrc/acs_layout.h: Decision). */
@@ -111,6 +116,8 @@ typedef struct {
 #define ACS_OF_NO_TARGET 0x08u
 #define ACS_OF_HAS_EFFECT 0x10u
 #define ACS_OF_OBL_OVERFLOW 0x20u
+
+#define ACS_HINT_ACL_NONE 0x1u /* acs_req_batch.hints */
 
 /* Replaces: the in-memory `AccessController.policySets` Map the reference scans
  * per request (accessController.ts:32,125; loaded by accessControlService.ts:36-54).

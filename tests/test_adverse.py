@@ -109,6 +109,7 @@ def test_acl_none_changes_no_record(adverse):
     assert np.array_equal(st_p, st_n)
     none = st_p == L.ACL_NONE
     assert none.sum() > 50, int(none.sum())
+    assert pb.hints == nb.hints == L.HINT_ACL_NONE  # K1 instantiates the ACL_NONE skips
     want = host_core.is_allowed(cs, pb).view(np.uint64).copy()
     pb.hdr["flags"] = np.where(none, pb.hdr["flags"] & ~np.uint32(3 << L.RQ_ACL_SHIFT), pb.hdr["flags"])
     pb.lines["h"]["flags"] = pb.hdr["flags"]
@@ -128,8 +129,13 @@ def test_adverse_gpu(adverse):
         codec.set_subject_scopes(k, v)
     nb = codec.encode(sb.json_text(), threads=4)
     t = native.Tables(compiler.store_blob(cs), 0)
-    dec = decisions_from_tensor(is_allowed_device(t, DeviceBatch(nb, 0)))
+    db = DeviceBatch(nb, 0)
+    assert db.struct.hints == L.HINT_ACL_NONE
+    dec = decisions_from_tensor(is_allowed_device(t, db))
     assert np.array_equal(np.ascontiguousarray(dec).view(np.uint64), host_core.is_allowed(cs, nb).view(np.uint64))
+    db.struct.hints = 0  # the plain K1 (no ACL_NONE skips) decides the same
+    plain = decisions_from_tensor(is_allowed_device(t, db))
+    assert np.array_equal(np.ascontiguousarray(plain).view(np.uint64), np.ascontiguousarray(dec).view(np.uint64))
     c = compare(cs, doc, sb, dec, np.arange(nb.n))
     assert c["host_cond"] > 0 and c["ok"] > 2000, c
     t.close()
