@@ -577,9 +577,12 @@ def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
     """The encoder's coherence order (acs_req_batch.perm): request indices grouped so that a
     wave shares its class row(s) — [bucket | second class] with bucket = 1 + class (0: an
     unfiltered request), or role-major [role key | bucket] with a role factor — stable (index
-    order within a key).  pad (default: 32 to 256 requests per class on average, and no
-    role factor): each bucket's run starts on a 64-lane wave boundary, the holes 0xFFFFFFFF
-    (shorter classes would multiply the launch width).
+    order within a key).  pad (default: 32 to 256 requests per class on average — at least 32
+    when no request has a second class — and no role factor): each bucket's run starts on a
+    64-lane wave boundary, the holes 0xFFFFFFFF (shorter classes would multiply the launch
+    width; with second classes a bucket's run mixes them anyway, so long runs gain nothing from
+    the holes: same-call A/B at 10M requests, c3r1 K1 1.95 -> 1.78 ms padded, c3 3.11 -> 3.19,
+    r04_o / r04_p).
     acs_codec.cpp writes the same order.  Returns u32 [lanes]."""
     n = len(cls)
     c = cls.astype(np.int64)
@@ -592,7 +595,7 @@ def coherence_order(cls, cls2, cand_rows, role_key=None, pad=None):
         key = (bucket << 17) | cls2.astype(np.int64)
     perm = np.argsort(key, kind="stable").astype(np.uint32)
     if pad is None:
-        pad = 32 * cand_rows <= n < 256 * cand_rows
+        pad = 32 * cand_rows <= n and (n < 256 * cand_rows or not cls2.any())
     if not pad or n == 0:
         return perm
     b = bucket[perm]

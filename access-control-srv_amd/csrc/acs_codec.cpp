@@ -2654,8 +2654,8 @@ double now_s() {
 // acs_req_batch.perm (candidates.coherence_order): request indices grouped by [bucket | second
 // class] (bucket = 1 + class; 0: an unfiltered request) or, with a role factor, role-major
 // [role key | bucket]; stable (index order within a key).  Runs of equal buckets start on
-// 64-lane wave boundaries (holes 0xFFFFFFFF) when the classes average 32 to 256 requests and
-// there is no role factor.  A parallel LSD radix sort of 32-bit (role-major: 48-bit) keys,
+// 64-lane wave boundaries (holes 0xFFFFFFFF) when the classes average 32 to 256 requests, or
+// at least 32 and no request has a second class, and there is no role factor.  A parallel LSD radix sort of 32-bit (role-major: 48-bit) keys,
 // 8-bit digits, a digit whose value every key shares skipped.
 void coherence_order(acs_codec_batch& B, int threads) {
   const size_t n = B.n;
@@ -2664,7 +2664,11 @@ void coherence_order(acs_codec_batch& B, int threads) {
   std::vector<uint32_t> idx(n), idx2(n);
   int T = threads < 1 ? 1 : threads;
   if ((size_t)T > n / 65536 + 1) T = (int)(n / 65536 + 1);
+  std::atomic<bool> any_cls2{false};
   parallel_ranges(T, n, [&](int, size_t lo, size_t hi) {
+    uint32_t c2 = 0;
+    for (size_t i = lo; i < hi; ++i) c2 |= B.lines[i].cls2;
+    if (c2) any_cls2 = true;
     for (size_t i = lo; i < hi; ++i) {
       const uint32_t c = B.lines[i].h.flags >> RQ_PCOL_SHIFT;
       const uint32_t bucket = c < B.cand_rows ? c + 1u : 0u;
@@ -2724,13 +2728,14 @@ void coherence_order(acs_codec_batch& B, int threads) {
     key.swap(key2);
     idx.swap(idx2);
   }
-  const bool pad = !rmaj && n >= 32ull * B.cand_rows && n < 256ull * B.cand_rows;
+  const bool pad = !rmaj && n >= 32ull * B.cand_rows && (n < 256ull * B.cand_rows || !any_cls2);
+  const int rs = 16;  // runs of equal buckets (key >> 16)
   size_t lanes = n;
   if (pad) {
     lanes = 0;
     for (size_t x = 0; x < n;) {
       size_t y = x + 1;
-      while (y < n && (key[y] >> 16) == (key[x] >> 16)) ++y;
+      while (y < n && (key[y] >> rs) == (key[x] >> rs)) ++y;
       lanes += (y - x + 63) & ~size_t(63);
       x = y;
     }
@@ -2745,7 +2750,7 @@ void coherence_order(acs_codec_batch& B, int threads) {
   size_t at = 0;
   for (size_t x = 0; x < n;) {
     size_t y = x + 1;
-    while (y < n && (key[y] >> 16) == (key[x] >> 16)) ++y;
+    while (y < n && (key[y] >> rs) == (key[x] >> rs)) ++y;
     memcpy(B.perm + at, idx.data() + x, (y - x) * sizeof(uint32_t));
     const size_t run = (y - x + 63) & ~size_t(63);
     for (size_t k = y - x; k < run; ++k) B.perm[at + k] = 0xFFFFFFFFu;

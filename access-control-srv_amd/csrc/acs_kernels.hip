@@ -566,8 +566,13 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 
 // AN: the batch holds ACL_NONE requests (acs_req_batch.hints): instantiate the skips for them
 // (acs_eval.h is_allowed_t; they cost c3's plain batches registers: K1 3.12 -> 3.44 ms, r04_n).
+// With the ACL_NONE skips K1 runs at 4 waves/SIMD (no VGPR spills; same-call A/B c3adv 1.98 ->
+// 1.90 ms, while the plain c3 K1 is faster at 5: 3.11 vs 3.23 ms, r04_o).
+#ifndef ACS_K1_AN_WAVES_PER_EU
+#define ACS_K1_AN_WAVES_PER_EU 4
+#endif
 template <class FL, bool CB, bool AN>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_K1_AN_WAVES_PER_EU : ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;

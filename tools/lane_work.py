@@ -76,6 +76,16 @@ def main():
            "acl_eval_share": float(acl_eval.mean()),
            "mean_work_acl": float(work[acl_eval].mean()) if acl_eval.any() else 0.0,
            "orders": {}}
+    st = (flags >> 11) & 3  # verifyACL state (acs_layout.h AclState): share, mean work
+    res["acl_states"] = {name: [float((st == v).mean()), float(work[st == v].mean()) if (st == v).any() else 0.0]
+                         for v, name in enumerate(("continue", "ret_true", "ret_false", "none"))}
+    perm = np.array(b.perm)
+    pl = np.full(((len(perm) + 63) // 64) * 64, -1, np.int64)
+    pl[:len(perm)] = np.where(perm == 0xFFFFFFFF, -1, perm.astype(np.int64))
+    pl = pl.reshape(-1, 64)
+    wmax = np.where(pl >= 0, work[np.maximum(pl, 0)], 0).max(axis=1)
+    has = (np.where(pl >= 0, acl_eval[np.maximum(pl, 0)], False)).any(axis=1)
+    res["codec_waves_with_acl_eval"] = [float(has.mean()), float(wmax[has].sum() / max(1, wmax.sum()))]
     res["orders"]["codec"] = wave_stats(work, np.array(b.perm))
     cls = flags >> 16
     cls2 = b.lines["cls2"].astype(np.int64)
