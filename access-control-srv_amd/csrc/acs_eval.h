@@ -321,10 +321,12 @@ struct FilterAll {
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
 // kernel before any lane diverges (all ones for a wave holding an unfiltered request).  The
-// target verdicts are class facts: a wave of one class (no composed lane) reads them from its
-// LDS row (`single`); in a wave that mixes classes each lane reads its own class row (`own`,
-// L2-resident; nullptr for an unfiltered lane: no verdicts) and a composed lane also its second
-// row (`own2`).
+// target verdicts are class facts: a wave of one class reads them from its LDS row (`single`:
+// there the verdict sections are that class's alone), a composed lane composing them with its
+// second row (`own2`); in a wave that mixes classes each lane reads its own class row (`own`,
+// L2-resident; nullptr for an unfiltered lane: no verdicts) and a composed lane also `own2`.
+// (c3: most waves hold composed lanes; reading the class's verdicts from LDS there instead of
+// two L2 gathers per lookup: same-call A/B K1 3.125 -> 3.106 ms, r04_q.)
 struct FilterLds {
   const uint32_t* lds;
   uint32_t wp, wr, wsu, wpu, wv;
@@ -342,7 +344,7 @@ struct FilterLds {
   // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane);
   // conj: a known-false section
   ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
-    if (single) return word(wv + sec + w);
+    if (single) return compose_verdict(word(wv + sec + w), own2, wv + sec + w, conj);
     return own ? compose_verdict(own[wv + sec + w], own2, wv + sec + w, conj) : 0u;
   }
   ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {

@@ -486,13 +486,16 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     }
     pending &= ~__ballot(valid && cls == c && rkey == r);
   }
-  if (!all && !or_second_rows(B, valid, c2, lds, W, &any2)) all = true;
+  // a wave of one class keeps that class's verdict sections in LDS: second rows are OR-ed into
+  // the candidate sections only
+  if (!all && !or_second_rows(B, valid, c2, lds, classes == 1 ? B.cand_wv : W, &any2)) all = true;
   if (all)
     for (uint32_t w = lane; w < W; w += 64) lds[w] = ~0u;
   // the verdicts are the class's (role keys may differ: role rows keep the verdict sections
-  // whole): a wave of one class and no composed lane reads them from LDS, any other lane from
-  // its own class row(s) (the LDS form is only chosen for batches that carry verdict sections)
-  F.single = !all && classes == 1 && !any2 && !B.no_verdicts;
+  // whole): a wave of one class reads them from LDS — a composed lane composing them with its
+  // second row's — any other lane from its own class row(s) (the LDS form is only chosen for
+  // batches that carry verdict sections)
+  F.single = !all && classes == 1 && !B.no_verdicts;
   const bool c2ok = c2 == 0u || c2 - 1u < B.cand_rows;
   F.own = valid && cls < B.cand_rows && c2ok && !B.no_verdicts ? B.cand + (size_t)cls * W : nullptr;
   F.own2 = F.own && c2 ? B.cand + (size_t)(c2 - 1u) * W : nullptr;
