@@ -120,7 +120,13 @@ def build_host_core(force=False):
 
 
 def build_all(force=False):
-    return build_product(force), build_host_core(force), build_napi(force), build_scan(force)
+    """The product, the counting build and the host core compile in parallel (each hipcc run is
+    single-threaded and takes minutes); the addon links against the product afterwards."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(3) as ex:
+        jobs = [ex.submit(f, force) for f in (build_product, build_host_core, build_scan)]
+        lib, host, scan = [j.result() for j in jobs]
+    return lib, host, build_napi(force), scan
 
 
 if __name__ == "__main__":

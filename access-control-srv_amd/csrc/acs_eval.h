@@ -52,6 +52,31 @@ enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET,
 #define PROF_ADD(k, v)
 #endif
 
+// Operation counting (tools/op_count.py; a separate -DACS_OP_COUNT build only): how many times
+// the waves execute each evaluation step (once per wave that runs it) and how many lanes are
+// active when they do — the per-wave attribution of K1's instruction and load counts.
+enum OpCount {
+  OP_SET_ITER, OP_SET_SKIP, OP_SET_EVAL, OP_SET_EVENTS, OP_SET_TARGET, OP_P2A_ITER, OP_P2A_TM, OP_MULTI,
+  OP_P2B_ITER, OP_P2B_TM, OP_P2B_HR, OP_RULE_LOOP, OP_RULE_ITER, OP_RULE_TM, OP_RULE_HR, OP_RULE_ACL,
+  OP_WORD, OP_V_LDS, OP_V_OWN, OP_V_OWN2, OP_ROWS, OP_ROWS2, OP_LANE_DONE, OP_N
+};
+#if defined(ACS_OP_COUNT)
+__device__ unsigned long long acs_op_wave[OP_N], acs_op_lane[OP_N];
+#endif
+#if defined(ACS_OP_COUNT) && defined(__HIP_DEVICE_COMPILE__)
+__device__ inline void op_count(int k) {
+  const uint64_t m = __ballot(1);
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (lane == (uint32_t)__builtin_ctzll(m)) {
+    atomicAdd(&acs_op_wave[k], 1ull);
+    atomicAdd(&acs_op_lane[k], (unsigned long long)__builtin_popcountll(m));
+  }
+}
+#define ACS_OPC(k) op_count(k)
+#else
+#define ACS_OPC(k)
+#endif
+
 // regex matrix cell bits (rule entity value row x request entity value column)
 enum RxBits : uint8_t { RX_HIT = 1, RX_RESET = 2, RX_THROW_TYPE = 4, RX_THROW_SYNTAX = 8, RX_HOST = 16 };
 
@@ -301,6 +326,7 @@ struct Filter {
     if (w < lds_n) return wave_uniform(((lds_u32*)lds)[w]);
 #endif
     ACS_SCAN(8);  // a word of the lanes' class and role rows (counted once per wave)
+    ACS_OPC(OP_WORD);
     uint32_t x = row[w];
     if (row2) x |= row2[w];
     if (rrow) x &= role_word(rrow, rrow2, w);
@@ -334,6 +360,7 @@ struct FilterLds {
   const uint32_t* own2;
   bool single;
   ACS_FN uint32_t word(uint32_t w) const {
+    ACS_OPC(OP_WORD);
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const uint32_t lds_u32;
     return wave_uniform(((lds_u32*)lds)[w]);
@@ -344,6 +371,10 @@ struct FilterLds {
   // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane);
   // conj: a known-false section
   ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
+#if defined(ACS_OP_COUNT)
+    ACS_OPC(single ? OP_V_LDS : OP_V_OWN);
+    if (own2) ACS_OPC(OP_V_OWN2);
+#endif
     if (single) return compose_verdict(word(wv + sec + w), own2, wv + sec + w, conj);
     return own ? compose_verdict(own[wv + sec + w], own2, wv + sec + w, conj) : 0u;
   }
@@ -1031,8 +1062,10 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
                     uint8_t* eff, uint8_t* ec, Decision* ev) {
   const Tables& T = R.T;
   const uint32_t WP = (T.n_pols + 31) >> 5;  // verdict section stride
+  ACS_OPC(events_only ? OP_SET_EVENTS : OP_SET_EVAL);
   if (S.nflags & NF_HAS_TARGET) {
     PROF_T0(t0);
+    ACS_OPC(OP_SET_TARGET);
     const tri m = target_match(S, R, EFF_PERMIT, false, false, nullptr);
     PROF_ADD(PH_SET_TARGET, t0);
     if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
@@ -1046,10 +1079,15 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     CandRange pols(F, F.wp, S.child_begin, S.child_end);
     uint32_t p;
     while (pols.next(p)) {
+      ACS_OPC(OP_P2A_ITER);
       const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) return *ev = make_err(-(tri)ERR_TYPE, s + 1), SET_EVENT;
       if (P.nflags & NF_HAS_TARGET) {
-        const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p, true) ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
+        const bool vt = F.verdict(0, p), vf = !vt && F.verdict(WP, p, true);
+#if defined(ACS_OP_COUNT)
+        if (!vt && !vf) ACS_OPC(OP_P2A_TM);
+#endif
+        const tri m = vt ? 1 : vf ? 0 : target_match(P, R, P.pe_at, false, false, nullptr);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
         if (m) {
           exact = true;
@@ -1062,6 +1100,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   PROF_ADD(PH_POL_EXACT, t2a);
   if (exact && R.flag(RQ_MULTI_ENT)) {
     PROF_T0(tm);
+    ACS_OPC(OP_MULTI);
     const tri m = multiple_entities(S, R);
     PROF_ADD(PH_MULTI, tm);
     if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
@@ -1072,6 +1111,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
   uint32_t p;
   while (pols.next(p)) {
+    ACS_OPC(OP_P2B_ITER);
     const NodeRec P = node_at(T, T.pols, p, T.n_pols);
     if (P.nflags & NF_NULL) continue;
     if (events_only && (P.nflags & NF_COND_FREE) && P.ca != CA_INVALID) continue;  // raises no event
@@ -1088,6 +1128,9 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       // the class's verdict for this lane's mode
       const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
       const bool kf = exact ? F.verdict(WP, p, true) : F.verdict(3 * WP, p, true);
+#if defined(ACS_OP_COUNT)
+      if (!kt && !kf) ACS_OPC(OP_P2B_TM);
+#endif
       const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, false, nullptr);
       if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
       if (!m) {
@@ -1095,6 +1138,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
         continue;
       }
       if (P.tflags & TF_HAS_SUBJECTS) {
+        ACS_OPC(OP_P2B_HR);
         const tri h = hierarchical_scope(P, R);
         if (h < 0) return *ev = make_err(h, s + 1), SET_EVENT;
         psm = h != 0;
@@ -1108,9 +1152,11 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     }
     Fold rf(P.ca);
     const bool cut_r = safe && (P.nflags & NF_COND_FREE);
+    ACS_OPC(OP_RULE_LOOP);
     CandRange rules(F, F.wr, P.child_begin, P.child_end);
     uint32_t r;
     while (rules.next(r)) {
+      ACS_OPC(OP_RULE_ITER);
       const NodeRec Q = rule_at(T, r);
       if (Q.nflags & NF_NULL) continue;
       if (cond_rules_only && !(Q.nflags & NF_HAS_CONDITION)) continue;
@@ -1119,11 +1165,16 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       tri m = 1;
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
-        m = F.verdict(4 * WP, r) ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
+        const bool vt = F.verdict(4 * WP, r);
+#if defined(ACS_OP_COUNT)
+        if (!vt) ACS_OPC(OP_RULE_TM);
+#endif
+        m = vt ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
         PROF_ADD(PH_RULE_TARGET, tr);
         if (!m) continue;
         PROF_T0(th);
+        ACS_OPC(OP_RULE_HR);
         m = hierarchical_scope(Q, R);
         PROF_ADD(PH_RULE_HR, th);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
@@ -1137,6 +1188,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       }
       if (m && (Q.nflags & NF_HAS_TARGET)) {
         PROF_T0(ta);
+        ACS_OPC(OP_RULE_ACL);
         m = verify_acl(Q, R);
         PROF_ADD(PH_RULE_ACL, ta);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
@@ -1213,10 +1265,14 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
   while (sets.next(s)) {
+    ACS_OPC(OP_SET_ITER);
     const NodeRec S = node_at(T, T.sets, s, T.n_sets);
     // below the deciding set (or an event) only an event can change the record, and a clean
     // set cannot raise one for a safe request: skip it (the unclean ones below are walked)
-    if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN)) continue;
+    if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN)) {
+      ACS_OPC(OP_SET_SKIP);
+      continue;
+    }
     uint8_t e2 = EFF_UNDEF, c2 = EC_UNDEF;
     Decision d2{};
     const bool events_only = (have_ev || last_set) && safe && S.ca != CA_INVALID;
@@ -1234,6 +1290,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     }
     if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN_BELOW)) break;
   }
+  ACS_OPC(OP_LANE_DONE);
   if (have_ev) return ev;
   Decision out{};
   if (!last_set) {

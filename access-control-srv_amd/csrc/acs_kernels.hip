@@ -396,6 +396,7 @@ __device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, u
     const uint32_t* row = B.cand + (size_t)(k - 1u) * W;
     for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w];
     ACS_SCAN(LW * 4u);
+    ACS_OPC(OP_ROWS2);
     pending &= ~__ballot(valid && c2 == k);
   }
   return true;
@@ -480,6 +481,7 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     if (r != NO_ROLE_KEY) role_rows_of(B, r, &q1, &q2);
     for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & role_word(q1, q2, w);
     ACS_SCAN(W * (q1 ? (q2 ? 12u : 8u) : 4u));
+    ACS_OPC(OP_ROWS);
     if (c != first_cls) {
       first_cls = c;
       ++classes;
@@ -1009,9 +1011,11 @@ extern "C" void acs_internal_shard_plan(const acs_req_batch* b, size_t lo, size_
                                         size_t plan[4]);
 extern "C" int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t n_pols, uint32_t n_rules,
                                          uint32_t rx_rows_min, uint32_t* arena_end);
+extern "C" int acs_internal_check_acl_none(const acs_req_batch* b, uint32_t id_user);
 
 static int check_batch(const acs_tables* t, const acs_req_batch* b) {
-  return acs_internal_check_batch(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min);
+  return acs_internal_check_batch(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min) ||
+         acs_internal_check_acl_none(b, t->view.id_user);
 }
 
 extern "C" {
@@ -1020,6 +1024,21 @@ const char* acs_last_error(void) { return g_err.c_str(); }
 
 // The codec (acs_codec.cpp) reports through the same thread-local message.
 void acs_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
+#if defined(ACS_OP_COUNT)
+// Operation-counting build only (tools/op_count.py): read and reset the per-operation wave and
+// lane counts (acs_eval.h OpCount); out[0..n) waves, out[n..2n) lanes.
+int acs_op_read(unsigned long long* out, int n) {
+  if (n > (int)OP_N) n = OP_N;
+  std::vector<unsigned long long> z(OP_N, 0);
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpyFromSymbol(out, HIP_SYMBOL(acs_op_wave), n * sizeof *out));
+  HIP_OK(hipMemcpyFromSymbol(out + n, HIP_SYMBOL(acs_op_lane), n * sizeof *out));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_op_wave), z.data(), OP_N * sizeof z[0]));
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(acs_op_lane), z.data(), OP_N * sizeof z[0]));
+  return 0;
+}
+#endif
 
 #if defined(ACS_SCAN_COUNT)
 // Counting build only: read and reset the table bytes the waves read (bench.py B_scan).
@@ -1225,7 +1244,9 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->view.n_rules = h.n_rules;
   t->view.id_user = h.id_user;
   t->view.rstride = rstride;
-  t->view.ev_index = (const uint32_t*)(base + ev_off);
+  // the index packs a set's rule end in 30 bits (flags in bits 30 / 31): a store of 2^30 rules or
+  // more runs without it (no set is skipped for it; the decisions are the same)
+  t->view.ev_index = h.n_rules < (1u << 30) ? (const uint32_t*)(base + ev_off) : nullptr;
   t->image_bytes = img_total;
   return t;
 }
@@ -1279,7 +1300,7 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
     r->view.rres = (const RuleResAttr*)rebase(t->view.rres);
     r->view.pairs = (const Pair*)rebase(t->view.pairs);
     r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
-    r->view.ev_index = (const uint32_t*)rebase(t->view.ev_index);
+    r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
     r->sort = t->sort;
     t->peers.push_back(r);
   }
@@ -2071,7 +2092,9 @@ static int multi_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t
 // primary MAX-reduces the keys (peer copies over xGMI, max_keys_kernel) and decodes them into
 // the records an unsharded evaluation writes.
 static int sharded_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
-  if (acs_internal_check_batch(b, t->g_sets, t->g_pols, t->g_rules, t->rx_rows_min)) return -1;
+  if (acs_internal_check_batch(b, t->g_sets, t->g_pols, t->g_rules, t->rx_rows_min) ||
+      acs_internal_check_acl_none(b, t->view.id_user))
+    return -1;
   if (b->n > 0xFFFFFFFFull) return fail("acs_is_allowed: batch too large");
   std::vector<acs_tables*> dev{t};
   dev.insert(dev.end(), t->peers.begin(), t->peers.end());
@@ -2155,7 +2178,8 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
   if (split_across_devices(t, b)) {
     std::vector<uint32_t> arena_end(b->n);
     if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
-                                  arena_end.data()))
+                                  arena_end.data()) ||
+        acs_internal_check_acl_none(b, t->view.id_user))
       return -1;
     return multi_is_allowed(t, b, out, arena_end.data());
   }
@@ -2183,7 +2207,8 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
   if (split_across_devices(t, b)) {
     std::vector<uint32_t> arena_end(b->n);
     if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
-                                  arena_end.data()))
+                                  arena_end.data()) ||
+        acs_internal_check_acl_none(b, t->view.id_user))
       return -1;
     return multi_what_is_allowed(t, b, bits, obl, obl_n, out, arena_end.data());
   }

@@ -238,6 +238,60 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
   return 0;
 }
 
+// ACL_NONE (acs_layout.h) is a claim K1 acts on (it skips ACL-gated rules and ACL-inert sets):
+// verifyACL (verifyACL.ts:89-251) is false for every rule, rule-independently, without an error.
+// Recomputed here from what verify_acl itself reads — the flags, the ACL instance lists, the
+// grants and the role-scoping pairs of the request's arena (encoder._acl_none,
+// acs_codec.cpp's ACL_NONE block) — and a request whose arena does not support it is rejected.
+// id_user: the image's interned urns.user.  Run after acs_internal_check_batch (arena bounds).
+int acs_internal_check_acl_none(const acs_req_batch* b, uint32_t id_user) {
+  const size_t n = b->n;
+  const bool compact = b->hdr == nullptr;
+  const ReqHdr* hdr = (const ReqHdr*)b->hdr;
+  const ReqLine* lines = (const ReqLine*)b->lines;
+  for (size_t i = 0; i < n; ++i) {
+    const ReqHdr hd = compact ? lines[i].h : hdr[i];
+    if (((hd.flags >> RQ_ACL_SHIFT) & 3u) != ACL_NONE || (hd.flags & (RQ_HOST | RQ_NO_TARGET))) continue;
+    const uint32_t f = hd.flags;
+    if ((f & RQ_SUBJ_MISSING) || !((f & RQ_RA_EMPTY) || (f & RQ_HRS_ITERABLE)))
+      return bad("batch: ACL_NONE on a request whose verifyACL can throw", i);
+    if ((f & RQ_RA_EMPTY) || !(f & (RQ_ACT_CREATE | RQ_ACT_RMD))) continue;  // false for every rule
+    const uint32_t* ar = b->arena + hd.arena_off;
+    const uint32_t c0 = ar[0], c1 = ar[1];
+    const uint32_t ng = c0 & 0xFF, nre = (c0 >> 8) & 0xFF, ns = (c0 >> 16) & 0xFF, nro = c0 >> 24;
+    const uint32_t nt = c1 & 0xFF, nh = (c1 >> 8) & 0xFF;
+    const uint32_t* grants = ar + 2;
+    const uint32_t* rolese = grants + 3 * ng;
+    const uint32_t* tse = rolese + 2 * nre + nro + nh + ns;
+    bool none;
+    if (nt == 0) {
+      none = false;  // verifyACL returns true when no ACL entity is left to check
+    } else if (f & RQ_ACT_CREATE) {
+      none = false;
+      for (uint32_t e = 0; e < nt && !none; ++e) {
+        const uint32_t se = tse[3 * e];
+        if (se == id_user) continue;
+        bool scoped = false;
+        for (uint32_t k = 0; k < nre && !scoped; ++k) scoped = rolese[2 * k + 1] == se;
+        if (!scoped) none = true;
+      }
+    } else {  // read / modify / delete: no instance is the subject (user entity) or a grant's
+      none = true;
+      for (uint32_t e = 0; e < nt && none; ++e) {
+        const uint32_t se = tse[3 * e], ni = tse[3 * e + 1];
+        const uint32_t* inst = ar + tse[3 * e + 2];
+        for (uint32_t x = 0; x < ni && none; ++x) {
+          if (se == id_user && inst[2 * x] == hd.subject_id) none = false;
+          for (uint32_t g = 0; g < ng && none; ++g)
+            if (grants[3 * g + 1] == se && grants[3 * g + 2] == inst[2 * x]) none = false;
+        }
+      }
+    }
+    if (!none) return bad("batch: ACL_NONE on a request whose ACLs can let a rule pass", i);
+  }
+  return 0;
+}
+
 // The slices of a compact batch that requests [lo, hi) read (the multi-device split uploads
 // only these): plan[0..1] = arena words [a0, a1), plan[2..3] = extension words [e0, e1).
 // arena_end from acs_internal_check_batch2.  Empty ranges are [0, 0).

@@ -122,10 +122,15 @@ function isEmptyValue(v) {
 }
 
 // unmarshallProtobufAny (src/accessControlService.ts:116-127) as JSON text: null for a nil
-// message or an empty value, else the value's text (the reference JSON.parses it)
+// message or an empty value, else the value's text.  The reference JSON.parses that text alone
+// and throws when it is not exactly one JSON value; it is parsed here alone too, so a value
+// that only parses as part of the batch text (`1}},{"target":…` injecting a request of its
+// own, or `1,"x":2` a context member) throws the same SyntaxError instead of being spliced.
 function unmarshalText(x) {
   if (!x || isEmptyValue(x.value)) return 'null';
-  return x.value.toString();
+  const text = x.value.toString();
+  JSON.parse(text);
+  return text;
 }
 
 // The JSON text of the request AccessControlService.isAllowed / whatIsAllowed builds from a
@@ -453,15 +458,20 @@ class GpuAccessController {
   // context members are protobuf Any messages: their JSON text goes to the codec as is
   // (grpcRequestJson), micro-batched like isAllowed().
   isAllowedGrpc(grpcRequest) {
-    return this._enqueue('isAllowed', null, grpcRequestJson(grpcRequest));
+    return this._enqueue('isAllowed', null, () => grpcRequestJson(grpcRequest));
   }
 
   whatIsAllowedGrpc(grpcRequest) {
-    return this._enqueue('whatIsAllowed', null, grpcRequestJson(grpcRequest));
+    return this._enqueue('whatIsAllowed', null, () => grpcRequestJson(grpcRequest));
   }
 
-  _enqueue(op, request, text) {
+  // The call's JSON text is made here, inside the promise executor: a request that cannot be
+  // serialised (BigInt, a cycle, a context Any value that is not one JSON value) rejects this
+  // call alone, as the reference's promise would, and never reaches a batch.
+  _enqueue(op, request, makeText) {
     return new Promise((resolve, reject) => {
+      const text = makeText ? makeText() : JSON.stringify(request);
+      if (typeof text !== 'string') throw new TypeError('request is not serialisable as JSON');
       const q = this._queues[op];
       q.push({ request, text, resolve, reject });
       if (q.length >= this.batchMax) {
@@ -478,19 +488,39 @@ class GpuAccessController {
     });
   }
 
-  // Decide the queued calls of `op` as one batch.  A batch whose text the codec rejects (a
-  // gRPC context value that is not JSON) is re-run without the requests whose text does not
-  // parse; those reject with the SyntaxError the reference's JSON.parse throws.
+  // Decide the queued calls of `op` as one batch.
   _flush(op) {
     const items = this._queues[op];
     if (!items.length) return;
     this._queues[op] = [];
-    const texts = items.map((x) => (x.text !== null ? x.text : JSON.stringify(x.request)));
+    this._decide(op, items);
+  }
+
+  // Decide `items` (queued calls of `op`) as one batch and settle each call with its own
+  // record.  A batch the codec rejects as a whole is re-run without the requests whose text does
+  // not parse (those reject with the SyntaxError of the reference's JSON.parse).  Records are
+  // matched to callers by position, so a batch must come back with exactly one record per call:
+  // if it does not, nothing is delivered, every call is re-run as a batch of its own, and a call
+  // that still does not decode as exactly one request rejects.
+  _decide(op, items) {
     const request = (i) => (items[i].request !== null ? items[i].request : JSON.parse(items[i].text));
-    const text = '[' + texts.join(',') + ']';
-    const run = op === 'isAllowed' ? this._isAllowedText(text, request)
-      : this.whatIsAllowedBatch(text, request);
+    let run;
+    try {
+      const text = '[' + items.map((x) => x.text).join(',') + ']';
+      run = op === 'isAllowed' ? this._isAllowedText(text, request) : this.whatIsAllowedBatch(text, request);
+    } catch (e) {
+      for (const it of items) it.reject(e);
+      return;
+    }
     run.then((out) => {
+      if (!out || out.length !== items.length) {
+        if (items.length === 1) {
+          items[0].reject(new Error('request text decoded as ' + (out ? out.length : 0) + ' requests'));
+          return;
+        }
+        for (const it of items) this._decide(op, [it]);
+        return;
+      }
       for (let i = 0; i < items.length; ++i) {
         if (out[i] instanceof Error) items[i].reject(out[i]);
         else items[i].resolve(out[i]);
@@ -499,7 +529,7 @@ class GpuAccessController {
       const ok = [];
       for (const it of items) {
         try {
-          if (it.text !== null) JSON.parse(it.text);
+          JSON.parse(it.text);
           ok.push(it);
         } catch (e) {
           it.reject(e);
@@ -509,8 +539,7 @@ class GpuAccessController {
         for (const it of items) it.reject(err);
         return;
       }
-      this._queues[op] = ok.concat(this._queues[op]);
-      this._flush(op);
+      if (ok.length) this._decide(op, ok);
     });
   }
 

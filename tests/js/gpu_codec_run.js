@@ -100,6 +100,16 @@ const enc = (x) => (x instanceof Error ? { $error: x.name, reason: x.reason } : 
       res.microSame = JSON.stringify(ia1.map(enc)) === JSON.stringify(res.isAllowed) &&
         JSON.stringify(wa1.map(enc)) === JSON.stringify(res.whatIsAllowed);
       res.grpcSame = JSON.stringify(ia2.map(enc)) === JSON.stringify(res.isAllowed);
+      // a concurrent call whose Any value would splice a request of its own into the batch
+      // (ADVICE r4): it rejects alone, and its neighbours get their own answers
+      if (c.isAllowed.length >= 2 && grpcable(c.isAllowed[0]) && grpcable(c.isAllowed[1])) {
+        const inj = '1}},{"target":' + JSON.stringify(c.isAllowed[1].target || {}) + ',"context":{"a":1';
+        const bad = { target: c.isAllowed[0].target, context: { subject: { type_url: 't', value: Buffer.from(inj) } } };
+        const r3 = await Promise.all([settle(ctl.isAllowedGrpc(grpc(c.isAllowed[0]))), settle(ctl.isAllowedGrpc(bad)),
+          settle(ctl.isAllowedGrpc(grpc(c.isAllowed[1])))]);
+        res.injectSafe = JSON.stringify(enc(r3[0])) === JSON.stringify(res.isAllowed[0]) &&
+          r3[1] instanceof SyntaxError && JSON.stringify(enc(r3[2])) === JSON.stringify(res.isAllowed[1]);
+      }
     }
     {  // the same requests through the decision pipeline (3-request chunks) on a handle
        // replicated twice on device 0: the same answers

@@ -39,6 +39,8 @@ const any = () => {
   if (r < 0.25) return { type_url: 't' };
   if (r < 0.3) return { type_url: 't', value: '' };
   if (r < 0.35) return { type_url: 't', value: JSON.stringify(jsonValue()) };  // a string value
+  // texts that are not one JSON value alone but splice into valid JSON: the reference throws
+  if (r < 0.4) return { type_url: 't', value: Buffer.from(pick(['1}},{"target":{},"context":{"a":1', '1,"x":2', '"a"]', '[1', '1 2', '{}{}'])) };
   return { type_url: 't', value: Buffer.from(JSON.stringify(jsonValue())) };
 };
 function grpcRequest() {

@@ -1,7 +1,7 @@
 """c5 (configs[4]): the full 1M-rule store (1,000 sets x 10 policies x 100 rules) on the GPU.
 
-* a request batch against the whole store: a C++-oracle sample (the reference's
-  algorithm over the decoded JSON requests) must match every record;
+* a request batch against the whole store: a 1 % C++-oracle sample (1,000 of 100,000; the
+  reference's algorithm over the decoded JSON requests) must match every record;
 * rule sharding at c5 scale: the store cut into 8 runs of whole policy sets (one per
   rank of the rule-sharded bench), each evaluated on this GPU, the 64-bit keys reduced
   with MAX (what the RCCL all-reduce does across ranks) — bit-identical to the
@@ -42,8 +42,9 @@ def test_c5_oracle_sample_gpu(c5):
     doc, full, cs, sb, dec = c5
     codes = np.bincount(dec["decision"], minlength=7)
     assert codes[L.DEC_PERMIT] > 0 and codes[L.DEC_DENY] > 0
-    idx = np.random.default_rng(55).choice(N, size=96, replace=False)
-    assert coracle_check(doc, cs, sb, dec, idx, chunk=96) == 96
+    # 1,000 requests (1 % of the batch): the C++ oracle decides ~60 c5 requests/s on 16 threads
+    idx = np.random.default_rng(55).choice(N, size=1000, replace=False)
+    assert coracle_check(doc, cs, sb, dec, idx, chunk=250) == 1000
 
 
 def test_c5_rule_shard_8_gpu(c5):

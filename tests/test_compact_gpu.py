@@ -120,3 +120,29 @@ def test_pipeline_errors_and_host_requests_gpu():
     p.close()
     codec.close()
     t.close()
+
+
+def test_pipeline_error_mid_run_then_single_request_gpu():
+    """Round-3 advisor / round-4 verdict: an item that only fails in the codec (malformed JSON inside
+    a well-delimited array) in the SECOND chunk — with the first chunk already in flight — fails
+    the call; the pipeline drains (pipeline_reset), and the next call, one request, gets exactly
+    its own record, not a stale record of the failed run."""
+    cs = compiler.compile_store(store.populate(synth.c2_store()), FULL_URNS, DEFAULT_CAS)
+    t = native.Tables(compiler.store_blob(cs), 0)
+    codec = NativeCodec(compiler.store_blob(cs))
+    sb = synth.requests(cs, 64, "c2", seed=9)
+    items = [sb.json_text(np.array([i])).decode()[1:-1] for i in range(8)]
+    want = t.is_allowed(codec.encode(("[" + ",".join(items) + "]").encode()))
+    p = Pipeline(t, codec, threads=2, chunk=3)
+    bad = items[:4] + ['{"target": {"subjects": [}, "context": {}}'] + items[5:]
+    with pytest.raises(RuntimeError):
+        p.is_allowed(("[" + ",".join(bad) + "]").encode(), len(bad))
+    for k in (7, 2, 0):
+        got, st = p.is_allowed(("[" + items[k] + "]").encode(), 1)
+        assert len(got) == 1 and st["chunks"] == 1
+        assert _u64(got)[0] == _u64(want)[k], k
+    got, _ = p.is_allowed(("[" + ",".join(items) + "]").encode(), len(items))  # the whole run still works
+    assert np.array_equal(_u64(got), _u64(want))
+    p.close()
+    codec.close()
+    t.close()

@@ -55,6 +55,7 @@ def _run(tmp, cases, mode, timeout=600):
         for k, res in enumerate(out):
             assert "compileError" in res or (res["pipelineSame"] and res["devices"] == [0, 0]), k
             assert "compileError" in res or (res["microSame"] and res["grpcSame"]), k
+            assert res.get("injectSafe", True), k
     return out
 
 

@@ -149,3 +149,37 @@ def test_corrupt_images_refused_before_device_work(lib):
         assert lib.acs_internal_check_blob(blob_bad, len(blob_bad), C.byref(rows)) != 0
         assert not lib.acs_compile(blob_bad, len(blob_bad), 0)
         assert "malformed image" in native.last_error(lib)
+
+
+def test_acl_none_claim_checked_against_arena(lib):
+    """ACL_NONE (K1 skips ACL-gated rules and ACL-inert sets for it) is recomputed from
+    the request's arena — ACL instance lists, grants, role-scoping pairs — and a request whose
+    ACLs could let a rule pass is refused; every ACL_NONE the codec writes passes."""
+    lib.acs_internal_check_acl_none.argtypes = [C.POINTER(native.ReqBatchC), C.c_uint32]
+    cs = compiler.compile_store(store.populate(synth.c3_adverse_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 4000, "c3", seed=11, acl=0.5, classes=False)
+    codec = NativeCodec(compiler.store_blob(cs))
+    for k, v in sb.hrs_forests().items():
+        codec.set_subject_scopes(k, v)
+    nb = codec.encode(sb.json_text(), threads=2)
+    s = native.batch_struct(nb, compact=True)
+    assert lib.acs_internal_check_acl_none(C.byref(s), cs.id_user) == 0, native.last_error(lib)
+    lines = nb.lines
+    state = (lines["h"]["flags"] >> np.uint32(L.RQ_ACL_SHIFT)) & np.uint32(3)
+    assert (state == L.ACL_NONE).sum() > 0
+    # ACL_CONTINUE requests with ACL entities: claiming ACL_NONE for them is refused for those whose
+    # ACLs can pass (an instance that is a grant's of the same entity, or the subject's)
+    cont = np.flatnonzero((state == L.ACL_CONTINUE) & ((lines["ar1"] & np.uint32(0xFF)) != 0)
+                          & ((lines["h"]["flags"] & np.uint32(L.RQ_ACT_RMD | L.RQ_ACT_CREATE)) != 0))
+    assert len(cont) > 0
+    refused = 0
+    for i in cont[:40]:
+        keep = lines["h"]["flags"][i]
+        lines["h"]["flags"][i] = (keep & ~np.uint32(3 << L.RQ_ACL_SHIFT)) | np.uint32(L.ACL_NONE << L.RQ_ACL_SHIFT)
+        s = native.batch_struct(nb, compact=True)
+        if lib.acs_internal_check_acl_none(C.byref(s), cs.id_user) != 0:
+            assert "ACL_NONE" in native.last_error(lib)
+            refused += 1
+        lines["h"]["flags"][i] = keep
+    assert refused > 0
+    codec.close()
