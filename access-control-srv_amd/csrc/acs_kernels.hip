@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -676,6 +677,11 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
 #endif
 }
 
+// Global set index g as an index of an image holding sets [base, base + n), clipped to [0, n].
+__device__ inline uint32_t obl_range_local(uint32_t g, uint32_t base, uint32_t n) {
+  return g <= base ? 0u : (g - base < n ? g - base : n);
+}
+
 // Obligation-only pass for requests idx[0..m) — those whose K2 log
 // overflowed (OF_OBL_OVERFLOW) — with a cap-entry maskedProperty log and no bitset, so long
 // obligation lists stay on the GPU instead of the host path.  whatIsAllowed keeps no state
@@ -689,7 +695,8 @@ template <class FL, bool CB>
 __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Batch B, const uint32_t* __restrict__ idx,
                                                                     uint32_t m, uint32_t chunks, uint32_t cap,
                                                                     uint32_t* __restrict__ obl,
-                                                                    uint32_t* __restrict__ obl_n) {
+                                                                    uint32_t* __restrict__ obl_n, uint32_t g_sets,
+                                                                    uint32_t set_base) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   // each range's lanes start on a wave boundary (m padded to 64): the set range, and with it
   // the candidate iteration, is wave-uniform
@@ -717,7 +724,10 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
     ReqRes* scol = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t q = 0; q < nq; ++q) scol[q * BLOCK] = ln ? ln->res[q] : B.res[(size_t)q * B.n + i];
-    const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks), s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
+    // range c of the whole store's sets (g_sets; a rule-sharded handle's image holds the sets
+    // [set_base, + n_sets) of it), clipped to this image's sets
+    const uint32_t s0 = obl_range_local((uint32_t)((uint64_t)g_sets * c / chunks), set_base, T.n_sets);
+    const uint32_t s1 = obl_range_local((uint32_t)((uint64_t)g_sets * (c + 1) / chunks), set_base, T.n_sets);
     NullSink none;
     const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BitsLayout{}, none, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
@@ -999,7 +1009,8 @@ struct acs_tables {
 // The entry points a rule-sharded handle does not serve (records need the cross-shard reduction)
 static int refuse_sharded(const acs_tables* t, const char* fn) {
   if (!t || !t->sharded) return 0;
-  g_err = std::string(fn) + ": a rule-sharded handle (acs_compile_sharded) serves acs_is_allowed only";
+  g_err = std::string(fn) + ": a rule-sharded handle (acs_compile_sharded) serves the host-buffer entry points only "
+          "(acs_is_allowed, acs_what_is_allowed, acs_what_is_allowed_obl)";
   return -1;
 }
 
@@ -1486,6 +1497,7 @@ int acs_device_list(const acs_tables* t, int* devices, int n) {
 }
 
 uint32_t acs_wia_words_per_request(const acs_tables* t) {
+  if (t->sharded) return bits_layout(t->g_sets, t->g_pols, t->g_rules).words;  // the joined rows
   return bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules).words;
 }
 
@@ -1749,6 +1761,25 @@ int acs_what_is_allowed_device(acs_tables* t, const acs_req_batch* b, uint32_t* 
 
 constexpr uint32_t OBL_CAP_LIMIT = 1u << 20;
 
+}  // extern "C"
+
+// The obligation-only pass on one image; the ranges cut the sets of the whole store (g_sets, this
+// image holding [set_base, + its n_sets): a shard of a rule-sharded handle).
+static int obl_launch(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t chunks,
+                      uint32_t cap, uint32_t* obl, uint32_t* obl_n, hipStream_t stream, uint32_t g_sets,
+                      uint32_t set_base) {
+  if (m == 0 || b->n == 0) return 0;
+  Batch B = to_batch(b);
+  const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
+  ACS_LAUNCH_FILTERED(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), filter_lds_bytes(B),
+                      stream, filter_form(B), B.hdr == nullptr, t->view, B, idx, (uint32_t)m, chunks, cap, obl,
+                      obl_n, g_sets, set_base);
+  HIP_OK(hipGetLastError());
+  return 0;
+}
+
+extern "C" {
+
 int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m,
                                    uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n, void* stream) {
   if (refuse_sharded(t, "acs_what_is_allowed_obl_device")) return -1;
@@ -1756,14 +1787,7 @@ int acs_what_is_allowed_obl_device(acs_tables* t, const acs_req_batch* b, const 
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl_device: cap must be in [1, 2^20]");
   if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl_device: chunks must be in [1, 64]");
   if (m > 0xFFFFFFFFull || m * chunks > 0xFFFFFFFFull) return fail("acs_what_is_allowed_obl_device: too many requests");
-  if (m == 0 || b->n == 0) return 0;
-  Batch B = to_batch(b);
-  const size_t lanes = ((m + 63) & ~(size_t)63) * chunks;  // each range padded to whole waves
-  ACS_LAUNCH_FILTERED(what_is_allowed_obl_kernel, dim3((unsigned)((lanes + BLOCK - 1) / BLOCK)), filter_lds_bytes(B),
-                      (hipStream_t)stream, filter_form(B), B.hdr == nullptr, t->view, B, idx, (uint32_t)m, chunks, cap, obl,
-                      obl_n);
-  HIP_OK(hipGetLastError());
-  return 0;
+  return obl_launch(t, b, idx, m, chunks, cap, obl, obl_n, (hipStream_t)stream, t->view.n_sets, 0);
 }
 
 }  // extern "C"
@@ -2086,6 +2110,310 @@ static int multi_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t
   });
 }
 
+// Shard T of rule-sharded handle t: the whole batch uploaded to T, its class rows (and role rows)
+// cut to T's nodes on the device (slice_rows_kernel, acs_eval.h RowSlice); *d: the device batch.
+static int upload_shard_batch(acs_tables* t, acs_tables* T, const acs_req_batch* b, acs_req_batch* d) {
+  if (upload_batch(T->hws, b, d, T->stream)) return -1;
+  if (!b->cand) return 0;
+  const RowSlice L = make_row_slice(t->g_pols, b->cand_wp, b->cand_wr, b->cand_wsu, b->cand_wpu, b->cand_wv, T->base,
+                                    T->view.n_sets, T->view.n_pols, T->view.n_rules);
+  const size_t rows_w = (size_t)b->cand_rows * L.words, role_w = b->role_key ? (size_t)b->role_rows * L.words : 0;
+  if (T->hws.slice.reserve((rows_w + role_w + 1) * sizeof(uint32_t))) return -1;
+  uint32_t* dst = (uint32_t*)T->hws.slice.p;
+  if (rows_w)
+    hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((rows_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, T->stream,
+                       d->cand, b->cand_words, b->cand_rows, L, dst);
+  if (role_w)
+    hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((role_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, T->stream,
+                       d->role_rows_bits, b->cand_words, b->role_rows, L, dst + rows_w);
+  if (hipGetLastError() != hipSuccess) return fail("rule-sharded handle: row slice launch failed");
+  d->cand = dst;
+  d->cand_words = L.words;
+  d->cand_wp = L.wp;
+  d->cand_wr = L.wr;
+  d->cand_wsu = L.wsu;
+  d->cand_wpu = L.wpu;
+  d->cand_wv = L.wv;
+  d->role_rows_bits = role_w ? dst + rows_w : nullptr;
+  return 0;
+}
+
+// ---- whatIsAllowed on a rule-sharded handle ("set-sharded bitsets concatenate
+// (gather, no reduction); obligations merged on the host in set order").  whatIsAllowed keeps no
+// state across policy sets but the push log and the first throw (accessController.ts:343-419), so
+// each shard's run of sets is evaluated alone and the results are joined on the host:
+//  * bitset rows: each section of a shard's row (its local sets / policies / rules) ORed into the
+//    whole store's row at the shard's first global index (disjoint ranges);
+//  * the first shard whose record carries an error decides the request (the walk stops at the
+//    first set that throws): its record, aux made global, bits up to and including that shard;
+//  * maskedProperty logs: the shards' logs concatenated in shard (= set) order, cut at
+//    ACS_OBL_MAX entries; OF_OBL_OVERFLOW when a shard's log overflowed or the joined one did.
+// The CPU test (tests/test_rule_shard_lib.py) runs the same join over the host core's shards.
+namespace {
+// OR bits [0, nbits) of src into dst from bit d0 (only words that receive a set bit are written)
+void or_bits_at(uint32_t* dst, uint32_t d0, const uint32_t* src, uint32_t nbits) {
+  const uint32_t words = (nbits + 31) / 32, sh = d0 & 31u;
+  uint32_t* d = dst + (d0 >> 5);
+  for (uint32_t w = 0; w < words; ++w) {
+    uint32_t x = src[w];
+    const uint32_t left = nbits - 32 * w;
+    if (left < 32) x &= (1u << left) - 1u;
+    if (!x) continue;
+    d[w] |= x << sh;
+    if (sh && (x >> (32u - sh))) d[w + 1] |= x >> (32u - sh);
+  }
+}
+}  // namespace
+
+extern "C" {
+// One shard's whatIsAllowed outputs for the join (csrc: acs_what_is_allowed on a sharded handle;
+// tests: the host core on the shard's sub-image).
+typedef struct {
+  acs_shard base;                     /* the shard's first global set / policy / rule */
+  uint32_t n_sets, n_pols, n_rules;   /* its image's node counts */
+  const uint32_t* bits;               /* [n][its words_per_req] */
+  const uint32_t* obl;                /* [n][ACS_OBL_MAX][2] */
+  const uint32_t* obl_n;              /* [n] */
+  const acs_decision* out;            /* [n] */
+} acs_internal_wia_part;
+
+// Requests [lo, hi) of the join; g_*: the whole store's node counts; bits / obl / obl_n / out: the
+// caller's outputs in the unsharded layout (bits zeroed here).
+void acs_internal_wia_join(uint32_t g_sets, uint32_t g_pols, uint32_t g_rules, int parts,
+                           const acs_internal_wia_part* P, size_t lo, size_t hi, uint32_t* bits, uint32_t* obl,
+                           uint32_t* obl_n, acs_decision* out) {
+  const BitsLayout G = bits_layout(g_sets, g_pols, g_rules);
+  std::vector<BitsLayout> LL(parts);
+  for (int k = 0; k < parts; ++k) LL[k] = bits_layout(P[k].n_sets, P[k].n_pols, P[k].n_rules);
+  for (size_t i = lo; i < hi; ++i) {
+    uint32_t* row = bits + i * G.words;
+    std::memset(row, 0, (size_t)G.words * sizeof(uint32_t));
+    Decision d{};
+    std::memcpy(&d, &P[0].out[i], sizeof d);
+    if (d.flags & OF_HOST_REQ) {  // request level: the same record from every shard, no bits, no log
+      std::memcpy(&out[i], &d, sizeof d);
+      obl_n[i] = 0;
+      continue;
+    }
+    int last = parts - 1;  // the shards whose bits count (up to the first that threw)
+    bool err = false;
+    for (int k = 0; k < parts && !err; ++k) {
+      Decision e;
+      std::memcpy(&e, &P[k].out[i], sizeof e);
+      if (e.flags & OF_ERR) {
+        err = true;
+        last = k;
+        d = e;
+        if (d.aux) d.aux += P[k].base.set_base;
+      }
+    }
+    for (int k = 0; k <= last; ++k) {
+      const uint32_t* src = P[k].bits + i * LL[k].words;
+      or_bits_at(row, P[k].base.set_base, src, P[k].n_sets);
+      or_bits_at(row + G.wp, P[k].base.pol_base, src + LL[k].wp, P[k].n_pols);
+      or_bits_at(row + G.wr, P[k].base.rule_base, src + LL[k].wr, P[k].n_rules);
+    }
+    if (err) {
+      std::memcpy(&out[i], &d, sizeof d);
+      obl_n[i] = 0;
+      continue;
+    }
+    Decision o{};
+    uint32_t n = 0;
+    for (int k = 0; k < parts; ++k) {
+      Decision e;
+      std::memcpy(&e, &P[k].out[i], sizeof e);
+      if (e.flags & OF_OBL_OVERFLOW) o.flags |= OF_OBL_OVERFLOW;
+      const uint32_t kn = P[k].obl_n[i];
+      const uint32_t take = kn < OBL_MAX - n ? kn : OBL_MAX - n;
+      if (take < kn) o.flags |= OF_OBL_OVERFLOW;
+      std::memcpy(obl + (i * OBL_MAX + n) * 2, P[k].obl + (i * OBL_MAX) * 2, (size_t)take * 2 * sizeof(uint32_t));
+      n += take;
+    }
+    obl_n[i] = n;
+    std::memcpy(&out[i], &o, sizeof o);
+  }
+}
+
+// The obligation-only pass's join: range c of request j is the concatenation of the shards' parts
+// of range c (each shard ran the same global ranges clipped to its sets); its total is their sum,
+// and its log is written only when it fits `cap` (else the caller re-runs with cap = the total).
+void acs_internal_wia_obl_join(int parts, const uint32_t* const* part_obl, const uint32_t* const* part_n, size_t m,
+                               uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
+  for (size_t x = 0; x < (size_t)chunks * m; ++x) {
+    uint64_t total = 0;
+    bool outside = false;
+    for (int k = 0; k < parts; ++k) {
+      if (part_n[k][x] == 0xFFFFFFFFu) outside = true;
+      total += part_n[k][x];
+    }
+    if (outside) {
+      obl_n[x] = 0xFFFFFFFFu;
+      continue;
+    }
+    obl_n[x] = total > 0xFFFFFFFEull ? 0xFFFFFFFEu : (uint32_t)total;
+    if (total > cap) continue;
+    uint32_t at = 0;
+    for (int k = 0; k < parts; ++k) {
+      std::memcpy(obl + (x * cap + at) * 2, part_obl[k] + x * cap * 2, (size_t)part_n[k][x] * 2 * sizeof(uint32_t));
+      at += part_n[k][x];
+    }
+  }
+}
+}  // extern "C"
+
+// The join over host threads (a few rows each).
+static void wia_join_threaded(const acs_tables* t, const std::vector<acs_internal_wia_part>& P, size_t n,
+                              uint32_t* bits, uint32_t* obl, uint32_t* obl_n, acs_decision* out) {
+  const size_t T = std::max<size_t>(1, std::min<size_t>(16, std::min<size_t>(std::thread::hardware_concurrency(),
+                                                                             n / 4096 + 1)));
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < T; ++k)
+    th.emplace_back([&, k] {
+      acs_internal_wia_join(t->g_sets, t->g_pols, t->g_rules, (int)P.size(), P.data(), n * k / T, n * (k + 1) / T,
+                            bits, obl, obl_n, out);
+    });
+  for (auto& x : th) x.join();
+}
+
+// Every shard evaluates the whole batch against its sets (K2 on its image, class rows cut to its
+// nodes), the outputs come back to host staging, and the join writes the caller's buffers.
+static int sharded_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
+                                   uint32_t* obl_n, acs_decision* out) {
+  if (acs_internal_check_batch(b, t->g_sets, t->g_pols, t->g_rules, t->rx_rows_min) ||
+      acs_internal_check_acl_none(b, t->view.id_user))
+    return -1;
+  if (b->n > 0xFFFFFFFFull) return fail("acs_what_is_allowed: batch too large");
+  std::vector<acs_tables*> dev{t};
+  dev.insert(dev.end(), t->peers.begin(), t->peers.end());
+  const size_t D = dev.size(), n = b->n;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
+  struct Stage {
+    std::vector<uint32_t> bits, obl, obl_n;
+    std::vector<acs_decision> out;
+  };
+  std::vector<Stage> st(D);
+  size_t launched = 0;
+  auto drain = [&] {
+    const std::string err = g_err;
+    for (size_t k = 0; k < launched; ++k) {
+      (void)hipSetDevice(dev[k]->device);
+      (void)hipStreamSynchronize(dev[k]->stream);
+    }
+    (void)hipSetDevice(t->device);
+    g_err = err;
+    return -1;
+  };
+  for (size_t k = 0; k < D; ++k) {
+    acs_tables* T = dev[k];
+    const size_t words = bits_layout(T->view.n_sets, T->view.n_pols, T->view.n_rules).words;  // its own rows
+    Stage& S = st[k];
+    S.bits.resize(n * words);
+    S.obl.resize(n * 2 * OBL_MAX);
+    S.obl_n.resize(n);
+    S.out.resize(n);
+    if (hipSetDevice(T->device) != hipSuccess) return fail("acs_what_is_allowed: hipSetDevice failed"), drain();
+    launched = k + 1;
+    acs_req_batch d;
+    if (upload_shard_batch(t, T, b, &d)) return drain();
+    OutLayout O;
+    const size_t o_bits = O.put(n * words * sizeof(uint32_t)), o_obl = O.put(n * 2 * OBL_MAX * sizeof(uint32_t));
+    const size_t o_n = O.put(n * sizeof(uint32_t)), o_out = O.put(n * sizeof(Decision));
+    if (T->hws.out.reserve(O.total)) return drain();
+    char* ob = (char*)T->hws.out.p;
+    if (what_is_allowed_launch(T, T->hws, &d, (uint32_t*)(ob + o_bits), (uint32_t*)(ob + o_obl), (uint32_t*)(ob + o_n),
+                               (acs_decision*)(ob + o_out), T->stream))
+      return drain();
+    if (hipMemcpyAsync(S.bits.data(), ob + o_bits, n * words * sizeof(uint32_t), hipMemcpyDeviceToHost, T->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(S.obl.data(), ob + o_obl, n * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       T->stream) != hipSuccess ||
+        hipMemcpyAsync(S.obl_n.data(), ob + o_n, n * sizeof(uint32_t), hipMemcpyDeviceToHost, T->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(S.out.data(), ob + o_out, n * sizeof(Decision), hipMemcpyDeviceToHost, T->stream) != hipSuccess)
+      return fail("acs_what_is_allowed: result copy failed"), drain();
+  }
+  for (size_t k = 0; k < D; ++k)
+    if (hipSetDevice(dev[k]->device) != hipSuccess || hipStreamSynchronize(dev[k]->stream) != hipSuccess)
+      return fail("acs_what_is_allowed: device synchronisation failed"), drain();
+  HIP_OK(hipSetDevice(t->device));
+  std::vector<acs_internal_wia_part> P(D);
+  for (size_t k = 0; k < D; ++k) {
+    const acs_tables* T = dev[k];
+    P[k].base = acs_shard{T->base.set_base, T->base.pol_base, T->base.rule_base};
+    P[k].n_sets = T->view.n_sets;
+    P[k].n_pols = T->view.n_pols;
+    P[k].n_rules = T->view.n_rules;
+    P[k].bits = st[k].bits.data();
+    P[k].obl = st[k].obl.data();
+    P[k].obl_n = st[k].obl_n.data();
+    P[k].out = st[k].out.data();
+  }
+  wia_join_threaded(t, P, n, bits, obl, obl_n, out);
+  return 0;
+}
+
+// The obligation-only pass on a rule-sharded handle: every shard runs the same global set ranges
+// clipped to its sets; the parts are joined per (range, request) in shard order.
+static int sharded_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m,
+                                       uint32_t chunks, uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
+  if (acs_internal_check_batch(b, t->g_sets, t->g_pols, t->g_rules, t->rx_rows_min) ||
+      acs_internal_check_acl_none(b, t->view.id_user))
+    return -1;
+  std::vector<acs_tables*> dev{t};
+  dev.insert(dev.end(), t->peers.begin(), t->peers.end());
+  const size_t D = dev.size(), lanes = m * chunks;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
+  std::vector<std::vector<uint32_t>> pobl(D), pn(D);
+  size_t launched = 0;
+  auto drain = [&] {
+    const std::string err = g_err;
+    for (size_t k = 0; k < launched; ++k) {
+      (void)hipSetDevice(dev[k]->device);
+      (void)hipStreamSynchronize(dev[k]->stream);
+    }
+    (void)hipSetDevice(t->device);
+    g_err = err;
+    return -1;
+  };
+  for (size_t k = 0; k < D; ++k) {
+    acs_tables* T = dev[k];
+    pobl[k].resize(lanes * 2 * (size_t)cap);
+    pn[k].resize(lanes);
+    if (hipSetDevice(T->device) != hipSuccess) return fail("acs_what_is_allowed_obl: hipSetDevice failed"), drain();
+    launched = k + 1;
+    acs_req_batch d;
+    if (upload_shard_batch(t, T, b, &d)) return drain();
+    OutLayout O;
+    const size_t o_idx = O.put(m * sizeof(uint32_t)), o_obl = O.put(lanes * 2 * (size_t)cap * sizeof(uint32_t));
+    const size_t o_n = O.put(lanes * sizeof(uint32_t));
+    if (T->hws.out.reserve(O.total)) return drain();
+    char* ob = (char*)T->hws.out.p;
+    if (hipMemcpyAsync(ob + o_idx, idx, m * sizeof(uint32_t), hipMemcpyHostToDevice, T->stream) != hipSuccess)
+      return fail("acs_what_is_allowed_obl: index upload failed"), drain();
+    if (obl_launch(T, &d, (const uint32_t*)(ob + o_idx), m, chunks, cap, (uint32_t*)(ob + o_obl), (uint32_t*)(ob + o_n),
+                   T->stream, t->g_sets, T->base.set_base))
+      return drain();
+    if (hipMemcpyAsync(pobl[k].data(), ob + o_obl, lanes * 2 * (size_t)cap * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                       T->stream) != hipSuccess ||
+        hipMemcpyAsync(pn[k].data(), ob + o_n, lanes * sizeof(uint32_t), hipMemcpyDeviceToHost, T->stream) != hipSuccess)
+      return fail("acs_what_is_allowed_obl: result copy failed"), drain();
+  }
+  for (size_t k = 0; k < D; ++k)
+    if (hipSetDevice(dev[k]->device) != hipSuccess || hipStreamSynchronize(dev[k]->stream) != hipSuccess)
+      return fail("acs_what_is_allowed_obl: device synchronisation failed"), drain();
+  HIP_OK(hipSetDevice(t->device));
+  std::vector<const uint32_t*> po(D), pc(D);
+  for (size_t k = 0; k < D; ++k) {
+    po[k] = pobl[k].data();
+    pc[k] = pn[k].data();
+  }
+  acs_internal_wia_obl_join((int)D, po.data(), pc.data(), m, chunks, cap, obl, obl_n);
+  return 0;
+}
+
 // A rule-sharded handle (acs_compile_sharded): every device evaluates the whole batch against
 // its run of policy sets — the batch uploaded to each, its class rows cut to the device's nodes
 // (slice_rows_kernel), K1, then the records turned into 64-bit keys (shard_key) — and the
@@ -2118,29 +2446,7 @@ static int sharded_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decisio
     if (hipSetDevice(T->device) != hipSuccess) return fail("acs_is_allowed: hipSetDevice failed"), drain();
     launched = k + 1;
     acs_req_batch d;
-    if (upload_batch(T->hws, b, &d, T->stream)) return drain();
-    if (b->cand) {
-      const RowSlice L = make_row_slice(t->g_pols, b->cand_wp, b->cand_wr, b->cand_wsu, b->cand_wpu, b->cand_wv,
-                                        T->base, T->view.n_sets, T->view.n_pols, T->view.n_rules);
-      const size_t rows_w = (size_t)b->cand_rows * L.words, role_w = b->role_key ? (size_t)b->role_rows * L.words : 0;
-      if (T->hws.slice.reserve((rows_w + role_w + 1) * sizeof(uint32_t))) return drain();
-      uint32_t* dst = (uint32_t*)T->hws.slice.p;
-      if (rows_w)
-        hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((rows_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                           T->stream, d.cand, b->cand_words, b->cand_rows, L, dst);
-      if (role_w)
-        hipLaunchKernelGGL(slice_rows_kernel, dim3((unsigned)((role_w + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                           T->stream, d.role_rows_bits, b->cand_words, b->role_rows, L, dst + rows_w);
-      if (hipGetLastError() != hipSuccess) return fail("acs_is_allowed: row slice launch failed"), drain();
-      d.cand = dst;
-      d.cand_words = L.words;
-      d.cand_wp = L.wp;
-      d.cand_wr = L.wr;
-      d.cand_wsu = L.wsu;
-      d.cand_wpu = L.wpu;
-      d.cand_wv = L.wv;
-      d.role_rows_bits = role_w ? dst + rows_w : nullptr;
-    }
+    if (upload_shard_batch(t, T, b, &d)) return drain();
     if (T->hws.out.reserve(n * sizeof(Decision)) || T->hws.keys.reserve(n * sizeof(uint64_t) * (k == 0 ? 2 : 1)))
       return drain();
     if (is_allowed_launch(T, T->hws, &d, (acs_decision*)T->hws.out.p, T->stream)) return drain();
@@ -2201,9 +2507,9 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
 
 int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, uint32_t* obl, uint32_t* obl_n,
                         acs_decision* out) {
-  if (refuse_sharded(t, "acs_what_is_allowed")) return -1;
   if (!t || !b || (b->n && (!bits || !obl || !obl_n || !out))) return fail("acs_what_is_allowed: null argument");
   if (b->n == 0) return 0;
+  if (t->sharded) return sharded_what_is_allowed(t, b, bits, obl, obl_n, out);
   if (split_across_devices(t, b)) {
     std::vector<uint32_t> arena_end(b->n);
     if (acs_internal_check_batch2(b, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
@@ -2239,13 +2545,14 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
 
 int acs_what_is_allowed_obl(acs_tables* t, const acs_req_batch* b, const uint32_t* idx, size_t m, uint32_t chunks,
                             uint32_t cap, uint32_t* obl, uint32_t* obl_n) {
-  if (refuse_sharded(t, "acs_what_is_allowed_obl")) return -1;
   if (!t || !b || (m && (!idx || !obl || !obl_n))) return fail("acs_what_is_allowed_obl: null argument");
   if (cap == 0 || cap > OBL_CAP_LIMIT) return fail("acs_what_is_allowed_obl: cap must be in [1, 2^20]");
   if (chunks == 0 || chunks > 64) return fail("acs_what_is_allowed_obl: chunks must be in [1, 64]");
   if (m == 0) return 0;
+  if (m > 0xFFFFFFFFull || m * chunks > 0xFFFFFFFFull) return fail("acs_what_is_allowed_obl: too many requests");
   for (size_t k = 0; k < m; ++k)
     if (idx[k] >= b->n) return fail("acs_what_is_allowed_obl: request index outside the batch");
+  if (t->sharded) return sharded_what_is_allowed_obl(t, b, idx, m, chunks, cap, obl, obl_n);
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));

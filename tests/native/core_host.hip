@@ -128,9 +128,27 @@ extern "C" int acs_host_what_is_allowed(const void* blob, size_t n, const acs_re
 // Obligation-only pass (acs_what_is_allowed_obl's CPU twin): requests idx[0..m) with the
 // policy sets cut into `chunks` ranges, a cap-entry log per (range, request) and no bitset;
 // obl_n[c][j] = total pushes of range c of request j.
+// g_sets / set_base: the ranges cut the whole store's sets, this image holding [set_base, + its
+// n_sets) of them (a shard of a rule-sharded handle); the plain form passes n_sets / 0.
+extern "C" int acs_host_what_is_allowed_obl_shard(const void* blob, size_t n, const acs_req_batch* b,
+                                                  const uint32_t* idx, size_t m, uint32_t chunks, uint32_t cap,
+                                                  uint32_t* obl, uint32_t* obl_n, uint32_t g_sets, uint32_t set_base);
+
 extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const acs_req_batch* b, const uint32_t* idx,
                                             size_t m, uint32_t chunks, uint32_t cap, uint32_t* obl,
                                             uint32_t* obl_n) {
+  acs_blob_header h;
+  std::memcpy(&h, blob, sizeof h);
+  return acs_host_what_is_allowed_obl_shard(blob, n, b, idx, m, chunks, cap, obl, obl_n, h.n_sets, 0);
+}
+
+static uint32_t clip_local(uint32_t g, uint32_t base, uint32_t n) {
+  return g <= base ? 0u : (g - base < n ? g - base : n);
+}
+
+extern "C" int acs_host_what_is_allowed_obl_shard(const void* blob, size_t n, const acs_req_batch* b,
+                                                  const uint32_t* idx, size_t m, uint32_t chunks, uint32_t cap,
+                                                  uint32_t* obl, uint32_t* obl_n, uint32_t g_sets, uint32_t set_base) {
   Tables T;
   if (!host_tables(blob, n, &T)) return -1;
   Batch B = host_batch(b);
@@ -143,8 +161,8 @@ extern "C" int acs_host_what_is_allowed_obl(const void* blob, size_t n, const ac
       OblLog log{obl + k * 2 * (size_t)cap, 0, false, cap, 0};
       uint32_t total = 0;
       if (!(h.flags & RQ_HOST)) {
-        const uint32_t s0 = (uint32_t)((uint64_t)T.n_sets * c / chunks);
-        const uint32_t s1 = (uint32_t)((uint64_t)T.n_sets * (c + 1) / chunks);
+        const uint32_t s0 = clip_local((uint32_t)((uint64_t)g_sets * c / chunks), set_base, T.n_sets);
+        const uint32_t s1 = clip_local((uint32_t)((uint64_t)g_sets * (c + 1) / chunks), set_base, T.n_sets);
         NullSink none;
         const Decision d =
             what_is_allowed_t(ReqMem(T, B, i, h, req_line(B, i)), request_filter(B, h, i), BitsLayout{}, none, log, s0,
