@@ -319,6 +319,15 @@ struct Filter {
   ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {
     return (vword(sec, i >> 5, conj) >> (i & 31)) & 1u;
   }
+  // word w of THIS lane's own row (class | second class, & role rows): the nodes its target
+  // filter keeps (a node outside it is inert for the lane)
+  ACS_FN uint32_t own_word(uint32_t w) const {
+    if (all) return ~0u;
+    uint32_t x = row[w];
+    if (row2) x |= row2[w];
+    if (rrow) x &= role_word(rrow, rrow2, w);
+    return x;
+  }
   ACS_FN uint32_t word(uint32_t w) const {
     if (all) return ~0u;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -341,6 +350,7 @@ struct Filter {
 struct FilterAll {
   uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
+  ACS_FN uint32_t own_word(uint32_t) const { return ~0u; }
   ACS_FN bool verdict(uint32_t, uint32_t, bool = false) const { return false; }  // no class rows
   ACS_FN uint32_t vword(uint32_t, uint32_t, bool = false) const { return 0u; }
 };
@@ -359,6 +369,10 @@ struct FilterLds {
   const uint32_t* own;
   const uint32_t* own2;
   bool single;
+  bool ownc;  // own (| own2) is the lane's whole filter row (no role factor rows to AND)
+  // word w of THIS lane's own row (a node outside it is inert for the lane); all ones when the
+  // lane's row is not at hand
+  ACS_FN uint32_t own_word(uint32_t w) const { return ownc ? own[w] | (own2 ? own2[w] : 0u) : ~0u; }
   ACS_FN uint32_t word(uint32_t w) const {
     ACS_OPC(OP_WORD);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -477,6 +491,10 @@ struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
   uint32_t cap = OBL_MAX;
   uint32_t total = 0;  // every push, written or not (sizes the overflow pass)
 };
+
+#ifndef ACS_OWN_SKIP
+#define ACS_OWN_SKIP 1  // lanes leave the rules outside their own rows (eval_set, what_is_allowed_t)
+#endif
 
 // ------------------------------------------------------------------ request views
 // Context arena + headers shared by both request views.
@@ -1155,6 +1173,9 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     ACS_OPC(OP_RULE_LOOP);
     CandRange rules(F, F.wr, P.child_begin, P.child_end);
     uint32_t r;
+#if ACS_OWN_SKIP
+    uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // the lane's own rule-section word last read
+#endif
     while (rules.next(r)) {
       ACS_OPC(OP_RULE_ITER);
       const NodeRec Q = rule_at(T, r);
@@ -1166,6 +1187,19 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
         const bool vt = F.verdict(4 * WP, r);
+#if ACS_OWN_SKIP
+        // the wave walks the union of its lanes' rows: a rule outside this lane's own row cannot
+        // match its target (the filter keeps every node whose target can pass), so the lane
+        // leaves it without target matching — a wave whose lanes all know the rule or do not
+        // hold it skips the match altogether
+        if (!vt) {
+          if ((r >> 5) != own_w) {
+            own_w = r >> 5;
+            own_bits = F.own_word(F.wr + own_w);
+          }
+          if (!((own_bits >> (r & 31u)) & 1u)) continue;
+        }
+#endif
 #if defined(ACS_OP_COUNT)
         if (!vt) ACS_OPC(OP_RULE_TM);
 #endif
@@ -1491,16 +1525,21 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         uint32_t m = F.word(F.wr + w);
         if (base < rb) m &= ~0u << (rb & 31u);
         if (re - base < 32u) m &= (1u << (re - base)) - 1u;
-        const uint32_t known = m & F.vword(4 * WP, w);  // this lane's
+#if ACS_OWN_SKIP
+        const uint32_t mine = m & F.own_word(F.wr + w);  // this lane's own candidates (the rest is inert for it)
+#else
+        const uint32_t mine = m;
+#endif
+        const uint32_t known = mine & F.vword(4 * WP, w);  // this lane's
         if (known) {
           bits.template set<2>(BL.wr + w, known);
           any_rule = true;
         }
-        uint32_t rest = wave_or(m & ~known);
+        uint32_t rest = wave_or(mine & ~known);
         while (rest) {
           const uint32_t r = wave_uniform(base + (uint32_t)__builtin_ctz(rest));
           rest &= rest - 1u;
-          if ((known >> (r & 31u)) & 1u) continue;  // included above
+          if (!((mine >> (r & 31u)) & 1u) || ((known >> (r & 31u)) & 1u)) continue;  // inert for it / included above
           const NodeRec Q = rule_at(T, r);
           if (Q.nflags & NF_NULL) continue;
           tri mt = 1;

@@ -461,7 +461,7 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
 __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t cls, uint32_t rk, uint32_t c2,
                                             uint32_t* lds) {
   FilterLds F{lds, B.cand_wp, B.cand_wr, B.cand_wsu, B.cand_wpu ? B.cand_wpu : B.cand_wp, B.cand_wv, nullptr, nullptr,
-              false};
+              false, false};
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   const uint32_t *r1, *r2;
   role_rows_of(B, rk, &r1, &r2);
@@ -502,6 +502,7 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
   const bool c2ok = c2 == 0u || c2 - 1u < B.cand_rows;
   F.own = valid && cls < B.cand_rows && c2ok && !B.no_verdicts ? B.cand + (size_t)cls * W : nullptr;
   F.own2 = F.own && c2 ? B.cand + (size_t)(c2 - 1u) * W : nullptr;
+  F.ownc = F.own != nullptr && B.role_key == nullptr;
   return F;
 }
 
@@ -543,8 +544,8 @@ __device__ inline uint32_t request_pcol(const ReqHdr& h) {
 }
 
 #if defined(ACS_WAVE_TIMES)
-// Diagnostic build only: per-wave first-start / last-end wall clock of K2 and the class of the
-// wave's first lane (tools/wave_times.py).  Every lane folds its own times in (vector atomics).
+// Diagnostic build only: per-wave first-start / last-end wall clock of K1 / K2 and the smallest
+// class of the wave's lanes (tools/wave_times.py, tools/wave_times_k1.py).  Every lane folds its own times in (vector atomics).
 constexpr uint32_t WT_MAX = 1u << 16;
 __device__ unsigned long long acs_wt0[WT_MAX], acs_wt1[WT_MAX];
 __device__ unsigned int acs_wt_cls[WT_MAX], acs_wt_lanes[WT_MAX];
@@ -591,6 +592,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
+#if defined(ACS_WAVE_TIMES)
+  const uint32_t wt = k >> 6;
+  if (wt < WT_MAX) {
+    atomicMin(&acs_wt0[wt], (unsigned long long)wall_clock64());
+    if (in) {
+      atomicAdd(&acs_wt_lanes[wt], 1u);
+      atomicMin(&acs_wt_cls[wt], request_pcol(h));
+    }
+  }
+#endif
   const FL F = FilterMaker<FL>::make(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                      lane_cls2(ln, in), wave_lds_row(B));
 #if defined(ACS_PHASE_PROF)
@@ -613,6 +624,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_
   }
 #if !defined(ACS_PHASE_PROF)
   out[i] = d;
+#if defined(ACS_WAVE_TIMES)
+  if (wt < WT_MAX) atomicMax(&acs_wt1[wt], (unsigned long long)wall_clock64());
+#endif
 #else
   if (in) out[i] = d;
   for (int k = 0; k < PH_N; ++k) {  // lane-cycles per phase, one atomic per wave

@@ -1,6 +1,6 @@
 """CPU timing of the native request codec (acs_codec_encode) on synthetic JSON requests.
 
-usage: python tools/codec_prof.py [c3|c2] [requests] [threads] [reps]
+usage: python tools/codec_prof.py [c3|c2] [requests] [threads] [reps] [second_role]
 Prints per-rep seconds of parse+encode / regex / classes / total and requests/s.
 """
 import os
@@ -21,9 +21,10 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 200_000
     threads = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    second = float(sys.argv[5]) if len(sys.argv) > 5 else 0.5
     doc = synth.c2_store() if kind == "c2" else synth.c3_store()
     cs = compiler.compile_store(store.populate(doc), SERVICE_URNS, COMBINING_ALGORITHMS)
-    sb = synth.requests(cs, n, kind, seed=0xACC1000)
+    sb = synth.requests(cs, n, kind, seed=0xACC1000, second_role=second if kind != "c2" else 0.0)
     idx = np.arange(n)
     t0 = time.perf_counter()
     text = sb.json_text(idx)
