@@ -29,6 +29,27 @@ namespace acs {
 
 #define ACS_FN __host__ __device__ inline
 
+// A/B switches.  ACS_VERDICT_ROLES (on): a composed lane reads its second class row's verdict
+// only for targets that test role associations (same-call A/B, r05_c: c3 K1 3.29 -> 3.17 ms, c4
+// K2 8.27 -> 7.96 ms).  ACS_OWN_SKIP (bits; off): lanes skip the rules (1), loop-2b policies (2),
+// sets (4) outside their own filter rows — fewer rule target matches per wave (c3: 2.52 -> 0.98,
+// r05_b op counts) but slower on every config (c3 3.17 -> 3.35 ms, c3r1 1.86 -> 2.09: the per-lane
+// row loads and their registers, r05_c).  ACS_CLEAN_BITS (off): clean sets below the deciding set
+// skipped from the event index's bits without loading their records (c3adv unchanged 1.83 ->
+// 1.85, c3 3.16 -> 3.29 ms: registers, r05_c).
+#ifndef ACS_OWN_SKIP
+#define ACS_OWN_SKIP 0
+#endif
+#ifndef ACS_VERDICT_ROLES
+#define ACS_VERDICT_ROLES 1
+#endif
+#ifndef ACS_CLEAN_BITS
+#define ACS_CLEAN_BITS 0
+#endif
+#ifndef ACS_WIA_TEMPLATES
+#define ACS_WIA_TEMPLATES 1  // whatIsAllowed from class templates (what_is_allowed_tpl)
+#endif
+
 // Value every active lane of the wave holds identically (a table index or bitset word of
 // the wave-shared candidate iteration): move it to an SGPR so the node records behind it
 // are fetched with scalar loads.  Identity in the host build of the core.
@@ -91,7 +112,20 @@ struct Tables {
   uint32_t id_user;  // interned urns.user
   uint32_t rstride;  // NodeRec slots per rule record: 1 (blob layout), 2 (device rule lines, acs_compile)
   const uint32_t* ev_index;  // event index (build_event_index; nullptr: K1 never skips a set for it)
+  const uint32_t* parents;   // [P] set of each policy, then [R] policy of each rule (build_parents;
+                             // nullptr: no whatIsAllowed templates)
 };
+
+// The parent of every policy (its set) and rule (its policy): parent_index_words(P, R) words.
+inline size_t parent_index_words(uint32_t n_pols, uint32_t n_rules) { return (size_t)n_pols + n_rules; }
+inline void build_parents(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols, uint32_t n_rules,
+                          uint32_t* out) {
+  for (size_t k = 0; k < parent_index_words(n_pols, n_rules); ++k) out[k] = 0;
+  for (uint32_t s = 0; s < n_sets; ++s)
+    for (uint32_t p = sets[s].child_begin; p < sets[s].child_end && p < n_pols; ++p) out[p] = s;
+  for (uint32_t p = 0; p < n_pols; ++p)
+    for (uint32_t r = pols[p].child_begin; r < pols[p].child_end && r < n_rules; ++r) out[n_pols + r] = p;
+}
 
 // K1's event index (is_allowed_body's events-only skip): per set its rules' range [r0, r1) and,
 // in bit 31 of the r1 word, whether it holds a null policy or a policy with an invalid combining
@@ -99,8 +133,13 @@ struct Tables {
 // ACL-gated (below); then one bit per rule carrying a condition; then one bit
 // per policy whose every non-null rule has a target and does not skip ACLs (ACL-gated: for an
 // ACL_NONE request none of its rules can push).
+// Last, one bit per set that is clean (NF_CLEAN): below the deciding set the walk skips those
+// without loading their records.
 // event_index_words(n_sets, n_pols, n_rules) u32 words, built on the host from the blob's records.
 inline size_t event_index_words(uint32_t n_sets, uint32_t n_pols, uint32_t n_rules) {
+  return 2 * (size_t)n_sets + ((size_t)n_rules + 31) / 32 + ((size_t)n_pols + 31) / 32 + ((size_t)n_sets + 31) / 32;
+}
+ACS_FN size_t event_index_clean_off(uint32_t n_sets, uint32_t n_pols, uint32_t n_rules) {
   return 2 * (size_t)n_sets + ((size_t)n_rules + 31) / 32 + ((size_t)n_pols + 31) / 32;
 }
 inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols,
@@ -142,6 +181,10 @@ inline void build_event_index(const NodeRec* sets, uint32_t n_sets, const NodeRe
       inert = !(pols[p].nflags & NF_NULL) && pols[p].map_size != 0 && ((gb[p >> 5] >> (p & 31)) & 1u);
     if (inert) out[2 * s + 1] |= 0x40000000u;
   }
+  uint32_t* clean = out + event_index_clean_off(n_sets, n_pols, n_rules);
+  for (uint32_t w = 0; w < (n_sets + 31) / 32; ++w) clean[w] = 0;
+  for (uint32_t s = 0; s < n_sets; ++s)
+    if (sets[s].nflags & NF_CLEAN) clean[s >> 5] |= 1u << (s & 31);
 }
 
 // Set s cannot push for an ACL_NONE request: every policy of it has rules and is ACL-gated.
@@ -312,12 +355,15 @@ struct Filter {
   bool vok;                // the verdicts apply: the rows are this request's own class rows
   bool all;                // no filtering
   // word w of the verdict section at word `sec` past wv (0 when the verdicts do not apply);
-  // conj: a known-false section (AND over the request's rows)
-  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
-    return vok ? compose_verdict(row[wv + sec + w], row2, wv + sec + w, conj) : 0u;
+  // conj: a known-false section (AND over the request's rows); roles: the node's target tests
+  // role associations (TF_SUBJ_ROLE) — else both class rows of a composed request hold the same
+  // verdict (they differ only in the role) and the second is not read
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false, bool roles = true) const {
+    return vok ? compose_verdict(row[wv + sec + w], roles || !ACS_VERDICT_ROLES ? row2 : nullptr, wv + sec + w, conj)
+               : 0u;
   }
-  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {
-    return (vword(sec, i >> 5, conj) >> (i & 31)) & 1u;
+  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false, bool roles = true) const {
+    return (vword(sec, i >> 5, conj, roles) >> (i & 31)) & 1u;
   }
   // word w of THIS lane's own row (class | second class, & role rows): the nodes its target
   // filter keeps (a node outside it is inert for the lane)
@@ -351,8 +397,8 @@ struct FilterAll {
   uint32_t wp, wr, wsu, wpu;
   ACS_FN uint32_t word(uint32_t) const { return ~0u; }
   ACS_FN uint32_t own_word(uint32_t) const { return ~0u; }
-  ACS_FN bool verdict(uint32_t, uint32_t, bool = false) const { return false; }  // no class rows
-  ACS_FN uint32_t vword(uint32_t, uint32_t, bool = false) const { return 0u; }
+  ACS_FN bool verdict(uint32_t, uint32_t, bool = false, bool = true) const { return false; }  // no class rows
+  ACS_FN uint32_t vword(uint32_t, uint32_t, bool = false, bool = true) const { return 0u; }
 };
 
 // FilterLds: rows that fit in LDS — the wave's OR of its (class & role) rows, built by the
@@ -384,16 +430,20 @@ struct FilterLds {
   }
   // word w of the verdict section at `sec` (wave-uniform in a one-class wave, else per lane);
   // conj: a known-false section
-  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false) const {
+  // roles: the node's target tests role associations (TF_SUBJ_ROLE); else a composed lane's two
+  // class rows hold the same verdict (same entity column and action, another role) and the
+  // second row is not read
+  ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false, bool roles = true) const {
+    const uint32_t* o2 = roles || !ACS_VERDICT_ROLES ? own2 : nullptr;
 #if defined(ACS_OP_COUNT)
     ACS_OPC(single ? OP_V_LDS : OP_V_OWN);
-    if (own2) ACS_OPC(OP_V_OWN2);
+    if (o2) ACS_OPC(OP_V_OWN2);
 #endif
-    if (single) return compose_verdict(word(wv + sec + w), own2, wv + sec + w, conj);
-    return own ? compose_verdict(own[wv + sec + w], own2, wv + sec + w, conj) : 0u;
+    if (single) return compose_verdict(word(wv + sec + w), o2, wv + sec + w, conj);
+    return own ? compose_verdict(own[wv + sec + w], o2, wv + sec + w, conj) : 0u;
   }
-  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false) const {
-    return (vword(sec, i >> 5, conj) >> (i & 31)) & 1u;
+  ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false, bool roles = true) const {
+    return (vword(sec, i >> 5, conj, roles) >> (i & 31)) & 1u;
   }
 };
 
@@ -492,9 +542,6 @@ struct OblLog {  // whatIsAllowed maskedProperty pushes, in evaluation order
   uint32_t total = 0;  // every push, written or not (sizes the overflow pass)
 };
 
-#ifndef ACS_OWN_SKIP
-#define ACS_OWN_SKIP 1  // lanes leave the rules outside their own rows (eval_set, what_is_allowed_t)
-#endif
 
 // ------------------------------------------------------------------ request views
 // Context arena + headers shared by both request views.
@@ -1101,7 +1148,8 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) return *ev = make_err(-(tri)ERR_TYPE, s + 1), SET_EVENT;
       if (P.nflags & NF_HAS_TARGET) {
-        const bool vt = F.verdict(0, p), vf = !vt && F.verdict(WP, p, true);
+        const bool rl = (P.tflags & TF_SUBJ_ROLE) != 0;
+        const bool vt = F.verdict(0, p, false, rl), vf = !vt && F.verdict(WP, p, true, rl);
 #if defined(ACS_OP_COUNT)
         if (!vt && !vf) ACS_OPC(OP_P2A_TM);
 #endif
@@ -1128,7 +1176,17 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   const bool cut_p = safe && (S.nflags & NF_COND_FREE);
   CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
   uint32_t p;
+#if ACS_OWN_SKIP & 2
+  uint32_t pw = 0xFFFFFFFFu, pbits = 0;  // the lane's own useful-policy word last read
+#endif
   while (pols.next(p)) {
+#if ACS_OWN_SKIP & 2
+    if ((p >> 5) != pw) {  // a policy outside the lane's own useful row cannot change its record
+      pw = p >> 5;
+      pbits = F.own_word(F.wpu + pw);
+    }
+    if (!((pbits >> (p & 31u)) & 1u)) continue;
+#endif
     ACS_OPC(OP_P2B_ITER);
     const NodeRec P = node_at(T, T.pols, p, T.n_pols);
     if (P.nflags & NF_NULL) continue;
@@ -1144,8 +1202,9 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     if (P.nflags & NF_HAS_TARGET) {
       PROF_T0(tp);
       // the class's verdict for this lane's mode
-      const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
-      const bool kf = exact ? F.verdict(WP, p, true) : F.verdict(3 * WP, p, true);
+      const bool rl = (P.tflags & TF_SUBJ_ROLE) != 0;
+      const bool kt = exact ? F.verdict(0, p, false, rl) : F.verdict(2 * WP, p, false, rl);
+      const bool kf = exact ? F.verdict(WP, p, true, rl) : F.verdict(3 * WP, p, true, rl);
 #if defined(ACS_OP_COUNT)
       if (!kt && !kf) ACS_OPC(OP_P2B_TM);
 #endif
@@ -1173,7 +1232,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     ACS_OPC(OP_RULE_LOOP);
     CandRange rules(F, F.wr, P.child_begin, P.child_end);
     uint32_t r;
-#if ACS_OWN_SKIP
+#if ACS_OWN_SKIP & 1
     uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // the lane's own rule-section word last read
 #endif
     while (rules.next(r)) {
@@ -1186,8 +1245,8 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       tri m = 1;
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
-        const bool vt = F.verdict(4 * WP, r);
-#if ACS_OWN_SKIP
+        const bool vt = F.verdict(4 * WP, r, false, (Q.tflags & TF_SUBJ_ROLE) != 0);
+#if ACS_OWN_SKIP & 1
         // the wave walks the union of its lanes' rows: a rule outside this lane's own row cannot
         // match its target (the filter keeps every node whose target can pass), so the lane
         // leaves it without target matching — a wave whose lanes all know the rule or do not
@@ -1298,7 +1357,41 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   bool have_ev = false;
   CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
+#if ACS_OWN_SKIP & 4
+  uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // the lane's own useful-set word last read
+#endif
+#if ACS_CLEAN_BITS
+  uint32_t clean_w = 0xFFFFFFFFu, clean_bits = 0;  // the event index's clean-set word last read
+  const uint32_t* clean_sec =
+      ACS_CLEAN_BITS && T.ev_index ? T.ev_index + event_index_clean_off(T.n_sets, T.n_pols, T.n_rules) : nullptr;
+#endif
   while (sets.next(s)) {
+#if ACS_CLEAN_BITS
+    // below the deciding set (or an event) only an event can change the record, and a clean set
+    // cannot raise one for a safe request: skip it — from the event index's clean bits, without
+    // loading its record (the unclean ones below are walked)
+    if ((have_ev || last_set) && safe && clean_sec) {
+      if ((s >> 5) != clean_w) {
+        clean_w = s >> 5;
+        ACS_SCAN(4);
+        clean_bits = clean_sec[wave_uniform(clean_w)];
+      }
+      if ((clean_bits >> (s & 31u)) & 1u) {
+        ACS_OPC(OP_SET_SKIP);
+        continue;
+      }
+    }
+#endif
+#if ACS_OWN_SKIP & 4
+    // the wave walks the union of its lanes' useful sets; a set outside this lane's own useful
+    // row cannot change its record (candidates.py: useful sections), so the lane leaves it —
+    // and the wave, once no active lane holds it
+    if ((s >> 5) != own_w) {
+      own_w = s >> 5;
+      own_bits = F.own_word(F.wsu + own_w);
+    }
+    if (!((own_bits >> (s & 31u)) & 1u)) continue;
+#endif
     ACS_OPC(OP_SET_ITER);
     const NodeRec S = node_at(T, T.sets, s, T.n_sets);
     // below the deciding set (or an event) only an event can change the record, and a clean
@@ -1486,7 +1579,10 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         if (P.nflags & NF_NULL) return make_err(-(tri)ERR_TYPE, s + 1);
         if (P.nflags & NF_HAS_TARGET) {
           // a verdict-known target has no property attribute, so it pushes no obligation
-          const tri m = F.verdict(0, p) ? 1 : F.verdict(WP, p, true) ? 0 : target_match(P, R, P.pe_at, false, true, &obl);
+          const bool rl = (P.tflags & TF_SUBJ_ROLE) != 0;
+          const tri m = F.verdict(0, p, false, rl)     ? 1
+                        : F.verdict(WP, p, true, rl) ? 0
+                                                     : target_match(P, R, P.pe_at, false, true, &obl);
           if (m < 0) return make_err(m, s + 1);
           if (m) {
             exact = true;
@@ -1508,8 +1604,9 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
       const NodeRec P = node_at(T, T.pols, p, T.n_pols);
       if (P.nflags & NF_NULL) continue;
       if (P.nflags & NF_HAS_TARGET) {
-        const bool kt = exact ? F.verdict(0, p) : F.verdict(2 * WP, p);
-        const bool kf = exact ? F.verdict(WP, p, true) : F.verdict(3 * WP, p, true);
+        const bool rl = (P.tflags & TF_SUBJ_ROLE) != 0;
+        const bool kt = exact ? F.verdict(0, p, false, rl) : F.verdict(2 * WP, p, false, rl);
+        const bool kf = exact ? F.verdict(WP, p, true, rl) : F.verdict(3 * WP, p, true, rl);
         const tri m = kt ? 1 : kf ? 0 : target_match(P, R, pe, !exact, true, &obl);
         if (m < 0) return make_err(m, s + 1);
         if (!m) continue;
@@ -1525,7 +1622,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         uint32_t m = F.word(F.wr + w);
         if (base < rb) m &= ~0u << (rb & 31u);
         if (re - base < 32u) m &= (1u << (re - base)) - 1u;
-#if ACS_OWN_SKIP
+#if ACS_OWN_SKIP & 1
         const uint32_t mine = m & F.own_word(F.wr + w);  // this lane's own candidates (the rest is inert for it)
 #else
         const uint32_t mine = m;
@@ -1562,6 +1659,204 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
   }
   if (obl.overflow) out.flags |= OF_OBL_OVERFLOW;
   return out;
+}
+
+// ------------------------------------------------------------------ whatIsAllowed templates
+// Most of a whatIsAllowed walk (accessController.ts:343-419) is decided by a request's class row
+// alone: which candidate sets are reached (sets without a target), loop 2a's `exact` (the first
+// candidate policy whose exact target match the class knows to be true, every one before it
+// known false), the loop-2b policy gates in that mode (verdict-known targets), and the rules
+// whose retried match the class knows to be true (targets without properties: no obligation).
+// A class's TEMPLATE records those inclusion bits; its WORK is the candidate rules of reached
+// policies whose match depends on the request (a property attribute: these are the only targets
+// that push maskedProperty obligations).  whatIsAllowed keeps no state across the walk but the
+// push log, so a request whose class has a template is decided by copying the template and
+// evaluating its work rules in index (= walk) order; its log is the same push sequence.  A class
+// is not templated (TPL_OK clear) when some reached node is not verdict-known, a set has a
+// target, or loop 2a meets a null policy (the walk throws there).  A composed request (two class
+// rows, two role associations) is templated when both classes are, neither class's walk reads a
+// target that tests role associations (TPL_ROLE_FREE: the two walks then take the same
+// decisions, and the composed walk is their union), and they agree on `exact` for the sets both
+// hold.  Anything else — no template, a multi-entity request (checkMultipleEntitiesMatch), a
+// work rule that throws — takes the full walk (what_is_allowed_t).
+enum TplFlags : uint32_t { TPL_OK = 1u, TPL_ROLE_FREE = 2u };
+
+// Per-class template record (u32 words): [BitsLayout row | work rule bits (R) | exact sets (S) |
+// work-word mask (a bit per nonzero work word) | flags], each section 4-word aligned.
+struct TplLayout {
+  uint32_t words;   // inclusion row (bits_layout(...).words), at 0
+  uint32_t work;    // offset of the work bits, ceil(R / 32) words
+  uint32_t exact;   // offset of the exact-set bits, ceil(S / 32) words
+  uint32_t mask;    // offset of the work-word mask, ceil(work words / 32) words
+  uint32_t flags;   // offset of the flags word
+  uint32_t stride;  // record length (multiple of 4)
+};
+ACS_FN TplLayout tpl_layout(uint32_t n_sets, uint32_t n_pols, uint32_t n_rules) {
+  TplLayout L;
+  L.words = bits_layout(n_sets, n_pols, n_rules).words;
+  const uint32_t ww = (n_rules + 31u) / 32u;
+  L.work = L.words;
+  L.exact = L.work + up4(ww);
+  L.mask = L.exact + up4((n_sets + 31u) / 32u);
+  L.flags = L.mask + up4((ww + 31u) / 32u);
+  L.stride = L.flags + 4u;
+  return L;
+}
+
+ACS_FN bool row_bit(const uint32_t* row, uint32_t off, uint32_t i) { return (row[off + (i >> 5)] >> (i & 31u)) & 1u; }
+
+// The template of candidate set s for class row `row` (batch layout wp / wr / wv): its inclusion
+// bits, work rules and exact decision go through acc (or_bits(word, bits) on the record);
+// *role_free cleared when a target it reads tests role associations.  false: s makes the class
+// untemplated.  Plain (per-lane) loads: the lanes of a template pass walk different sets.
+template <class Acc>
+ACS_FN bool wia_template_set(const Tables& T, const uint32_t* row, uint32_t wp, uint32_t wr, uint32_t wv,
+                             const BitsLayout& BL, const TplLayout& TL, uint32_t s, Acc& acc, bool* role_free) {
+  const uint32_t WP = (T.n_pols + 31) >> 5;
+  const NodeRec S = T.sets[s];
+  if (S.nflags & NF_HAS_TARGET) return false;
+  bool exact = false;
+  for (uint32_t p = S.child_begin; p < S.child_end; ++p) {  // loop 2a
+    if (!row_bit(row, wp, p)) continue;
+    const NodeRec P = T.pols[p];
+    if (P.nflags & NF_NULL) return false;
+    if (!(P.nflags & NF_HAS_TARGET)) continue;
+    if (P.tflags & TF_SUBJ_ROLE) *role_free = false;
+    if (row_bit(row, wv, p)) {
+      exact = true;
+      break;
+    }
+    if (!row_bit(row, wv + WP, p)) return false;
+  }
+  if (exact) acc.or_bits(TL.exact + (s >> 5), 1u << (s & 31u));
+  bool any_pol = false;
+  for (uint32_t p = S.child_begin; p < S.child_end; ++p) {  // loop 2b
+    if (!row_bit(row, wp, p)) continue;
+    const NodeRec P = T.pols[p];
+    if (P.nflags & NF_NULL) continue;
+    if (P.nflags & NF_HAS_TARGET) {
+      if (P.tflags & TF_SUBJ_ROLE) *role_free = false;
+      if (!row_bit(row, wv + (exact ? 0u : 2u * WP), p)) {
+        if (row_bit(row, wv + (exact ? WP : 3u * WP), p)) continue;
+        return false;
+      }
+    }
+    bool any_rule = false;
+    for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
+      if (!row_bit(row, wr, r)) continue;
+      const NodeRec Q = T.rules[(size_t)r * T.rstride];
+      if (Q.nflags & NF_NULL) continue;
+      if (!(Q.nflags & NF_HAS_TARGET) || row_bit(row, wv + 4u * WP, r)) {
+        acc.or_bits(BL.wr + (r >> 5), 1u << (r & 31u));
+        any_rule = true;
+      } else {
+        acc.or_bits(TL.work + (r >> 5), 1u << (r & 31u));
+      }
+    }
+    if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
+      acc.or_bits(BL.wp + (p >> 5), 1u << (p & 31u));
+      any_pol = true;
+    }
+  }
+  if (any_pol) acc.or_bits(s >> 5, 1u << (s & 31u));
+  return true;
+}
+
+// Sink for a templated request: every 16-B chunk of the row is written once, as the template(s)
+// OR the bits the work rules add (ChunkSink's order rule: each section's bits arrive with
+// non-decreasing word index).
+struct TplSink {
+  uint32_t* row;
+  const uint32_t* t1;  // template rows (t2: the second class's, or nullptr)
+  const uint32_t* t2;
+  uint32_t cur[3], lim[3];
+  uint32_t buf[3][4];
+  ACS_FN TplSink(uint32_t* r, const BitsLayout& L, const uint32_t* a, const uint32_t* b) : row(r), t1(a), t2(b) {
+    cur[0] = 0; lim[0] = L.wp >> 2;
+    cur[1] = L.wp >> 2; lim[1] = L.wr >> 2;
+    cur[2] = L.wr >> 2; lim[2] = L.words >> 2;
+    for (int k = 0; k < 3; ++k)
+      for (int q = 0; q < 4; ++q) buf[k][q] = 0u;
+  }
+  ACS_FN void put(uint32_t c, const uint32_t* extra) {
+    ACS_SCAN(t2 ? 32 : 16);  // the template chunk(s), shared by the class's lanes
+    uint32_t v[4];
+    for (int q = 0; q < 4; ++q) v[q] = t1[4 * c + q] | (t2 ? t2[4 * c + q] : 0u) | (extra ? extra[q] : 0u);
+#if defined(__HIP_DEVICE_COMPILE__)
+    reinterpret_cast<uint4*>(row)[c] = make_uint4(v[0], v[1], v[2], v[3]);
+#else
+    for (int q = 0; q < 4; ++q) row[4 * c + q] = v[q];
+#endif
+  }
+  template <int S> ACS_FN void flush(uint32_t upto) {
+    put(cur[S], buf[S]);
+    for (uint32_t c = cur[S] + 1; c < upto; ++c) put(c, nullptr);
+    cur[S] = upto;
+    for (int q = 0; q < 4; ++q) buf[S][q] = 0u;
+  }
+  template <int S> ACS_FN void set(uint32_t w, uint32_t bit) {
+    const uint32_t c = w >> 2;
+    if (c != cur[S]) flush<S>(c);
+    buf[S][w & 3u] |= bit;
+  }
+  ACS_FN void finish() {
+    if (cur[0] < lim[0]) flush<0>(lim[0]);
+    if (cur[1] < lim[1]) flush<1>(lim[1]);
+    if (cur[2] < lim[2]) flush<2>(lim[2]);
+  }
+};
+
+// Whether request R (class rows c1, c2: template records t1 / t2, nullptr for none) is decided
+// from templates: both templated, composition exact (see above), not a multi-entity request.
+ACS_FN bool tpl_usable(const TplLayout& TL, const uint32_t* t1, const uint32_t* t2, const uint32_t* row1,
+                       const uint32_t* row2, uint32_t n_sets, uint32_t req_flags) {
+  if (!t1 || !(t1[TL.flags] & TPL_OK) || (req_flags & (RQ_MULTI_ENT | RQ_HOST | RQ_NO_TARGET))) return false;
+  if (!row2) return true;
+  if (!t2 || !(t2[TL.flags] & TPL_OK) || !(t1[TL.flags] & t2[TL.flags] & TPL_ROLE_FREE)) return false;
+  for (uint32_t w = 0; w < (n_sets + 31u) / 32u; ++w)
+    if ((t1[TL.exact + w] ^ t2[TL.exact + w]) & row1[w] & row2[w]) return false;
+  return true;
+}
+
+// A templated request: the template row(s) plus its work rules (t1 / t2's work bits, less the
+// rules the other class's template already includes — known true there, so the full walk would
+// not match them either), evaluated in index order with the pushes they make.  Work words are
+// visited wave-uniformly (the union of the active lanes' work-word masks), a word's rules for the
+// lanes that hold them.  Returns false when a work rule throws: the caller re-runs the request
+// with the full walk (the row is then rewritten from scratch).
+template <class RQ>
+ACS_FN bool what_is_allowed_tpl(const RQ& R, const TplLayout& TL, const BitsLayout& BL, const uint32_t* t1,
+                                const uint32_t* t2, TplSink& sink, OblLog& obl) {
+  const Tables& T = R.T;
+  const uint32_t MW = (TL.flags - TL.mask);  // mask words (padded)
+  for (uint32_t k = 0; k < MW; ++k) {
+    ACS_SCAN(t2 ? 8 : 4);
+    uint32_t u = wave_or(t1[TL.mask + k] | (t2 ? t2[TL.mask + k] : 0u));
+    while (u) {
+      const uint32_t w = wave_uniform(32u * k + (uint32_t)__builtin_ctz(u));
+      u &= u - 1u;
+      ACS_SCAN(t2 ? 16 : 4);
+      uint32_t mine = t1[TL.work + w] & ~(t2 ? t2[BL.wr + w] : 0u);
+      if (t2) mine |= t2[TL.work + w] & ~t1[BL.wr + w];
+      uint32_t rest = wave_or(mine);
+      while (rest) {
+        const uint32_t r = wave_uniform(32u * w + (uint32_t)__builtin_ctz(rest));
+        rest &= rest - 1u;
+        if (!((mine >> (r & 31u)) & 1u)) continue;
+        const NodeRec Q = rule_at(T, r);
+        const tri m = target_match_retry(Q, R, Q.effect, true, &obl);
+        if (m < 0) return false;
+        if (m) {
+          const uint32_t p = T.parents[r + T.n_pols], s = T.parents[p];
+          sink.template set<0>(s >> 5, 1u << (s & 31u));
+          sink.template set<1>(BL.wp + (p >> 5), 1u << (p & 31u));
+          sink.template set<2>(BL.wr + w, 1u << (r & 31u));
+        }
+      }
+    }
+  }
+  sink.finish();
+  return true;
 }
 
 // Host build: row = this request's zeroed BitsLayout row.

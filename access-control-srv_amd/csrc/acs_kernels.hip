@@ -637,6 +637,47 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_
 #endif
 }
 
+// whatIsAllowed templates (acs_eval.h wia_template_set): one wave per class row of the batch; its
+// lanes take the row's candidate sets in turn (sets are independent in whatIsAllowed), OR their
+// bits into the wave's record in LDS, and the wave writes the record.  A set that makes the class
+// untemplated clears the record's flags (the class's requests take the full walk).
+struct LdsAcc {
+  uint32_t* rec;
+  __device__ void or_bits(uint32_t w, uint32_t bit) { atomicOr(rec + w, bit); }
+};
+__global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, TplLayout TL, BitsLayout BL,
+                                                             uint32_t* __restrict__ out) {
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t c = blockIdx.x * (BLOCK / 64) + wave;
+  uint32_t* rec = acs_dyn_lds + wave * TL.stride;
+  for (uint32_t w = lane; w < TL.stride; w += 64) rec[w] = 0u;
+  __syncthreads();
+  bool ok = true, role_free = true;
+  if (c < B.cand_rows) {
+    const uint32_t* row = B.cand + (size_t)c * B.cand_words;
+    LdsAcc acc{rec};
+    uint32_t k = 0;  // rank of the candidate set among the row's
+    for (uint32_t w = 0; w < (T.n_sets + 31u) / 32u && ok; ++w)
+      for (uint32_t x = row[w]; x && ok; x &= x - 1u, ++k)
+        if ((k & 63u) == lane)
+          ok = wia_template_set(T, row, B.cand_wp, B.cand_wr, B.cand_wv, BL, TL, 32u * w + (uint32_t)__builtin_ctz(x),
+                                acc, &role_free);
+  }
+  const bool all_ok = __ballot(!ok) == 0, all_free = __ballot(!role_free) == 0;
+  __syncthreads();
+  if (c >= B.cand_rows) return;
+  const uint32_t ww = TL.exact - TL.work;
+  for (uint32_t w = lane; w < ww; w += 64)
+    if (rec[TL.work + w]) atomicOr(rec + TL.mask + (w >> 5), 1u << (w & 31u));
+  __syncthreads();
+  uint32_t* dst = out + (size_t)c * TL.stride;
+  for (uint32_t w = lane; w < TL.stride; w += 64) {
+    uint32_t v = all_ok ? rec[w] : 0u;
+    if (w == TL.flags) v = all_ok ? (TPL_OK | (all_free ? TPL_ROLE_FREE : 0u)) : 0u;
+    dst[w] = v;
+  }
+}
+
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
@@ -648,7 +689,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
                                                                 uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
                                                                 uint32_t* __restrict__ obl_n,
-                                                                Decision* __restrict__ out) {
+                                                                Decision* __restrict__ out,
+                                                                const uint32_t* __restrict__ tpl, TplLayout TL) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
@@ -668,23 +710,51 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     }
   }
 #endif
-  const FL F = FilterMaker<FL>::make(B, in && !host, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
-                                     lane_cls2(ln, in), wave_lds_row(B));
-  if (!in) return;
+  // Every lane stays to the end: the wave filter (the full walk's) is built, with all lanes
+  // present, only when some lane still needs the full walk after the template phase.
   const uint32_t o = i;
-  ChunkSink sink(bits + (size_t)o * BL.words, BL);
-  OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
   Decision d{};
-  if (host) {
+  bool done = !in;
+  if (in && host) {
+    ChunkSink sink(bits + (size_t)o * BL.words, BL);
     d.flags = OF_HOST_REQ;
-  } else {
-    ReqRes* scol = stage + threadIdx.x;
+    sink.finish();
+    obl_n[o] = 0u;
+    done = true;
+  }
+  ReqRes* scol = stage + threadIdx.x;
+  if (!done) {
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
-    d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
   }
-  sink.finish();
-  obl_n[o] = (d.flags & OF_ERR) ? 0u : log.n;
+  if (tpl && !done) {  // the class template(s) plus the work rules (acs_eval.h what_is_allowed_tpl)
+    const uint32_t c1 = request_pcol(h), c2 = lane_cls2(ln, in);
+    const uint32_t* t1 = c1 < B.cand_rows ? tpl + (size_t)c1 * TL.stride : nullptr;
+    const uint32_t* t2 = t1 && c2 && c2 - 1u < B.cand_rows ? tpl + (size_t)(c2 - 1u) * TL.stride : nullptr;
+    const uint32_t* r1 = t1 ? B.cand + (size_t)c1 * B.cand_words : nullptr;
+    const uint32_t* r2 = t2 ? B.cand + (size_t)(c2 - 1u) * B.cand_words : nullptr;
+    if (!(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags)) {
+      TplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
+      OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
+      if (what_is_allowed_tpl(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), TL, BL, t1, t2, sink, log)) {
+        if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
+        obl_n[o] = log.n;
+        done = true;
+      }
+    }
+  }
+  if (__ballot(!done)) {  // the full walk (rewrites a failed template lane's whole row)
+    const FL F = FilterMaker<FL>::make(B, !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
+                                       lane_cls2(ln, in && !done), wave_lds_row(B));
+    if (!done) {
+      ChunkSink sink(bits + (size_t)o * BL.words, BL);
+      OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
+      d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
+      sink.finish();
+      obl_n[o] = (d.flags & OF_ERR) ? 0u : log.n;
+    }
+  }
+  if (!in) return;
   out[o] = d;
 #if defined(ACS_WAVE_TIMES)
   if (wt < WT_MAX) atomicMax(&acs_wt1[wt], (unsigned long long)wall_clock64());
@@ -978,7 +1048,9 @@ struct DevBuf {
 struct Workspace {
   DevBuf sort, img, out;
   DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
+  DevBuf tpl;          // whatIsAllowed templates of the batch's class rows
   void release() {
+    tpl.release();
     sort.release();
     img.release();
     out.release();
@@ -1237,9 +1309,13 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
     for (int k = 0; k < 6; ++k) doff[k] = off[k];
   }
   // the event index (acs_eval.h build_event_index) after the image, from the blob's records
-  std::vector<uint32_t> evx(event_index_words(h.n_sets, h.n_pols, h.n_rules));
+  // and the parent index (acs_eval.h build_parents: whatIsAllowed templates) after it
+  const size_t ev_words = event_index_words(h.n_sets, h.n_pols, h.n_rules);
+  std::vector<uint32_t> evx(ev_words + parent_index_words(h.n_pols, h.n_rules));
   build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
                     (const NodeRec*)(bsrc + off[2]), h.n_rules, evx.data());
+  build_parents((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols, h.n_rules,
+                evx.data() + ev_words);
   const size_t ev_off = align16(up_bytes);
   auto* t = new acs_tables();
   t->device = device;
@@ -1272,6 +1348,7 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   // the index packs a set's rule end in 30 bits (flags in bits 30 / 31): a store of 2^30 rules or
   // more runs without it (no set is skipped for it; the decisions are the same)
   t->view.ev_index = h.n_rules < (1u << 30) ? (const uint32_t*)(base + ev_off) : nullptr;
+  t->view.parents = (const uint32_t*)(base + ev_off) + ev_words;
   t->image_bytes = img_total;
   return t;
 }
@@ -1326,6 +1403,7 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
     r->view.pairs = (const Pair*)rebase(t->view.pairs);
     r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
     r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
+    r->view.parents = (const uint32_t*)rebase(t->view.parents);
     r->sort = t->sort;
     t->peers.push_back(r);
   }
@@ -1753,10 +1831,21 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
+  const TplLayout TL = tpl_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
+  // templates: batches whose class rows carry verdicts in the LDS form, without a role factor
+  const bool use_tpl = ACS_WIA_TEMPLATES && filter_form(B) == FilterForm::Lds && !B.role_key && B.cand_rows &&
+                       t->view.parents && (size_t)(BLOCK / 64) * TL.stride * 4 <= 64 * 1024;
   const int slot = (int)(t->launches % acs_tables::RING);
-  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
+  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));  // the template pass is part of the timed K2
+  const uint32_t* tpl = nullptr;
+  if (use_tpl) {
+    if (W.tpl.reserve((size_t)B.cand_rows * TL.stride * sizeof(uint32_t))) return -1;
+    tpl = (const uint32_t*)W.tpl.p;
+    hipLaunchKernelGGL(wia_template_kernel, dim3((B.cand_rows + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK),
+                       (size_t)(BLOCK / 64) * TL.stride * 4, s, t->view, B, TL, BL, (uint32_t*)W.tpl.p);
+  }
   ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, BL, bits,
-                      obl, obl_n, (Decision*)out);
+                      obl, obl_n, (Decision*)out, tpl, TL);
   HIP_OK(hipGetLastError());
   if (t->timing) {
     HIP_OK(hipEventRecord(t->tev[2 * slot + 1], s));

@@ -43,6 +43,10 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   evx.assign(event_index_words(h.n_sets, h.n_pols, h.n_rules), 0u);
   build_event_index(T->sets, h.n_sets, T->pols, h.n_pols, T->rules, h.n_rules, evx.data());
   T->ev_index = getenv("ACS_HOST_NO_EV_INDEX") ? nullptr : evx.data();
+  static thread_local std::vector<uint32_t> par;
+  par.assign(parent_index_words(h.n_pols, h.n_rules), 0u);
+  build_parents(T->sets, h.n_sets, T->pols, h.n_pols, h.n_rules, par.data());
+  T->parents = par.data();
   return true;
 }
 
@@ -209,3 +213,76 @@ extern "C" int acs_host_what_is_allowed_work(const void* blob, size_t n, const a
   return 0;
 }
 #endif
+
+// whatIsAllowed templates (csrc/acs_eval.h wia_template_set): the template record of every class
+// row of the batch, as the GPU's template pass writes them; out: [cand_rows][stride] words.
+extern "C" int acs_host_wia_templates(const void* blob, size_t n, const acs_req_batch* b, uint32_t* out,
+                                      uint32_t* stride) {
+  Tables T;
+  if (!host_tables(blob, n, &T)) return -1;
+  const TplLayout TL = tpl_layout(T.n_sets, T.n_pols, T.n_rules);
+  const BitsLayout BL = bits_layout(T.n_sets, T.n_pols, T.n_rules);
+  *stride = TL.stride;
+  if (!out) return 0;
+  if (!b->cand || !b->cand_wv) return -1;
+  struct Acc {
+    uint32_t* rec;
+    void or_bits(uint32_t w, uint32_t bit) { rec[w] |= bit; }
+  };
+  for (uint32_t c = 0; c < b->cand_rows; ++c) {
+    uint32_t* rec = out + (size_t)c * TL.stride;
+    for (uint32_t w = 0; w < TL.stride; ++w) rec[w] = 0;
+    const uint32_t* row = b->cand + (size_t)c * b->cand_words;
+    Acc acc{rec};
+    bool ok = true, role_free = true;
+    for (uint32_t s = 0; s < T.n_sets && ok; ++s)
+      if (row_bit(row, 0, s)) ok = wia_template_set(T, row, b->cand_wp, b->cand_wr, b->cand_wv, BL, TL, s, acc, &role_free);
+    if (!ok) {
+      for (uint32_t w = 0; w < TL.stride; ++w) rec[w] = 0;
+      continue;
+    }
+    for (uint32_t w = 0; w < TL.exact - TL.work; ++w)
+      if (rec[TL.work + w]) rec[TL.mask + (w >> 5)] |= 1u << (w & 31u);
+    rec[TL.flags] = TPL_OK | (role_free ? TPL_ROLE_FREE : 0u);
+  }
+  return 0;
+}
+
+// whatIsAllowed from the templates where usable (tpl_usable), else the full walk: the outputs
+// of acs_host_what_is_allowed; *templated: how many requests took a template.
+extern "C" int acs_host_what_is_allowed_tpl(const void* blob, size_t n, const acs_req_batch* b, const uint32_t* tpl,
+                                            uint32_t* bits, uint32_t* obl, uint32_t* obl_n, acs_decision* out,
+                                            size_t* templated) {
+  Tables T;
+  if (!host_tables(blob, n, &T)) return -1;
+  Batch B = host_batch(b);
+  const TplLayout TL = tpl_layout(T.n_sets, T.n_pols, T.n_rules);
+  const BitsLayout BL = bits_layout(T.n_sets, T.n_pols, T.n_rules);
+  *templated = 0;
+  for (uint32_t i = 0; i < B.n; ++i) {
+    uint32_t* row = bits + (size_t)i * BL.words;
+    const ReqHdr h = req_hdr(B, i);
+    const uint32_t c1 = h.flags >> RQ_PCOL_SHIFT;
+    const uint32_t c2 = B.lines ? B.lines[i].cls2 : 0u;
+    const uint32_t* t1 = B.cand && c1 < B.cand_rows ? tpl + (size_t)c1 * TL.stride : nullptr;
+    const uint32_t* t2 = t1 && c2 && c2 - 1u < B.cand_rows ? tpl + (size_t)(c2 - 1u) * TL.stride : nullptr;
+    const uint32_t* r1 = t1 ? B.cand + (size_t)c1 * B.cand_words : nullptr;
+    const uint32_t* r2 = t2 ? B.cand + (size_t)(c2 - 1u) * B.cand_words : nullptr;
+    if (!(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags)) {
+      OblLog log{obl + (size_t)i * 2 * OBL_MAX, 0, false};
+      TplSink sink(row, BL, t1, t2);
+      if (what_is_allowed_tpl(ReqMem(T, B, i, h, req_line(B, i)), TL, BL, t1, t2, sink, log)) {
+        Decision d{};
+        if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
+        std::memcpy(&out[i], &d, sizeof d);
+        obl_n[i] = log.n;
+        ++*templated;
+        continue;
+      }
+    }
+    for (uint32_t w = 0; w < BL.words; ++w) row[w] = 0;
+    Decision d = what_is_allowed(T, B, i, row, obl + (size_t)i * 2 * OBL_MAX, obl_n + i);
+    std::memcpy(&out[i], &d, sizeof d);
+  }
+  return 0;
+}

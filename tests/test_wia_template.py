@@ -1,0 +1,121 @@
+"""whatIsAllowed templates (csrc/acs_eval.h: wia_template_set, what_is_allowed_tpl), CPU build of
+the core: a request decided from its class template(s) plus its work rules gets exactly the
+outputs of the full walk (inclusion rows, maskedProperty logs in push order, records) — random
+stores (errors, conditions, multi-entity requests, regex cells, properties), and c4-shaped batches
+with 1-2 role associations (composed class rows) from both encoders; most c4 requests are
+templated."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import host_core
+import randgen
+from diff_utils import build
+from acs_mi355x import compiler, encoder, native, store, synth, layout as L
+from acs_mi355x.codec import NativeCodec
+from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS
+
+
+def _lib():
+    lib = host_core.lib()
+    vp = C.c_void_p
+    lib.acs_host_wia_templates.argtypes = [vp, C.c_size_t, C.POINTER(native.ReqBatchC), vp, C.POINTER(C.c_uint32)]
+    lib.acs_host_what_is_allowed_tpl.argtypes = [vp, C.c_size_t, C.POINTER(native.ReqBatchC), vp, vp, vp, vp, vp,
+                                                 C.POINTER(C.c_size_t)]
+    return lib
+
+
+def templated_wia(cs, batch, compact):
+    """(bits, obl, obl_n, out, templated requests, templates) through the template path."""
+    from acs_mi355x.results import bits_layout
+    lib = _lib()
+    blob = compiler.store_blob(cs)
+    s = host_core._struct(batch, compact)
+    stride = C.c_uint32()
+    assert lib.acs_host_wia_templates(blob, len(blob), C.byref(s), None, C.byref(stride)) == 0
+    rows = int(s.cand_rows) if s.cand else 0
+    tpl = np.zeros((max(rows, 1), stride.value), np.uint32)
+    if s.cand and s.cand_wv:
+        assert lib.acs_host_wia_templates(blob, len(blob), C.byref(s), tpl.ctypes.data, C.byref(stride)) == 0
+    words = bits_layout(cs.n_sets, cs.n_pols, cs.n_rules)[2]
+    n = batch.n
+    bits = np.zeros((n, max(words, 1)), np.uint32)
+    obl = np.zeros((n, L.OBL_MAX, 2), np.uint32)
+    obl_n = np.zeros(n, np.uint32)
+    out = np.zeros(n, L.DECISION_DT)
+    k = C.c_size_t()
+    assert lib.acs_host_what_is_allowed_tpl(blob, len(blob), C.byref(s), tpl.ctypes.data, bits.ctypes.data,
+                                            obl.ctypes.data, obl_n.ctypes.data, out.ctypes.data, C.byref(k)) == 0
+    return bits, obl, obl_n, out, k.value, tpl
+
+
+def _same(got, want, ctx):
+    bits, obl, obl_n, out = got[:4]
+    wbits, wobl, wobl_n, wout = want
+    assert np.array_equal(np.ascontiguousarray(out).view(np.uint64), np.ascontiguousarray(wout).view(np.uint64)), ctx
+    assert np.array_equal(obl_n, wobl_n), ctx
+    assert np.array_equal(bits, wbits), ctx
+    for i in np.flatnonzero(obl_n):
+        assert np.array_equal(obl[i, :obl_n[i]], wobl[i, :obl_n[i]]), (ctx, int(i))
+
+
+def test_templates_equal_full_walk_random_stores():
+    checked = templated = 0
+    for seed in range(0, 240, 2):
+        urns, doc, reqs = randgen.rand_case(seed)
+        try:
+            _, cs = build(urns, doc)
+        except Exception:
+            continue
+        b = encoder.Encoder(cs).encode(reqs)
+        got = templated_wia(cs, b, compact=False)
+        _same(got, host_core.what_is_allowed(cs, b), seed)
+        templated += got[4]
+        checked += 1
+    assert checked >= 60 and templated > 0
+
+
+@pytest.mark.parametrize("second", [0.0, 0.5])
+def test_templates_c4_both_encoders(second):
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 3000, "c3", seed=21, second_role=second)
+    got = templated_wia(cs, sb.batch, compact=False)
+    _same(got, host_core.what_is_allowed(cs, sb.batch), ("synth", second))
+    assert got[4] > 0.9 * sb.batch.n  # c4: nearly every request decided from templates
+    codec = NativeCodec(compiler.store_blob(cs))
+    for k, v in sb.hrs_forests().items():
+        codec.set_subject_scopes(k, v)
+    nb = codec.encode(sb.json_text(), threads=2)
+    got = templated_wia(cs, nb, compact=True)
+    _same(got, host_core.what_is_allowed(cs, nb, compact=True), ("codec", second))
+    assert got[4] > 0.9 * nb.n
+    nb.close()
+    codec.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("second", [0.0, 0.5])
+def test_templates_gpu_equal_full_walk(second):
+    """K2 with the template pass (the product path for c4-shaped batches) equals the CPU build's
+    full walk: rows, logs and records, synthetic (SoA + lines) and codec (compact) batches."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from acs_mi355x.device import DeviceBatch, what_is_allowed_device
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 20_000, "c3", seed=23, second_role=second)
+    t = native.Tables(compiler.store_blob(cs), 0)
+    got = [x.cpu().numpy() for x in what_is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True))]
+    want = host_core.what_is_allowed(cs, sb.batch)
+    _same((got[0].view(np.uint32), got[1].view(np.uint32), got[2].view(np.uint32),
+           got[3].reshape(-1).view(L.DECISION_DT)), want, ("device", second))
+    _same(t.what_is_allowed(sb.batch), want, ("host buffers", second))
+    codec = NativeCodec(compiler.store_blob(cs))
+    for k, v in sb.hrs_forests().items():
+        codec.set_subject_scopes(k, v)
+    nb = codec.encode(sb.json_text(), threads=4)
+    _same(t.what_is_allowed(nb), host_core.what_is_allowed(cs, nb, compact=True), ("codec", second))
+    nb.close()
+    codec.close()
+    t.close()
