@@ -1984,9 +1984,16 @@ void Classes::run() {
   std::vector<uint32_t> ak(n, 0);
   std::vector<uint64_t> pairs_k;
   {
+    // per-thread counts of the single-action pairs (few distinct), merged
+    std::vector<std::unordered_map<uint64_t, uint32_t>> local(threads < 1 ? 1 : threads);
+    parallel_ranges(threads, n, [&](int t, size_t lo, size_t hi) {
+      auto& m = local[t];
+      for (size_t i = lo; i < hi; ++i)
+        if (B.h((uint32_t)i).nact == 1) ++m[(uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value];
+    });
     std::unordered_map<uint64_t, uint32_t> cnt;
-    for (uint32_t i = 0; i < n; ++i)
-      if (B.h(i).nact == 1) ++cnt[(uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value];
+    for (const auto& m : local)
+      for (const auto& kv : m) cnt[kv.first] += kv.second;
     std::vector<std::pair<uint64_t, uint32_t>> v(cnt.begin(), cnt.end());
     std::sort(v.begin(), v.end());
     if (v.size() > 62) {
@@ -1999,15 +2006,17 @@ void Classes::run() {
       idx[v[k].first] = k;
       pairs_k.push_back(v[k].first);
     }
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t na = B.h(i).nact;
-      if (na == 0) ak[i] = 0;
-      else if (na > 1) ak[i] = 1;
-      else {
-        auto it = idx.find((uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value);
-        ak[i] = it == idx.end() ? 1 : 2 + it->second;
+    parallel_ranges(threads, n, [&](int, size_t lo, size_t hi) {  // idx: read only here
+      for (size_t i = lo; i < hi; ++i) {
+        const uint32_t na = B.h((uint32_t)i).nact;
+        if (na == 0) ak[i] = 0;
+        else if (na > 1) ak[i] = 1;
+        else {
+          auto it = idx.find((uint64_t)B.lines[i].a0.id << 32 | B.lines[i].a0.value);
+          ak[i] = it == idx.end() ? 1 : 2 + it->second;
+        }
       }
-    }
+    });
   }
   // per-batch inputs of a row computation, built only when some key misses the cache
   std::vector<std::shared_ptr<const Row>> ent, arow;
@@ -2126,6 +2135,11 @@ void Classes::run() {
       return kb;
     };
     std::vector<uint32_t> key_of(N, NONE32), key_first;  // key_first: first item of each key
+    // the level is given up (below) past this many keys: the merge stops there
+    const size_t key_limit = level >= 3 ? ~size_t(0)
+                             : std::min(KEY_ROW_BYTES / ((size_t)W * 4),
+                                        level == 0 && force < 0 ? (size_t)n / 4 : ~size_t(0));
+    bool over_limit = false;
     {
       int T = threads < 1 ? 1 : threads;
       if ((size_t)T > N / 4096 + 1) T = (int)(N / 4096 + 1);
@@ -2153,9 +2167,9 @@ void Classes::run() {
       std::vector<std::vector<uint32_t>> remap(T);
       U64Map gm(4096);
       std::unordered_map<std::string, uint32_t> gs;
-      for (int t = 0; t < T; ++t) {
+      for (int t = 0; t < T && !over_limit; ++t) {
         remap[t].resize(firsts[t].size());
-        for (size_t k = 0; k < firsts[t].size(); ++k) {
+        for (size_t k = 0; k < firsts[t].size() && !over_limit; ++k) {
           const uint32_t x = firsts[t][k];
           uint32_t g;
           bool ins;
@@ -2168,9 +2182,11 @@ void Classes::run() {
           }
           if (ins) key_first.push_back(x);
           remap[t][k] = g;
+          over_limit = key_first.size() > key_limit;
         }
       }
-      parallel_ranges(T, N, [&](int t, size_t lo, size_t hi) {
+      if (!over_limit)
+        parallel_ranges(T, N, [&](int t, size_t lo, size_t hi) {
         for (size_t x = lo; x < hi; ++x)
           if (key_of[x] != NONE32) key_of[x] = remap[t][key_of[x]];
       });
@@ -2178,12 +2194,14 @@ void Classes::run() {
     const size_t nk = key_first.size();
     // over the row budget; or joint keys covering fewer than 4 requests each (candidates.classes:
     // waves could not share them, and the rows would outweigh the requests)
-    if (level < 3 && (nk * W * 4 > KEY_ROW_BYTES || (level == 0 && force < 0 && 4 * nk > (size_t)n))) continue;
+    if (over_limit || (level < 3 && (nk * W * 4 > KEY_ROW_BYTES || (level == 0 && force < 0 && 4 * nk > (size_t)n))))
+      continue;
     // cache lookup by (level, entity value, action, roles); compute the misses in parallel
     std::vector<std::string> gkey(nk);
     std::vector<std::shared_ptr<const ClassEntry>> entry(nk);
     std::vector<uint32_t> miss;
-    for (size_t k = 0; k < nk; ++k) {
+    parallel_ranges(threads, nk, [&](int, size_t lo, size_t hi) {
+    for (size_t k = lo; k < hi; ++k) {
       const uint32_t x = key_first[k], i = req_of(x);
       std::string g(1, (char)('0' + level));
       g += col_key(pcol[i]);
@@ -2199,13 +2217,21 @@ void Classes::run() {
       g.append((const char*)r, 4 * (size_t)m);
       gkey[k] = std::move(g);
     }
-    {
-      std::shared_lock<std::shared_mutex> lock(C.classes.mu);
-      for (size_t k = 0; k < nk; ++k) {
-        auto it = C.classes.by_key.find(gkey[k]);
-        if (it != C.classes.by_key.end()) entry[k] = it->second;
-        else miss.push_back((uint32_t)k);
-      }
+    });
+    {  // lookups over the threads (shared lock: concurrent readers), misses in key order
+      std::vector<uint8_t> hit(nk, 0);
+      parallel_ranges(threads, nk, [&](int, size_t lo, size_t hi) {
+        std::shared_lock<std::shared_mutex> lock(C.classes.mu);
+        for (size_t k = lo; k < hi; ++k) {
+          auto it = C.classes.by_key.find(gkey[k]);
+          if (it != C.classes.by_key.end()) {
+            entry[k] = it->second;
+            hit[k] = 1;
+          }
+        }
+      });
+      for (size_t k = 0; k < nk; ++k)
+        if (!hit[k]) miss.push_back((uint32_t)k);
     }
     B.classes_new += (uint32_t)miss.size();
     if (!miss.empty()) {
@@ -2283,16 +2309,20 @@ void Classes::run() {
         memcpy(B.cand + (size_t)rank[u] * W, uent[u]->row.data(), (size_t)W * 4);
     });
     std::vector<uint32_t> cls(n, PCOL_ALL);
-    for (uint32_t i = 0; i < n; ++i)
-      if (active[i]) cls[i] = rank[cls_of_key[key_of[i]]];
+    parallel_ranges(threads, n, [&](int, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i)
+        if (active[i]) cls[i] = rank[cls_of_key[key_of[i]]];
+    });
     if (composed) {
       // the second class of each two-role request: the heavier class first (the coherence
       // order groups by it), the same row once
-      for (size_t j = 0; j < two.size(); ++j) {
-        const uint32_t i = two[j], a = cls[i], b = rank[cls_of_key[key_of[n + j]]];
-        cls[i] = a < b ? a : b;
-        B.lines[i].cls2 = a == b ? 0u : (a < b ? b : a) + 1u;
-      }
+      parallel_ranges(threads, two.size(), [&](int, size_t lo, size_t hi) {
+        for (size_t j = lo; j < hi; ++j) {
+          const uint32_t i = two[j], a = cls[i], b = rank[cls_of_key[key_of[n + j]]];
+          cls[i] = a < b ? a : b;
+          B.lines[i].cls2 = a == b ? 0u : (a < b ? b : a) + 1u;
+        }
+      });
     }
     finish(cls);
     if (role_filter || !have_roles) return;

@@ -1049,8 +1049,10 @@ struct Workspace {
   DevBuf sort, img, out;
   DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
   DevBuf tpl;          // whatIsAllowed templates of the batch's class rows
+  DevBuf spread;       // a small batch's order spread over more waves (spread_waves)
   void release() {
     tpl.release();
+    spread.release();
     sort.release();
     img.release();
     out.release();
@@ -1068,6 +1070,7 @@ struct acs_tables {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
+  uint32_t simds = 0;   // the device's SIMDs (spread_waves; 0 until first asked)
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
   static constexpr int RING = 256;
   int timing = 0;
@@ -1776,6 +1779,44 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
   return coherence_perm(t, W, B, s, perm, pad, lanes);
 }
 
+// Small batches: a batch of fewer waves than the device holds runs as long as its longest wave,
+// and short class runs make every wave mix several classes (it walks the union of their
+// candidates).  Such a batch is spread over more waves, L requests each (the rest holes), L the
+// smallest of 64 / 32 / 16 that keeps the waves within ACS_SPREAD_PER_SIMD per SIMD of the device:
+// each wave then holds fewer classes (profiles/r05_a: at 131,072 c3 requests every wave lasts
+// about as long as the launch).
+#ifndef ACS_SPREAD_PER_SIMD
+#define ACS_SPREAD_PER_SIMD 4  // 0: off
+#endif
+__global__ __launch_bounds__(BLOCK) void spread_perm_kernel(const uint32_t* __restrict__ in, uint32_t lanes, uint32_t L,
+                                                            uint32_t out_lanes, uint32_t* __restrict__ out) {
+  const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+  if (j >= out_lanes) return;
+  const uint32_t q = j & 63u, k = (j >> 6) * L + q;
+  out[j] = q < L && k < lanes ? (in ? in[k] : k) : 0xFFFFFFFFu;
+}
+
+static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32_t** perm, size_t* lanes) {
+  if (!ACS_SPREAD_PER_SIMD || !t->sort) return 0;
+  if (!t->simds) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, t->device) != hipSuccess || cus <= 0) cus = 256;
+    t->simds = 4 * (uint32_t)cus;
+  }
+  const size_t cap = (size_t)t->simds * ACS_SPREAD_PER_SIMD;
+  uint32_t L = 64;
+  while (L > 16 && (*lanes + L / 2 - 1) / (L / 2) <= cap) L /= 2;
+  if (L == 64) return 0;
+  const size_t out_lanes = (*lanes + L - 1) / L * 64;
+  if (W.spread.reserve(out_lanes * sizeof(uint32_t))) return -1;
+  hipLaunchKernelGGL(spread_perm_kernel, dim3((unsigned)((out_lanes + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, *perm,
+                     (uint32_t)*lanes, L, (uint32_t)out_lanes, (uint32_t*)W.spread.p);
+  HIP_OK(hipGetLastError());
+  *perm = (const uint32_t*)W.spread.p;
+  *lanes = out_lanes;
+  return 0;
+}
+
 static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
@@ -1785,7 +1826,7 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   const bool pad = !ACS_AB_NO_PAD && B.cand && (uint64_t)B.n >= 32ull * B.cand_rows &&
                    (uint64_t)B.n < 256ull * B.cand_rows;
   size_t lanes = b->n;
-  if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, pad, &lanes) || spread_waves(t, W, s, &perm, &lanes)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
@@ -1827,7 +1868,7 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
   size_t lanes = b->n;
-  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes) || spread_waves(t, W, s, &perm, &lanes)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
