@@ -214,13 +214,18 @@ class AccessController:
             cs = self._compiler.compile(self._policy_sets, None)
         self._dirty, self._all_dirty = set(), False
         blob = compiler.store_blob(cs)
-        if self._tables is not None:
-            self._tables.close()
+        prev, self._tables = self._tables, None
         if self._engine is not None:
+            if prev is not None:
+                prev.close()
             self._tables = self._engine(blob)
         else:
             from . import native
-            self._tables = native.Tables(blob, self.device)
+            # the previous image with only its changed blocks uploaded (acs_compile_update)
+            self._tables = prev.updated(blob) if prev is not None else native.Tables(blob, self.device)
+            if prev is not None:
+                prev.close()
+            self.stats["upload_bytes"] = self._tables.upload_bytes
         self._cs = cs
         self._encoder = encoder.Encoder(cs)
         self.stats["compiles"] += 1

@@ -39,7 +39,8 @@ EXPORTS = ["acs_compile", "acs_free", "acs_is_allowed", "acs_is_allowed_device",
            "acs_codec_batch_view", "acs_codec_batch_reason", "acs_codec_string", "acs_codec_ec_values",
            "acs_codec_batch_stats", "acs_codec_batch_free", "acs_codec_batch_expand", "acs_pipeline_create",
            "acs_pipeline_free", "acs_pipeline_is_allowed", "acs_compile_multi", "acs_compile_sharded", "acs_device_list",
-           "acs_pipeline_host_reason", "acs_overflow_index_device", "acs_overflow_repass_device"]
+           "acs_pipeline_host_reason", "acs_overflow_index_device", "acs_overflow_repass_device",
+           "acs_compile_update", "acs_image_upload_bytes"]
 
 
 class ShardC(C.Structure):
@@ -53,6 +54,10 @@ def _declare(lib):
     lib.acs_compile.argtypes = [vp, C.c_size_t, C.c_int]
     lib.acs_compile_multi.restype = vp
     lib.acs_compile_multi.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    lib.acs_compile_update.restype = vp
+    lib.acs_compile_update.argtypes = [vp, vp, C.c_size_t]
+    lib.acs_image_upload_bytes.restype = C.c_size_t
+    lib.acs_image_upload_bytes.argtypes = [vp]
     lib.acs_compile_sharded.restype = vp
     lib.acs_compile_sharded.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
     lib.acs_device_list.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
@@ -220,6 +225,22 @@ class Tables:
         self.device = device
         self.words = int(self.lib.acs_wia_words_per_request(self.h))
 
+    def updated(self, blob: bytes) -> "Tables":
+        """A new handle for the changed store's blob (acs_compile_update: a device-side copy of this
+        image with only the differing blocks uploaded when the shape is unchanged); this handle
+        stays valid.  .upload_bytes: what the compile uploaded."""
+        t = Tables.__new__(Tables)
+        t.lib, t._blob, t.device = self.lib, blob, self.device
+        t.h = self.lib.acs_compile_update(self.h, blob, len(blob))
+        if not t.h:
+            raise RuntimeError(f"acs_compile_update failed: {last_error(self.lib)}")
+        t.words = int(self.lib.acs_wia_words_per_request(t.h))
+        return t
+
+    @property
+    def upload_bytes(self) -> int:
+        return int(self.lib.acs_image_upload_bytes(self.h))
+
     def devices(self):
         """The handle's devices (acs_device_list), primary first."""
         arr = (C.c_int * 64)()
@@ -239,10 +260,13 @@ class Tables:
         except Exception:
             pass
 
-    def is_allowed(self, batch, compact: bool = False) -> np.ndarray:
+    def is_allowed(self, batch, compact: bool = False, out=None) -> np.ndarray:
         """acs_is_allowed on host buffers: a CodecBatch ships its own (compact) form; a
-        RequestBatch its SoA rows + lines, or with compact=True its lines + extension records."""
-        out = np.zeros(batch.n, L.DECISION_DT)
+        RequestBatch its SoA rows + lines, or with compact=True its lines + extension records.
+        out: the caller's record array (e.g. page-locked), else a new one."""
+        if out is None:
+            out = np.zeros(batch.n, L.DECISION_DT)
+        assert out.dtype == L.DECISION_DT and len(out) >= batch.n and out.flags["C_CONTIGUOUS"]
         if batch.n:
             s = host_struct(batch, compact)
             if self.lib.acs_is_allowed(self.h, C.byref(s), out.ctypes.data) != 0:

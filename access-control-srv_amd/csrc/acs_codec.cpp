@@ -2137,7 +2137,7 @@ void Classes::run() {
     std::vector<uint32_t> key_of(N, NONE32), key_first;  // key_first: first item of each key
     // the level is given up (below) past this many keys: the merge stops there
     const size_t key_limit = level >= 3 ? ~size_t(0)
-                             : std::min(KEY_ROW_BYTES / ((size_t)W * 4),
+                             : std::min(W ? KEY_ROW_BYTES / ((size_t)W * 4) : ~size_t(0),
                                         level == 0 && force < 0 ? (size_t)n / 4 : ~size_t(0));
     bool over_limit = false;
     {

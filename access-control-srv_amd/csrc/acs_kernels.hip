@@ -1071,6 +1071,8 @@ struct acs_tables {
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
   uint32_t simds = 0;   // the device's SIMDs (spread_waves; 0 until first asked)
+  std::vector<char> host_img;  // the device image as uploaded (acs_compile_update diffs against it)
+  size_t upload_bytes = 0;     // bytes the compile uploaded (acs_compile_update: the differing blocks)
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
   static constexpr int RING = 256;
   int timing = 0;
@@ -1223,7 +1225,36 @@ int acs_layout_sizes(uint32_t* out, int n) {
   return 5;
 }
 
+}  // extern "C"
+static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, const acs_tables* prev);
+extern "C" {
+
 acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
+  return compile_image(blob, n_bytes, device, nullptr);
+}
+
+// A new handle for a changed store (the delta upload): the image is laid out
+// as acs_compile lays it out; when it has the previous handle's size (same node and pool counts:
+// an updateRule / updatePolicy that keeps the shape), the new device image is a device-side copy
+// of the previous one with only the 64-KB blocks that differ uploaded.  The previous handle stays
+// valid (in-flight batches keep it).
+acs_tables* acs_compile_update(const acs_tables* prev, const void* blob, size_t n_bytes) {
+  if (!prev) {
+    fail("acs_compile_update: null previous handle");
+    return nullptr;
+  }
+  if (prev->sharded || !prev->peers.empty()) {
+    fail("acs_compile_update: a multi-device or rule-sharded handle (recompile it with its own entry point)");
+    return nullptr;
+  }
+  return compile_image(blob, n_bytes, prev->device, prev);
+}
+
+size_t acs_image_upload_bytes(const acs_tables* t) { return t ? t->upload_bytes : 0; }
+
+}  // extern "C"
+
+static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, const acs_tables* prev) {
   if (!blob || n_bytes < sizeof(acs_blob_header)) {
     fail("acs_compile: blob too small");
     return nullptr;
@@ -1324,10 +1355,26 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->device = device;
   t->rx_rows_min = rx_rows_min;
   const size_t img_total = ev_off + evx.size() * sizeof(uint32_t);
-  const bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess &&
-                      hipMemcpy(t->dev, up, up_bytes, hipMemcpyHostToDevice) == hipSuccess &&
-                      (evx.empty() || hipMemcpy((char*)t->dev + ev_off, evx.data(), evx.size() * sizeof(uint32_t),
-                                                hipMemcpyHostToDevice) == hipSuccess);
+  // the host copy of the device image: acs_compile_update diffs the next image against it
+  t->host_img.assign(img_total, 0);
+  std::memcpy(t->host_img.data(), up, up_bytes);
+  if (!evx.empty()) std::memcpy(t->host_img.data() + ev_off, evx.data(), evx.size() * sizeof(uint32_t));
+  const char* hi = t->host_img.data();
+  bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess;
+  if (copied && prev && prev->device == device && prev->host_img.size() == img_total && prev->view.rstride == rstride) {
+    // delta: the previous image copied on the device, the differing 64-KB blocks uploaded
+    constexpr size_t BLK = 64 * 1024;
+    copied = hipMemcpy(t->dev, prev->dev, img_total, hipMemcpyDeviceToDevice) == hipSuccess;
+    for (size_t o = 0; copied && o < img_total; o += BLK) {
+      const size_t len = std::min(BLK, img_total - o);
+      if (std::memcmp(hi + o, prev->host_img.data() + o, len) == 0) continue;
+      copied = hipMemcpy((char*)t->dev + o, hi + o, len, hipMemcpyHostToDevice) == hipSuccess;
+      t->upload_bytes += len;
+    }
+  } else if (copied) {
+    copied = hipMemcpy(t->dev, hi, img_total, hipMemcpyHostToDevice) == hipSuccess;
+    t->upload_bytes = img_total;
+  }
   if (!copied ||
       hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&t->ev0) != hipSuccess || hipEventCreate(&t->ev1) != hipSuccess) {
@@ -1355,6 +1402,8 @@ acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
   t->image_bytes = img_total;
   return t;
 }
+
+extern "C" {
 
 void acs_free(acs_tables* t) {
   if (!t) return;

@@ -12,7 +12,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <cstddef>
+#include <thread>
 #include <vector>
 
 #include "../../include/acs_mi355x.h"
@@ -33,6 +35,24 @@ int bad(const char* what, size_t at) {
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 uint32_t words32(uint32_t n) { return (n + 31) >> 5; }
+
+// f(lo, hi) over [0, n) on up to 16 host threads (one per 64k items); returns the smallest item
+// index any call reported (f returns its first bad index, or n when none), so the error message
+// names the same request as a serial walk would.
+template <class F>
+size_t parallel_first_bad(size_t n, F f) {
+  size_t T = std::thread::hardware_concurrency();
+  T = T < 1 ? 1 : (T > 16 ? 16 : T);
+  if (T > n / 65536 + 1) T = n / 65536 + 1;
+  std::vector<size_t> bad(T, n);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; ++t) th.emplace_back([&, t] { bad[t] = f(n * t / T, n * (t + 1) / T); });
+  bad[0] = f(0, n / T);
+  for (auto& x : th) x.join();
+  size_t m = n;
+  for (size_t b : bad) m = b < m ? b : m;
+  return m;
+}
 
 }  // namespace
 
@@ -116,15 +136,21 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
   // skip an index >= n; a request missing from it would leave its record unwritten)
   if (b->perm) {
     if (b->perm_lanes < n || b->perm_lanes > 0xFFFFFFFFull) return bad("batch: perm_lanes", b->perm_lanes);
-    std::vector<uint8_t> seen(n, 0);
-    size_t got = 0;
-    for (size_t x = 0; x < b->perm_lanes; ++x) {
-      const uint32_t i = b->perm[x];
-      if (i == 0xFFFFFFFFu) continue;
-      if (i >= n || seen[i]) return bad("batch: perm (an index outside the batch, or twice)", x);
-      seen[i] = 1;
-      ++got;
-    }
+    std::vector<std::atomic<uint8_t>> seen(n);
+    for (auto& x : seen) x.store(0, std::memory_order_relaxed);
+    std::atomic<size_t> got{0};
+    const size_t at = parallel_first_bad(b->perm_lanes, [&](size_t lo, size_t hi) -> size_t {
+      size_t mine = 0;
+      for (size_t x = lo; x < hi; ++x) {
+        const uint32_t i = b->perm[x];
+        if (i == 0xFFFFFFFFu) continue;
+        if (i >= n || seen[i].exchange(1, std::memory_order_relaxed)) return x;
+        ++mine;
+      }
+      got += mine;
+      return b->perm_lanes;
+    });
+    if (at < b->perm_lanes) return bad("batch: perm (an index outside the batch, or twice)", at);
     if (got != n) return bad("batch: perm misses requests", got);
   }
   // RES_RX_SAFE on an attribute lets K1 stop early (the clean-below set walk, the final-fold
@@ -144,11 +170,12 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
   const ReqRes* res = (const ReqRes*)b->res;
   const size_t W = b->arena_words;
   const ReqLine* lines = (const ReqLine*)b->lines;
-  for (size_t i = 0; i < n; ++i) {
+  // one request's checks: nullptr, or what is malformed (the per-request loop runs on host threads)
+  auto check_one = [&](size_t i) -> const char* {
     const ReqHdr hd = compact ? lines[i].h : hdr[i];
-    if (hd.nres > QMAX || hd.nsubj > SMAX || hd.nact > AMAX || hd.nroles > RMAX) return bad("batch: counts", i);
+    if (hd.nres > QMAX || hd.nsubj > SMAX || hd.nact > AMAX || hd.nroles > RMAX) return "batch: counts";
     const size_t o = hd.arena_off;
-    if (o + 2 > W) return bad("batch: arena offset", i);
+    if (o + 2 > W) return "batch: arena offset";
     const uint32_t* ar = b->arena + o;
     const size_t room = W - o;
     const bool live = !(hd.flags & (RQ_HOST | RQ_NO_TARGET));
@@ -158,11 +185,11 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
       const ExtGeom g = ext_geom(hd.nres, hd.nsubj, hd.nact, hd.nroles);
       if (g.words) {
         const uint32_t e = lines[i].ext;
-        if (!e || !b->ext || ((size_t)e - 1) * 4 + g.words > b->ext_words) return bad("batch: extension record", i);
+        if (!e || !b->ext || ((size_t)e - 1) * 4 + g.words > b->ext_words) return "batch: extension record";
         ex = b->ext + ((size_t)e - 1) * 4;
       }
       if (lines[i].ar0 != (live ? ar[0] : 0u) || lines[i].ar1 != (live ? ar[1] : 0u))
-        return bad("batch: request line arena counts", i);
+        return "batch: request line arena counts";
     } else if (lines) {  // the packed line must equal the SoA rows (K1 trusts it for addressing)
       ReqLine want{};
       want.h = hd;
@@ -180,7 +207,7 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
       }
       want.ext = lines[i].ext;  // (an SoA batch reads its rows, not extension records)
       want.cls2 = lines[i].cls2;  // (a class fact, not a row: checked below)
-      if (std::memcmp(&want, &lines[i], sizeof want) != 0) return bad("batch: request line differs from its rows", i);
+      if (std::memcmp(&want, &lines[i], sizeof want) != 0) return "batch: request line differs from its rows";
     }
     auto res_at = [&](uint32_t j) -> ReqRes {
       if (!compact) return res[(size_t)j * n + i];
@@ -192,49 +219,56 @@ int acs_internal_check_batch2(const acs_req_batch* b, uint32_t n_sets, uint32_t 
     const uint32_t c0 = ar[0], c1 = ar[1];
     const uint32_t ng = c0 & 0xFF, nre = (c0 >> 8) & 0xFF, ns = (c0 >> 16) & 0xFF, nro = c0 >> 24;
     const uint32_t nt = c1 & 0xFF, nh = (c1 >> 8) & 0xFF;
-    if (nro > MAX_ROOTS || nh > MAX_HRKEYS || ns > MAX_SLOTS) return bad("batch: arena header", i);
+    if (nro > MAX_ROOTS || nh > MAX_HRKEYS || ns > MAX_SLOTS) return "batch: arena header";
     const size_t head = 2 + 3 * (size_t)ng + 2 * (size_t)nre + nro + nh + ns + 3 * (size_t)nt;
-    if (head > room) return bad("batch: arena header", i);
+    if (head > room) return "batch: arena header";
     size_t used = head;  // words of this request's records past its offset
     const uint32_t* slotoff = ar + 2 + 3 * ng + 2 * nre + nro + nh;
     const uint32_t* tse = slotoff + ns;
     for (uint32_t s = 0; s < ns; ++s) {  // [owners_empty, n_owners, owner...]
       size_t at = slotoff[s];
-      if (at + 2 > room) return bad("batch: arena slot record", i);
+      if (at + 2 > room) return "batch: arena slot record";
       const uint32_t no = ar[at + 1];
       at += 2;
       for (uint32_t k = 0; k < no; ++k) {  // [is_oe | n_attrs << 8, value, n_attrs x 3]
-        if (at + 2 > room) return bad("batch: arena owner record", i);
+        if (at + 2 > room) return "batch: arena owner record";
         at += 2 + 3 * (size_t)(ar[at] >> 8);
-        if (at > room) return bad("batch: arena owner record", i);
+        if (at > room) return "batch: arena owner record";
       }
       if (at > used) used = at;
     }
     for (uint32_t e = 0; e < nt; ++e) {  // (se, n_inst, inst_rel_off) -> n_inst x 2
       const uint32_t ni = tse[3 * e + 1];
-      if (ni > 32 || (size_t)tse[3 * e + 2] + 2 * (size_t)ni > room) return bad("batch: arena instance list", i);
+      if (ni > 32 || (size_t)tse[3 * e + 2] + 2 * (size_t)ni > room) return "batch: arena instance list";
       if ((size_t)tse[3 * e + 2] + 2 * (size_t)ni > used) used = (size_t)tse[3 * e + 2] + 2 * (size_t)ni;
     }
     if (arena_end) arena_end[i] = (uint32_t)(o + used);
     // composed class rows: a second class needs a valid first one, and no role factor
     if (lines && lines[i].cls2) {
       const uint32_t c1 = hd.flags >> RQ_PCOL_SHIFT, c2 = lines[i].cls2 - 1u;
-      if (!b->cand || b->role_key || c1 >= b->cand_rows || c2 >= b->cand_rows) return bad("batch: second class row", i);
+      if (!b->cand || b->role_key || c1 >= b->cand_rows || c2 >= b->cand_rows) return "batch: second class row";
     }
     const uint32_t ent = (hd.flags >> RQ_ENT_SHIFT) & 7u;
     const uint32_t e0 = ent >= 1 && ent <= 6 ? ent - 1 : (uint32_t)QMAX;  // the lone entity attr's slot
-    if (compact && e0 < QMAX && e0 >= hd.nres) return bad("batch: entity slot", i);
+    if (compact && e0 < QMAX && e0 >= hd.nres) return "batch: entity slot";
     for (uint32_t j = 0; j < QMAX; ++j) {
       if (j >= hd.nres && j != e0) continue;
       const ReqRes q = res_at(j);
       if (rx_rows_min && ((q.kind & K_ENT_LOOSE) || j == e0) && q.col >= b->rx_cols)
-        return bad("batch: regex matrix column", i);
+        return "batch: regex matrix column";
       if (!col_unsafe.empty() && (q.kind & K_ENT_LOOSE) && (q.pad & RES_RX_SAFE) && col_unsafe[q.col])
-        return bad("batch: RES_RX_SAFE on a regex column that throws or needs the host", i);
+        return "batch: RES_RX_SAFE on a regex column that throws or needs the host";
       if ((q.slot_a != NONE8 && q.slot_a >= ns) || (q.slot_b != NONE8 && q.slot_b >= ns))
-        return bad("batch: context resource slot", i);
+        return "batch: context resource slot";
     }
-  }
+    return nullptr;
+  };
+  const size_t first = parallel_first_bad(n, [&](size_t lo, size_t hi) -> size_t {
+    for (size_t i = lo; i < hi; ++i)
+      if (check_one(i)) return i;
+    return n;
+  });
+  if (first < n) return bad(check_one(first), first);
   return 0;
 }
 

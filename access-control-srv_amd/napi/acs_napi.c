@@ -745,6 +745,47 @@ static napi_value js_compile(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* compileUpdate(prev, blob): acs_compile_update — the changed store's image from prev's with
+ * only the differing blocks uploaded (same shape), else a full upload; prev stays valid */
+static napi_value js_compile_update(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  void* blob;
+  size_t len;
+  int freed = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tables_h* prev = argc > 0 ? (tables_h*)lookup(env, argv[0], H_TABLES, &freed) : NULL;
+  if (!prev || argc < 2 || get_bytes(env, argv[1], &blob, &len) || !blob) {
+    if (!freed) napi_throw_type_error(env, NULL, "compileUpdate(tables, blob: Uint8Array)");
+    return NULL;
+  }
+  acs_tables* t = acs_compile_update(prev->t, blob, len);
+  if (!t) return throw_acs(env, "acs_compile_update");
+  tables_h* h = (tables_h*)calloc(1, sizeof *h);
+  if (!h) {
+    acs_free(t);
+    napi_throw_error(env, NULL, "out of memory");
+    return NULL;
+  }
+  h->t = t;
+  return make_handle(env, &h->base, H_TABLES);
+}
+
+/* uploadBytes(tables): the bytes its compile uploaded (acs_image_upload_bytes) */
+static napi_value js_upload_bytes(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  int freed = 0;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  tables_h* h = argc > 0 ? (tables_h*)lookup(env, argv[0], H_TABLES, &freed) : NULL;
+  if (!h) {
+    if (!freed) napi_throw_type_error(env, NULL, "uploadBytes(tables)");
+    return NULL;
+  }
+  CHECK(env, napi_create_double(env, (double)acs_image_upload_bytes(h->t), &out));
+  return out;
+}
+
 static napi_value js_devices(napi_env env, napi_callback_info info) {
   size_t argc = 1;
   napi_value argv[1], out;
@@ -1491,6 +1532,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"storeBuilderCompile", NULL, js_builder_compile, NULL, NULL, NULL, napi_enumerable, NULL},
       {"storeBuilderFree", NULL, js_builder_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"compile", NULL, js_compile, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"compileUpdate", NULL, js_compile_update, NULL, NULL, NULL, napi_enumerable, NULL},
+      {"uploadBytes", NULL, js_upload_bytes, NULL, NULL, NULL, napi_enumerable, NULL},
       {"free", NULL, js_free, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecCreate", NULL, js_codec_create, NULL, NULL, NULL, napi_enumerable, NULL},
       {"codecFree", NULL, js_codec_free, NULL, NULL, NULL, napi_enumerable, NULL},

@@ -260,7 +260,9 @@ class GpuAccessController {
       this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
       return;
     }
-    const tables = addon.compile(blob, this.device);
+    // one device: the previous image with only its changed blocks uploaded (acs_compile_update)
+    const tables = this.tables && !Array.isArray(this.device) ? addon.compileUpdate(this.tables, blob)
+      : addon.compile(blob, this.device);
     const codec = addon.codecCreate(blob);
     const pipeline = this.pipelineBytes === null ? null : addon.pipelineCreate(tables, codec, this.threads, this.chunk);
     // the old handles: released once the batches still in flight are done with them
@@ -278,7 +280,8 @@ class GpuAccessController {
     this.policySets = policySets;
     this.dirty = new Set();
     this.stale = false;
-    this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
+    this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length,
+                         uploadBytes: addon.uploadBytes(tables) };
   }
 
   // node index of the compiled Map (whatIsAllowed's ReverseQuery assembly), built lazily: it

@@ -341,14 +341,17 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
 
 
 def pinned_compact(batch):
-    """The batch's compact arrays (lines, extension records, arena, regex matrix, class rows)
-    copied into page-locked host memory (torch pin_memory), as the native codec leaves them:
-    what a service hands to acs_is_allowed."""
+    """The batch's compact arrays (lines, extension records, arena, regex matrix, class rows,
+    coherence order) copied into page-locked host memory (torch pin_memory), as the native codec
+    leaves them: what a service hands to acs_is_allowed."""
     import types
     out = types.SimpleNamespace(n=batch.n, rx_rows=batch.rx_rows, cand_wp=batch.cand_wp, cand_wr=batch.cand_wr,
-                                cand_wsu=batch.cand_wsu, cand_wpu=batch.cand_wpu, cand_wv=batch.cand_wv)
+                                cand_wsu=batch.cand_wsu, cand_wpu=batch.cand_wpu, cand_wv=batch.cand_wv,
+                                hints=getattr(batch, "hints", 0))
     keep = []
-    for k in ("lines", "ext", "arena", "rx", "cand", "role_key", "role_bits"):
+    # perm: the encoder's coherence order travels with the batch (as the codec leaves it), so the
+    # host-buffer path runs K1 in that order instead of re-sorting on the device
+    for k in ("lines", "ext", "arena", "rx", "cand", "role_key", "role_bits", "perm"):
         a = getattr(batch, k)
         if a is None:
             setattr(out, k, None)
@@ -646,14 +649,16 @@ def main():
         # host buffers through acs_is_allowed: H2D + sort + K1 + D2H (reported beside, never
         # `value`), from the compact form in page-locked memory, as the codec leaves a batch
         hb = pinned_compact(sb.batch)
-        tables.is_allowed(hb, compact=True)
+        pinned_out = torch.empty(n * 8, dtype=torch.uint8, pin_memory=True)
+        host_dec = pinned_out.numpy().view(L.DECISION_DT)
+        tables.is_allowed(hb, compact=True, out=host_dec)
         t1 = time.perf_counter()
-        host_dec = tables.is_allowed(hb, compact=True)
+        tables.is_allowed(hb, compact=True, out=host_dec)
         pcie_s = time.perf_counter() - t1
         pcie = {"value": n / pcie_s, "unit": "decisions/s", "ms": pcie_s * 1e3,
                 "input_bytes": int(sb.batch.compact_nbytes()),
-                "input": "compact batch (request lines + extension records + arena + regex matrix + class rows) "
-                         "in page-locked host memory",
+                "input": "compact batch (request lines + extension records + arena + regex matrix + class rows + "
+                         "coherence order) in page-locked host memory, records into page-locked memory",
                 "identical_to_device_path": bool(np.array_equal(host_dec.view(np.uint64), dec.view(np.uint64)))}
         del hb
     if rank == 0:

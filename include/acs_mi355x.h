@@ -146,6 +146,15 @@ int acs_device_list(const acs_tables* t, int* devices, int n);
  * evaluation entry points refuse a sharded handle. */
 acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 
+/* Replaces: the device side of a store change (AccessController.updateRule / updatePolicy / ...,
+ * accessController.ts:897-937, after the host recompiles the changed sets).  A new handle for the
+ * changed store's blob on prev's device: when the image keeps prev's shape (same node and pool
+ * counts), the device image is a device-side copy of prev's with only the 64-KB blocks that differ
+ * uploaded (acs_image_upload_bytes: the bytes a compile uploaded); otherwise a full upload.  prev
+ * stays valid (batches in flight keep it) and is freed by the caller.  Single-device handles. */
+acs_tables* acs_compile_update(const acs_tables* prev, const void* blob, size_t n_bytes);
+size_t acs_image_upload_bytes(const acs_tables* t);
+
 /* Replaces: AccessController.isAllowed (accessController.ts:88-324), for a batch.
  * Host buffers in and out; synchronous (H2D, kernel, D2H on an internal stream).  Safe to
  * call from several host threads on one handle (calls are serialised per handle). */

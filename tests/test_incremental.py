@@ -309,3 +309,56 @@ def test_incremental_gpu(seed):
             compared += 1
     ctl.close()
     assert compared > 0 or not reqs
+
+
+@pytest.mark.gpu
+def test_delta_upload_gpu():
+    """acs_compile_update (the delta upload): after an updateRule that keeps
+    the store's shape, the new handle's image is the previous one with only the changed 64-KB
+    blocks uploaded, and it decides exactly like a fresh handle of the new image; a change of
+    shape (a rule added) uploads the whole image, with the same guarantee."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from acs_mi355x import native, synth
+    from oracle.acs_oracle import FULL_URNS
+    base = pstore.populate(synth.c3_store())
+    ic = compiler.IncrementalCompiler(FULL_URNS, DEFAULT_CAS)
+    cs = ic.compile(base)
+    t = native.Tables(compiler.store_blob(cs), 0)
+    assert t.upload_bytes >= len(compiler.store_blob(cs)) // 2
+    sb = synth.requests(cs, 20_000, "c3", seed=3, second_role=0.5)
+    texts = sb.json_text()
+    import json
+    reqs = json.loads(texts)
+    key = list(base)[150]
+    ps = base[key]
+    pkey = list(ps["combinables"])[2]
+    rules = ps["combinables"][pkey]["combinables"]
+    rkey = list(rules)[4]
+    r = dict(rules[rkey])
+    r["effect"] = "DENY" if r.get("effect") == "PERMIT" else "PERMIT"
+    rules[rkey] = r
+    cs2 = ic.compile(base, dirty={key})
+    blob2 = compiler.store_blob(cs2)
+    t2 = t.updated(blob2)
+    assert 0 < t2.upload_bytes <= 1 << 20, t2.upload_bytes
+    fresh = native.Tables(blob2, 0)
+    b2 = encoder.Encoder(cs2).encode(reqs)
+    want = fresh.is_allowed(b2)
+    assert np.array_equal(t2.is_allowed(b2).view(np.uint64), want.view(np.uint64))
+    assert np.array_equal(t.is_allowed(encoder.Encoder(cs).encode(reqs)).view(np.uint64),
+                          native.Tables(compiler.store_blob(cs), 0).is_allowed(
+                              encoder.Encoder(cs).encode(reqs)).view(np.uint64))  # the old handle still works
+    # a new rule: another shape, a full upload
+    nr = dict(r)
+    nr["id"] = "added-rule"
+    rules["added-rule"] = nr
+    cs3 = ic.compile(base, dirty={key})
+    blob3 = compiler.store_blob(cs3)
+    t3 = t2.updated(blob3)
+    assert t3.upload_bytes >= len(blob3) // 2
+    b3 = encoder.Encoder(cs3).encode(reqs)
+    assert np.array_equal(t3.is_allowed(b3).view(np.uint64), native.Tables(blob3, 0).is_allowed(b3).view(np.uint64))
+    for x in (t, t2, t3, fresh):
+        x.close()

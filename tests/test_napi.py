@@ -37,7 +37,8 @@ def test_addon_loads_with_surface():
                                    "decideAsync", "pipelineCreate", "pipelineFree", "pipelineDecideAsync",
                                    "storeBuilderCreate", "storeBuilderStage", "storeBuilderCompile", "storeBuilderFree",
                                    "devices", "isAllowed", "isAllowedAsync", "whatIsAllowed", "whatIsAllowedObl",
-                                   "wordsPerRequest", "layoutSizes", "deviceCount", "lastError"])
+                                   "wordsPerRequest", "layoutSizes", "deviceCount", "lastError", "compileUpdate",
+                                   "uploadBytes"])
     assert info["sizes"] == [64, 16, 16, 16, 8]
     assert "magic" in r.stdout.splitlines()[1]  # a bad image is rejected with acs_last_error's message
 
