@@ -54,10 +54,11 @@ def _declare(lib):
     lib.acs_compile.argtypes = [vp, C.c_size_t, C.c_int]
     lib.acs_compile_multi.restype = vp
     lib.acs_compile_multi.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
-    lib.acs_compile_update.restype = vp
-    lib.acs_compile_update.argtypes = [vp, vp, C.c_size_t]
-    lib.acs_image_upload_bytes.restype = C.c_size_t
-    lib.acs_image_upload_bytes.argtypes = [vp]
+    if hasattr(lib, "acs_compile_update"):  # (A/B builds of earlier sources lack it)
+        lib.acs_compile_update.restype = vp
+        lib.acs_compile_update.argtypes = [vp, vp, C.c_size_t]
+        lib.acs_image_upload_bytes.restype = C.c_size_t
+        lib.acs_image_upload_bytes.argtypes = [vp]
     lib.acs_compile_sharded.restype = vp
     lib.acs_compile_sharded.argtypes = [vp, C.c_size_t, C.POINTER(C.c_int), C.c_int]
     lib.acs_device_list.argtypes = [vp, C.POINTER(C.c_int), C.c_int]
