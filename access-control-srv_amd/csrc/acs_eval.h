@@ -38,7 +38,10 @@ namespace acs {
 // skipped from the event index's bits without loading their records (c3adv unchanged 1.83 ->
 // 1.85, c3 3.16 -> 3.29 ms: registers, r05_c).
 #ifndef ACS_OWN_SKIP
-#define ACS_OWN_SKIP 0
+#define ACS_OWN_SKIP 7  // the skips K1's SK instantiation takes (K1 launches it for mixed-class waves)
+#endif
+#ifndef ACS_K2_OWN_SKIP
+#define ACS_K2_OWN_SKIP 0  // K2's rule skip (what_is_allowed_t)
 #endif
 #ifndef ACS_VERDICT_ROLES
 #define ACS_VERDICT_ROLES 1
@@ -1097,13 +1100,15 @@ ACS_FN Decision make_err(tri e, uint32_t at = 0) {
 
 // AN: compile the ACL_NONE skips (acs_req_batch.hints); without them an ACL_NONE request is
 // still decided exactly (verify_acl vetoes its pushes), the skips only cost registers.
-template <bool AN = true, class RQ, class FL>
+template <bool AN = true, bool SK = false, class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F);
 
-template <bool AN = true, class RQ, class FL>
+// SK: lanes skip the sets / policies / rules outside their own rows (ACS_OWN_SKIP bits) — the
+// instantiation for waves that mix classes (spread small batches)
+template <bool AN = true, bool SK = false, class RQ, class FL>
 ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
   PROF_T0(t_total);
-  const Decision d = is_allowed_body<AN>(R, F);
+  const Decision d = is_allowed_body<AN, SK>(R, F);
   PROF_ADD(PH_TOTAL, t_total);
   return d;
 }
@@ -1122,7 +1127,7 @@ ACS_FN Decision is_allowed_t(const RQ& R, const FL& F) {
 // algorithm are never evaluated this way (their event depends on any push).
 enum SetOutcome { SET_NONE = 0, SET_EFFECT = 1, SET_EVENT = 2 };
 
-template <bool AN, class RQ, class FL>
+template <bool AN, bool SK, class RQ, class FL>
 ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool safe, bool events_only,
                     uint8_t* eff, uint8_t* ec, Decision* ev) {
   const Tables& T = R.T;
@@ -1176,17 +1181,15 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
   const bool cut_p = safe && (S.nflags & NF_COND_FREE);
   CandRange pols(F, F.wpu, S.child_begin, S.child_end);  // loop 2b: the useful policies
   uint32_t p;
-#if ACS_OWN_SKIP & 2
-  uint32_t pw = 0xFFFFFFFFu, pbits = 0;  // the lane's own useful-policy word last read
-#endif
+  uint32_t pw = 0xFFFFFFFFu, pbits = 0;  // SK: the lane's own useful-policy word last read
   while (pols.next(p)) {
-#if ACS_OWN_SKIP & 2
-    if ((p >> 5) != pw) {  // a policy outside the lane's own useful row cannot change its record
-      pw = p >> 5;
-      pbits = F.own_word(F.wpu + pw);
+    if constexpr (SK && (ACS_OWN_SKIP & 2)) {
+      if ((p >> 5) != pw) {  // a policy outside the lane's own useful row cannot change its record
+        pw = p >> 5;
+        pbits = F.own_word(F.wpu + pw);
+      }
+      if (!((pbits >> (p & 31u)) & 1u)) continue;
     }
-    if (!((pbits >> (p & 31u)) & 1u)) continue;
-#endif
     ACS_OPC(OP_P2B_ITER);
     const NodeRec P = node_at(T, T.pols, p, T.n_pols);
     if (P.nflags & NF_NULL) continue;
@@ -1232,9 +1235,7 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
     ACS_OPC(OP_RULE_LOOP);
     CandRange rules(F, F.wr, P.child_begin, P.child_end);
     uint32_t r;
-#if ACS_OWN_SKIP & 1
-    uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // the lane's own rule-section word last read
-#endif
+    uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // SK: the lane's own rule-section word last read
     while (rules.next(r)) {
       ACS_OPC(OP_RULE_ITER);
       const NodeRec Q = rule_at(T, r);
@@ -1246,19 +1247,19 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
       if (Q.nflags & NF_HAS_TARGET) {
         PROF_T0(tr);
         const bool vt = F.verdict(4 * WP, r, false, (Q.tflags & TF_SUBJ_ROLE) != 0);
-#if ACS_OWN_SKIP & 1
-        // the wave walks the union of its lanes' rows: a rule outside this lane's own row cannot
-        // match its target (the filter keeps every node whose target can pass), so the lane
-        // leaves it without target matching — a wave whose lanes all know the rule or do not
-        // hold it skips the match altogether
-        if (!vt) {
-          if ((r >> 5) != own_w) {
-            own_w = r >> 5;
-            own_bits = F.own_word(F.wr + own_w);
+        // SK: the wave walks the union of its lanes' rows: a rule outside this lane's own row
+        // cannot match its target (the filter keeps every node whose target can pass), so the
+        // lane leaves it without target matching — a wave whose lanes all know the rule or do
+        // not hold it skips the match altogether
+        if constexpr (SK && (ACS_OWN_SKIP & 1)) {
+          if (!vt) {
+            if ((r >> 5) != own_w) {
+              own_w = r >> 5;
+              own_bits = F.own_word(F.wr + own_w);
+            }
+            if (!((own_bits >> (r & 31u)) & 1u)) continue;
           }
-          if (!((own_bits >> (r & 31u)) & 1u)) continue;
         }
-#endif
 #if defined(ACS_OP_COUNT)
         if (!vt) ACS_OPC(OP_RULE_TM);
 #endif
@@ -1336,7 +1337,7 @@ ACS_FN bool set_may_raise(const Tables& T, const FL& F, uint32_t s) {
 // over everything.  Once something was found and every set below is clean (NF_CLEAN_BELOW)
 // and the request safe (nothing of it can throw there: see `safe`), no set below can change
 // the record and the lane stops; otherwise it walks on to set 0.
-template <bool AN, class RQ, class FL>
+template <bool AN, bool SK, class RQ, class FL>
 ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   const Tables& T = R.T;
   // Cutting a combining loop short: once a fold's result is final (Fold::final), the rest of
@@ -1357,9 +1358,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   bool have_ev = false;
   CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
-#if ACS_OWN_SKIP & 4
-  uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // the lane's own useful-set word last read
-#endif
+  uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // SK: the lane's own useful-set word last read
 #if ACS_CLEAN_BITS
   uint32_t clean_w = 0xFFFFFFFFu, clean_bits = 0;  // the event index's clean-set word last read
   const uint32_t* clean_sec =
@@ -1382,16 +1381,16 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       }
     }
 #endif
-#if ACS_OWN_SKIP & 4
-    // the wave walks the union of its lanes' useful sets; a set outside this lane's own useful
-    // row cannot change its record (candidates.py: useful sections), so the lane leaves it —
-    // and the wave, once no active lane holds it
-    if ((s >> 5) != own_w) {
-      own_w = s >> 5;
-      own_bits = F.own_word(F.wsu + own_w);
+    if constexpr (SK && (ACS_OWN_SKIP & 4)) {
+      // the wave walks the union of its lanes' useful sets; a set outside this lane's own useful
+      // row cannot change its record (candidates.py: useful sections), so the lane leaves it —
+      // and the wave, once no active lane holds it
+      if ((s >> 5) != own_w) {
+        own_w = s >> 5;
+        own_bits = F.own_word(F.wsu + own_w);
+      }
+      if (!((own_bits >> (s & 31u)) & 1u)) continue;
     }
-    if (!((own_bits >> (s & 31u)) & 1u)) continue;
-#endif
     ACS_OPC(OP_SET_ITER);
     const NodeRec S = node_at(T, T.sets, s, T.n_sets);
     // below the deciding set (or an event) only an event can change the record, and a clean
@@ -1406,7 +1405,7 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     if (events_only && !set_may_raise(T, F, s)) continue;
     // an ACL_NONE request gets no push from an ACL-inert set: only its events matter
     if (acl_none && set_acl_inert(T, s) && !set_may_raise(T, F, s)) continue;
-    const int o = eval_set<AN>(R, F, s, S, safe, events_only, &e2, &c2, &d2);
+    const int o = eval_set<AN, SK>(R, F, s, S, safe, events_only, &e2, &c2, &d2);
     if (o == SET_EVENT) {
       ev = d2;  // lower than any event found so far
       have_ev = true;
@@ -1622,7 +1621,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         uint32_t m = F.word(F.wr + w);
         if (base < rb) m &= ~0u << (rb & 31u);
         if (re - base < 32u) m &= (1u << (re - base)) - 1u;
-#if ACS_OWN_SKIP & 1
+#if ACS_K2_OWN_SKIP
         const uint32_t mine = m & F.own_word(F.wr + w);  // this lane's own candidates (the rest is inert for it)
 #else
         const uint32_t mine = m;

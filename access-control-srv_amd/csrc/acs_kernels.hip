@@ -578,8 +578,16 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 #ifndef ACS_K1_AN_WAVES_PER_EU
 #define ACS_K1_AN_WAVES_PER_EU 4
 #endif
-template <class FL, bool CB, bool AN>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_K1_AN_WAVES_PER_EU : ACS_K1_WAVES_PER_EU))) void is_allowed_kernel(
+// SK: the lanes skip the sets, policies and rules outside their own class rows (acs_eval.h
+// is_allowed_t) — the instantiation for spread small batches, whose waves mix classes (c3 131,072
+// requests: K1 0.670 -> 0.578 ms with 32 lanes per wave, r05_e; whole 1M-request c3 chunks run
+// slower with the skips, r05_b)
+#ifndef ACS_K1_SK_WAVES_PER_EU
+#define ACS_K1_SK_WAVES_PER_EU ACS_K1_WAVES_PER_EU
+#endif
+template <class FL, bool CB, bool AN, bool SK = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
+    AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
@@ -616,10 +624,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(AN ? ACS_
     for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
     const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
-    d = is_allowed_t<AN>(R, F);
+    d = is_allowed_t<AN, SK>(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t<AN>(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
+    d = is_allowed_t<AN, SK>(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -1002,6 +1010,7 @@ FilterForm filter_form(const Batch& B) {
 #define ACS_TARGS_NONE
 #define ACS_TARGS_ACL_NONE , true
 #define ACS_TARGS_ACL_PLAIN , false
+#define ACS_TARGS_ACL_PLAIN_SK , false, true
 #define ACS_LAUNCH_FILTERED(kernel, ...) ACS_LAUNCH_FILTERED_X(kernel, ACS_TARGS_NONE, __VA_ARGS__)
 #define ACS_LAUNCH_FILTERED_X(kernel, X, grid, lds, stream, form, compact, ...)                           \
   do {                                                                                                  \
@@ -1834,8 +1843,11 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 // smallest of 64 / 32 / 16 that keeps the waves within ACS_SPREAD_PER_SIMD per SIMD of the device:
 // each wave then holds fewer classes (profiles/r05_a: at 131,072 c3 requests every wave lasts
 // about as long as the launch).
+#ifndef ACS_K1_SPREAD_SKIPS
+#define ACS_K1_SPREAD_SKIPS 1  // 0: spread batches take K1's plain instantiation
+#endif
 #ifndef ACS_SPREAD_PER_SIMD
-#define ACS_SPREAD_PER_SIMD 4  // 0: off
+#define ACS_SPREAD_PER_SIMD 8  // 0: off (c3 131,072 requests: K1 0.814 ms unspread, 0.670 at 4, 0.543 at 8; r05_e)
 #endif
 __global__ __launch_bounds__(BLOCK) void spread_perm_kernel(const uint32_t* __restrict__ in, uint32_t lanes, uint32_t L,
                                                             uint32_t out_lanes, uint32_t* __restrict__ out) {
@@ -1845,7 +1857,10 @@ __global__ __launch_bounds__(BLOCK) void spread_perm_kernel(const uint32_t* __re
   out[j] = q < L && k < lanes ? (in ? in[k] : k) : 0xFFFFFFFFu;
 }
 
-static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32_t** perm, size_t* lanes) {
+// *spread: set when the batch was spread (its waves hold fewer than 64 requests)
+static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32_t** perm, size_t* lanes,
+                        bool* spread = nullptr) {
+  if (spread) *spread = false;
   if (!ACS_SPREAD_PER_SIMD || !t->sort) return 0;
   if (!t->simds) {
     int cus = 0;
@@ -1863,6 +1878,7 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
   HIP_OK(hipGetLastError());
   *perm = (const uint32_t*)W.spread.p;
   *lanes = out_lanes;
+  if (spread) *spread = true;
   return 0;
 }
 
@@ -1875,12 +1891,16 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   const bool pad = !ACS_AB_NO_PAD && B.cand && (uint64_t)B.n >= 32ull * B.cand_rows &&
                    (uint64_t)B.n < 256ull * B.cand_rows;
   size_t lanes = b->n;
-  if (batch_order(t, W, b, B, s, &perm, pad, &lanes) || spread_waves(t, W, s, &perm, &lanes)) return -1;
+  bool spread = false;
+  if (batch_order(t, W, b, B, s, &perm, pad, &lanes) || spread_waves(t, W, s, &perm, &lanes, &spread)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
+                          B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
+  else if (spread && ACS_K1_SPREAD_SKIPS)
+    ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN_SK, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   else
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN, grid, filter_lds_bytes(B), s, filter_form(B),
