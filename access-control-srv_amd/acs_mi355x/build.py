@@ -20,8 +20,11 @@ LIB = os.path.join(PKG, "lib", "libacs_mi355x.so")
 HOST_LIB = os.path.join(ROOT, "tests", "native", "libacs_core_host.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# host code (codec, compiler, validation): x86-64-v3 (AVX2 / BMI2 / POPCNT), which every EPYC host
+# of an MI355X and this build container have; ACS_HOST_ARCH="" builds baseline x86-64
+HOST_ARCH = [f"-march={a}" for a in [os.environ.get("ACS_HOST_ARCH", "x86-64-v3")] if a]
 
-_HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h", "acs_json.h")] + \
+_HEADERS = [os.path.join(CSRC, f) for f in ("acs_layout.h", "acs_eval.h", "acs_json.h", "acs_pool.h")] + \
     [os.path.join(ROOT, "include", "acs_mi355x.h")]
 # host-only C++ of the product library: the native request codec and its JSON reader
 _HOST_SRCS = [os.path.join(CSRC, f) for f in ("acs_codec.cpp", "acs_compiler.cpp", "acs_json.cpp", "acs_validate.cpp")]
@@ -41,7 +44,7 @@ def _hipcc(src, out, extra=(), host_srcs=()):
     objs = []
     for h in host_srcs:
         o = out + "." + os.path.basename(h) + ".o"
-        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread",
+        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread", *HOST_ARCH,
                         "-I", CSRC, "-I", os.path.join(ROOT, "include"), *extra, "-c", h, "-o", o], check=True)
         objs.append(o)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",

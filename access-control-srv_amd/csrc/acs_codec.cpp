@@ -41,6 +41,7 @@
 #include "../../include/acs_mi355x.h"
 #include "acs_json.h"
 #include "acs_layout.h"
+#include "acs_pool.h"
 
 extern "C" void acs_internal_set_error(const char* msg);
 // acs_kernels.hip: page-locked (portable) host memory when a device is present, else malloc
@@ -1134,8 +1135,25 @@ void Encoder::encode(uint32_t i, const char* p, const char* e) {
   }
 }
 
+#if defined(ACS_CODEC_TIMING)
+std::atomic<uint64_t> g_cyc_sect[8];
+#define SECT(k)                                            \
+  do {                                                     \
+    const uint64_t t_ = __builtin_ia32_rdtsc();            \
+    g_cyc_sect[k].fetch_add(t_ - t_sect_, std::memory_order_relaxed); \
+    t_sect_ = t_;                                          \
+  } while (0)
+#else
+#define SECT(k) \
+  do {          \
+  } while (0)
+#endif
+
 // encoder.py Encoder._encode_one, restated.
 void Encoder::encode_one(uint32_t i, const JV* req) {
+#if defined(ACS_CODEC_TIMING)
+  uint64_t t_sect_ = __builtin_ia32_rdtsc();
+#endif
   uint32_t flags = 0;
   if (req->t != J_OBJ) unsup("request is not an object");
   const JV* target = get(req, "target");
@@ -1199,6 +1217,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     unsup("hierarchical_scopes is not an array");
   }
   if (have_forest && forest.is_array) flags |= RQ_HRS_ITERABLE;
+  SECT(0);
 
   // ---- resources: kinds, ids, regex columns, suffixes, indexOf masks
   uint8_t kinds[QMAX] = {};
@@ -1305,6 +1324,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     q.slot_a = sa;
     q.slot_b = sb;
   }
+  SECT(1);
   for (auto& b : keys_b)  // HR map key shared by a resource id and an operation name
     for (auto& a : keys_a)
       if (a.first == b.first && a.second != b.second) unsup("resource-id / operation key collision in HR owners map");
@@ -1346,6 +1366,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     }
   }
   if (grants.size() / 3 > 255 || rolese.size() / 2 > 255) unsup("too many role scoping grants");
+  SECT(2);
 
   // ---- hierarchical_scopes: owner masks from the subject's forest (roots / keys above)
   auto masks_of = [&](const JV* v) -> uint64_t {
@@ -1404,6 +1425,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     }
   }
   flags |= acl_state << RQ_ACL_SHIFT;
+  SECT(3);
   if (na > 0) {
     const JV* a0 = &actions[0];
     if (eq_urn(get(a0, "id"), U_ACTID)) {
@@ -1465,6 +1487,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     }
   }
   if (tse.size() > 255) unsup("too many ACL scoping entities");
+  SECT(4);
   w[0] = (uint32_t)(grants.size() / 3) | (uint32_t)(rolese.size() / 2) << 8 | (uint32_t)slot_objs.size() << 16 |
          (uint32_t)roots.size() << 24;
   w[1] = (uint32_t)tse.size() | (uint32_t)hr_keys.size() << 8;
@@ -1504,6 +1527,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
       hints |= HINT_ACL_NONE;
     }
   }
+  SECT(5);
   ReqHdr h{};
   h.flags = flags;
   h.nres = (uint8_t)nr;
@@ -1543,6 +1567,7 @@ void Encoder::encode_one(uint32_t i, const JV* req) {
     for (uint32_t j = LINE_ACT; j < na; ++j) memcpy(d + g.act + 2 * (j - LINE_ACT), &ap[j], 8);
     for (uint32_t j = LINE_ROLES; j < n_ras; ++j) d[g.roles + (j - LINE_ROLES)] = roles[j];
   }
+  SECT(6);
 }
 
 }  // namespace
@@ -1860,10 +1885,7 @@ template <class F>
 void parallel_ranges(int threads, size_t n, F f) {
   int T = threads < 1 ? 1 : threads;
   if ((size_t)T > n / 4096 + 1) T = (int)(n / 4096 + 1);
-  std::vector<std::thread> pool;
-  for (int t = 1; t < T; ++t) pool.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
-  f(0, 0, n / T);
-  for (auto& th : pool) th.join();
+  acs_pool::run(T, [&](int t) { f(t, n * t / T, n * (t + 1) / T); });
 }
 
 // Open-addressing u64 -> u32 map (linear probing; key ~0 is reserved).
@@ -2059,10 +2081,8 @@ void Classes::run() {
         thr[c] = throw_row(c);
       }
     };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads && (size_t)t < items; ++t) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
+    acs_pool::run((int)std::min<size_t>((size_t)std::max(threads, 1), std::max<size_t>(items, 1)),
+                  [&](int) { work(); });
   };
   // the column part of a cache key: the entity value (a padding column: never a key)
   auto col_key = [&](uint32_t c) -> std::string {
@@ -2252,10 +2272,8 @@ void Classes::run() {
           verdicts(rows[m], pcol[i], a, r, nr, role_filter, action_filter, arow);
         }
       };
-      std::vector<std::thread> pool;
-      for (int t = 1; t < threads && (size_t)t < miss.size(); ++t) pool.emplace_back(work);
-      work();
-      for (auto& th : pool) th.join();
+      acs_pool::run((int)std::min<size_t>((size_t)std::max(threads, 1), std::max<size_t>(miss.size(), 1)),
+                    [&](int) { work(); });
       std::unique_lock<std::shared_mutex> lock(C.classes.mu);
       ClassCache& K = C.classes;
       if (K.bytes > ClassCache::MAX_BYTES) K.clear_locked();  // this batch holds its own references
@@ -2638,12 +2656,7 @@ std::vector<std::pair<const char*, const char*>> split_items(const char* p, cons
     lowest[t] = on.lo;
     commas[t] = std::move(on.out);  // (a thread-local vector: no shared cache line per push)
   };
-  auto run = [&](auto&& f) {
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T; ++t) pool.emplace_back(f, t);
-    f(0);
-    for (auto& th : pool) th.join();
-  };
+  auto run = [&](auto&& f) { acs_pool::run(T, [&](int t) { f(t); }); };
   run(pass1);
   uint64_t parity = 0;
   for (int t = 0; t < T; ++t) {
@@ -2717,17 +2730,13 @@ void coherence_order(acs_codec_batch& B, int threads) {
       lo = n * t / T;
       hi = n * (t + 1) / T;
     };
-    std::vector<std::thread> pool;
     auto hist = [&](int t) {
       size_t lo, hi;
       range(t, lo, hi);
       cnt[t].fill(0);
       for (size_t x = lo; x < hi; ++x) ++cnt[t][(key[x] >> sh) & 255u];
     };
-    for (int t = 1; t < T; ++t) pool.emplace_back(hist, t);
-    hist(0);
-    for (auto& th : pool) th.join();
-    pool.clear();
+    acs_pool::run(T, hist);
     size_t total = 0;
     bool constant = false;
     for (uint32_t d = 0; d < 256 && !constant; ++d) {
@@ -2752,9 +2761,7 @@ void coherence_order(acs_codec_batch& B, int threads) {
         idx2[at] = idx[x];
       }
     };
-    for (int t = 1; t < T; ++t) pool.emplace_back(scatter, t);
-    scatter(0);
-    for (auto& th : pool) th.join();
+    acs_pool::run(T, scatter);
     key.swap(key2);
     idx.swap(idx2);
   }
@@ -2844,12 +2851,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
       errs[t] = e.what();
     }
   };
-  {
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
-    work(0);
-    for (auto& th : pool) th.join();
-  }
+  acs_pool::run(T, work);
   for (auto& e : errs)
     if (!e.empty()) throw std::runtime_error(e);
   B->hr_hits = hits;
@@ -2893,10 +2895,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
         std::copy(col->begin(), col->end(), B->rx.begin() + k * B->rx_rows);
       }
     };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < T && (size_t)t < order.size(); ++t) pool.emplace_back(cells);
-    cells();
-    for (auto& th : pool) th.join();
+    acs_pool::run((int)std::min<size_t>((size_t)T, std::max<size_t>(order.size(), 1)), [&](int) { cells(); });
   }
   // RES_RX_SAFE on every entity attribute whose column holds no throwing / host cell (K1 may
   // then cut a combining loop short once its result is final: encoder.mark_rx_safe)
@@ -2919,7 +2918,6 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
   B->ext = (uint32_t*)B->ext_b.p;
   B->ext_words = ebase[T];
   {
-    std::vector<std::thread> pool;
     auto fix = [&](int t) {
       if (!arenas[t].empty()) memcpy(B->arena + abase[t], arenas[t].data(), arenas[t].size() * 4);
       if (!exts[t].empty()) memcpy(B->ext + ebase[t], exts[t].data(), exts[t].size() * 4);
@@ -2937,9 +2935,7 @@ acs_codec_batch* encode_items(acs_codec* c, const std::pair<const char*, const c
         }
       }
     };
-    for (int t = 1; t < T; ++t) pool.emplace_back(fix, t);
-    fix(0);
-    for (auto& th : pool) th.join();
+    acs_pool::run(T, fix);
   }
   const double t2 = now_s();
   Classes cl(*c, *B, T);
@@ -3029,6 +3025,7 @@ int acs_codec_set_subject_scopes(acs_codec* c, const char* key, size_t key_len, 
 int acs_internal_codec_cycles(uint64_t* parse, uint64_t* encode) {
   *parse = g_cyc_parse.exchange(0);
   *encode = g_cyc_encode.exchange(0);
+  for (int k = 0; k < 7; ++k) encode[1 + k] = g_cyc_sect[k].exchange(0);
   return 0;
 }
 #endif

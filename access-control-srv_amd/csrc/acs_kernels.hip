@@ -583,7 +583,7 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 // requests: K1 0.670 -> 0.578 ms with 32 lanes per wave, r05_e; whole 1M-request c3 chunks run
 // slower with the skips, r05_b)
 #ifndef ACS_K1_SK_WAVES_PER_EU
-#define ACS_K1_SK_WAVES_PER_EU ACS_K1_WAVES_PER_EU
+#define ACS_K1_SK_WAVES_PER_EU 4  // c3 131,072: 0.448 ms at 5, 0.437 at 4; 8,192: 0.373 vs 0.332 (r05_g)
 #endif
 template <class FL, bool CB, bool AN, bool SK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
@@ -653,31 +653,76 @@ struct LdsAcc {
   uint32_t* rec;
   __device__ void or_bits(uint32_t w, uint32_t bit) { atomicOr(rec + w, bit); }
 };
+// Requests per class row (a composed request counts for both of its rows).
+template <bool CB>
+__global__ __launch_bounds__(BLOCK) void class_count_kernel(Batch B, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= B.n) return;
+  const ReqLine* ln = lane_line<CB>(B, true, i);
+  const ReqHdr h = ln ? ln->h : B.hdr[i];
+  const uint32_t c1 = request_pcol(h), c2 = lane_cls2(ln, true);
+  if (c1 < B.cand_rows) atomicAdd(cnt + c1, 1u);
+  if (c2 && c2 - 1u < B.cand_rows) atomicAdd(cnt + c2 - 1u, 1u);
+}
+
+// cnt / min_reqs: a class row with fewer requests than min_reqs gets no template (its flags word
+// 0; its requests take the full walk) — a template costs about one wave's walk of the class's
+// candidate sets, and it saves per request (c4 at 131,072 requests: 13,725 classes, median 2
+// requests each)
+// LDS writes of this wave's lanes visible to its other lanes (waves that share no LDS)
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, TplLayout TL, BitsLayout BL,
+                                                             const uint32_t* __restrict__ cnt, uint32_t min_reqs,
                                                              uint32_t* __restrict__ out) {
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t c = blockIdx.x * (BLOCK / 64) + wave;
+  if (c >= B.cand_rows) return;  // the waves share no LDS: they sync alone (wave_sync)
+  if (cnt && cnt[c] < min_reqs) {
+    if (lane == 0) out[(size_t)c * TL.stride + TL.flags] = 0u;
+    return;
+  }
   uint32_t* rec = acs_dyn_lds + wave * TL.stride;
   for (uint32_t w = lane; w < TL.stride; w += 64) rec[w] = 0u;
-  __syncthreads();
+  wave_sync();
   bool ok = true, role_free = true;
-  if (c < B.cand_rows) {
+  {
+    // rounds of 64 candidate sets, all lanes at once: in round r lane j takes the row's set of
+    // rank 64 r + j.  The wave-uniform cursor (w, before) walks the row's words; a word that also
+    // holds ranks of the next round is read again then.  (Set by set, one lane active, the pass
+    // cost 5.0 ms at c4's 1M requests, r05_g.)
     const uint32_t* row = B.cand + (size_t)c * B.cand_words;
+    const uint32_t nw = (T.n_sets + 31u) / 32u;
     LdsAcc acc{rec};
-    uint32_t k = 0;  // rank of the candidate set among the row's
-    for (uint32_t w = 0; w < (T.n_sets + 31u) / 32u && ok; ++w)
-      for (uint32_t x = row[w]; x && ok; x &= x - 1u, ++k)
-        if ((k & 63u) == lane)
-          ok = wia_template_set(T, row, B.cand_wp, B.cand_wr, B.cand_wv, BL, TL, 32u * w + (uint32_t)__builtin_ctz(x),
-                                acc, &role_free);
+    uint32_t w = 0, before = 0;  // words consumed, candidate sets in them
+    for (uint32_t r0 = 0;; r0 += 64u) {
+      const uint32_t want = r0 + lane;
+      uint32_t set = 0xFFFFFFFFu;
+      for (; w < nw; ++w) {
+        uint32_t x = row[w];
+        const uint32_t pc = (uint32_t)__builtin_popcount(x);
+        if (want >= before && want < before + pc) {
+          for (uint32_t q = want - before; q; --q) x &= x - 1u;
+          set = 32u * w + (uint32_t)__builtin_ctz(x);
+        }
+        if (before + pc > r0 + 63u) break;  // the word holds next-round ranks too
+        before += pc;
+      }
+      if (!__ballot(set != 0xFFFFFFFFu)) break;
+      if (set != 0xFFFFFFFFu)
+        ok = wia_template_set(T, row, B.cand_wp, B.cand_wr, B.cand_wv, BL, TL, set, acc, &role_free);
+      if (__ballot(!ok)) break;  // the class is untemplated
+    }
   }
   const bool all_ok = __ballot(!ok) == 0, all_free = __ballot(!role_free) == 0;
-  __syncthreads();
-  if (c >= B.cand_rows) return;
+  wave_sync();
   const uint32_t ww = TL.exact - TL.work;
   for (uint32_t w = lane; w < ww; w += 64)
     if (rec[TL.work + w]) atomicOr(rec + TL.mask + (w >> 5), 1u << (w & 31u));
-  __syncthreads();
+  wave_sync();
   uint32_t* dst = out + (size_t)c * TL.stride;
   for (uint32_t w = lane; w < TL.stride; w += 64) {
     uint32_t v = all_ok ? rec[w] : 0u;
@@ -1058,9 +1103,11 @@ struct Workspace {
   DevBuf sort, img, out;
   DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
   DevBuf tpl;          // whatIsAllowed templates of the batch's class rows
+  DevBuf tcnt;         // requests per class row (the template pass skips the rare classes)
   DevBuf spread;       // a small batch's order spread over more waves (spread_waves)
   void release() {
     tpl.release();
+    tcnt.release();
     spread.release();
     sort.release();
     img.release();
@@ -1846,6 +1893,9 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 #ifndef ACS_K1_SPREAD_SKIPS
 #define ACS_K1_SPREAD_SKIPS 1  // 0: spread batches take K1's plain instantiation
 #endif
+#ifndef ACS_K1_SK_ALWAYS
+#define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
+#endif
 #ifndef ACS_SPREAD_PER_SIMD
 #define ACS_SPREAD_PER_SIMD 8  // 0: off (c3 131,072 requests: K1 0.814 ms unspread, 0.670 at 4, 0.543 at 8; r05_e)
 #endif
@@ -1899,7 +1949,7 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
-  else if (spread && ACS_K1_SPREAD_SKIPS)
+  else if ((spread || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN_SK, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   else
@@ -1932,6 +1982,9 @@ int acs_kernel_times(acs_tables* t, float* ms, int n) {
   return m;
 }
 
+#ifndef ACS_TPL_MIN_REQS
+#define ACS_TPL_MIN_REQS 32  // a class row takes a template for at least this many requests
+#endif
 static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
                                   uint32_t* obl_n, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
@@ -1951,8 +2004,20 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   if (use_tpl) {
     if (W.tpl.reserve((size_t)B.cand_rows * TL.stride * sizeof(uint32_t))) return -1;
     tpl = (const uint32_t*)W.tpl.p;
+    const uint32_t* cnt = nullptr;
+    if (ACS_TPL_MIN_REQS > 1) {
+      if (W.tcnt.reserve((size_t)B.cand_rows * sizeof(uint32_t))) return -1;
+      HIP_OK(hipMemsetAsync(W.tcnt.p, 0, (size_t)B.cand_rows * sizeof(uint32_t), s));
+      const dim3 g((unsigned)((B.n + BLOCK - 1) / BLOCK));
+      if (B.hdr == nullptr)
+        hipLaunchKernelGGL(class_count_kernel<true>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
+      else
+        hipLaunchKernelGGL(class_count_kernel<false>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
+      cnt = (const uint32_t*)W.tcnt.p;
+    }
     hipLaunchKernelGGL(wia_template_kernel, dim3((B.cand_rows + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK),
-                       (size_t)(BLOCK / 64) * TL.stride * 4, s, t->view, B, TL, BL, (uint32_t*)W.tpl.p);
+                       (size_t)(BLOCK / 64) * TL.stride * 4, s, t->view, B, TL, BL, cnt, (uint32_t)ACS_TPL_MIN_REQS,
+                       (uint32_t*)W.tpl.p);
   }
   ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, BL, bits,
                       obl, obl_n, (Decision*)out, tpl, TL);

@@ -17,6 +17,7 @@
 #include <thread>
 #include <vector>
 
+#include "acs_pool.h"
 #include "../../include/acs_mi355x.h"
 #include "acs_layout.h"
 
@@ -36,7 +37,7 @@ int bad(const char* what, size_t at) {
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 uint32_t words32(uint32_t n) { return (n + 31) >> 5; }
 
-// f(lo, hi) over [0, n) on up to 16 host threads (one per 64k items); returns the smallest item
+// f(lo, hi) over [0, n) on up to 16 host threads (acs_pool.h workers) (one per 64k items); returns the smallest item
 // index any call reported (f returns its first bad index, or n when none), so the error message
 // names the same request as a serial walk would.
 template <class F>
@@ -45,10 +46,7 @@ size_t parallel_first_bad(size_t n, F f) {
   T = T < 1 ? 1 : (T > 16 ? 16 : T);
   if (T > n / 65536 + 1) T = n / 65536 + 1;
   std::vector<size_t> bad(T, n);
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < T; ++t) th.emplace_back([&, t] { bad[t] = f(n * t / T, n * (t + 1) / T); });
-  bad[0] = f(0, n / T);
-  for (auto& x : th) x.join();
+  acs_pool::run((int)T, [&](int t) { bad[t] = f(n * t / T, n * (t + 1) / T); });
   size_t m = n;
   for (size_t b : bad) m = b < m ? b : m;
   return m;

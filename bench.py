@@ -303,11 +303,19 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
         for k, v in sb.hrs_forests(idx).items():
             codec.set_subject_scopes(k, v)
             registered += 1
-    pipe = Pipeline(tables, codec, threads=threads, chunk=131072)
-    pipe.is_allowed(text, n)  # warm: HR forests, class rows, regex columns, page-locked blocks
-    dec, st = pipe.is_allowed(text, n)
-    same = bool(np.array_equal(dec.view(np.uint64), dec_resident[idx].view(np.uint64)))
-    pipe.close()
+    # chunk sizes: the device work of a chunk is ~1/20 of its encode (c3), so the overlap hides
+    # little and each chunk repeats per-batch codec work (class keys, thread-local string and
+    # forest caches); the larger chunk is reported when it is faster
+    by_chunk, st, same = {}, None, True
+    for chunk in (131072, 262144):
+        pipe = Pipeline(tables, codec, threads=threads, chunk=chunk)
+        pipe.is_allowed(text, n)  # warm: HR forests, class rows, regex columns, page-locked blocks
+        dec, s1 = pipe.is_allowed(text, n)
+        same = same and bool(np.array_equal(dec.view(np.uint64), dec_resident[idx].view(np.uint64)))
+        pipe.close()
+        by_chunk[chunk] = n / s1["total_s"]
+        if st is None or s1["total_s"] < st["total_s"]:
+            st, best_chunk = s1, chunk
     # sequential: one encode call, then acs_is_allowed on its (compact, page-locked) buffers
     t0 = time.perf_counter()
     b = codec.encode(text, threads=threads)
@@ -321,8 +329,9 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
     codec.close()
     return {"requests": n, "json_bytes": len(text), "json_bytes_per_request": len(text) / n,
             "json_generation_s": gen_s, "threads": threads,
-            "requests_per_s": n / st["total_s"],
-            "what": "JSON text -> acs_pipeline (delimit; per 131072-request chunk: native encode into page-locked "
+            "requests_per_s": n / st["total_s"], "chunk": best_chunk,
+            "requests_per_s_by_chunk": {str(k): v for k, v in by_chunk.items()},
+            "what": "JSON text -> acs_pipeline (delimit; per chunk: native encode into page-locked "
                     "blocks || upload + coherence sort + K1 + download of the previous chunk on a second stream) -> "
                     "decision records in host memory; codec caches warm (steady state)",
             "stages": {"total_s": st["total_s"], "split_s": st["split_s"], "encode_s": st["encode_s"],

@@ -248,6 +248,11 @@ extern "C" int acs_host_wia_templates(const void* blob, size_t n, const acs_req_
   return 0;
 }
 
+// acs_host_set_tpl_which(w): acs_host_what_is_allowed_tpl also sets w[i] = 1 for each request i
+// a template decided (tools: which waves keep a full-walk lane)
+static uint8_t* g_tpl_which = nullptr;
+extern "C" void acs_host_set_tpl_which(uint8_t* w) { g_tpl_which = w; }
+
 // whatIsAllowed from the templates where usable (tpl_usable), else the full walk: the outputs
 // of acs_host_what_is_allowed; *templated: how many requests took a template.
 extern "C" int acs_host_what_is_allowed_tpl(const void* blob, size_t n, const acs_req_batch* b, const uint32_t* tpl,
@@ -277,6 +282,7 @@ extern "C" int acs_host_what_is_allowed_tpl(const void* blob, size_t n, const ac
         std::memcpy(&out[i], &d, sizeof d);
         obl_n[i] = log.n;
         ++*templated;
+        if (g_tpl_which) g_tpl_which[i] = 1;
         continue;
       }
     }
