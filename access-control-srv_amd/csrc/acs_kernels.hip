@@ -579,9 +579,10 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 #define ACS_K1_AN_WAVES_PER_EU 4
 #endif
 // SK: the lanes skip the sets, policies and rules outside their own class rows (acs_eval.h
-// is_allowed_t) — the instantiation for spread small batches, whose waves mix classes (c3 131,072
-// requests: K1 0.670 -> 0.578 ms with 32 lanes per wave, r05_e; whole 1M-request c3 chunks run
-// slower with the skips, r05_b)
+// is_allowed_t) — the instantiation for batches whose waves mix classes: spread small batches and
+// batches without wave-aligned class runs (c3 131,072 requests: K1 0.670 -> 0.578 ms with 32
+// lanes per wave, r05_e; c3 524,288 unpadded 0.905 -> 0.790; c5 1M 8.64 -> 3.05 ms, r05_i).
+// Padded batches (one class per wave) keep the plain form (c3 1M: 0.770 vs 0.789 ms, r05_i)
 #ifndef ACS_K1_SK_WAVES_PER_EU
 #define ACS_K1_SK_WAVES_PER_EU 4  // c3 131,072: 0.448 ms at 5, 0.437 at 4; 8,192: 0.373 vs 0.332 (r05_g)
 #endif
@@ -655,7 +656,7 @@ struct LdsAcc {
 };
 // Requests per class row (a composed request counts for both of its rows).
 template <bool CB>
-__global__ __launch_bounds__(BLOCK) void class_count_kernel(Batch B, uint32_t* __restrict__ cnt) {
+__global__ __launch_bounds__(BLOCK) void tpl_count_kernel(Batch B, uint32_t* __restrict__ cnt) {
   const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
   if (i >= B.n) return;
   const ReqLine* ln = lane_line<CB>(B, true, i);
@@ -1897,7 +1898,9 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 #define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
 #endif
 #ifndef ACS_SPREAD_PER_SIMD
-#define ACS_SPREAD_PER_SIMD 8  // 0: off (c3 131,072 requests: K1 0.814 ms unspread, 0.670 at 4, 0.543 at 8; r05_e)
+// 0: off.  c3 131,072 requests: K1 0.814 ms unspread, 0.670 at 4, 0.543 at 8 (r05_e), 0.446 at 16
+// with the skips; 524,288: 0.905 at 8 (unspread), 0.658 at 16 (r05_g, r05_i)
+#define ACS_SPREAD_PER_SIMD 16
 #endif
 __global__ __launch_bounds__(BLOCK) void spread_perm_kernel(const uint32_t* __restrict__ in, uint32_t lanes, uint32_t L,
                                                             uint32_t out_lanes, uint32_t* __restrict__ out) {
@@ -1942,14 +1945,16 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
                    (uint64_t)B.n < 256ull * B.cand_rows;
   size_t lanes = b->n;
   bool spread = false;
-  if (batch_order(t, W, b, B, s, &perm, pad, &lanes) || spread_waves(t, W, s, &perm, &lanes, &spread)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
+  const bool padded = lanes > b->n;  // wave-aligned class runs (holes): one class per wave
+  if (spread_waves(t, W, s, &perm, &lanes, &spread)) return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
-  else if ((spread || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
+  else if ((spread || !padded || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN_SK, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   else
@@ -1983,7 +1988,11 @@ int acs_kernel_times(acs_tables* t, float* ms, int n) {
 }
 
 #ifndef ACS_TPL_MIN_REQS
-#define ACS_TPL_MIN_REQS 32  // a class row takes a template for at least this many requests
+// A/B: a class row takes a template only for at least this many requests (1: every row, no
+// count pass).  A threshold measured slower (c4 1M K2: 4.01 ms at 1, 8.75 at 32 and 128; 131k:
+// 1.78 / 2.72 ms; r05_i): most waves then hold a lane whose class (or second class) went
+// untemplated and pay the full walk besides
+#define ACS_TPL_MIN_REQS 1
 #endif
 static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
                                   uint32_t* obl_n, acs_decision* out, hipStream_t s) {
@@ -2010,9 +2019,9 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
       HIP_OK(hipMemsetAsync(W.tcnt.p, 0, (size_t)B.cand_rows * sizeof(uint32_t), s));
       const dim3 g((unsigned)((B.n + BLOCK - 1) / BLOCK));
       if (B.hdr == nullptr)
-        hipLaunchKernelGGL(class_count_kernel<true>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
+        hipLaunchKernelGGL(tpl_count_kernel<true>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
       else
-        hipLaunchKernelGGL(class_count_kernel<false>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
+        hipLaunchKernelGGL(tpl_count_kernel<false>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
       cnt = (const uint32_t*)W.tcnt.p;
     }
     hipLaunchKernelGGL(wia_template_kernel, dim3((B.cand_rows + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK),
