@@ -40,6 +40,9 @@ namespace acs {
 #ifndef ACS_OWN_SKIP
 #define ACS_OWN_SKIP 7  // the skips K1's SK instantiation takes (K1 launches it for mixed-class waves)
 #endif
+#ifndef ACS_WAVE_CLEAN_SKIP
+#define ACS_WAVE_CLEAN_SKIP 1  // K1: a wave below its deciding sets drops the clean sets by words
+#endif
 #ifndef ACS_K2_OWN_SKIP
 #define ACS_K2_OWN_SKIP 0  // K2's rule skip (what_is_allowed_t)
 #endif
@@ -82,7 +85,8 @@ enum ProfPhase { PH_TOTAL, PH_SET_TARGET, PH_POL_EXACT, PH_MULTI, PH_POL_TARGET,
 enum OpCount {
   OP_SET_ITER, OP_SET_SKIP, OP_SET_EVAL, OP_SET_EVENTS, OP_SET_TARGET, OP_P2A_ITER, OP_P2A_TM, OP_MULTI,
   OP_P2B_ITER, OP_P2B_TM, OP_P2B_HR, OP_RULE_LOOP, OP_RULE_ITER, OP_RULE_TM, OP_RULE_HR, OP_RULE_ACL,
-  OP_WORD, OP_V_LDS, OP_V_OWN, OP_V_OWN2, OP_ROWS, OP_ROWS2, OP_LANE_DONE, OP_N
+  OP_WORD, OP_V_LDS, OP_V_OWN, OP_V_OWN2, OP_ROWS, OP_ROWS2, OP_LANE_DONE,
+  OP_TPL_REQ, OP_TPL_WORD, OP_TPL_RULE, OP_TPL_TM, OP_TPL_HIT, OP_N
 };
 #if defined(ACS_OP_COUNT)
 __device__ unsigned long long acs_op_wave[OP_N], acs_op_lane[OP_N];
@@ -340,6 +344,15 @@ ACS_FN uint32_t wave_or(uint32_t x) {
 #endif
 }
 
+// Whether b holds on every ACTIVE lane of the wave.  Host build: b (one request).
+ACS_FN bool wave_all(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(!b) == 0;
+#else
+  return b;
+#endif
+}
+
 // General candidate filter (rows longer than the LDS row form takes, and the host build).
 // Each lane holds pointers to its own request's rows.  GPU: words below lds_n come from the
 // wave's OR row in LDS (built before any lane diverges); a later word is the OR of the
@@ -481,6 +494,7 @@ template <class FL>
 struct CandRangeRev {
   const FL& F;
   uint32_t off, b, lo, base, bits;  // lo: base of the word holding index b (the last word read)
+  const uint32_t* drop = nullptr;   // drop_clean: indices to leave out of every word from now on
   ACS_FN CandRangeRev(const FL& f, uint32_t section_off, uint32_t b_, uint32_t e)
       : F(f), off(section_off), b(b_), lo(b_ & ~31u), base(b_ & ~31u), bits(0) {
     if (b < e) {
@@ -502,7 +516,17 @@ struct CandRangeRev {
       if (base <= lo) return false;
       base -= 32;
       bits = F.word(off + (base >> 5));
+      if (drop) {
+        ACS_SCAN(4);
+        bits &= ~drop[wave_uniform(base >> 5)];
+      }
     }
+  }
+  // leave the indices set in `d` (a bit row over the range) out of the rest of the walk
+  ACS_FN void drop_clean(const uint32_t* d) {
+    drop = d;
+    ACS_SCAN(4);
+    bits &= ~d[wave_uniform(base >> 5)];
   }
 };
 
@@ -1358,6 +1382,14 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   bool have_ev = false;
   CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
+#if ACS_WAVE_CLEAN_SKIP
+  // Once every active lane of the wave is safe and below its deciding set (or an event), each
+  // skips the clean sets (NF_CLEAN): the walk then drops them a word at a time, from the event
+  // index's clean bits, instead of loading each one's record to find it clean (c3adv: 18 of the
+  // 22 useful sets a wave visits, r05_k)
+  const uint32_t* clean_rows = T.ev_index ? T.ev_index + event_index_clean_off(T.n_sets, T.n_pols, T.n_rules) : nullptr;
+  bool wave_below = clean_rows == nullptr;
+#endif
   uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // SK: the lane's own useful-set word last read
 #if ACS_CLEAN_BITS
   uint32_t clean_w = 0xFFFFFFFFu, clean_bits = 0;  // the event index's clean-set word last read
@@ -1415,6 +1447,12 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       last_set = s + 1;
     }
     if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN_BELOW)) break;
+#if ACS_WAVE_CLEAN_SKIP
+    if (!wave_below && wave_all((have_ev || last_set) && safe)) {
+      wave_below = true;
+      sets.drop_clean(clean_rows);
+    }
+#endif
   }
   ACS_OPC(OP_LANE_DONE);
   if (have_ev) return ev;
@@ -1823,17 +1861,23 @@ ACS_FN bool tpl_usable(const TplLayout& TL, const uint32_t* t1, const uint32_t* 
 // visited wave-uniformly (the union of the active lanes' work-word masks), a word's rules for the
 // lanes that hold them.  Returns false when a work rule throws: the caller re-runs the request
 // with the full walk (the row is then rewritten from scratch).
-template <class RQ>
+template <class RQ, class SINK>
 ACS_FN bool what_is_allowed_tpl(const RQ& R, const TplLayout& TL, const BitsLayout& BL, const uint32_t* t1,
-                                const uint32_t* t2, TplSink& sink, OblLog& obl) {
+                                const uint32_t* t2, SINK& sink, OblLog& obl) {
   const Tables& T = R.T;
   const uint32_t MW = (TL.flags - TL.mask);  // mask words (padded)
+  ACS_OPC(OP_TPL_REQ);
+#if defined(ACS_AB_TPL_NO_WORK)  // timing A/B only (wrong rows): the template copy alone
+  for (uint32_t k = 0; k < 0; ++k) {
+#else
   for (uint32_t k = 0; k < MW; ++k) {
+#endif
     ACS_SCAN(t2 ? 8 : 4);
     uint32_t u = wave_or(t1[TL.mask + k] | (t2 ? t2[TL.mask + k] : 0u));
     while (u) {
       const uint32_t w = wave_uniform(32u * k + (uint32_t)__builtin_ctz(u));
       u &= u - 1u;
+      ACS_OPC(OP_TPL_WORD);
       ACS_SCAN(t2 ? 16 : 4);
       uint32_t mine = t1[TL.work + w] & ~(t2 ? t2[BL.wr + w] : 0u);
       if (t2) mine |= t2[TL.work + w] & ~t1[BL.wr + w];
@@ -1841,11 +1885,14 @@ ACS_FN bool what_is_allowed_tpl(const RQ& R, const TplLayout& TL, const BitsLayo
       while (rest) {
         const uint32_t r = wave_uniform(32u * w + (uint32_t)__builtin_ctz(rest));
         rest &= rest - 1u;
+        ACS_OPC(OP_TPL_RULE);
         if (!((mine >> (r & 31u)) & 1u)) continue;
+        ACS_OPC(OP_TPL_TM);
         const NodeRec Q = rule_at(T, r);
         const tri m = target_match_retry(Q, R, Q.effect, true, &obl);
         if (m < 0) return false;
         if (m) {
+          ACS_OPC(OP_TPL_HIT);
           const uint32_t p = T.parents[r + T.n_pols], s = T.parents[p];
           sink.template set<0>(s >> 5, 1u << (s & 31u));
           sink.template set<1>(BL.wp + (p >> 5), 1u << (p & 31u));

@@ -582,7 +582,8 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 // is_allowed_t) — the instantiation for batches whose waves mix classes: spread small batches and
 // batches without wave-aligned class runs (c3 131,072 requests: K1 0.670 -> 0.578 ms with 32
 // lanes per wave, r05_e; c3 524,288 unpadded 0.905 -> 0.790; c5 1M 8.64 -> 3.05 ms, r05_i).
-// Padded batches (one class per wave) keep the plain form (c3 1M: 0.770 vs 0.789 ms, r05_i)
+// Batches of long class runs keep the plain form (c3 1M padded: 0.770 vs 0.789 ms, r05_i; c3 10M
+// unpadded, ~300 requests per class: 3.02 vs 3.10 ms, r05_j)
 #ifndef ACS_K1_SK_WAVES_PER_EU
 #define ACS_K1_SK_WAVES_PER_EU 4  // c3 131,072: 0.448 ms at 5, 0.437 at 4; 8,192: 0.373 vs 0.332 (r05_g)
 #endif
@@ -732,6 +733,17 @@ __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, 
   }
 }
 
+// A templated lane's work-rule bits, OR-ed into the row the wave wrote (device atomics; a bit
+// arrives at most once per matched rule)
+struct OrSink {
+  uint32_t* row;
+  template <int S> __device__ void set(uint32_t w, uint32_t bit) { atomicOr(row + w, bit); }
+  __device__ void finish() {}
+};
+#ifndef ACS_TPL_WAVE_COPY
+#define ACS_TPL_WAVE_COPY 1
+#endif
+
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
@@ -781,14 +793,42 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
     for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
   }
-  if (tpl && !done) {  // the class template(s) plus the work rules (acs_eval.h what_is_allowed_tpl)
+  if (tpl) {  // the class template(s) plus the work rules (acs_eval.h what_is_allowed_tpl)
     const uint32_t c1 = request_pcol(h), c2 = lane_cls2(ln, in);
-    const uint32_t* t1 = c1 < B.cand_rows ? tpl + (size_t)c1 * TL.stride : nullptr;
+    const uint32_t* t1 = !done && c1 < B.cand_rows ? tpl + (size_t)c1 * TL.stride : nullptr;
     const uint32_t* t2 = t1 && c2 && c2 - 1u < B.cand_rows ? tpl + (size_t)(c2 - 1u) * TL.stride : nullptr;
     const uint32_t* r1 = t1 ? B.cand + (size_t)c1 * B.cand_words : nullptr;
     const uint32_t* r2 = t2 ? B.cand + (size_t)(c2 - 1u) * B.cand_words : nullptr;
-    if (!(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags)) {
+    const bool usable = t1 && !(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags);
+#if ACS_TPL_WAVE_COPY
+    // The wave writes its templated lanes' rows one after the other, 16 B per lane per store
+    // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane ORs
+    // the bits its work rules add into its own row
+    const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
+    for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
+      const int j = __builtin_ctzll(m);
+      const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
+                     c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
+      uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)oj * BL.words);
+      const uint4* s1 = reinterpret_cast<const uint4*>(tpl + (size_t)c1j * TL.stride);
+      const uint4* s2 = c2j ? reinterpret_cast<const uint4*>(tpl + (size_t)(c2j - 1u) * TL.stride) : nullptr;
+      ACS_SCAN(16u * q4 * (s2 ? 2u : 1u));  // the template row(s); the row write is B_out
+      for (uint32_t q = lane; q < q4; q += 64u) {
+        uint4 v = s1[q];
+        if (s2) {
+          const uint4 u = s2[q];
+          v.x |= u.x; v.y |= u.y; v.z |= u.z; v.w |= u.w;
+        }
+        dst[q] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the rows are in L2 before the ORs
+    if (usable) {
+      OrSink sink{bits + (size_t)o * BL.words};
+#else
+    if (usable) {
       TplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
+#endif
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
       if (what_is_allowed_tpl(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), TL, BL, t1, t2, sink, log)) {
         if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
@@ -798,6 +838,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     }
   }
   if (__ballot(!done)) {  // the full walk (rewrites a failed template lane's whole row)
+#if ACS_TPL_WAVE_COPY
+    if (tpl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // a failed lane's ORs land first
+#endif
     const FL F = FilterMaker<FL>::make(B, !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                        lane_cls2(ln, in && !done), wave_lds_row(B));
     if (!done) {
@@ -1948,13 +1991,18 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
   const bool padded = lanes > b->n;  // wave-aligned class runs (holes): one class per wave
   if (spread_waves(t, W, s, &perm, &lanes, &spread)) return -1;
+  // waves that mix classes: spread, or unpadded with short class runs (< 256 requests per class
+  // row on average), or long rows (the general Filter form: a wave ORs its lanes' rule words)
+  const FilterForm form = filter_form(B);
+  const bool mixed = spread || (!padded && form != FilterForm::All &&
+                                (form == FilterForm::General || (uint64_t)b->n < 256ull * B.cand_rows));
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
-  else if ((spread || !padded || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
+  else if ((mixed || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN_SK, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   else

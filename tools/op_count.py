@@ -19,12 +19,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from acs_mi355x import build, compiler, native, store, synth  # noqa: E402
-from acs_mi355x.device import DeviceBatch, is_allowed_device  # noqa: E402
+from acs_mi355x.device import DeviceBatch, is_allowed_device, what_is_allowed_device  # noqa: E402
 from oracle.acs_oracle import FULL_URNS, DEFAULT_CAS  # noqa: E402
 
 OPS = ["set_iter", "set_skip", "set_eval", "set_events", "set_target", "p2a_iter", "p2a_tm", "multi", "p2b_iter",
        "p2b_tm", "p2b_hr", "rule_loop", "rule_iter", "rule_tm", "rule_hr", "rule_acl", "word", "v_lds", "v_own",
-       "v_own2", "rows", "rows2", "lane_done"]
+       "v_own2", "rows", "rows2", "lane_done", "tpl_req", "tpl_word", "tpl_rule", "tpl_tm", "tpl_hit"]
 
 
 def batch_for(kind, n):
@@ -47,7 +47,7 @@ def main():
     path = os.environ.get("ACS_OPCOUNT_LIB") or build.build_variant("opcount", ["ACS_OP_COUNT"])
     lib = native._declare(C.CDLL(path))
     lib.acs_op_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    cs, sb = batch_for(kind, n)
+    cs, sb = batch_for("c3" if kind == "c4" else kind, n)
     blob = compiler.store_blob(cs)
 
     class _T:  # the duck-typed tables handle device.py's launchers take
@@ -60,14 +60,18 @@ def main():
     db = DeviceBatch(sb.batch, 0, compact=True)
     acc = (C.c_ulonglong * (2 * len(OPS)))()
     lib.acs_op_read(acc, len(OPS))  # reset
-    is_allowed_device(t, db)
+    if kind == "c4":
+        what_is_allowed_device(t, db)
+    else:
+        is_allowed_device(t, db)
     torch.cuda.synchronize()
     lib.acs_op_read(acc, len(OPS))
     waves = np.array(acc[:len(OPS)], np.float64)
     lanes = np.array(acc[len(OPS):2 * len(OPS)], np.float64)
-    ew = max(waves[OPS.index("lane_done")], 1.0)  # waves that evaluated (reached the end of the walk)
+    # waves that evaluated (reached the end of the walk; c4: took the template path)
+    ew = max(waves[OPS.index("tpl_req" if kind == "c4" else "lane_done")], 1.0)
     res = {"config": kind, "requests": n, "evaluating_waves": int(ew),
-           "lanes_per_wave": float(lanes[OPS.index("lane_done")] / ew),
+           "lanes_per_wave": float(lanes[OPS.index("tpl_req" if kind == "c4" else "lane_done")] / ew),
            "per_wave": {o: float(waves[k] / ew) for k, o in enumerate(OPS)},
            "lanes_active": {o: float(lanes[k] / waves[k]) if waves[k] else 0.0 for k, o in enumerate(OPS)}}
     print(json.dumps(res))
