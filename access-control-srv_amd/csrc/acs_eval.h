@@ -1397,6 +1397,14 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       ACS_CLEAN_BITS && T.ev_index ? T.ev_index + event_index_clean_off(T.n_sets, T.n_pols, T.n_rules) : nullptr;
 #endif
   while (sets.next(s)) {
+#if ACS_WAVE_CLEAN_SKIP
+    // (at the top of the body: every lane still walking is active here — a lane that leaves an
+    // iteration early by `continue` would be missing from the vote further down)
+    if (!wave_below && wave_all((have_ev || last_set) && safe)) {
+      wave_below = true;
+      sets.drop_clean(clean_rows);
+    }
+#endif
 #if ACS_CLEAN_BITS
     // below the deciding set (or an event) only an event can change the record, and a clean set
     // cannot raise one for a safe request: skip it — from the event index's clean bits, without
@@ -1447,12 +1455,6 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
       last_set = s + 1;
     }
     if ((have_ev || last_set) && safe && (S.nflags & NF_CLEAN_BELOW)) break;
-#if ACS_WAVE_CLEAN_SKIP
-    if (!wave_below && wave_all((have_ev || last_set) && safe)) {
-      wave_below = true;
-      sets.drop_clean(clean_rows);
-    }
-#endif
   }
   ACS_OPC(OP_LANE_DONE);
   if (have_ev) return ev;
