@@ -532,6 +532,10 @@ struct acs_codec {
   std::unordered_map<uint64_t, std::shared_ptr<const std::vector<uint32_t>>> act_rows;      // pair -> [W]
   std::atomic<uint64_t> hr_hits{0}, hr_misses{0};
   int force_level = -1;  // tests only (acs_internal_codec_force_level): pin the class key level
+  // the largest batch whose level-0 keys (entity + roles + action) were given up (too many keys
+  // per request): a batch no larger starts at level 1 — keys per request only fall as batches
+  // grow (c3: level 0 was tried and dropped on every batch, ≈ 40 % of the class work)
+  std::atomic<uint32_t> level0_given_up{0};
   // recycled page-locked blocks of the batches' arrays (shared: a batch may be freed after its
   // codec, e.g. by a garbage collector that finalises both in either order)
   std::shared_ptr<HostPool> pool = std::make_shared<HostPool>();
@@ -1938,7 +1942,23 @@ class U64Map {
   size_t n_ = 0;
 };
 
+#if defined(ACS_CODEC_TIMING)
+std::atomic<uint64_t> g_cls_ns[8];
+#define CLS_T(k)                                                                          \
+  do {                                                                                    \
+    const auto t_ = std::chrono::steady_clock::now();                                     \
+    g_cls_ns[k] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_ - cls_t0_).count(); \
+    cls_t0_ = t_;                                                                         \
+  } while (0)
+#else
+#define CLS_T(k) \
+  do {           \
+  } while (0)
+#endif
 void Classes::run() {
+#if defined(ACS_CODEC_TIMING)
+  auto cls_t0_ = std::chrono::steady_clock::now();
+#endif
   const uint32_t n = B.n, W = C.W2;  // output rows: [S | P | useful S | useful P | R]
   const uint32_t ncols = B.rx_cols;
   B.cand_words = W;
@@ -1983,6 +2003,7 @@ void Classes::run() {
     }
     if (any) any_active = true;
   });
+  CLS_T(0);
   auto finish = [&](const std::vector<uint32_t>& cls) {
     parallel_ranges(threads, n, [&](int, size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
@@ -2040,6 +2061,7 @@ void Classes::run() {
       }
     });
   }
+  CLS_T(1);
   // per-batch inputs of a row computation, built only when some key misses the cache
   std::vector<std::shared_ptr<const Row>> ent, arow;
   std::vector<std::unique_ptr<Row>> thr;
@@ -2095,7 +2117,7 @@ void Classes::run() {
   // ORs, two required roles), 2 entity+action (+ role factor), 3 entity; tests pin one
   // (candidates.FORCE_LEVEL) through acs_internal_codec_force_level
   const int force = C.force_level;
-  const int first_level = force >= 0 && force <= 3 ? force : 0;
+  const int first_level = force >= 0 && force <= 3 ? force : (n <= C.level0_given_up.load() ? 1 : 0);
   const int last_level = force >= 0 && force <= 3 ? first_level + 1 : 4;
   const bool packable = C.role_ids.size() < 512;
   // requests with exactly two required roles (the composed level's second keys)
@@ -2212,10 +2234,23 @@ void Classes::run() {
       });
     }
     const size_t nk = key_first.size();
+    CLS_T(2);
+#if defined(ACS_CODEC_TIMING)
+    if (getenv("ACS_CLS_DEBUG")) fprintf(stderr, "level %d: n %u N %zu keys %zu over %d\n", level, n, N, nk, (int)over_limit);
+#endif
     // over the row budget; or joint keys covering fewer than 4 requests each (candidates.classes:
     // waves could not share them, and the rows would outweigh the requests)
-    if (over_limit || (level < 3 && (nk * W * 4 > KEY_ROW_BYTES || (level == 0 && force < 0 && 4 * nk > (size_t)n))))
+    auto give_up = [&] {  // (level 0 as the first choice: remember the batch size)
+      if (lv == 0 && force < 0) {
+        uint32_t v = C.level0_given_up.load();
+        while (v < n && !C.level0_given_up.compare_exchange_weak(v, n)) {
+        }
+      }
+    };
+    if (over_limit || (level < 3 && (nk * W * 4 > KEY_ROW_BYTES || (level == 0 && force < 0 && 4 * nk > (size_t)n)))) {
+      give_up();
       continue;
+    }
     // cache lookup by (level, entity value, action, roles); compute the misses in parallel
     std::vector<std::string> gkey(nk);
     std::vector<std::shared_ptr<const ClassEntry>> entry(nk);
@@ -2254,6 +2289,7 @@ void Classes::run() {
         if (!hit[k]) miss.push_back((uint32_t)k);
     }
     B.classes_new += (uint32_t)miss.size();
+    CLS_T(3);
     if (!miss.empty()) {
       prepare();
       std::vector<Row> rows(miss.size());
@@ -2310,11 +2346,15 @@ void Classes::run() {
       if (it.second) uent.push_back(entry[k].get());
       cls_of_key[k] = it.first->second;
     }
-    if (uent.size() > MAX_CLASSES && level < 3) continue;
+    if (uent.size() > MAX_CLASSES && level < 3) {
+      give_up();
+      continue;
+    }
     if (uent.size() > MAX_CLASSES) {
       acs_internal_set_error("acs_codec_encode: too many request classes");
       throw Unsup{"too many request classes"};
     }
+    CLS_T(4);
     std::vector<uint32_t> order(uent.size()), rank(uent.size());
     for (size_t u = 0; u < uent.size(); ++u) order[u] = (uint32_t)u;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return uent[a]->cost > uent[b]->cost; });
@@ -2343,6 +2383,7 @@ void Classes::run() {
       });
     }
     finish(cls);
+    CLS_T(5);
     if (role_filter || !have_roles) return;
     // role factor (candidates._role_factor): role-relaxed rows like the composed level's, one per
     // required role (and one for "no required role"; a request with more than two roles: one
@@ -3026,6 +3067,7 @@ int acs_internal_codec_cycles(uint64_t* parse, uint64_t* encode) {
   *parse = g_cyc_parse.exchange(0);
   *encode = g_cyc_encode.exchange(0);
   for (int k = 0; k < 7; ++k) encode[1 + k] = g_cyc_sect[k].exchange(0);
+  for (int k = 0; k < 6; ++k) encode[8 + k] = g_cls_ns[k].exchange(0);
   return 0;
 }
 #endif
