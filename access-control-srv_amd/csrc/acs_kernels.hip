@@ -733,12 +733,51 @@ __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, 
   }
 }
 
-// A templated lane's work-rule bits, OR-ed into the row the wave wrote (device atomics; a bit
-// arrives at most once per matched rule)
-struct OrSink {
-  uint32_t* row;
-  template <int S> __device__ void set(uint32_t w, uint32_t bit) { atomicOr(row + w, bit); }
-  __device__ void finish() {}
+// A templated lane's work-rule bits over the row the wave already wrote from the template(s):
+// as TplSink, each section's current 16-B chunk gathers bits in registers, but only a chunk that
+// got some is rewritten (template chunk(s) | bits); the lane is its row's only writer by then.
+// (Device atomics per bit measured slower: c4 1M K2 4.71 vs 4.05 ms, r05_n.)
+struct SparseTplSink {
+  uint4* row;
+  const uint4* t1;
+  const uint4* t2;
+  uint32_t cur[3];
+  uint4 buf[3];
+  __device__ SparseTplSink(uint32_t* r, const BitsLayout& L, const uint32_t* a, const uint32_t* b)
+      : row(reinterpret_cast<uint4*>(r)), t1(reinterpret_cast<const uint4*>(a)), t2(reinterpret_cast<const uint4*>(b)) {
+    cur[0] = 0;
+    cur[1] = L.wp >> 2;
+    cur[2] = L.wr >> 2;
+    for (int k = 0; k < 3; ++k) buf[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  template <int S> __device__ void flush() {
+    const uint4 b = buf[S];
+    if (!(b.x | b.y | b.z | b.w)) return;
+    uint4 v = t1[cur[S]];
+    if (t2) {
+      const uint4 u = t2[cur[S]];
+      v.x |= u.x; v.y |= u.y; v.z |= u.z; v.w |= u.w;
+    }
+    v.x |= b.x; v.y |= b.y; v.z |= b.z; v.w |= b.w;
+    row[cur[S]] = v;
+    buf[S] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  template <int S> __device__ void set(uint32_t w, uint32_t bit) {
+    const uint32_t c = w >> 2, q = w & 3u;
+    if (c != cur[S]) {
+      flush<S>();
+      cur[S] = c;
+    }
+    buf[S].x |= q == 0u ? bit : 0u;
+    buf[S].y |= q == 1u ? bit : 0u;
+    buf[S].z |= q == 2u ? bit : 0u;
+    buf[S].w |= q == 3u ? bit : 0u;
+  }
+  __device__ void finish() {
+    flush<0>();
+    flush<1>();
+    flush<2>();
+  }
 };
 #ifndef ACS_TPL_WAVE_COPY
 #define ACS_TPL_WAVE_COPY 1
@@ -802,8 +841,8 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     const bool usable = t1 && !(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags);
 #if ACS_TPL_WAVE_COPY
     // The wave writes its templated lanes' rows one after the other, 16 B per lane per store
-    // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane ORs
-    // the bits its work rules add into its own row
+    // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane
+    // rewrites the chunks of its own row that its work rules add bits to
     const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
     for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
       const int j = __builtin_ctzll(m);
@@ -822,9 +861,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
         dst[q] = v;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the rows are in L2 before the ORs
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the copy's stores land before the lanes' own
     if (usable) {
-      OrSink sink{bits + (size_t)o * BL.words};
+      SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
 #else
     if (usable) {
       TplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
@@ -839,7 +878,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
   }
   if (__ballot(!done)) {  // the full walk (rewrites a failed template lane's whole row)
 #if ACS_TPL_WAVE_COPY
-    if (tpl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // a failed lane's ORs land first
+    if (tpl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // a failed lane's chunks land first
 #endif
     const FL F = FilterMaker<FL>::make(B, !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                        lane_cls2(ln, in && !done), wave_lds_row(B));
