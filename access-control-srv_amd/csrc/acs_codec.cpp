@@ -485,7 +485,19 @@ struct ClassCache {
 struct acs_codec {
   // store image
   uint32_t S = 0, P = 0, R = 0, ws = 0, wp = 0, wr = 0, W = 0;
-  std::vector<NodeRec> nodes;  // sets | policies | rules
+  // sets | policies | rules (uninitialised storage: codec_load fills it, in parallel)
+  struct NodeTable {
+    std::unique_ptr<NodeRec[]> p;
+    size_t n = 0;
+    void alloc(size_t k) {
+      p.reset(new NodeRec[k]);
+      n = k;
+    }
+    NodeRec& operator[](size_t i) { return p[i]; }
+    const NodeRec& operator[](size_t i) const { return p[i]; }
+    NodeRec* data() { return p.get(); }
+    size_t size() const { return n; }
+  } nodes;
   std::vector<Pair> pairs;
   // dictionary
   std::string sbytes;
@@ -573,7 +585,33 @@ bool take(const uint8_t*& p, const uint8_t* e, std::vector<T>& out, size_t n, si
   return true;
 }
 
+// host threads for a store load (the pool's workers; at most 16)
+size_t load_threads() {
+#if defined(ACS_CODEC_TIMING)
+  if (const char* e = getenv("ACS_LOAD_THREADS")) return (size_t)atoi(e);
+#endif
+  const size_t h = std::thread::hardware_concurrency();
+  return h < 1 ? 1 : (h > 16 ? 16 : h);
+}
+
+#if defined(ACS_CODEC_TIMING)
+#define LOAD_T(name)                                                                                \
+  do {                                                                                              \
+    const auto t_ = std::chrono::steady_clock::now();                                               \
+    if (getenv("ACS_LOAD_DEBUG"))                                                                   \
+      fprintf(stderr, "codec_load %s %.1f ms\n", name,                                              \
+              std::chrono::duration<double, std::milli>(t_ - load_t0_).count());                   \
+    load_t0_ = t_;                                                                                  \
+  } while (0)
+#else
+#define LOAD_T(name) \
+  do {               \
+  } while (0)
+#endif
 bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err) {
+#if defined(ACS_CODEC_TIMING)
+  auto load_t0_ = std::chrono::steady_clock::now();
+#endif
   acs_blob_header h;
   if (!blob || n_bytes < sizeof h) return err = "blob too small", false;
   memcpy(&h, blob, sizeof h);
@@ -594,17 +632,30 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
   auto a16 = [](size_t x) { return (x + 15) & ~size_t(15); };
   const size_t nn = (size_t)c->S + c->P + c->R;
   if ((size_t)(e - p) < a16(nn * 64)) return err = "truncated node tables", false;
-  c->nodes.resize(nn);
-  memcpy(c->nodes.data(), p, c->S * 64);
-  p += a16(c->S * 64ull);
-  memcpy(c->nodes.data() + c->S, p, c->P * 64ull);
-  p += a16(c->P * 64ull);
-  memcpy(c->nodes.data() + c->S + c->P, p, c->R * 64ull);
-  p += a16(c->R * 64ull);
+  c->nodes.alloc(nn);
+  {  // the three sections, copied in 4-MB pieces over the pool (c5: 65 MB, page faults included)
+    const uint8_t* src[3] = {p, p + a16(c->S * 64ull), p + a16(c->S * 64ull) + a16(c->P * 64ull)};
+    uint8_t* dst[3] = {(uint8_t*)c->nodes.data(), (uint8_t*)(c->nodes.data() + c->S),
+                       (uint8_t*)(c->nodes.data() + c->S + c->P)};
+    const size_t len[3] = {c->S * 64ull, c->P * 64ull, c->R * 64ull};
+    constexpr size_t PIECE = size_t(4) << 20;
+    std::vector<std::array<size_t, 3>> pieces;  // (section, offset, bytes)
+    for (int k = 0; k < 3; ++k)
+      for (size_t o = 0; o < len[k]; o += PIECE) pieces.push_back({(size_t)k, o, std::min(PIECE, len[k] - o)});
+    std::atomic<size_t> next{0};
+    acs_pool::run((int)std::min<size_t>(load_threads(), std::max<size_t>(pieces.size(), 1)), [&](int) {
+      for (size_t x; (x = next.fetch_add(1)) < pieces.size();) {
+        const auto& q = pieces[x];
+        memcpy(dst[q[0]] + q[1], src[q[0]] + q[1], q[2]);
+      }
+    });
+    p = src[2] + a16(c->R * 64ull);
+  }
   p += a16(h.n_rres * 16ull);
   if ((size_t)(e - p) < h.n_pairs * 8ull) return err = "truncated pair pool", false;
   c->pairs.resize(h.n_pairs);
   if (h.n_pairs) memcpy(c->pairs.data(), p, h.n_pairs * 8ull);
+  LOAD_T("tables");
   // codec section
   p = base + off;
   e = p + len;
@@ -629,6 +680,7 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
   p += 4;
   if ((size_t)(e - p) < ecn) return err = "truncated codec section", false;
   c->ec_json.assign((const char*)p, ecn);
+  LOAD_T("sections");
   c->n_dict = n_str;
   c->dict = StrMap<uint32_t>(n_str);
   for (uint32_t i = ID_EMPTY; i < n_str; ++i) {
@@ -636,6 +688,7 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     const uint64_t h = fast_hash(v.data(), v.size());
     if (!c->dict.find(h, v)) c->dict.insert(h, v.data(), (uint32_t)v.size(), i);  // first id of a string
   }
+  LOAD_T("dict");
   for (int k = 0; k < U_COUNT; ++k) {
     c->urn[k] = urns[k];
     c->urn_s[k] = c->string_of(urns[k]);
@@ -646,6 +699,7 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     c->row_of_id.emplace(id, r);
     prepare_pattern(c->rx_pat[r], id <= ID_NULL, c->string_of(id));
   }
+  LOAD_T("rx");
   // candidate specs
   c->always_bits.assign(c->W, 0);
   std::vector<std::vector<uint32_t>> per_row(n_rx);
@@ -660,6 +714,7 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     c->row_ptr[r + 1] = c->row_ptr[r] + (uint32_t)per_row[r].size();
     c->row_nodes.insert(c->row_nodes.end(), per_row[r].begin(), per_row[r].end());
   }
+  LOAD_T("specs");
   // useful-section statics (candidates.useful_static)
   c->WV = 2 * c->ws + 2 * c->wp + c->wr;
   c->W2 = c->WV + 4 * c->wp + c->wr;
@@ -679,58 +734,91 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     for (uint32_t q = N.child_begin; q < N.child_end && q < c->P; ++q)
       if (c->nodes[c->S + q].nflags & NF_NULL) c->set_null[s] = 1;
   }
-  // role requirements (candidates.role_requirements) and action requirements
+  // role requirements (candidates.role_requirements), action requirements and the per-node
+  // bit rows, in parallel over pieces of whole words of each section (a word's bits belong to one
+  // piece; c5: 1M nodes, 150 -> ~30 ms)
+  LOAD_T("useful statics");
   c->node_role.assign(nn, -1);
   c->node_need_act.assign(nn, 0);
   std::vector<uint32_t> req_role(nn, NONE32);
-  for (uint32_t g = 0; g < nn; ++g) {
-    const NodeRec& N = c->nodes[g];
-    const bool tgt = (N.nflags & NF_HAS_TARGET) != 0;
-    if (tgt && (N.tflags & TF_SUBJ_ROLE) && !(N.tflags & TF_SUBJ_EMPTY)) {
-      req_role[g] = N.role;
-      c->role_ids.push_back(N.role);
-    }
-    c->node_need_act[g] = tgt && N.act_n > 0;
-  }
-  std::sort(c->role_ids.begin(), c->role_ids.end());
-  c->role_ids.erase(std::unique(c->role_ids.begin(), c->role_ids.end()), c->role_ids.end());
   c->tgt_bits.assign(c->W, 0);
   c->subj_empty_bits.assign(c->W, 0);
   c->subj_role_bits.assign(c->W, 0);
   c->need_act_bits.assign(c->W, 0);
-  for (uint32_t g = 0; g < nn; ++g) {
-    const NodeRec& N = c->nodes[g];
-    if (!(N.nflags & NF_HAS_TARGET)) continue;
-    const uint32_t w = c->node_word(g), b = c->node_bit(g);
-    c->tgt_bits[w] |= b;
-    if (N.tflags & TF_SUBJ_EMPTY) c->subj_empty_bits[w] |= b;
-    else if (N.tflags & TF_SUBJ_ROLE) c->subj_role_bits[w] |= b;
-    if (c->node_need_act[g]) c->need_act_bits[w] |= b;
-  }
-  for (uint32_t g = 0; g < nn; ++g)
-    if (c->node_need_act[g]) c->need_act_nodes.push_back(g);
   c->res_empty_p.assign(c->wp ? c->wp : 1, 0);
   c->ent_only_p.assign(c->wp ? c->wp : 1, 0);
   c->res_empty_r.assign(c->wr ? c->wr : 1, 0);
   c->ent_only_r.assign(c->wr ? c->wr : 1, 0);
-  for (uint32_t g = c->S; g < nn; ++g) {
-    const bool pol = g < c->S + c->P;
-    const uint32_t l = pol ? g - c->S : g - c->S - c->P;
-    const uint16_t tf = (uint16_t)c->nodes[g].tflags;
-    if (tf & TF_RES_EMPTY) (pol ? c->res_empty_p : c->res_empty_r)[l >> 5] |= 1u << (l & 31);
-    else if (tf & TF_RES_ENT_ONLY) (pol ? c->ent_only_p : c->ent_only_r)[l >> 5] |= 1u << (l & 31);
-  }
   c->norole_bits.assign(c->W, 0);
-  c->role_node_list.assign(c->role_ids.size(), {});
-  for (uint32_t g = 0; g < nn; ++g) {
-    if (req_role[g] == NONE32) {
-      c->norole_bits[c->node_word(g)] |= c->node_bit(g);
-    } else {
-      const int k = (int)(std::lower_bound(c->role_ids.begin(), c->role_ids.end(), req_role[g]) - c->role_ids.begin());
-      c->node_role[g] = k;
-      c->role_node_list[k].push_back(g);
-    }
+  std::vector<std::pair<uint32_t, uint32_t>> pieces;  // node ranges, word-aligned per section
+  {
+    const uint32_t sec[4] = {0, c->S, c->S + c->P, (uint32_t)nn};
+    for (int k = 0; k < 3; ++k)
+      for (uint32_t g = sec[k]; g < sec[k + 1]; g += 8192) pieces.push_back({g, std::min(sec[k + 1], g + 8192)});
   }
+  const int LT = (int)std::min<size_t>(load_threads(), std::max<size_t>(pieces.size(), 1));
+  std::vector<std::vector<uint32_t>> roles_t(LT);
+  LOAD_T("alloc");
+  {
+    std::atomic<size_t> next{0};
+    acs_pool::run(LT, [&](int t) {
+      std::vector<uint32_t>& mine = roles_t[t];
+      for (size_t x; (x = next.fetch_add(1)) < pieces.size();) {
+        for (uint32_t g = pieces[x].first; g < pieces[x].second; ++g) {
+          const NodeRec& N = c->nodes[g];
+          const bool tgt = (N.nflags & NF_HAS_TARGET) != 0;
+          if (tgt && (N.tflags & TF_SUBJ_ROLE) && !(N.tflags & TF_SUBJ_EMPTY)) {
+            req_role[g] = N.role;
+            if (std::find(mine.begin(), mine.end(), N.role) == mine.end()) mine.push_back(N.role);
+          }
+          c->node_need_act[g] = tgt && N.act_n > 0;
+          if (tgt) {
+            const uint32_t w = c->node_word(g), b = c->node_bit(g);
+            c->tgt_bits[w] |= b;
+            if (N.tflags & TF_SUBJ_EMPTY) c->subj_empty_bits[w] |= b;
+            else if (N.tflags & TF_SUBJ_ROLE) c->subj_role_bits[w] |= b;
+            if (c->node_need_act[g]) c->need_act_bits[w] |= b;
+          }
+          if (g >= c->S) {
+            const bool pol = g < c->S + c->P;
+            const uint32_t l = pol ? g - c->S : g - c->S - c->P;
+            const uint16_t tf = (uint16_t)N.tflags;
+            if (tf & TF_RES_EMPTY) (pol ? c->res_empty_p : c->res_empty_r)[l >> 5] |= 1u << (l & 31);
+            else if (tf & TF_RES_ENT_ONLY) (pol ? c->ent_only_p : c->ent_only_r)[l >> 5] |= 1u << (l & 31);
+          }
+        }
+      }
+    });
+  }
+#if defined(ACS_CODEC_TIMING)
+  if (getenv("ACS_LOAD_DEBUG")) {
+    size_t used = 0;
+    for (const auto& v : roles_t) used += !v.empty();
+    fprintf(stderr, "pass1: LT %d, threads with roles %zu, pieces %zu\n", LT, used, pieces.size());
+  }
+#endif
+  LOAD_T("pass1");
+  for (const auto& v : roles_t) c->role_ids.insert(c->role_ids.end(), v.begin(), v.end());
+  std::sort(c->role_ids.begin(), c->role_ids.end());
+  c->role_ids.erase(std::unique(c->role_ids.begin(), c->role_ids.end()), c->role_ids.end());
+  {
+    std::atomic<size_t> next{0};
+    acs_pool::run(LT, [&](int) {
+      for (size_t x; (x = next.fetch_add(1)) < pieces.size();)
+        for (uint32_t g = pieces[x].first; g < pieces[x].second; ++g) {
+          if (req_role[g] == NONE32) c->norole_bits[c->node_word(g)] |= c->node_bit(g);
+          else c->node_role[g] = (int)(std::lower_bound(c->role_ids.begin(), c->role_ids.end(), req_role[g]) -
+                                       c->role_ids.begin());
+        }
+    });
+  }
+  LOAD_T("pass2");
+  for (uint32_t g = 0; g < nn; ++g)
+    if (c->node_need_act[g]) c->need_act_nodes.push_back(g);
+  c->role_node_list.assign(c->role_ids.size(), {});
+  for (uint32_t g = 0; g < nn; ++g)
+    if (c->node_role[g] >= 0) c->role_node_list[c->node_role[g]].push_back(g);
+  LOAD_T("statics");
   return true;
 }
 
