@@ -35,6 +35,7 @@
 #include <string_view>
 #include <thread>
 #include <emmintrin.h>
+#include <sys/mman.h>
 #include <unordered_map>
 #include <vector>
 
@@ -486,15 +487,28 @@ struct acs_codec {
   // store image
   uint32_t S = 0, P = 0, R = 0, ws = 0, wp = 0, wr = 0, W = 0;
   // sets | policies | rules (uninitialised storage: codec_load fills it, in parallel)
+  // Large stores: 2-MB pages (MADV_HUGEPAGE) — a c5 load faulted in 65 MB of 4-KB pages, the
+  // kernel's page-fault path serialising the copy (~70 ms, no gain from more threads)
   struct NodeTable {
-    std::unique_ptr<NodeRec[]> p;
+    struct Free {
+      void operator()(NodeRec* q) const { free(q); }
+    };
+    std::unique_ptr<NodeRec, Free> p;
     size_t n = 0;
     void alloc(size_t k) {
-      p.reset(new NodeRec[k]);
+      const size_t huge = size_t(2) << 20, bytes = std::max<size_t>(k * sizeof(NodeRec), 64);
+      void* q = nullptr;
+      if (bytes >= huge) {
+        q = aligned_alloc(huge, (bytes + huge - 1) / huge * huge);
+        if (q) madvise(q, (bytes + huge - 1) / huge * huge, MADV_HUGEPAGE);
+      }
+      if (!q) q = malloc(bytes);
+      if (!q) throw std::bad_alloc();
+      p.reset((NodeRec*)q);
       n = k;
     }
-    NodeRec& operator[](size_t i) { return p[i]; }
-    const NodeRec& operator[](size_t i) const { return p[i]; }
+    NodeRec& operator[](size_t i) { return p.get()[i]; }
+    const NodeRec& operator[](size_t i) const { return p.get()[i]; }
     NodeRec* data() { return p.get(); }
     size_t size() const { return n; }
   } nodes;
@@ -763,13 +777,19 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
     std::atomic<size_t> next{0};
     acs_pool::run(LT, [&](int t) {
       std::vector<uint32_t>& mine = roles_t[t];
+      uint32_t seen[256];  // direct-mapped: roles this thread already listed
+      for (uint32_t& v : seen) v = NONE32;
       for (size_t x; (x = next.fetch_add(1)) < pieces.size();) {
         for (uint32_t g = pieces[x].first; g < pieces[x].second; ++g) {
           const NodeRec& N = c->nodes[g];
           const bool tgt = (N.nflags & NF_HAS_TARGET) != 0;
           if (tgt && (N.tflags & TF_SUBJ_ROLE) && !(N.tflags & TF_SUBJ_EMPTY)) {
             req_role[g] = N.role;
-            if (std::find(mine.begin(), mine.end(), N.role) == mine.end()) mine.push_back(N.role);
+            uint32_t& sl = seen[(N.role * 2654435761u) >> 24];
+            if (sl != N.role) {
+              sl = N.role;
+              if (std::find(mine.begin(), mine.end(), N.role) == mine.end()) mine.push_back(N.role);
+            }
           }
           c->node_need_act[g] = tgt && N.act_n > 0;
           if (tgt) {
