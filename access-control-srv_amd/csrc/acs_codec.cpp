@@ -824,11 +824,21 @@ bool codec_load(acs_codec* c, const void* blob, size_t n_bytes, std::string& err
   {
     std::atomic<size_t> next{0};
     acs_pool::run(LT, [&](int) {
+      uint32_t memo_role[256], memo_idx[256];  // direct-mapped role id -> row
+      for (uint32_t& v : memo_role) v = NONE32;
       for (size_t x; (x = next.fetch_add(1)) < pieces.size();)
         for (uint32_t g = pieces[x].first; g < pieces[x].second; ++g) {
-          if (req_role[g] == NONE32) c->norole_bits[c->node_word(g)] |= c->node_bit(g);
-          else c->node_role[g] = (int)(std::lower_bound(c->role_ids.begin(), c->role_ids.end(), req_role[g]) -
-                                       c->role_ids.begin());
+          const uint32_t r = req_role[g];
+          if (r == NONE32) {
+            c->norole_bits[c->node_word(g)] |= c->node_bit(g);
+            continue;
+          }
+          const uint32_t h = (r * 2654435761u) >> 24;
+          if (memo_role[h] != r) {
+            memo_role[h] = r;
+            memo_idx[h] = (uint32_t)(std::lower_bound(c->role_ids.begin(), c->role_ids.end(), r) - c->role_ids.begin());
+          }
+          c->node_role[g] = (int)memo_idx[h];
         }
     });
   }
