@@ -1976,6 +1976,9 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 #ifndef ACS_K1_SPREAD_SKIPS
 #define ACS_K1_SPREAD_SKIPS 1  // 0: spread batches take K1's plain instantiation
 #endif
+#ifndef ACS_SPREAD_MIN_L
+#define ACS_SPREAD_MIN_L 16  // fewest requests per spread wave
+#endif
 #ifndef ACS_K1_SK_ALWAYS
 #define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
 #endif
@@ -2004,7 +2007,7 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
   }
   const size_t cap = (size_t)t->simds * ACS_SPREAD_PER_SIMD;
   uint32_t L = 64;
-  while (L > 16 && (*lanes + L / 2 - 1) / (L / 2) <= cap) L /= 2;
+  while (L > ACS_SPREAD_MIN_L && (*lanes + L / 2 - 1) / (L / 2) <= cap) L /= 2;
   if (L == 64) return 0;
   const size_t out_lanes = (*lanes + L - 1) / L * 64;
   if (W.spread.reserve(out_lanes * sizeof(uint32_t))) return -1;
