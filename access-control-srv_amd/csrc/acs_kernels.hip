@@ -788,8 +788,13 @@ struct SparseTplSink {
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
 // K2 occupancy A/B (5/6/8 waves per SIMD: 96/80/64 VGPRs with spills) measured no gain on c4
 // (6.92-6.95 ms vs 6.62, r03_g): the compiler's own 4 waves/SIMD stay.
+#if defined(ACS_K2_WAVES_PER_EU)  // A/B only: K2's occupancy (default: the compiler's, 4 waves/SIMD)
+#define ACS_K2_ATTR __attribute__((amdgpu_waves_per_eu(ACS_K2_WAVES_PER_EU)))
+#else
+#define ACS_K2_ATTR
+#endif
 template <class FL, bool CB>
-__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                                 uint32_t lanes, BitsLayout BL,
                                                                 uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
@@ -1970,14 +1975,17 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 // Small batches: a batch of fewer waves than the device holds runs as long as its longest wave,
 // and short class runs make every wave mix several classes (it walks the union of their
 // candidates).  Such a batch is spread over more waves, L requests each (the rest holes), L the
-// smallest of 64 / 32 / 16 that keeps the waves within ACS_SPREAD_PER_SIMD per SIMD of the device:
+// smallest of 64 / 32 / ... / ACS_SPREAD_MIN_L that keeps the waves within ACS_SPREAD_PER_SIMD per
+// SIMD of the device:
 // each wave then holds fewer classes (profiles/r05_a: at 131,072 c3 requests every wave lasts
 // about as long as the launch).
 #ifndef ACS_K1_SPREAD_SKIPS
 #define ACS_K1_SPREAD_SKIPS 1  // 0: spread batches take K1's plain instantiation
 #endif
 #ifndef ACS_SPREAD_MIN_L
-#define ACS_SPREAD_MIN_L 16  // fewest requests per spread wave
+// fewest requests per spread wave: c3 K1 at 131,072 / 32,768 / 4,096 requests 0.432 / 0.348 /
+// 0.353 ms at 16, 0.390 / 0.276 / 0.236 at 8, 0.390 / 0.283 / 0.168 at 4 (r05_final/ab_c3_*)
+#define ACS_SPREAD_MIN_L 4
 #endif
 #ifndef ACS_K1_SK_ALWAYS
 #define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
