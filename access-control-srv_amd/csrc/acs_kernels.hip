@@ -1144,6 +1144,7 @@ FilterForm filter_form(const Batch& B) {
 #define ACS_TARGS_ACL_NONE , true
 #define ACS_TARGS_ACL_PLAIN , false
 #define ACS_TARGS_ACL_PLAIN_SK , false, true
+#define ACS_TARGS_ACL_NONE_SK , true, true
 #define ACS_LAUNCH_FILTERED(kernel, ...) ACS_LAUNCH_FILTERED_X(kernel, ACS_TARGS_NONE, __VA_ARGS__)
 #define ACS_LAUNCH_FILTERED_X(kernel, X, grid, lds, stream, form, compact, ...)                           \
   do {                                                                                                  \
@@ -1987,6 +1988,9 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 // 0.353 ms at 16, 0.390 / 0.276 / 0.236 at 8, 0.390 / 0.283 / 0.168 at 4 (r05_final/ab_c3_*)
 #define ACS_SPREAD_MIN_L 4
 #endif
+#ifndef ACS_K1_AN_SK
+#define ACS_K1_AN_SK 0  // A/B: the own-row skips also in the ACL_NONE instantiation
+#endif
 #ifndef ACS_K1_SK_ALWAYS
 #define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
 #endif
@@ -2049,6 +2053,12 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
+#if ACS_K1_AN_SK
+  if ((b->hints & ACS_HINT_ACL_NONE) && mixed)
+    ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE_SK, grid, filter_lds_bytes(B), s, filter_form(B),
+                          B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
+  else
+#endif
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
