@@ -1988,8 +1988,11 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 // 0.353 ms at 16, 0.390 / 0.276 / 0.236 at 8, 0.390 / 0.283 / 0.168 at 4 (r05_final/ab_c3_*)
 #define ACS_SPREAD_MIN_L 4
 #endif
+#ifndef ACS_K2_SPREAD_MIN_L
+#define ACS_K2_SPREAD_MIN_L 16  // K2 (c4 131,072: 1.683 ms at 16, 1.875 at 8; r05_o, r05_u)
+#endif
 #ifndef ACS_K1_AN_SK
-#define ACS_K1_AN_SK 0  // A/B: the own-row skips also in the ACL_NONE instantiation
+#define ACS_K1_AN_SK 0  // A/B: the skips in the ACL_NONE instantiation (c3adv 1M 1.773 vs 1.782 ms, r05_u)
 #endif
 #ifndef ACS_K1_SK_ALWAYS
 #define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
@@ -2009,7 +2012,7 @@ __global__ __launch_bounds__(BLOCK) void spread_perm_kernel(const uint32_t* __re
 
 // *spread: set when the batch was spread (its waves hold fewer than 64 requests)
 static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32_t** perm, size_t* lanes,
-                        bool* spread = nullptr) {
+                        uint32_t min_l, bool* spread = nullptr) {
   if (spread) *spread = false;
   if (!ACS_SPREAD_PER_SIMD || !t->sort) return 0;
   if (!t->simds) {
@@ -2019,7 +2022,7 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
   }
   const size_t cap = (size_t)t->simds * ACS_SPREAD_PER_SIMD;
   uint32_t L = 64;
-  while (L > ACS_SPREAD_MIN_L && (*lanes + L / 2 - 1) / (L / 2) <= cap) L /= 2;
+  while (L > min_l && (*lanes + L / 2 - 1) / (L / 2) <= cap) L /= 2;
   if (L == 64) return 0;
   const size_t out_lanes = (*lanes + L - 1) / L * 64;
   if (W.spread.reserve(out_lanes * sizeof(uint32_t))) return -1;
@@ -2044,7 +2047,7 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   bool spread = false;
   if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
   const bool padded = lanes > b->n;  // wave-aligned class runs (holes): one class per wave
-  if (spread_waves(t, W, s, &perm, &lanes, &spread)) return -1;
+  if (spread_waves(t, W, s, &perm, &lanes, ACS_SPREAD_MIN_L, &spread)) return -1;
   // waves that mix classes: spread, or unpadded with short class runs (< 256 requests per class
   // row on average), or long rows (the general Filter form: a wave ORs its lanes' rule words)
   const FilterForm form = filter_form(B);
@@ -2107,7 +2110,9 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
   size_t lanes = b->n;
-  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes) || spread_waves(t, W, s, &perm, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes) ||
+      spread_waves(t, W, s, &perm, &lanes, ACS_K2_SPREAD_MIN_L))
+    return -1;
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
