@@ -305,9 +305,9 @@ def end_to_end(kind, cs, sb, tables, dec_resident, n_e2e, threads):
             registered += 1
     # chunk sizes: the device work of a chunk is ~1/20 of its encode (c3), so the overlap hides
     # little and each chunk repeats per-batch codec work (class keys, thread-local string and
-    # forest caches); the larger chunk is reported when it is faster
+    # forest caches); the fastest chunk size is reported, every one in requests_per_s_by_chunk
     by_chunk, st, same = {}, None, True
-    for chunk in (131072, 262144):
+    for chunk in (131072, 262144, 524288):
         pipe = Pipeline(tables, codec, threads=threads, chunk=chunk)
         pipe.is_allowed(text, n)  # warm: HR forests, class rows, regex columns, page-locked blocks
         dec, s1 = pipe.is_allowed(text, n)
