@@ -2045,6 +2045,11 @@ class U64Map {
     h ^= h >> 33;
     return h;
   }
+
+ public:
+  static uint64_t mixed(uint64_t h) { return mix(h); }
+
+ private:
   void grow() {
     std::vector<uint64_t> k(std::move(k_));
     std::vector<uint32_t> v(std::move(v_));
@@ -2323,11 +2328,61 @@ void Classes::run() {
           }
         }
       });
-      // merge: thread-local key index -> global key index
+      // merge: thread-local key index -> global key index, global keys in order of first
+      // appearance (the first thread's range first: every thread's keys are in item order)
       std::vector<std::vector<uint32_t>> remap(T);
+      if (pack_ok && T > 1) {
+        // over the threads: keys split into T partitions by hash; partition p merges its keys
+        // thread after thread, recording each new key's first item; the global order is the
+        // sort by first item — the serial merge's order exactly
+        const int Pn = T;
+        auto part = [&](uint64_t k) { return (int)((U64Map::mixed(k) >> 32) % (uint64_t)Pn); };
+        std::vector<std::vector<std::vector<uint32_t>>> fb(T, std::vector<std::vector<uint32_t>>(Pn));
+        acs_pool::run(T, [&](int t) {
+          for (uint32_t k = 0; k < firsts[t].size(); ++k) fb[t][part(kv(firsts[t][k]))].push_back(k);
+        });
+        std::vector<U64Map> pm;
+        for (int q = 0; q < Pn; ++q) pm.emplace_back(1024);
+        std::vector<std::vector<uint32_t>> pfirst(Pn);  // partition key j -> its first item
+        acs_pool::run(Pn, [&](int q) {
+          bool ins;
+          for (int t = 0; t < T; ++t)
+            for (const uint32_t k : fb[t][q]) {
+              const uint32_t x = firsts[t][k];
+              pm[q].get_or_put(kv(x), (uint32_t)pfirst[q].size(), &ins);
+              if (ins) pfirst[q].push_back(x);
+            }
+        });
+        size_t total = 0;
+        for (const auto& v : pfirst) total += v.size();
+        over_limit = total > key_limit;
+        if (!over_limit) {
+          std::vector<std::pair<uint32_t, uint32_t>> ord;  // (first item, partition << 24 | j)
+          ord.reserve(total);
+          for (int q = 0; q < Pn; ++q)
+            for (uint32_t j = 0; j < pfirst[q].size(); ++j) ord.push_back({pfirst[q][j], (uint32_t)q << 24 | j});
+          std::sort(ord.begin(), ord.end());
+          std::vector<std::vector<uint32_t>> gid(Pn);
+          for (int q = 0; q < Pn; ++q) gid[q].resize(pfirst[q].size());
+          key_first.resize(total);
+          for (uint32_t g = 0; g < total; ++g) {
+            key_first[g] = ord[g].first;
+            gid[ord[g].second >> 24][ord[g].second & 0xFFFFFFu] = g;
+          }
+          acs_pool::run(T, [&](int t) {
+            bool ins;
+            remap[t].resize(firsts[t].size());
+            for (uint32_t k = 0; k < firsts[t].size(); ++k) {
+              const uint64_t key = kv(firsts[t][k]);
+              const int q = part(key);
+              remap[t][k] = gid[q][pm[q].get_or_put(key, 0u, &ins)];
+            }
+          });
+        }
+      }
       U64Map gm(4096);
       std::unordered_map<std::string, uint32_t> gs;
-      for (int t = 0; t < T && !over_limit; ++t) {
+      for (int t = 0; t < T && !over_limit && !(pack_ok && T > 1); ++t) {
         remap[t].resize(firsts[t].size());
         for (size_t k = 0; k < firsts[t].size() && !over_limit; ++k) {
           const uint32_t x = firsts[t][k];
