@@ -386,6 +386,44 @@ constexpr uint32_t LDS_FILTER_WORDS = 1024;
 // OR the second class rows of the wave's composed lanes (ReqLine.cls2 = c2, 1 + class) into
 // its LDS row, words [0, LW); *any: the wave holds a composed lane.  False when one names a row
 // outside the batch (the wave then runs unfiltered).
+// lds[w] |= row[w] for w = lane, lane + 64, ... < LW: eight loads in flight per lane before the
+// ORs (the rolled loop waited on each load in turn)
+#ifndef ACS_ROW_UNROLL
+#define ACS_ROW_UNROLL 1
+#endif
+__device__ inline void lds_or_row(uint32_t* lds, const uint32_t* __restrict__ row, uint32_t LW, uint32_t lane) {
+  uint32_t w = lane;
+#if ACS_ROW_UNROLL
+  for (; w + 7u * 64u < LW; w += 8u * 64u) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = row[w + 64u * k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lds[w + 64u * k] |= v[k];
+  }
+#endif
+  for (; w < LW; w += 64u) lds[w] |= row[w];
+}
+
+// the same with the row AND-ed with a role-factor row (or the OR of two)
+__device__ inline void lds_or_row_roles(uint32_t* lds, const uint32_t* __restrict__ row, const uint32_t* q1,
+                                        const uint32_t* q2, uint32_t LW, uint32_t lane) {
+  uint32_t w = lane;
+#if ACS_ROW_UNROLL
+  for (; w + 3u * 64u < LW; w += 4u * 64u) {
+    uint32_t v[4], m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = row[w + 64u * k];
+      m[k] = role_word(q1, q2, w + 64u * k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds[w + 64u * k] |= v[k] & m[k];
+  }
+#endif
+  for (; w < LW; w += 64u) lds[w] |= row[w] & role_word(q1, q2, w);
+}
+
 __device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, uint32_t* lds, uint32_t LW, bool* any) {
   const uint32_t lane = threadIdx.x & 63u, W = B.cand_words;
   uint64_t pending = __ballot(valid && c2 != 0u);
@@ -395,7 +433,7 @@ __device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, u
     const uint32_t k = __builtin_amdgcn_readlane(c2, leader);
     if (k - 1u >= B.cand_rows) return false;
     const uint32_t* row = B.cand + (size_t)(k - 1u) * W;
-    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w];
+    lds_or_row(lds, row, LW, lane);
     ACS_SCAN(LW * 4u);
     ACS_OPC(OP_ROWS2);
     pending &= ~__ballot(valid && c2 == k);
@@ -447,7 +485,10 @@ __device__ inline Filter wave_filter(const Batch& B, bool valid, uint32_t cls, u
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t *q1 = nullptr, *q2 = nullptr;
     if (r != NO_ROLE_KEY) role_rows_of(B, r, &q1, &q2);
-    for (uint32_t w = lane; w < LW; w += 64) lds[w] |= row[w] & role_word(q1, q2, w);
+    if (q1)
+      lds_or_row_roles(lds, row, q1, q2, LW, lane);
+    else
+      lds_or_row(lds, row, LW, lane);
     ACS_SCAN(LW * (q1 ? (q2 ? 12u : 8u) : 4u));
     pending &= ~__ballot(valid && cls == c && rkey == r);
   }
@@ -480,7 +521,10 @@ __device__ inline FilterLds wave_filter_lds(const Batch& B, bool valid, uint32_t
     const uint32_t* row = B.cand + (size_t)c * W;
     const uint32_t *q1 = nullptr, *q2 = nullptr;
     if (r != NO_ROLE_KEY) role_rows_of(B, r, &q1, &q2);
-    for (uint32_t w = lane; w < W; w += 64) lds[w] |= row[w] & role_word(q1, q2, w);
+    if (q1)
+      lds_or_row_roles(lds, row, q1, q2, W, lane);
+    else
+      lds_or_row(lds, row, W, lane);
     ACS_SCAN(W * (q1 ? (q2 ? 12u : 8u) : 4u));
     ACS_OPC(OP_ROWS);
     if (c != first_cls) {
