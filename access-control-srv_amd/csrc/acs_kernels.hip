@@ -386,10 +386,11 @@ constexpr uint32_t LDS_FILTER_WORDS = 1024;
 // OR the second class rows of the wave's composed lanes (ReqLine.cls2 = c2, 1 + class) into
 // its LDS row, words [0, LW); *any: the wave holds a composed lane.  False when one names a row
 // outside the batch (the wave then runs unfiltered).
-// lds[w] |= row[w] for w = lane, lane + 64, ... < LW: eight loads in flight per lane before the
-// ORs (the rolled loop waited on each load in turn)
+// lds[w] |= row[w] for w = lane, lane + 64, ... < LW.  ACS_ROW_UNROLL (A/B, off): eight loads in
+// flight per lane before the ORs — slower (c3 10M K1 3.08 vs 2.93 ms, c3 131,072 0.387 vs 0.368;
+// c5 1M 3.00 vs 3.03, c4 equal; r05_x)
 #ifndef ACS_ROW_UNROLL
-#define ACS_ROW_UNROLL 1
+#define ACS_ROW_UNROLL 0
 #endif
 __device__ inline void lds_or_row(uint32_t* lds, const uint32_t* __restrict__ row, uint32_t LW, uint32_t lane) {
   uint32_t w = lane;
