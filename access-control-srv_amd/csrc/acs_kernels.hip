@@ -613,6 +613,45 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
   return CB ? B.lines + i : (in && B.lines ? B.lines + i : nullptr);  // one gather for the first rows
 }
 
+#ifndef ACS_NT_LINES
+#define ACS_NT_LINES 0
+#endif
+
+// A 16-B record read once (request line parts): A/B ACS_NT_LINES reads it non-temporally, so
+// the streamed lines do not displace the tables and class rows in L2
+template <class T16>
+__device__ inline T16 line_load(const T16* p) {
+  static_assert(sizeof(T16) == 16, "16-B record");
+#if ACS_NT_LINES
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  T16 out;
+  __builtin_memcpy(&out, &v, 16);
+  return out;
+#else
+  return *p;
+#endif
+}
+// The tile a block takes.  Blocks reach the 8 XCDs round-robin (block b on XCD b % 8), so
+// neighbouring tiles of the coherence order — the same classes, the same table nodes — would
+// land on eight different L2s.  ACS_XCD_GROUP = G (A/B; 0: identity) gives each XCD runs of G
+// consecutive tiles, the runs interleaved over the XCDs (load stays balanced, unlike whole
+// XCD-contiguous ranges, r04_j); the tail beyond the last full 8·G tiles keeps the identity.
+#ifndef ACS_XCD_GROUP
+#define ACS_XCD_GROUP 0
+#endif
+__device__ inline uint32_t xcd_tile(uint32_t b, uint32_t nb) {
+#if ACS_XCD_GROUP
+  constexpr uint32_t G = ACS_XCD_GROUP, SPAN = 8u * G;
+  if (b >= nb / SPAN * SPAN) return b;
+  const uint32_t x = b & 7u, i = b >> 3;
+  return (i / G) * SPAN + x * G + (i % G);
+#else
+  (void)nb;
+  return b;
+#endif
+}
+
 // 1 + the lane's second class (composed class rows; 0: none)
 __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && ln ? ln->cls2 : 0u; }
 
@@ -637,13 +676,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
   const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
-  if (in) h = ln ? ln->h : B.hdr[i];
+  if (in) h = ln ? line_load(&ln->h) : B.hdr[i];
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
@@ -668,7 +707,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? line_load(&ln->res[j]) : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
     const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
     d = is_allowed_t<AN, SK>(R, F);
@@ -847,7 +886,7 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
                                                                 Decision* __restrict__ out,
                                                                 const uint32_t* __restrict__ tpl, TplLayout TL) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
