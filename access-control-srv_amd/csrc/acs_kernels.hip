@@ -614,7 +614,7 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
 }
 
 #ifndef ACS_NT_LINES
-#define ACS_NT_LINES 0
+#define ACS_NT_LINES 0  // A/B (off): slower, c3 10M K1 3.125 vs 2.930 ms, c5 3.115 vs 2.999 (r05_y)
 #endif
 
 // A 16-B record read once (request line parts): A/B ACS_NT_LINES reads it non-temporally, so
@@ -634,22 +634,28 @@ __device__ inline T16 line_load(const T16* p) {
 }
 // The tile a block takes.  Blocks reach the 8 XCDs round-robin (block b on XCD b % 8), so
 // neighbouring tiles of the coherence order — the same classes, the same table nodes — would
-// land on eight different L2s.  ACS_XCD_GROUP = G (A/B; 0: identity) gives each XCD runs of G
-// consecutive tiles, the runs interleaved over the XCDs (load stays balanced, unlike whole
-// XCD-contiguous ranges, r04_j); the tail beyond the last full 8·G tiles keeps the identity.
-#ifndef ACS_XCD_GROUP
-#define ACS_XCD_GROUP 0
+// land on eight different L2s.  G > 0 gives each XCD runs of G consecutive tiles, the runs
+// interleaved over the XCDs (load stays balanced, unlike whole XCD-contiguous ranges, r04_j);
+// the tail beyond the last full 8·G tiles keeps the identity.  Same-call A/B (r05_y): K1 with
+// G = 16 c3 10M 2.886 vs 2.930 ms (c5, c3adv equal; G = 4 / 64: 2.937 / 2.935); K2 slower with
+// any G (c4 4.14 vs 4.02 at 16), so it keeps the identity.
+#ifndef ACS_XCD_GROUP_K1
+#define ACS_XCD_GROUP_K1 16
 #endif
+#ifndef ACS_XCD_GROUP_K2
+#define ACS_XCD_GROUP_K2 0
+#endif
+template <uint32_t G>
 __device__ inline uint32_t xcd_tile(uint32_t b, uint32_t nb) {
-#if ACS_XCD_GROUP
-  constexpr uint32_t G = ACS_XCD_GROUP, SPAN = 8u * G;
-  if (b >= nb / SPAN * SPAN) return b;
-  const uint32_t x = b & 7u, i = b >> 3;
-  return (i / G) * SPAN + x * G + (i % G);
-#else
-  (void)nb;
-  return b;
-#endif
+  if constexpr (G == 0) {
+    (void)nb;
+    return b;
+  } else {
+    constexpr uint32_t SPAN = 8u * G;
+    if (b >= nb / SPAN * SPAN) return b;
+    const uint32_t x = b & 7u, i = b >> 3;
+    return (i / G) * SPAN + x * G + (i % G);
+  }
 }
 
 // 1 + the lane's second class (composed class rows; 0: none)
@@ -676,7 +682,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = xcd_tile<ACS_XCD_GROUP_K1>(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
@@ -886,7 +892,7 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
                                                                 Decision* __restrict__ out,
                                                                 const uint32_t* __restrict__ tpl, TplLayout TL) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = xcd_tile<ACS_XCD_GROUP_K2>(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
