@@ -636,11 +636,12 @@ __device__ inline T16 line_load(const T16* p) {
 // neighbouring tiles of the coherence order — the same classes, the same table nodes — would
 // land on eight different L2s.  G > 0 gives each XCD runs of G consecutive tiles, the runs
 // interleaved over the XCDs (load stays balanced, unlike whole XCD-contiguous ranges, r04_j);
-// the tail beyond the last full 8·G tiles keeps the identity.  Same-call A/B (r05_y): K1 with
-// G = 16 c3 10M 2.886 vs 2.930 ms (c5, c3adv equal; G = 4 / 64: 2.937 / 2.935); K2 slower with
-// any G (c4 4.14 vs 4.02 at 16), so it keeps the identity.
+// the tail beyond the last full 8·G tiles keeps the identity.  Same-call A/Bs: K1 with G = 16
+// c3 10M 2.886 vs 2.930 ms (r05_y) and 2.909 vs 2.923 (r05_z), but c3r1 1M 0.415 vs 0.399 and
+// c2 0.129 vs 0.127 (r05_z): within the boxes' noise, so off; K2 slower with any G (c4 4.14 vs
+// 4.02 at 16).
 #ifndef ACS_XCD_GROUP_K1
-#define ACS_XCD_GROUP_K1 16
+#define ACS_XCD_GROUP_K1 0
 #endif
 #ifndef ACS_XCD_GROUP_K2
 #define ACS_XCD_GROUP_K2 0
