@@ -244,8 +244,10 @@ class GpuAccessController {
       items[k] = dirty && prev && prev.obj === ps && !dirty.has(key) ? prev.index
         : addon.storeBuilderStage(this.builder, JSON.stringify(snapshotSet(ps)));
     }
+    const tStaged = Date.now();
     const r = addon.storeBuilderCompile(this.builder, items); // throws: the builder is unchanged
     const blob = r.blob;
+    const tCompiled = Date.now();
     // the builder now holds this compile's fragments, in this Map order
     const setIndex = new Map();
     for (let k = 0; k < entries.length; ++k) setIndex.set(entries[k][0], { obj: entries[k][1], index: k });
@@ -263,7 +265,9 @@ class GpuAccessController {
     // one device: the previous image with only its changed blocks uploaded (acs_compile_update)
     const tables = this.tables && !Array.isArray(this.device) ? addon.compileUpdate(this.tables, blob)
       : addon.compile(blob, this.device);
+    const tDevice = Date.now();
     const codec = addon.codecCreate(blob);
+    const tCodec = Date.now();
     const pipeline = this.pipelineBytes === null ? null : addon.pipelineCreate(tables, codec, this.threads, this.chunk);
     // the old handles: released once the batches still in flight are done with them
     if (this.pipeline) addon.pipelineFree(this.pipeline);
@@ -280,8 +284,12 @@ class GpuAccessController {
     this.policySets = policySets;
     this.dirty = new Set();
     this.stale = false;
+    // phases (ms): the changed sets serialised and staged, the image compiled, the device image
+    // updated, the request codec built for the new image
     this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length,
-                         uploadBytes: addon.uploadBytes(tables) };
+                         uploadBytes: addon.uploadBytes(tables),
+                         phases: { stage: tStaged - t0, compile: tCompiled - tStaged, device: tDevice - tCompiled,
+                                   codec: tCodec - tDevice } };
   }
 
   // node index of the compiled Map (whatIsAllowed's ReverseQuery assembly), built lazily: it
