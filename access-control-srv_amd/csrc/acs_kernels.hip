@@ -17,6 +17,8 @@
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <atomic>
+#include <sys/mman.h>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -24,6 +26,7 @@
 
 #include "../../include/acs_mi355x.h"
 #include "acs_eval.h"
+#include "acs_pool.h"
 
 using namespace acs;
 
@@ -1307,7 +1310,30 @@ struct acs_tables {
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
   uint32_t simds = 0;   // the device's SIMDs (spread_waves; 0 until first asked)
-  std::vector<char> host_img;  // the device image as uploaded (acs_compile_update diffs against it)
+  // the device image as uploaded (acs_compile_update diffs against it): uninitialised storage,
+  // 2-MB pages for a large store (every byte is written by compile_image)
+  struct HostImage {
+    struct Free {
+      void operator()(char* q) const { free(q); }
+    };
+    std::unique_ptr<char, Free> p;
+    size_t n = 0;
+    bool alloc(size_t k) {
+      const size_t huge = size_t(2) << 20;
+      void* q = nullptr;
+      if (k >= huge) {
+        q = aligned_alloc(huge, (k + huge - 1) / huge * huge);
+        if (q) madvise(q, (k + huge - 1) / huge * huge, MADV_HUGEPAGE);
+      }
+      if (!q) q = malloc(k ? k : 1);
+      p.reset((char*)q);
+      n = q ? k : 0;
+      return q != nullptr;
+    }
+    char* data() { return p.get(); }
+    const char* data() const { return p.get(); }
+    size_t size() const { return n; }
+  } host_img;
   size_t upload_bytes = 0;     // bytes the compile uploaded (acs_compile_update: the differing blocks)
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
   static constexpr int RING = 256;
@@ -1522,10 +1548,8 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   // addresses both: every node's res_off / act_off / subj_off is rebased, inline attributes
   // point into their line (pools too large for rebased u32 offsets keep the blob layout).
   const char* bsrc = (const char*)blob + src;
-  std::vector<char> img;
   size_t doff[6];
   uint32_t rstride = 1;
-  const void* up = bsrc;
   size_t up_bytes = total;
   const size_t lines = (size_t)h.n_rules * 128;
   const size_t l0 = (align16(sz[0]) + align16(sz[1]) + 127) & ~size_t(127);
@@ -1539,13 +1563,55 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
     doff[4] = l0 + p_rel;
     doff[5] = doff[4] + align16(sz[4]);
     up_bytes = doff[5] + align16(sz[5]);
-    img.assign(up_bytes, 0);
-    char* d = img.data();
-    std::memcpy(d + doff[0], bsrc + off[0], sz[0]);
-    std::memcpy(d + doff[1], bsrc + off[1], sz[1]);
-    std::memcpy(d + doff[3], bsrc + off[3], sz[3]);
-    std::memcpy(d + doff[4], bsrc + off[4], sz[4]);
-    std::memcpy(d + doff[5], bsrc + off[5], sz[5]);
+  } else {
+    for (int k = 0; k < 6; ++k) doff[k] = off[k];
+  }
+  // the event index (acs_eval.h build_event_index) after the image, from the blob's records
+  // and the parent index (acs_eval.h build_parents: whatIsAllowed templates) after it
+  const size_t ev_words = event_index_words(h.n_sets, h.n_pols, h.n_rules);
+  const size_t ex_words = ev_words + parent_index_words(h.n_pols, h.n_rules);
+  const size_t ev_off = align16(up_bytes);
+  const size_t img_total = ev_off + ex_words * sizeof(uint32_t);
+  auto* t = new acs_tables();
+  t->device = device;
+  t->rx_rows_min = rx_rows_min;
+  // The host image (kept: acs_compile_update diffs the next image against it), written in
+  // place over the host threads — c5 (1M rules, 130 MB): one pass instead of a zero-fill, a
+  // staging copy and a second copy.
+  if (!t->host_img.alloc(img_total)) {
+    fail("acs_compile: host image allocation failed");
+    delete t;
+    return nullptr;
+  }
+  char* d = t->host_img.data();
+  const size_t T = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+  // copy [from, from + len) of the blob to d + to in pieces over the pool
+  struct Piece {
+    const char* from;
+    char* to;
+    size_t len;
+  };
+  std::vector<Piece> pieces;
+  auto add_copy = [&](const char* from, char* to, size_t len) {
+    constexpr size_t PIECE = size_t(4) << 20;
+    for (size_t o = 0; o < len; o += PIECE) pieces.push_back({from + o, to + o, std::min(PIECE, len - o)});
+  };
+  auto run_pieces = [&] {
+    std::atomic<size_t> next{0};
+    acs_pool::run((int)std::min(T, std::max<size_t>(pieces.size(), 1)), [&](int) {
+      for (size_t x; (x = next.fetch_add(1)) < pieces.size();) std::memcpy(pieces[x].to, pieces[x].from, pieces[x].len);
+    });
+    pieces.clear();
+  };
+  if (rstride == 2) {
+    // sections 0, 1, 3, 4, 5 as in the blob; the padding after each zeroed
+    const int secs[5] = {0, 1, 3, 4, 5};
+    const size_t ends[6] = {doff[1], l0, 0, doff[4], doff[5], up_bytes};
+    for (int k : secs) {
+      add_copy(bsrc + off[k], d + doff[k], sz[k]);
+      std::memset(d + doff[k] + sz[k], 0, ends[k] - doff[k] - sz[k]);
+    }
+    run_pieces();
     const uint32_t R0 = (uint32_t)(lines / 16), P0 = (uint32_t)(p_rel / 8);
     auto rebase = [&](NodeRec& N) {
       N.res_off += R0;
@@ -1558,52 +1624,59 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
     }
     const RuleResAttr* rres = (const RuleResAttr*)(bsrc + off[3]);
     const Pair* pairs = (const Pair*)(bsrc + off[4]);
-    for (uint32_t r = 0; r < h.n_rules; ++r) {
-      NodeRec N;
-      std::memcpy(&N, bsrc + off[2] + (size_t)r * 64, 64);
-      char* line = d + l0 + (size_t)r * 128;
-      const uint32_t res_off = N.res_off, act_off = N.act_off;
-      rebase(N);
-      if (N.res_n <= 3) {  // validated: [res_off, res_off + res_n) lies in the pool
-        std::memcpy(line + 64, rres + res_off, (size_t)N.res_n * sizeof(RuleResAttr));
-        N.res_off = r * 8 + 4;
-      }
-      if (N.act_n <= 2) {
-        std::memcpy(line + 112, pairs + act_off, (size_t)N.act_n * sizeof(Pair));
-        N.act_off = r * 16 + 14;
-      }
-      std::memcpy(line, &N, 64);
-    }
-    up = d;
+    const size_t nr = h.n_rules, chunk = 8192;
+    std::atomic<size_t> next{0};
+    acs_pool::run((int)std::min(T, (nr + chunk - 1) / chunk), [&](int) {
+      for (size_t c; (c = next.fetch_add(1)) * chunk < nr;)
+        for (uint32_t r = (uint32_t)(c * chunk); r < std::min(nr, (c + 1) * chunk); ++r) {
+          NodeRec N;
+          std::memcpy(&N, bsrc + off[2] + (size_t)r * 64, 64);
+          char* line = d + l0 + (size_t)r * 128;
+          std::memset(line + 64, 0, 64);
+          const uint32_t res_off = N.res_off, act_off = N.act_off;
+          rebase(N);
+          if (N.res_n <= 3) {  // validated: [res_off, res_off + res_n) lies in the pool
+            std::memcpy(line + 64, rres + res_off, (size_t)N.res_n * sizeof(RuleResAttr));
+            N.res_off = r * 8 + 4;
+          }
+          if (N.act_n <= 2) {
+            std::memcpy(line + 112, pairs + act_off, (size_t)N.act_n * sizeof(Pair));
+            N.act_off = r * 16 + 14;
+          }
+          std::memcpy(line, &N, 64);
+        }
+    });
   } else {
-    for (int k = 0; k < 6; ++k) doff[k] = off[k];
+    add_copy(bsrc, d, total);
+    run_pieces();
   }
-  // the event index (acs_eval.h build_event_index) after the image, from the blob's records
-  // and the parent index (acs_eval.h build_parents: whatIsAllowed templates) after it
-  const size_t ev_words = event_index_words(h.n_sets, h.n_pols, h.n_rules);
-  std::vector<uint32_t> evx(ev_words + parent_index_words(h.n_pols, h.n_rules));
-  build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
-                    (const NodeRec*)(bsrc + off[2]), h.n_rules, evx.data());
-  build_parents((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols, h.n_rules,
-                evx.data() + ev_words);
-  const size_t ev_off = align16(up_bytes);
-  auto* t = new acs_tables();
-  t->device = device;
-  t->rx_rows_min = rx_rows_min;
-  const size_t img_total = ev_off + evx.size() * sizeof(uint32_t);
-  // the host copy of the device image: acs_compile_update diffs the next image against it
-  t->host_img.assign(img_total, 0);
-  std::memcpy(t->host_img.data(), up, up_bytes);
-  if (!evx.empty()) std::memcpy(t->host_img.data() + ev_off, evx.data(), evx.size() * sizeof(uint32_t));
+  std::memset(d + up_bytes, 0, ev_off - up_bytes);
+  uint32_t* evx = (uint32_t*)(d + ev_off);
+  std::memset(evx, 0, ex_words * sizeof(uint32_t));  // (the builders OR bits into it)
+  if (ex_words) {
+    build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
+                      (const NodeRec*)(bsrc + off[2]), h.n_rules, evx);
+    build_parents((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols, h.n_rules,
+                  evx + ev_words);
+  }
   const char* hi = t->host_img.data();
   bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess;
   if (copied && prev && prev->device == device && prev->host_img.size() == img_total && prev->view.rstride == rstride) {
     // delta: the previous image copied on the device, the differing 64-KB blocks uploaded
     constexpr size_t BLK = 64 * 1024;
     copied = hipMemcpy(t->dev, prev->dev, img_total, hipMemcpyDeviceToDevice) == hipSuccess;
-    for (size_t o = 0; copied && o < img_total; o += BLK) {
-      const size_t len = std::min(BLK, img_total - o);
-      if (std::memcmp(hi + o, prev->host_img.data() + o, len) == 0) continue;
+    const size_t nblk = (img_total + BLK - 1) / BLK;
+    std::vector<uint8_t> differs(nblk, 0);  // blocks compared over the pool, uploaded in order
+    std::atomic<size_t> next{0};
+    acs_pool::run((int)std::min(T, std::max<size_t>(nblk / 16, 1)), [&](int) {
+      for (size_t b; (b = next.fetch_add(1)) < nblk;) {
+        const size_t o = b * BLK, len = std::min(BLK, img_total - o);
+        differs[b] = std::memcmp(hi + o, prev->host_img.data() + o, len) != 0;
+      }
+    });
+    for (size_t b = 0; copied && b < nblk; ++b) {
+      if (!differs[b]) continue;
+      const size_t o = b * BLK, len = std::min(BLK, img_total - o);
       copied = hipMemcpy((char*)t->dev + o, hi + o, len, hipMemcpyHostToDevice) == hipSuccess;
       t->upload_bytes += len;
     }

@@ -84,12 +84,23 @@ int acs_internal_check_blob(const void* blob, size_t n_bytes, uint32_t* rx_rows_
         t.fe > t.child_end)
       return bad("image: policy", q);
   }
-  for (uint32_t r = 0; r < h.n_rules; ++r)
-    if (!node_ok(rules[r])) return bad("image: rule", r);
-  uint32_t rows = 0;
-  for (uint32_t k = 0; k < h.n_rres; ++k)
-    if ((rres[k].kind & K_ENT_LOOSE) && (uint32_t)rres[k].row + 1 > rows) rows = (uint32_t)rres[k].row + 1;
-  *rx_rows_min = rows;
+  // rules and rule attributes over the host threads (c5: 1M rules)
+  const size_t first_bad = parallel_first_bad(h.n_rules, [&](size_t lo, size_t hi) {
+    for (size_t r = lo; r < hi; ++r)
+      if (!node_ok(rules[r])) return r;
+    return (size_t)h.n_rules;
+  });
+  if (first_bad < h.n_rules) return bad("image: rule", first_bad);
+  std::atomic<uint32_t> rows{0};
+  parallel_first_bad(h.n_rres, [&](size_t lo, size_t hi) {
+    uint32_t m = 0;
+    for (size_t k = lo; k < hi; ++k)
+      if ((rres[k].kind & K_ENT_LOOSE) && (uint32_t)rres[k].row + 1 > m) m = (uint32_t)rres[k].row + 1;
+    for (uint32_t v = rows.load(); v < m && !rows.compare_exchange_weak(v, m);) {
+    }
+    return (size_t)h.n_rres;
+  });
+  *rx_rows_min = rows.load();
   return 0;
 }
 
