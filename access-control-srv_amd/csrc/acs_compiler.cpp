@@ -17,6 +17,7 @@
 // Snapshot format: a JSON array of the Map's values in Map order; a set's `combinables` is
 // the array of its policies (Map order, null entries kept), a policy's `combinables` the
 // array of its rules — JSON.stringify of Array.from(map.values()) at each level.
+#include <sys/mman.h>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -37,6 +38,39 @@ extern "C" void acs_internal_set_error(const char* msg);
 
 using namespace acs;
 using namespace acs_json;
+
+namespace {
+
+// Image blobs: zeroed storage behind a 64-B header (kind, mapping size).  Large images are
+// anonymous mappings with 2-MB pages (zero on first touch; the fragments are written in
+// parallel, and 4-KB page faults serialised a c5 image's 120 MB); small ones come from calloc.
+constexpr uint64_t BLOB_MMAP = 0x6d6d6170u, BLOB_HEAP = 0x68656170u;
+void* blob_alloc_zeroed(size_t n) {
+  constexpr size_t HDR = 64, HUGE = size_t(2) << 20;
+  if (n >= 8 * HUGE) {
+    const size_t m = (n + HDR + HUGE - 1) / HUGE * HUGE;
+    void* p = mmap(nullptr, m, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p != MAP_FAILED) {
+      madvise(p, m, MADV_HUGEPAGE);
+      uint64_t* h = (uint64_t*)p;
+      h[0] = BLOB_MMAP;
+      h[1] = m;
+      return (char*)p + HDR;
+    }
+  }
+  uint64_t* h = (uint64_t*)calloc(n + HDR, 1);
+  if (!h) return nullptr;
+  h[0] = BLOB_HEAP;
+  return (char*)h + HDR;
+}
+void blob_release(void* blob) {
+  if (!blob) return;
+  uint64_t* h = (uint64_t*)((char*)blob - 64);
+  if (h[0] == BLOB_MMAP) munmap(h, (size_t)h[1]);
+  else free(h);
+}
+
+}  // namespace
 
 namespace {
 
@@ -640,7 +674,7 @@ void* write_image(Builder& b, const std::vector<const Fragment*>& F, size_t* len
   const size_t total = c_ec + a4(ecj.size());
   if (K > UINT32_MAX || I > UINT32_MAX || sb > UINT32_MAX || total - o_sec > UINT32_MAX || o_sec > UINT32_MAX)
     fail("store too large");
-  uint8_t* out = (uint8_t*)calloc(total, 1);  // zeroed: the padding
+  uint8_t* out = (uint8_t*)blob_alloc_zeroed(total);  // zeroed: the padding
   if (!out) fail("out of memory");
   const uint32_t hdr[16] = {ACS_BLOB_MAGIC, ACS_ABI_VERSION, (uint32_t)T.s, (uint32_t)T.p, (uint32_t)T.r,
                             (uint32_t)T.rres, (uint32_t)T.pairs, (uint32_t)T.u32, id_user, (uint32_t)o_sec,
@@ -823,7 +857,10 @@ int acs_store_compile(const char* store_json, size_t store_len, const char* urns
   return -1;
 }
 
-void acs_blob_free(void* blob) { free(blob); }
+void acs_blob_free(void* blob) { blob_release(blob); }
+
+// (internal) zeroed storage for a blob the caller frees with acs_blob_free
+void* acs_internal_blob_alloc(size_t n) { return blob_alloc_zeroed(n); }
 
 acs_store_builder* acs_store_builder_create(const char* urns_json, size_t urns_len, const char* cas_json,
                                             size_t cas_len) {

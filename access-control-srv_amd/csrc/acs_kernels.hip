@@ -1856,6 +1856,7 @@ static std::vector<uint32_t> shard_cuts(const void* blob, int parts) {
 }
 
 // Test hook (tests/test_rule_shard_lib.py): shard k of `parts` as acs_compile_sharded cuts it.
+void* acs_internal_blob_alloc(size_t n);  // acs_compiler.cpp
 int acs_internal_shard_blob(const void* blob, size_t n_bytes, int parts, int k, void** out, size_t* out_len,
                             acs_shard* base) {
   if (!blob || n_bytes < sizeof(acs_blob_header) || parts < 1 || k < 0 || k >= parts || !out || !out_len || !base)
@@ -1865,7 +1866,7 @@ int acs_internal_shard_blob(const void* blob, size_t n_bytes, int parts, int k, 
   const std::vector<uint32_t> cut = shard_cuts(blob, parts);
   ShardBase b{};
   std::vector<char> img = slice_blob(blob, cut[k], cut[k + 1], &b);
-  void* mem = malloc(img.size());
+  void* mem = acs_internal_blob_alloc(img.size());  // freed by acs_blob_free
   if (!mem) return fail("acs_internal_shard_blob: out of memory");
   std::memcpy(mem, img.data(), img.size());
   *out = mem;
