@@ -159,6 +159,33 @@ def test_codec_synthetic_threads(kind, threads, second):
         assert st2["hr_cache_misses"] == 0 and st2["hr_cache_hits"] == sb.batch.n
 
 
+def test_codec_classes_independent_of_threads():
+    """The class work runs over the worker pool (per-thread key sets merged by hash partition,
+    codec load over the pool): the same batch encoded on 1, 3 and 8 threads gets the same class
+    of every request, the same class rows in the same order and the same coherence order, and
+    a batch no larger than one whose level-0 keys were given up gets the same rows again."""
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 30000, "c3", seed=5, second_role=0.5)
+    text = sb.json_text()
+    outs = []
+    for th in (1, 3, 8):
+        codec = NativeCodec(compiler.store_blob(cs))
+        for k, v in sb.hrs_forests().items():
+            codec.set_subject_scopes(k, v)
+        b = codec.encode(text, threads=th)
+        outs.append((b.lines["h"]["flags"].copy(), b.lines["cls2"].copy(), b.cand.copy(),
+                     None if b.perm is None else b.perm.copy()))
+        b2 = codec.encode(text, threads=th)  # second batch: the level-0 attempt may be skipped
+        assert np.array_equal(b2.cand, b.cand) and np.array_equal(b2.lines["cls2"], b.lines["cls2"])
+        b2.close()
+        b.close()
+        codec.close()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
+        assert np.array_equal(outs[0][2], o[2])
+        assert (outs[0][3] is None) == (o[3] is None) and (o[3] is None or np.array_equal(outs[0][3], o[3]))
+
+
 def test_codec_subject_scope_registry():
     """A request naming a registered forest ("$hrs") decides exactly as one carrying the
     forest inline; eviction sends it to the host; replacing the forest changes it."""
