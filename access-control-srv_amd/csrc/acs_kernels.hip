@@ -679,7 +679,9 @@ __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && 
 // Batches of long class runs keep the plain form (c3 1M padded: 0.770 vs 0.789 ms, r05_i; c3 10M
 // unpadded, ~300 requests per class: 3.02 vs 3.10 ms, r05_j)
 #ifndef ACS_K1_SK_WAVES_PER_EU
-#define ACS_K1_SK_WAVES_PER_EU 4  // c3 131,072: 0.448 ms at 5, 0.437 at 4; 8,192: 0.373 vs 0.332 (r05_g)
+// c3 131,072: 0.448 ms at 5, 0.437 at 4 with 16-request spread waves (r05_g); with 8-request waves
+// 0.359 at 5 vs 0.375 at 4, c3 524,288 0.592 vs 0.595, c5 1M 3.150 vs 3.178 (r05_af)
+#define ACS_K1_SK_WAVES_PER_EU 5
 #endif
 template <class FL, bool CB, bool AN, bool SK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
