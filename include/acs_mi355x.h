@@ -142,8 +142,11 @@ int acs_device_list(const acs_tables* t, int* devices, int n);
  * run k compiled alone onto devices[k].  acs_is_allowed then evaluates every request on every
  * device — the batch uploaded to each, its class rows cut to the device's nodes on the device —
  * turns each device's records into acs_shard_keys_device keys, MAX-reduces them on devices[0]
- * (peer copies over xGMI) and decodes them: the records of an unsharded evaluation.  The other
- * evaluation entry points refuse a sharded handle. */
+ * (peer copies over xGMI) and decodes them: the records of an unsharded evaluation.
+ * acs_what_is_allowed / acs_what_is_allowed_obl (host buffers) evaluate every request on every
+ * device and join the devices' set / policy / rule sections into the caller's rows, obligation
+ * logs merged in set order.  The device-buffer entry points, the pipeline and acs_compile_update
+ * refuse a sharded handle. */
 acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 
 /* Replaces: the device side of a store change (AccessController.updateRule / updatePolicy / ...,
