@@ -221,8 +221,22 @@ class AccessController:
             self._tables = self._engine(blob)
         else:
             from . import native
-            # the previous image with only its changed blocks uploaded (acs_compile_update)
-            self._tables = prev.updated(blob) if prev is not None else native.Tables(blob, self.device)
+            # the previous image with only its changed blocks uploaded (acs_compile_update); if
+            # that fails (a device allocation, an image the update refuses), a full upload; the
+            # previous handle is closed only once a new one exists, and kept if neither succeeds
+            new = None
+            try:
+                if prev is not None:
+                    try:
+                        new = prev.updated(blob)
+                    except Exception:
+                        new = None
+                if new is None:
+                    new = native.Tables(blob, self.device)
+            except Exception:
+                self._tables = prev  # the old image still serves the old store until a retry
+                raise
+            self._tables = new
             if prev is not None:
                 prev.close()
             self.stats["upload_bytes"] = self._tables.upload_bytes

@@ -108,6 +108,26 @@ __device__ inline void op_count(int k) {
 #define ACS_OPC(k)
 #endif
 
+// Cost probes (timing-only A/B builds, records unchanged): ACS_AB_PROBE_HR2 / ACS_AB_PROBE_TM2
+// evaluate a rule's checkHierarchicalScope / target match a second time on an opaque copy of its
+// record and keep the first result, so the difference to the product's time is one more check of
+// that kind per call.  acs_opaque0(): a zero the compiler cannot see through.
+#ifndef ACS_AB_PROBE_HR2
+#define ACS_AB_PROBE_HR2 0
+#endif
+#ifndef ACS_AB_PROBE_TM2
+#define ACS_AB_PROBE_TM2 0
+#endif
+ACS_FN uint32_t acs_opaque0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+#else
+  return 0u;
+#endif
+}
+
 // regex matrix cell bits (rule entity value row x request entity value column)
 enum RxBits : uint8_t { RX_HIT = 1, RX_RESET = 2, RX_THROW_TYPE = 4, RX_THROW_SYNTAX = 8, RX_HOST = 16 };
 
@@ -124,6 +144,8 @@ struct Tables {
   const uint32_t* ev_index;  // event index (build_event_index; nullptr: K1 never skips a set for it)
   const uint32_t* parents;   // [P] set of each policy, then [R] policy of each rule (build_parents;
                              // nullptr: no whatIsAllowed templates)
+  const char* img;           // the device image every section above lies in (ACS_SCALAR_RECORDS:
+  uint32_t img_bytes;        // load_words clamps its offsets below img_bytes, >= 64, inside the allocation)
 };
 
 // The parent of every policy (its set) and rule (its policy): parent_index_words(P, R) words.
@@ -227,19 +249,63 @@ extern thread_local unsigned long long acs_host_work;
 #define ACS_SCAN(bytes)
 #endif
 
-// Table records are read as whole dwords through wave-uniform addresses and unpacked in
-// registers.  Vector loads (exec-masked, so a block entered with no active lane loads
-// nothing), then the wave-uniform record moves to SGPRs: its fields feed scalar compares and
-// branches and free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself
-// proves the address uniform it emits s_load; nothing here forces a scalar load (a scalar
-// load ignores EXEC, so a block entered with no active lane would read an unchecked address:
-// the round-3 scalar-load A/B form faulted on c4 and was removed).  One-lane vector loads
-// measured slower (c3 K1 1.891 vs 1.851 ms, r03_g).
+// Table records are read as whole dwords through wave-uniform addresses, straight into SGPRs:
+// their fields feed scalar compares and branches.  GPU (ACS_SCALAR_RECORDS): scalar buffer
+// loads per record (s_buffer_load_dwordx4 / x2 through the scalar cache) against a buffer
+// resource spanning the device image.  A scalar load ignores EXEC, so it also runs in a block no
+// lane entered; the resource's range check makes any such read return zeros instead of touching
+// memory outside the image (the round-3 plain s_load form faulted there and was removed).  The
+// earlier form — exec-masked vector loads of the record into VGPRs, then v_readfirstlane per dword
+// — held 16 VGPRs per in-flight record (A/B in DESIGN §3).
+#ifndef ACS_SCALAR_RECORDS
+#define ACS_SCALAR_RECORDS 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef int acs_v4i __attribute__((ext_vector_type(4)));
+typedef uint32_t acs_v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t acs_v4u __attribute__((ext_vector_type(4)));
+__device__ acs_v2u acs_sbuf_load2(acs_v4i rsrc, int off, int aux) __asm("llvm.amdgcn.s.buffer.load.v2i32");
+__device__ acs_v4u acs_sbuf_load4(acs_v4i rsrc, int off, int aux) __asm("llvm.amdgcn.s.buffer.load.v4i32");
+// raw buffer resource over the image: stride 0, num_records = bytes (range-checked), dword format
+__device__ inline acs_v4i image_rsrc(const Tables& T) {
+  const uint64_t a = (uint64_t)(uintptr_t)T.img;
+  return acs_v4i{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xFFFFu), (int)T.img_bytes, 0x00027FAC};
+}
+#endif
 template <class X, int NW = sizeof(X) / 4>
 ACS_FN X load_words(const Tables& T, const X* p) {
   static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
   (void)T;
   ACS_SCAN(sizeof(X));
+  X out;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (ACS_SCALAR_RECORDS && (NW == 16 || NW == 4 || NW == 2)) {
+    // clamped into the image (img_bytes >= 64): in a region the wave runs with no active lane the
+    // offset can be stale, and the scalar unit reads it anyway
+    uint32_t o = wave_uniform((uint32_t)((const char*)p - T.img));
+    o = o < T.img_bytes - (uint32_t)sizeof(X) ? o : T.img_bytes - (uint32_t)sizeof(X);
+    const int off = (int)o;
+    uint32_t v[NW];
+    if constexpr (NW == 16) {  // four x4 loads (the backend cannot split a divergent x16 one)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const acs_v4u x = acs_sbuf_load4(image_rsrc(T), off + 16 * q, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * q + k] = x[k];
+      }
+    } else if constexpr (NW == 4) {
+      const acs_v4u x = acs_sbuf_load4(image_rsrc(T), off, 0);
+#pragma unroll
+      for (int k = 0; k < NW; ++k) v[k] = x[k];
+    } else {
+      const acs_v2u x = acs_sbuf_load2(image_rsrc(T), off, 0);
+#pragma unroll
+      for (int k = 0; k < NW; ++k) v[k] = x[k];
+    }
+    __builtin_memcpy(&out, v, sizeof(X));
+    return out;
+  }
+#endif
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -249,7 +315,6 @@ ACS_FN X load_words(const Tables& T, const X* p) {
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];
 #endif
-  X out;
   __builtin_memcpy(&out, v, sizeof(X));
   return out;
 }
@@ -674,14 +739,12 @@ struct ReqCtx {
 
 // Resource attributes staged in LDS by the kernel (slots < LDS_SLOTS, column = lane,
 // stride = block size): dynamic indexing without scratch, one ds_read_b128 per use.
-#ifndef ACS_LDS_SLOTS
-// 4 x 16 B x 256 lanes = 16 KB: with a c3 filter row (832 words x 4 waves, 13 KB) a block
-// fits 5 times into the CU's 160 KB of LDS, for K1's 5 waves/SIMD (A/B r02_q: 6 slots 1.98,
-// 4 slots 1.95, 4 slots + 5 waves 1.87 ms at c3; 8 slots: 3 blocks/CU, round-2 A/B 20.6 vs
-// 17.6 ms with 6).  Attributes past the slots are read from HBM.
-#define ACS_LDS_SLOTS 4
-#endif
-constexpr int LDS_SLOTS = ACS_LDS_SLOTS;
+// LDS_SLOTS = LINE_RES: the slots are exactly the line's attributes, and res_row serves only
+// attributes past the line (a compact batch's extension record).  4 x 16 B x 256 lanes = 16 KB:
+// with a c3 filter row (832 words x 4 waves, 13 KB) a block fits 5 times into the CU's 160 KB of
+// LDS, for K1's 5 waves/SIMD (A/B r02_q: 6 slots 1.98, 4 slots 1.95, 4 slots + 5 waves 1.87 ms at
+// c3; 8 slots: 3 blocks/CU, round-2 A/B 20.6 vs 17.6 ms with 6).
+constexpr int LDS_SLOTS = LINE_RES;
 
 struct ReqLds : ReqCtx {
   const ReqRes* col;  // this lane's LDS column
@@ -708,7 +771,7 @@ struct ReqLds : ReqCtx {
     return res_row((uint32_t)j);
   }
 };
-static_assert(LDS_SLOTS <= LINE_RES, "the kernels stage LDS slots from the request line");
+static_assert(LDS_SLOTS == LINE_RES, "the kernels stage exactly the request line's attributes in LDS");
 
 // Resource attributes read from HBM on every use (host build of the core).
 struct ReqMem : ReqCtx {
@@ -1291,12 +1354,28 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
         if (!vt) ACS_OPC(OP_RULE_TM);
 #endif
         m = vt ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
+#if ACS_AB_PROBE_TM2
+        if (!vt) {
+          NodeRec Q2 = Q;
+          Q2.role ^= acs_opaque0();
+          const tri m2 = target_match_retry(Q2, R, Q.effect, false, nullptr);
+          m = m2 == m ? m : m2;
+        }
+#endif
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
         PROF_ADD(PH_RULE_TARGET, tr);
         if (!m) continue;
         PROF_T0(th);
         ACS_OPC(OP_RULE_HR);
         m = hierarchical_scope(Q, R);
+#if ACS_AB_PROBE_HR2
+        {
+          NodeRec Q2 = Q;
+          Q2.se ^= acs_opaque0();
+          const tri m2 = hierarchical_scope(Q2, R);
+          m = m2 == m ? m : m2;
+        }
+#endif
         PROF_ADD(PH_RULE_HR, th);
         if (m < 0) return *ev = make_err(m, s + 1), SET_EVENT;
       }

@@ -801,6 +801,8 @@ __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, 
       uint32_t set = 0xFFFFFFFFu;
       for (; w < nw; ++w) {
         uint32_t x = row[w];
+        // bits past n_sets in the last word are not sets (a caller's row may carry them): dropped
+        if (w == nw - 1u && (T.n_sets & 31u)) x &= (1u << (T.n_sets & 31u)) - 1u;
         const uint32_t pc = (uint32_t)__builtin_popcount(x);
         if (want >= before && want < before + pc) {
           for (uint32_t q = want - before; q; --q) x &= x - 1u;
@@ -1574,6 +1576,10 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   const size_t ex_words = ev_words + parent_index_words(h.n_pols, h.n_rules);
   const size_t ev_off = align16(up_bytes);
   const size_t img_total = ev_off + ex_words * sizeof(uint32_t);
+  if (img_total > 0xFFFFFF00ull) {  // the kernels may address records by 32-bit offsets into the image
+    fail("acs_compile: device image larger than 4 GB");
+    return nullptr;
+  }
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
@@ -1710,6 +1716,8 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   // more runs without it (no set is skipped for it; the decisions are the same)
   t->view.ev_index = h.n_rules < (1u << 30) ? (const uint32_t*)(base + ev_off) : nullptr;
   t->view.parents = (const uint32_t*)(base + ev_off) + ev_words;
+  t->view.img = base;
+  t->view.img_bytes = (uint32_t)(img_total + 64);  // the allocation holds img_total + 128 bytes
   t->image_bytes = img_total;
   return t;
 }
@@ -1767,6 +1775,7 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
     r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
     r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
     r->view.parents = (const uint32_t*)rebase(t->view.parents);
+    r->view.img = (const char*)r->dev;
     r->sort = t->sort;
     t->peers.push_back(r);
   }

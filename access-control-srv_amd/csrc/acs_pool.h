@@ -13,6 +13,7 @@
 
 #include <condition_variable>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <pthread.h>
@@ -32,27 +33,49 @@ class Pool {
     return **p;
   }
 
-  void run(int n, const std::function<void(int)>& f) {
+  // inline_if_busy: when another run holds the pool, run the tasks inline on this thread instead
+  // of waiting for it (batch validation: a pipeline's check of chunk k must not queue behind the
+  // encoder phases of chunk k + 1).  An exception thrown by any task is rethrown here, after every
+  // worker has finished the run (the first one thrown; the others are dropped).
+  void run(int n, const std::function<void(int)>& f, bool inline_if_busy = false) {
     if (n <= 1 || inside()) {
       for (int t = 0; t < n; ++t) f(t);
       return;
     }
-    std::lock_guard<std::mutex> one(run_mu_);
+    std::unique_lock<std::mutex> one(run_mu_, std::defer_lock);
+    if (inline_if_busy) {
+      if (!one.try_lock()) {
+        for (int t = 0; t < n; ++t) f(t);
+        return;
+      }
+    } else {
+      one.lock();
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
       grow(n - 1);
       task_ = &f;
       n_ = n;
       pending_ = n - 1;
+      error_ = nullptr;
       ++gen_;
     }
     cv_.notify_all();
+    std::exception_ptr mine;
     inside() = true;
-    f(0);
+    try {
+      f(0);
+    } catch (...) {
+      mine = std::current_exception();
+    }
     inside() = false;
     std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0; });
+    done_.wait(lk, [&] { return pending_ == 0; });  // no worker still runs f before it unwinds
     task_ = nullptr;
+    std::exception_ptr e = mine ? mine : error_;
+    error_ = nullptr;
+    lk.unlock();
+    if (e) std::rethrow_exception(e);
   }
 
  private:
@@ -81,8 +104,14 @@ class Pool {
       if (idx + 1 >= n_) continue;
       const std::function<void(int)>* f = task_;
       lk.unlock();
-      (*f)(idx + 1);
+      std::exception_ptr e;
+      try {
+        (*f)(idx + 1);
+      } catch (...) {
+        e = std::current_exception();
+      }
       lk.lock();
+      if (e && !error_) error_ = e;
       if (--pending_ == 0) done_.notify_all();
     }
   }
@@ -91,11 +120,14 @@ class Pool {
   std::condition_variable cv_, done_;
   std::vector<std::thread> workers_;
   const std::function<void(int)>* task_ = nullptr;
+  std::exception_ptr error_;  // (mu_) the first exception a worker's task threw this run
   int n_ = 0, pending_ = 0;
   uint64_t gen_ = 0;
 };
 
 // f(t) for t in [0, n) on the pool
-inline void run(int n, const std::function<void(int)>& f) { Pool::instance().run(n, f); }
+inline void run(int n, const std::function<void(int)>& f, bool inline_if_busy = false) {
+  Pool::instance().run(n, f, inline_if_busy);
+}
 
 }  // namespace acs_pool

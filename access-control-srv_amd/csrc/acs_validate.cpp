@@ -46,7 +46,8 @@ size_t parallel_first_bad(size_t n, F f) {
   T = T < 1 ? 1 : (T > 16 ? 16 : T);
   if (T > n / 65536 + 1) T = n / 65536 + 1;
   std::vector<size_t> bad(T, n);
-  acs_pool::run((int)T, [&](int t) { bad[t] = f(n * t / T, n * (t + 1) / T); });
+  // inline when the pool is busy (a pipeline encoding the next chunk): the check does not wait for it
+  acs_pool::run((int)T, [&](int t) { bad[t] = f(n * t / T, n * (t + 1) / T); }, true);
   size_t m = n;
   for (size_t b : bad) m = b < m ? b : m;
   return m;

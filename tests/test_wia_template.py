@@ -119,3 +119,25 @@ def test_templates_gpu_equal_full_walk(second):
     nb.close()
     codec.close()
     t.close()
+
+
+@pytest.mark.gpu
+def test_templates_gpu_stray_set_bits():
+    """A caller's class rows with bits set past n_sets in the last word of the candidate-set
+    section (padding, not sets): the template pass drops them (wia_template_kernel), so K2 with
+    templates still equals the CPU build's full walk on the clean rows."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from acs_mi355x.device import DeviceBatch, what_is_allowed_device
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    assert cs.n_sets % 32, "the store must leave padding bits in its last set word"
+    sb = synth.requests(cs, 8_000, "c3", seed=29, second_role=0.5)
+    want = host_core.what_is_allowed(cs, sb.batch)
+    pad = np.uint32((0xFFFFFFFF << (cs.n_sets & 31)) & 0xFFFFFFFF)
+    sb.batch.cand[:, cs.n_sets // 32] |= pad
+    t = native.Tables(compiler.store_blob(cs), 0)
+    got = [x.cpu().numpy() for x in what_is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True))]
+    _same((got[0].view(np.uint32), got[1].view(np.uint32), got[2].view(np.uint32),
+           got[3].reshape(-1).view(L.DECISION_DT)), want, "stray set bits")
+    t.close()
