@@ -310,6 +310,11 @@ class Tables:
         if self.lib.acs_set_option(self.h, 1, int(bool(enable))) != 0:
             raise RuntimeError(last_error(self.lib))
 
+    def set_chunk(self, requests: int):
+        """ACS_OPT_CHUNK: requests per overlapped chunk of the host-buffer isAllowed (0: off)."""
+        if self.lib.acs_set_option(self.h, 3, int(requests)) != 0:
+            raise RuntimeError(last_error(self.lib))
+
     def set_timing(self, enable: bool):
         if self.lib.acs_set_option(self.h, 2, int(bool(enable))) != 0:
             raise RuntimeError(last_error(self.lib))

@@ -29,34 +29,18 @@ namespace acs {
 
 #define ACS_FN __host__ __device__ inline
 
-// A/B switches.  ACS_VERDICT_ROLES (on): a composed lane reads its second class row's verdict
-// only for targets that test role associations (same-call A/B, r05_c: c3 K1 3.29 -> 3.17 ms, c4
-// K2 8.27 -> 7.96 ms).  ACS_OWN_SKIP (bits; off): lanes skip the rules (1), loop-2b policies (2),
-// sets (4) outside their own filter rows — fewer rule target matches per wave (c3: 2.52 -> 0.98,
-// r05_b op counts) but slower on every config (c3 3.17 -> 3.35 ms, c3r1 1.86 -> 2.09: the per-lane
-// row loads and their registers, r05_c).  ACS_CLEAN_BITS (off): clean sets below the deciding set
-// skipped from the event index's bits without loading their records (c3adv unchanged 1.83 ->
-// 1.85, c3 3.16 -> 3.29 ms: registers, r05_c).
+// A composed lane reads its second class row's verdict only for targets that test role
+// associations (same-call A/B, r05_c: c3 K1 3.29 -> 3.17 ms, c4 K2 8.27 -> 7.96 ms).
+// ACS_OWN_SKIP (bits): the skips K1's SK instantiation takes for waves that mix classes — lanes
+// leave the rules (1), loop-2b policies (2), sets (4) outside their own filter rows.  In the plain
+// instantiation the same skips cut rule target matches per wave (c3: 2.52 -> 0.98, r05_b op counts)
+// but were slower on long class runs (c3 3.17 -> 3.35 ms, c3r1 1.86 -> 2.09: the per-lane row loads
+// and their registers, r05_c).  Rejected forms (removed): clean sets below the deciding
+// set dropped from the event index's bits (c3 3.16 -> 3.29 ms, r05_c) or a word at a time once the
+// whole wave is below it (c3adv 1.794 vs 1.756 ms, r05_n; a parity bug in its first form, r05_m),
+// and K2 lanes skipping the rules outside their own rows.
 #ifndef ACS_OWN_SKIP
-#define ACS_OWN_SKIP 7  // the skips K1's SK instantiation takes (K1 launches it for mixed-class waves)
-#endif
-#ifndef ACS_WAVE_CLEAN_SKIP
-// A/B (off): a wave below its deciding sets drops the clean sets by words.  It cut c3adv's set
-// iterations per wave only 22.4 -> 20.8 (every lane must be below first) and measured slower:
-// c3adv 1M 1.794 vs 1.756 ms, c3 10M 3.055 vs 3.011 (r05_n)
-#define ACS_WAVE_CLEAN_SKIP 0
-#endif
-#ifndef ACS_K2_OWN_SKIP
-#define ACS_K2_OWN_SKIP 0  // K2's rule skip (what_is_allowed_t)
-#endif
-#ifndef ACS_VERDICT_ROLES
-#define ACS_VERDICT_ROLES 1
-#endif
-#ifndef ACS_CLEAN_BITS
-#define ACS_CLEAN_BITS 0
-#endif
-#ifndef ACS_WIA_TEMPLATES
-#define ACS_WIA_TEMPLATES 1  // whatIsAllowed from class templates (what_is_allowed_tpl)
+#define ACS_OWN_SKIP 7
 #endif
 
 // Value every active lane of the wave holds identically (a table index or bitset word of
@@ -144,8 +128,6 @@ struct Tables {
   const uint32_t* ev_index;  // event index (build_event_index; nullptr: K1 never skips a set for it)
   const uint32_t* parents;   // [P] set of each policy, then [R] policy of each rule (build_parents;
                              // nullptr: no whatIsAllowed templates)
-  const char* img;           // the device image every section above lies in (ACS_SCALAR_RECORDS:
-  uint32_t img_bytes;        // load_words clamps its offsets below img_bytes, >= 64, inside the allocation)
 };
 
 // The parent of every policy (its set) and rule (its policy): parent_index_words(P, R) words.
@@ -249,63 +231,20 @@ extern thread_local unsigned long long acs_host_work;
 #define ACS_SCAN(bytes)
 #endif
 
-// Table records are read as whole dwords through wave-uniform addresses, straight into SGPRs:
-// their fields feed scalar compares and branches.  GPU (ACS_SCALAR_RECORDS): scalar buffer
-// loads per record (s_buffer_load_dwordx4 / x2 through the scalar cache) against a buffer
-// resource spanning the device image.  A scalar load ignores EXEC, so it also runs in a block no
-// lane entered; the resource's range check makes any such read return zeros instead of touching
-// memory outside the image (the round-3 plain s_load form faulted there and was removed).  The
-// earlier form — exec-masked vector loads of the record into VGPRs, then v_readfirstlane per dword
-// — held 16 VGPRs per in-flight record (A/B in DESIGN §3).
-#ifndef ACS_SCALAR_RECORDS
-#define ACS_SCALAR_RECORDS 0
-#endif
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef int acs_v4i __attribute__((ext_vector_type(4)));
-typedef uint32_t acs_v2u __attribute__((ext_vector_type(2)));
-typedef uint32_t acs_v4u __attribute__((ext_vector_type(4)));
-__device__ acs_v2u acs_sbuf_load2(acs_v4i rsrc, int off, int aux) __asm("llvm.amdgcn.s.buffer.load.v2i32");
-__device__ acs_v4u acs_sbuf_load4(acs_v4i rsrc, int off, int aux) __asm("llvm.amdgcn.s.buffer.load.v4i32");
-// raw buffer resource over the image: stride 0, num_records = bytes (range-checked), dword format
-__device__ inline acs_v4i image_rsrc(const Tables& T) {
-  const uint64_t a = (uint64_t)(uintptr_t)T.img;
-  return acs_v4i{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xFFFFu), (int)T.img_bytes, 0x00027FAC};
-}
-#endif
+// Table records are read as whole dwords through wave-uniform addresses and unpacked in
+// registers.  Vector loads (exec-masked, so a block entered with no active lane loads
+// nothing), then the wave-uniform record moves to SGPRs: its fields feed scalar compares and
+// branches and free VGPRs (K1 VGPR spills 45 -> 1; A/B c3 +5 %).  Where the compiler itself
+// proves the address uniform it emits s_load; nothing here forces a scalar load.  Rejected
+// forms (A/B): one-lane vector loads (c3 K1 1.891 vs 1.851 ms, r03_g); plain s_load
+// (a scalar load ignores EXEC, so in a region no lane entered it reads a stale address: faulted on
+// c4, r03); scalar buffer loads clamped into the image (safe; c3 10M 2.978 vs 2.929 ms, c5 3.26 vs
+// 3.08, c4 K2 3.89 vs 4.00, r06_a).
 template <class X, int NW = sizeof(X) / 4>
 ACS_FN X load_words(const Tables& T, const X* p) {
   static_assert(sizeof(X) == 4 * NW && sizeof(X) <= 64, "record must be whole dwords, at most 64 B");
   (void)T;
   ACS_SCAN(sizeof(X));
-  X out;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (ACS_SCALAR_RECORDS && (NW == 16 || NW == 4 || NW == 2)) {
-    // clamped into the image (img_bytes >= 64): in a region the wave runs with no active lane the
-    // offset can be stale, and the scalar unit reads it anyway
-    uint32_t o = wave_uniform((uint32_t)((const char*)p - T.img));
-    o = o < T.img_bytes - (uint32_t)sizeof(X) ? o : T.img_bytes - (uint32_t)sizeof(X);
-    const int off = (int)o;
-    uint32_t v[NW];
-    if constexpr (NW == 16) {  // four x4 loads (the backend cannot split a divergent x16 one)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const acs_v4u x = acs_sbuf_load4(image_rsrc(T), off + 16 * q, 0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[4 * q + k] = x[k];
-      }
-    } else if constexpr (NW == 4) {
-      const acs_v4u x = acs_sbuf_load4(image_rsrc(T), off, 0);
-#pragma unroll
-      for (int k = 0; k < NW; ++k) v[k] = x[k];
-    } else {
-      const acs_v2u x = acs_sbuf_load2(image_rsrc(T), off, 0);
-#pragma unroll
-      for (int k = 0; k < NW; ++k) v[k] = x[k];
-    }
-    __builtin_memcpy(&out, v, sizeof(X));
-    return out;
-  }
-#endif
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
   uint32_t v[NW];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -315,6 +254,7 @@ ACS_FN X load_words(const Tables& T, const X* p) {
 #pragma unroll
   for (int k = 0; k < NW; ++k) v[k] = w[k];
 #endif
+  X out;
   __builtin_memcpy(&out, v, sizeof(X));
   return out;
 }
@@ -443,7 +383,7 @@ struct Filter {
   // role associations (TF_SUBJ_ROLE) — else both class rows of a composed request hold the same
   // verdict (they differ only in the role) and the second is not read
   ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false, bool roles = true) const {
-    return vok ? compose_verdict(row[wv + sec + w], roles || !ACS_VERDICT_ROLES ? row2 : nullptr, wv + sec + w, conj)
+    return vok ? compose_verdict(row[wv + sec + w], roles ? row2 : nullptr, wv + sec + w, conj)
                : 0u;
   }
   ACS_FN bool verdict(uint32_t sec, uint32_t i, bool conj = false, bool roles = true) const {
@@ -518,7 +458,7 @@ struct FilterLds {
   // class rows hold the same verdict (same entity column and action, another role) and the
   // second row is not read
   ACS_FN uint32_t vword(uint32_t sec, uint32_t w, bool conj = false, bool roles = true) const {
-    const uint32_t* o2 = roles || !ACS_VERDICT_ROLES ? own2 : nullptr;
+    const uint32_t* o2 = roles ? own2 : nullptr;
 #if defined(ACS_OP_COUNT)
     ACS_OPC(single ? OP_V_LDS : OP_V_OWN);
     if (o2) ACS_OPC(OP_V_OWN2);
@@ -562,7 +502,6 @@ template <class FL>
 struct CandRangeRev {
   const FL& F;
   uint32_t off, b, lo, base, bits;  // lo: base of the word holding index b (the last word read)
-  const uint32_t* drop = nullptr;   // drop_clean: indices to leave out of every word from now on
   ACS_FN CandRangeRev(const FL& f, uint32_t section_off, uint32_t b_, uint32_t e)
       : F(f), off(section_off), b(b_), lo(b_ & ~31u), base(b_ & ~31u), bits(0) {
     if (b < e) {
@@ -584,17 +523,7 @@ struct CandRangeRev {
       if (base <= lo) return false;
       base -= 32;
       bits = F.word(off + (base >> 5));
-      if (drop) {
-        ACS_SCAN(4);
-        bits &= ~drop[wave_uniform(base >> 5)];
-      }
     }
-  }
-  // leave the indices set in `d` (a bit row over the range) out of the rest of the walk
-  ACS_FN void drop_clean(const uint32_t* d) {
-    drop = d;
-    ACS_SCAN(4);
-    bits &= ~d[wave_uniform(base >> 5)];
   }
 };
 
@@ -975,6 +904,101 @@ ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, boo
   return resource_match(t, R, eff, true, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
 }
 
+#ifndef ACS_FUSED_RETRY
+#define ACS_FUSED_RETRY 1
+#endif
+// isAllowed's rule targets (accessController.ts:214-219): the exact resourceAttributesMatch and,
+// when it is false, the RegExp retry — here both in ONE pass over the (request attribute, rule
+// attribute) pairs, each mode with its own state machine (resource_match above, wia false, no
+// log).  The exact mode never throws; its result wins when true, else the RegExp mode's result
+// (an error included) is the answer, as in the two-call form.  The RegExp cells are read even
+// when the exact mode matches (one per entity pair); the request attributes are read once.
+template <class RQ>
+ACS_FN tri resource_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, bool rpe) {
+  if (t.tflags & TF_RES_EMPTY) return 1;
+  const RuleResAttr* ra = R.T.rres + t.res_off;
+  const uint32_t ent = (R.h.flags >> RQ_ENT_SHIFT) & 7u;
+  if ((t.tflags & TF_RES_ENT_ONLY) && ent != 7u) {  // the entity-only form: exact, then RegExp
+    const tri m = resource_match(t, R, effect, false, false, 0, R.h.nres, rpe, nullptr);
+    return m != 0 ? m : resource_match(t, R, effect, true, false, 0, R.h.nres, rpe, nullptr);
+  }
+  bool rp = false;
+  bool em_x = false, pm_x = false, om_x = false, sd_x = true, done_x = false;  // exact mode
+  bool em_r = false, pm_r = false, sd_r = true, done_r = false;                // RegExp mode
+  tri res_r = 0;
+  int ent_j = 0;
+  RuleResAttr rc[ACS_RA_CACHE > 0 ? ACS_RA_CACHE : 1];
+#pragma unroll
+  for (int k = 0; k < ACS_RA_CACHE; ++k)
+    if (k < (int)t.res_n) rc[k] = load_words(R.T, ra + k);
+  for (int j = 0; j < (int)R.h.nres && !(done_x && done_r); ++j) {
+    const ReqRes q = R.res(j);
+    pm_x = pm_r = false;
+    auto step = [&](const RuleResAttr& r) {
+      if (r.kind & K_PROP) rp = true;
+      if (!done_x) {
+        if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
+          em_x = true;
+          ent_j = j;
+        } else if ((q.kind & K_OP) && (r.kind & K_OP) && q.value == r.value) {
+          om_x = true;
+        } else if (em_x && (q.kind & K_PROP) && (r.kind & K_PROP)) {
+          if ((q.contains >> ent_j) & 1u) {
+            if (r.value == q.value) pm_x = true;
+          } else if (effect == EFF_PERMIT) {
+            pm_x = true;
+          }
+        }
+      }
+      if (!done_r) {
+        if ((q.kind & K_ENT) && (r.kind & K_ENT)) {
+          const uint8_t c = R.rx(q.col, r.row);
+          if (c & (RX_THROW_TYPE | RX_THROW_SYNTAX | RX_HOST)) {
+            res_r = (c & RX_THROW_TYPE) ? -(tri)ERR_TYPE : (c & RX_THROW_SYNTAX) ? -(tri)ERR_REGEX_SYNTAX
+                                                                                 : -(tri)ERR_REGEX_HOST;
+            done_r = true;
+          } else {
+            if (c & RX_RESET) em_r = false;
+            if (c & RX_HIT) em_r = true;
+          }
+        } else if (em_r && (q.kind & K_PROP) && (r.kind & K_PROP)) {
+          if (r.hash_sfx == q.hash_sfx) pm_r = true;
+        }
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < ACS_RA_CACHE; ++k)
+      if (k < (int)t.res_n) step(rc[k]);
+    for (uint32_t k = ACS_RA_CACHE; k < t.res_n; ++k) step(load_words(R.T, ra + wave_uniform(k)));
+    const bool scope = (q.kind & K_PROP) || !rpe;
+    if (!done_x) {
+      if (effect == EFF_DENY && scope && em_x && rp && pm_x) sd_x = false;
+      if (effect == EFF_PERMIT && scope && em_x && rp && !pm_x) done_x = true;  // exact: false
+    }
+    if (!done_r) {
+      if (effect == EFF_DENY && scope && em_r && rp && pm_r) sd_r = false;
+      if (effect == EFF_PERMIT && scope && em_r && rp && !pm_r) done_r = true;  // RegExp: false (res_r 0)
+    }
+  }
+  if (!done_x && !(sd_x && rp && rpe && effect == EFF_DENY && !pm_x) && (em_x || om_x)) return 1;
+  if (done_r) return res_r;
+  if (sd_r && rp && rpe && effect == EFF_DENY && !pm_r) return 0;
+  return em_r ? 1 : 0;
+}
+
+// target_match_retry for isAllowed (no obligations): one pass for both resource modes
+template <class RQ>
+ACS_FN tri target_match_retry_k1(const NodeRec& t, const RQ& R, uint8_t effect) {
+#if ACS_FUSED_RETRY
+  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
+  if (!subject_match(t, R)) return 0;
+  if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
+  return resource_match_retry(t, R, effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect, R.flag(RQ_ANY_PROP));
+#else
+  return target_match_retry(t, R, effect, false, nullptr);
+#endif
+}
+
 // ------------------------------------------------------------------ checkHierarchicalScope
 ACS_FN const uint32_t* slot_rec(const ReqCtx& R, uint32_t slot) { return R.ar() + R.slotoff()[slot]; }
 
@@ -1353,12 +1377,12 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
 #if defined(ACS_OP_COUNT)
         if (!vt) ACS_OPC(OP_RULE_TM);
 #endif
-        m = vt ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
+        m = vt ? 1 : target_match_retry_k1(Q, R, Q.effect);
 #if ACS_AB_PROBE_TM2
         if (!vt) {
           NodeRec Q2 = Q;
           Q2.role ^= acs_opaque0();
-          const tri m2 = target_match_retry(Q2, R, Q.effect, false, nullptr);
+          const tri m2 = target_match_retry_k1(Q2, R, Q.effect);
           m = m2 == m ? m : m2;
         }
 #endif
@@ -1464,45 +1488,8 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
   bool have_ev = false;
   CandRangeRev sets(F, F.wsu, 0, T.n_sets);  // the useful sets (candidates.py), descending
   uint32_t s;
-#if ACS_WAVE_CLEAN_SKIP
-  // Once every active lane of the wave is safe and below its deciding set (or an event), each
-  // skips the clean sets (NF_CLEAN): the walk then drops them a word at a time, from the event
-  // index's clean bits, instead of loading each one's record to find it clean (c3adv: 18 of the
-  // 22 useful sets a wave visits, r05_k)
-  const uint32_t* clean_rows = T.ev_index ? T.ev_index + event_index_clean_off(T.n_sets, T.n_pols, T.n_rules) : nullptr;
-  bool wave_below = clean_rows == nullptr;
-#endif
   uint32_t own_w = 0xFFFFFFFFu, own_bits = 0;  // SK: the lane's own useful-set word last read
-#if ACS_CLEAN_BITS
-  uint32_t clean_w = 0xFFFFFFFFu, clean_bits = 0;  // the event index's clean-set word last read
-  const uint32_t* clean_sec =
-      ACS_CLEAN_BITS && T.ev_index ? T.ev_index + event_index_clean_off(T.n_sets, T.n_pols, T.n_rules) : nullptr;
-#endif
   while (sets.next(s)) {
-#if ACS_WAVE_CLEAN_SKIP
-    // (at the top of the body: every lane still walking is active here — a lane that leaves an
-    // iteration early by `continue` would be missing from the vote further down)
-    if (!wave_below && wave_all((have_ev || last_set) && safe)) {
-      wave_below = true;
-      sets.drop_clean(clean_rows);
-    }
-#endif
-#if ACS_CLEAN_BITS
-    // below the deciding set (or an event) only an event can change the record, and a clean set
-    // cannot raise one for a safe request: skip it — from the event index's clean bits, without
-    // loading its record (the unclean ones below are walked)
-    if ((have_ev || last_set) && safe && clean_sec) {
-      if ((s >> 5) != clean_w) {
-        clean_w = s >> 5;
-        ACS_SCAN(4);
-        clean_bits = clean_sec[wave_uniform(clean_w)];
-      }
-      if ((clean_bits >> (s & 31u)) & 1u) {
-        ACS_OPC(OP_SET_SKIP);
-        continue;
-      }
-    }
-#endif
     if constexpr (SK && (ACS_OWN_SKIP & 4)) {
       // the wave walks the union of its lanes' useful sets; a set outside this lane's own useful
       // row cannot change its record (candidates.py: useful sections), so the lane leaves it —
@@ -1743,11 +1730,7 @@ ACS_FN Decision what_is_allowed_t(const RQ& R, const FL& F, const BitsLayout& BL
         uint32_t m = F.word(F.wr + w);
         if (base < rb) m &= ~0u << (rb & 31u);
         if (re - base < 32u) m &= (1u << (re - base)) - 1u;
-#if ACS_K2_OWN_SKIP
-        const uint32_t mine = m & F.own_word(F.wr + w);  // this lane's own candidates (the rest is inert for it)
-#else
         const uint32_t mine = m;
-#endif
         const uint32_t known = mine & F.vword(4 * WP, w);  // this lane's
         if (known) {
           bits.template set<2>(BL.wr + w, known);
@@ -1951,11 +1934,7 @@ ACS_FN bool what_is_allowed_tpl(const RQ& R, const TplLayout& TL, const BitsLayo
   const Tables& T = R.T;
   const uint32_t MW = (TL.flags - TL.mask);  // mask words (padded)
   ACS_OPC(OP_TPL_REQ);
-#if defined(ACS_AB_TPL_NO_WORK)  // timing A/B only (wrong rows): the template copy alone
-  for (uint32_t k = 0; k < 0; ++k) {
-#else
   for (uint32_t k = 0; k < MW; ++k) {
-#endif
     ACS_SCAN(t2 ? 8 : 4);
     uint32_t u = wave_or(t1[TL.mask + k] | (t2 ? t2[TL.mask + k] : 0u));
     while (u) {

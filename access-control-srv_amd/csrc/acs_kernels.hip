@@ -383,49 +383,19 @@ __global__ __launch_bounds__(CS_THREADS) void class_scatter_kernel(const uint32_
 // form); for longer rows (large stores) a B.lds_pref-word union prefix — the set and policy
 // sections, at most LDS_FILTER_WORDS — while rule words come from the lanes' own rows.
 constexpr uint32_t LDS_FILTER_WORDS = 1024;
-#ifndef ACS_SORT_ROLE_MAJOR_DEFAULT
-#define ACS_SORT_ROLE_MAJOR_DEFAULT 1  // c5 A/B: 269 ms class-major, 244 ms role-major (r02_h)
-#endif
 // OR the second class rows of the wave's composed lanes (ReqLine.cls2 = c2, 1 + class) into
 // its LDS row, words [0, LW); *any: the wave holds a composed lane.  False when one names a row
 // outside the batch (the wave then runs unfiltered).
-// lds[w] |= row[w] for w = lane, lane + 64, ... < LW.  ACS_ROW_UNROLL (A/B, off): eight loads in
-// flight per lane before the ORs — slower (c3 10M K1 3.08 vs 2.93 ms, c3 131,072 0.387 vs 0.368;
-// c5 1M 3.00 vs 3.03, c4 equal; r05_x)
-#ifndef ACS_ROW_UNROLL
-#define ACS_ROW_UNROLL 0
-#endif
+// lds[w] |= row[w] for w = lane, lane + 64, ... < LW.  (Rejected A/B, r05_x: eight loads in flight
+// per lane before the ORs — c3 10M K1 3.08 vs 2.93 ms, c3 131,072 0.387 vs 0.368.)
 __device__ inline void lds_or_row(uint32_t* lds, const uint32_t* __restrict__ row, uint32_t LW, uint32_t lane) {
-  uint32_t w = lane;
-#if ACS_ROW_UNROLL
-  for (; w + 7u * 64u < LW; w += 8u * 64u) {
-    uint32_t v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = row[w + 64u * k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) lds[w + 64u * k] |= v[k];
-  }
-#endif
-  for (; w < LW; w += 64u) lds[w] |= row[w];
+  for (uint32_t w = lane; w < LW; w += 64u) lds[w] |= row[w];
 }
 
 // the same with the row AND-ed with a role-factor row (or the OR of two)
 __device__ inline void lds_or_row_roles(uint32_t* lds, const uint32_t* __restrict__ row, const uint32_t* q1,
                                         const uint32_t* q2, uint32_t LW, uint32_t lane) {
-  uint32_t w = lane;
-#if ACS_ROW_UNROLL
-  for (; w + 3u * 64u < LW; w += 4u * 64u) {
-    uint32_t v[4], m[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = row[w + 64u * k];
-      m[k] = role_word(q1, q2, w + 64u * k);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lds[w + 64u * k] |= v[k] & m[k];
-  }
-#endif
-  for (; w < LW; w += 64u) lds[w] |= row[w] & role_word(q1, q2, w);
+  for (uint32_t w = lane; w < LW; w += 64u) lds[w] |= row[w] & role_word(q1, q2, w);
 }
 
 __device__ inline bool or_second_rows(const Batch& B, bool valid, uint32_t c2, uint32_t* lds, uint32_t LW, bool* any) {
@@ -616,51 +586,6 @@ __device__ inline const ReqLine* lane_line(const Batch& B, bool in, uint32_t i) 
   return CB ? B.lines + i : (in && B.lines ? B.lines + i : nullptr);  // one gather for the first rows
 }
 
-#ifndef ACS_NT_LINES
-#define ACS_NT_LINES 0  // A/B (off): slower, c3 10M K1 3.125 vs 2.930 ms, c5 3.115 vs 2.999 (r05_y)
-#endif
-
-// A 16-B record read once (request line parts): A/B ACS_NT_LINES reads it non-temporally, so
-// the streamed lines do not displace the tables and class rows in L2
-template <class T16>
-__device__ inline T16 line_load(const T16* p) {
-  static_assert(sizeof(T16) == 16, "16-B record");
-#if ACS_NT_LINES
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  T16 out;
-  __builtin_memcpy(&out, &v, 16);
-  return out;
-#else
-  return *p;
-#endif
-}
-// The tile a block takes.  Blocks reach the 8 XCDs round-robin (block b on XCD b % 8), so
-// neighbouring tiles of the coherence order — the same classes, the same table nodes — would
-// land on eight different L2s.  G > 0 gives each XCD runs of G consecutive tiles, the runs
-// interleaved over the XCDs (load stays balanced, unlike whole XCD-contiguous ranges, r04_j);
-// the tail beyond the last full 8·G tiles keeps the identity.  Same-call A/Bs: K1 with G = 16
-// c3 10M 2.886 vs 2.930 ms (r05_y) and 2.909 vs 2.923 (r05_z), but c3r1 1M 0.415 vs 0.399 and
-// c2 0.129 vs 0.127 (r05_z): within the boxes' noise, so off; K2 slower with any G (c4 4.14 vs
-// 4.02 at 16).
-#ifndef ACS_XCD_GROUP_K1
-#define ACS_XCD_GROUP_K1 0
-#endif
-#ifndef ACS_XCD_GROUP_K2
-#define ACS_XCD_GROUP_K2 0
-#endif
-template <uint32_t G>
-__device__ inline uint32_t xcd_tile(uint32_t b, uint32_t nb) {
-  if constexpr (G == 0) {
-    (void)nb;
-    return b;
-  } else {
-    constexpr uint32_t SPAN = 8u * G;
-    if (b >= nb / SPAN * SPAN) return b;
-    const uint32_t x = b & 7u, i = b >> 3;
-    return (i / G) * SPAN + x * G + (i % G);
-  }
-}
 
 // 1 + the lane's second class (composed class rows; 0: none)
 __device__ inline uint32_t lane_cls2(const ReqLine* ln, bool in) { return in && ln ? ln->cls2 : 0u; }
@@ -688,13 +613,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile<ACS_XCD_GROUP_K1>(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
   const ReqLine* ln = lane_line<CB>(B, in, i);
   ReqHdr h{};
-  if (in) h = ln ? line_load(&ln->h) : B.hdr[i];
+  if (in) h = ln ? ln->h : B.hdr[i];
   bool done = true;
   Decision d{};
   if (in) d = early_decision(h, &done);
@@ -719,7 +644,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
     const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? line_load(&ln->res[j]) : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
+    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
 #if defined(ACS_PHASE_PROF)
     const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
     d = is_allowed_t<AN, SK>(R, F);
@@ -751,38 +676,20 @@ struct LdsAcc {
   uint32_t* rec;
   __device__ void or_bits(uint32_t w, uint32_t bit) { atomicOr(rec + w, bit); }
 };
-// Requests per class row (a composed request counts for both of its rows).
-template <bool CB>
-__global__ __launch_bounds__(BLOCK) void tpl_count_kernel(Batch B, uint32_t* __restrict__ cnt) {
-  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-  if (i >= B.n) return;
-  const ReqLine* ln = lane_line<CB>(B, true, i);
-  const ReqHdr h = ln ? ln->h : B.hdr[i];
-  const uint32_t c1 = request_pcol(h), c2 = lane_cls2(ln, true);
-  if (c1 < B.cand_rows) atomicAdd(cnt + c1, 1u);
-  if (c2 && c2 - 1u < B.cand_rows) atomicAdd(cnt + c2 - 1u, 1u);
-}
-
-// cnt / min_reqs: a class row with fewer requests than min_reqs gets no template (its flags word
-// 0; its requests take the full walk) — a template costs about one wave's walk of the class's
-// candidate sets, and it saves per request (c4 at 131,072 requests: 13,725 classes, median 2
-// requests each)
 // LDS writes of this wave's lanes visible to its other lanes (waves that share no LDS)
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
+// Every class row of the batch gets a template.  (Rejected A/B, r05_i: a request-count gate, rows
+// of fewer than 32 / 128 requests untemplated — c4 1M K2 8.75 vs 4.01 ms: most waves then hold a
+// lane whose class went untemplated and pay the full walk besides.)
 __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, TplLayout TL, BitsLayout BL,
-                                                             const uint32_t* __restrict__ cnt, uint32_t min_reqs,
                                                              uint32_t* __restrict__ out) {
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t c = blockIdx.x * (BLOCK / 64) + wave;
   if (c >= B.cand_rows) return;  // the waves share no LDS: they sync alone (wave_sync)
-  if (cnt && cnt[c] < min_reqs) {
-    if (lane == 0) out[(size_t)c * TL.stride + TL.flags] = 0u;
-    return;
-  }
   uint32_t* rec = acs_dyn_lds + wave * TL.stride;
   for (uint32_t w = lane; w < TL.stride; w += 64) rec[w] = 0u;
   wave_sync();
@@ -877,22 +784,13 @@ struct SparseTplSink {
     flush<2>();
   }
 };
-#ifndef ACS_TPL_WAVE_COPY
-#define ACS_TPL_WAVE_COPY 1
-#endif
-
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
 // K2 occupancy A/B (5/6/8 waves per SIMD: 96/80/64 VGPRs with spills) measured no gain on c4
-// (6.92-6.95 ms vs 6.62, r03_g): the compiler's own 4 waves/SIMD stay.
-#if defined(ACS_K2_WAVES_PER_EU)  // A/B only: K2's occupancy (default: the compiler's, 4 waves/SIMD)
-#define ACS_K2_ATTR __attribute__((amdgpu_waves_per_eu(ACS_K2_WAVES_PER_EU)))
-#else
-#define ACS_K2_ATTR
-#endif
+// (6.92-6.95 ms vs 6.62, r03_g; 3.97 / 4.00 vs 4.03, r05_final): the compiler's own 4 waves/SIMD stay.
 template <class FL, bool CB>
-__global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
+__global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch B, const uint32_t* __restrict__ perm,
                                                                 uint32_t lanes, BitsLayout BL,
                                                                 uint32_t* __restrict__ bits,
                                                                 uint32_t* __restrict__ obl,
@@ -900,7 +798,7 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
                                                                 Decision* __restrict__ out,
                                                                 const uint32_t* __restrict__ tpl, TplLayout TL) {
   __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
-  const uint32_t k = xcd_tile<ACS_XCD_GROUP_K2>(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+  const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
   const uint32_t i = in ? pk : 0u;
@@ -942,7 +840,6 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
     const uint32_t* r1 = t1 ? B.cand + (size_t)c1 * B.cand_words : nullptr;
     const uint32_t* r2 = t2 ? B.cand + (size_t)(c2 - 1u) * B.cand_words : nullptr;
     const bool usable = t1 && !(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags);
-#if ACS_TPL_WAVE_COPY
     // The wave writes its templated lanes' rows one after the other, 16 B per lane per store
     // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane
     // rewrites the chunks of its own row that its work rules add bits to
@@ -967,10 +864,6 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the copy's stores land before the lanes' own
     if (usable) {
       SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
-#else
-    if (usable) {
-      TplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
-#endif
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
       if (what_is_allowed_tpl(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), TL, BL, t1, t2, sink, log)) {
         if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
@@ -980,9 +873,7 @@ __global__ __launch_bounds__(BLOCK) ACS_K2_ATTR void what_is_allowed_kernel(Tabl
     }
   }
   if (__ballot(!done)) {  // the full walk (rewrites a failed template lane's whole row)
-#if ACS_TPL_WAVE_COPY
     if (tpl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // a failed lane's chunks land first
-#endif
     const FL F = FilterMaker<FL>::make(B, !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                        lane_cls2(ln, in && !done), wave_lds_row(B));
     if (!done) {
@@ -1085,6 +976,94 @@ __global__ __launch_bounds__(BLOCK) void max_keys_kernel(uint64_t* __restrict__ 
                                                          uint32_t n) {
   const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
   if (i < n && other[i] > keys[i]) keys[i] = other[i];
+}
+
+// ---------------------------------------------------------------- dense obligation logs
+// The host-buffer whatIsAllowed downloads each request's maskedProperty log only up to its
+// length (obl_n entries of 8 B) instead of the whole OBL_MAX-entry slot: the logs are packed on
+// the device, request by request in index order, and the host places them into the caller's
+// [n][OBL_MAX][2] slots (c4: 16.4 entries per request on average against 128).
+// blk_tot[b] = entries of requests [b * BLOCK, (b + 1) * BLOCK)
+__global__ __launch_bounds__(BLOCK) void obl_block_sums_kernel(const uint32_t* __restrict__ obl_n, uint32_t n,
+                                                               uint32_t* __restrict__ blk_tot) {
+  __shared__ uint32_t ws[BLOCK / 64];
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  uint32_t c = i < n ? min(obl_n[i], (uint32_t)OBL_MAX) : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) t += ws[w];
+    blk_tot[blockIdx.x] = t;
+  }
+}
+
+// In place: blk[b] = entries before block b (exclusive scan, one block, 64-bit safe total in
+// blk[nb] as two words: low, high)
+__global__ __launch_bounds__(BLOCK) void obl_scan_blocks_kernel(uint32_t* __restrict__ blk, uint32_t nb) {
+  __shared__ uint32_t ws[BLOCK / 64];
+  __shared__ unsigned long long carry;
+  if (threadIdx.x == 0) carry = 0ull;
+  __syncthreads();
+  for (uint32_t base = 0; base < nb; base += BLOCK) {
+    const uint32_t b = base + threadIdx.x;
+    const uint32_t v = b < nb ? blk[b] : 0u;
+    uint32_t x = v;  // inclusive scan within the wave
+    const uint32_t lane = threadIdx.x & 63u;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63u) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += ws[w];
+    const unsigned long long c0 = carry;
+    if (b < nb) blk[b] = (uint32_t)(c0 + before + x - v);
+    __syncthreads();
+    if (threadIdx.x == BLOCK - 1) carry = c0 + before + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    blk[nb] = (uint32_t)carry;
+    blk[nb + 1] = (uint32_t)(carry >> 32);
+  }
+}
+
+// dense[blk[b] + ...] = the logs of block b's requests in index order; each thread copies every
+// BLOCK-th entry of the block's concatenated log (a binary search over the block's prefix in LDS
+// finds its request), so the stores are contiguous
+__global__ __launch_bounds__(BLOCK) void obl_pack_kernel(const uint2* __restrict__ obl, const uint32_t* __restrict__ obl_n,
+                                                         uint32_t n, const uint32_t* __restrict__ blk,
+                                                         uint2* __restrict__ dense) {
+  __shared__ uint32_t pre[BLOCK + 1];
+  __shared__ uint32_t ws[BLOCK / 64];
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x, lane = threadIdx.x & 63u;
+  const uint32_t c = i < n ? min(obl_n[i], (uint32_t)OBL_MAX) : 0u;
+  uint32_t x = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63u) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += ws[w];
+  pre[threadIdx.x + 1] = before + x;
+  if (threadIdx.x == 0) pre[0] = 0u;
+  __syncthreads();
+  const uint32_t total = pre[BLOCK];
+  const size_t base = blk[blockIdx.x];
+  for (uint32_t e = threadIdx.x; e < total; e += BLOCK) {
+    uint32_t lo = 0, hi = BLOCK;  // the request r with pre[r] <= e < pre[r + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= e) lo = mid; else hi = mid;
+    }
+    const size_t r = (size_t)blockIdx.x * BLOCK + lo;
+    dense[base + e] = obl[r * OBL_MAX + (e - pre[lo])];
+  }
 }
 
 // ---------------------------------------------------------------- stable selection
@@ -1242,7 +1221,6 @@ FilterForm filter_form(const Batch& B) {
 #define ACS_TARGS_ACL_NONE , true
 #define ACS_TARGS_ACL_PLAIN , false
 #define ACS_TARGS_ACL_PLAIN_SK , false, true
-#define ACS_TARGS_ACL_NONE_SK , true, true
 #define ACS_LAUNCH_FILTERED(kernel, ...) ACS_LAUNCH_FILTERED_X(kernel, ACS_TARGS_NONE, __VA_ARGS__)
 #define ACS_LAUNCH_FILTERED_X(kernel, X, grid, lds, stream, form, compact, ...)                           \
   do {                                                                                                  \
@@ -1290,11 +1268,9 @@ struct Workspace {
   DevBuf sort, img, out;
   DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
   DevBuf tpl;          // whatIsAllowed templates of the batch's class rows
-  DevBuf tcnt;         // requests per class row (the template pass skips the rare classes)
   DevBuf spread;       // a small batch's order spread over more waves (spread_waves)
   void release() {
     tpl.release();
-    tcnt.release();
     spread.release();
     sort.release();
     img.release();
@@ -1313,6 +1289,7 @@ struct acs_tables {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   float last_ms = -1.f;
   int sort = 1;         // coherence sort of each batch (ACS_OPT_SORT)
+  size_t chunk = 262144;  // host-buffer calls: requests per overlapped chunk (ACS_OPT_CHUNK; 0: off)
   uint32_t simds = 0;   // the device's SIMDs (spread_waves; 0 until first asked)
   // the device image as uploaded (acs_compile_update diffs against it): uninitialised storage,
   // 2-MB pages for a large store (every byte is written by compile_image)
@@ -1350,6 +1327,16 @@ struct acs_tables {
   // from several host threads at once (e.g. the N-API addon's libuv pool): one at a time
   Workspace hws;
   Workspace ows;  // acs_overflow_*_device: selection scratch (.out) and the sort (.sort)
+  // host-buffer calls cut into chunks (chunk_run): a workspace and a stream per pipeline slot
+  static constexpr int CHUNK_SLOTS = 2;
+  Workspace cws[CHUNK_SLOTS];
+  hipStream_t cstream[CHUNK_SLOTS] = {};
+  // page-locked host staging of the packed obligation logs, and of the chunks' coherence orders
+  // (chunk_run), both grow-only
+  void* hstage = nullptr;
+  size_t hstage_bytes = 0;
+  uint32_t* hperm = nullptr;
+  size_t hperm_n = 0;
   std::mutex mu;
   uint32_t rx_rows_min = 0;  // regex-matrix rows the rule resource attributes read
   // acs_compile_multi: replicas of the same image on further devices (C0); the host-buffer
@@ -1576,10 +1563,6 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   const size_t ex_words = ev_words + parent_index_words(h.n_pols, h.n_rules);
   const size_t ev_off = align16(up_bytes);
   const size_t img_total = ev_off + ex_words * sizeof(uint32_t);
-  if (img_total > 0xFFFFFF00ull) {  // the kernels may address records by 32-bit offsets into the image
-    fail("acs_compile: device image larger than 4 GB");
-    return nullptr;
-  }
   auto* t = new acs_tables();
   t->device = device;
   t->rx_rows_min = rx_rows_min;
@@ -1716,8 +1699,6 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   // more runs without it (no set is skipped for it; the decisions are the same)
   t->view.ev_index = h.n_rules < (1u << 30) ? (const uint32_t*)(base + ev_off) : nullptr;
   t->view.parents = (const uint32_t*)(base + ev_off) + ev_words;
-  t->view.img = base;
-  t->view.img_bytes = (uint32_t)(img_total + 64);  // the allocation holds img_total + 128 bytes
   t->image_bytes = img_total;
   return t;
 }
@@ -1736,6 +1717,12 @@ void acs_free(acs_tables* t) {
   t->dws.release();
   t->hws.release();
   t->ows.release();
+  for (int k = 0; k < acs_tables::CHUNK_SLOTS; ++k) {
+    t->cws[k].release();
+    if (t->cstream[k]) (void)hipStreamDestroy(t->cstream[k]);
+  }
+  if (t->hstage) (void)hipHostFree(t->hstage);
+  if (t->hperm) (void)hipHostFree(t->hperm);
   for (hipEvent_t e : t->tev)
     if (e) (void)hipEventDestroy(e);
   delete t;
@@ -1775,7 +1762,6 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
     r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
     r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
     r->view.parents = (const uint32_t*)rebase(t->view.parents);
-    r->view.img = (const char*)r->dev;
     r->sort = t->sort;
     t->peers.push_back(r);
   }
@@ -1991,7 +1977,7 @@ static Batch to_batch(const acs_req_batch* b) {
   B.no_cut = ACS_AB_NO_CUT ? 1u : 0u;
   // long rows: the LDS union covers the set and policy sections (rule words: the lanes' rows)
   B.lds_pref = b->cand_wr < LDS_FILTER_WORDS ? b->cand_wr : LDS_FILTER_WORDS;
-  B.role_major = b->role_key && ACS_SORT_ROLE_MAJOR_DEFAULT ? 1u : 0u;
+  B.role_major = b->role_key ? 1u : 0u;  // role-major keys (c5 A/B: 269 ms class-major, 244 ms role-major, r02_h)
   B.cand_rows = b->cand ? b->cand_rows : 0u;
   B.role_key = b->cand ? b->role_key : nullptr;
   B.role_bits = b->role_rows_bits;
@@ -2007,6 +1993,11 @@ int acs_set_option(acs_tables* t, int option, int value) {
   std::lock_guard<std::mutex> lock(t->mu);  // the host-buffer entry points read these under it
   if (option == ACS_OPT_SORT) {
     t->sort = value ? 1 : 0;
+    return 0;
+  }
+  if (option == ACS_OPT_CHUNK) {
+    if (value < 0) return fail("acs_set_option: ACS_OPT_CHUNK must be >= 0");
+    t->chunk = (size_t)value;
     return 0;
   }
   if (option == ACS_OPT_TIMING) {
@@ -2156,9 +2147,6 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 // SIMD of the device:
 // each wave then holds fewer classes (profiles/r05_a: at 131,072 c3 requests every wave lasts
 // about as long as the launch).
-#ifndef ACS_K1_SPREAD_SKIPS
-#define ACS_K1_SPREAD_SKIPS 1  // 0: spread batches take K1's plain instantiation
-#endif
 #ifndef ACS_SPREAD_MIN_L
 // fewest requests per spread wave: c3 K1 at 131,072 / 32,768 / 4,096 requests 0.432 / 0.348 /
 // 0.353 ms at 16, 0.390 / 0.276 / 0.236 at 8, 0.390 / 0.283 / 0.168 at 4 (r05_final/ab_c3_*)
@@ -2166,12 +2154,6 @@ static int batch_order(acs_tables* t, Workspace& W, const acs_req_batch* b, cons
 #endif
 #ifndef ACS_K2_SPREAD_MIN_L
 #define ACS_K2_SPREAD_MIN_L 16  // K2 (c4 131,072: 1.683 ms at 16, 1.875 at 8; r05_o, r05_u)
-#endif
-#ifndef ACS_K1_AN_SK
-#define ACS_K1_AN_SK 0  // A/B: the skips in the ACL_NONE instantiation (c3adv 1M 1.773 vs 1.782 ms, r05_u)
-#endif
-#ifndef ACS_K1_SK_ALWAYS
-#define ACS_K1_SK_ALWAYS 0  // A/B: the skipping instantiation for every plain batch
 #endif
 #ifndef ACS_SPREAD_PER_SIMD
 // 0: off.  c3 131,072 requests: K1 0.814 ms unspread, 0.670 at 4, 0.543 at 8 (r05_e), 0.446 at 16
@@ -2232,16 +2214,12 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
-#if ACS_K1_AN_SK
-  if ((b->hints & ACS_HINT_ACL_NONE) && mixed)
-    ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE_SK, grid, filter_lds_bytes(B), s, filter_form(B),
-                          B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
-  else
-#endif
+  // (Rejected A/Bs: the own-row skips in the ACL_NONE instantiation, c3adv 1M 1.773 vs 1.782 ms,
+  // r05_u; the skipping instantiation for every plain batch, c3 10M 3.10 vs 3.02 ms, r05_j.)
   if (b->hints & ACS_HINT_ACL_NONE)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_NONE, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
-  else if ((mixed || ACS_K1_SK_ALWAYS) && ACS_K1_SPREAD_SKIPS)
+  else if (mixed)
     ACS_LAUNCH_FILTERED_X(is_allowed_kernel, ACS_TARGS_ACL_PLAIN_SK, grid, filter_lds_bytes(B), s, filter_form(B),
                           B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, (Decision*)out);
   else
@@ -2274,13 +2252,6 @@ int acs_kernel_times(acs_tables* t, float* ms, int n) {
   return m;
 }
 
-#ifndef ACS_TPL_MIN_REQS
-// A/B: a class row takes a template only for at least this many requests (1: every row, no
-// count pass).  A threshold measured slower (c4 1M K2: 4.01 ms at 1, 8.75 at 32 and 128; 131k:
-// 1.78 / 2.72 ms; r05_i): most waves then hold a lane whose class (or second class) went
-// untemplated and pay the full walk besides
-#define ACS_TPL_MIN_REQS 1
-#endif
 static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, uint32_t* bits, uint32_t* obl,
                                   uint32_t* obl_n, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
@@ -2294,7 +2265,7 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const TplLayout TL = tpl_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   // templates: batches whose class rows carry verdicts in the LDS form, without a role factor
-  const bool use_tpl = ACS_WIA_TEMPLATES && filter_form(B) == FilterForm::Lds && !B.role_key && B.cand_rows &&
+  const bool use_tpl = filter_form(B) == FilterForm::Lds && !B.role_key && B.cand_rows &&
                        t->view.parents && (size_t)(BLOCK / 64) * TL.stride * 4 <= 64 * 1024;
   const int slot = (int)(t->launches % acs_tables::RING);
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));  // the template pass is part of the timed K2
@@ -2302,20 +2273,8 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   if (use_tpl) {
     if (W.tpl.reserve((size_t)B.cand_rows * TL.stride * sizeof(uint32_t))) return -1;
     tpl = (const uint32_t*)W.tpl.p;
-    const uint32_t* cnt = nullptr;
-    if (ACS_TPL_MIN_REQS > 1) {
-      if (W.tcnt.reserve((size_t)B.cand_rows * sizeof(uint32_t))) return -1;
-      HIP_OK(hipMemsetAsync(W.tcnt.p, 0, (size_t)B.cand_rows * sizeof(uint32_t), s));
-      const dim3 g((unsigned)((B.n + BLOCK - 1) / BLOCK));
-      if (B.hdr == nullptr)
-        hipLaunchKernelGGL(tpl_count_kernel<true>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
-      else
-        hipLaunchKernelGGL(tpl_count_kernel<false>, g, dim3(BLOCK), 0, s, B, (uint32_t*)W.tcnt.p);
-      cnt = (const uint32_t*)W.tcnt.p;
-    }
     hipLaunchKernelGGL(wia_template_kernel, dim3((B.cand_rows + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK),
-                       (size_t)(BLOCK / 64) * TL.stride * 4, s, t->view, B, TL, BL, cnt, (uint32_t)ACS_TPL_MIN_REQS,
-                       (uint32_t*)W.tpl.p);
+                       (size_t)(BLOCK / 64) * TL.stride * 4, s, t->view, B, TL, BL, (uint32_t*)W.tpl.p);
   }
   ACS_LAUNCH_FILTERED(what_is_allowed_kernel, grid, filter_lds_bytes(B), s, filter_form(B), B.hdr == nullptr, t->view, B, perm, (uint32_t)lanes, BL, bits,
                       obl, obl_n, (Decision*)out, tpl, TL);
@@ -2524,8 +2483,11 @@ int upload_batch(Workspace& W, const acs_req_batch* b, acs_req_batch* dev, hipSt
 // regex matrix and class rows.  arena_end: per request, one past its last arena word.
 // sperm: the shard's coherence order (shard-relative indices, the batch's order restricted to
 // the shard) or empty.
+// shared (optional): device copies of the batch-wide sections (regex matrix, class rows, role
+// rows) already uploaded once for every chunk of a call (chunk_run); they are not copied again.
 int upload_shard(Workspace& W, const acs_req_batch* b, size_t lo, size_t hi, const uint32_t* arena_end,
-                 const std::vector<uint32_t>& sperm, acs_req_batch* dev, hipStream_t s) {
+                 const uint32_t* sperm, size_t sperm_n, acs_req_batch* dev, hipStream_t s,
+                 const acs_req_batch* shared = nullptr) {
   size_t plan[4];
   acs_internal_shard_plan(b, lo, hi, arena_end, plan);
   const size_t a0 = plan[0], a1 = plan[1], e0 = plan[2], e1 = plan[3];
@@ -2538,18 +2500,23 @@ int upload_shard(Workspace& W, const acs_req_batch* b, size_t lo, size_t hi, con
   const void* arena_dst = nullptr;
   I.add(b->ext ? b->ext + e0 : (const uint32_t*)b->lines, (e1 - e0) * 4, &ext_dst);
   I.add(b->arena + a0, (a1 - a0) * 4, &arena_dst);
-  I.add(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&I.d.rx);
-  if (b->cand) I.add(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t), (const void**)&I.d.cand);
-  if (b->role_key) {
-    I.add(b->role_key + lo, m * sizeof(uint32_t), (const void**)&I.d.role_key);
-    I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
-          (const void**)&I.d.role_rows_bits);
+  if (shared) {
+    I.d.rx = shared->rx;
+    I.d.cand = shared->cand;
+    I.d.role_rows_bits = shared->role_rows_bits;
+  } else {
+    I.add(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&I.d.rx);
+    if (b->cand) I.add(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t), (const void**)&I.d.cand);
+    if (b->role_key)
+      I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
+            (const void**)&I.d.role_rows_bits);
   }
+  if (b->role_key) I.add(b->role_key + lo, m * sizeof(uint32_t), (const void**)&I.d.role_key);
   I.d.perm = nullptr;
   I.d.perm_lanes = 0;
-  if (!sperm.empty()) {
-    I.add(sperm.data(), sperm.size() * sizeof(uint32_t), (const void**)&I.d.perm);
-    I.d.perm_lanes = sperm.size();
+  if (sperm && sperm_n) {
+    I.add(sperm, sperm_n * sizeof(uint32_t), (const void**)&I.d.perm);
+    I.d.perm_lanes = sperm_n;
   }
   if (W.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
   char* base = (char*)W.img.p;
@@ -2580,6 +2547,182 @@ struct OutLayout {
 
 }  // namespace
 
+// Each of D contiguous shards' coherence order (shard-relative indices): the batch's order
+// restricted to the shard, holes dropped (empty vectors when the batch carries none).
+static std::vector<std::vector<uint32_t>> shard_perms(const acs_req_batch* b, size_t D) {
+  const size_t n = b->n;
+  auto lo_of = [&](size_t k) { return n * k / D; };
+  std::vector<std::vector<uint32_t>> sperm(D);
+  if (!b->perm) return sperm;
+  for (size_t k = 0; k < D; ++k) sperm[k].reserve(lo_of(k + 1) - lo_of(k));
+  for (size_t x = 0; x < b->perm_lanes; ++x) {
+    const uint32_t i = b->perm[x];
+    if (i >= n) continue;
+    size_t k = std::min(D - 1, (size_t)i * D / n);
+    while (k > 0 && i < lo_of(k)) --k;
+    while (k + 1 < D && i >= lo_of(k + 1)) ++k;
+    sperm[k].push_back((uint32_t)(i - lo_of(k)));
+  }
+  return sperm;
+}
+
+// One device, overlapped (host buffers): a large compact batch is cut into K contiguous chunks,
+// each validated, uploaded as a shard (its lines, extension and arena slices, its coherence order)
+// and evaluated on the pipeline slots' streams in turn, so chunk k + 1 is validated and uploaded
+// while chunk k is evaluated and chunk k - 1's results come back (validate, H2D, kernel and D2H
+// of one call were serial before: 17 GB/s effective at c3's 10M requests, BENCH_r05).  Before a
+// slot is reused its stream is drained (its workspace may grow for the next chunk).  On an error
+// the chunks already queued are drained and the outputs of the call are unspecified.
+static constexpr size_t CHUNK_MAX_K = 16;  // chunks per call, at most (t->chunk: requests per chunk, at least)
+static bool chunk_host_batch(const acs_tables* t, const acs_req_batch* b) {
+  return t->chunk && t->peers.empty() && !t->sharded && !b->hdr && b->lines && b->n >= 2 * t->chunk;
+}
+
+// The chunks' coherence orders into the page-locked t->hperm: chunk k's order (the batch's
+// perm restricted to [lo_k, hi_k), chunk-relative, holes dropped) at [lo_k, hi_k), built over the
+// pool in two passes (count per part and chunk, then place), and checked as acs_internal_check_batch2
+// checks a perm: every index < n or a hole, every request exactly once.
+static int chunk_perms(acs_tables* t, const acs_req_batch* b, size_t K) {
+  const size_t n = b->n, L = b->perm_lanes;
+  if (L < n || L > 0xFFFFFFFFull) return fail("batch: perm_lanes");
+  if (t->hperm_n < n) {
+    if (t->hperm) HIP_OK(hipHostFree(t->hperm));
+    t->hperm = nullptr;
+    t->hperm_n = 0;
+    HIP_OK(hipHostMalloc((void**)&t->hperm, (n + n / 8) * sizeof(uint32_t), 0));
+    t->hperm_n = n + n / 8;
+  }
+  auto lo_of = [&](size_t k) { return n * k / K; };
+  auto chunk_of = [&](uint32_t i) {
+    size_t k = std::min(K - 1, (size_t)i * K / n);
+    while (k > 0 && i < lo_of(k)) --k;
+    while (k + 1 < K && i >= lo_of(k + 1)) ++k;
+    return k;
+  };
+  const size_t T = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), L / 65536 + 1}));
+  std::vector<size_t> cnt(T * K, 0);
+  std::atomic<size_t> bad{L};
+  acs_pool::run((int)T, [&](int p) {
+    size_t* c = cnt.data() + (size_t)p * K;
+    for (size_t x = L * p / T; x < L * (p + 1) / T; ++x) {
+      const uint32_t i = b->perm[x];
+      if (i == 0xFFFFFFFFu) continue;
+      if (i >= n) {
+        size_t cur = bad.load();
+        while (x < cur && !bad.compare_exchange_weak(cur, x)) {}
+        return;
+      }
+      ++c[chunk_of(i)];
+    }
+  });
+  if (bad.load() < L) return fail("batch: perm (an index outside the batch, or twice)");
+  for (size_t k = 0; k < K; ++k) {  // per chunk: its parts' positions, and its count
+    size_t at = lo_of(k);
+    for (size_t p = 0; p < T; ++p) {
+      const size_t c = cnt[p * K + k];
+      cnt[p * K + k] = at;
+      at += c;
+    }
+    if (at != lo_of(k + 1)) return fail("batch: perm misses requests (or holds one twice)");
+  }
+  acs_pool::run((int)T, [&](int p) {
+    size_t* pos = cnt.data() + (size_t)p * K;
+    for (size_t x = L * p / T; x < L * (p + 1) / T; ++x) {
+      const uint32_t i = b->perm[x];
+      if (i == 0xFFFFFFFFu) continue;
+      const size_t k = chunk_of(i);
+      t->hperm[pos[k]++] = (uint32_t)(i - lo_of(k));
+    }
+  });
+  // with every chunk's count right, an index twice means another one missing: a bitmap per chunk
+  std::atomic<int> dup{0};
+  acs_pool::run((int)std::min(T, K), [&](int p) {
+    for (size_t k = p; k < K; k += std::min(T, K)) {
+      const size_t lo = lo_of(k), m = lo_of(k + 1) - lo;
+      std::vector<uint64_t> seen((m + 63) / 64, 0);
+      for (size_t x = 0; x < m; ++x) {
+        const uint32_t r = t->hperm[lo + x];
+        if (seen[r >> 6] >> (r & 63) & 1u) {
+          dup = 1;
+          return;
+        }
+        seen[r >> 6] |= 1ull << (r & 63);
+      }
+    }
+  });
+  if (dup) return fail("batch: perm (an index outside the batch, or twice)");
+  return 0;
+}
+
+extern "C++" {
+template <class F>
+static int chunk_run(acs_tables* t, const acs_req_batch* b, const char* what, F chunk) {
+  const size_t n = b->n, K = std::min(CHUNK_MAX_K, n / t->chunk);
+  std::lock_guard<std::mutex> lock(t->mu);
+  HIP_OK(hipSetDevice(t->device));
+  if (b->perm && chunk_perms(t, b, K)) return -1;
+  for (int q = 0; q < acs_tables::CHUNK_SLOTS; ++q)
+    if (!t->cstream[q]) HIP_OK(hipStreamCreateWithFlags(&t->cstream[q], hipStreamNonBlocking));
+  auto drain = [&] {
+    const std::string err = g_err;
+    for (int q = 0; q < acs_tables::CHUNK_SLOTS; ++q) (void)hipStreamSynchronize(t->cstream[q]);
+    g_err = err;
+    return -1;
+  };
+  const std::string sync_msg = std::string(what) + ": device synchronisation failed";
+  // the batch-wide sections (regex matrix, class rows, role rows: c3 10M ~90 MB of class rows),
+  // once per call into the handle's host-path workspace; the other slots wait for them
+  acs_req_batch shared{};
+  {
+    Image I;
+    I.add(b->rx, (size_t)b->rx_cols * b->rx_rows, (const void**)&shared.rx);
+    if (b->cand) I.add(b->cand, (size_t)b->cand_rows * b->cand_words * sizeof(uint32_t), (const void**)&shared.cand);
+    if (b->role_key && b->role_rows_bits)
+      I.add(b->role_rows_bits, (size_t)b->role_rows * b->cand_words * sizeof(uint32_t),
+            (const void**)&shared.role_rows_bits);
+    if (t->hws.img.reserve(I.total ? I.total : IMG_ALIGN)) return -1;
+    char* base = (char*)t->hws.img.p;
+    size_t off = 0;
+    for (const Image::Sec& x : I.secs) {
+      if (x.bytes && hipMemcpyAsync(base + off, x.src, x.bytes, hipMemcpyHostToDevice, t->cstream[0]) != hipSuccess)
+        return fail(sync_msg.c_str()), drain();
+      *x.dst = base + off;
+      off += (x.bytes + IMG_ALIGN - 1) & ~(IMG_ALIGN - 1);
+    }
+    if (hipEventRecord(t->ev0, t->cstream[0]) != hipSuccess) return fail(sync_msg.c_str()), drain();
+    for (int q = 1; q < acs_tables::CHUNK_SLOTS; ++q)
+      if (hipStreamWaitEvent(t->cstream[q], t->ev0, 0) != hipSuccess) return fail(sync_msg.c_str()), drain();
+  }
+  std::vector<uint32_t> arena_end(n / K + 1);
+  for (size_t k = 0; k < K; ++k) {
+    const int q = (int)(k % acs_tables::CHUNK_SLOTS);
+    hipStream_t s = t->cstream[q];
+    const size_t lo = n * k / K, hi = n * (k + 1) / K;
+    // chunk k's requests validated (on the host threads, while the device works on chunk k - 1)
+    acs_req_batch v = *b;
+    v.n = hi - lo;
+    v.lines = (const ReqLine*)b->lines + lo;
+    if (b->role_key) v.role_key = b->role_key + lo;
+    v.perm = nullptr;
+    v.perm_lanes = 0;
+    if (acs_internal_check_batch2(&v, t->view.n_sets, t->view.n_pols, t->view.n_rules, t->rx_rows_min,
+                                  arena_end.data()) ||
+        acs_internal_check_acl_none(&v, t->view.id_user))
+      return drain();
+    if (k >= (size_t)acs_tables::CHUNK_SLOTS && hipStreamSynchronize(s) != hipSuccess)
+      return fail(sync_msg.c_str()), drain();
+    acs_req_batch d;
+    if (upload_shard(t->cws[q], &v, 0, hi - lo, arena_end.data(), b->perm ? t->hperm + lo : nullptr, hi - lo, &d, s,
+                     &shared))
+      return drain();
+    if (chunk(t->cws[q], s, &d, lo, hi)) return drain();
+  }
+  for (int q = 0; q < acs_tables::CHUNK_SLOTS; ++q)
+    if (hipStreamSynchronize(t->cstream[q]) != hipSuccess) return fail(sync_msg.c_str()), drain();
+  return 0;
+}
+}  // extern "C++"
+
 // A compact batch split over the handle and its replicas (acs_compile_multi): contiguous
 // request shards, one per device, each uploaded (its slices only), sorted, decided and
 // downloaded on that device's stream; all devices run concurrently.
@@ -2604,18 +2747,7 @@ static int multi_run(acs_tables* t, const acs_req_batch* b, const uint32_t* aren
   const size_t n = b->n;
   auto lo_of = [&](size_t k) { return n * k / D; };
   // each shard's coherence order: the batch's order restricted to the shard (holes dropped)
-  std::vector<std::vector<uint32_t>> sperm(D);
-  if (b->perm) {
-    for (size_t k = 0; k < D; ++k) sperm[k].reserve(lo_of(k + 1) - lo_of(k));
-    for (size_t x = 0; x < b->perm_lanes; ++x) {
-      const uint32_t i = b->perm[x];
-      if (i >= n) continue;
-      size_t k = std::min(D - 1, (size_t)i * D / n);
-      while (k > 0 && i < lo_of(k)) --k;
-      while (k + 1 < D && i >= lo_of(k + 1)) ++k;
-      sperm[k].push_back((uint32_t)(i - lo_of(k)));
-    }
-  }
+  const std::vector<std::vector<uint32_t>> sperm = shard_perms(b, D);
   std::vector<std::unique_lock<std::mutex>> locks;
   for (size_t k = 0; k < D; ++k) locks.emplace_back(dev[k]->mu);
   size_t launched = 0;  // devices with work queued into the caller's buffers
@@ -2636,7 +2768,7 @@ static int multi_run(acs_tables* t, const acs_req_batch* b, const uint32_t* aren
     if (hipSetDevice(T->device) != hipSuccess) return fail(sync_msg.c_str()), drain();
     launched = k + 1;  // the copies below are queued on T's stream from here on
     acs_req_batch d;
-    if (upload_shard(T->hws, b, lo, hi, arena_end, sperm[k], &d, T->stream)) return drain();
+    if (upload_shard(T->hws, b, lo, hi, arena_end, sperm[k].data(), sperm[k].size(), &d, T->stream)) return drain();
     if (shard(T, &d, lo, hi)) return drain();
   }
   for (size_t k = 0; k < D; ++k) {
@@ -3065,6 +3197,17 @@ int acs_is_allowed(acs_tables* t, const acs_req_batch* b, acs_decision* out) {
       return -1;
     return multi_is_allowed(t, b, out, arena_end.data());
   }
+  if (chunk_host_batch(t, b)) {
+    if (!b->lines) return fail("batch: compact batch without request lines");
+    return chunk_run(t, b, "acs_is_allowed",
+                     [&](Workspace& W, hipStream_t s, const acs_req_batch* d, size_t lo, size_t hi) {
+      if (W.out.reserve((hi - lo) * sizeof(Decision))) return -1;
+      if (is_allowed_launch(t, W, d, (acs_decision*)W.out.p, s)) return -1;
+      if (hipMemcpyAsync(out + lo, W.out.p, (hi - lo) * sizeof(Decision), hipMemcpyDeviceToHost, s) != hipSuccess)
+        return fail("acs_is_allowed: result copy failed");
+      return 0;
+    });
+  }
   if (check_batch(t, b)) return -1;
   std::lock_guard<std::mutex> lock(t->mu);
   HIP_OK(hipSetDevice(t->device));
@@ -3099,10 +3242,16 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
   HIP_OK(hipSetDevice(t->device));
   acs_req_batch d;
   if (upload_batch(t->hws, b, &d, t->stream)) return -1;
-  const size_t words = acs_wia_words_per_request(t);
+  const size_t n = b->n, words = acs_wia_words_per_request(t);
+  // the logs come back packed (obl_n entries per request; see obl_pack_kernel) when the packed
+  // offsets fit 32 bits
+  const bool dense = n * (size_t)OBL_MAX < 0xFFFFFFFFull;
+  const uint32_t nb = (uint32_t)((n + BLOCK - 1) / BLOCK);
   OutLayout O;
-  const size_t o_bits = O.put(b->n * words * sizeof(uint32_t)), o_obl = O.put(b->n * 2 * OBL_MAX * sizeof(uint32_t));
-  const size_t o_n = O.put(b->n * sizeof(uint32_t)), o_out = O.put(b->n * sizeof(Decision));
+  const size_t o_bits = O.put(n * words * sizeof(uint32_t)), o_obl = O.put(n * 2 * OBL_MAX * sizeof(uint32_t));
+  const size_t o_n = O.put(n * sizeof(uint32_t)), o_out = O.put(n * sizeof(Decision));
+  const size_t o_blk = dense ? O.put(((size_t)nb + 2) * sizeof(uint32_t)) : 0;
+  const size_t o_dense = dense ? O.put(n * 2 * OBL_MAX * sizeof(uint32_t)) : 0;
   if (t->hws.out.reserve(O.total)) return -1;
   char* ob = (char*)t->hws.out.p;
   HIP_OK(hipEventRecord(t->ev0, t->stream));
@@ -3110,11 +3259,60 @@ int acs_what_is_allowed(acs_tables* t, const acs_req_batch* b, uint32_t* bits, u
                              (acs_decision*)(ob + o_out), t->stream))
     return -1;
   HIP_OK(hipEventRecord(t->ev1, t->stream));
-  HIP_OK(hipMemcpyAsync(bits, ob + o_bits, b->n * words * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl, ob + o_obl, b->n * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(obl_n, ob + o_n, b->n * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
-  HIP_OK(hipMemcpyAsync(out, ob + o_out, b->n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(bits, ob + o_bits, n * words * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(obl_n, ob + o_n, n * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+  HIP_OK(hipMemcpyAsync(out, ob + o_out, n * sizeof(Decision), hipMemcpyDeviceToHost, t->stream));
+  if (!dense) {
+    HIP_OK(hipMemcpyAsync(obl, ob + o_obl, n * 2 * OBL_MAX * sizeof(uint32_t), hipMemcpyDeviceToHost, t->stream));
+    HIP_OK(hipStreamSynchronize(t->stream));
+    HIP_OK(hipEventElapsedTime(&t->last_ms, t->ev0, t->ev1));
+    return 0;
+  }
+  uint32_t* blk = (uint32_t*)(ob + o_blk);
+  hipLaunchKernelGGL(obl_block_sums_kernel, dim3(nb), dim3(BLOCK), 0, t->stream, (const uint32_t*)(ob + o_n),
+                     (uint32_t)n, blk);
+  hipLaunchKernelGGL(obl_scan_blocks_kernel, dim3(1), dim3(BLOCK), 0, t->stream, blk, nb);
+  hipLaunchKernelGGL(obl_pack_kernel, dim3(nb), dim3(BLOCK), 0, t->stream, (const uint2*)(ob + o_obl),
+                     (const uint32_t*)(ob + o_n), (uint32_t)n, (const uint32_t*)blk, (uint2*)(ob + o_dense));
+  HIP_OK(hipGetLastError());
+  uint32_t tot[2] = {0, 0};
+  HIP_OK(hipMemcpyAsync(tot, blk + nb, sizeof tot, hipMemcpyDeviceToHost, t->stream));
   HIP_OK(hipStreamSynchronize(t->stream));
+  const size_t total = (size_t)tot[0] | ((size_t)tot[1] << 32);
+  if (total > n * (size_t)OBL_MAX) return fail("acs_what_is_allowed: packed log size out of range");
+  if (total * 8 > t->hstage_bytes) {
+    if (t->hstage) HIP_OK(hipHostFree(t->hstage));
+    t->hstage = nullptr;
+    t->hstage_bytes = 0;
+    const size_t want = total * 8 + total * 8 / 8 + 4096;
+    HIP_OK(hipHostMalloc(&t->hstage, want, 0));
+    t->hstage_bytes = want;
+  }
+  if (total) {
+    HIP_OK(hipMemcpyAsync(t->hstage, ob + o_dense, total * 8, hipMemcpyDeviceToHost, t->stream));
+    HIP_OK(hipStreamSynchronize(t->stream));
+  }
+  // each request's entries into its OBL_MAX-entry slot (its offset: the counts before it)
+  const size_t T = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+  const size_t parts = std::min(T, (n + 65535) / 65536);
+  std::vector<size_t> start(parts + 1, 0);
+  for (size_t p = 0; p < parts; ++p) {  // entries before each part (one pass over obl_n per part)
+    const size_t lo = n * p / parts, hi = n * (p + 1) / parts;
+    size_t c = 0;
+    for (size_t i = lo; i < hi; ++i) c += std::min<uint32_t>(obl_n[i], OBL_MAX);
+    start[p + 1] = c;
+  }
+  for (size_t p = 0; p < parts; ++p) start[p + 1] += start[p];
+  if (start[parts] != total) return fail("acs_what_is_allowed: packed log size mismatch");
+  const uint64_t* src = (const uint64_t*)t->hstage;
+  acs_pool::run((int)parts, [&](int p) {
+    size_t at = start[p];
+    for (size_t i = n * p / parts, hi = n * (p + 1) / parts; i < hi; ++i) {
+      const uint32_t c = std::min<uint32_t>(obl_n[i], OBL_MAX);
+      if (c) std::memcpy(obl + i * 2 * OBL_MAX, src + at, (size_t)c * 8);
+      at += c;
+    }
+  });
   HIP_OK(hipEventElapsedTime(&t->last_ms, t->ev0, t->ev1));
   return 0;
 }

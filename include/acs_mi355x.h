@@ -240,6 +240,11 @@ int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* de
  * acs_is_allowed_device, K2 of acs_what_is_allowed_device); acs_kernel_times returns the durations (ms) of the last n
  * launches (a ring of 256), returning how many were written. */
 #define ACS_OPT_TIMING 2
+/* ACS_OPT_CHUNK (default 262144): acs_is_allowed on one device cuts a compact batch of at least
+ * twice this many requests into up to 16 contiguous chunks and overlaps chunk k + 1's upload
+ * with chunk k's evaluation and chunk k - 1's download (two streams); 0: one upload, one
+ * launch, one download.  The records are the same either way. */
+#define ACS_OPT_CHUNK 3
 int acs_set_option(acs_tables* t, int option, int value);
 int acs_kernel_times(acs_tables* t, float* ms, int n);
 

@@ -146,3 +146,51 @@ def test_pipeline_error_mid_run_then_single_request_gpu():
     p.close()
     codec.close()
     t.close()
+
+
+def test_chunked_host_path_gpu(monkeypatch):
+    """acs_is_allowed on one device in overlapped chunks (ACS_OPT_CHUNK: each chunk uploaded as a
+    shard, the class / role rows once per call, two streams) equals one upload and one launch:
+    a c3 batch with composed rows and the encoder's coherence order in 2 and 16 chunks, a
+    role-factor batch, and random stores' wide requests (extension records, arena tails) in
+    chunks of a few requests."""
+    cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 600_000, "c3", seed=31, second_role=0.5)
+    t = native.Tables(compiler.store_blob(cs), 0)
+    t.set_chunk(0)
+    want = t.is_allowed(sb.batch, compact=True)
+    dev = decisions_from_tensor(is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True)))
+    assert np.array_equal(_u64(want), _u64(dev))
+    for c in (262144, 30_000):
+        t.set_chunk(c)
+        assert np.array_equal(_u64(t.is_allowed(sb.batch, compact=True)), _u64(want)), c
+    t.close()
+    from acs_mi355x import candidates
+    monkeypatch.setattr(candidates, "FORCE_LEVEL", "entity+action")
+    rb = synth.requests(cs, 40_000, "c3", seed=32, tree=synth.OrgTree(fanout=4, depth=5))
+    assert rb.batch.role_key is not None
+    t = native.Tables(compiler.store_blob(cs), 0)
+    t.set_chunk(0)
+    want = t.is_allowed(rb.batch, compact=True)
+    t.set_chunk(4000)
+    assert np.array_equal(_u64(t.is_allowed(rb.batch, compact=True)), _u64(want))
+    t.close()
+    monkeypatch.undo()
+    checked = 0
+    for s in range(1, 80, 3):
+        urns, doc, reqs = randgen.rand_case(s)
+        try:
+            _, rcs = build(urns, doc)
+        except Exception:
+            continue
+        b = encoder.Encoder(rcs).encode(reqs)
+        if b.n < 8:
+            continue
+        t = native.Tables(compiler.store_blob(rcs), 0)
+        t.set_chunk(0)
+        want = t.is_allowed(b, compact=True)
+        t.set_chunk(max(1, b.n // 7))
+        assert np.array_equal(_u64(t.is_allowed(b, compact=True)), _u64(want)), s
+        t.close()
+        checked += 1
+    assert checked >= 10
