@@ -102,6 +102,9 @@ __device__ inline void op_count(int k) {
 #ifndef ACS_AB_PROBE_TM2
 #define ACS_AB_PROBE_TM2 0
 #endif
+#ifndef ACS_AB_PROBE_NR2
+#define ACS_AB_PROBE_NR2 0
+#endif
 ACS_FN uint32_t acs_opaque0() {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t z;
@@ -259,10 +262,19 @@ ACS_FN X load_words(const Tables& T, const X* p) {
   return out;
 }
 
-// Node record `x` of a table section of `n` records.
+// Node record `x` of a table section of `n` records.  (ACS_AB_PROBE_NR2, timing probe: every
+// record read a second time after the first, through an opaque zero offset — the cost of one more
+// dependent record round trip per node visit.)
 ACS_FN NodeRec node_at(const Tables& T, const NodeRec* sec, uint32_t x, uint32_t n) {
   (void)n;
+#if ACS_AB_PROBE_NR2
+  NodeRec a = load_words(T, sec + x);  // the second read depends on the first: one more round trip
+  const NodeRec b = load_words(T, sec + x + (a.child_end & acs_opaque0()));
+  a.child_begin = b.child_begin == a.child_begin ? a.child_begin : b.child_begin;
+  return a;
+#else
   return load_words(T, sec + x);
+#endif
 }
 
 // Rule r.  The device image stores each rule in a 128-B line (record + inline attributes).
@@ -893,6 +905,9 @@ ACS_FN tri target_match(const NodeRec& t, const RQ& R, uint8_t effect, bool rege
 
 // Rule targets: the exact pass, then the RegExp retry (accessController.ts:214-219, 400-409).
 // Subjects and actions do not depend on the mode, so when they fail both passes are false.
+// (Rejected A/B, r06_c: both resource modes in one pass over the attribute pairs — the RegExp
+// cells then read even when the exact pass matches — c3 10M K1 3.25 vs 2.93 ms, c3r1 0.452 vs
+// 0.404, c3adv 1.96 vs 1.75.)
 template <class RQ>
 ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, bool wia, OblLog* obl) {
   if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
@@ -902,101 +917,6 @@ ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, boo
   const tri m = resource_match(t, R, eff, false, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
   if (m != 0) return m;
   return resource_match(t, R, eff, true, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
-}
-
-#ifndef ACS_FUSED_RETRY
-#define ACS_FUSED_RETRY 1
-#endif
-// isAllowed's rule targets (accessController.ts:214-219): the exact resourceAttributesMatch and,
-// when it is false, the RegExp retry — here both in ONE pass over the (request attribute, rule
-// attribute) pairs, each mode with its own state machine (resource_match above, wia false, no
-// log).  The exact mode never throws; its result wins when true, else the RegExp mode's result
-// (an error included) is the answer, as in the two-call form.  The RegExp cells are read even
-// when the exact mode matches (one per entity pair); the request attributes are read once.
-template <class RQ>
-ACS_FN tri resource_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, bool rpe) {
-  if (t.tflags & TF_RES_EMPTY) return 1;
-  const RuleResAttr* ra = R.T.rres + t.res_off;
-  const uint32_t ent = (R.h.flags >> RQ_ENT_SHIFT) & 7u;
-  if ((t.tflags & TF_RES_ENT_ONLY) && ent != 7u) {  // the entity-only form: exact, then RegExp
-    const tri m = resource_match(t, R, effect, false, false, 0, R.h.nres, rpe, nullptr);
-    return m != 0 ? m : resource_match(t, R, effect, true, false, 0, R.h.nres, rpe, nullptr);
-  }
-  bool rp = false;
-  bool em_x = false, pm_x = false, om_x = false, sd_x = true, done_x = false;  // exact mode
-  bool em_r = false, pm_r = false, sd_r = true, done_r = false;                // RegExp mode
-  tri res_r = 0;
-  int ent_j = 0;
-  RuleResAttr rc[ACS_RA_CACHE > 0 ? ACS_RA_CACHE : 1];
-#pragma unroll
-  for (int k = 0; k < ACS_RA_CACHE; ++k)
-    if (k < (int)t.res_n) rc[k] = load_words(R.T, ra + k);
-  for (int j = 0; j < (int)R.h.nres && !(done_x && done_r); ++j) {
-    const ReqRes q = R.res(j);
-    pm_x = pm_r = false;
-    auto step = [&](const RuleResAttr& r) {
-      if (r.kind & K_PROP) rp = true;
-      if (!done_x) {
-        if ((q.kind & K_ENT) && (r.kind & K_ENT) && q.value == r.value) {
-          em_x = true;
-          ent_j = j;
-        } else if ((q.kind & K_OP) && (r.kind & K_OP) && q.value == r.value) {
-          om_x = true;
-        } else if (em_x && (q.kind & K_PROP) && (r.kind & K_PROP)) {
-          if ((q.contains >> ent_j) & 1u) {
-            if (r.value == q.value) pm_x = true;
-          } else if (effect == EFF_PERMIT) {
-            pm_x = true;
-          }
-        }
-      }
-      if (!done_r) {
-        if ((q.kind & K_ENT) && (r.kind & K_ENT)) {
-          const uint8_t c = R.rx(q.col, r.row);
-          if (c & (RX_THROW_TYPE | RX_THROW_SYNTAX | RX_HOST)) {
-            res_r = (c & RX_THROW_TYPE) ? -(tri)ERR_TYPE : (c & RX_THROW_SYNTAX) ? -(tri)ERR_REGEX_SYNTAX
-                                                                                 : -(tri)ERR_REGEX_HOST;
-            done_r = true;
-          } else {
-            if (c & RX_RESET) em_r = false;
-            if (c & RX_HIT) em_r = true;
-          }
-        } else if (em_r && (q.kind & K_PROP) && (r.kind & K_PROP)) {
-          if (r.hash_sfx == q.hash_sfx) pm_r = true;
-        }
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < ACS_RA_CACHE; ++k)
-      if (k < (int)t.res_n) step(rc[k]);
-    for (uint32_t k = ACS_RA_CACHE; k < t.res_n; ++k) step(load_words(R.T, ra + wave_uniform(k)));
-    const bool scope = (q.kind & K_PROP) || !rpe;
-    if (!done_x) {
-      if (effect == EFF_DENY && scope && em_x && rp && pm_x) sd_x = false;
-      if (effect == EFF_PERMIT && scope && em_x && rp && !pm_x) done_x = true;  // exact: false
-    }
-    if (!done_r) {
-      if (effect == EFF_DENY && scope && em_r && rp && pm_r) sd_r = false;
-      if (effect == EFF_PERMIT && scope && em_r && rp && !pm_r) done_r = true;  // RegExp: false (res_r 0)
-    }
-  }
-  if (!done_x && !(sd_x && rp && rpe && effect == EFF_DENY && !pm_x) && (em_x || om_x)) return 1;
-  if (done_r) return res_r;
-  if (sd_r && rp && rpe && effect == EFF_DENY && !pm_r) return 0;
-  return em_r ? 1 : 0;
-}
-
-// target_match_retry for isAllowed (no obligations): one pass for both resource modes
-template <class RQ>
-ACS_FN tri target_match_retry_k1(const NodeRec& t, const RQ& R, uint8_t effect) {
-#if ACS_FUSED_RETRY
-  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
-  if (!subject_match(t, R)) return 0;
-  if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
-  return resource_match_retry(t, R, effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect, R.flag(RQ_ANY_PROP));
-#else
-  return target_match_retry(t, R, effect, false, nullptr);
-#endif
 }
 
 // ------------------------------------------------------------------ checkHierarchicalScope
@@ -1055,6 +975,10 @@ ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uin
   return d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
 }
 
+// (Rejected A/B, r06_d: the owner tests of every (slot, grant / role-scoping pair) of a request
+// computed once in K1's prologue, each rule's test then a bit lookup — c3 10M K1 3.62 vs 2.94 ms,
+// c3r1 0.454 vs 0.403, c3adv 1.67 vs 1.76: the slot-record chains of all 64 lanes cost more up
+// front than the walk's on-demand tests, which run for ~13 lanes per check.)
 template <class RQ>
 ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
   if (ACS_AB_TIMING_NO_HR || (t.tflags & TF_HR_TRIVIAL)) return 1;
@@ -1377,12 +1301,12 @@ ACS_FN int eval_set(const RQ& R, const FL& F, uint32_t s, const NodeRec& S, bool
 #if defined(ACS_OP_COUNT)
         if (!vt) ACS_OPC(OP_RULE_TM);
 #endif
-        m = vt ? 1 : target_match_retry_k1(Q, R, Q.effect);
+        m = vt ? 1 : target_match_retry(Q, R, Q.effect, false, nullptr);
 #if ACS_AB_PROBE_TM2
         if (!vt) {
           NodeRec Q2 = Q;
           Q2.role ^= acs_opaque0();
-          const tri m2 = target_match_retry_k1(Q2, R, Q.effect);
+          const tri m2 = target_match_retry(Q2, R, Q.effect, false, nullptr);
           m = m2 == m ? m : m2;
         }
 #endif

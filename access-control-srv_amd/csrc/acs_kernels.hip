@@ -1316,6 +1316,11 @@ struct acs_tables {
     size_t size() const { return n; }
   } host_img;
   size_t upload_bytes = 0;     // bytes the compile uploaded (acs_compile_update: the differing blocks)
+  // acs_compile_update: the 64-KB blocks that differ from prev's image (delta_ok: the image is a
+  // copy of prev's with those blocks replaced; else uploaded whole) — replicas apply the same delta
+  static constexpr size_t DELTA_BLOCK = 64 * 1024;
+  bool delta_ok = false;
+  std::vector<uint32_t> delta_blocks;
   // ACS_OPT_TIMING: HIP events recorded on the launch stream around every eval kernel
   static constexpr int RING = 256;
   int timing = 0;
@@ -1480,6 +1485,9 @@ int acs_layout_sizes(uint32_t* out, int n) {
 
 }  // extern "C"
 static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, const acs_tables* prev);
+static acs_tables* make_replica(const acs_tables* t, int device, const acs_tables* prev);
+static acs_tables* compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices,
+                                   const acs_tables* prev);
 extern "C" {
 
 acs_tables* acs_compile(const void* blob, size_t n_bytes, int device) {
@@ -1496,14 +1504,36 @@ acs_tables* acs_compile_update(const acs_tables* prev, const void* blob, size_t 
     fail("acs_compile_update: null previous handle");
     return nullptr;
   }
-  if (prev->sharded || !prev->peers.empty()) {
-    fail("acs_compile_update: a multi-device or rule-sharded handle (recompile it with its own entry point)");
-    return nullptr;
+  if (prev->sharded) {  // every shard against its previous image (the store's new cut)
+    std::vector<int> dev{prev->device};
+    for (const acs_tables* p : prev->peers) dev.push_back(p->device);
+    return compile_sharded(blob, n_bytes, dev.data(), (int)dev.size(), prev);
   }
-  return compile_image(blob, n_bytes, prev->device, prev);
+  acs_tables* t = compile_image(blob, n_bytes, prev->device, prev);
+  if (!t) return nullptr;
+  t->sort = prev->sort;
+  t->chunk = prev->chunk;
+  for (const acs_tables* p : prev->peers) {  // replicas: each its previous image + the primary's delta
+    acs_tables* r = make_replica(t, p->device, p);
+    if (!r) {
+      acs_free(t);
+      return nullptr;
+    }
+    t->peers.push_back(r);
+  }
+  (void)hipSetDevice(t->device);
+  return t;
 }
 
-size_t acs_image_upload_bytes(const acs_tables* t) { return t ? t->upload_bytes : 0; }
+// host-to-device bytes of the compile (every shard of a rule-sharded handle; replicas copy
+// device to device)
+size_t acs_image_upload_bytes(const acs_tables* t) {
+  if (!t) return 0;
+  size_t b = t->upload_bytes;
+  if (t->sharded)
+    for (const acs_tables* p : t->peers) b += p->upload_bytes;
+  return b;
+}
 
 }  // extern "C"
 
@@ -1654,8 +1684,9 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess;
   if (copied && prev && prev->device == device && prev->host_img.size() == img_total && prev->view.rstride == rstride) {
     // delta: the previous image copied on the device, the differing 64-KB blocks uploaded
-    constexpr size_t BLK = 64 * 1024;
+    constexpr size_t BLK = acs_tables::DELTA_BLOCK;
     copied = hipMemcpy(t->dev, prev->dev, img_total, hipMemcpyDeviceToDevice) == hipSuccess;
+    t->delta_ok = true;
     const size_t nblk = (img_total + BLK - 1) / BLK;
     std::vector<uint8_t> differs(nblk, 0);  // blocks compared over the pool, uploaded in order
     std::atomic<size_t> next{0};
@@ -1670,6 +1701,7 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
       const size_t o = b * BLK, len = std::min(BLK, img_total - o);
       copied = hipMemcpy((char*)t->dev + o, hi + o, len, hipMemcpyHostToDevice) == hipSuccess;
       t->upload_bytes += len;
+      t->delta_blocks.push_back((uint32_t)b);
     }
   } else if (copied) {
     copied = hipMemcpy(t->dev, hi, img_total, hipMemcpyHostToDevice) == hipSuccess;
@@ -1728,6 +1760,48 @@ void acs_free(acs_tables* t) {
   delete t;
 }
 
+// A replica of primary t's image on `device` (C0: copied over the device interconnect, not again
+// from the host).  prev (optional): this device's replica of the image t was updated from
+// (acs_compile_update) — then the replica is prev's image copied on the device with only t's
+// delta blocks copied from t.
+static acs_tables* make_replica(const acs_tables* t, int device, const acs_tables* prev) {
+  auto* r = new acs_tables();
+  r->device = device;
+  r->rx_rows_min = t->rx_rows_min;
+  r->view = t->view;
+  r->image_bytes = t->image_bytes;
+  bool ok = hipSetDevice(r->device) == hipSuccess && hipMalloc(&r->dev, t->image_bytes + 128) == hipSuccess;
+  if (ok && prev && t->delta_ok && prev->device == device && prev->image_bytes == t->image_bytes) {
+    ok = hipMemcpy(r->dev, prev->dev, t->image_bytes, hipMemcpyDeviceToDevice) == hipSuccess;
+    for (size_t k = 0; ok && k < t->delta_blocks.size(); ++k) {
+      const size_t o = (size_t)t->delta_blocks[k] * acs_tables::DELTA_BLOCK;
+      const size_t len = std::min(acs_tables::DELTA_BLOCK, t->image_bytes - o);
+      ok = hipMemcpyPeer((char*)r->dev + o, r->device, (const char*)t->dev + o, t->device, len) == hipSuccess;
+    }
+  } else if (ok) {
+    ok = hipMemcpyPeer(r->dev, r->device, t->dev, t->device, t->image_bytes) == hipSuccess;
+  }
+  if (!ok || hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&r->ev0) != hipSuccess || hipEventCreate(&r->ev1) != hipSuccess) {
+    fail("acs_compile_multi: replica allocation / peer copy failed");
+    acs_free(r);
+    return nullptr;
+  }
+  // rebase the view's pointers from the primary's image onto the replica's
+  auto rebase = [&](const void* p) -> const void* { return (const char*)r->dev + ((const char*)p - (const char*)t->dev); };
+  r->view.sets = (const NodeRec*)rebase(t->view.sets);
+  r->view.pols = (const NodeRec*)rebase(t->view.pols);
+  r->view.rules = (const NodeRec*)rebase(t->view.rules);
+  r->view.rres = (const RuleResAttr*)rebase(t->view.rres);
+  r->view.pairs = (const Pair*)rebase(t->view.pairs);
+  r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
+  r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
+  r->view.parents = (const uint32_t*)rebase(t->view.parents);
+  r->sort = t->sort;
+  r->chunk = t->chunk;
+  return r;
+}
+
 acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devices, int n_devices) {
   if (!devices || n_devices < 1) {
     fail("acs_compile_multi: no devices");
@@ -1736,33 +1810,11 @@ acs_tables* acs_compile_multi(const void* blob, size_t n_bytes, const int* devic
   acs_tables* t = acs_compile(blob, n_bytes, devices[0]);
   if (!t) return nullptr;
   for (int k = 1; k < n_devices; ++k) {
-    // C0: the replica's image comes from the primary's over the device interconnect (xGMI
-    // peer copy), not again from the host
-    auto* r = new acs_tables();
-    r->device = devices[k];
-    r->rx_rows_min = t->rx_rows_min;
-    r->view = t->view;
-    r->image_bytes = t->image_bytes;
-    if (hipSetDevice(r->device) != hipSuccess || hipMalloc(&r->dev, t->image_bytes + 128) != hipSuccess ||
-        hipMemcpyPeer(r->dev, r->device, t->dev, t->device, t->image_bytes) != hipSuccess ||
-        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&r->ev0) != hipSuccess || hipEventCreate(&r->ev1) != hipSuccess) {
-      fail("acs_compile_multi: replica allocation / peer copy failed");
-      acs_free(r);
+    acs_tables* r = make_replica(t, devices[k], nullptr);
+    if (!r) {
       acs_free(t);
       return nullptr;
     }
-    // rebase the view's pointers from the primary's image onto the replica's
-    auto rebase = [&](const void* p) -> const void* { return (const char*)r->dev + ((const char*)p - (const char*)t->dev); };
-    r->view.sets = (const NodeRec*)rebase(t->view.sets);
-    r->view.pols = (const NodeRec*)rebase(t->view.pols);
-    r->view.rules = (const NodeRec*)rebase(t->view.rules);
-    r->view.rres = (const RuleResAttr*)rebase(t->view.rres);
-    r->view.pairs = (const Pair*)rebase(t->view.pairs);
-    r->view.u32pool = (const uint32_t*)rebase(t->view.u32pool);
-    r->view.ev_index = t->view.ev_index ? (const uint32_t*)rebase(t->view.ev_index) : nullptr;
-    r->view.parents = (const uint32_t*)rebase(t->view.parents);
-    r->sort = t->sort;
     t->peers.push_back(r);
   }
   (void)hipSetDevice(t->device);
@@ -1896,7 +1948,10 @@ int acs_internal_slice_rows(const acs_req_batch* b, uint32_t g_pols, const acs_s
   return 0;
 }
 
-acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices) {
+// prev (optional, acs_compile_update): the sharded handle this store replaces — shard k compiled
+// against prev's shard k (a delta when its slice keeps the shape)
+static acs_tables* compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices,
+                                   const acs_tables* prev) {
   if (!blob || n_bytes < sizeof(acs_blob_header) || !devices || n_devices < 1) {
     fail("acs_compile_sharded: bad argument");
     return nullptr;
@@ -1922,7 +1977,8 @@ acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* dev
   for (int k = 0; k < n_devices; ++k) {
     ShardBase b{};
     const std::vector<char> img = slice_blob(blob, cut[k], cut[k + 1], &b);
-    acs_tables* s = acs_compile(img.data(), img.size(), devices[k]);
+    const acs_tables* p = prev ? (k == 0 ? prev : prev->peers[(size_t)k - 1]) : nullptr;
+    acs_tables* s = compile_image(img.data(), img.size(), devices[k], p && p->device == devices[k] ? p : nullptr);
     if (!s) {
       acs_free(t);
       return nullptr;
@@ -1933,11 +1989,19 @@ acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* dev
     s->g_pols = h.n_pols;
     s->g_rules = h.n_rules;
     s->rx_rows_min = rows;
+    if (prev) {
+      s->sort = prev->sort;
+      s->chunk = prev->chunk;
+    }
     if (!t) t = s;
     else t->peers.push_back(s);
   }
   (void)hipSetDevice(t->device);
   return t;
+}
+
+acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices) {
+  return compile_sharded(blob, n_bytes, devices, n_devices, nullptr);
 }
 
 int acs_device_list(const acs_tables* t, int* devices, int n) {

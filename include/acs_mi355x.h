@@ -145,8 +145,8 @@ int acs_device_list(const acs_tables* t, int* devices, int n);
  * (peer copies over xGMI) and decodes them: the records of an unsharded evaluation.
  * acs_what_is_allowed / acs_what_is_allowed_obl (host buffers) evaluate every request on every
  * device and join the devices' set / policy / rule sections into the caller's rows, obligation
- * logs merged in set order.  The device-buffer entry points, the pipeline and acs_compile_update
- * refuse a sharded handle. */
+ * logs merged in set order.  The device-buffer entry points and the pipeline refuse a sharded
+ * handle; acs_compile_update serves it (below). */
 acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 
 /* Replaces: the device side of a store change (AccessController.updateRule / updatePolicy / ...,
@@ -154,7 +154,11 @@ acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* dev
  * changed store's blob on prev's device: when the image keeps prev's shape (same node and pool
  * counts), the device image is a device-side copy of prev's with only the 64-KB blocks that differ
  * uploaded (acs_image_upload_bytes: the bytes a compile uploaded); otherwise a full upload.  prev
- * stays valid (batches in flight keep it) and is freed by the caller.  Single-device handles. */
+ * stays valid (batches in flight keep it) and is freed by the caller.  A replicated handle
+ * (acs_compile_multi): each replica is its previous image copied on its device with the primary's
+ * changed blocks copied over the interconnect.  A rule-sharded handle (acs_compile_sharded): the new
+ * store cut again, each shard compiled against the previous shard on its device (a delta when the
+ * shard's slice keeps its shape); acs_image_upload_bytes sums the shards. */
 acs_tables* acs_compile_update(const acs_tables* prev, const void* blob, size_t n_bytes);
 size_t acs_image_upload_bytes(const acs_tables* t);
 

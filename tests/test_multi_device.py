@@ -184,3 +184,69 @@ def test_two_replicas_on_one_device_gpu():
     b.close()
     two.close()
     one.close()
+
+
+@pytest.mark.gpu
+def test_eight_devices_replicated_and_sharded_update_gpu():
+    """Eight replicas and eight rule shards on device 0 == one handle for isAllowed and
+    whatIsAllowed; then acs_compile_update on both (SURVEY §8(e) with a store change): the last
+    set's rule effects flipped (same shape: the replicas take the primary's changed blocks device to device,
+    each shard a delta of its previous image) and a rule added (new shape: full images), each
+    equal to a fresh single-device compile of the changed store."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import copy
+    doc = synth.c3_store()
+    sb = synth.requests(compiler.compile_store(store.populate(doc), FULL_URNS, DEFAULT_CAS), 20_000, "c3",
+                        seed=41, second_role=0.5)
+
+    def batch_for(d):
+        cs = compiler.compile_store(store.populate(d), FULL_URNS, DEFAULT_CAS)
+        blob = compiler.store_blob(cs)
+        codec = NativeCodec(blob)
+        for k, v in sb.hrs_forests().items():
+            codec.set_subject_scopes(k, v)
+        return blob, codec, codec.encode(sb.json_text(), threads=4)
+
+    blob, codec, b = batch_for(doc)
+    one = native.Tables(blob, 0)
+    want, wia = one.is_allowed(b), one.what_is_allowed(b)
+    rep = native.Tables(blob, devices=[0] * 8)
+    sh = native.Tables(blob, devices=[0] * 8, sharded=True)
+    for t, name in ((rep, "replicated"), (sh, "sharded")):
+        assert t.devices() == [0] * 8
+        assert np.array_equal(_u64(t.is_allowed(b)), _u64(want)), name
+        _same_wia(t.what_is_allowed(b), wia)
+    full = rep.upload_bytes
+    flip = copy.deepcopy(doc)  # every rule of the last set (the walk's first) flipped: same shape
+    for pol in flip["policy_sets"][-1]["policies"]:
+        for r in pol["rules"]:
+            r["effect"] = "DENY" if r["effect"] == "PERMIT" else "PERMIT"
+    grow = copy.deepcopy(doc)
+    grow["policy_sets"][20]["policies"][0]["rules"].append(dict(copy.deepcopy(r), id="added_rule"))
+    for changed, same_shape in ((flip, True), (grow, False)):
+        blob2, codec2, b2 = batch_for(changed)
+        fresh = native.Tables(blob2, 0)
+        want2, wia2 = fresh.is_allowed(b2), fresh.what_is_allowed(b2)
+        for t, name in ((rep, "replicated"), (sh, "sharded")):
+            u = t.updated(blob2)
+            assert u.devices() == [0] * 8, name
+            assert np.array_equal(_u64(u.is_allowed(b2)), _u64(want2)), (name, same_shape)
+            _same_wia(u.what_is_allowed(b2), wia2)
+            if same_shape:
+                assert u.upload_bytes < full // 4, (name, u.upload_bytes, full)
+            u.close()
+        fresh.close()
+        b2.close()
+        codec2.close()
+    blob2, codec2, b2 = batch_for(flip)  # the flipped rule changes some records (not a no-op update)
+    fresh = native.Tables(blob2, 0)
+    assert not np.array_equal(_u64(fresh.is_allowed(b2)), _u64(want))
+    fresh.close()
+    b2.close()
+    codec2.close()
+    for t in (rep, sh, one):
+        t.close()
+    b.close()
+    codec.close()

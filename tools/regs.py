@@ -14,7 +14,7 @@ FIELDS = ("VGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs 
 def main():
     path = sys.argv[1] if len(sys.argv) > 1 else "/tmp/isa/remarks.txt"
     rows, cur = [], None
-    pat = re.compile(r":\d+:\d+: +(Function Name|" + "|".join(re.escape(f) for f in FIELDS) + r"): (\S+)")
+    pat = re.compile(r":\d+:\d+: +(?:remark: +)?(Function Name|" + "|".join(re.escape(f) for f in FIELDS) + r"): (\S+)")
     for line in open(path, errors="replace"):
         m = pat.search(line)
         if not m:
