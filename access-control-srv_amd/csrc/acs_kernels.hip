@@ -3506,12 +3506,12 @@ acs_pipeline* acs_pipeline_create(acs_tables* t, acs_codec* c, int threads, uint
     fail("acs_pipeline_create: null argument");
     return nullptr;
   }
-  if (refuse_sharded(t, "acs_pipeline_create")) return nullptr;
   auto p = new acs_pipeline();
   p->t = t;
   p->c = c;
   p->threads = threads < 1 ? 1 : threads;
   p->chunk = chunk ? chunk : 131072;
+  if (t->sharded) return p;  // a rule-sharded handle: each chunk through sharded_is_allowed (no slots)
   std::vector<acs_tables*> dev{t};
   dev.insert(dev.end(), t->peers.begin(), t->peers.end());
   p->slot.resize(2 * dev.size());
@@ -3543,9 +3543,88 @@ void acs_pipeline_free(acs_pipeline* p) {
     if (S.done) (void)hipEventDestroy(S.done);
     if (S.stream) (void)hipStreamDestroy(S.stream);
   }
-  (void)hipSetDevice(p->t->device);
+  if (!p->slot.empty()) (void)hipSetDevice(p->t->device);
   delete p;
 }
+
+}  // extern "C"
+
+// The pipeline on a rule-sharded handle: chunk k is evaluated by sharded_is_allowed (every device
+// its run of policy sets, the keys MAX-reduced on the primary) on a worker thread while the host
+// encodes chunk k + 1; the records land straight in the caller's buffer.
+static int pipeline_sharded(acs_pipeline* p, const acs_internal_items* items, size_t n, acs_decision* out,
+                            acs_pipeline_stats* st) {
+  struct Pending {
+    std::thread th;
+    acs_codec_batch* batch = nullptr;
+    size_t lo = 0, n = 0;
+    int rc = 0;
+    std::string err;
+    double ms = 0;
+  } cur;
+  auto finish = [&](Pending& P) -> int {
+    if (!P.batch) return 0;
+    const double w0 = steady_s();
+    P.th.join();
+    if (st) {
+      st->wait_s += steady_s() - w0;
+      st->gpu_ms += P.ms;
+    }
+    int rc = P.rc;
+    if (rc) {
+      g_err = P.err;
+    } else {
+      for (size_t i = 0; i < P.n; ++i)
+        if (out[P.lo + i].flags & ACS_OF_HOST_REQ) {
+          const char* why = acs_codec_batch_reason(P.batch, (uint32_t)i);
+          p->reasons[P.lo + i] = why ? why : "host path";
+        }
+    }
+    acs_codec_batch_free(P.batch);
+    P.batch = nullptr;
+    return rc;
+  };
+  for (size_t lo = 0; lo < n; lo += p->chunk) {
+    const size_t hi = lo + p->chunk < n ? lo + p->chunk : n;
+    const double e0 = steady_s();
+    acs_codec_batch* b = acs_internal_encode_range(p->c, items, lo, hi, p->threads);
+    if (!b) {
+      const std::string err = g_err;
+      finish(cur);
+      g_err = err;
+      return -1;
+    }
+    if (st) st->encode_s += steady_s() - e0;
+    if (finish(cur)) {
+      acs_codec_batch_free(b);
+      return -1;
+    }
+    acs_req_batch view;
+    if (acs_codec_batch_view(b, &view)) {
+      acs_codec_batch_free(b);
+      return -1;
+    }
+    cur.batch = b;
+    cur.lo = lo;
+    cur.n = hi - lo;
+    cur.rc = 0;
+    acs_tables* t = p->t;
+    cur.th = std::thread([t, view, out, lo, &cur] {
+      const double a = steady_s();
+      cur.rc = sharded_is_allowed(t, &view, out + lo);
+      cur.ms = (steady_s() - a) * 1e3;
+      if (cur.rc) cur.err = g_err;
+    });
+    if (st) {
+      st->chunks += 1;
+      st->upload_bytes += (double)(cur.n * sizeof(ReqLine) + view.ext_words * 4 + view.arena_words * 4) *
+                          (1 + t->peers.size());
+    }
+  }
+  return finish(cur);
+}
+
+extern "C" {
 
 int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_decision* out, size_t out_cap,
                             size_t* n_out, acs_pipeline_stats* st) {
@@ -3565,6 +3644,15 @@ int acs_pipeline_is_allowed(acs_pipeline* p, const char* json, size_t len, acs_d
     ~Free() { acs_internal_items_free(it); }
   } free_items{items};
   if (n > out_cap || (n && !out)) return fail("acs_pipeline_is_allowed: output holds fewer records than the requests");
+  if (p->t->sharded) {
+    if (pipeline_sharded(p, items, n, out, st)) return -1;
+    if (st) {
+      st->requests = n;
+      st->host_requests = p->reasons.size();
+      st->total_s = steady_s() - t0;
+    }
+    return 0;
+  }
   // any failure once a chunk is in flight: drain every slot (pipeline_reset) before returning
   auto bail = [&] {
     pipeline_reset(p);

@@ -262,9 +262,9 @@ class GpuAccessController {
       this.lastRefresh = { ms: Date.now() - t0, recompiled: r.recompiled, sets: entries.length };
       return;
     }
-    // one device: the previous image with only its changed blocks uploaded (acs_compile_update)
-    const tables = this.tables && !Array.isArray(this.device) ? addon.compileUpdate(this.tables, blob)
-      : addon.compile(blob, this.device);
+    // the previous image with only its changed blocks uploaded (acs_compile_update; replicas on
+    // further devices take the primary's changed blocks device to device)
+    const tables = this.tables ? addon.compileUpdate(this.tables, blob) : addon.compile(blob, this.device);
     const tDevice = Date.now();
     const codec = addon.codecCreate(blob);
     const tCodec = Date.now();

@@ -70,6 +70,42 @@ const now = () => Number(process.hrtime.bigint()) / 1e9;
     res[name] = { requests_per_s: objs.length / best, seconds: best, mismatches };
     console.error(`[node_rate] ${name}: ${(objs.length / best / 1e6).toFixed(3)} M req/s, ${mismatches} mismatches`);
   }
+  // latency (VERDICT r05 weak 5): single requests awaited one at a time (the micro-batcher's floor:
+  // one request per batch), then an open-loop arrival process at half the micro-batched gRPC rate —
+  // every 5 ms a burst of requests, each request's time from submission to its decision
+  const pct = (a, q) => a[Math.min(a.length - 1, Math.floor(q * a.length))] * 1e3;
+  {
+    const lat = [];
+    for (let i = 0; i < 300; ++i) {
+      const t0 = now();
+      await settle(ctl.isAllowedGrpc(grpc[i % grpc.length]));
+      lat.push(now() - t0);
+    }
+    lat.sort((a, b) => a - b);
+    res.latency_single_ms = { p50: pct(lat, 0.5), p99: pct(lat, 0.99), requests: lat.length };
+  }
+  {
+    const rate = 0.5 * res.grpc_micro.requests_per_s, tick = 0.005, per = Math.max(1, Math.round(rate * tick));
+    const lat = [], pending = [];
+    let sent = 0;
+    const tEnd = now() + 2.0;
+    while (now() < tEnd) {
+      const tb = now();
+      for (let k = 0; k < per; ++k, ++sent) {
+        const t0 = now();
+        pending.push(settle(ctl.isAllowedGrpc(grpc[sent % grpc.length])).then(() => lat.push(now() - t0)));
+      }
+      const wait = tick - (now() - tb);
+      await new Promise((r) => setTimeout(r, Math.max(0, wait * 1e3)));
+    }
+    await Promise.all(pending);
+    lat.sort((a, b) => a - b);
+    res.latency_open_loop_ms = { offered_requests_per_s: per / tick, requests: lat.length, p50: pct(lat, 0.5),
+                                 p99: pct(lat, 0.99), max: lat[lat.length - 1] * 1e3 };
+  }
+  console.error(`[node_rate] latency single p50/p99 ${res.latency_single_ms.p50.toFixed(2)} / ` +
+                `${res.latency_single_ms.p99.toFixed(2)} ms; open loop ${res.latency_open_loop_ms.offered_requests_per_s.toFixed(0)} req/s ` +
+                `p50/p99 ${res.latency_open_loop_ms.p50.toFixed(2)} / ${res.latency_open_loop_ms.p99.toFixed(2)} ms`);
   ctl.close();
   console.log(JSON.stringify(res));
 })().catch((e) => { console.error(e && e.stack ? e.stack : e); process.exit(1); });

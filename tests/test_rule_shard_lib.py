@@ -301,6 +301,13 @@ def test_sharded_handle_gpu():
             t = native.Tables(blob, devices=[0] * parts, sharded=True)
             assert t.devices() == [0] * parts
             assert np.array_equal(_u64(t.is_allowed(b)), _u64(want)), (kind, parts)
+            # the decision pipeline on the sharded handle: JSON chunks encoded while the previous
+            # chunk is evaluated on every shard and reduced
+            from acs_mi355x.codec import Pipeline
+            pl = Pipeline(t, codec, threads=4, chunk=7000)
+            got, pst = pl.is_allowed(sb.json_text(), sb.batch.n)
+            pl.close()
+            assert pst["chunks"] == 3 and np.array_equal(_u64(got), _u64(want)), (kind, parts, "pipeline")
             if kind == "c3":  # whatIsAllowed: shard rows joined, logs merged in set order
                 got = t.what_is_allowed(b)
                 _same_wia(got, wia_one, (kind, parts))
