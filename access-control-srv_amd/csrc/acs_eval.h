@@ -593,6 +593,7 @@ struct ReqCtx {
   bool soa;         // the rows past the line are SoA rows (else the extension record); false as a
                     // constant in the compact-batch kernels, so their SoA paths compile away
   uint32_t s0i, s0v, s1i, s1v, a0i, a0v, role0, role1;
+  mutable uint32_t hrd = 0;  // checkHierarchicalScope digest (hr_digest below; 0: none)
 #if defined(ACS_PHASE_PROF)
   mutable uint64_t prof[PH_N] = {};
 #endif
@@ -970,15 +971,63 @@ ACS_FN bool hr_tree(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) 
 // The owner tests of checkHierarchicalScope for one context slot: bit 0 the direct owner <->
 // grant match (hierarchicalScope.ts:165-191), bit 1 the HR-tree match (:199-245, only when not
 // direct).
-ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
+ACS_FN uint32_t hr_owner_bits_walk(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
   const uint32_t d = hr_direct(R, slot, role, se) ? 1u : 0u;
   return d | ((!d && hr_tree(R, slot, role, se)) ? 2u : 0u);
 }
 
-// (Rejected A/B, r06_d: the owner tests of every (slot, grant / role-scoping pair) of a request
-// computed once in K1's prologue, each rule's test then a bit lookup — c3 10M K1 3.62 vs 2.94 ms,
-// c3r1 0.454 vs 0.403, c3adv 1.67 vs 1.76: the slot-record chains of all 64 lanes cost more up
-// front than the walk's on-demand tests, which run for ~13 lanes per check.)
+// The owner tests of a request's context slots computed once per request, so that a rule's
+// checkHierarchicalScope reads no slot record (the slot offset -> owners -> owner attributes chain
+// of dependent arena reads).  hr_direct(slot, role, se) can hold only for the (role, se) of one of
+// the request's grants and then depends on that pair alone: bit 8 slot + g for grant g.
+// hr_tree(slot, role, se) needs (role, se) among the role scoping pairs and then depends on that
+// pair alone: bit 8 slot + 4 + k for pair k.  Bit 16 + slot: the slot's owners are missing.  Bit
+// 31: the digest holds (at most 2 slots, 4 grants, 4 pairs; else the tests walk the records).
+// K1 computes it only in the instantiation for batches with ACL_NONE requests (c3adv 1M 1.76 ->
+// 1.67 ms, r06_d): there the ACL lanes run many checks; in the plain one it cost more up front than
+// the walk's on-demand tests, which run for ~13 lanes of a wave per check (c3 10M 2.94 -> 3.62 ms,
+// c3r1 1M 0.403 -> 0.454).
+constexpr uint32_t HRD_OK = 1u << 31;
+#ifndef ACS_AN_HR_DIGEST
+#define ACS_AN_HR_DIGEST 1  // 0: A/B builds without the digest
+#endif
+ACS_FN uint32_t hr_digest(const ReqCtx& R) {
+  const uint32_t ns = R.n_slots(), ng = R.n_grants(), nk = R.n_rolese();
+  if (ns == 0 || ns > 2 || ng > 4 || nk > 4) return 0u;
+  uint32_t d = HRD_OK;
+  for (uint32_t s = 0; s < ns; ++s) {
+    if (slot_rec(R, s)[0]) d |= 1u << (16 + s);
+    for (uint32_t g = 0; g < ng; ++g) {
+      const uint32_t* gr = R.grants() + 3 * g;
+      if (hr_direct(R, s, gr[0], gr[1])) d |= 1u << (8 * s + g);
+    }
+    for (uint32_t k = 0; k < nk; ++k) {
+      const uint32_t* rs = R.rolese() + 2 * k;
+      if (hr_tree(R, s, rs[0], rs[1])) d |= 1u << (8 * s + 4 + k);
+    }
+  }
+  return d;
+}
+
+// hr_direct (bit 0) and, when not direct, hr_tree (bit 1) of slot `slot` for (role, se)
+ACS_FN uint32_t hr_owner_bits(const ReqCtx& R, uint32_t slot, uint32_t role, uint32_t se) {
+  if (!(R.hrd & HRD_OK)) return hr_owner_bits_walk(R, slot, role, se);
+  for (uint32_t g = 0; g < R.n_grants(); ++g) {
+    const uint32_t* gr = R.grants() + 3 * g;
+    if (gr[0] == role && gr[1] == se && ((R.hrd >> (8 * slot + g)) & 1u)) return 1u;
+  }
+  for (uint32_t k = 0; k < R.n_rolese(); ++k) {
+    const uint32_t* rs = R.rolese() + 2 * k;
+    if (rs[0] == role && rs[1] == se) return ((R.hrd >> (8 * slot + 4 + k)) & 1u) ? 2u : 0u;
+  }
+  return 0u;
+}
+
+// slot `slot`'s owners are missing (the context resource's meta.owners is empty)
+ACS_FN bool hr_owners_missing(const ReqCtx& R, uint32_t slot) {
+  return (R.hrd & HRD_OK) ? ((R.hrd >> (16 + slot)) & 1u) != 0u : slot_rec(R, slot)[0] != 0u;
+}
+
 template <class RQ>
 ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
   if (ACS_AB_TIMING_NO_HR || (t.tflags & TF_HR_TRIVIAL)) return 1;
@@ -1005,7 +1054,7 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
         } else if ((q.kind & K_RID_LOOSE) && em) {
           const uint32_t slot = q.slot_a;
           if (slot == NONE8) return 0;
-          if (slot_rec(R, slot)[0]) return 0;  // owners missing
+          if (hr_owners_missing(R, slot)) return 0;
           const uint32_t b = hr_owner_bits(R, slot, t.role, t.se);
           all_direct = all_direct && (b & 1u);
           all_ok = all_ok && b != 0u;
@@ -1017,7 +1066,7 @@ ACS_FN tri hierarchical_scope(const NodeRec& t, const RQ& R) {
         if (!((q.kind & K_OP) && q.value == r.value)) continue;
         const uint32_t slot = q.slot_b;
         if (slot == NONE8) return 0;
-        if (slot_rec(R, slot)[0]) return 0;
+        if (hr_owners_missing(R, slot)) return 0;
         const uint32_t b = hr_owner_bits(R, slot, t.role, t.se);
         all_direct = all_direct && (b & 1u);
         all_ok = all_ok && b != 0u;
@@ -1406,6 +1455,9 @@ ACS_FN Decision is_allowed_body(const RQ& R, const FL& F) {
     if ((q.kind & K_ENT_LOOSE) && !(q.pad & RES_RX_SAFE)) safe = false;
   }
   const bool acl_none = AN && safe && ((R.h.flags >> RQ_ACL_SHIFT) & 3u) == ACL_NONE;
+  if constexpr (AN && ACS_AN_HR_DIGEST) {
+    if (!R.flag(RQ_CTX_EMPTY)) R.hrd = hr_digest(R);
+  }
   uint8_t eff = EFF_UNDEF, ec = EC_UNDEF;
   uint32_t last_set = 0;  // 1 + the last set with an effect (0: none yet)
   Decision ev{};
