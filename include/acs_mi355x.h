@@ -145,8 +145,9 @@ int acs_device_list(const acs_tables* t, int* devices, int n);
  * (peer copies over xGMI) and decodes them: the records of an unsharded evaluation.
  * acs_what_is_allowed / acs_what_is_allowed_obl (host buffers) evaluate every request on every
  * device and join the devices' set / policy / rule sections into the caller's rows, obligation
- * logs merged in set order.  The device-buffer entry points and the pipeline refuse a sharded
- * handle; acs_compile_update serves it (below). */
+ * logs merged in set order.  The decision pipeline (acs_pipeline_*) runs each chunk that way on a
+ * worker thread while the host encodes the next; acs_compile_update serves the handle (below);
+ * the device-buffer entry points refuse it. */
 acs_tables* acs_compile_sharded(const void* blob, size_t n_bytes, const int* devices, int n_devices);
 
 /* Replaces: the device side of a store change (AccessController.updateRule / updatePolicy / ...,
