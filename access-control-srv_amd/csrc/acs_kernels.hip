@@ -787,9 +787,6 @@ struct SparseTplSink {
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
-#ifndef ACS_TPL_REG_COPY
-#define ACS_TPL_REG_COPY 1  // 0: A/B builds with the per-row template copy
-#endif
 // K2 occupancy A/B (5/6/8 waves per SIMD: 96/80/64 VGPRs with spills) measured no gain on c4
 // (6.92-6.95 ms vs 6.62, r03_g; 3.97 / 4.00 vs 4.03, r05_final): the compiler's own 4 waves/SIMD stay.
 template <class FL, bool CB>
@@ -845,62 +842,25 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     const bool usable = t1 && !(c2 && !t2) && tpl_usable(TL, t1, t2, r1, r2, T.n_sets, h.flags);
     // The wave writes its templated lanes' rows one after the other, 16 B per lane per store
     // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane
-    // rewrites the chunks of its own row that its work rules add bits to
+    // rewrites the chunks of its own row that its work rules add bits to.  (Rejected A/B, r06_g:
+    // the template chunks held in registers and re-read only when the (class, second class) pair
+    // changes — c4 1M K2 3.975 vs 4.007 ms, 131,072 1.751 vs 1.727: within the noise.)
     const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
-    if (ACS_TPL_REG_COPY && q4 <= 128u) {
-      // rows of at most 128 16-B chunks (c4: 89): each lane holds chunks lane and lane + 64 of the
-      // current template (or template pair) in registers and stores them into every templated
-      // lane's row; the template is read again only when the (class, second class) pair changes —
-      // the coherence order keeps equal pairs together — so most rows are stores that wait for
-      // no load (the per-row form loaded and waited for the template row once per lane)
-      uint32_t pc1 = 0xFFFFFFFFu, pc2 = 0xFFFFFFFFu;
-      uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
-      for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
-        const int j = __builtin_ctzll(m);
-        const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
-                       c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
-        if (c1j != pc1 || c2j != pc2) {  // wave-uniform: every lane holds lane j's values
-          pc1 = c1j;
-          pc2 = c2j;
-          const uint4* s1 = reinterpret_cast<const uint4*>(tpl + (size_t)c1j * TL.stride);
-          const uint4* s2 = c2j ? reinterpret_cast<const uint4*>(tpl + (size_t)(c2j - 1u) * TL.stride) : nullptr;
-          ACS_SCAN(16u * q4 * (s2 ? 2u : 1u));  // the template row(s); the row writes are B_out
-          if (lane < q4) {
-            v0 = s1[lane];
-            if (s2) {
-              const uint4 u = s2[lane];
-              v0.x |= u.x; v0.y |= u.y; v0.z |= u.z; v0.w |= u.w;
-            }
-          }
-          if (lane + 64u < q4) {
-            v1 = s1[lane + 64u];
-            if (s2) {
-              const uint4 u = s2[lane + 64u];
-              v1.x |= u.x; v1.y |= u.y; v1.z |= u.z; v1.w |= u.w;
-            }
-          }
+    for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
+      const int j = __builtin_ctzll(m);
+      const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
+                     c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
+      uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)oj * BL.words);
+      const uint4* s1 = reinterpret_cast<const uint4*>(tpl + (size_t)c1j * TL.stride);
+      const uint4* s2 = c2j ? reinterpret_cast<const uint4*>(tpl + (size_t)(c2j - 1u) * TL.stride) : nullptr;
+      ACS_SCAN(16u * q4 * (s2 ? 2u : 1u));  // the template row(s); the row write is B_out
+      for (uint32_t q = lane; q < q4; q += 64u) {
+        uint4 v = s1[q];
+        if (s2) {
+          const uint4 u = s2[q];
+          v.x |= u.x; v.y |= u.y; v.z |= u.z; v.w |= u.w;
         }
-        uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)oj * BL.words);
-        if (lane < q4) dst[lane] = v0;
-        if (lane + 64u < q4) dst[lane + 64u] = v1;
-      }
-    } else {
-      for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
-        const int j = __builtin_ctzll(m);
-        const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
-                       c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
-        uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)oj * BL.words);
-        const uint4* s1 = reinterpret_cast<const uint4*>(tpl + (size_t)c1j * TL.stride);
-        const uint4* s2 = c2j ? reinterpret_cast<const uint4*>(tpl + (size_t)(c2j - 1u) * TL.stride) : nullptr;
-        ACS_SCAN(16u * q4 * (s2 ? 2u : 1u));  // the template row(s); the row write is B_out
-        for (uint32_t q = lane; q < q4; q += 64u) {
-          uint4 v = s1[q];
-          if (s2) {
-            const uint4 u = s2[q];
-            v.x |= u.x; v.y |= u.y; v.z |= u.z; v.w |= u.w;
-          }
-          dst[q] = v;
-        }
+        dst[q] = v;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the copy's stores land before the lanes' own
