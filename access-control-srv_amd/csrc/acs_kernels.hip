@@ -1080,6 +1080,13 @@ struct FlaggedRecords {  // decision records carrying `mask`
   __device__ uint32_t val(uint32_t) const { return 0; }
 };
 
+struct PermEntries {  // the requests of a coherence order, holes (indices >= n) left out
+  const uint32_t* perm;
+  uint32_t n;
+  __device__ bool sel(uint32_t k) const { return perm[k] < n; }
+  __device__ uint32_t val(uint32_t) const { return 0; }
+};
+
 struct TruncatedLogs {  // a pass's obl_n [chunks][m]: some range pushed more than cap
   const uint32_t* obl_n;
   uint32_t m, chunks, cap;
@@ -1271,9 +1278,11 @@ struct Workspace {
   DevBuf slice, keys;  // rule-sharded handles: the shard's class rows, decision keys
   DevBuf tpl;          // whatIsAllowed templates of the batch's class rows
   DevBuf spread;       // a small batch's order spread over more waves (spread_waves)
+  DevBuf nopad;        // whatIsAllowed: the encoder's order with its holes left out (drop_holes)
   void release() {
     tpl.release();
     spread.release();
+    nopad.release();
     sort.release();
     img.release();
     out.release();
@@ -2259,6 +2268,35 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
   return 0;
 }
 
+// whatIsAllowed runs without wave-aligned class runs: an encoder order that carries holes (0xFFFFFFFF
+// lanes padding each class run to a wave) is compacted on the device, stably, into its n requests
+// (select_* kernels, no host sync: every request appears exactly once).  K2's waves then mix the
+// ~36-request classes of a 1M batch, but there are 2.3x fewer of them: c4 1M K2 4.03 -> 3.43 ms
+// (r06_h), while K1 keeps the holes (c3r1 1M 0.41 padded vs 0.75, c3 0.76 vs 0.84).
+#ifndef ACS_K2_PAD
+#define ACS_K2_PAD 0  // 1: A/B builds that keep the holes for K2
+#endif
+static int drop_holes(Workspace& W, const uint32_t** perm, size_t* lanes, uint32_t n, hipStream_t s) {
+  if (ACS_K2_PAD || !*perm || *lanes <= n) return 0;
+  const uint32_t nt = (uint32_t)((*lanes + SORT_TILE - 1) / SORT_TILE);
+  // room for every lane of the order (a malformed order of the device entry points, which do not
+  // validate it, can select more than n: still written inside the buffer)
+  if (W.nopad.reserve((*lanes + 2 * (size_t)nt + 4) * sizeof(uint32_t))) return -1;
+  uint32_t* out = (uint32_t*)W.nopad.p;
+  uint32_t* cnt = out + *lanes;
+  uint32_t* mx = cnt + nt;
+  uint32_t* total = mx + nt;
+  const PermEntries p{*perm, n};
+  hipLaunchKernelGGL(select_count_kernel<PermEntries>, dim3(nt), dim3(BLOCK), 0, s, p, (uint32_t)*lanes, cnt, mx);
+  hipLaunchKernelGGL(select_scan_kernel, dim3(1), dim3(BLOCK), 0, s, cnt, (const uint32_t*)mx, nt, total);
+  hipLaunchKernelGGL(select_write_kernel<PermEntries>, dim3(nt), dim3(BLOCK), 0, s, p, (uint32_t)*lanes,
+                     (const uint32_t*)cnt, *perm, out);
+  HIP_OK(hipGetLastError());
+  *perm = out;
+  *lanes = n;
+  return 0;
+}
+
 static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b, acs_decision* out, hipStream_t s) {
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
@@ -2323,18 +2361,18 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   Batch B = to_batch(b);
   const uint32_t* perm = nullptr;
   size_t lanes = b->n;
-  if (batch_order(t, W, b, B, s, &perm, !ACS_AB_NO_PAD, &lanes) ||
-      spread_waves(t, W, s, &perm, &lanes, ACS_K2_SPREAD_MIN_L))
-    return -1;
-  dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
+  if (batch_order(t, W, b, B, s, &perm, ACS_K2_PAD && !ACS_AB_NO_PAD, &lanes)) return -1;
+  const int slot = (int)(t->launches % acs_tables::RING);
+  // the timed K2 includes the order's compaction and the template pass
+  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
+  if (drop_holes(W, &perm, &lanes, B.n, s) || spread_waves(t, W, s, &perm, &lanes, ACS_K2_SPREAD_MIN_L)) return -1;
+  dim3 grid((unsigned)((lanes + BLOCK - 1) / BLOCK));
   const BitsLayout BL = bits_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   const TplLayout TL = tpl_layout(t->view.n_sets, t->view.n_pols, t->view.n_rules);
   // templates: batches whose class rows carry verdicts in the LDS form, without a role factor
   const bool use_tpl = filter_form(B) == FilterForm::Lds && !B.role_key && B.cand_rows &&
                        t->view.parents && (size_t)(BLOCK / 64) * TL.stride * 4 <= 64 * 1024;
-  const int slot = (int)(t->launches % acs_tables::RING);
-  if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));  // the template pass is part of the timed K2
   const uint32_t* tpl = nullptr;
   if (use_tpl) {
     if (W.tpl.reserve((size_t)B.cand_rows * TL.stride * sizeof(uint32_t))) return -1;
