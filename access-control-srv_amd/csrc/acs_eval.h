@@ -752,7 +752,8 @@ ACS_FN bool attrs_match(const Pair* rule, uint32_t rn, const ReqCtx& R, bool sub
 }
 
 // ------------------------------------------------------------------ checkSubjectMatches
-ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
+// sp: the target's subject pairs (R.T.pairs + t.subj_off, or a staged copy)
+ACS_FN bool subject_match_at(const NodeRec& t, const Pair* sp, const ReqCtx& R) {
   if (t.tflags & TF_SUBJ_EMPTY) return true;
   if (t.tflags & TF_SUBJ_ROLE) {
     if (!R.flag(RQ_RA_TRUTHY)) return false;
@@ -760,19 +761,20 @@ ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) {
       if (R.role(k) == t.role) return true;
     return false;
   }
-  return attrs_match(R.T.pairs + t.subj_off, t.subj_n, R, true);
+  return attrs_match(sp, t.subj_n, R, true);
 }
+ACS_FN bool subject_match(const NodeRec& t, const ReqCtx& R) { return subject_match_at(t, R.T.pairs + t.subj_off, R); }
 
 // ------------------------------------------------------------------ resourceAttributesMatch
 #ifndef ACS_RA_CACHE
 #define ACS_RA_CACHE 2  // rule resource attributes held in registers per resource_match call (A/B: 2 >= 4 > 0)
 #endif
 // Request attrs [j0, j1) with requestPropertiesExist = rpe.  wia: 'whatIsAllowed' op.
+// ra: the target's resource attributes (R.T.rres + t.res_off, or a staged copy)
 template <class RQ>
-ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool regex, bool wia, int j0, int j1,
-                          bool rpe, OblLog* obl) {
+ACS_FN tri resource_match_at(const NodeRec& t, const RuleResAttr* ra, const RQ& R, uint8_t effect, bool regex,
+                             bool wia, int j0, int j1, bool rpe, OblLog* obl) {
   if (t.tflags & TF_RES_EMPTY) return 1;
-  const RuleResAttr* ra = R.T.rres + t.res_off;
   const uint32_t ent = (R.h.flags >> RQ_ENT_SHIFT) & 7u;
   if ((t.tflags & TF_RES_ENT_ONLY) && ent != 7u && j0 == 0 && j1 == (int)R.h.nres) {
     // Target without property / operation attributes and a request with at most one entity
@@ -893,6 +895,11 @@ ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool re
   if (!em && !om) return 0;
   return 1;
 }
+template <class RQ>
+ACS_FN tri resource_match(const NodeRec& t, const RQ& R, uint8_t effect, bool regex, bool wia, int j0, int j1,
+                          bool rpe, OblLog* obl) {
+  return resource_match_at(t, R.T.rres + t.res_off, R, effect, regex, wia, j0, j1, rpe, obl);
+}
 
 // ------------------------------------------------------------------ targetMatches
 template <class RQ>
@@ -909,15 +916,22 @@ ACS_FN tri target_match(const NodeRec& t, const RQ& R, uint8_t effect, bool rege
 // (Rejected A/B, r06_c: both resource modes in one pass over the attribute pairs — the RegExp
 // cells then read even when the exact pass matches — c3 10M K1 3.25 vs 2.93 ms, c3r1 0.452 vs
 // 0.404, c3adv 1.96 vs 1.75.)
+// sp / ap / ra: the target's subject pairs, action pairs and resource attributes
+template <class RQ>
+ACS_FN tri target_match_retry_at(const NodeRec& t, const Pair* sp, const Pair* ap, const RuleResAttr* ra, const RQ& R,
+                                 uint8_t effect, bool wia, OblLog* obl) {
+  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
+  if (!subject_match_at(t, sp, R)) return 0;
+  if (!attrs_match(ap, t.act_n, R, false)) return 0;
+  const uint8_t eff = effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect;
+  const tri m = resource_match_at(t, ra, R, eff, false, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
+  if (m != 0) return m;
+  return resource_match_at(t, ra, R, eff, true, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
+}
 template <class RQ>
 ACS_FN tri target_match_retry(const NodeRec& t, const RQ& R, uint8_t effect, bool wia, OblLog* obl) {
-  if (R.flag(RQ_NO_TARGET)) return -(tri)ERR_TYPE;
-  if (!subject_match(t, R)) return 0;
-  if (!attrs_match(R.T.pairs + t.act_off, t.act_n, R, false)) return 0;
-  const uint8_t eff = effect == EFF_UNDEF ? (uint8_t)EFF_PERMIT : effect;
-  const tri m = resource_match(t, R, eff, false, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
-  if (m != 0) return m;
-  return resource_match(t, R, eff, true, wia, 0, R.h.nres, R.flag(RQ_ANY_PROP), obl);
+  return target_match_retry_at(t, R.T.pairs + t.subj_off, R.T.pairs + t.act_off, R.T.rres + t.res_off, R, effect, wia,
+                               obl);
 }
 
 // ------------------------------------------------------------------ checkHierarchicalScope

@@ -784,6 +784,120 @@ struct SparseTplSink {
     flush<2>();
   }
 };
+// K2's work rules with their rule lines staged in LDS (what_is_allowed_tpl's walk and results).
+// A work rule's target match is a chain of dependent reads — the rule record, then its action
+// pairs and resource attributes (inline in the record's 128-B line), then its policy and set —
+// and a wave meets ~12 of them one after the other.  Here the wave first lists its work rules in
+// walk order (the union over its lanes), then loads up to `cap` rule lines and their (policy, set)
+// at once into its LDS region (the filter-row region, free until a full walk), all active lanes
+// sharing the 16-B pieces, and evaluates the listed rules from LDS.  Region layout (u32 words):
+// [cap lines of 32 | cap (policy, set) | cap rule ids]; needs device rule lines (rstride 2).
+constexpr uint32_t STAGE_WORDS_PER_RULE = 32u + 2u + 1u;
+#ifndef ACS_K2_STAGE
+#define ACS_K2_STAGE 1  // 0: the unstaged walk (what_is_allowed_tpl), A/B
+#endif
+template <class RQ, class SINK>
+__device__ bool what_is_allowed_tpl_staged(const RQ& R, const TplLayout& TL, const BitsLayout& BL, const uint32_t* t1,
+                                           const uint32_t* t2, SINK& sink, OblLog& obl, uint32_t* lds, uint32_t cap) {
+  const Tables& T = R.T;
+  uint32_t* lines = lds;
+  uint32_t* ps = lds + 32u * cap;
+  uint32_t* ids = ps + 2u * cap;
+  const uint64_t act = __ballot(1);
+  const uint32_t nact = (uint32_t)__builtin_popcountll(act);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  bool ok = true;
+  uint32_t n = 0, have = 0;  // listed rules (wave-uniform); this lane's among them (bit e)
+  auto flush = [&]() {
+    wave_sync();  // the listed ids
+    for (uint32_t q = rank; q < 8u * n; q += nact) {
+      const uint32_t r = ids[q >> 3];
+      reinterpret_cast<uint4*>(lines)[q] =
+          reinterpret_cast<const uint4*>(T.rules + (size_t)r * T.rstride)[q & 7u];
+    }
+    for (uint32_t e = rank; e < n; e += nact) {
+      const uint32_t p = T.parents[ids[e] + T.n_pols];
+      ps[2u * e] = p;
+      ps[2u * e + 1u] = T.parents[p];
+    }
+    ACS_SCAN(n * 136u);
+    wave_sync();
+    for (uint32_t e = 0; e < n; ++e) {
+      if (!ok || !((have >> e) & 1u)) continue;
+      ACS_OPC(OP_TPL_TM);
+      const uint32_t* L = lines + 32u * e;
+      const NodeRec Q = load_words(T, reinterpret_cast<const NodeRec*>(L));
+      const uint32_t r = wave_uniform(ids[e]);
+      // inline attributes (acs_compile's rule lines): offsets that point into the rule's own line
+      const RuleResAttr* ra =
+          Q.res_off == r * 8u + 4u ? reinterpret_cast<const RuleResAttr*>(L + 16) : T.rres + Q.res_off;
+      const Pair* ap = Q.act_off == r * 16u + 14u ? reinterpret_cast<const Pair*>(L + 28) : T.pairs + Q.act_off;
+      const tri m = target_match_retry_at(Q, T.pairs + Q.subj_off, ap, ra, R, Q.effect, true, &obl);
+      if (m < 0) {
+        ok = false;
+        continue;
+      }
+      if (m) {
+        ACS_OPC(OP_TPL_HIT);
+        const uint32_t p = ps[2u * e], s = ps[2u * e + 1u];
+        sink.template set<0>(s >> 5, 1u << (s & 31u));
+        sink.template set<1>(BL.wp + (p >> 5), 1u << (p & 31u));
+        sink.template set<2>(BL.wr + (r >> 5), 1u << (r & 31u));
+      }
+    }
+    wave_sync();  // the next batch overwrites the lines
+    n = 0;
+    have = 0;
+  };
+  const uint32_t MW = (TL.flags - TL.mask);
+  ACS_OPC(OP_TPL_REQ);
+  for (uint32_t k = 0; k < MW; ++k) {
+    uint32_t u = wave_or(t1[TL.mask + k] | (t2 ? t2[TL.mask + k] : 0u));
+    while (u) {
+      const uint32_t w = wave_uniform(32u * k + (uint32_t)__builtin_ctz(u));
+      u &= u - 1u;
+      ACS_OPC(OP_TPL_WORD);
+      uint32_t mine = t1[TL.work + w] & ~(t2 ? t2[BL.wr + w] : 0u);
+      if (t2) mine |= t2[TL.work + w] & ~t1[BL.wr + w];
+      uint32_t rest = wave_or(mine);
+      while (rest) {
+        const uint32_t b = (uint32_t)__builtin_ctz(rest);
+        rest &= rest - 1u;
+        ACS_OPC(OP_TPL_RULE);
+        if (n == cap) flush();
+        ids[n] = 32u * w + b;  // every active lane writes the same id
+        have |= ((mine >> b) & 1u) << n;
+        ++n;
+      }
+    }
+  }
+  if (n) flush();
+  if (!ok) return false;
+  sink.finish();
+  return true;
+}
+
+// Order of one wave's stores to the same row chunk (the wave's template copy, then a lane's own
+// rewrite of that chunk): the earlier stores complete before the later issue.  Workgroup scope is
+// a wait for the wave's outstanding stores; agent scope (ACS_K2_FENCE_AGENT=1, the round-5 form)
+// also writes the XCD's L2 back to memory at every wave, which the ordering does not need.
+#ifndef ACS_K2_FENCE_AGENT
+#define ACS_K2_FENCE_AGENT 0
+#endif
+__device__ inline void k2_store_order() {
+#if ACS_K2_FENCE_AGENT
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#endif
+}
+// Timing probes (K2 results differ): no template copy / no work rules
+#ifndef ACS_AB_PROBE_K2_NOCOPY
+#define ACS_AB_PROBE_K2_NOCOPY 0
+#endif
+#ifndef ACS_AB_PROBE_K2_NOWORK
+#define ACS_AB_PROBE_K2_NOWORK 0
+#endif
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
@@ -846,7 +960,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     // the template chunks held in registers and re-read only when the (class, second class) pair
     // changes — c4 1M K2 3.975 vs 4.007 ms, 131,072 1.751 vs 1.727: within the noise.)
     const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
-    for (uint64_t m = __ballot(usable); m; m &= m - 1u) {
+    for (uint64_t m = ACS_AB_PROBE_K2_NOCOPY ? 0u : __ballot(usable); m; m &= m - 1u) {
       const int j = __builtin_ctzll(m);
       const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
                      c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
@@ -863,11 +977,17 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
         dst[q] = v;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the copy's stores land before the lanes' own
-    if (usable) {
+    k2_store_order();  // the copy's stores land before the lanes' own
+    if (usable && ACS_AB_PROBE_K2_NOWORK) {  // timing probe: no work rules (rows lack their bits)
+      obl_n[o] = 0u;
+      done = true;
+    } else if (usable) {
       SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
-      if (what_is_allowed_tpl(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), TL, BL, t1, t2, sink, log)) {
+      const ReqLds R(T, B, i, h, scol, BLOCK, ln, !CB);
+      const uint32_t cap = ACS_K2_STAGE && T.rstride == 2u ? min(32u, lds_wave_words(B) / STAGE_WORDS_PER_RULE) : 0u;
+      if (cap ? what_is_allowed_tpl_staged(R, TL, BL, t1, t2, sink, log, wave_lds_row(B), cap)
+              : what_is_allowed_tpl(R, TL, BL, t1, t2, sink, log)) {
         if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
         obl_n[o] = log.n;
         done = true;
@@ -875,7 +995,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     }
   }
   if (__ballot(!done)) {  // the full walk (rewrites a failed template lane's whole row)
-    if (tpl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // a failed lane's chunks land first
+    if (tpl) k2_store_order();  // a failed lane's chunks land first
     const FL F = FilterMaker<FL>::make(B, !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                        lane_cls2(ln, in && !done), wave_lds_row(B));
     if (!done) {
