@@ -133,16 +133,29 @@ struct Tables {
                              // nullptr: no whatIsAllowed templates)
 };
 
-// The parent of every policy (its set) and rule (its policy): parent_index_words(P, R) words.
-inline size_t parent_index_words(uint32_t n_pols, uint32_t n_rules) { return (size_t)n_pols + n_rules; }
-inline void build_parents(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols, uint32_t n_rules,
-                          uint32_t* out) {
+// The parent of every policy (its set) and rule (its policy), then two rule bitsets: non-null
+// rules and rules with a target (the whatIsAllowed template pass decides a policy's rules a word
+// at a time from them, without reading the rule records): parent_index_words(P, R) words.
+inline size_t parent_index_words(uint32_t n_pols, uint32_t n_rules) {
+  return (size_t)n_pols + n_rules + 2 * (((size_t)n_rules + 31) / 32);
+}
+// rules: the blob's 64-B rule records
+inline void build_parents(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols,
+                          const NodeRec* rules, uint32_t n_rules, uint32_t* out) {
   for (size_t k = 0; k < parent_index_words(n_pols, n_rules); ++k) out[k] = 0;
   for (uint32_t s = 0; s < n_sets; ++s)
     for (uint32_t p = sets[s].child_begin; p < sets[s].child_end && p < n_pols; ++p) out[p] = s;
   for (uint32_t p = 0; p < n_pols; ++p)
     for (uint32_t r = pols[p].child_begin; r < pols[p].child_end && r < n_rules; ++r) out[n_pols + r] = p;
+  uint32_t* live = out + (size_t)n_pols + n_rules;
+  uint32_t* tgt = live + (n_rules + 31) / 32;
+  for (uint32_t r = 0; r < n_rules; ++r) {
+    if (!(rules[r].nflags & NF_NULL)) live[r >> 5] |= 1u << (r & 31);
+    if (rules[r].nflags & NF_HAS_TARGET) tgt[r >> 5] |= 1u << (r & 31);
+  }
 }
+ACS_FN const uint32_t* rule_live_bits(const Tables& T) { return T.parents + (size_t)T.n_pols + T.n_rules; }
+ACS_FN const uint32_t* rule_target_bits(const Tables& T) { return rule_live_bits(T) + (T.n_rules + 31u) / 32u; }
 
 // K1's event index (is_allowed_body's events-only skip): per set its rules' range [r0, r1) and,
 // in bit 31 of the r1 word, whether it holds a null policy or a policy with an invalid combining
@@ -1835,17 +1848,22 @@ ACS_FN bool wia_template_set(const Tables& T, const uint32_t* row, uint32_t wp, 
         return false;
       }
     }
+    // the policy's candidate non-null rules a word at a time: known true (no target, or a
+    // retried match the class knows) go into the row, the others are work
     bool any_rule = false;
-    for (uint32_t r = P.child_begin; r < P.child_end; ++r) {
-      if (!row_bit(row, wr, r)) continue;
-      const NodeRec Q = T.rules[(size_t)r * T.rstride];
-      if (Q.nflags & NF_NULL) continue;
-      if (!(Q.nflags & NF_HAS_TARGET) || row_bit(row, wv + 4u * WP, r)) {
-        acc.or_bits(BL.wr + (r >> 5), 1u << (r & 31u));
+    const uint32_t* live = rule_live_bits(T);
+    const uint32_t* tgt = rule_target_bits(T);
+    for (uint32_t base = P.child_begin & ~31u; base < P.child_end; base += 32u) {
+      const uint32_t w = base >> 5;
+      uint32_t m = row[wr + w] & live[w];
+      if (base < P.child_begin) m &= ~0u << (P.child_begin & 31u);
+      if (P.child_end - base < 32u) m &= (1u << (P.child_end - base)) - 1u;
+      const uint32_t known = m & (~tgt[w] | row[wv + 4u * WP + w]), work = m & ~known;
+      if (known) {
+        acc.or_bits(BL.wr + w, known);
         any_rule = true;
-      } else {
-        acc.or_bits(TL.work + (r >> 5), 1u << (r & 31u));
       }
+      if (work) acc.or_bits(TL.work + w, work);
     }
     if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
       acc.or_bits(BL.wp + (p >> 5), 1u << (p & 31u));

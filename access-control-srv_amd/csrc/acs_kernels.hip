@@ -1808,8 +1808,8 @@ static acs_tables* compile_image(const void* blob, size_t n_bytes, int device, c
   if (ex_words) {
     build_event_index((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
                       (const NodeRec*)(bsrc + off[2]), h.n_rules, evx);
-    build_parents((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols, h.n_rules,
-                  evx + ev_words);
+    build_parents((const NodeRec*)(bsrc + off[0]), h.n_sets, (const NodeRec*)(bsrc + off[1]), h.n_pols,
+                  (const NodeRec*)(bsrc + off[2]), h.n_rules, evx + ev_words);
   }
   const char* hi = t->host_img.data();
   bool copied = hipSetDevice(device) == hipSuccess && hipMalloc(&t->dev, img_total + 128) == hipSuccess;

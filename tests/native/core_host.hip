@@ -45,7 +45,7 @@ static bool host_tables(const void* blob, size_t n, Tables* T) {
   T->ev_index = getenv("ACS_HOST_NO_EV_INDEX") ? nullptr : evx.data();
   static thread_local std::vector<uint32_t> par;
   par.assign(parent_index_words(h.n_pols, h.n_rules), 0u);
-  build_parents(T->sets, h.n_sets, T->pols, h.n_pols, h.n_rules, par.data());
+  build_parents(T->sets, h.n_sets, T->pols, h.n_pols, T->rules, h.n_rules, par.data());
   T->parents = par.data();
   return true;
 }
