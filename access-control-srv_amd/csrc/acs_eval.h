@@ -701,7 +701,10 @@ struct ReqCtx {
 // c3; 8 slots: 3 blocks/CU, round-2 A/B 20.6 vs 17.6 ms with 6).
 constexpr int LDS_SLOTS = LINE_RES;
 
+// NS: the LDS slots the kernel staged (LDS_SLOTS; K2 also stages the first extension attribute)
+template <int NS = LDS_SLOTS>
 struct ReqLds : ReqCtx {
+  static_assert(NS >= LINE_RES, "slots past the line come from the extension record");
   const ReqRes* col;  // this lane's LDS column
   uint32_t stride;
   uint32_t e0_val, e0_col;  // the request's only entity attribute (RQ_ENT_SHIFT field 1..6)
@@ -719,9 +722,9 @@ struct ReqLds : ReqCtx {
   ACS_FN ReqRes res(int j) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(3))) const ReqRes lds_res;  // ds_read, not flat
-    if (j < LDS_SLOTS) return ((lds_res*)col)[j * stride];
+    if (j < NS) return ((lds_res*)col)[j * stride];
 #else
-    if (j < LDS_SLOTS) return col[j * stride];
+    if (j < NS) return col[j * stride];
 #endif
     return res_row((uint32_t)j);
   }

@@ -572,6 +572,30 @@ __device__ unsigned int acs_wt_cls[WT_MAX], acs_wt_lanes[WT_MAX];
 __device__ unsigned long long acs_phase_acc[PH_N];
 #endif
 
+// A lane's first NS resource attributes into its LDS column (stride BLOCK): the line's, then
+// past the line the extension record's (compact batches) or the SoA rows.
+template <int NS, bool CB>
+__device__ inline void stage_attrs(ReqRes* col, const Batch& B, const ReqLine* ln, uint32_t i, uint32_t nres) {
+  const uint32_t nq = nres < (uint32_t)LINE_RES ? nres : (uint32_t)LINE_RES;
+  for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];
+  for (uint32_t j = LINE_RES; j < nres && j < (uint32_t)NS; ++j) {
+    if (ln && CB) {
+      ReqRes q;
+      __builtin_memcpy(&q, B.ext + (size_t)(ln->ext - 1u) * 4u + 4u * (j - LINE_RES), sizeof q);
+      col[j * BLOCK] = q;
+    } else {
+      col[j * BLOCK] = B.res[(size_t)j * B.n + i];
+    }
+  }
+}
+
+// K1's LDS attribute slots (ACS_K1_SLOTS = 5 stages the first extension attribute too, at the
+// cost of a fifth block per CU)
+#ifndef ACS_K1_SLOTS
+#define ACS_K1_SLOTS 4
+#endif
+constexpr int K1_SLOTS = ACS_K1_SLOTS;
+
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
 // 5 waves/SIMD (VGPR <= 96, with 4 LDS attribute slots so 5 blocks fit a CU's LDS): c3 K1
@@ -612,7 +636,7 @@ template <class FL, bool CB, bool AN, bool SK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
-  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
+  __shared__ ReqRes stage[K1_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
@@ -643,14 +667,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
 #endif
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
-    const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) col[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
+    stage_attrs<K1_SLOTS, CB>(col, B, ln, i, h.nres);
 #if defined(ACS_PHASE_PROF)
-    const ReqLds R(T, B, i, h, col, BLOCK, ln, !CB);
+    const ReqLds<K1_SLOTS> R(T, B, i, h, col, BLOCK, ln, !CB);
     d = is_allowed_t<AN, SK>(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t<AN, SK>(ReqLds(T, B, i, h, col, BLOCK, ln, !CB), F);
+    d = is_allowed_t<AN, SK>(ReqLds<K1_SLOTS>(T, B, i, h, col, BLOCK, ln, !CB), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
@@ -898,6 +921,12 @@ __device__ inline void k2_store_order() {
 #ifndef ACS_AB_PROBE_K2_NOWORK
 #define ACS_AB_PROBE_K2_NOWORK 0
 #endif
+// K2's LDS attribute slots: the line's 4, then the first extension attribute (c4: a quarter of the
+// requests carry 5 resource attributes; every work rule's match reads all of them)
+#ifndef ACS_K2_SLOTS
+#define ACS_K2_SLOTS 5
+#endif
+constexpr int K2_SLOTS = ACS_K2_SLOTS;
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
 // once, 16 B per store (ChunkSink): no scratch buffer, no zeroing pass, no transpose.
@@ -911,7 +940,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
                                                                 uint32_t* __restrict__ obl_n,
                                                                 Decision* __restrict__ out,
                                                                 const uint32_t* __restrict__ tpl, TplLayout TL) {
-  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
+  __shared__ ReqRes stage[K2_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
@@ -943,10 +972,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     done = true;
   }
   ReqRes* scol = stage + threadIdx.x;
-  if (!done) {
-    const uint32_t nq = h.nres < LDS_SLOTS ? h.nres : LDS_SLOTS;
-    for (uint32_t j = 0; j < nq; ++j) scol[j * BLOCK] = ln ? ln->res[j] : B.res[(size_t)j * B.n + i];  // nq <= LINE_RES
-  }
+  if (!done) stage_attrs<K2_SLOTS, CB>(scol, B, ln, i, h.nres);
   if (tpl) {  // the class template(s) plus the work rules (acs_eval.h what_is_allowed_tpl)
     const uint32_t c1 = request_pcol(h), c2 = lane_cls2(ln, in);
     const uint32_t* t1 = !done && c1 < B.cand_rows ? tpl + (size_t)c1 * TL.stride : nullptr;
@@ -984,7 +1010,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     } else if (usable) {
       SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
-      const ReqLds R(T, B, i, h, scol, BLOCK, ln, !CB);
+      const ReqLds<K2_SLOTS> R(T, B, i, h, scol, BLOCK, ln, !CB);
       const uint32_t cap = ACS_K2_STAGE && T.rstride == 2u ? min(32u, lds_wave_words(B) / STAGE_WORDS_PER_RULE) : 0u;
       if (cap ? what_is_allowed_tpl_staged(R, TL, BL, t1, t2, sink, log, wave_lds_row(B), cap)
               : what_is_allowed_tpl(R, TL, BL, t1, t2, sink, log)) {
@@ -1001,7 +1027,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     if (!done) {
       ChunkSink sink(bits + (size_t)o * BL.words, BL);
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
-      d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
+      d = what_is_allowed_t(ReqLds<K2_SLOTS>(T, B, i, h, scol, BLOCK, ln, !CB), F, BL, sink, log);
       sink.finish();
       obl_n[o] = (d.flags & OF_ERR) ? 0u : log.n;
     }
@@ -1065,7 +1091,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_obl_kernel(Tables T, Ba
     const uint32_t s0 = obl_range_local((uint32_t)((uint64_t)g_sets * c / chunks), set_base, T.n_sets);
     const uint32_t s1 = obl_range_local((uint32_t)((uint64_t)g_sets * (c + 1) / chunks), set_base, T.n_sets);
     NullSink none;
-    const Decision d = what_is_allowed_t(ReqLds(T, B, i, h, scol, BLOCK, ln, !CB), F, BitsLayout{}, none, log, s0, s1);
+    const Decision d = what_is_allowed_t(ReqLds<>(T, B, i, h, scol, BLOCK, ln, !CB), F, BitsLayout{}, none, log, s0, s1);
     total = (d.flags & OF_ERR) ? 0u : log.total;
   }
   obl_n[k] = total;
