@@ -589,12 +589,9 @@ __device__ inline void stage_attrs(ReqRes* col, const Batch& B, const ReqLine* l
   }
 }
 
-// K1's LDS attribute slots (ACS_K1_SLOTS = 5 stages the first extension attribute too, at the
-// cost of a fifth block per CU)
-#ifndef ACS_K1_SLOTS
-#define ACS_K1_SLOTS 4
-#endif
-constexpr int K1_SLOTS = ACS_K1_SLOTS;
+// K1 stages the line's 4 attributes (LDS_SLOTS).  (Rejected A/B, r06_p: a fifth slot for the first
+// extension attribute, which leaves 4 blocks per CU — c3 10M 3.34 ms at 5 waves/SIMD with spills,
+// 3.19 at 4 without, vs 2.95; c3adv, already at 4 waves, 1.639 vs 1.646.)
 
 // K1: one request per lane; its resource attributes are staged in this lane's LDS column.
 #ifndef ACS_K1_WAVES_PER_EU
@@ -636,7 +633,7 @@ template <class FL, bool CB, bool AN, bool SK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     AN ? ACS_K1_AN_WAVES_PER_EU : (SK ? ACS_K1_SK_WAVES_PER_EU : ACS_K1_WAVES_PER_EU)))) void is_allowed_kernel(
     Tables T, Batch B, const uint32_t* __restrict__ perm, uint32_t lanes, Decision* __restrict__ out) {
-  __shared__ ReqRes stage[K1_SLOTS * BLOCK];
+  __shared__ ReqRes stage[LDS_SLOTS * BLOCK];
   const uint32_t k = blockIdx.x * BLOCK + threadIdx.x;
   const uint32_t pk = k < lanes ? (perm ? perm[k] : k) : 0xFFFFFFFFu;  // padded perm: holes
   const bool in = pk < B.n;
@@ -667,13 +664,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
 #endif
   if (!done) {
     ReqRes* col = stage + threadIdx.x;
-    stage_attrs<K1_SLOTS, CB>(col, B, ln, i, h.nres);
+    stage_attrs<LDS_SLOTS, CB>(col, B, ln, i, h.nres);
 #if defined(ACS_PHASE_PROF)
-    const ReqLds<K1_SLOTS> R(T, B, i, h, col, BLOCK, ln, !CB);
+    const ReqLds<> R(T, B, i, h, col, BLOCK, ln, !CB);
     d = is_allowed_t<AN, SK>(R, F);
     for (int k = 0; k < PH_N; ++k) prof_lane[k] = R.prof[k];
 #else
-    d = is_allowed_t<AN, SK>(ReqLds<K1_SLOTS>(T, B, i, h, col, BLOCK, ln, !CB), F);
+    d = is_allowed_t<AN, SK>(ReqLds<>(T, B, i, h, col, BLOCK, ln, !CB), F);
 #endif
   }
 #if !defined(ACS_PHASE_PROF)
