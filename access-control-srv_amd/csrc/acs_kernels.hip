@@ -589,6 +589,12 @@ __device__ inline void stage_attrs(ReqRes* col, const Batch& B, const ReqLine* l
   }
 }
 
+#ifndef ACS_AB_PROBE_K1_NOWALK
+#define ACS_AB_PROBE_K1_NOWALK 0
+#endif
+#ifndef ACS_AB_PROBE_K1_NOROWS
+#define ACS_AB_PROBE_K1_NOROWS 0
+#endif
 // K1 stages the line's 4 attributes (LDS_SLOTS).  (Rejected A/B, r06_p: a fifth slot for the first
 // extension attribute, which leaves 4 blocks per CU — c3 10M 3.34 ms at 5 waves/SIMD with spills,
 // 3.19 at 4 without, vs 2.95; c3adv, already at 4 waves, 1.639 vs 1.646.)
@@ -654,8 +660,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(
     }
   }
 #endif
+#if ACS_AB_PROBE_K1_NOROWS  // timing probe: no filter rows, no walk (the prologue's line and attribute reads)
+  if (in) out[i] = d;
+  return;
+#endif
   const FL F = FilterMaker<FL>::make(B, in && !done, request_pcol(h), B.role_key && in ? B.role_key[i] : 0xFFFFu,
                                      lane_cls2(ln, in), wave_lds_row(B));
+#if ACS_AB_PROBE_K1_NOWALK  // timing probe: the prologue without the walk
+  if (in) out[i] = d;
+  (void)F;
+  return;
+#endif
 #if defined(ACS_PHASE_PROF)
   uint64_t prof_lane[PH_N] = {};
   if (!in) done = true;
