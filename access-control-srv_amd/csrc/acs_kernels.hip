@@ -2430,7 +2430,8 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
 // lanes padding each class run to a wave) is compacted on the device, stably, into its n requests
 // (select_* kernels, no host sync: every request appears exactly once).  K2's waves then mix the
 // ~36-request classes of a 1M batch, but there are 2.3x fewer of them: c4 1M K2 4.03 -> 3.43 ms
-// (r06_h), while K1 keeps the holes (c3r1 1M 0.41 padded vs 0.75, c3 0.76 vs 0.84).
+// (r06_h), while K1 keeps the holes (c3r1 1M 0.41 padded vs 0.75, c3 0.76 vs 0.84) except in a
+// batch with ACL_NONE requests whose lanes are mostly holes (is_allowed_launch).
 #ifndef ACS_K2_PAD
 #define ACS_K2_PAD 0  // 1: A/B builds that keep the holes for K2
 #endif
@@ -2466,6 +2467,12 @@ static int is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_batch* b
   size_t lanes = b->n;
   bool spread = false;
   if (batch_order(t, W, b, B, s, &perm, pad, &lanes)) return -1;
+  // a batch with ACL_NONE requests whose wave-aligned class runs are mostly holes (more than 40 %
+  // of the lanes) runs without them: its waves are as long as their ACL lanes' walks whichever
+  // classes they mix (c3adv 1M, 57 % holes: 1.669 → 1.638 ms, r06_h)
+  if ((b->hints & ACS_HINT_ACL_NONE) && perm && (lanes - b->n) * 5 > lanes * 2 &&
+      drop_holes(W, &perm, &lanes, B.n, s))
+    return -1;
   const bool padded = lanes > b->n;  // wave-aligned class runs (holes): one class per wave
   if (spread_waves(t, W, s, &perm, &lanes, ACS_SPREAD_MIN_L, &spread)) return -1;
   // waves that mix classes: spread, or unpadded with short class runs (< 256 requests per class
@@ -2836,8 +2843,12 @@ static std::vector<std::vector<uint32_t>> shard_perms(const acs_req_batch* b, si
 // slot is reused its stream is drained (its workspace may grow for the next chunk).  On an error
 // the chunks already queued are drained and the outputs of the call are unspecified.
 static constexpr size_t CHUNK_MAX_K = 16;  // chunks per call, at most (t->chunk: requests per chunk, at least)
+// A batch is cut only into 8 chunks or more: a K1 launch on a small chunk lasts about as long as
+// its longest wave, so a few chunks each pay that (c3adv 1M in 4 chunks: 61 M/s against 74 M/s in
+// one launch, r06_final; c3 10M in 16 chunks: 155 M/s against 116 M/s)
+static constexpr size_t CHUNK_MIN_K = 8;
 static bool chunk_host_batch(const acs_tables* t, const acs_req_batch* b) {
-  return t->chunk && t->peers.empty() && !t->sharded && !b->hdr && b->lines && b->n >= 2 * t->chunk;
+  return t->chunk && t->peers.empty() && !t->sharded && !b->hdr && b->lines && b->n >= CHUNK_MIN_K * t->chunk;
 }
 
 // The chunks' coherence orders into the page-locked t->hperm: chunk k's order (the batch's

@@ -246,7 +246,7 @@ int acs_shard_decode_device(const uint64_t* dev_keys, size_t n, acs_decision* de
  * launches (a ring of 256), returning how many were written. */
 #define ACS_OPT_TIMING 2
 /* ACS_OPT_CHUNK (default 262144): acs_is_allowed on one device cuts a compact batch of at least
- * twice this many requests into up to 16 contiguous chunks and overlaps chunk k + 1's upload
+ * eight times this many requests into 8 to 16 contiguous chunks and overlaps chunk k + 1's upload
  * with chunk k's evaluation and chunk k - 1's download (two streams); 0: one upload, one
  * launch, one download.  The records are the same either way. */
 #define ACS_OPT_CHUNK 3

@@ -151,7 +151,8 @@ def test_pipeline_error_mid_run_then_single_request_gpu():
 def test_chunked_host_path_gpu(monkeypatch):
     """acs_is_allowed on one device in overlapped chunks (ACS_OPT_CHUNK: each chunk uploaded as a
     shard, the class / role rows once per call, two streams) equals one upload and one launch:
-    a c3 batch with composed rows and the encoder's coherence order in 2 and 16 chunks, a
+    a c3 batch with composed rows and the encoder's coherence order in 9 and 16 chunks (a batch is
+    cut only into 8 chunks or more), a
     role-factor batch, and random stores' wide requests (extension records, arena tails) in
     chunks of a few requests."""
     cs = compiler.compile_store(store.populate(synth.c3_store()), FULL_URNS, DEFAULT_CAS)
@@ -161,7 +162,7 @@ def test_chunked_host_path_gpu(monkeypatch):
     want = t.is_allowed(sb.batch, compact=True)
     dev = decisions_from_tensor(is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True)))
     assert np.array_equal(_u64(want), _u64(dev))
-    for c in (262144, 30_000):
+    for c in (65_000, 30_000):
         t.set_chunk(c)
         assert np.array_equal(_u64(t.is_allowed(sb.batch, compact=True)), _u64(want)), c
     t.close()
@@ -189,7 +190,7 @@ def test_chunked_host_path_gpu(monkeypatch):
         t = native.Tables(compiler.store_blob(rcs), 0)
         t.set_chunk(0)
         want = t.is_allowed(b, compact=True)
-        t.set_chunk(max(1, b.n // 7))
+        t.set_chunk(max(1, b.n // 9))
         assert np.array_equal(_u64(t.is_allowed(b, compact=True)), _u64(want)), s
         t.close()
         checked += 1
