@@ -776,7 +776,8 @@ __global__ __launch_bounds__(BLOCK) void wia_template_kernel(Tables T, Batch B, 
 // A templated lane's work-rule bits over the row the wave already wrote from the template(s):
 // as TplSink, each section's current 16-B chunk gathers bits in registers, but only a chunk that
 // got some is rewritten (template chunk(s) | bits); the lane is its row's only writer by then.
-// (Device atomics per bit measured slower: c4 1M K2 4.71 vs 4.05 ms, r05_n.)
+// (Device atomics per bit measured slower: c4 1M K2 4.71 vs 4.05 ms, r05_n; a word at a time,
+// without the template read, too: 3.16 vs 2.22 ms, 4M 9.78 vs 6.10, r06_s.)
 struct SparseTplSink {
   uint4* row;
   const uint4* t1;
