@@ -22,7 +22,8 @@ elif [ "$PART" = b ]; then
 else
   for cfg in c3 c4 c3adv c3r1; do
     k=is_allowed_kernel; [ $cfg = c4 ] && k=what_is_allowed_kernel
-    PMC_OUT=$O/pmc_$cfg CFG=$cfg KERNEL=$k timeout -k 10 600 bash tools/pmc.sh > $O/pmc_$cfg.log 2>&1 || { echo "STOP pmc $cfg"; exit 1; }
+    n=1000000; case $cfg in c3|c3r1) n=10000000;; esac
+    PMC_OUT=$O/pmc_$cfg CFG=$cfg KERNEL=$k KEY=$cfg/n$n/w1/requests timeout -k 10 600 bash tools/pmc.sh > $O/pmc_$cfg.log 2>&1 || { echo "STOP pmc $cfg"; exit 1; }
     tail -n 2 $O/pmc_$cfg.log
   done
 fi
