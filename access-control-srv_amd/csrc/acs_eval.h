@@ -134,10 +134,12 @@ struct Tables {
 };
 
 // The parent of every policy (its set) and rule (its policy), then two rule bitsets: non-null
-// rules and rules with a target (the whatIsAllowed template pass decides a policy's rules a word
-// at a time from them, without reading the rule records): parent_index_words(P, R) words.
+// rules and rules with a target, then four policy bitsets: null, with a target, with a target
+// testing role associations, truthy effect (the whatIsAllowed template pass decides a set's
+// policies and a policy's rules a word at a time from them, without reading every record):
+// parent_index_words(P, R) words.
 inline size_t parent_index_words(uint32_t n_pols, uint32_t n_rules) {
-  return (size_t)n_pols + n_rules + 2 * (((size_t)n_rules + 31) / 32);
+  return (size_t)n_pols + n_rules + 2 * (((size_t)n_rules + 31) / 32) + 4 * (((size_t)n_pols + 31) / 32);
 }
 // rules: the blob's 64-B rule records
 inline void build_parents(const NodeRec* sets, uint32_t n_sets, const NodeRec* pols, uint32_t n_pols,
@@ -153,9 +155,22 @@ inline void build_parents(const NodeRec* sets, uint32_t n_sets, const NodeRec* p
     if (!(rules[r].nflags & NF_NULL)) live[r >> 5] |= 1u << (r & 31);
     if (rules[r].nflags & NF_HAS_TARGET) tgt[r >> 5] |= 1u << (r & 31);
   }
+  const uint32_t PW = (n_pols + 31) / 32;
+  uint32_t* pb = tgt + (n_rules + 31) / 32;
+  for (uint32_t p = 0; p < n_pols; ++p) {
+    const uint32_t bit = 1u << (p & 31), w = p >> 5;
+    if (pols[p].nflags & NF_NULL) pb[w] |= bit;
+    if (pols[p].nflags & NF_HAS_TARGET) pb[PW + w] |= bit;
+    if ((pols[p].nflags & NF_HAS_TARGET) && (pols[p].tflags & TF_SUBJ_ROLE)) pb[2 * PW + w] |= bit;
+    if (pols[p].nflags & NF_EFFECT_TRUTHY) pb[3 * PW + w] |= bit;
+  }
 }
 ACS_FN const uint32_t* rule_live_bits(const Tables& T) { return T.parents + (size_t)T.n_pols + T.n_rules; }
 ACS_FN const uint32_t* rule_target_bits(const Tables& T) { return rule_live_bits(T) + (T.n_rules + 31u) / 32u; }
+// policy bitset k (0 null, 1 with a target, 2 role-testing target, 3 truthy effect)
+ACS_FN const uint32_t* policy_bits(const Tables& T, uint32_t k) {
+  return rule_target_bits(T) + (T.n_rules + 31u) / 32u + k * ((T.n_pols + 31u) / 32u);
+}
 
 // K1's event index (is_allowed_body's events-only skip): per set its rules' range [r0, r1) and,
 // in bit 31 of the r1 word, whether it holds a null policy or a policy with an invalid combining
@@ -1826,51 +1841,70 @@ ACS_FN bool wia_template_set(const Tables& T, const uint32_t* row, uint32_t wp, 
   const NodeRec S = T.sets[s];
   if (S.nflags & NF_HAS_TARGET) return false;
   bool exact = false;
-  for (uint32_t p = S.child_begin; p < S.child_end; ++p) {  // loop 2a
-    if (!row_bit(row, wp, p)) continue;
-    const NodeRec P = T.pols[p];
-    if (P.nflags & NF_NULL) return false;
-    if (!(P.nflags & NF_HAS_TARGET)) continue;
-    if (P.tflags & TF_SUBJ_ROLE) *role_free = false;
-    if (row_bit(row, wv, p)) {
-      exact = true;
-      break;
+  // the set's candidate policies a word at a time from the policy bitsets: loop 2a stops at the
+  // first candidate that is null (untemplated), has a target the class does not decide
+  // (untemplated) or has a target it knows exact (`exact`); role-testing targets up to there
+  // clear role_free
+  const uint32_t* pnull = policy_bits(T, 0);
+  const uint32_t* ptgt = policy_bits(T, 1);
+  const uint32_t* prole = policy_bits(T, 2);
+  auto range_mask = [&](uint32_t base) {
+    uint32_t m = ~0u;
+    if (base < S.child_begin) m &= ~0u << (S.child_begin & 31u);
+    if (S.child_end - base < 32u) m &= (1u << (S.child_end - base)) - 1u;
+    return m;
+  };
+  for (uint32_t base = S.child_begin & ~31u; base < S.child_end; base += 32u) {
+    const uint32_t w = base >> 5;
+    const uint32_t cand = row[wp + w] & range_mask(base);
+    const uint32_t nul = cand & pnull[w], tg = cand & ptgt[w] & ~nul;
+    const uint32_t xt = tg & row[wv + w], xf = tg & row[wv + WP + w];
+    const uint32_t stop = nul | (tg & ~xt & ~xf) | xt;
+    if (!stop) {
+      if (tg & prole[w]) *role_free = false;
+      continue;
     }
-    if (!row_bit(row, wv + WP, p)) return false;
+    const uint32_t b = (uint32_t)__builtin_ctz(stop), upto = b == 31u ? ~0u : (2u << b) - 1u;
+    if (tg & prole[w] & upto) *role_free = false;
+    if (!((xt >> b) & 1u)) return false;  // a null policy or an undecided target
+    exact = true;
+    break;
   }
   if (exact) acc.or_bits(TL.exact + (s >> 5), 1u << (s & 31u));
   bool any_pol = false;
-  for (uint32_t p = S.child_begin; p < S.child_end; ++p) {  // loop 2b
-    if (!row_bit(row, wp, p)) continue;
-    const NodeRec P = T.pols[p];
-    if (P.nflags & NF_NULL) continue;
-    if (P.nflags & NF_HAS_TARGET) {
-      if (P.tflags & TF_SUBJ_ROLE) *role_free = false;
-      if (!row_bit(row, wv + (exact ? 0u : 2u * WP), p)) {
-        if (row_bit(row, wv + (exact ? WP : 3u * WP), p)) continue;
-        return false;
+  // loop 2b: the candidate non-null policies whose target the class knows true in this mode (or
+  // that have none) are kept, those it knows false skipped; an undecided one leaves the class
+  // untemplated.  A kept policy's candidate non-null rules go a word at a time: known true (no
+  // target, or a retried match the class knows) into the row, the others are work.
+  const uint32_t* rlive = rule_live_bits(T);
+  const uint32_t* rtgt = rule_target_bits(T);
+  const uint32_t kts = exact ? 0u : 2u * WP, kfs = exact ? WP : 3u * WP;
+  for (uint32_t base = S.child_begin & ~31u; base < S.child_end; base += 32u) {
+    const uint32_t w = base >> 5;
+    const uint32_t live = row[wp + w] & range_mask(base) & ~pnull[w], tg = live & ptgt[w];
+    if (tg & prole[w]) *role_free = false;
+    const uint32_t kt = row[wv + kts + w], kf = row[wv + kfs + w];
+    if (tg & ~kt & ~kf) return false;
+    for (uint32_t kept = live & ~(tg & ~kt); kept; kept &= kept - 1u) {
+      const uint32_t p = base + (uint32_t)__builtin_ctz(kept);
+      const NodeRec P = T.pols[p];
+      bool any_rule = false;
+      for (uint32_t rb = P.child_begin & ~31u; rb < P.child_end; rb += 32u) {
+        const uint32_t rw = rb >> 5;
+        uint32_t m = row[wr + rw] & rlive[rw];
+        if (rb < P.child_begin) m &= ~0u << (P.child_begin & 31u);
+        if (P.child_end - rb < 32u) m &= (1u << (P.child_end - rb)) - 1u;
+        const uint32_t known = m & (~rtgt[rw] | row[wv + 4u * WP + rw]), work = m & ~known;
+        if (known) {
+          acc.or_bits(BL.wr + rw, known);
+          any_rule = true;
+        }
+        if (work) acc.or_bits(TL.work + rw, work);
       }
-    }
-    // the policy's candidate non-null rules a word at a time: known true (no target, or a
-    // retried match the class knows) go into the row, the others are work
-    bool any_rule = false;
-    const uint32_t* live = rule_live_bits(T);
-    const uint32_t* tgt = rule_target_bits(T);
-    for (uint32_t base = P.child_begin & ~31u; base < P.child_end; base += 32u) {
-      const uint32_t w = base >> 5;
-      uint32_t m = row[wr + w] & live[w];
-      if (base < P.child_begin) m &= ~0u << (P.child_begin & 31u);
-      if (P.child_end - base < 32u) m &= (1u << (P.child_end - base)) - 1u;
-      const uint32_t known = m & (~tgt[w] | row[wv + 4u * WP + w]), work = m & ~known;
-      if (known) {
-        acc.or_bits(BL.wr + w, known);
-        any_rule = true;
+      if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
+        acc.or_bits(BL.wp + (p >> 5), 1u << (p & 31u));
+        any_pol = true;
       }
-      if (work) acc.or_bits(TL.work + w, work);
-    }
-    if ((P.nflags & NF_EFFECT_TRUTHY) || any_rule) {
-      acc.or_bits(BL.wp + (p >> 5), 1u << (p & 31u));
-      any_pol = true;
     }
   }
   if (any_pol) acc.or_bits(s >> 5, 1u << (s & 31u));

@@ -997,7 +997,9 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     // (1 KB contiguous per store instead of 64 lanes' 16-B pieces of 64 rows), then each lane
     // rewrites the chunks of its own row that its work rules add bits to.  (Rejected A/B, r06_g:
     // the template chunks held in registers and re-read only when the (class, second class) pair
-    // changes — c4 1M K2 3.975 vs 4.007 ms, 131,072 1.751 vs 1.727: within the noise.)
+    // changes — c4 1M K2 3.975 vs 4.007 ms, 131,072 1.751 vs 1.727: within the noise; the wave's rows
+    // as one flat run of chunks, four steps' loads in flight — 2.290 vs 2.298 ms, 4M 6.27 vs 6.37,
+    // r06_u: the copy is bound by its 1.4 GB of writes, not by the loads' latency.)
     const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
     for (uint64_t m = ACS_AB_PROBE_K2_NOCOPY ? 0u : __ballot(usable); m; m &= m - 1u) {
       const int j = __builtin_ctzll(m);
