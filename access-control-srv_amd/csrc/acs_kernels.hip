@@ -829,9 +829,8 @@ struct SparseTplSink {
 // sharing the 16-B pieces, and evaluates the listed rules from LDS.  Region layout (u32 words):
 // [cap lines of 32 | cap (policy, set) | cap rule ids]; needs device rule lines (rstride 2).
 constexpr uint32_t STAGE_WORDS_PER_RULE = 32u + 2u + 1u;
-#ifndef ACS_K2_STAGE
-#define ACS_K2_STAGE 1  // 0: the unstaged walk (what_is_allowed_tpl), A/B
-#endif
+// (The unstaged walk, what_is_allowed_tpl, serves images without rule lines and regions too small
+// to stage a rule: c4 1M 2.722 vs 2.523 ms staged, r06_l.)
 template <class RQ, class SINK>
 __device__ bool what_is_allowed_tpl_staged(const RQ& R, const TplLayout& TL, const BitsLayout& BL, const uint32_t* t1,
                                            const uint32_t* t2, SINK& sink, OblLog& obl, uint32_t* lds, uint32_t cap) {
@@ -915,18 +914,9 @@ __device__ bool what_is_allowed_tpl_staged(const RQ& R, const TplLayout& TL, con
 
 // Order of one wave's stores to the same row chunk (the wave's template copy, then a lane's own
 // rewrite of that chunk): the earlier stores complete before the later issue.  Workgroup scope is
-// a wait for the wave's outstanding stores; agent scope (ACS_K2_FENCE_AGENT=1, the round-5 form)
-// also writes the XCD's L2 back to memory at every wave, which the ordering does not need.
-#ifndef ACS_K2_FENCE_AGENT
-#define ACS_K2_FENCE_AGENT 0
-#endif
-__device__ inline void k2_store_order() {
-#if ACS_K2_FENCE_AGENT
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#else
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#endif
-}
+// a wait for the wave's outstanding stores.  (Rejected, r06_k: agent scope, the round-5 form, also
+// writes the XCD's L2 back to memory at every wave — c4 1M K2 3.445 vs 2.705 ms.)
+__device__ inline void k2_store_order() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
 // Timing probes (K2 results differ): no template copy / no work rules
 #ifndef ACS_AB_PROBE_K2_NOCOPY
 #define ACS_AB_PROBE_K2_NOCOPY 0
@@ -1026,7 +1016,7 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
       SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
       const ReqLds<K2_SLOTS> R(T, B, i, h, scol, BLOCK, ln, !CB);
-      const uint32_t cap = ACS_K2_STAGE && T.rstride == 2u ? min(32u, lds_wave_words(B) / STAGE_WORDS_PER_RULE) : 0u;
+      const uint32_t cap = T.rstride == 2u ? min(32u, lds_wave_words(B) / STAGE_WORDS_PER_RULE) : 0u;
       if (cap ? what_is_allowed_tpl_staged(R, TL, BL, t1, t2, sink, log, wave_lds_row(B), cap)
               : what_is_allowed_tpl(R, TL, BL, t1, t2, sink, log)) {
         if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
@@ -2435,11 +2425,9 @@ static int spread_waves(acs_tables* t, Workspace& W, hipStream_t s, const uint32
 // ~36-request classes of a 1M batch, but there are 2.3x fewer of them: c4 1M K2 4.03 -> 3.43 ms
 // (r06_h), while K1 keeps the holes (c3r1 1M 0.41 padded vs 0.75, c3 0.76 vs 0.84) except in a
 // batch with ACL_NONE requests whose lanes are mostly holes (is_allowed_launch).
-#ifndef ACS_K2_PAD
-#define ACS_K2_PAD 0  // 1: A/B builds that keep the holes for K2
-#endif
+
 static int drop_holes(Workspace& W, const uint32_t** perm, size_t* lanes, uint32_t n, hipStream_t s) {
-  if (ACS_K2_PAD || !*perm || *lanes <= n) return 0;
+  if (!*perm || *lanes <= n) return 0;
   const uint32_t nt = (uint32_t)((*lanes + SORT_TILE - 1) / SORT_TILE);
   // room for every lane of the order (a malformed order of the device entry points, which do not
   // validate it, can select more than n: still written inside the buffer)
@@ -2530,7 +2518,7 @@ static int what_is_allowed_launch(acs_tables* t, Workspace& W, const acs_req_bat
   const uint32_t* perm = nullptr;
   size_t lanes = b->n;
   if (((uintptr_t)bits & 15u) != 0) return fail("acs_what_is_allowed_device: bits must be 16-byte aligned");
-  if (batch_order(t, W, b, B, s, &perm, ACS_K2_PAD && !ACS_AB_NO_PAD, &lanes)) return -1;
+  if (batch_order(t, W, b, B, s, &perm, false, &lanes)) return -1;
   const int slot = (int)(t->launches % acs_tables::RING);
   // the timed K2 includes the order's compaction and the template pass
   if (t->timing) HIP_OK(hipEventRecord(t->tev[2 * slot], s));
