@@ -141,3 +141,57 @@ def test_templates_gpu_stray_set_bits():
     _same((got[0].view(np.uint32), got[1].view(np.uint32), got[2].view(np.uint32),
            got[3].reshape(-1).view(L.DECISION_DT)), want, "stray set bits")
     t.close()
+
+
+def _many_work_rules_store():
+    """c3 store plus a last policy set whose one policy holds 400 property rules (10 entities x 40
+    properties, no subjects, PERMIT / DENY alternating): a class of one of those entities reaches 40
+    work rules there, more than K2 stages in one batch (23 at c3's row length, acs_kernels.hip
+    what_is_allowed_tpl_staged)."""
+    doc = synth.c3_store()
+    ent = "urn:restorecommerce:acs:names:model:entity"
+    prop = "urn:restorecommerce:acs:names:model:property"
+    rules = []
+    for e in range(10):
+        for k in range(40):
+            v = f"urn:restorecommerce:acs:model:ent{e}.Ent{e}"
+            rules.append({"id": f"rw_{e}_{k}", "target": {"resources": [{"id": ent, "value": v},
+                                                                        {"id": prop, "value": f"{v}#p{k}"}]},
+                          "effect": "PERMIT" if k % 2 == 0 else "DENY", "evaluation_cacheable": False})
+    doc["policy_sets"].append({"id": "s_work", "combining_algorithm":
+                               "urn:oasis:names:tc:xacml:3.0:rule-combining-algorithm:deny-overrides",
+                               "policies": [{"id": "p_work", "combining_algorithm":
+                                             "urn:oasis:names:tc:xacml:3.0:rule-combining-algorithm:deny-overrides",
+                                             "rules": rules}]})
+    return doc
+
+
+def test_templates_many_work_rules():
+    """CPU build: the store with 40 work rules per class in one policy — templates equal the full
+    walk."""
+    cs = compiler.compile_store(store.populate(_many_work_rules_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 3_000, "c3", seed=41, second_role=0.5)
+    got = templated_wia(cs, sb.batch, compact=True)
+    want = host_core.what_is_allowed(cs, sb.batch)
+    _same(got[:4], want, "many work rules")
+    assert got[4] > 0.5 * sb.batch.n
+
+
+@pytest.mark.gpu
+def test_templates_gpu_many_work_rules():
+    """K2 with several staged batches of work rules per wave (40 work rules per class in one
+    policy, more than one LDS batch holds) equals the CPU build's full walk: rows, logs and
+    records."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from acs_mi355x.device import DeviceBatch, what_is_allowed_device
+    cs = compiler.compile_store(store.populate(_many_work_rules_store()), FULL_URNS, DEFAULT_CAS)
+    sb = synth.requests(cs, 20_000, "c3", seed=43, second_role=0.5)
+    t = native.Tables(compiler.store_blob(cs), 0)
+    got = [x.cpu().numpy() for x in what_is_allowed_device(t, DeviceBatch(sb.batch, 0, compact=True))]
+    want = host_core.what_is_allowed(cs, sb.batch)
+    _same((got[0].view(np.uint32), got[1].view(np.uint32), got[2].view(np.uint32),
+           got[3].reshape(-1).view(L.DECISION_DT)), want, "many work rules, device")
+    _same(t.what_is_allowed(sb.batch), want, "many work rules, host buffers")
+    t.close()
