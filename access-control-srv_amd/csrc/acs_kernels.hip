@@ -784,6 +784,7 @@ struct SparseTplSink {
   const uint4* t2;
   uint32_t cur[3];
   uint4 buf[3];
+  uint32_t wm[3] = {0u, 0u, 0u};  // the chunks written (bit q of chunk q; rows of at most 96 chunks)
   __device__ SparseTplSink(uint32_t* r, const BitsLayout& L, const uint32_t* a, const uint32_t* b)
       : row(reinterpret_cast<uint4*>(r)), t1(reinterpret_cast<const uint4*>(a)), t2(reinterpret_cast<const uint4*>(b)) {
     cur[0] = 0;
@@ -801,6 +802,10 @@ struct SparseTplSink {
     }
     v.x |= b.x; v.y |= b.y; v.z |= b.z; v.w |= b.w;
     row[cur[S]] = v;
+    const uint32_t c = cur[S], bit = 1u << (c & 31u);
+    wm[0] |= c < 32u ? bit : 0u;
+    wm[1] |= c >= 32u && c < 64u ? bit : 0u;
+    wm[2] |= c >= 64u && c < 96u ? bit : 0u;
     buf[S] = make_uint4(0u, 0u, 0u, 0u);
   }
   template <int S> __device__ void set(uint32_t w, uint32_t bit) {
@@ -929,6 +934,9 @@ __device__ inline void k2_store_order() { __builtin_amdgcn_fence(__ATOMIC_RELEAS
 #ifndef ACS_K2_SLOTS
 #define ACS_K2_SLOTS 5
 #endif
+#ifndef ACS_K2_WORK_FIRST
+#define ACS_K2_WORK_FIRST 1  // 0: the copy first, then the rewrites (A/B)
+#endif
 constexpr int K2_SLOTS = ACS_K2_SLOTS;
 // K2: whatIsAllowed inclusion bitset + maskedProperty log, one request per lane (perm
 // order k).  Lane k writes request perm[k]'s BitsLayout row of the [n][words] output itself,
@@ -991,7 +999,14 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
     // as one flat run of chunks, four steps' loads in flight — 2.290 vs 2.298 ms, 4M 6.27 vs 6.37,
     // r06_u: the copy is bound by its 1.4 GB of writes, not by the loads' latency.)
     const uint32_t q4 = BL.words >> 2, lane = threadIdx.x & 63u;
-    for (uint64_t m = ACS_AB_PROBE_K2_NOCOPY ? 0u : __ballot(usable); m; m &= m - 1u) {
+    // Rows of at most 96 chunks (c4: 89): the lanes' work rules first, each writing the chunks its
+    // bits fall in (template | bits) and noting them, then the wave copies the template into the
+    // other chunks only — every chunk written once, no store ordering between lanes.  Longer rows:
+    // the copy first, then the rewrites after a store-order fence.
+    const bool work_first = ACS_K2_WORK_FIRST && q4 <= 96u;
+    uint32_t wm0 = 0, wm1 = 0, wm2 = 0;
+    bool tpl_ok = false;
+    for (uint64_t m = ACS_AB_PROBE_K2_NOCOPY || work_first ? 0u : __ballot(usable); m; m &= m - 1u) {
       const int j = __builtin_ctzll(m);
       const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
                      c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
@@ -1008,10 +1023,10 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
         dst[q] = v;
       }
     }
-    k2_store_order();  // the copy's stores land before the lanes' own
+    if (!work_first) k2_store_order();  // the copy's stores land before the lanes' own
     if (usable && ACS_AB_PROBE_K2_NOWORK) {  // timing probe: no work rules (rows lack their bits)
       obl_n[o] = 0u;
-      done = true;
+      done = tpl_ok = true;
     } else if (usable) {
       SparseTplSink sink(bits + (size_t)o * BL.words, BL, t1, t2);
       OblLog log{obl + (size_t)o * 2 * OBL_MAX, 0, false};
@@ -1021,7 +1036,33 @@ __global__ __launch_bounds__(BLOCK) void what_is_allowed_kernel(Tables T, Batch 
               : what_is_allowed_tpl(R, TL, BL, t1, t2, sink, log)) {
         if (log.overflow) d.flags |= OF_OBL_OVERFLOW;
         obl_n[o] = log.n;
-        done = true;
+        done = tpl_ok = true;
+        wm0 = sink.wm[0];
+        wm1 = sink.wm[1];
+        wm2 = sink.wm[2];
+      }
+    }
+    // work first: the template into the chunks of each templated row that its lane did not write (a
+    // lane whose template walk failed takes the full walk, which writes its whole row)
+    for (uint64_t m = work_first && !ACS_AB_PROBE_K2_NOCOPY ? __ballot(tpl_ok) : 0u; m; m &= m - 1u) {
+      const int j = __builtin_ctzll(m);
+      const uint32_t oj = (uint32_t)__shfl((int)o, j), c1j = (uint32_t)__shfl((int)c1, j),
+                     c2j = (uint32_t)__shfl((int)(t2 ? c2 : 0u), j);
+      const uint32_t k0 = __builtin_amdgcn_readlane(wm0, j), k1 = __builtin_amdgcn_readlane(wm1, j),
+                     k2 = __builtin_amdgcn_readlane(wm2, j);
+      uint4* dst = reinterpret_cast<uint4*>(bits + (size_t)oj * BL.words);
+      const uint4* s1 = reinterpret_cast<const uint4*>(tpl + (size_t)c1j * TL.stride);
+      const uint4* s2 = c2j ? reinterpret_cast<const uint4*>(tpl + (size_t)(c2j - 1u) * TL.stride) : nullptr;
+      ACS_SCAN(16u * q4 * (s2 ? 2u : 1u));
+      for (uint32_t q = lane; q < q4; q += 64u) {
+        const uint32_t km = q < 32u ? k0 : q < 64u ? k1 : k2;
+        if ((km >> (q & 31u)) & 1u) continue;
+        uint4 v = s1[q];
+        if (s2) {
+          const uint4 u = s2[q];
+          v.x |= u.x; v.y |= u.y; v.z |= u.z; v.w |= u.w;
+        }
+        dst[q] = v;
       }
     }
   }
