@@ -43,16 +43,29 @@ function apply(ctl, st) {
     const t0 = Date.now();
     const ctl = new g.GpuAccessController(maps, sc.urns, sc.cas, { threads: 8 });
     const first = Date.now() - t0;
+    // one batch's wall time (ms); the codec's class rows are cached across batches of one store
+    const batch = async () => {
+      const tb = process.hrtime.bigint();
+      const r = await ctl.isAllowedBatch(sc.requests);
+      return { ms: Number(process.hrtime.bigint() - tb) / 1e6, n: r.length };
+    };
+    const cold = await batch();
+    const warm = await batch();
     const [sid, pid, rule] = sc.steps[0].args;
     ctl.updateRule(sid, pid, rule);
     const t1 = Date.now();
     ctl._sync();
     const incr = { ms: Date.now() - t1, stats: ctl.lastRefresh };
+    // the first batch after the update recomputes the class rows (DESIGN §8.4), the next is warm
+    const afterUpdate = await batch();
+    const afterWarm = await batch();
     const t2 = Date.now();
     ctl.refresh(ctl.policySets);
     const full = { ms: Date.now() - t2, stats: ctl.lastRefresh };
     const r = await ctl.isAllowedBatch(sc.requests);
-    out.push({ first_ms: first, incremental: incr, full_refresh: full, decided: r.length });
+    out.push({ first_ms: first, incremental: incr, full_refresh: full, decided: r.length,
+               batch_ms: { cold: cold.ms, warm: warm.ms, first_after_update: afterUpdate.ms,
+                           second_after_update: afterWarm.ms, requests: warm.n } });
     ctl.close();
   } else {
     const ctl = new g.GpuAccessController(maps, sc.urns, sc.cas, { threads: 2, compileOnly: mode === 'compile' });
